@@ -1,0 +1,162 @@
+"""ctypes binding of include/arcanefem_amd.h (libafem.so, built in-tree).
+
+The product path has no fallback: if the HIP library is missing or fails to
+load, every call raises.  Python is the host driver only; all compute runs in
+libafem.so on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libafem.so")
+
+AFEM_OK = 0
+AFEM_MEM_HOST = 0
+AFEM_MEM_DEVICE = 1
+UNIQUE_ID_BYTES = 128
+ERRORS = {1: "ArgumentException", 2: "HipError", 3: "NotImplementedException", 4: "StateError",
+          5: "NotFound", 6: "CommError", 7: "LimitExceeded"}
+
+
+class AfemError(RuntimeError):
+    def __init__(self, code, func, msg):
+        self.code = code
+        super().__init__(f"{func}: [{ERRORS.get(code, code)}] {msg}")
+
+
+class MeshInfo(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int32), ("nb_node_per_cell", ctypes.c_int32), ("n_nodes", ctypes.c_int64),
+                ("n_own_nodes", ctypes.c_int64), ("n_cells", ctypes.c_int64)]
+
+
+class CsrView(ctypes.Structure):
+    _fields_ = [("n_block_rows", ctypes.c_int64), ("n_block_cols", ctypes.c_int64), ("nnz_blocks", ctypes.c_int64),
+                ("block_size", ctypes.c_int32), ("ordered_per_block", ctypes.c_int32), ("rows", ctypes.c_void_p),
+                ("columns", ctypes.c_void_p), ("values", ctypes.c_void_p)]
+
+
+class BsrStats(ctypes.Structure):
+    _fields_ = [("n_incidences", ctypes.c_int64), ("inc_table_entries", ctypes.c_int64),
+                ("max_row_len", ctypes.c_int32), ("rows_per_block", ctypes.c_int32), ("max_seg", ctypes.c_int64)]
+
+
+class SolverOpts(ctypes.Structure):
+    _fields_ = [("method", ctypes.c_int32), ("max_iter", ctypes.c_int32), ("rtol", ctypes.c_double),
+                ("atol", ctypes.c_double), ("check_every", ctypes.c_int32), ("fixed_iterations", ctypes.c_int32)]
+
+
+class SolveStats(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int32), ("converged", ctypes.c_int32), ("rel_residual", ctypes.c_double),
+                ("residual_norm", ctypes.c_double), ("solve_ms", ctypes.c_double)]
+
+
+P = ctypes.c_void_p
+PP = ctypes.POINTER(ctypes.c_void_p)
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+U64 = ctypes.c_uint64
+D = ctypes.c_double
+INT = ctypes.c_int
+
+# name -> argtypes (all return int status, except afem_last_error / afem_version)
+SIGNATURES = {
+    "afem_device_count": [ctypes.POINTER(INT)],
+    "afem_ctx_create": [INT, P, PP],
+    "afem_ctx_destroy": [P],
+    "afem_ctx_synchronize": [P],
+    "afem_ctx_stream": [P, PP],
+    "afem_ctx_timer_start": [P],
+    "afem_ctx_timer_stop": [P, ctypes.POINTER(ctypes.c_float)],
+    "afem_ctx_event_record": [P, INT],
+    "afem_ctx_event_elapsed": [P, INT, INT, ctypes.POINTER(ctypes.c_float)],
+    "afem_malloc": [P, ctypes.c_size_t, PP],
+    "afem_free": [P, P],
+    "afem_memcpy": [P, P, P, ctypes.c_size_t, INT, INT],
+    "afem_mesh_create": [P, INT, INT, I64, I64, I64, P, P, INT, PP],
+    "afem_mesh_create_structured": [P, INT, INT, INT, D, U64, INT, INT, PP],
+    "afem_mesh_get_info": [P, ctypes.POINTER(MeshInfo)],
+    "afem_mesh_download": [P, P, P, P],
+    "afem_mesh_structured_bottom_nodes": [P, P, ctypes.POINTER(I64)],
+    "afem_mesh_destroy": [P],
+    "afem_bsr_create": [P, INT, INT, PP],
+    "afem_bsr_compute_sparsity": [P],
+    "afem_bsr_assemble_poisson_p1": [P, D, D, P],
+    "afem_bsr_assemble_elasticity_p1": [P, D, D],
+    "afem_bsr_reset_values": [P],
+    "afem_bsr_set_value": [P, I32, I32, D],
+    "afem_bsr_get_value": [P, I32, I32, ctypes.POINTER(D)],
+    "afem_bsr_view": [P, ctypes.POINTER(CsrView)],
+    "afem_bsr_get_stats": [P, ctypes.POINTER(BsrStats)],
+    "afem_bsr_get_sizes": [P, ctypes.POINTER(I64), ctypes.POINTER(I64)],
+    "afem_bsr_export_csr32": [P, P, P, P, P],
+    "afem_bsr_download": [P, P, P, P],
+    "afem_bsr_to_linear_system": [P, P],
+    "afem_bsr_destroy": [P],
+    "afem_ls_create": [P, I64, I64, PP],
+    "afem_ls_set_solver_options": [P, ctypes.POINTER(SolverOpts)],
+    "afem_ls_get_solver_options": [P, ctypes.POINTER(SolverOpts)],
+    "afem_ls_matrix_add_value": [P, I32, I32, D],
+    "afem_ls_matrix_set_value": [P, I32, I32, D],
+    "afem_ls_eliminate_row": [P, I32, D],
+    "afem_ls_eliminate_row_column": [P, I32, D],
+    "afem_ls_set_csr_values": [P, P, P, P, P, I32, I32, INT],
+    "afem_ls_has_set_csr_values": [P, ctypes.POINTER(INT)],
+    "afem_ls_get_csr_values": [P, ctypes.POINTER(CsrView)],
+    "afem_ls_rhs": [P, PP],
+    "afem_ls_solution": [P, PP],
+    "afem_ls_forced_info": [P, PP],
+    "afem_ls_forced_value": [P, PP],
+    "afem_ls_elimination_info": [P, PP],
+    "afem_ls_elimination_value": [P, PP],
+    "afem_ls_dirichlet_penalty": [P, P, I64, D, D, INT],
+    "afem_ls_dirichlet_row_elimination": [P, P, I64, D, INT],
+    "afem_ls_apply_boundary_conditions": [P],
+    "afem_ls_clear_values": [P],
+    "afem_ls_solve": [P, ctypes.POINTER(SolveStats)],
+    "afem_ls_spmv": [P, P, P],
+    "afem_ls_destroy": [P],
+    "afem_comm_unique_id": [P],
+    "afem_comm_create": [P, P, INT, INT, PP],
+    "afem_comm_destroy": [P],
+    "afem_comm_allreduce_sum": [P, P, I64],
+    "afem_ls_set_halo": [P, P, INT, P, P, P, P, P],
+    "afem_ls_set_halo_structured": [P, P, P],
+    "afem_structured_halo_plan": [INT, INT, INT, INT, INT, ctypes.POINTER(INT), P, P, P, P, P],
+    "afem_ls_synchronize": [P, P],
+}
+
+_lib = None
+
+
+def load():
+    """Load libafem.so (raises OSError if it was not built: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "or `make -C arcanefem_amd/csrc`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.afem_last_error.restype = ctypes.c_char_p
+        L.afem_last_error.argtypes = []
+        L.afem_version.restype = ctypes.c_int
+        L.afem_version.argtypes = []
+        for name, args in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = ctypes.c_int
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    L = load()
+    rc = getattr(L, name)(*args)
+    if rc != AFEM_OK:
+        raise AfemError(rc, name, L.afem_last_error().decode(errors="replace"))
+    return rc
+
+
+def exported_symbols():
+    return ["afem_last_error", "afem_version"] + list(SIGNATURES)

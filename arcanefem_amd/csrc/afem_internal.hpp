@@ -1,0 +1,231 @@
+// Internal declarations of the MI355X FEM assembly + CG library (libafem.so).
+// Host side is C++17; kernels are hand-written HIP for gfx950 (CDNA4,
+// wave64).  See DESIGN.md for the data layout and the roofline of each kernel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/arcanefem_amd.h"
+
+namespace afem {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+[[noreturn]] void throw_hip(hipError_t e, const char* expr, const char* file, int line);
+
+#define AFEM_HIP(x)                                              \
+  do {                                                           \
+    hipError_t e_ = (x);                                         \
+    if (e_ != hipSuccess) ::afem::throw_hip(e_, #x, __FILE__, __LINE__); \
+  } while (0)
+
+#define AFEM_REQUIRE(cond, code, msg)                 \
+  do {                                                \
+    if (!(cond)) throw ::afem::Error((code), (msg));  \
+  } while (0)
+
+// Launch-error check right after a kernel launch (asynchronous faults surface
+// at the next synchronising call).
+#define AFEM_LAUNCHED() AFEM_HIP(hipGetLastError())
+
+constexpr int kWave = 64;
+
+// ------------------------------------------------------------------ device buffer
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) { reset(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+    return *this;
+  }
+  ~DevBuf() { reset(); }
+  void alloc(size_t count) {
+    reset();
+    if (count) AFEM_HIP(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)));
+    n = count;
+  }
+  void reset() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  size_t bytes() const { return n * sizeof(T); }
+};
+
+// ------------------------------------------------------------------ context
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> pool;  // AFEM_EVENT_SLOTS, created lazily
+  int n_cu = 256;
+  void set_device() const { AFEM_HIP(hipSetDevice(device)); }
+  void sync() const { AFEM_HIP(hipStreamSynchronize(stream)); }
+};
+
+// ------------------------------------------------------------------ mesh
+struct StructuredInfo {
+  bool valid = false;
+  int dim = 3, n = 0, nz = 0, nranks = 1, rank = 0;
+  int64_t L = 0;            // nodes per layer
+  int k0 = 0, k1 = 0;       // owned node layers [k0,k1)
+  int ghost_lo = -1, ghost_hi = -1;  // ghost layers (or -1)
+  double jitter = 0.0;
+  uint64_t seed = 0;
+};
+
+struct Mesh {
+  Ctx* ctx = nullptr;
+  int dim = 3;
+  int nv = 4;
+  int64_t n_nodes = 0, n_own = 0, n_cells = 0;
+  DevBuf<int32_t> cell_node;  // [n_cells*nv]
+  DevBuf<double> coords;      // [n_nodes*3]  AoS x,y,z (VariableNodeReal3 layout)
+  StructuredInfo st;
+};
+
+// ------------------------------------------------------------------ sparsity
+// Scalar (node-node) structure shared by every NB_DOF: rows = owned nodes.
+struct Structure {
+  int64_t n_rows = 0, n_cols = 0, nnz = 0;
+  DevBuf<int64_t> row_ptr;  // [n_rows+1]
+  DevBuf<int32_t> cols;     // [nnz], sorted ascending per row
+  // Row-local incidence table, sliced ELLPACK with C = 64 (one wavefront):
+  // entry (slice s, k, lane) at inc_slice_ptr[s] + k*64 + lane describes the
+  // k-th cell incident to row 64*s+lane as the row-slots of the cell's other
+  // nodes (one byte each) and the row's diagonal slot in the top byte.
+  DevBuf<uint32_t> inc;
+  DevBuf<int64_t> inc_slice_ptr;  // [n_slices+1]
+  DevBuf<int32_t> inc_slice_k;    // [n_slices] max incidences in the slice
+  int64_t n_slices = 0;
+  int64_t n_incidences = 0;  // real (non-padding) entries
+  int max_row_len = 0;
+  int64_t max_seg = 0;       // max nnz over assembly blocks of rows_per_block rows
+  int rows_per_block = 256;
+  DevBuf<int64_t> diag_pos;  // [n_rows] position of the diagonal in cols
+};
+
+struct LinearSystem;
+
+struct Bsr {
+  Mesh* mesh = nullptr;
+  int nb_dof = 1;
+  bool order_per_block = true;  // false: CSR row order (use_csr_in_linear_system)
+  bool has_sparsity = false;
+  Structure s;
+  DevBuf<double> values;       // [nnz * nb_dof^2]
+  // scalar CSR expansion for NB_DOF>1 (built on demand)
+  DevBuf<int64_t> csr_rows;
+  DevBuf<int32_t> csr_cols;
+  DevBuf<double> csr_vals;  // per-block layout permuted to CSR order
+};
+
+// ------------------------------------------------------------------ communicator / halo
+struct Comm;
+struct Halo {
+  Comm* comm = nullptr;
+  std::vector<int> nbr;
+  std::vector<int64_t> send_cnt, recv_cnt, send_off, recv_off;
+  DevBuf<int32_t> send_ids, recv_ids;
+  DevBuf<double> send_buf, recv_buf;
+  int64_t n_send = 0, n_recv = 0;
+};
+
+void halo_exchange(Halo& h, Ctx& ctx, double* x);
+void comm_allreduce(Comm* c, Ctx& ctx, double* d, int64_t n);
+
+// ------------------------------------------------------------------ linear system
+struct LinearSystem {
+  Ctx* ctx = nullptr;
+  int64_t n_rows = 0, n_cols = 0;
+  afem_solver_opts opts{};
+  DevBuf<double> rhs, sol;
+  DevBuf<uint8_t> forced_info, elim_info;
+  DevBuf<double> forced_value, elim_value;
+  // CSR view (device)
+  bool has_csr = false;
+  int64_t csr_n = 0, csr_nnz = 0;
+  const int64_t* csr_rows = nullptr;
+  const int32_t* csr_cols = nullptr;
+  double* csr_vals = nullptr;
+  DevBuf<int64_t> own_rows;   // when the view came in the reference int32 layout
+  DevBuf<int32_t> own_cols;
+  DevBuf<double> own_vals;    // COO-built matrix
+  // host COO (Aleph semantics)
+  std::map<std::pair<int32_t, int32_t>, double> add_map, set_map;
+  std::map<int32_t, std::pair<uint8_t, double>> host_elim;
+  // solver work
+  DevBuf<double> r, z, p, q, dinv, partial, scal;
+  DevBuf<uint8_t> cons;  // constraint-row flags of the stopping test
+  double* pinned = nullptr;
+  std::unique_ptr<Halo> halo;
+};
+
+// ------------------------------------------------------------------ kernels (host launchers)
+void exclusive_scan_i64(Ctx& ctx, const int64_t* in, int64_t* out, int64_t n, DevBuf<int64_t>* tmp_pool = nullptr);
+void exclusive_scan_i32_to_i64(Ctx& ctx, const int32_t* in, int64_t* out, int64_t n);
+int64_t read_i64(Ctx& ctx, const int64_t* d);
+
+void build_structure(Mesh& m, Structure& s);
+void assemble_scalar(Bsr& b, double coef, double f, double* rhs);
+void assemble_elasticity_tri(Bsr& b, double lambda, double mu2);
+
+void ls_apply_bcs(LinearSystem& ls);
+void ls_solve(LinearSystem& ls, afem_solve_stats* st);
+void ls_spmv(LinearSystem& ls, const double* x, double* y);
+void ls_build_from_host_coo(LinearSystem& ls);
+void ls_point_update(LinearSystem& ls, int32_t row, int32_t col, double v, bool set);
+void ls_set_list(LinearSystem& ls, const int32_t* ids, int64_t n, int mem, int kind, double value, double penalty);
+
+void mesh_structured(Ctx& ctx, Mesh& m, int dim, int n, int nz, double jitter, uint64_t seed, int nranks, int rank);
+void mesh_structured_bottom(Mesh& m, std::vector<int32_t>& ids);
+void mesh_local_to_global(Mesh& m, int64_t* host_out);
+void structured_halo_lists(int dim, int n, int nz, int nranks, int rank, std::vector<int>& nbr,
+                           std::vector<int64_t>& send_cnt, std::vector<int64_t>& recv_cnt,
+                           std::vector<int32_t>& send_ids, std::vector<int32_t>& recv_ids);
+
+// op: 0 get, 1 set, 2 add on the (scalar DoF row, scalar DoF col) entry of a BSR
+// matrix; returns false when the entry is not in the structure.
+bool bsr_point(Bsr& b, int32_t row, int32_t col, int op, double v, double* out);
+// Scalar CSR expansion of an NB_DOF>1 matrix (BSRMatrix::toCsr,
+// femutils/BSRFormat.h:194-256) into b.csr_rows/b.csr_cols; values: the
+// per-row layout is already CSR order, the per-block one is permuted into
+// `vals_out` (device, nnz*k^2).
+void bsr_expand_scalar(Bsr& b, double* vals_out);
+
+void comm_unique_id(uint8_t* out);
+Comm* comm_create(Ctx& ctx, const uint8_t* id, int nranks, int rank);
+void comm_destroy(Comm* c);
+int comm_nranks(Comm* c);
+int comm_rank(Comm* c);
+void halo_setup(Halo& h, Ctx& ctx, Comm* comm, int n_nbr, const int32_t* nbr, const int64_t* send_cnt,
+                const int32_t* send_ids, const int64_t* recv_cnt, const int32_t* recv_ids);
+
+}  // namespace afem
+
+// Opaque C handles map 1:1 to the internal objects.
+struct afem_ctx : afem::Ctx {};
+struct afem_mesh : afem::Mesh {};
+struct afem_bsr : afem::Bsr {};
+struct afem_ls : afem::LinearSystem {};
+struct afem_comm {
+  afem::Comm* c = nullptr;
+  afem::Ctx* ctx = nullptr;
+};

@@ -1,0 +1,137 @@
+// RCCL over xGMI: ghost-DoF halo exchange and the CG scalar all-reduce.
+// One process per GPU; the ncclUniqueId is produced by afem_comm_unique_id on
+// rank 0 and broadcast by the caller (torch.distributed in the Python
+// driver).  Replaces the reference's IParallelMng traffic: the ghost
+// synchronize() of femutils/HypreDoFLinearSystem.cc:299 /
+// modules/poisson/FemModule.cc:369 and the PCG dot-product reductions inside
+// Hypre (femutils/HypreDoFLinearSystem.cc:731-742).
+#include <rccl/rccl.h>
+
+#include <cstring>
+
+#include "afem_internal.hpp"
+
+namespace afem {
+
+struct Comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+#define AFEM_NCCL(x)                                                                                  \
+  do {                                                                                                \
+    ncclResult_t r_ = (x);                                                                            \
+    if (r_ != ncclSuccess)                                                                            \
+      throw ::afem::Error(AFEM_ERR_COMM, std::string(#x) + " failed: " + ncclGetErrorString(r_));     \
+  } while (0)
+
+namespace {
+__global__ void k_gather(int64_t n, const int32_t* __restrict__ ids, const double* __restrict__ x,
+                         double* __restrict__ out)
+{
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) out[t] = x[ids[t]];
+}
+__global__ void k_scatter(int64_t n, const int32_t* __restrict__ ids, const double* __restrict__ in,
+                          double* __restrict__ x)
+{
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) x[ids[t]] = in[t];
+}
+inline unsigned grid_for(int64_t n, int threads) { return (unsigned)((n + threads - 1) / threads); }
+}  // namespace
+
+void comm_unique_id(uint8_t* out)
+{
+  static_assert(sizeof(ncclUniqueId) <= AFEM_UNIQUE_ID_BYTES, "ncclUniqueId larger than the ABI buffer");
+  ncclUniqueId id;
+  AFEM_NCCL(ncclGetUniqueId(&id));
+  memset(out, 0, AFEM_UNIQUE_ID_BYTES);
+  memcpy(out, &id, sizeof(id));
+}
+
+Comm* comm_create(Ctx& ctx, const uint8_t* idb, int nranks, int rank)
+{
+  AFEM_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, AFEM_ERR_ARG, "afem_comm_create: bad rank/nranks");
+  ctx.set_device();
+  ncclUniqueId id;
+  memcpy(&id, idb, sizeof(id));
+  auto* c = new Comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    throw Error(AFEM_ERR_COMM, std::string("ncclCommInitRank failed: ") + ncclGetErrorString(r));
+  }
+  return c;
+}
+
+void comm_destroy(Comm* c)
+{
+  if (!c) return;
+  if (c->comm) ncclCommDestroy(c->comm);
+  delete c;
+}
+
+void comm_allreduce(Comm* c, Ctx& ctx, double* d, int64_t n)
+{
+  if (!c || c->nranks == 1) return;
+  AFEM_NCCL(ncclAllReduce(d, d, (size_t)n, ncclDouble, ncclSum, c->comm, ctx.stream));
+}
+
+int comm_nranks(Comm* c) { return c ? c->nranks : 1; }
+int comm_rank(Comm* c) { return c ? c->rank : 0; }
+
+void halo_setup(Halo& h, Ctx& ctx, Comm* comm, int n_nbr, const int32_t* nbr, const int64_t* send_cnt,
+                const int32_t* send_ids, const int64_t* recv_cnt, const int32_t* recv_ids)
+{
+  h.comm = comm;
+  h.nbr.assign(nbr, nbr + n_nbr);
+  h.send_cnt.assign(send_cnt, send_cnt + n_nbr);
+  h.recv_cnt.assign(recv_cnt, recv_cnt + n_nbr);
+  h.send_off.assign(n_nbr + 1, 0);
+  h.recv_off.assign(n_nbr + 1, 0);
+  for (int i = 0; i < n_nbr; ++i) {
+    h.send_off[i + 1] = h.send_off[i] + send_cnt[i];
+    h.recv_off[i + 1] = h.recv_off[i] + recv_cnt[i];
+  }
+  h.n_send = h.send_off[n_nbr];
+  h.n_recv = h.recv_off[n_nbr];
+  h.send_ids.alloc(h.n_send);
+  h.recv_ids.alloc(h.n_recv);
+  h.send_buf.alloc(h.n_send);
+  h.recv_buf.alloc(h.n_recv);
+  if (h.n_send)
+    AFEM_HIP(hipMemcpyAsync(h.send_ids.p, send_ids, h.send_ids.bytes(), hipMemcpyHostToDevice, ctx.stream));
+  if (h.n_recv)
+    AFEM_HIP(hipMemcpyAsync(h.recv_ids.p, recv_ids, h.recv_ids.bytes(), hipMemcpyHostToDevice, ctx.stream));
+  ctx.sync();
+}
+
+void halo_exchange(Halo& h, Ctx& ctx, double* x)
+{
+  if (!h.comm || h.comm->nranks == 1 || h.nbr.empty()) return;
+  if (h.n_send) {
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(h.n_send, 256)), dim3(256), 0, ctx.stream, h.n_send, h.send_ids.p, x,
+                       h.send_buf.p);
+    AFEM_LAUNCHED();
+  }
+  AFEM_NCCL(ncclGroupStart());
+  for (size_t i = 0; i < h.nbr.size(); ++i) {
+    if (h.send_cnt[i])
+      AFEM_NCCL(ncclSend(h.send_buf.p + h.send_off[i], (size_t)h.send_cnt[i], ncclDouble, h.nbr[i], h.comm->comm,
+                         ctx.stream));
+    if (h.recv_cnt[i])
+      AFEM_NCCL(ncclRecv(h.recv_buf.p + h.recv_off[i], (size_t)h.recv_cnt[i], ncclDouble, h.nbr[i], h.comm->comm,
+                         ctx.stream));
+  }
+  AFEM_NCCL(ncclGroupEnd());
+  if (h.n_recv) {
+    hipLaunchKernelGGL(k_scatter, dim3(grid_for(h.n_recv, 256)), dim3(256), 0, ctx.stream, h.n_recv, h.recv_ids.p,
+                       h.recv_buf.p, x);
+    AFEM_LAUNCHED();
+  }
+}
+
+}  // namespace afem

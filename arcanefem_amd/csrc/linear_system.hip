@@ -1,0 +1,584 @@
+// DoFLinearSystemImpl on the GPU: boundary-condition kernels (K16-K19 of
+// SURVEY.md §2.4), the Jacobi-preconditioned CG whose SpMV reuses the
+// assembled CSR (replaces Hypre PCG+BoomerAMG / the Sequential MatVec CG,
+// femutils/HypreDoFLinearSystem.cc:387-762, femutils/DoFLinearSystem.cc:106-164),
+// and the host COO path for modules that call matrixAddValue entry by entry
+// (Aleph semantics, femutils/AlephDoFLinearSystem.cc:192-223,501-583).
+#include "afem_internal.hpp"
+
+#include <cmath>
+#include <cstring>
+
+namespace afem {
+namespace {
+
+constexpr int kThreads = 256;
+inline unsigned grid_for(int64_t n, int threads) { return (unsigned)((n + threads - 1) / threads); }
+constexpr uint8_t kElimRow = 1, kElimRowCol = 2;
+
+// ---------------------------------------------------------------- BC kernels
+// kind 0: penalty  (femutils/ArcaneFemFunctionsGpu.h:434-456)
+// kind 1: row elimination, kind 2: row+column elimination (:461-482)
+__global__ void k_set_list(int64_t n, const int32_t* __restrict__ ids, int kind, double value, double penalty,
+                           int64_t n_rows, uint8_t* __restrict__ forced_info, double* __restrict__ forced_value,
+                           uint8_t* __restrict__ elim_info, double* __restrict__ elim_value, double* __restrict__ rhs)
+{
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  int32_t d = ids[t];
+  if (d < 0 || d >= n_rows) return;  // isOwn() filter
+  if (kind == 0) {
+    forced_info[d] = 1;
+    forced_value[d] = penalty;
+    rhs[d] = penalty * value;
+  }
+  else {
+    elim_info[d] = (kind == 1) ? kElimRow : kElimRowCol;
+    elim_value[d] = value;
+  }
+}
+
+// Row+column elimination, phase 1: rhs_j -= A[j,i] * g_i for every eliminated
+// column i != j of a non-eliminated row j, and A[j,i] = 0 (Aleph _fillMatrix,
+// femutils/AlephDoFLinearSystem.cc:539-565).
+__global__ void k_elim_columns(int64_t n_rows, const int64_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                               double* __restrict__ vals, const uint8_t* __restrict__ elim_info,
+                               const double* __restrict__ elim_value, double* __restrict__ rhs)
+{
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_rows) return;
+  if (elim_info[j] != 0) return;
+  double acc = 0.0;
+  for (int64_t k = rows[j]; k < rows[j + 1]; ++k) {
+    int32_t i = cols[k];
+    if (i != (int32_t)j && i < n_rows && elim_info[i] == kElimRowCol) {
+      acc += vals[k] * elim_value[i];
+      vals[k] = 0.0;
+    }
+  }
+  if (acc != 0.0) rhs[j] -= acc;
+}
+
+// _applyRowElimination then _applyForcedValuesToLhs
+// (femutils/HypreDoFLinearSystem.cc:319-382).
+__global__ void k_apply_bcs(int64_t n_rows, const int64_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                            double* __restrict__ vals, const uint8_t* __restrict__ forced_info,
+                            const double* __restrict__ forced_value, const uint8_t* __restrict__ elim_info,
+                            const double* __restrict__ elim_value, double* __restrict__ rhs)
+{
+  int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n_rows) return;
+  const uint8_t ei = elim_info[d];
+  const uint8_t fi = forced_info[d];
+  if (!ei && !fi) return;
+  const int64_t b = rows[d], e = rows[d + 1];
+  if (ei) {
+    for (int64_t k = b; k < e; ++k) vals[k] = (cols[k] == (int32_t)d) ? 1.0 : 0.0;
+    rhs[d] = elim_value[d];
+  }
+  if (fi) {
+    for (int64_t k = b; k < e; ++k)
+      if (cols[k] == (int32_t)d) {
+        vals[k] = forced_value[d];
+        break;
+      }
+  }
+}
+
+__global__ void k_point_update(const int64_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                               double* __restrict__ vals, int32_t row, int32_t col, double v, int set,
+                               int32_t* __restrict__ found)
+{
+  if (threadIdx.x != 0) return;
+  for (int64_t k = rows[row]; k < rows[row + 1]; ++k)
+    if (cols[k] == col) {
+      if (set)
+        vals[k] = v;
+      else
+        vals[k] += v;
+      *found = 1;
+      return;
+    }
+  *found = 0;
+}
+
+// ---------------------------------------------------------------- CG kernels
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d, 64);
+  return v;
+}
+
+__device__ __forceinline__ double block_sum(double v)
+{
+  __shared__ double ws[kThreads / 64];
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) ws[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += ws[w];
+  }
+  __syncthreads();
+  return s;  // valid in thread 0
+}
+
+__device__ __forceinline__ int64_t xcd_swizzle(int64_t b, int64_t nb)
+{
+  const int64_t q = nb >> 3, rem = nb & 7;
+  const int64_t x = b & 7, i = b >> 3;
+  return x * q + (x < rem ? x : rem) + i;
+}
+
+// CSR SpMV y = A x over a block of rows (CSR-stream: the block's contiguous
+// value/column segment is read with coalesced loads, products staged in LDS,
+// one lane per row reduces its products).  DOT: block partial of x[r]*y[r].
+template <bool DOT>
+__global__ __launch_bounds__(kThreads) void k_spmv_stream(int64_t n_rows, const int64_t* __restrict__ rows,
+                                                          const int32_t* __restrict__ cols,
+                                                          const double* __restrict__ vals,
+                                                          const double* __restrict__ x, double* __restrict__ y,
+                                                          double* __restrict__ partial)
+{
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* prod = reinterpret_cast<double*>(smem);
+  const int rpb = blockDim.x;
+  const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t r0 = blk * rpb;
+  const int64_t r1 = (r0 + rpb < n_rows) ? r0 + rpb : n_rows;
+  const int64_t seg0 = rows[r0], seglen = rows[r1] - seg0;
+  for (int64_t t = threadIdx.x; t < seglen; t += rpb) prod[t] = vals[seg0 + t] * x[cols[seg0 + t]];
+  __syncthreads();
+  const int64_t r = r0 + threadIdx.x;
+  double d = 0.0;
+  if (r < r1) {
+    double s = 0.0;
+    for (int64_t k = rows[r] - seg0, e = rows[r + 1] - seg0; k < e; ++k) s += prod[k];
+    y[r] = s;
+    if (DOT) d = x[r] * s;
+  }
+  if (DOT) {
+    double bs = block_sum(d);
+    if (threadIdx.x == 0) partial[blockIdx.x] = bs;
+  }
+}
+
+// Fallback for segments that do not fit LDS: one lane per row.
+template <bool DOT>
+__global__ __launch_bounds__(kThreads) void k_spmv_row(int64_t n_rows, const int64_t* __restrict__ rows,
+                                                       const int32_t* __restrict__ cols,
+                                                       const double* __restrict__ vals, const double* __restrict__ x,
+                                                       double* __restrict__ y, double* __restrict__ partial)
+{
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double d = 0.0;
+  if (r < n_rows) {
+    double s = 0.0;
+    for (int64_t k = rows[r]; k < rows[r + 1]; ++k) s += vals[k] * x[cols[k]];
+    y[r] = s;
+    if (DOT) d = x[r] * s;
+  }
+  if (DOT) {
+    double bs = block_sum(d);
+    if (threadIdx.x == 0) partial[blockIdx.x] = bs;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_reduce(int64_t n, const double* __restrict__ partial,
+                                                 double* __restrict__ out)
+{
+  __shared__ double ws[16];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += partial[i];
+  s = wave_sum(s);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) ws[wid] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += ws[w];
+    *out = t;
+  }
+}
+
+// Jacobi preconditioner + constraint-row flag: a row whose diagonal exceeds
+// the rest of the row by > 1e10 (penalty P = 1e30, eliminated identity rows)
+// is excluded from the reference value of the stopping test (same rule as
+// oracle/oracle.c::orc_pcg_jacobi).
+__global__ void k_inv_diag(int64_t n_rows, const int64_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                           const double* __restrict__ vals, double* __restrict__ dinv, uint8_t* __restrict__ cons)
+{
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  double d = 0.0, off = 0.0;
+  for (int64_t k = rows[r]; k < rows[r + 1]; ++k) {
+    if (cols[k] == (int32_t)r)
+      d = vals[k];
+    else
+      off += fabs(vals[k]);
+  }
+  dinv[r] = (d != 0.0) ? 1.0 / d : 0.0;
+  cons[r] = fabs(d) > 1e10 * off ? 1 : 0;
+}
+
+constexpr int kVecBlocks = 2048;
+
+// x = 0, r = b, z = D^-1 r, p = z ; partials r.z (all rows) and r.z (free rows)
+__global__ __launch_bounds__(kThreads) void k_cg_init(int64_t n, const double* __restrict__ b, double* __restrict__ x,
+                                                      double* __restrict__ r, double* __restrict__ z,
+                                                      double* __restrict__ p, const double* __restrict__ dinv,
+                                                      const uint8_t* __restrict__ cons, double* __restrict__ partial,
+                                                      double* __restrict__ partial_free)
+{
+  double s = 0.0, sf = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double ri = b[i];
+    double zi = ri * dinv[i];
+    x[i] = 0.0;
+    r[i] = ri;
+    z[i] = zi;
+    p[i] = zi;
+    s += ri * zi;
+    if (!cons[i]) sf += ri * zi;
+  }
+  double bs = block_sum(s);
+  double bf = block_sum(sf);
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = bs;
+    partial_free[blockIdx.x] = bf;
+  }
+}
+
+// alpha = rz/pq ; x += alpha p ; r -= alpha q ; z = D^-1 r ; partial r.z (and r.r)
+__global__ __launch_bounds__(kThreads) void k_cg_update(int64_t n, const double* __restrict__ scal, int par,
+                                                        double* __restrict__ x, const double* __restrict__ p,
+                                                        double* __restrict__ r, const double* __restrict__ q,
+                                                        double* __restrict__ z, const double* __restrict__ dinv,
+                                                        double* __restrict__ partial)
+{
+  const double rz = scal[par], pq = scal[2];
+  const double alpha = (pq != 0.0) ? rz / pq : 0.0;
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    x[i] += alpha * p[i];
+    double ri = r[i] - alpha * q[i];
+    r[i] = ri;
+    double zi = ri * dinv[i];
+    z[i] = zi;
+    s += ri * zi;
+  }
+  double bs = block_sum(s);
+  if (threadIdx.x == 0) partial[blockIdx.x] = bs;
+}
+
+// beta = rz_new / rz_old ; p = z + beta p
+__global__ __launch_bounds__(kThreads) void k_cg_dir(int64_t n, const double* __restrict__ scal, int par,
+                                                     const double* __restrict__ z, double* __restrict__ p)
+{
+  const double rz_old = scal[par], rz_new = scal[par ^ 1];
+  const double beta = (rz_old != 0.0) ? rz_new / rz_old : 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = z[i] + beta * p[i];
+}
+
+__global__ __launch_bounds__(kThreads) void k_dot(int64_t n, const double* __restrict__ a,
+                                                  const double* __restrict__ b, double* __restrict__ partial)
+{
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    s += a[i] * b[i];
+  double bs = block_sum(s);
+  if (threadIdx.x == 0) partial[blockIdx.x] = bs;
+}
+
+// ---------------------------------------------------------------- helpers
+struct SpmvPlan {
+  int rpb = 0;          // rows per block (0: row kernel)
+  int64_t max_seg = 0;
+  int64_t nblocks = 0;
+};
+
+__global__ void k_block_seg(int64_t n_rows, int rpb, const int64_t* __restrict__ row_ptr, unsigned long long* out)
+{
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t r0 = b * rpb;
+  if (r0 >= n_rows) return;
+  int64_t r1 = r0 + rpb < n_rows ? r0 + rpb : n_rows;
+  atomicMax(out, (unsigned long long)(row_ptr[r1] - row_ptr[r0]));
+}
+
+SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows)
+{
+  SpmvPlan pl;
+  DevBuf<unsigned long long> mx;
+  mx.alloc(1);
+  AFEM_HIP(hipMemsetAsync(mx.p, 0, mx.bytes(), ctx.stream));
+  int64_t nb = (n_rows + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(k_block_seg, dim3(grid_for(nb, 256)), dim3(256), 0, ctx.stream, n_rows, kThreads, rows, mx.p);
+  AFEM_LAUNCHED();
+  unsigned long long hm = 0;
+  AFEM_HIP(hipMemcpyAsync(&hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  pl.nblocks = nb;
+  if (hm * 8ull <= 64ull * 1024ull) {
+    pl.rpb = kThreads;
+    pl.max_seg = (int64_t)hm;
+  }
+  return pl;
+}
+
+void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* rows, const int32_t* cols,
+                 const double* vals, const double* x, double* y, double* partial)
+{
+  const unsigned nb = (unsigned)pl.nblocks;
+  if (pl.rpb) {
+    if (partial)
+      hipLaunchKernelGGL(k_spmv_stream<true>, dim3(nb), dim3(kThreads), (size_t)pl.max_seg * 8, ctx.stream, n_rows,
+                         rows, cols, vals, x, y, partial);
+    else
+      hipLaunchKernelGGL(k_spmv_stream<false>, dim3(nb), dim3(kThreads), (size_t)pl.max_seg * 8, ctx.stream, n_rows,
+                         rows, cols, vals, x, y, partial);
+  }
+  else {
+    if (partial)
+      hipLaunchKernelGGL(k_spmv_row<true>, dim3(nb), dim3(kThreads), 0, ctx.stream, n_rows, rows, cols, vals, x, y,
+                         partial);
+    else
+      hipLaunchKernelGGL(k_spmv_row<false>, dim3(nb), dim3(kThreads), 0, ctx.stream, n_rows, rows, cols, vals, x, y,
+                         partial);
+  }
+  AFEM_LAUNCHED();
+}
+
+void reduce_to(Ctx& ctx, const double* partial, int64_t n, double* out)
+{
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, ctx.stream, n, partial, out);
+  AFEM_LAUNCHED();
+}
+
+void require_csr(LinearSystem& ls)
+{
+  AFEM_REQUIRE(ls.has_csr, AFEM_ERR_STATE, "linear system has no matrix (setCSRValues / toLinearSystem / matrixAddValue)");
+}
+
+}  // namespace
+
+void ls_set_list(LinearSystem& ls, const int32_t* ids, int64_t n, int mem, int kind, double value, double penalty)
+{
+  Ctx& ctx = *ls.ctx;
+  if (n <= 0) return;
+  const int32_t* dids = ids;
+  DevBuf<int32_t> tmp;
+  if (mem == AFEM_MEM_HOST) {
+    tmp.alloc(n);
+    AFEM_HIP(hipMemcpyAsync(tmp.p, ids, tmp.bytes(), hipMemcpyHostToDevice, ctx.stream));
+    dids = tmp.p;
+  }
+  hipLaunchKernelGGL(k_set_list, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, ctx.stream, n, dids, kind, value,
+                     penalty, ls.n_rows, ls.forced_info.p, ls.forced_value.p, ls.elim_info.p, ls.elim_value.p,
+                     ls.rhs.p);
+  AFEM_LAUNCHED();
+  if (tmp.p) ctx.sync();
+}
+
+void ls_point_update(LinearSystem& ls, int32_t row, int32_t col, double v, bool set)
+{
+  Ctx& ctx = *ls.ctx;
+  AFEM_REQUIRE(row >= 0 && row < ls.csr_n, AFEM_ERR_ARG, "matrix{Add,Set}Value: row out of range");
+  DevBuf<int32_t> found;
+  found.alloc(1);
+  hipLaunchKernelGGL(k_point_update, dim3(1), dim3(64), 0, ctx.stream, ls.csr_rows, ls.csr_cols, ls.csr_vals, row,
+                     col, v, set ? 1 : 0, found.p);
+  AFEM_LAUNCHED();
+  int32_t h = 0;
+  AFEM_HIP(hipMemcpyAsync(&h, found.p, sizeof(h), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  AFEM_REQUIRE(h == 1, AFEM_ERR_NOT_FOUND, "matrix{Add,Set}Value: (row,col) is not in the CSR structure");
+}
+
+void ls_build_from_host_coo(LinearSystem& ls)
+{
+  // Aleph semantics: set values override added ones; eliminated rows are
+  // handled by the BC kernels (elimination info set from the host map).
+  Ctx& ctx = *ls.ctx;
+  std::map<std::pair<int32_t, int32_t>, double> merged = ls.add_map;
+  for (auto& kv : ls.set_map) merged[kv.first] = kv.second;
+  // rows must contain their diagonal for the Jacobi preconditioner
+  for (int64_t r = 0; r < ls.n_rows; ++r) merged.emplace(std::make_pair((int32_t)r, (int32_t)r), 0.0);
+  std::vector<int64_t> rows(ls.n_rows + 1, 0);
+  std::vector<int32_t> cols;
+  std::vector<double> vals;
+  cols.reserve(merged.size());
+  vals.reserve(merged.size());
+  for (auto& kv : merged) {
+    int32_t r = kv.first.first;
+    AFEM_REQUIRE(r >= 0 && r < ls.n_rows, AFEM_ERR_ARG, "matrixAddValue: row out of range");
+    AFEM_REQUIRE(kv.first.second >= 0 && kv.first.second < ls.n_cols, AFEM_ERR_ARG,
+                 "matrixAddValue: column out of range");
+    rows[r + 1]++;
+    cols.push_back(kv.first.second);
+    vals.push_back(kv.second);
+  }
+  for (int64_t r = 0; r < ls.n_rows; ++r) rows[r + 1] += rows[r];
+  ls.own_rows.alloc(rows.size());
+  ls.own_cols.alloc(cols.size());
+  ls.own_vals.alloc(vals.size());
+  AFEM_HIP(hipMemcpyAsync(ls.own_rows.p, rows.data(), ls.own_rows.bytes(), hipMemcpyHostToDevice, ctx.stream));
+  AFEM_HIP(hipMemcpyAsync(ls.own_cols.p, cols.data(), ls.own_cols.bytes(), hipMemcpyHostToDevice, ctx.stream));
+  AFEM_HIP(hipMemcpyAsync(ls.own_vals.p, vals.data(), ls.own_vals.bytes(), hipMemcpyHostToDevice, ctx.stream));
+  // host eliminations -> device info arrays
+  for (auto& kv : ls.host_elim) {
+    int32_t d = kv.first;
+    uint8_t info = kv.second.first;
+    double v = kv.second.second;
+    AFEM_HIP(hipMemcpyAsync(ls.elim_info.p + d, &info, 1, hipMemcpyHostToDevice, ctx.stream));
+    AFEM_HIP(hipMemcpyAsync(ls.elim_value.p + d, &v, sizeof(double), hipMemcpyHostToDevice, ctx.stream));
+    ctx.sync();
+  }
+  ctx.sync();
+  ls.has_csr = true;
+  ls.csr_n = ls.n_rows;
+  ls.csr_nnz = (int64_t)cols.size();
+  ls.csr_rows = ls.own_rows.p;
+  ls.csr_cols = ls.own_cols.p;
+  ls.csr_vals = ls.own_vals.p;
+}
+
+void ls_apply_bcs(LinearSystem& ls)
+{
+  Ctx& ctx = *ls.ctx;
+  require_csr(ls);
+  // row+column elimination needs a column pass first (only when present)
+  bool has_rc = false;
+  for (auto& kv : ls.host_elim)
+    if (kv.second.first == kElimRowCol) has_rc = true;
+  if (has_rc) {
+    hipLaunchKernelGGL(k_elim_columns, dim3(grid_for(ls.n_rows, kThreads)), dim3(kThreads), 0, ctx.stream, ls.n_rows,
+                       ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.elim_info.p, ls.elim_value.p, ls.rhs.p);
+    AFEM_LAUNCHED();
+  }
+  hipLaunchKernelGGL(k_apply_bcs, dim3(grid_for(ls.n_rows, kThreads)), dim3(kThreads), 0, ctx.stream, ls.n_rows,
+                     ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.forced_info.p, ls.forced_value.p, ls.elim_info.p,
+                     ls.elim_value.p, ls.rhs.p);
+  AFEM_LAUNCHED();
+}
+
+void ls_spmv(LinearSystem& ls, const double* x, double* y)
+{
+  Ctx& ctx = *ls.ctx;
+  require_csr(ls);
+  if (ls.halo) halo_exchange(*ls.halo, ctx, const_cast<double*>(x));
+  SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, ls.n_rows);
+  launch_spmv(ctx, pl, ls.n_rows, ls.csr_rows, ls.csr_cols, ls.csr_vals, x, y, nullptr);
+}
+
+void ls_solve(LinearSystem& ls, afem_solve_stats* st)
+{
+  Ctx& ctx = *ls.ctx;
+  ctx.set_device();
+  if (!ls.has_csr && (!ls.add_map.empty() || !ls.set_map.empty() || !ls.host_elim.empty()))
+    ls_build_from_host_coo(ls);
+  require_csr(ls);
+  AFEM_REQUIRE(ls.csr_n == ls.n_rows, AFEM_ERR_ARG, "CSR view row count differs from the linear system size");
+  ls_apply_bcs(ls);
+
+  const int64_t n = ls.n_rows;
+  if (ls.r.n != (size_t)n) {
+    ls.r.alloc(n);
+    ls.z.alloc(n);
+    ls.q.alloc(n);
+    ls.dinv.alloc(n);
+    ls.p.alloc(ls.n_cols);
+    AFEM_HIP(hipMemsetAsync(ls.p.p, 0, ls.p.bytes(), ctx.stream));
+  }
+  SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, n);
+  const int64_t n_part = 2 * std::max<int64_t>(pl.nblocks, kVecBlocks);
+  if (ls.partial.n < (size_t)n_part) ls.partial.alloc(n_part);
+  if (ls.cons.n != (size_t)n) ls.cons.alloc(n);
+  if (ls.scal.n < 8) ls.scal.alloc(8);
+  if (!ls.pinned) AFEM_HIP(hipHostMalloc(reinterpret_cast<void**>(&ls.pinned), 8 * sizeof(double), hipHostMallocDefault));
+  const unsigned vb = (unsigned)std::min<int64_t>(kVecBlocks, std::max<int64_t>(1, (n + kThreads - 1) / kThreads));
+
+  AFEM_HIP(hipEventRecord(ctx.ev0, ctx.stream));
+  hipLaunchKernelGGL(k_inv_diag, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, ctx.stream, n, ls.csr_rows,
+                     ls.csr_cols, ls.csr_vals, ls.dinv.p, ls.cons.p);
+  AFEM_LAUNCHED();
+  hipLaunchKernelGGL(k_cg_init, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.sol.p, ls.r.p, ls.z.p, ls.p.p,
+                     ls.dinv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
+  AFEM_LAUNCHED();
+  double* scal = ls.scal.p;  // [0],[1]: r.z ping-pong, [2]: p.q, [3]: r0.z0 over free rows, [4]: r.r
+  reduce_to(ctx, ls.partial.p, vb, scal + 0);
+  reduce_to(ctx, ls.partial.p + vb, vb, scal + 3);
+  Comm* comm = ls.halo ? ls.halo->comm : nullptr;
+  if (comm) {
+    comm_allreduce(comm, ctx, scal + 0, 1);
+    comm_allreduce(comm, ctx, scal + 3, 1);
+  }
+  AFEM_HIP(hipMemcpyAsync(ls.pinned, scal, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  // reference value of the stopping test: r0.z0 over the free rows (all rows
+  // if every row is a constraint)
+  double rz0 = ls.pinned[3] > 0.0 ? ls.pinned[3] : ls.pinned[0];
+
+  const afem_solver_opts& o = ls.opts;
+  const bool fixed = o.fixed_iterations > 0;
+  const int max_it = fixed ? o.fixed_iterations : o.max_iter;
+  const int check = o.check_every > 0 ? o.check_every : 8;
+  double rel = rz0 > 0 ? std::sqrt(std::fabs(ls.pinned[0] / rz0)) : 0.0;
+  int it = 0;
+  bool converged = fixed ? false : (ls.pinned[0] == 0.0 || rel <= o.rtol);
+  while (!converged && it < max_it) {
+    const int par = it & 1;
+    if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
+    launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p);
+    reduce_to(ctx, ls.partial.p, pl.nblocks, scal + 2);
+    if (comm) comm_allreduce(comm, ctx, scal + 2, 1);
+    hipLaunchKernelGGL(k_cg_update, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p, ls.r.p,
+                       ls.q.p, ls.z.p, ls.dinv.p, ls.partial.p);
+    AFEM_LAUNCHED();
+    reduce_to(ctx, ls.partial.p, vb, scal + (par ^ 1));
+    if (comm) comm_allreduce(comm, ctx, scal + (par ^ 1), 1);
+    hipLaunchKernelGGL(k_cg_dir, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.z.p, ls.p.p);
+    AFEM_LAUNCHED();
+    ++it;
+    if (!fixed && (it % check == 0 || it == max_it)) {
+      AFEM_HIP(hipMemcpyAsync(ls.pinned, scal, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+      ctx.sync();
+      const double rz = ls.pinned[it & 1];
+      rel = std::sqrt(std::fabs(rz / rz0));
+      if (rel <= o.rtol) converged = true;
+      if (!converged && o.atol > 0) {
+        hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.r.p, ls.r.p, ls.partial.p);
+        AFEM_LAUNCHED();
+        reduce_to(ctx, ls.partial.p, vb, scal + 4);
+        if (comm) comm_allreduce(comm, ctx, scal + 4, 1);
+        AFEM_HIP(hipMemcpyAsync(ls.pinned + 4, scal + 4, sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+        ctx.sync();
+        if (std::sqrt(ls.pinned[4]) <= o.atol) converged = true;
+      }
+    }
+  }
+  AFEM_HIP(hipEventRecord(ctx.ev1, ctx.stream));
+  // final residual norm (recurrence residual) and relative preconditioned residual
+  hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.r.p, ls.r.p, ls.partial.p);
+  AFEM_LAUNCHED();
+  reduce_to(ctx, ls.partial.p, vb, scal + 4);
+  if (comm) comm_allreduce(comm, ctx, scal + 4, 1);
+  AFEM_HIP(hipMemcpyAsync(ls.pinned, scal, 5 * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  float ms = 0.f;
+  AFEM_HIP(hipEventElapsedTime(&ms, ctx.ev0, ctx.ev1));
+  rel = rz0 > 0 ? std::sqrt(std::fabs(ls.pinned[it & 1] / rz0)) : 0.0;
+  if (ls.halo) halo_exchange(*ls.halo, ctx, ls.sol.p);  // m_u.synchronize()
+  if (st) {
+    st->iterations = it;
+    st->converged = fixed ? (rel <= o.rtol) : converged;
+    st->rel_residual = rel;
+    st->residual_norm = std::sqrt(std::fabs(ls.pinned[4]));
+    st->solve_ms = ms;
+  }
+}
+
+}  // namespace afem

@@ -1,0 +1,294 @@
+/*
+ * arcanefem_amd.h — C ABI of the MI355X-native FEM assembly + CG path.
+ *
+ * This is the drop-in boundary for the reference's linear-system plugin
+ * surface (toutane/arcanefem @ 2025-02-20, paths relative to its root):
+ *
+ *   DoFLinearSystemImpl        femutils/DoFLinearSystem.h:84-110   -> afem_ls_*
+ *   IDoFLinearSystemFactory    femutils/IDoFLinearSystemFactory.h:34-44
+ *                                                                  -> afem_ls_create
+ *   CSRFormatView              femutils/DoFLinearSystem.h:42-76    -> afem_csr_view
+ *   BSRFormat<NB_DOF>          femutils/BSRFormat.h:353-1140       -> afem_bsr_*
+ *   FemDoFsOnNodes             femutils/FemDoFsOnNodes.cc:71-128   -> DoF lid = node_lid*k + i
+ *   Gpu BC kernels             femutils/ArcaneFemFunctionsGpu.h:401-482
+ *                                                                  -> afem_ls_dirichlet_* / afem_bsr_assemble_*
+ *
+ * Conventions
+ *   - Every function returns AFEM_OK (0) or an AFEM_ERR_* code and never
+ *     throws; afem_last_error() returns the thread-local message of the last
+ *     failure (the reference raises ARCANE_FATAL / NotImplementedException /
+ *     ArgumentException; the same conditions map to the codes below).
+ *   - Handles are opaque; the caller owns them and releases them with the
+ *     matching *_destroy.  Device arrays returned by *_view / *_rhs / ... are
+ *     owned by the handle and stay valid until it is destroyed (or, for a CSR
+ *     view, until the structure is recomputed).
+ *   - Pointers passed with mem == AFEM_MEM_HOST are host memory and are copied;
+ *     with AFEM_MEM_DEVICE they are device pointers on the handle's device.
+ *   - All device work of a handle is enqueued on its context's HIP stream;
+ *     functions that return host data synchronise that stream.
+ *   - Index types: DoF / node / cell local ids are int32 (as the reference's
+ *     Int32 local ids); row offsets are int64 internally so a single
+ *     subdomain may exceed 2^31 non-zeros (288 GB of HBM allows ~1e9 DoF).
+ *   - One host thread drives one handle (the reference is not thread-safe
+ *     either, SURVEY.md §8b "Threading").
+ */
+#ifndef ARCANEFEM_AMD_H
+#define ARCANEFEM_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AFEM_OK 0
+#define AFEM_ERR_ARG 1        /* ArgumentException */
+#define AFEM_ERR_HIP 2        /* HIP runtime / device failure */
+#define AFEM_ERR_NOT_IMPL 3   /* NotImplementedException */
+#define AFEM_ERR_STATE 4      /* call out of order (e.g. assemble before sparsity) */
+#define AFEM_ERR_NOT_FOUND 5  /* (row,col) not in the sparsity (BSRMatrix::findValueIndex throws) */
+#define AFEM_ERR_COMM 6       /* RCCL failure */
+#define AFEM_ERR_LIMIT 7      /* an implementation limit was exceeded (message says which) */
+
+#define AFEM_MEM_HOST 0
+#define AFEM_MEM_DEVICE 1
+
+typedef struct afem_ctx afem_ctx;   /* device + HIP stream (+ timing events) */
+typedef struct afem_mesh afem_mesh; /* device-resident P1 mesh (Arcane IMesh subset) */
+typedef struct afem_bsr afem_bsr;   /* BSRFormat<NB_DOF> */
+typedef struct afem_ls afem_ls;     /* DoFLinearSystemImpl */
+typedef struct afem_comm afem_comm; /* RCCL communicator (IParallelMng subset) */
+
+/* ---------------------------------------------------------------- basics */
+const char* afem_last_error(void);
+int afem_version(void); /* major*10000 + minor*100 + patch */
+int afem_device_count(int* count);
+
+/* ---------------------------------------------------------------- context */
+/* hip_stream may be NULL: the context then creates and owns a non-blocking
+ * stream on `device`. */
+int afem_ctx_create(int device, void* hip_stream, afem_ctx** out);
+int afem_ctx_destroy(afem_ctx* ctx);
+int afem_ctx_synchronize(afem_ctx* ctx);
+int afem_ctx_stream(afem_ctx* ctx, void** hip_stream);
+/* Event timing on the context stream: afem_ctx_timer_start(), enqueue work,
+ * afem_ctx_timer_stop(&ms) (synchronises). */
+int afem_ctx_timer_start(afem_ctx* ctx);
+int afem_ctx_timer_stop(afem_ctx* ctx, float* ms);
+/* Event pool (AFEM_EVENT_SLOTS events per context) for timing individual
+ * launches inside a pipelined region without synchronising: record slots on
+ * the context stream, read the elapsed time between two slots afterwards
+ * (afem_ctx_event_elapsed waits for the later one). */
+#define AFEM_EVENT_SLOTS 256
+int afem_ctx_event_record(afem_ctx* ctx, int slot);
+int afem_ctx_event_elapsed(afem_ctx* ctx, int slot_a, int slot_b, float* ms);
+/* Device memory helpers for callers without their own allocator. */
+int afem_malloc(afem_ctx* ctx, size_t bytes, void** dptr);
+int afem_free(afem_ctx* ctx, void* dptr);
+int afem_memcpy(afem_ctx* ctx, void* dst, const void* src, size_t bytes, int dst_mem, int src_mem);
+
+/* ---------------------------------------------------------------- mesh */
+typedef struct afem_mesh_info {
+  int32_t dim;           /* 2 or 3 */
+  int32_t nb_node_per_cell; /* 3 (TRIA3) or 4 (TETRA4) */
+  int64_t n_nodes;       /* local nodes: owned first, then ghosts */
+  int64_t n_own_nodes;   /* nodes [0, n_own_nodes) are owned (isOwn()) */
+  int64_t n_cells;       /* local cells (own + one ghost layer) */
+} afem_mesh_info;
+
+/* Mesh from caller arrays: cell_node[n_cells*nv] (int32 local node ids, nodes
+ * [0,n_own_nodes) owned) and coords[n_nodes*3] (x,y,z per node, the layout of
+ * Arcane's VariableNodeReal3). */
+int afem_mesh_create(afem_ctx* ctx, int dim, int nb_node_per_cell, int64_t n_nodes, int64_t n_own_nodes,
+                     int64_t n_cells, const int32_t* cell_node, const double* coords, int mem, afem_mesh** out);
+/* Synthetic jittered structured mesh generated on the device (DESIGN.md
+ * "Synthetic inputs"): unit square split in 2 triangles per square (dim 2)
+ * or box [0,1]^2 x [0,nz/n] split in 6 Kuhn tetrahedra per cube (dim 3),
+ * coordinate jitter uniform in +-jitter*h/2, seeded hash.  The global mesh is
+ * cut in `nranks` slabs along the last axis and this call builds the slab of
+ * `rank` with one ghost node/cell layer (nranks = 1: the whole mesh). */
+int afem_mesh_create_structured(afem_ctx* ctx, int dim, int n, int nz, double jitter, uint64_t seed, int nranks,
+                                int rank, afem_mesh** out);
+int afem_mesh_get_info(const afem_mesh* mesh, afem_mesh_info* info);
+/* Copies to host: cell_node[n_cells*nv], coords[n_nodes*3], local_to_global[n_nodes]
+ * (any pointer may be NULL). local_to_global is the identity for meshes from
+ * afem_mesh_create. */
+int afem_mesh_download(afem_mesh* mesh, int32_t* cell_node, double* coords, int64_t* local_to_global);
+/* Structured meshes: local ids of the owned nodes on the z = 0 face (y = 0 in
+ * 2D), i.e. the Dirichlet group of the benchmark configs.  *count receives the
+ * size; ids may be NULL to query it. */
+int afem_mesh_structured_bottom_nodes(afem_mesh* mesh, int32_t* ids, int64_t* count);
+int afem_mesh_destroy(afem_mesh* mesh);
+
+/* ---------------------------------------------------------------- BSRFormat */
+/* CSR / BSR arrays (device pointers).  rows[n_block_rows+1] has the n+1
+ * sentinel (the reference's CSRFormatView::rows has none, its row end is
+ * derived, femutils/HypreDoFLinearSystem.cc:140-141; afem_bsr_export_csr32
+ * produces exactly that layout).  Columns are sorted ascending within a row. */
+typedef struct afem_csr_view {
+  int64_t n_block_rows;
+  int64_t n_block_cols;  /* local columns (owned + ghost nodes) */
+  int64_t nnz_blocks;
+  int32_t block_size;    /* NB_DOF */
+  int32_t ordered_per_block; /* 1: values[k*bs*bs + i*bs + j]; 0: CSR-row order */
+  const int64_t* rows;   /* device [n_block_rows+1] */
+  const int32_t* columns;/* device [nnz_blocks] */
+  double* values;        /* device [nnz_blocks*bs*bs] */
+} afem_csr_view;
+
+/* BSRFormat::initialize (femutils/BSRFormat.h:389-409). use_csr_in_linear_system
+ * selects the "ordered per row" value layout (values of a scalar row contiguous,
+ * as Hypre consumes them) instead of "ordered per block". */
+int afem_bsr_create(afem_mesh* mesh, int nb_dof, int use_csr_in_linear_system, afem_bsr** out);
+/* BSRFormat::computeSparsity (femutils/BSRFormat.h:749-781): rows are the
+ * owned nodes, columns every node sharing an edge (plus the diagonal).  Also
+ * builds the row-local incidence table the assembly kernels gather from. */
+int afem_bsr_compute_sparsity(afem_bsr* bsr);
+/* BSRFormat::assembleBilinear with the P1 Laplacian element of
+ * modules/poisson/FemModule.h:139-186, scaled by `coef`, fused with
+ * applyConstantSourceToRhs (femutils/ArcaneFemFunctionsGpu.h:401-429) when
+ * rhs != NULL: rhs[dof] = sum f*|K|/nv over cells of own node dof (rhs is
+ * overwritten, not accumulated; device pointer of length n_own_nodes).
+ * Every matrix value of the structure is written (no separate zeroing). */
+int afem_bsr_assemble_poisson_p1(afem_bsr* bsr, double coef, double f, double* rhs);
+/* Block-2 P1 elasticity on triangles (modules/elasticity/FemModule.h:112-140),
+ * mu2 = 2*mu, lambda as in modules/elasticity/FemModule.cc:130-134. */
+int afem_bsr_assemble_elasticity_p1(afem_bsr* bsr, double lambda, double mu2);
+int afem_bsr_reset_values(afem_bsr* bsr);                       /* resetMatrixValues */
+int afem_bsr_set_value(afem_bsr* bsr, int32_t row, int32_t col, double v); /* BSRMatrix::setValue */
+int afem_bsr_get_value(afem_bsr* bsr, int32_t row, int32_t col, double* v); /* BSRMatrix::getValue */
+int afem_bsr_view(afem_bsr* bsr, afem_csr_view* view);
+/* Structure statistics (for roofline accounting and diagnostics). */
+typedef struct afem_bsr_stats {
+  int64_t n_incidences;     /* (owned row, incident cell) pairs = entries of the incidence table */
+  int64_t inc_table_entries;/* incidence table size including sliced-ELL padding */
+  int32_t max_row_len;      /* max non-zero blocks in a row */
+  int32_t rows_per_block;   /* assembly workgroup rows (0: global-memory accumulation variant) */
+  int64_t max_seg;          /* max non-zeros of one workgroup's row block */
+} afem_bsr_stats;
+int afem_bsr_get_stats(afem_bsr* bsr, afem_bsr_stats* stats);
+/* Copies the scalar CSR expansion to host in the reference's CSRFormatView
+ * layout (BSRMatrix::toCsr, femutils/BSRFormat.h:194-256): rows[n] without
+ * sentinel, rows_nb_column[n], columns[nnz], values[nnz] with n = rows*NB_DOF.
+ * Any pointer may be NULL; sizes via afem_bsr_get_sizes. */
+int afem_bsr_get_sizes(afem_bsr* bsr, int64_t* n_scalar_rows, int64_t* nnz_scalar);
+int afem_bsr_export_csr32(afem_bsr* bsr, int32_t* rows, int32_t* rows_nb_column, int32_t* columns, double* values);
+/* Copies the internal (block) arrays to host. */
+int afem_bsr_download(afem_bsr* bsr, int64_t* rows, int32_t* columns, double* values);
+/* BSRFormat::toLinearSystem (femutils/BSRFormat.h:414-430): hands the matrix to
+ * the linear system as a CSR view (no copy).  The view stays owned by bsr. */
+int afem_bsr_to_linear_system(afem_bsr* bsr, afem_ls* ls);
+int afem_bsr_destroy(afem_bsr* bsr);
+
+/* ---------------------------------------------------------------- linear system */
+#define AFEM_SOLVER_AUTO 0   /* Jacobi-PCG (the reference's Auto picks a direct solver below 500 rows) */
+#define AFEM_SOLVER_PCG 1    /* Jacobi (diagonal) preconditioned CG */
+
+typedef struct afem_solver_opts {
+  int32_t method;       /* AFEM_SOLVER_* */
+  int32_t max_iter;     /* default 10000 */
+  double rtol;          /* stop when sqrt(r.z/r0.z0) <= rtol (default 1e-15, the reference epsilon) */
+  double atol;          /* or when ||r||_2 <= atol (default 0 = off) */
+  int32_t check_every;  /* iterations between host convergence checks (default 8) */
+  int32_t fixed_iterations; /* >0: run exactly this many iterations, no test (benchmarking) */
+} afem_solver_opts;
+
+typedef struct afem_solve_stats {
+  int32_t iterations;
+  int32_t converged;
+  double rel_residual;  /* sqrt(r.z / r0.z0) */
+  double residual_norm; /* ||b - A x||_2 over all ranks (recurrence residual) */
+  double solve_ms;      /* device time of the solve */
+} afem_solve_stats;
+
+/* IDoFLinearSystemFactory::createInstance: a linear system over n_rows owned
+ * DoFs; n_cols_local >= n_rows counts owned + ghost DoFs (column space of a
+ * subdomain). */
+int afem_ls_create(afem_ctx* ctx, int64_t n_rows, int64_t n_cols_local, afem_ls** out);
+int afem_ls_set_solver_options(afem_ls* ls, const afem_solver_opts* opts);
+int afem_ls_get_solver_options(afem_ls* ls, afem_solver_opts* opts);
+/* matrixAddValue / matrixSetValue.  With a CSR view set (Hypre semantics,
+ * femutils/HypreDoFLinearSystem.cc:148-156) they update the view in place and
+ * fail with AFEM_ERR_NOT_FOUND outside the structure.  Without a view they are
+ * recorded on the host (Aleph semantics, femutils/AlephDoFLinearSystem.cc:
+ * 192-223: adds of 0 skipped, a set overrides every add at solve time) and
+ * turned into a device CSR by afem_ls_solve. */
+int afem_ls_matrix_add_value(afem_ls* ls, int32_t row, int32_t col, double v);
+int afem_ls_matrix_set_value(afem_ls* ls, int32_t row, int32_t col, double v);
+/* eliminateRow / eliminateRowColumn (femutils/DoFLinearSystem.h:161-190,
+ * semantics of femutils/AlephDoFLinearSystem.cc:501-583), applied at solve. */
+int afem_ls_eliminate_row(afem_ls* ls, int32_t row, double v);
+int afem_ls_eliminate_row_column(afem_ls* ls, int32_t row, double v);
+/* setCSRValues with the reference's CSRFormatView layout: rows[nb_row] (no
+ * sentinel; the last row ends at nb_nz), rows_nb_column[nb_row] (may be NULL),
+ * columns[nb_nz], values[nb_nz].  The view is non-owning and must stay valid
+ * until solve (femutils/DoFLinearSystem.h:251-258); values are updated in
+ * place by the BC kernels at solve. */
+int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows_nb_column, const int32_t* columns,
+                           double* values, int32_t nb_row, int32_t nb_nz, int mem);
+int afem_ls_has_set_csr_values(afem_ls* ls, int* has);
+int afem_ls_get_csr_values(afem_ls* ls, afem_csr_view* view);
+/* rhsVariable / solutionVariable / getForced{Info,Value} / getElimination{Info,Value}:
+ * device arrays of length n_rows (solution: n_cols_local, ghost part filled by
+ * the halo after a distributed solve). */
+int afem_ls_rhs(afem_ls* ls, double** dptr);
+int afem_ls_solution(afem_ls* ls, double** dptr);
+int afem_ls_forced_info(afem_ls* ls, uint8_t** dptr);
+int afem_ls_forced_value(afem_ls* ls, double** dptr);
+int afem_ls_elimination_info(afem_ls* ls, uint8_t** dptr);
+int afem_ls_elimination_value(afem_ls* ls, double** dptr);
+/* BoundaryConditionsHelpers::applyDirichletToNodeGroupViaPenalty
+ * (femutils/ArcaneFemFunctionsGpu.h:434-456): for each owned DoF of the list,
+ * forced_info = 1, forced_value = penalty, rhs = penalty * value. */
+int afem_ls_dirichlet_penalty(afem_ls* ls, const int32_t* dofs, int64_t n, double value, double penalty, int mem);
+/* ...ViaRowElimination (femutils/ArcaneFemFunctionsGpu.h:461-482): elimination_info = 1, value. */
+int afem_ls_dirichlet_row_elimination(afem_ls* ls, const int32_t* dofs, int64_t n, double value, int mem);
+/* _applyRowElimination + _applyForcedValuesToLhs (femutils/HypreDoFLinearSystem.cc:
+ * 319-382) on the CSR view; afem_ls_solve calls it, it is exposed so the
+ * assembly step can be timed with it. */
+int afem_ls_apply_boundary_conditions(afem_ls* ls);
+/* clearValues (femutils/HypreDoFLinearSystem.cc:180-187) */
+int afem_ls_clear_values(afem_ls* ls);
+/* solve: BCs into the CSR, then Jacobi-PCG from x0 = 0 (SequentialDoFLinearSystemImpl
+ * iterative branch, femutils/DoFLinearSystem.cc:137-151).  With a communicator
+ * attached the SpMV exchanges ghost values and the dot products are summed
+ * over ranks (RCCL). */
+int afem_ls_solve(afem_ls* ls, afem_solve_stats* stats);
+/* y[0:n_rows] = A x (x of length n_cols_local, ghost part exchanged first when
+ * a communicator is attached).  Device pointers. */
+int afem_ls_spmv(afem_ls* ls, const double* x, double* y);
+int afem_ls_destroy(afem_ls* ls);
+
+/* ---------------------------------------------------------------- communicator */
+#define AFEM_UNIQUE_ID_BYTES 128
+/* ncclGetUniqueId on the root rank; the bytes are broadcast by the caller
+ * (e.g. torch.distributed) and passed to afem_comm_create on every rank. */
+int afem_comm_unique_id(uint8_t id[AFEM_UNIQUE_ID_BYTES]);
+int afem_comm_create(afem_ctx* ctx, const uint8_t id[AFEM_UNIQUE_ID_BYTES], int nranks, int rank, afem_comm** out);
+int afem_comm_destroy(afem_comm* comm);
+/* In-place sum over ranks of n doubles (device pointer) on the context stream. */
+int afem_comm_allreduce_sum(afem_comm* comm, double* dbuf, int64_t n);
+/* Attach a halo plan (FemDoFsOnNodes::computeSynchronizeInfos equivalent):
+ * per neighbour rank, owned DoFs to send and ghost DoFs (ids >= n_rows) to
+ * receive, concatenated in neighbour order; counts per neighbour. */
+int afem_ls_set_halo(afem_ls* ls, afem_comm* comm, int n_neighbors, const int32_t* neighbor_ranks,
+                     const int64_t* send_counts, const int32_t* send_ids, const int64_t* recv_counts,
+                     const int32_t* recv_ids);
+/* Halo plan of a structured slab mesh (neighbours rank-1 / rank+1). */
+int afem_ls_set_halo_structured(afem_ls* ls, afem_comm* comm, afem_mesh* mesh);
+/* Host-only (no GPU needed): the halo plan of a structured slab mesh, i.e.
+ * the ghost synchronisation lists FemDoFsOnNodes::computeSynchronizeInfos
+ * builds (femutils/FemDoFsOnNodes.cc:125-126).  Neighbours are rank-1 and
+ * rank+1; *n_neighbors receives 0..2; counts per neighbour; pass NULL id
+ * arrays to query the counts. */
+int afem_structured_halo_plan(int dim, int n, int nz, int nranks, int rank, int* n_neighbors,
+                              int32_t* neighbor_ranks, int64_t* send_counts, int64_t* recv_counts, int32_t* send_ids,
+                              int32_t* recv_ids);
+/* m_u.synchronize(): owner -> ghost copy of a length-n_cols_local device vector. */
+int afem_ls_synchronize(afem_ls* ls, double* x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ARCANEFEM_AMD_H */

@@ -1,0 +1,402 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C, single-threaded restatement of the reference (toutane/arcanefem @
+ * 2025-02-20) algorithms on the FEM assembly + solve hot path.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ * library, and only as the checker / the timed CPU baseline.  The product path
+ * (arcanefem_amd/libafem.so) never links, loads or calls it.
+ *
+ * Pinning: the reference cannot be built here (Arcane 3.14.14, .NET, Hypre,
+ * PETSc and MPI are absent), so this restatement is pinned by
+ * the reference's own golden result files (tests/golden/<case>.txt replayed on the
+ * reference's own meshes tests/golden/<mesh>.msh, see tests/test_oracle_golden.py).
+ *
+ * Every function names the reference lines it follows.  Compiled with
+ * -ffp-contract=off so that no FMA contraction changes the rounding of the
+ * restated expressions.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* Element matrices                                                          */
+/* ------------------------------------------------------------------------ */
+
+/* Tetrahedron volume: femutils/ArcaneFemFunctionsGpu.h:110-122
+ * (computeVolumeTetra4): |dot(v1-v0, cross(v2-v0, v3-v0))| / 6. */
+static double tet_volume(const double* c0, const double* c1, const double* c2, const double* c3)
+{
+  double v0x = c1[0] - c0[0], v0y = c1[1] - c0[1], v0z = c1[2] - c0[2];
+  double v1x = c2[0] - c0[0], v1y = c2[1] - c0[1], v1z = c2[2] - c0[2];
+  double v2x = c3[0] - c0[0], v2y = c3[1] - c0[1], v2z = c3[2] - c0[2];
+  double cx = v1y * v2z - v1z * v2y;
+  double cy = v1z * v2x - v1x * v2z;
+  double cz = v1x * v2y - v1y * v2x;
+  return fabs(v0x * cx + v0y * cy + v0z * cz) / 6.0;
+}
+
+/* P1 tetrahedron stiffness K = V (dx^dx + dy^dy + dz^dz):
+ * modules/poisson/FemModule.h:177-186 (_computeElementMatrixTetra4Gpu) with the
+ * gradients of femutils/ArcaneFemFunctionsGpu.h:280-392 (computeGradient{X,Y,Z}Tetra4)
+ * and operator^ / FixedMatrix of femutils/FemUtils.h:191-226. */
+void orc_element_tet4(const double* xyz /* [4][3] */, double* K /* [16] */, double* vol_out)
+{
+  const double *m0 = xyz, *m1 = xyz + 3, *m2 = xyz + 6, *m3 = xyz + 9;
+  double V6; /* 6 x Volume, as computed in computeGradient{X,Y,Z}Tetra4 */
+  {
+    double v0x = m1[0] - m0[0], v0y = m1[1] - m0[1], v0z = m1[2] - m0[2];
+    double v1x = m2[0] - m0[0], v1y = m2[1] - m0[1], v1z = m2[2] - m0[2];
+    double v2x = m3[0] - m0[0], v2y = m3[1] - m0[1], v2z = m3[2] - m0[2];
+    double cx = v1y * v2z - v1z * v2y, cy = v1z * v2x - v1x * v2z, cz = v1x * v2y - v1y * v2x;
+    V6 = fabs(v0x * cx + v0y * cy + v0z * cz);
+  }
+  double vol = tet_volume(m0, m1, m2, m3);
+  double dx[4], dy[4], dz[4];
+  dx[0] = (m1[1] * (m3[2] - m2[2]) + m2[1] * (m1[2] - m3[2]) + m3[1] * (m2[2] - m1[2])) / V6;
+  dx[1] = (m0[1] * (m2[2] - m3[2]) + m2[1] * (m3[2] - m0[2]) + m3[1] * (m0[2] - m2[2])) / V6;
+  dx[2] = (m0[1] * (m3[2] - m1[2]) + m1[1] * (m0[2] - m3[2]) + m3[1] * (m1[2] - m0[2])) / V6;
+  dx[3] = (m0[1] * (m1[2] - m2[2]) + m1[1] * (m2[2] - m0[2]) + m2[1] * (m0[2] - m1[2])) / V6;
+  dy[0] = (m1[2] * (m3[0] - m2[0]) + m2[2] * (m1[0] - m3[0]) + m3[2] * (m2[0] - m1[0])) / V6;
+  dy[1] = (m0[2] * (m2[0] - m3[0]) + m2[2] * (m3[0] - m0[0]) + m3[2] * (m0[0] - m2[0])) / V6;
+  dy[2] = (m0[2] * (m3[0] - m1[0]) + m1[2] * (m0[0] - m3[0]) + m3[2] * (m1[0] - m0[0])) / V6;
+  dy[3] = (m0[2] * (m1[0] - m2[0]) + m1[2] * (m2[0] - m0[0]) + m2[2] * (m0[0] - m1[0])) / V6;
+  dz[0] = (m1[0] * (m3[1] - m2[1]) + m2[0] * (m1[1] - m3[1]) + m3[0] * (m2[1] - m1[1])) / V6;
+  dz[1] = (m0[0] * (m2[1] - m3[1]) + m2[0] * (m3[1] - m0[1]) + m3[0] * (m0[1] - m2[1])) / V6;
+  dz[2] = (m0[0] * (m3[1] - m1[1]) + m1[0] * (m0[1] - m3[1]) + m3[0] * (m1[1] - m0[1])) / V6;
+  dz[3] = (m0[0] * (m1[1] - m2[1]) + m1[0] * (m2[1] - m0[1]) + m2[0] * (m0[1] - m1[1])) / V6;
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b)
+      K[4 * a + b] = vol * (dx[a] * dx[b]) + vol * (dy[a] * dy[b]) + vol * (dz[a] * dz[b]);
+  if (vol_out)
+    *vol_out = vol;
+}
+
+/* P1 triangle stiffness K = A (dx^dx + dy^dy):
+ * modules/poisson/FemModule.h:139-147 (_computeElementMatrixTria3Gpu),
+ * area femutils/ArcaneFemFunctionsGpu.h:75-83 (|cross|/2), gradients
+ * femutils/ArcaneFemFunctionsGpu.h:218-252 (signed A2). */
+void orc_element_tri3(const double* xyz /* [3][3] */, double* K /* [9] */, double* area_out)
+{
+  const double *v0 = xyz, *v1 = xyz + 3, *v2 = xyz + 6;
+  double ax = v1[0] - v0[0], ay = v1[1] - v0[1], az = v1[2] - v0[2];
+  double bx = v2[0] - v0[0], by = v2[1] - v0[1], bz = v2[2] - v0[2];
+  double cx = ay * bz - az * by, cy = az * bx - ax * bz, cz = ax * by - ay * bx;
+  double area = sqrt(cx * cx + cy * cy + cz * cz) / 2.0;
+  double A2 = (v1[0] - v0[0]) * (v2[1] - v0[1]) - (v2[0] - v0[0]) * (v1[1] - v0[1]);
+  double dx[3] = { (v1[1] - v2[1]) / A2, (v2[1] - v0[1]) / A2, (v0[1] - v1[1]) / A2 };
+  double dy[3] = { (v2[0] - v1[0]) / A2, (v0[0] - v2[0]) / A2, (v1[0] - v0[0]) / A2 };
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b)
+      K[3 * a + b] = area * (dx[a] * dx[b]) + area * (dy[a] * dy[b]);
+  if (area_out)
+    *area_out = area;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Sparsity: femutils/BSRFormat.h:583-770 (computeSparsityAtomic)            */
+/* ------------------------------------------------------------------------ */
+
+static int cmp_u64(const void* a, const void* b)
+{
+  uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return (x > y) - (x < y);
+}
+static int cmp_i32(const void* a, const void* b)
+{
+  int32_t x = *(const int32_t*)a, y = *(const int32_t*)b;
+  return (x > y) - (x < y);
+}
+
+/* pack/unpack: femutils/BSRFormat.h:583-597 */
+static uint64_t pack_edge(int32_t n0, int32_t n1)
+{
+  int32_t mn = n0 > n1 ? n1 : n0, mx = n0 > n1 ? n0 : n1;
+  return ((uint64_t)(uint32_t)mn << 32) | (uint64_t)(uint32_t)mx;
+}
+
+/* Builds the node-node (via edges) scalar structure of `n_rows` rows: row r
+ * holds r itself plus every node sharing an edge with it
+ * (computeSortedEdges :602-651, computeNeighbors :656-672, computeRowIndex
+ * :677-688, computeColumns :703-744).  Rows are restricted to r < n_rows (the
+ * owned nodes; ghost rows are not materialised).  Unlike the reference (whose
+ * atomic column fill leaves the order run-dependent, doc/BSRFormat.md:86-89)
+ * the columns of each row are emitted in ascending order: this is the
+ * canonical form the GPU path is compared against.
+ * Two calls: cols==NULL returns nnz and fills row_ptr[n_rows+1]; the second
+ * call fills cols[nnz]. */
+int64_t orc_sparsity(int64_t n_nodes, int64_t n_rows, int64_t n_cells, int nv, const int32_t* cell_node,
+                     int64_t* row_ptr, int32_t* cols)
+{
+  int epc = (nv == 3) ? 3 : 6; /* edges per element (:757) */
+  int64_t ne = n_cells * epc;
+  uint64_t* edges = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(ne > 0 ? ne : 1));
+  for (int64_t c = 0; c < n_cells; ++c) {
+    const int32_t* n = cell_node + c * nv;
+    uint64_t* e = edges + c * epc;
+    if (nv == 3) {
+      e[0] = pack_edge(n[0], n[1]);
+      e[1] = pack_edge(n[0], n[2]);
+      e[2] = pack_edge(n[1], n[2]);
+    }
+    else {
+      e[0] = pack_edge(n[0], n[1]);
+      e[1] = pack_edge(n[0], n[2]);
+      e[2] = pack_edge(n[0], n[3]);
+      e[3] = pack_edge(n[1], n[2]);
+      e[4] = pack_edge(n[1], n[3]);
+      e[5] = pack_edge(n[2], n[3]);
+    }
+  }
+  qsort(edges, (size_t)ne, sizeof(uint64_t), cmp_u64);
+  /* neighbors initialised to 1 (the diagonal, :679) */
+  int64_t* cnt = (int64_t*)calloc((size_t)n_nodes + 1, sizeof(int64_t));
+  for (int64_t r = 0; r < n_rows; ++r)
+    cnt[r] = 1;
+  for (int64_t t = 0; t < ne; ++t) {
+    if (t == ne - 1 || edges[t] != edges[t + 1]) {
+      int32_t n0 = (int32_t)(edges[t] >> 32), n1 = (int32_t)(edges[t] & 0xFFFFFFFFu);
+      if (n0 < n_rows)
+        cnt[n0]++;
+      if (n1 < n_rows)
+        cnt[n1]++;
+    }
+  }
+  row_ptr[0] = 0;
+  for (int64_t r = 0; r < n_rows; ++r)
+    row_ptr[r + 1] = row_ptr[r] + cnt[r];
+  int64_t nnz = row_ptr[n_rows];
+  if (cols) {
+    for (int64_t r = 0; r < n_rows; ++r) {
+      cols[row_ptr[r]] = (int32_t)r; /* diagonal first, :712-717 */
+      cnt[r] = 1;
+    }
+    for (int64_t t = 0; t < ne; ++t) {
+      if (t == ne - 1 || edges[t] != edges[t + 1]) {
+        int32_t n0 = (int32_t)(edges[t] >> 32), n1 = (int32_t)(edges[t] & 0xFFFFFFFFu);
+        if (n0 < n_rows)
+          cols[row_ptr[n0] + cnt[n0]++] = n1;
+        if (n1 < n_rows)
+          cols[row_ptr[n1] + cnt[n1]++] = n0;
+      }
+    }
+    for (int64_t r = 0; r < n_rows; ++r)
+      qsort(cols + row_ptr[r], (size_t)(row_ptr[r + 1] - row_ptr[r]), sizeof(int32_t), cmp_i32);
+  }
+  free(cnt);
+  free(edges);
+  return nnz;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Assembly: femutils/BSRFormat.h:786-837 (assembleBilinearOrderedPerBlock)   */
+/* with NB_DOF = 1: cell loop, owned-row filter, linear column search, add.   */
+/* The RHS source term of femutils/ArcaneFemFunctionsGpu.h:401-429            */
+/* (applyConstantSourceToRhsBase: rhs[dof] += f*|K|/nbNode for own nodes) is  */
+/* done in the same cell loop when rhs != NULL.                               */
+/* Returns the number of (row,col) pairs not found in the structure.          */
+/* ------------------------------------------------------------------------ */
+int64_t orc_assemble_poisson(int64_t n_rows, int64_t n_cells, int nv, const int32_t* cell_node, const double* coords,
+                             const int64_t* row_ptr, const int32_t* cols, double* vals, double f, double* rhs)
+{
+  int64_t missing = 0;
+  double xyz[12], K[16], meas;
+  for (int64_t c = 0; c < n_cells; ++c) {
+    const int32_t* n = cell_node + c * nv;
+    for (int a = 0; a < nv; ++a) {
+      xyz[3 * a + 0] = coords[3 * (int64_t)n[a] + 0];
+      xyz[3 * a + 1] = coords[3 * (int64_t)n[a] + 1];
+      xyz[3 * a + 2] = coords[3 * (int64_t)n[a] + 2];
+    }
+    if (nv == 4)
+      orc_element_tet4(xyz, K, &meas);
+    else
+      orc_element_tri3(xyz, K, &meas);
+    for (int a = 0; a < nv; ++a) {
+      int32_t row = n[a];
+      if (row >= n_rows)
+        continue; /* nodes_infos.isOwn(row_node_lid) (:815) */
+      for (int b = 0; b < nv; ++b) {
+        int32_t col = n[b];
+        int64_t k = row_ptr[row], end = row_ptr[row + 1];
+        while (k < end && cols[k] != col)
+          ++k;
+        if (k == end) {
+          ++missing;
+          continue;
+        }
+        vals[k] += K[nv * a + b];
+      }
+      if (rhs)
+        rhs[row] += f * meas / nv;
+    }
+  }
+  return missing;
+}
+
+/* Block (vector) P1 elasticity on triangles, NB_DOF = 2, "ordered per block"
+ * BSR values (block_start*4 + i*2 + j, femutils/BSRFormat.h:820-829) with the
+ * element matrix of modules/elasticity/FemModule.h:112-140
+ * (computeElementMatrixTRIA3Base): K = (lambda*...)+(mu2*...) / (4A) on the
+ * [u1,u2]-interleaved 6x6 matrix; mu2 = 2*mu as in modules/elasticity/FemModule.cc:133. */
+void orc_element_elasticity_tri3(const double* xyz, double lambda, double mu2, double* K /* [36] */)
+{
+  const double *m0 = xyz, *m1 = xyz + 3, *m2 = xyz + 6;
+  double ax = m1[0] - m0[0], ay = m1[1] - m0[1], az = m1[2] - m0[2];
+  double bx = m2[0] - m0[0], by = m2[1] - m0[1], bz = m2[2] - m0[2];
+  double cx = ay * bz - az * by, cy = az * bx - ax * bz, cz = ax * by - ay * bx;
+  double area = sqrt(cx * cx + cy * cy + cz * cz) / 2.0;
+  /* 2A * grad: dPhi0 = (y1-y2, x2-x1) etc. (FemModule.h:118-124) */
+  double dPhi0x = m1[1] - m2[1], dPhi0y = m2[0] - m1[0];
+  double dPhi1x = m2[1] - m0[1], dPhi1y = m0[0] - m2[0];
+  double dPhi2x = m0[1] - m1[1], dPhi2y = m1[0] - m0[0];
+  double b[3][6] = {
+    { dPhi0x, 0., dPhi1x, 0., dPhi2x, 0. },
+    { 0., dPhi0y, 0., dPhi1y, 0., dPhi2y },
+    { dPhi0y, dPhi0x, dPhi1y, dPhi1x, dPhi2y, dPhi2x }
+  };
+  double s = 1.0 / (4.0 * area);
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) {
+      double lam = (b[0][i] + b[1][i]) * (b[0][j] + b[1][j]);
+      double shr = b[0][i] * b[0][j] + b[1][i] * b[1][j] + 0.5 * b[2][i] * b[2][j];
+      K[6 * i + j] = (lambda * lam + mu2 * shr) * s;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Dirichlet via penalty: femutils/ArcaneFemFunctionsGpu.h:434-456 (forced    */
+/* info/value, rhs = P*g) then femutils/HypreDoFLinearSystem.cc:356-382       */
+/* (_applyForcedValuesToLhs: A[i,i] = P).                                     */
+/* ------------------------------------------------------------------------ */
+void orc_dirichlet_penalty(int64_t n_dofs, const int32_t* dofs, double value, double penalty, const int64_t* row_ptr,
+                           const int32_t* cols, double* vals, double* rhs)
+{
+  for (int64_t t = 0; t < n_dofs; ++t) {
+    int32_t d = dofs[t];
+    for (int64_t k = row_ptr[d]; k < row_ptr[d + 1]; ++k)
+      if (cols[k] == d)
+        vals[k] = penalty;
+    rhs[d] = penalty * value;
+  }
+}
+
+/* Row elimination: femutils/HypreDoFLinearSystem.cc:319-351 */
+void orc_row_elimination(int64_t n_dofs, const int32_t* dofs, double value, const int64_t* row_ptr, const int32_t* cols,
+                         double* vals, double* rhs)
+{
+  for (int64_t t = 0; t < n_dofs; ++t) {
+    int32_t d = dofs[t];
+    for (int64_t k = row_ptr[d]; k < row_ptr[d + 1]; ++k)
+      vals[k] = cols[k] == d ? 1.0 : 0.0;
+    rhs[d] = value;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* CSR SpMV and Jacobi-preconditioned CG.  Restates the iterative branch of   */
+/* SequentialDoFLinearSystemImpl::solve (femutils/DoFLinearSystem.cc:137-151: */
+/* DiagonalPreconditioner + ConjugateGradientSolver, x0 = 0).  Arcane MatVec   */
+/* is external and not vendored, so its stopping test is unpinned; this       */
+/* oracle stops on sqrt(r.z) <= rtol*sqrt(r0.z0|free) or ||r||_2 <= atol,     */
+/* where r0.z0|free sums the non-constraint rows only (see below).            */
+/* ------------------------------------------------------------------------ */
+void orc_spmv(int64_t n_rows, const int64_t* row_ptr, const int32_t* cols, const double* vals, const double* x, double* y)
+{
+  for (int64_t r = 0; r < n_rows; ++r) {
+    double s = 0.0;
+    for (int64_t k = row_ptr[r]; k < row_ptr[r + 1]; ++k)
+      s += vals[k] * x[cols[k]];
+    y[r] = s;
+  }
+}
+
+static double dot(int64_t n, const double* a, const double* b)
+{
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i)
+    s += a[i] * b[i];
+  return s;
+}
+
+/* Returns iterations done; *res_out = final sqrt(r.z)/sqrt(r0.z0);
+ * *rnorm_out = ||r||_2. max_iter < 0 means "exactly -max_iter iterations, no
+ * stopping test" (fixed-work timing). */
+int orc_pcg_jacobi(int64_t n, const int64_t* row_ptr, const int32_t* cols, const double* vals, const double* b,
+                   double* x, double rtol, double atol, int max_iter, double* res_out, double* rnorm_out)
+{
+  int fixed = max_iter < 0;
+  if (fixed)
+    max_iter = -max_iter;
+  double* r = (double*)malloc(sizeof(double) * (size_t)n);
+  double* z = (double*)malloc(sizeof(double) * (size_t)n);
+  double* p = (double*)malloc(sizeof(double) * (size_t)n);
+  double* q = (double*)malloc(sizeof(double) * (size_t)n);
+  double* dinv = (double*)malloc(sizeof(double) * (size_t)n);
+  /* constraint rows (penalty or eliminated: the diagonal dominates the rest
+   * of the row by > 1e10) are excluded from the reference value of the
+   * stopping test, otherwise P = 1e30 makes any relative test meaningless */
+  unsigned char* constraint = (unsigned char*)malloc((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    double d = 0.0, off = 0.0;
+    for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k)
+      if (cols[k] == i)
+        d = vals[k];
+      else
+        off += fabs(vals[k]);
+    dinv[i] = d != 0.0 ? 1.0 / d : 0.0;
+    constraint[i] = fabs(d) > 1e10 * off;
+  }
+  orc_spmv(n, row_ptr, cols, vals, x, q);
+  double rz0 = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    r[i] = b[i] - q[i];
+    z[i] = r[i] * dinv[i];
+    p[i] = z[i];
+    if (!constraint[i])
+      rz0 += r[i] * z[i];
+  }
+  double rz = dot(n, r, z);
+  if (rz0 == 0.0)
+    rz0 = rz;
+  free(constraint);
+  int it = 0;
+  double res = rz0 > 0 ? 1.0 : 0.0;
+  while (it < max_iter) {
+    if (!fixed) {
+      if (rz0 == 0.0)
+        break;
+      res = sqrt(fabs(rz / rz0));
+      if (res <= rtol)
+        break;
+      if (atol > 0 && sqrt(dot(n, r, r)) <= atol)
+        break;
+    }
+    orc_spmv(n, row_ptr, cols, vals, p, q);
+    double pq = dot(n, p, q);
+    double alpha = rz / pq;
+    for (int64_t i = 0; i < n; ++i) {
+      x[i] += alpha * p[i];
+      r[i] -= alpha * q[i];
+      z[i] = r[i] * dinv[i];
+    }
+    double rz_new = dot(n, r, z);
+    double beta = rz_new / rz;
+    rz = rz_new;
+    for (int64_t i = 0; i < n; ++i)
+      p[i] = z[i] + beta * p[i];
+    ++it;
+  }
+  if (res_out)
+    *res_out = rz0 > 0 ? sqrt(fabs(rz / rz0)) : 0.0;
+  if (rnorm_out)
+    *rnorm_out = sqrt(dot(n, r, r));
+  free(r);
+  free(z);
+  free(p);
+  free(q);
+  free(dinv);
+  return it;
+}

@@ -1,0 +1,310 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+Python side of the CPU oracle: ctypes bindings to ``oracle/build/liboracle.so``
+(the plain-C restatement of the reference, see oracle.c for the file:line each
+function follows) plus numpy helpers:
+
+* ``structured_mesh`` — the synthetic-input specification (jittered Kuhn
+  tetrahedra / split squares, seeded counter-based hash).  The product path
+  generates the same mesh on the GPU (``afem_mesh_create_structured``); the
+  parity tests check the two agree bit for bit.
+* ``sequential_dense_solve`` — the SequentialBasicDoFLinearSystem semantics of
+  config C1 (dense N x N matrix, `femutils/DoFLinearSystem.cc:72-164`).
+* ``check_node_result`` — the golden comparison of
+  `femutils/FemUtils.cc:84-169` (relative epsilon, keyed by node unique id).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg import this module, as the checker or the timed CPU
+baseline.  Parity status: pinned by the reference's golden result files
+(tests/golden, replayed in tests/test_oracle_golden.py); the Arcane MatVec CG
+stopping rule is external to the reference tree and therefore unpinned (the
+goldens used here are all solved by the direct branch, N < 500).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "oracle.c")):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.orc_element_tet4.argtypes = [_f64p, _f64p, ctypes.POINTER(ctypes.c_double)]
+        L.orc_element_tri3.argtypes = [_f64p, _f64p, ctypes.POINTER(ctypes.c_double)]
+        L.orc_element_elasticity_tri3.argtypes = [_f64p, ctypes.c_double, ctypes.c_double, _f64p]
+        L.orc_sparsity.restype = ctypes.c_int64
+        L.orc_sparsity.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _i32p, _i64p,
+                                   ctypes.c_void_p]
+        L.orc_assemble_poisson.restype = ctypes.c_int64
+        L.orc_assemble_poisson.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _i32p, _f64p, _i64p, _i32p,
+                                           _f64p, ctypes.c_double, ctypes.c_void_p]
+        L.orc_dirichlet_penalty.argtypes = [ctypes.c_int64, _i32p, ctypes.c_double, ctypes.c_double, _i64p, _i32p,
+                                            _f64p, _f64p]
+        L.orc_row_elimination.argtypes = [ctypes.c_int64, _i32p, ctypes.c_double, _i64p, _i32p, _f64p, _f64p]
+        L.orc_spmv.argtypes = [ctypes.c_int64, _i64p, _i32p, _f64p, _f64p, _f64p]
+        L.orc_pcg_jacobi.restype = ctypes.c_int
+        L.orc_pcg_jacobi.argtypes = [ctypes.c_int64, _i64p, _i32p, _f64p, _f64p, _f64p, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double)]
+        _lib = L
+    return _lib
+
+
+# --------------------------------------------------------------------------
+# element matrices
+# --------------------------------------------------------------------------
+def element_tet4(xyz):
+    xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(4, 3)
+    K = np.zeros(16)
+    v = ctypes.c_double()
+    lib().orc_element_tet4(xyz.ravel(), K, ctypes.byref(v))
+    return K.reshape(4, 4), v.value
+
+
+def element_tri3(xyz):
+    xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(3, 3)
+    K = np.zeros(9)
+    v = ctypes.c_double()
+    lib().orc_element_tri3(xyz.ravel(), K, ctypes.byref(v))
+    return K.reshape(3, 3), v.value
+
+
+def element_elasticity_tri3(xyz, lam, mu2):
+    xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(3, 3)
+    K = np.zeros(36)
+    lib().orc_element_elasticity_tri3(xyz.ravel(), lam, mu2, K)
+    return K.reshape(6, 6)
+
+
+# --------------------------------------------------------------------------
+# sparsity / assembly / BC / solve
+# --------------------------------------------------------------------------
+def sparsity(n_nodes, n_rows, cells):
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    nv = cells.shape[1]
+    row_ptr = np.zeros(n_rows + 1, dtype=np.int64)
+    L = lib()
+    nnz = L.orc_sparsity(n_nodes, n_rows, cells.shape[0], nv, cells.ravel(), row_ptr, None)
+    cols = np.zeros(max(nnz, 1), dtype=np.int32)
+    L.orc_sparsity(n_nodes, n_rows, cells.shape[0], nv, cells.ravel(), row_ptr,
+                   cols.ctypes.data_as(ctypes.c_void_p))
+    return row_ptr, cols[:nnz]
+
+
+def assemble_poisson(n_rows, cells, coords, row_ptr, cols, f=0.0, with_rhs=True):
+    """Matrix values (+ constant-source RHS) on a fixed structure."""
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    coords = np.ascontiguousarray(coords, dtype=np.float64).reshape(-1, 3)
+    vals = np.zeros(cols.shape[0], dtype=np.float64)
+    rhs = np.zeros(n_rows, dtype=np.float64)
+    missing = lib().orc_assemble_poisson(n_rows, cells.shape[0], cells.shape[1], cells.ravel(), coords.ravel(),
+                                         row_ptr, cols, vals, f,
+                                         rhs.ctypes.data_as(ctypes.c_void_p) if with_rhs else None)
+    if missing:
+        raise RuntimeError(f"{missing} (row,col) pairs missing from the structure")
+    return vals, rhs
+
+
+def dirichlet_penalty(dofs, value, penalty, row_ptr, cols, vals, rhs):
+    dofs = np.ascontiguousarray(dofs, dtype=np.int32)
+    lib().orc_dirichlet_penalty(dofs.shape[0], dofs, value, penalty, row_ptr, cols, vals, rhs)
+
+
+def row_elimination(dofs, value, row_ptr, cols, vals, rhs):
+    dofs = np.ascontiguousarray(dofs, dtype=np.int32)
+    lib().orc_row_elimination(dofs.shape[0], dofs, value, row_ptr, cols, vals, rhs)
+
+
+def spmv(row_ptr, cols, vals, x):
+    n = row_ptr.shape[0] - 1
+    y = np.zeros(n)
+    lib().orc_spmv(n, row_ptr, cols, vals, np.ascontiguousarray(x, dtype=np.float64), y)
+    return y
+
+
+def pcg_jacobi(row_ptr, cols, vals, b, rtol=1e-12, atol=0.0, max_iter=10000, x0=None):
+    n = row_ptr.shape[0] - 1
+    x = np.zeros(n) if x0 is None else np.array(x0, dtype=np.float64)
+    res = ctypes.c_double()
+    rn = ctypes.c_double()
+    it = lib().orc_pcg_jacobi(n, row_ptr, cols, vals, np.ascontiguousarray(b, dtype=np.float64), x, rtol, atol,
+                              max_iter, ctypes.byref(res), ctypes.byref(rn))
+    return x, it, res.value, rn.value
+
+
+def csr_to_dense(row_ptr, cols, vals, n_cols=None):
+    n = row_ptr.shape[0] - 1
+    m = n if n_cols is None else n_cols
+    A = np.zeros((n, m))
+    for r in range(n):
+        s, e = row_ptr[r], row_ptr[r + 1]
+        A[r, cols[s:e]] += vals[s:e]
+    return A
+
+
+def sequential_dense_solve(A, b, epsilon=1e-15):
+    """SequentialDoFLinearSystemImpl::solve (femutils/DoFLinearSystem.cc:106-164):
+    dense -> CSR dropping exact zeros (femutils/FemUtils.cc:35-76), direct
+    solver when N < 500, else diagonal-preconditioned CG with epsilon."""
+    n = A.shape[0]
+    if n < 500:
+        return np.linalg.solve(A, b)
+    mask = A != 0.0
+    row_ptr = np.concatenate([[0], np.cumsum(mask.sum(axis=1))]).astype(np.int64)
+    r, c = np.nonzero(mask)
+    x, _, _, _ = pcg_jacobi(row_ptr, c.astype(np.int32), A[r, c].copy(), b, rtol=epsilon, max_iter=20 * n)
+    return x
+
+
+# --------------------------------------------------------------------------
+# synthetic structured meshes (the input specification shared with the GPU
+# generator; see DESIGN.md "Synthetic inputs")
+# --------------------------------------------------------------------------
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+KUHN_PERMS = ((0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1), (2, 1, 0))
+
+
+def hash_u01(seed: int, idx: np.ndarray) -> np.ndarray:
+    """splitmix64(seed + (idx+1)*golden) -> double in [0,1) with 53 bits."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (idx.astype(np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+def slab_range(nz: int, nranks: int, rank: int):
+    """Owned node layers [k0, k1) of `rank` in a z-slab split of nz+1 layers."""
+    nl = nz + 1
+    return rank * nl // nranks, (rank + 1) * nl // nranks
+
+
+def structured_mesh(dim, n, nz=None, jitter=0.2, seed=20250220, nranks=1, rank=0):
+    """Jittered structured mesh of the unit square (2D: 2 triangles per square)
+    or the box [0,1]^2 x [0, nz/n] (3D: 6 Kuhn tetrahedra per cube), cut into
+    `nranks` z-slabs (y-slabs in 2D).  Returns dict with coords [n_local,3],
+    cells [n_cells,nv] (local ids: owned nodes first, then ghost nodes),
+    n_own, local_to_global, and dirichlet (local ids of owned nodes on the
+    z=0 (2D: y=0) face)."""
+    nz = n if nz is None else nz
+    h = 1.0 / n
+    amp = jitter * h
+    nx = ny = n
+    if dim == 3:
+        L = (nx + 1) * (ny + 1)
+        nlayers = nz + 1
+    else:
+        L = nx + 1
+        nlayers = ny + 1
+        nz = ny
+    k0, k1 = slab_range(nz, nranks, rank)
+    layers = list(range(k0, k1))
+    ghost = []
+    if k0 > 0:
+        ghost.append(k0 - 1)
+    if k1 < nlayers:
+        ghost.append(k1)
+    all_layers = layers + ghost
+    # global ids of local nodes
+    inplane = np.arange(L, dtype=np.int64)
+    l2g = np.concatenate([inplane + k * L for k in all_layers]) if all_layers else np.zeros(0, np.int64)
+    g2l_layer = {k: idx for idx, k in enumerate(all_layers)}
+    g = l2g
+    if dim == 3:
+        i = g % (nx + 1)
+        j = (g // (nx + 1)) % (ny + 1)
+        k = g // L
+        comps = [i, j, k]
+    else:
+        i = g % (nx + 1)
+        j = g // (nx + 1)
+        comps = [i, j]
+    coords = np.zeros((g.shape[0], 3))
+    for c, ic in enumerate(comps):
+        u = hash_u01(seed, g * 3 + c)
+        coords[:, c] = ic.astype(np.float64) * h + (u - 0.5) * amp
+    n_own = len(layers) * L
+
+    def lid(gid):
+        layer = gid // L
+        pos = gid % L
+        return np.array([g2l_layer[int(x)] for x in np.atleast_1d(layer)]).reshape(np.shape(gid)) * L + pos
+
+    # cells touching owned nodes: cell layers [max(k0-1,0), min(k1, nz))
+    c_lo, c_hi = max(k0 - 1, 0), min(k1, nz)
+    if dim == 3:
+        ci, cj, ck = np.meshgrid(np.arange(nx), np.arange(ny), np.arange(c_lo, c_hi), indexing="ij")
+        ci, cj, ck = (a.transpose(2, 1, 0).ravel() for a in (ci, cj, ck))  # lexicographic: i fastest
+        e = np.eye(3, dtype=np.int64)
+        tets = []
+        for perm in KUHN_PERMS:
+            v0 = np.stack([ci, cj, ck], 1)
+            v1 = v0 + e[perm[0]]
+            v2 = v1 + e[perm[1]]
+            v3 = v0 + 1
+            tets.append(np.stack([v0, v1, v2, v3], 1))  # [ncube, 4, 3]
+        T = np.stack(tets, 1).reshape(-1, 4, 3)  # cube-major, 6 tets per cube
+        gid = T[..., 0] + (nx + 1) * (T[..., 1] + (ny + 1) * T[..., 2])
+    else:
+        ci, cj = np.meshgrid(np.arange(nx), np.arange(c_lo, c_hi), indexing="xy")
+        ci, cj = ci.ravel(), cj.ravel()
+        v00 = ci + (nx + 1) * cj
+        v10 = v00 + 1
+        v01 = v00 + (nx + 1)
+        v11 = v01 + 1
+        gid = np.stack([np.stack([v00, v10, v11], 1), np.stack([v00, v11, v01], 1)], 1).reshape(-1, 3)
+    layer = gid // L
+    pos = gid % L
+    lut = np.full(nlayers, -1, dtype=np.int64)
+    for kk, idx in g2l_layer.items():
+        lut[kk] = idx
+    cells = (lut[layer] * L + pos).astype(np.int32)
+    dirichlet = np.arange(L, dtype=np.int32) if k0 == 0 else np.zeros(0, np.int32)
+    return dict(coords=coords, cells=cells, n_own=n_own, n_local=g.shape[0], local_to_global=l2g,
+                dirichlet=dirichlet, dim=dim)
+
+
+# --------------------------------------------------------------------------
+# golden comparison (femutils/FemUtils.cc:84-169)
+# --------------------------------------------------------------------------
+def is_nearly_equal(ref, v, eps):
+    d = abs(ref - v)
+    if d == 0.0:
+        return True
+    return d < (abs(ref) + abs(v)) * eps
+
+
+def check_node_result(values_by_uid: dict, golden: dict, eps: float, min_value: float = 0.0):
+    """Returns (nb_error, max_rel) with Arcane's comparison semantics."""
+    nb_error = 0
+    max_rel = 0.0
+    for uid, v in values_by_uid.items():
+        if uid not in golden:
+            continue
+        ref = golden[uid]
+        if abs(ref) < min_value and abs(v) < min_value:
+            continue
+        denom = max(abs(ref), abs(v), 1e-300)
+        max_rel = max(max_rel, abs(ref - v) / denom)
+        if not is_nearly_equal(ref, v, eps):
+            nb_error += 1
+    return nb_error, max_rel

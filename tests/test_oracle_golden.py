@@ -1,0 +1,101 @@
+"""CPU: pin the oracle against the reference's golden result files, and check
+the oracle's own building blocks against known answers."""
+import numpy as np
+import pytest
+
+from arcanefem_amd.gmsh import read_gmsh, read_node_result_file
+from oracle import oracle as O
+
+from golden_cases import CASES, GOLDEN_TOL, path
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_oracle_reproduces_reference_golden(case):
+    mfile, f, bcs, gfile, P = CASES[case]
+    m = read_gmsh(path(mfile))
+    rp, cols = O.sparsity(m.n_nodes, m.n_nodes, m.cells)
+    vals, rhs = O.assemble_poisson(m.n_nodes, m.cells, m.coords, rp, cols, 0.0 if f is None else f)
+    for g, v in bcs:
+        O.dirichlet_penalty(m.group_nodes(g), v, P, rp, cols, vals, rhs)
+    x = O.sequential_dense_solve(O.csr_to_dense(rp, cols, vals), rhs)
+    gold = read_node_result_file(path(gfile))
+    assert len(gold) == m.n_nodes
+    nerr, mx = O.check_node_result({int(t): x[i] for i, t in enumerate(m.node_tags)}, gold, 1e-4)
+    assert nerr == 0, f"{nerr} nodes outside the reference's 1e-4 gate"
+    assert mx <= GOLDEN_TOL[case], f"max rel error {mx:.3e}"
+
+
+def test_mesh_counts_match_survey():
+    # circle_cut 101/166, sphere_cut 194/527, plancher 117/196,
+    # L-shape 151/254, L-shape-3D 108/259, bar 80/122
+    expect = {"circle_cut": (101, 166), "sphere_cut": (194, 527), "plancher": (117, 196), "L-shape": (151, 254),
+              "L-shape-3D": (108, 259), "bar": (80, 122)}
+    for name, (nn, nc) in expect.items():
+        m = read_gmsh(path(name + ".msh"))
+        assert (m.n_nodes, m.n_cells) == (nn, nc)
+
+
+def test_element_known_answers():
+    # reference tetrahedron: K = V * G G^T with V = 1/6, grads (-1,-1,-1), e1, e2, e3
+    K, v = O.element_tet4(np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]], dtype=float))
+    G = np.array([[-1, -1, -1], [1, 0, 0], [0, 1, 0], [0, 0, 1]], dtype=float)
+    assert abs(v - 1 / 6) < 1e-15
+    assert np.allclose(K, G @ G.T / 6, atol=1e-15)
+    # invariant to node order and orientation
+    K2, _ = O.element_tet4(np.array([[0, 1, 0], [1, 0, 0], [0, 0, 0], [0, 0, 1]], dtype=float))
+    perm = [2, 1, 0, 3]
+    assert np.allclose(K2, K[np.ix_(perm, perm)], atol=1e-15)
+    Kt, a = O.element_tri3(np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], dtype=float))
+    assert abs(a - 0.5) < 1e-15
+    assert np.allclose(Kt, np.array([[1, -0.5, -0.5], [-0.5, 0.5, 0], [-0.5, 0, 0.5]]), atol=1e-15)
+
+
+def test_elasticity_element_rigid_modes():
+    rng = np.random.default_rng(1)
+    xyz = np.c_[rng.random((3, 2)), np.zeros(3)]
+    K = O.element_elasticity_tri3(xyz, 1.2, 0.8)
+    assert np.allclose(K, K.T, atol=1e-12 * np.abs(K).max())
+    tx = np.tile([1.0, 0.0], 3)
+    ty = np.tile([0.0, 1.0], 3)
+    rot = np.ravel(np.c_[-xyz[:, 1], xyz[:, 0]])
+    for mode in (tx, ty, rot):
+        assert np.abs(K @ mode).max() < 1e-12 * np.abs(K).max()
+
+
+def test_sparsity_is_edge_graph():
+    m = O.structured_mesh(3, 4)
+    rp, cols = O.sparsity(m["n_local"], m["n_own"], m["cells"])
+    # Kuhn interior node: 14 neighbours + diagonal
+    assert np.diff(rp).max() == 15
+    # rows sorted, diagonal present
+    for r in range(m["n_own"]):
+        seg = cols[rp[r]:rp[r + 1]]
+        assert np.all(np.diff(seg) > 0) and r in seg
+    # nnz = 2 E + N  (femutils/BSRFormat.h:397-399)
+    edges = set()
+    for c in m["cells"]:
+        for a in range(4):
+            for b in range(a + 1, 4):
+                edges.add((min(c[a], c[b]), max(c[a], c[b])))
+    assert rp[-1] == 2 * len(edges) + m["n_own"]
+
+
+def test_structured_mesh_spec_slabs_cover_global_mesh():
+    g = O.structured_mesh(3, 4, nz=6)
+    seen = np.zeros(g["n_own"], dtype=int)
+    for r in range(3):
+        s = O.structured_mesh(3, 4, nz=6, nranks=3, rank=r)
+        seen[s["local_to_global"][:s["n_own"]]] += 1
+        assert np.array_equal(s["coords"], g["coords"][s["local_to_global"]])
+    assert np.all(seen == 1)
+
+
+def test_pcg_matches_direct():
+    m = O.structured_mesh(3, 6)
+    rp, cols = O.sparsity(m["n_local"], m["n_own"], m["cells"])
+    vals, rhs = O.assemble_poisson(m["n_own"], m["cells"], m["coords"], rp, cols, 5.5)
+    O.dirichlet_penalty(m["dirichlet"], 0.5, 1e30, rp, cols, vals, rhs)
+    x, it, res, _ = O.pcg_jacobi(rp, cols, vals, rhs, rtol=1e-14)
+    xd = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
+    assert np.abs(x - xd).max() / np.abs(xd).max() < 1e-10
+    assert np.allclose(x[m["dirichlet"]], 0.5, atol=1e-14)
