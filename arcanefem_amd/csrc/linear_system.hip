@@ -225,18 +225,36 @@ __global__ void k_inv_diag(int64_t n_rows, const int64_t* __restrict__ rows, con
 
 constexpr int kVecBlocks = 2048;
 
-// x = 0, r = b, z = D^-1 r, p = z ; partials r.z (all rows) and r.z (free rows)
-__global__ __launch_bounds__(kThreads) void k_cg_init(int64_t n, const double* __restrict__ b, double* __restrict__ x,
-                                                      double* __restrict__ r, double* __restrict__ z,
-                                                      double* __restrict__ p, const double* __restrict__ dinv,
+// Initial guess: constraint rows solved on their own (x0_i = b_i / a_ii: the
+// Dirichlet value for penalty and eliminated rows), 0 elsewhere.  This lifts
+// the Dirichlet data into x0, so the residual of the free rows carries it
+// from the start (the stopping reference is then meaningful also for
+// problems driven only by Dirichlet data), and the eliminated rows keep a
+// zero residual and search direction, so a row-eliminated (non-symmetric)
+// system is iterated on its symmetric free block.
+__global__ __launch_bounds__(kThreads) void k_cg_x0(int64_t n, const double* __restrict__ b,
+                                                    const double* __restrict__ dinv, const uint8_t* __restrict__ cons,
+                                                    double* __restrict__ x, double* __restrict__ p)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double xi = cons[i] ? b[i] * dinv[i] : 0.0;
+    x[i] = xi;
+    p[i] = xi;
+  }
+}
+
+// r = b - A x0 (q), z = D^-1 r, p = z ; partials r.z (all rows) and r.z (free rows)
+__global__ __launch_bounds__(kThreads) void k_cg_init(int64_t n, const double* __restrict__ b,
+                                                      const double* __restrict__ q, double* __restrict__ r,
+                                                      double* __restrict__ z, double* __restrict__ p,
+                                                      const double* __restrict__ dinv,
                                                       const uint8_t* __restrict__ cons, double* __restrict__ partial,
                                                       double* __restrict__ partial_free)
 {
   double s = 0.0, sf = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    double ri = b[i];
+    double ri = b[i] - q[i];
     double zi = ri * dinv[i];
-    x[i] = 0.0;
     r[i] = ri;
     z[i] = zi;
     p[i] = zi;
@@ -505,7 +523,12 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   hipLaunchKernelGGL(k_inv_diag, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, ctx.stream, n, ls.csr_rows,
                      ls.csr_cols, ls.csr_vals, ls.dinv.p, ls.cons.p);
   AFEM_LAUNCHED();
-  hipLaunchKernelGGL(k_cg_init, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.sol.p, ls.r.p, ls.z.p, ls.p.p,
+  hipLaunchKernelGGL(k_cg_x0, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.dinv.p, ls.cons.p, ls.sol.p,
+                     ls.p.p);
+  AFEM_LAUNCHED();
+  if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
+  launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, nullptr);
+  hipLaunchKernelGGL(k_cg_init, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.q.p, ls.r.p, ls.z.p, ls.p.p,
                      ls.dinv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
   AFEM_LAUNCHED();
   double* scal = ls.scal.p;  // [0],[1]: r.z ping-pong, [2]: p.q, [3]: r0.z0 over free rows, [4]: r.r

@@ -40,6 +40,7 @@ struct Layers {
 __global__ void k_gen_coords(int dim, int64_t n_nodes, Layers ly, int np1, double h, double amp, uint64_t seed,
                              double* __restrict__ coords)
 {
+#pragma clang fp contract(off)  // no a*b+c -> fma here (the file is also built with -ffp-contract=off)
   int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= n_nodes) return;
   int64_t li = l / ly.L, pos = l - li * ly.L;
@@ -60,7 +61,9 @@ __global__ void k_gen_coords(int dim, int64_t n_nodes, Layers ly, int np1, doubl
     double x = 0.0;
     if (c < dim) {
       double u = hash_u01(seed, (uint64_t)(g * 3 + c));
-      x = __dadd_rn(__dmul_rn((double)ic[c], h), __dmul_rn(__dsub_rn(u, 0.5), amp));
+      const double a = (double)ic[c] * h;
+      const double b = (u - 0.5) * amp;
+      x = a + b;
     }
     coords[3 * l + c] = x;
   }

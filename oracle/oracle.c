@@ -298,7 +298,8 @@ void orc_row_elimination(int64_t n_dofs, const int32_t* dofs, double value, cons
 /* ------------------------------------------------------------------------ */
 /* CSR SpMV and Jacobi-preconditioned CG.  Restates the iterative branch of   */
 /* SequentialDoFLinearSystemImpl::solve (femutils/DoFLinearSystem.cc:137-151: */
-/* DiagonalPreconditioner + ConjugateGradientSolver, x0 = 0).  Arcane MatVec   */
+/* DiagonalPreconditioner + ConjugateGradientSolver; the reference starts at   */
+/* x0 = 0, here constraint rows start at their Dirichlet value).  Arcane MatVec*/
 /* is external and not vendored, so its stopping test is unpinned; this       */
 /* oracle stops on sqrt(r.z) <= rtol*sqrt(r0.z0|free) or ||r||_2 <= atol,     */
 /* where r0.z0|free sums the non-constraint rows only (see below).            */
@@ -349,6 +350,10 @@ int orc_pcg_jacobi(int64_t n, const int64_t* row_ptr, const int32_t* cols, const
     dinv[i] = d != 0.0 ? 1.0 / d : 0.0;
     constraint[i] = fabs(d) > 1e10 * off;
   }
+  /* x0: constraint rows solved on their own (the Dirichlet values), 0
+   * elsewhere -- lifts the Dirichlet data into x0 (see k_cg_x0). */
+  for (int64_t i = 0; i < n; ++i)
+    x[i] = constraint[i] ? b[i] * dinv[i] : 0.0;
   orc_spmv(n, row_ptr, cols, vals, x, q);
   double rz0 = 0.0;
   for (int64_t i = 0; i < n; ++i) {

@@ -99,3 +99,26 @@ def test_pcg_matches_direct():
     xd = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
     assert np.abs(x - xd).max() / np.abs(xd).max() < 1e-10
     assert np.allclose(x[m["dirichlet"]], 0.5, atol=1e-14)
+
+
+def test_pcg_dirichlet_driven_and_row_elimination():
+    """No source term (Dirichlet data only) and row elimination (non-symmetric
+    rows) both converge to the direct solution: the x0 lifting of the
+    constraint rows (oracle.c::orc_pcg_jacobi, k_cg_x0)."""
+    m = read_gmsh(path("plancher.msh"))
+    rp, cols = O.sparsity(m.n_nodes, m.n_nodes, m.cells)
+    vals, rhs = O.assemble_poisson(m.n_nodes, m.cells, m.coords, rp, cols, 0.0)
+    for g, v in CASES["point_dirichlet_2D"][2]:
+        O.dirichlet_penalty(m.group_nodes(g), v, 1e30, rp, cols, vals, rhs)
+    x, it, res, _ = O.pcg_jacobi(rp, cols, vals, rhs, rtol=1e-14)
+    xd = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
+    assert np.abs(x - xd).max() / np.abs(xd).max() < 1e-12
+    m = read_gmsh(path("circle_cut.msh"))
+    rp, cols = O.sparsity(m.n_nodes, m.n_nodes, m.cells)
+    vals, rhs = O.assemble_poisson(m.n_nodes, m.cells, m.coords, rp, cols, 5.5)
+    ids = m.group_nodes("horizontal")
+    O.row_elimination(ids, 0.5, rp, cols, vals, rhs)
+    x, it, res, _ = O.pcg_jacobi(rp, cols, vals, rhs, rtol=1e-14)
+    xd = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
+    assert res <= 1e-14 and np.abs(x - xd).max() / np.abs(xd).max() < 1e-12
+    assert np.all(x[ids] == 0.5)
