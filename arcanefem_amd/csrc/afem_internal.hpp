@@ -108,7 +108,7 @@ struct Structure {
   DevBuf<int64_t> row_ptr;  // [n_rows+1]
   DevBuf<int32_t> cols;     // [nnz], sorted ascending per row
   // Row-local incidence table, sliced ELLPACK with C = 64 (one wavefront):
-  // entry (slice s, k, lane) at inc_slice_ptr[s] + k*64 + lane describes the
+  // entry (slice s, k, lane) at inc_slice_ptr[s] + (k/4)*256 + lane*4 + k%4 describes the
   // k-th cell incident to row 64*s+lane as the row-slots of the cell's other
   // nodes (one byte each) and the row's diagonal slot in the top byte.
   DevBuf<uint32_t> inc;

@@ -54,46 +54,66 @@ __device__ __forceinline__ V3 cross(V3 a, V3 b)
 }
 __device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 
+// 1/a to full double precision: hardware reciprocal estimate + two Newton
+// steps (5 VALU ops instead of the ~10 of an IEEE division; within 1 ulp).
+__device__ __forceinline__ double recip(double a)
+{
+  double r = __builtin_amdgcn_rcp(a);
+  double e = fma(-a, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-a, r, 1.0);
+  return fma(r, e, r);
+}
+
 // Element row of the P1 Laplacian for the row node x0 of a tetrahedron
 // (x0,x1,x2,x3):  K_0b = V grad N_0 . grad N_b = (c_0 . c_b) / (6 |det|) with
-// c_1 = e2 x e3, c_2 = e3 x e1, c_3 = e1 x e2, c_0 = (x3-x1) x (x2-x1),
+// c_1 = e2 x e3, c_2 = e3 x e1, c_3 = e1 x e2, c_0 = -(c_1 + c_2 + c_3),
 // e_k = x_k - x0 and det = e1 . c_1 = 6 V (signed).  Same quantity as
 // modules/poisson/FemModule.h:177-186 with the gradients of
 // femutils/ArcaneFemFunctionsGpu.h:280-392 (node order does not matter:
 // the products are invariant under permutations and orientation).
-__device__ __forceinline__ void tet_row(V3 x0, V3 x1, V3 x2, V3 x3, double& k0, double& k1, double& k2, double& k3,
-                                        double& vol)
+// `s6` = coef/6, the returned |det| = 6V.
+__device__ __forceinline__ double tet_row(V3 x0, V3 x1, V3 x2, V3 x3, double s6, double& k0, double& k1, double& k2,
+                                          double& k3)
 {
-  V3 e1 = sub(x1, x0), e2 = sub(x2, x0), e3 = sub(x3, x0);
-  V3 c1 = cross(e2, e3), c2 = cross(e3, e1), c3 = cross(e1, e2);
-  V3 c0 = cross(sub(x3, x1), sub(x2, x1));
-  double det = fabs(dot(e1, c1));
-  double s = 1.0 / (6.0 * det);
+  const V3 e1 = sub(x1, x0), e2 = sub(x2, x0), e3 = sub(x3, x0);
+  const V3 c1 = cross(e2, e3), c2 = cross(e3, e1), c3 = cross(e1, e2);
+  const V3 c0 = V3{ -(c1.x + c2.x + c3.x), -(c1.y + c2.y + c3.y), -(c1.z + c2.z + c3.z) };  // sum of grads = 0
+  const double det = fabs(dot(e1, c1));
+  const double s = s6 * recip(det);
   k0 = dot(c0, c0) * s;
   k1 = dot(c0, c1) * s;
   k2 = dot(c0, c2) * s;
   k3 = dot(c0, c3) * s;
-  vol = det / 6.0;
+  return det;
 }
 
 // Triangle (x0,x1,x2) in the xy plane: grad N_a = c_a / A2 with
-// c_0 = (y1-y2, x2-x1), c_1 = (y2-y0, x0-x2), c_2 = (y0-y1, x1-x0),
+// c_1 = (e2.y, -e2.x), c_2 = (-e1.y, e1.x), c_0 = -(c_1 + c_2),
 // K_0b = |A2|/2 * c_0.c_b / A2^2 = c_0.c_b / (2|A2|)
 // (modules/poisson/FemModule.h:139-147, femutils/ArcaneFemFunctionsGpu.h:218-252).
-__device__ __forceinline__ void tri_row(V3 x0, V3 x1, V3 x2, double& k0, double& k1, double& k2, double& area)
+// `s2` = coef/2, returns |A2| = 2 * area.
+__device__ __forceinline__ double tri_row(V3 x0, V3 x1, V3 x2, double s2, double& k0, double& k1, double& k2)
 {
-  double c0x = x1.y - x2.y, c0y = x2.x - x1.x;
-  double c1x = x2.y - x0.y, c1y = x0.x - x2.x;
-  double c2x = x0.y - x1.y, c2y = x1.x - x0.x;
-  double A2 = fabs((x1.x - x0.x) * (x2.y - x0.y) - (x2.x - x0.x) * (x1.y - x0.y));
-  double s = 1.0 / (2.0 * A2);
+  const double e1x = x1.x - x0.x, e1y = x1.y - x0.y, e2x = x2.x - x0.x, e2y = x2.y - x0.y;
+  const double c1x = e2y, c1y = -e2x, c2x = -e1y, c2y = e1x;
+  const double c0x = -(c1x + c2x), c0y = -(c1y + c2y);
+  const double A2 = fabs(e1x * e2y - e2x * e1y);
+  const double s = s2 * recip(A2);
   k0 = (c0x * c0x + c0y * c0y) * s;
   k1 = (c0x * c1x + c0y * c1y) * s;
   k2 = (c0x * c2x + c0y * c2y) * s;
-  area = A2 * 0.5;
+  return A2;
 }
 
 // ---------------------------------------------------------------- scalar P1
+// Incidence entry k of the row in lane `lane` of slice `sl` lives at
+// inc[slice_ptr[sl] + (k/4)*256 + lane*4 + k%4]: one 16-B load per lane per 4
+// incidences, coalesced over the wave (1 KiB per load instruction).
+// Accumulation into the row's LDS slice uses ds_add_f64: a row is owned by a
+// single lane and a wave's LDS operations execute in program order, so the
+// summation order of every entry is fixed (bitwise reproducible) while the
+// read-modify-write latency stays off the lane's dependency chain.
 template <int NV, bool USE_LDS>
 __global__ __launch_bounds__(256) void k_assemble_p1(int64_t n_rows, int64_t seg_cap,
                                                      const int64_t* __restrict__ row_ptr,
@@ -101,8 +121,9 @@ __global__ __launch_bounds__(256) void k_assemble_p1(int64_t n_rows, int64_t seg
                                                      const uint32_t* __restrict__ inc,
                                                      const int64_t* __restrict__ slice_ptr,
                                                      const int32_t* __restrict__ slice_k,
-                                                     const double* __restrict__ coords, double coef, double f,
-                                                     double* __restrict__ vals, double* __restrict__ rhs)
+                                                     const double* __restrict__ coords, double s_coef,
+                                                     double f_meas, double* __restrict__ vals,
+                                                     double* __restrict__ rhs)
 {
   extern __shared__ __align__(16) unsigned char smem[];
   double* acc = reinterpret_cast<double*>(smem);
@@ -125,58 +146,66 @@ __global__ __launch_bounds__(256) void k_assemble_p1(int64_t n_rows, int64_t seg
   }
   if (r < r1) {
     const int64_t rb = row_ptr[r];
-    const int64_t off = rb - seg0;
+    double* arow = USE_LDS ? acc + (rb - seg0) : vals + rb;
+    const int32_t* crow = USE_LDS ? scol + (rb - seg0) : cols + rb;
     if (!USE_LDS) {
       const int64_t re = row_ptr[r + 1];
-      for (int64_t t = rb; t < re; ++t) vals[t] = 0.0;
+      for (int64_t t = 0; t < re - rb; ++t) arow[t] = 0.0;
     }
     const V3 xi = ld3(coords, r);
     const int64_t sl = r >> 6;
-    const uint32_t* ip = inc + slice_ptr[sl] + (r & 63);
-    const int kmax = slice_k[sl];
-    double dacc = 0.0, racc = 0.0;
+    const uint4* ip = reinterpret_cast<const uint4*>(inc + slice_ptr[sl]) + (r & 63);
+    const int ngroups = slice_k[sl] >> 2;
+    double dacc = 0.0, macc = 0.0;
     uint32_t dslot = 0xFFu;
-    for (int k = 0; k < kmax; ++k) {
-      const uint32_t e = ip[(int64_t)k * 64];
-      if (e == kPad) break;
-      const uint32_t s1 = e & 0xFFu, s2 = (e >> 8) & 0xFFu, s3 = (e >> 16) & 0xFFu;
-      dslot = e >> 24;
-      int32_t j1, j2, j3 = 0;
-      if (USE_LDS) {
-        j1 = scol[off + s1];
-        j2 = scol[off + s2];
-        if (NV == 4) j3 = scol[off + s3];
+    // Branch-free groups of 4 incidences (padding entries become a zero
+    // contribution to slot 0), so every LDS read and coordinate gather of
+    // the group is issued before the first element row is computed; the
+    // next group's incidence word is prefetched one group ahead.
+    uint4 e4 = ngroups > 0 ? ip[0] : make_uint4(kPad, kPad, kPad, kPad);
+    for (int g = 0; g < ngroups; ++g) {
+      const uint4 cur = e4;
+      if (cur.x == kPad) break;
+      if (g + 1 < ngroups) e4 = ip[(int64_t)(g + 1) * 64];
+      const uint32_t ev[4] = { cur.x, cur.y, cur.z, cur.w };
+      V3 xa[4], xb[4], xc[4];
+      uint32_t sa[4], sb[4], sc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t e = ev[j] == kPad ? 0u : ev[j];
+        sa[j] = e & 0xFFu;
+        sb[j] = (e >> 8) & 0xFFu;
+        sc[j] = (NV == 4) ? (e >> 16) & 0xFFu : 0u;
+        xa[j] = ld3(coords, crow[sa[j]]);
+        xb[j] = ld3(coords, crow[sb[j]]);
+        if (NV == 4) xc[j] = ld3(coords, crow[sc[j]]);
       }
-      else {
-        j1 = cols[rb + s1];
-        j2 = cols[rb + s2];
-        if (NV == 4) j3 = cols[rb + s3];
-      }
-      double k0, k1, k2, k3 = 0.0, meas;
-      if (NV == 4)
-        tet_row(xi, ld3(coords, j1), ld3(coords, j2), ld3(coords, j3), k0, k1, k2, k3, meas);
-      else
-        tri_row(xi, ld3(coords, j1), ld3(coords, j2), k0, k1, k2, meas);
-      dacc += coef * k0;
-      racc += f * meas / NV;
-      if (USE_LDS) {
-        acc[off + s1] += coef * k1;
-        acc[off + s2] += coef * k2;
-        if (NV == 4) acc[off + s3] += coef * k3;
-      }
-      else {
-        vals[rb + s1] += coef * k1;
-        vals[rb + s2] += coef * k2;
-        if (NV == 4) vals[rb + s3] += coef * k3;
+      dslot = (cur.x >> 24);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool valid = ev[j] != kPad;
+        double k0, k1, k2, k3 = 0.0, meas;
+        if (NV == 4)
+          meas = tet_row(xi, xa[j], xb[j], xc[j], s_coef, k0, k1, k2, k3);
+        else
+          meas = tri_row(xi, xa[j], xb[j], s_coef, k0, k1, k2);
+        if (!valid) k0 = k1 = k2 = k3 = meas = 0.0;
+        dacc += k0;
+        macc += meas;
+        if (USE_LDS) {
+          atomicAdd(arow + sa[j], k1);
+          atomicAdd(arow + sb[j], k2);
+          if (NV == 4) atomicAdd(arow + sc[j], k3);
+        }
+        else {
+          arow[sa[j]] += k1;
+          arow[sb[j]] += k2;
+          if (NV == 4) arow[sc[j]] += k3;
+        }
       }
     }
-    if (dslot != 0xFFu) {
-      if (USE_LDS)
-        acc[off + dslot] = dacc;
-      else
-        vals[rb + dslot] = dacc;
-    }
-    if (rhs) rhs[r] = racc;
+    if (dslot != 0xFFu) arow[dslot] = dacc;
+    if (rhs) rhs[r] = f_meas * macc;
   }
   if (USE_LDS) {
     __syncthreads();
@@ -231,12 +260,12 @@ __global__ __launch_bounds__(256) void k_assemble_elast_tri(int64_t n_rows, int6
       for (int64_t t = 0; t < 4 * nnz_row; ++t) vals[rb * 4 + t] = 0.0;
     const V3 x0 = ld3(coords, r);
     const int64_t sl = r >> 6;
-    const uint32_t* ip = inc + slice_ptr[sl] + (r & 63);
+    const uint32_t* ip = inc + slice_ptr[sl] + (r & 63) * 4;
     const int kmax = slice_k[sl];
     double d00 = 0, d01 = 0, d10 = 0, d11 = 0;
     uint32_t dslot = 0xFFu;
     for (int k = 0; k < kmax; ++k) {
-      const uint32_t e = ip[(int64_t)k * 64];
+      const uint32_t e = ip[(int64_t)(k >> 2) * 256 + (k & 3)];
       if (e == kPad) break;
       const int s[2] = { (int)(e & 0xFFu), (int)((e >> 8) & 0xFFu) };
       dslot = e >> 24;
@@ -420,25 +449,29 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
   const int rpb = lds ? s.rows_per_block : 256;
   const unsigned nblk = (unsigned)((s.n_rows + rpb - 1) / rpb);
   const size_t shm = lds ? (size_t)s.max_seg * 12 : 0;
+  // K = coef * c0.cb / (6|det|) (tets) or / (2|A2|) (triangles);
+  // RHS = f * |K| / nv = f*|det|/24 (tets) or f*|A2|/6 (triangles)
+  const double s_coef = (nv == 4) ? coef / 6.0 : coef / 2.0;
+  const double f_meas = (nv == 4) ? f / 24.0 : f / 6.0;
   if (nv == 4) {
     if (lds)
       hipLaunchKernelGGL((k_assemble_p1<4, true>), dim3(nblk), dim3(rpb), shm, ctx.stream, s.n_rows, s.max_seg,
-                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, coef, f,
-                         b.values.p, rhs);
+                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef,
+                         f_meas, b.values.p, rhs);
     else
       hipLaunchKernelGGL((k_assemble_p1<4, false>), dim3(nblk), dim3(rpb), 0, ctx.stream, s.n_rows, s.max_seg,
-                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, coef, f,
-                         b.values.p, rhs);
+                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef,
+                         f_meas, b.values.p, rhs);
   }
   else {
     if (lds)
       hipLaunchKernelGGL((k_assemble_p1<3, true>), dim3(nblk), dim3(rpb), shm, ctx.stream, s.n_rows, s.max_seg,
-                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, coef, f,
-                         b.values.p, rhs);
+                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef,
+                         f_meas, b.values.p, rhs);
     else
       hipLaunchKernelGGL((k_assemble_p1<3, false>), dim3(nblk), dim3(rpb), 0, ctx.stream, s.n_rows, s.max_seg,
-                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, coef, f,
-                         b.values.p, rhs);
+                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef,
+                         f_meas, b.values.p, rhs);
   }
   AFEM_LAUNCHED();
 }

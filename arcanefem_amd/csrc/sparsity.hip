@@ -14,8 +14,9 @@
 //   3. the row-local incidence table used by the assembly kernels: for every
 //      (row, incident cell) the row-slots of the cell's other nodes packed in
 //      one uint32 (8 bits per slot, diagonal slot in the top byte), stored as
-//      sliced ELLPACK with slice height 64 = one wavefront, so a wave reads
-//      one coalesced 256-byte line per incidence step.
+//      sliced ELLPACK with slice height 64 = one wavefront, 4 consecutive
+//      incidences of a row packed per lane, so a wave reads one coalesced
+//      1-KiB line (a 16-B load per lane) per 4 incidence steps.
 #include "afem_internal.hpp"
 
 namespace afem {
@@ -143,6 +144,7 @@ __global__ void k_slice_width(int64_t n_rows, int64_t n_slices, const int64_t* _
     int64_t c = nc_ptr[r + 1] - nc_ptr[r];
     w = c > w ? c : w;
   }
+  w = (w + 3) & ~(int64_t)3;  // groups of 4 incidences per lane (one 16-B load)
   slice_k[s] = (int32_t)w;
   slice_sz[s] = w * 64;
 }
@@ -172,7 +174,7 @@ __global__ void k_fill_inc(int64_t n_rows, int nv, const int32_t* __restrict__ c
   const int32_t* c = cols + row_ptr[r];
   const int len = (int)(row_ptr[r + 1] - row_ptr[r]);
   const uint32_t dslot = (uint32_t)find_slot(c, len, (int32_t)r);
-  uint32_t* out = inc + slice_ptr[s] + lane;
+  uint32_t* out = inc + slice_ptr[s] + lane * 4;  // entry k at (k/4)*256 + lane*4 + k%4
   const int64_t b = nc_ptr[r];
   const int cnt = (int)(nc_ptr[r + 1] - b);
   for (int k = 0; k < cnt; ++k) {
@@ -186,9 +188,9 @@ __global__ void k_fill_inc(int64_t n_rows, int nv, const int32_t* __restrict__ c
       ++o;
     }
     if (nv == 3) packed |= 0xFFu << 16;  // unused third slot
-    out[(int64_t)k * 64] = packed;
+    out[(int64_t)(k >> 2) * 256 + (k & 3)] = packed;
   }
-  for (int k = cnt; k < slice_k[s]; ++k) out[(int64_t)k * 64] = kPad;
+  for (int k = cnt; k < slice_k[s]; ++k) out[(int64_t)(k >> 2) * 256 + (k & 3)] = kPad;
 }
 
 __global__ void k_block_seg(int64_t n_rows, int rpb, const int64_t* __restrict__ row_ptr, unsigned long long* out)
