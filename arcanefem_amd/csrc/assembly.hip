@@ -24,6 +24,8 @@
 //     values, RHS, coordinates once.
 #include "afem_internal.hpp"
 
+#include <cstdlib>
+
 namespace afem {
 namespace {
 
@@ -107,6 +109,8 @@ __device__ __forceinline__ double tri_row(V3 x0, V3 x1, V3 x2, double s2, double
 }
 
 // ---------------------------------------------------------------- scalar P1
+__host__ __device__ constexpr int64_t lds_acc_bytes(int64_t seg_cap) { return ((8 * (seg_cap + 2)) + 15) & ~int64_t(15); }
+__host__ __device__ constexpr int64_t lds_scalar_bytes(int64_t seg_cap) { return lds_acc_bytes(seg_cap) + 4 * (seg_cap + 8); }
 // Incidence entry k of the row in lane `lane` of slice `sl` lives at
 // inc[slice_ptr[sl] + (k/4)*256 + lane*4 + k%4]: one 16-B load per lane per 4
 // incidences, coalesced over the wave (1 KiB per load instruction).
@@ -114,7 +118,9 @@ __device__ __forceinline__ double tri_row(V3 x0, V3 x1, V3 x2, double s2, double
 // single lane and a wave's LDS operations execute in program order, so the
 // summation order of every entry is fixed (bitwise reproducible) while the
 // read-modify-write latency stays off the lane's dependency chain.
-template <int NV, bool USE_LDS>
+// ABL != 0 only in diagnostic runs (AFEM_ASSEMBLY_ABLATION, results wrong):
+// 1 = no element arithmetic, 2 = no coordinate gathers, 3 = no LDS adds.
+template <int NV, bool USE_LDS, int ABL = 0>
 __global__ __launch_bounds__(256) void k_assemble_p1(int64_t n_rows, int64_t seg_cap,
                                                      const int64_t* __restrict__ row_ptr,
                                                      const int32_t* __restrict__ cols,
@@ -126,43 +132,64 @@ __global__ __launch_bounds__(256) void k_assemble_p1(int64_t n_rows, int64_t seg
                                                      double* __restrict__ rhs)
 {
   extern __shared__ __align__(16) unsigned char smem[];
-  double* acc = reinterpret_cast<double*>(smem);
-  int32_t* scol = reinterpret_cast<int32_t*>(smem + 8 * seg_cap);
+  double* acc = reinterpret_cast<double*>(smem);  // [seg_cap + 2] (16-B zeroing)
+  int32_t* scol = reinterpret_cast<int32_t*>(smem + lds_acc_bytes(seg_cap));  // [seg_cap + 8] (16-B aligned window)
 
   const int rpb = blockDim.x;
   const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
   const int64_t r0 = blk * rpb;
   const int64_t r1 = (r0 + rpb < n_rows) ? r0 + rpb : n_rows;
-  const int64_t seg0 = row_ptr[r0];
   const int64_t r = r0 + threadIdx.x;
+  const bool active = r < r1;
 
+  // Per-lane prologue loads first, so their latency overlaps the staging of
+  // the block's columns below (nothing orders them after the barrier).
+  const int64_t seg0 = row_ptr[r0];
+  const int64_t seg1 = row_ptr[r1];
+  const int64_t rb = active ? row_ptr[r] : seg0;
+  const int64_t re = active ? row_ptr[r + 1] : seg0;
+  const V3 xi = ld3(coords, active ? r : r0);
+  const int64_t sl = (active ? r : r0) >> 6;
+  const uint4* ip = reinterpret_cast<const uint4*>(inc + slice_ptr[sl]) + (r & 63);
+  const int ngroups = active ? (slice_k[sl] >> 2) : 0;
+  uint4 e4 = ngroups > 0 ? ip[0] : make_uint4(kPad, kPad, kPad, kPad);
+
+  // Columns of the block staged in LDS with 16-B loads from the 16-B aligned
+  // start (cols is allocated with 4 ints of tail padding), all of a thread's
+  // loads issued before its LDS writes; accumulators zeroed with 16-B stores.
+  const int64_t q0 = seg0 >> 2;  // first uint4 of the segment
   if (USE_LDS) {
-    const int64_t seglen = row_ptr[r1] - seg0;
-    for (int64_t t = threadIdx.x; t < seglen; t += rpb) {
-      scol[t] = cols[seg0 + t];
-      acc[t] = 0.0;
+    const int64_t nq = ((seg1 + 3) >> 2) - q0;
+    const uint4* src = reinterpret_cast<const uint4*>(cols) + q0;
+    uint4* dst = reinterpret_cast<uint4*>(scol);
+    for (int64_t q = threadIdx.x; q < nq; q += 4 * rpb) {
+      const bool b1 = q + rpb < nq, b2 = q + 2 * rpb < nq, b3 = q + 3 * rpb < nq;
+      const uint4 v0 = src[q];
+      const uint4 v1 = b1 ? src[q + rpb] : make_uint4(0, 0, 0, 0);
+      const uint4 v2 = b2 ? src[q + 2 * rpb] : make_uint4(0, 0, 0, 0);
+      const uint4 v3 = b3 ? src[q + 3 * rpb] : make_uint4(0, 0, 0, 0);
+      dst[q] = v0;
+      if (b1) dst[q + rpb] = v1;
+      if (b2) dst[q + 2 * rpb] = v2;
+      if (b3) dst[q + 3 * rpb] = v3;
     }
+    const int64_t n2 = (seg1 - seg0 + 1) >> 1;
+    double2* a2 = reinterpret_cast<double2*>(acc);
+    for (int64_t t = threadIdx.x; t < n2; t += rpb) a2[t] = make_double2(0.0, 0.0);
     __syncthreads();
   }
-  if (r < r1) {
-    const int64_t rb = row_ptr[r];
+  if (active) {
     double* arow = USE_LDS ? acc + (rb - seg0) : vals + rb;
-    const int32_t* crow = USE_LDS ? scol + (rb - seg0) : cols + rb;
+    const int32_t* crow = USE_LDS ? scol + (rb - 4 * q0) : cols + rb;
     if (!USE_LDS) {
-      const int64_t re = row_ptr[r + 1];
       for (int64_t t = 0; t < re - rb; ++t) arow[t] = 0.0;
     }
-    const V3 xi = ld3(coords, r);
-    const int64_t sl = r >> 6;
-    const uint4* ip = reinterpret_cast<const uint4*>(inc + slice_ptr[sl]) + (r & 63);
-    const int ngroups = slice_k[sl] >> 2;
     double dacc = 0.0, macc = 0.0;
     uint32_t dslot = 0xFFu;
     // Branch-free groups of 4 incidences (padding entries become a zero
     // contribution to slot 0), so every LDS read and coordinate gather of
     // the group is issued before the first element row is computed; the
     // next group's incidence word is prefetched one group ahead.
-    uint4 e4 = ngroups > 0 ? ip[0] : make_uint4(kPad, kPad, kPad, kPad);
     for (int g = 0; g < ngroups; ++g) {
       const uint4 cur = e4;
       if (cur.x == kPad) break;
@@ -176,23 +203,42 @@ __global__ __launch_bounds__(256) void k_assemble_p1(int64_t n_rows, int64_t seg
         sa[j] = e & 0xFFu;
         sb[j] = (e >> 8) & 0xFFu;
         sc[j] = (NV == 4) ? (e >> 16) & 0xFFu : 0u;
-        xa[j] = ld3(coords, crow[sa[j]]);
-        xb[j] = ld3(coords, crow[sb[j]]);
-        if (NV == 4) xc[j] = ld3(coords, crow[sc[j]]);
+        if (ABL == 2) {
+          const double da = 1e-3 * (double)crow[sa[j]], db = 2e-3 * (double)crow[sb[j]],
+                       dc = 3e-3 * (double)crow[sc[j]];
+          xa[j] = V3{ xi.x + da, xi.y, xi.z };
+          xb[j] = V3{ xi.x, xi.y + db, xi.z };
+          xc[j] = V3{ xi.x, xi.y, xi.z + dc };
+        }
+        else {
+          xa[j] = ld3(coords, crow[sa[j]]);
+          xb[j] = ld3(coords, crow[sb[j]]);
+          if (NV == 4) xc[j] = ld3(coords, crow[sc[j]]);
+        }
       }
       dslot = (cur.x >> 24);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bool valid = ev[j] != kPad;
         double k0, k1, k2, k3 = 0.0, meas;
-        if (NV == 4)
+        if (ABL == 1) {
+          k0 = xa[j].x;
+          k1 = xa[j].y + xb[j].x;
+          k2 = xb[j].y + xc[j].x;
+          k3 = xc[j].y + xc[j].z;
+          meas = xa[j].z + xb[j].z;
+        }
+        else if (NV == 4)
           meas = tet_row(xi, xa[j], xb[j], xc[j], s_coef, k0, k1, k2, k3);
         else
           meas = tri_row(xi, xa[j], xb[j], s_coef, k0, k1, k2);
         if (!valid) k0 = k1 = k2 = k3 = meas = 0.0;
         dacc += k0;
         macc += meas;
-        if (USE_LDS) {
+        if (ABL == 3) {
+          dacc += k1 + k2 + k3;
+        }
+        else if (USE_LDS) {
           atomicAdd(arow + sa[j], k1);
           atomicAdd(arow + sb[j], k2);
           if (NV == 4) atomicAdd(arow + sc[j], k3);
@@ -209,8 +255,7 @@ __global__ __launch_bounds__(256) void k_assemble_p1(int64_t n_rows, int64_t seg
   }
   if (USE_LDS) {
     __syncthreads();
-    const int64_t seglen = row_ptr[r1] - seg0;
-    for (int64_t t = threadIdx.x; t < seglen; t += rpb) vals[seg0 + t] = acc[t];
+    for (int64_t t = threadIdx.x; t < seg1 - seg0; t += rpb) vals[seg0 + t] = acc[t];
   }
 }
 
@@ -448,31 +493,32 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
   const bool lds = s.rows_per_block > 0;
   const int rpb = lds ? s.rows_per_block : 256;
   const unsigned nblk = (unsigned)((s.n_rows + rpb - 1) / rpb);
-  const size_t shm = lds ? (size_t)s.max_seg * 12 : 0;
+  const size_t shm = lds ? (size_t)lds_scalar_bytes(s.max_seg) : 0;
   // K = coef * c0.cb / (6|det|) (tets) or / (2|A2|) (triangles);
   // RHS = f * |K| / nv = f*|det|/24 (tets) or f*|A2|/6 (triangles)
   const double s_coef = (nv == 4) ? coef / 6.0 : coef / 2.0;
   const double f_meas = (nv == 4) ? f / 24.0 : f / 6.0;
-  if (nv == 4) {
-    if (lds)
-      hipLaunchKernelGGL((k_assemble_p1<4, true>), dim3(nblk), dim3(rpb), shm, ctx.stream, s.n_rows, s.max_seg,
-                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef,
-                         f_meas, b.values.p, rhs);
-    else
-      hipLaunchKernelGGL((k_assemble_p1<4, false>), dim3(nblk), dim3(rpb), 0, ctx.stream, s.n_rows, s.max_seg,
-                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef,
-                         f_meas, b.values.p, rhs);
+  static const int abl = [] {
+    const char* e = getenv("AFEM_ASSEMBLY_ABLATION");
+    return e ? atoi(e) : 0;
+  }();
+#define AFEM_ASM_ARGS s.n_rows, s.max_seg, s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, \
+                      b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs
+  if (nv == 4 && lds) {
+    switch (abl) {
+      case 1: hipLaunchKernelGGL((k_assemble_p1<4, true, 1>), dim3(nblk), dim3(rpb), shm, ctx.stream, AFEM_ASM_ARGS); break;
+      case 2: hipLaunchKernelGGL((k_assemble_p1<4, true, 2>), dim3(nblk), dim3(rpb), shm, ctx.stream, AFEM_ASM_ARGS); break;
+      case 3: hipLaunchKernelGGL((k_assemble_p1<4, true, 3>), dim3(nblk), dim3(rpb), shm, ctx.stream, AFEM_ASM_ARGS); break;
+      default: hipLaunchKernelGGL((k_assemble_p1<4, true>), dim3(nblk), dim3(rpb), shm, ctx.stream, AFEM_ASM_ARGS);
+    }
   }
-  else {
-    if (lds)
-      hipLaunchKernelGGL((k_assemble_p1<3, true>), dim3(nblk), dim3(rpb), shm, ctx.stream, s.n_rows, s.max_seg,
-                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef,
-                         f_meas, b.values.p, rhs);
-    else
-      hipLaunchKernelGGL((k_assemble_p1<3, false>), dim3(nblk), dim3(rpb), 0, ctx.stream, s.n_rows, s.max_seg,
-                         s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef,
-                         f_meas, b.values.p, rhs);
-  }
+  else if (nv == 4)
+    hipLaunchKernelGGL((k_assemble_p1<4, false>), dim3(nblk), dim3(rpb), 0, ctx.stream, AFEM_ASM_ARGS);
+  else if (lds)
+    hipLaunchKernelGGL((k_assemble_p1<3, true>), dim3(nblk), dim3(rpb), shm, ctx.stream, AFEM_ASM_ARGS);
+  else
+    hipLaunchKernelGGL((k_assemble_p1<3, false>), dim3(nblk), dim3(rpb), 0, ctx.stream, AFEM_ASM_ARGS);
+#undef AFEM_ASM_ARGS
   AFEM_LAUNCHED();
 }
 

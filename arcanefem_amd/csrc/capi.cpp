@@ -469,7 +469,8 @@ int afem_bsr_download(afem_bsr* b, int64_t* rows, int32_t* cols, double* vals)
   Ctx& ctx = *b->mesh->ctx;
   ctx.set_device();
   if (rows) AFEM_HIP(hipMemcpyAsync(rows, b->s.row_ptr.p, b->s.row_ptr.bytes(), hipMemcpyDeviceToHost, ctx.stream));
-  if (cols && b->s.nnz) AFEM_HIP(hipMemcpyAsync(cols, b->s.cols.p, b->s.cols.bytes(), hipMemcpyDeviceToHost, ctx.stream));
+  if (cols && b->s.nnz)
+    AFEM_HIP(hipMemcpyAsync(cols, b->s.cols.p, (size_t)b->s.nnz * sizeof(int32_t), hipMemcpyDeviceToHost, ctx.stream));
   if (vals && b->values.n)
     AFEM_HIP(hipMemcpyAsync(vals, b->values.p, b->values.bytes(), hipMemcpyDeviceToHost, ctx.stream));
   ctx.sync();

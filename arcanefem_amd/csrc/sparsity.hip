@@ -261,7 +261,8 @@ void build_structure(Mesh& m, Structure& s)
   s.row_ptr.alloc(n_rows + 1);
   exclusive_scan_i32_to_i64(ctx, row_len.p, s.row_ptr.p, n_rows);
   s.nnz = read_i64(ctx, s.row_ptr.p + n_rows);
-  s.cols.alloc(s.nnz);
+  s.cols.alloc(s.nnz + 4);  // tail padding: the assembly stages columns with 16-B loads
+  AFEM_HIP(hipMemsetAsync(s.cols.p + s.nnz, 0, 4 * sizeof(int32_t), ctx.stream));
   s.diag_pos.alloc(n_rows);
   hipLaunchKernelGGL(k_row_union<true>, dim3(grid_for(n_rows, kUnionThreads)), dim3(kUnionThreads), 0, ctx.stream,
                      n_rows, nv, m.cell_node.p, nc_ptr.p, nc.p, nullptr, s.row_ptr.p, s.cols.p, s.diag_pos.p);
@@ -298,7 +299,7 @@ void build_structure(Mesh& m, Structure& s)
     unsigned long long hm = 0;
     AFEM_HIP(hipMemcpyAsync(&hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
     ctx.sync();
-    if (hm * 12ull <= 64ull * 1024ull) {
+    if (hm * 12ull + 128ull <= 64ull * 1024ull) {
       s.rows_per_block = rpb;
       s.max_seg = (int64_t)hm;
       break;
