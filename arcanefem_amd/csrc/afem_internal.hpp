@@ -119,6 +119,7 @@ struct Structure {
   int max_row_len = 0;
   int64_t max_seg = 0;       // max nnz over assembly blocks of rows_per_block rows
   int rows_per_block = 256;
+  int64_t max_wave_seg = 0;  // max nnz of one slice of 64 rows
   DevBuf<int64_t> diag_pos;  // [n_rows] position of the diagonal in cols
 };
 

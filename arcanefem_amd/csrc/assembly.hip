@@ -110,7 +110,10 @@ __device__ __forceinline__ double tri_row(V3 x0, V3 x1, V3 x2, double s2, double
 
 // ---------------------------------------------------------------- scalar P1
 __host__ __device__ constexpr int64_t lds_acc_bytes(int64_t seg_cap) { return ((8 * (seg_cap + 2)) + 15) & ~int64_t(15); }
-__host__ __device__ constexpr int64_t lds_scalar_bytes(int64_t seg_cap) { return lds_acc_bytes(seg_cap) + 4 * (seg_cap + 8); }
+__host__ __device__ constexpr int64_t lds_scalar_bytes(int64_t seg_cap)
+{
+  return (lds_acc_bytes(seg_cap) + 4 * (seg_cap + 8) + 15) & ~int64_t(15);
+}
 // Incidence entry k of the row in lane `lane` of slice `sl` lives at
 // inc[slice_ptr[sl] + (k/4)*256 + lane*4 + k%4]: one 16-B load per lane per 4
 // incidences, coalesced over the wave (1 KiB per load instruction).
@@ -131,52 +134,61 @@ __global__ __launch_bounds__(256) void k_assemble_p1(int64_t n_rows, int64_t seg
                                                      double f_meas, double* __restrict__ vals,
                                                      double* __restrict__ rhs)
 {
+  // Wave-local: each wave owns one slice of 64 consecutive rows and its own
+  // LDS region (accumulators + the slice's columns).  No workgroup barrier:
+  // a wave's LDS operations execute in order, so its staging, accumulation
+  // and write-back need no synchronisation with the other waves, and the
+  // waves of a CU drift through the stage/compute/write phases independently.
   extern __shared__ __align__(16) unsigned char smem[];
-  double* acc = reinterpret_cast<double*>(smem);  // [seg_cap + 2] (16-B zeroing)
-  int32_t* scol = reinterpret_cast<int32_t*>(smem + lds_acc_bytes(seg_cap));  // [seg_cap + 8] (16-B aligned window)
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  unsigned char* wmem = smem + (size_t)wid * (size_t)lds_scalar_bytes(seg_cap);
+  double* acc = reinterpret_cast<double*>(wmem);                                // [seg_cap + 2]
+  int32_t* scol = reinterpret_cast<int32_t*>(wmem + lds_acc_bytes(seg_cap));  // [seg_cap + 8]
 
-  const int rpb = blockDim.x;
+  const int64_t n_slices = (n_rows + 63) >> 6;
   const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int64_t r0 = blk * rpb;
-  const int64_t r1 = (r0 + rpb < n_rows) ? r0 + rpb : n_rows;
-  const int64_t r = r0 + threadIdx.x;
+  const int64_t sl = blk * (int64_t)(blockDim.x >> 6) + wid;
+  if (sl >= n_slices) return;  // whole wave: no barrier follows
+  const int64_t r0 = sl << 6;
+  const int64_t r1 = (r0 + 64 < n_rows) ? r0 + 64 : n_rows;
+  const int64_t r = r0 + lane;
   const bool active = r < r1;
 
-  // Per-lane prologue loads first, so their latency overlaps the staging of
-  // the block's columns below (nothing orders them after the barrier).
+  // Per-lane prologue loads first, so their latency overlaps the staging.
   const int64_t seg0 = row_ptr[r0];
   const int64_t seg1 = row_ptr[r1];
   const int64_t rb = active ? row_ptr[r] : seg0;
   const int64_t re = active ? row_ptr[r + 1] : seg0;
   const V3 xi = ld3(coords, active ? r : r0);
-  const int64_t sl = (active ? r : r0) >> 6;
-  const uint4* ip = reinterpret_cast<const uint4*>(inc + slice_ptr[sl]) + (r & 63);
+  const uint4* ip = reinterpret_cast<const uint4*>(inc + slice_ptr[sl]) + lane;
   const int ngroups = active ? (slice_k[sl] >> 2) : 0;
   uint4 e4 = ngroups > 0 ? ip[0] : make_uint4(kPad, kPad, kPad, kPad);
 
-  // Columns of the block staged in LDS with 16-B loads from the 16-B aligned
-  // start (cols is allocated with 4 ints of tail padding), all of a thread's
-  // loads issued before its LDS writes; accumulators zeroed with 16-B stores.
+  // The slice's columns staged in LDS with 16-B loads from the 16-B aligned
+  // start (cols carries 4 ints of tail padding), all of a lane's loads issued
+  // before its LDS writes; accumulators zeroed with 16-B stores.
   const int64_t q0 = seg0 >> 2;  // first uint4 of the segment
   if (USE_LDS) {
     const int64_t nq = ((seg1 + 3) >> 2) - q0;
     const uint4* src = reinterpret_cast<const uint4*>(cols) + q0;
     uint4* dst = reinterpret_cast<uint4*>(scol);
-    for (int64_t q = threadIdx.x; q < nq; q += 4 * rpb) {
-      const bool b1 = q + rpb < nq, b2 = q + 2 * rpb < nq, b3 = q + 3 * rpb < nq;
+    for (int64_t q = lane; q < nq; q += 256) {
+      const bool b1 = q + 64 < nq, b2 = q + 128 < nq, b3 = q + 192 < nq;
       const uint4 v0 = src[q];
-      const uint4 v1 = b1 ? src[q + rpb] : make_uint4(0, 0, 0, 0);
-      const uint4 v2 = b2 ? src[q + 2 * rpb] : make_uint4(0, 0, 0, 0);
-      const uint4 v3 = b3 ? src[q + 3 * rpb] : make_uint4(0, 0, 0, 0);
+      const uint4 v1 = b1 ? src[q + 64] : make_uint4(0, 0, 0, 0);
+      const uint4 v2 = b2 ? src[q + 128] : make_uint4(0, 0, 0, 0);
+      const uint4 v3 = b3 ? src[q + 192] : make_uint4(0, 0, 0, 0);
       dst[q] = v0;
-      if (b1) dst[q + rpb] = v1;
-      if (b2) dst[q + 2 * rpb] = v2;
-      if (b3) dst[q + 3 * rpb] = v3;
+      if (b1) dst[q + 64] = v1;
+      if (b2) dst[q + 128] = v2;
+      if (b3) dst[q + 192] = v3;
     }
     const int64_t n2 = (seg1 - seg0 + 1) >> 1;
     double2* a2 = reinterpret_cast<double2*>(acc);
-    for (int64_t t = threadIdx.x; t < n2; t += rpb) a2[t] = make_double2(0.0, 0.0);
-    __syncthreads();
+    for (int64_t t = lane; t < n2; t += 64) a2[t] = make_double2(0.0, 0.0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
   if (active) {
     double* arow = USE_LDS ? acc + (rb - seg0) : vals + rb;
@@ -254,8 +266,9 @@ __global__ __launch_bounds__(256) void k_assemble_p1(int64_t n_rows, int64_t seg
     if (rhs) rhs[r] = f_meas * macc;
   }
   if (USE_LDS) {
-    __syncthreads();
-    for (int64_t t = threadIdx.x; t < seg1 - seg0; t += rpb) vals[seg0 + t] = acc[t];
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int64_t t = lane; t < seg1 - seg0; t += 64) vals[seg0 + t] = acc[t];
   }
 }
 
@@ -490,10 +503,12 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
   Ctx& ctx = *b.mesh->ctx;
   const int nv = b.mesh->nv;
   AFEM_REQUIRE(b.nb_dof == 1, AFEM_ERR_ARG, "assembleBilinear(P1 Laplacian) needs NB_DOF = 1");
-  const bool lds = s.rows_per_block > 0;
-  const int rpb = lds ? s.rows_per_block : 256;
-  const unsigned nblk = (unsigned)((s.n_rows + rpb - 1) / rpb);
-  const size_t shm = lds ? (size_t)lds_scalar_bytes(s.max_seg) : 0;
+  // wave-local kernel: 4 waves per workgroup, one LDS region per wave
+  const int64_t wave_lds = lds_scalar_bytes(s.max_wave_seg);
+  const bool lds = 4 * wave_lds <= 64 * 1024;
+  const int rpb = 256;
+  const unsigned nblk = lds ? (unsigned)((s.n_slices + 3) / 4) : (unsigned)((s.n_rows + rpb - 1) / rpb);
+  const size_t shm = lds ? (size_t)(4 * wave_lds) : 0;
   // K = coef * c0.cb / (6|det|) (tets) or / (2|A2|) (triangles);
   // RHS = f * |K| / nv = f*|det|/24 (tets) or f*|A2|/6 (triangles)
   const double s_coef = (nv == 4) ? coef / 6.0 : coef / 2.0;
@@ -502,7 +517,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
     const char* e = getenv("AFEM_ASSEMBLY_ABLATION");
     return e ? atoi(e) : 0;
   }();
-#define AFEM_ASM_ARGS s.n_rows, s.max_seg, s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, \
+#define AFEM_ASM_ARGS s.n_rows, s.max_wave_seg, s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, \
                       b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs
   if (nv == 4 && lds) {
     switch (abl) {

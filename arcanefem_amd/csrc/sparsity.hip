@@ -305,6 +305,17 @@ void build_structure(Mesh& m, Structure& s)
       break;
     }
   }
+  // per-wave (slice of 64 rows) maximum segment, for the wave-local kernels
+  {
+    AFEM_HIP(hipMemsetAsync(mx.p, 0, mx.bytes(), ctx.stream));
+    hipLaunchKernelGGL(k_block_seg, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, n_rows, 64, s.row_ptr.p,
+                       mx.p);
+    AFEM_LAUNCHED();
+    unsigned long long hm = 0;
+    AFEM_HIP(hipMemcpyAsync(&hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    s.max_wave_seg = (int64_t)hm;
+  }
   ctx.sync();
 }
 
