@@ -39,7 +39,9 @@ class CsrView(ctypes.Structure):
 
 class BsrStats(ctypes.Structure):
     _fields_ = [("n_incidences", ctypes.c_int64), ("inc_table_entries", ctypes.c_int64),
-                ("max_row_len", ctypes.c_int32), ("rows_per_block", ctypes.c_int32), ("max_seg", ctypes.c_int64)]
+                ("max_row_len", ctypes.c_int32), ("rows_per_block", ctypes.c_int32), ("max_seg", ctypes.c_int64),
+                ("max_slice_nodes", ctypes.c_int32), ("max_slice_width", ctypes.c_int32),
+                ("n_slices", ctypes.c_int64), ("brick_order", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class SolverOpts(ctypes.Structure):

@@ -107,19 +107,37 @@ struct Structure {
   int64_t n_rows = 0, n_cols = 0, nnz = 0;
   DevBuf<int64_t> row_ptr;  // [n_rows+1]
   DevBuf<int32_t> cols;     // [nnz], sorted ascending per row
+  // Assembly processing order: slice s (one wavefront) processes the rows
+  // perm[64*s + lane] (-1 = idle lane).  Structured boxes use 4x4x4 (3D) /
+  // 8x8 (2D) node bricks, so a slice's rows share most neighbours; other
+  // meshes use the node order.  The matrix itself stays in node order.
+  DevBuf<int32_t> perm;  // [n_slices*64]
+  bool brick_order = false;
+  // Lanes [j*run, (j+1)*run) of a slice hold consecutive rows (an x-run of a
+  // brick, or the whole slice in node order), idle lanes only at the end of
+  // a run: their value segments are one contiguous range.
+  int run = 64;
   // Row-local incidence table, sliced ELLPACK with C = 64 (one wavefront):
   // entry (slice s, k, lane) at inc_slice_ptr[s] + (k/4)*256 + lane*4 + k%4 describes the
-  // k-th cell incident to row 64*s+lane as the row-slots of the cell's other
-  // nodes (one byte each) and the row's diagonal slot in the top byte.
+  // k-th cell incident to row perm[64*s+lane] as the row-slots of the cell's
+  // other nodes (one byte each) and the row's diagonal slot in the top byte.
   DevBuf<uint32_t> inc;
   DevBuf<int64_t> inc_slice_ptr;  // [n_slices+1]
   DevBuf<int32_t> inc_slice_k;    // [n_slices] max incidences in the slice
+  // Per slice: the sorted unique nodes its rows couple to (snode, the
+  // coordinate cache the assembly stages in LDS) and, for every (slot t,
+  // lane), the index of column cols[row_ptr[row]+t] in that list:
+  // lidx[lidx_ptr[s] + 64*t + lane] (0 past the row's end).
+  DevBuf<int32_t> slice_w;     // [n_slices] max row length in the slice
+  DevBuf<int64_t> lidx_ptr;    // [n_slices+1] = 64 * prefix sum of slice_w
+  DevBuf<uint16_t> lidx;
+  DevBuf<int64_t> snode_ptr;   // [n_slices+1]
+  DevBuf<int32_t> snode;
+  int max_slice_nodes = 0, max_slice_w = 0;
   int64_t n_slices = 0;
   int64_t n_incidences = 0;  // real (non-padding) entries
   int max_row_len = 0;
-  int64_t max_seg = 0;       // max nnz over assembly blocks of rows_per_block rows
-  int rows_per_block = 256;
-  int64_t max_wave_seg = 0;  // max nnz of one slice of 64 rows
+  int64_t max_wave_seg = 0;  // max nnz of one slice
   DevBuf<int64_t> diag_pos;  // [n_rows] position of the diagonal in cols
 };
 
@@ -187,6 +205,7 @@ int64_t read_i64(Ctx& ctx, const int64_t* d);
 void build_structure(Mesh& m, Structure& s);
 void assemble_scalar(Bsr& b, double coef, double f, double* rhs);
 void assemble_elasticity_tri(Bsr& b, double lambda, double mu2);
+bool assembly_uses_lds(const Bsr& b);  // slice tile fits the LDS budget
 
 void ls_apply_bcs(LinearSystem& ls);
 void ls_solve(LinearSystem& ls, afem_solve_stats* st);

@@ -3,17 +3,16 @@
 // femutils/BSRFormat.h:786-898, and the RHS source term of
 // femutils/ArcaneFemFunctionsGpu.h:401-429).
 //
-// Design: a workgroup owns a contiguous block of rows,
-// i.e. a contiguous segment of the CSR value array.  Each lane owns one row
-// and walks the row's incident cells through the row-local incidence table
-// (sliced ELL, one coalesced 256-B wave load per step).  An incidence gives
-// the row-slots of the cell's other nodes, so the lane recovers their node
-// ids from the row's columns (staged in LDS), gathers their coordinates
-// (L1/L2/Infinity-Cache resident: each node is a neighbour of ~15 rows),
-// recomputes the element row K_e[row node, :] and accumulates it into the
-// row's slice of an LDS accumulator.  The diagonal and the RHS are
-// accumulated in registers.  The block then streams its finished segment to
-// HBM with coalesced stores.  Consequences:
+// Design: a wavefront owns a slice of 64 rows (a 4x4x4
+// node brick on structured meshes) and stages in LDS the coordinates of the
+// nodes those rows couple to plus the rows' local column indices.  Each lane
+// owns one row and walks the row's incident cells through the row-local
+// incidence table (sliced ELL, one coalesced 1-KiB wave load per 4 steps).
+// An incidence gives the row-slots of the cell's other nodes; the lane reads
+// their coordinates from LDS, recomputes the element row K_e[row node, :] and
+// accumulates it into the row's LDS accumulators.  The diagonal and the RHS
+// are accumulated in registers; the finished rows are written once.
+// Consequences:
 //   * every value is written exactly once, no zero-fill pass, no float
 //     atomics (global f64 atomics run at ~1.3 TB/s at best and ~0.08 TB/s
 //     when 64 lanes hit 64 rows — the reference's access pattern);
@@ -25,6 +24,7 @@
 #include "afem_internal.hpp"
 
 #include <cstdlib>
+
 
 namespace afem {
 namespace {
@@ -108,168 +108,340 @@ __device__ __forceinline__ double tri_row(V3 x0, V3 x1, V3 x2, double s2, double
   return A2;
 }
 
-// ---------------------------------------------------------------- scalar P1
-__host__ __device__ constexpr int64_t lds_acc_bytes(int64_t seg_cap) { return ((8 * (seg_cap + 2)) + 15) & ~int64_t(15); }
-__host__ __device__ constexpr int64_t lds_scalar_bytes(int64_t seg_cap)
+// ---------------------------------------------------------------- slice tiles
+// One wavefront per slice of 64 rows (Structure::perm).  LDS image of a
+// slice, per wave:
+//   acc [NACC*w_cap][64]  f64 accumulators, (slot, lane) at (slot*NACC + c)*64 + lane:
+//                         a lane's ds_add_f64 hits its own bank pair, no conflicts;
+//   cx, cy, (cz) [ucap]   coordinates of the slice's nodes (Structure::snode), SoA;
+//   li [w_cap][64]        u16 index of the row's column `slot` in that list;
+//   offs [2][64]          row offsets inside each run and row lengths (write-back).
+// The coordinates of a cell's other nodes then come from LDS (3 ds_read_b64
+// per node instead of 2 vector-memory gathers through the texture path,
+// which bound the previous, row-contiguous version at ~85-92 % TA busy).
+// UCAP > 0 fixes the coordinate array stride at compile time so that y and
+// z are immediate offsets of the x address; the odd strides (257, 513, ...)
+// keep the compiler from fusing the three reads into the half-rate
+// ds_read2(st64)_b64 forms.  UCAP = 0: runtime stride.
+__host__ __device__ constexpr int64_t tile_acc_bytes(int nacc, int64_t w_cap) { return 8 * 64 * (int64_t)nacc * w_cap; }
+__host__ __device__ constexpr int64_t tile_coord_bytes(int dimc, int64_t u_cap)
 {
-  return (lds_acc_bytes(seg_cap) + 4 * (seg_cap + 8) + 15) & ~int64_t(15);
+  return (8 * (int64_t)dimc * u_cap + 15) & ~int64_t(15);
 }
-// Incidence entry k of the row in lane `lane` of slice `sl` lives at
-// inc[slice_ptr[sl] + (k/4)*256 + lane*4 + k%4]: one 16-B load per lane per 4
-// incidences, coalesced over the wave (1 KiB per load instruction).
-// Accumulation into the row's LDS slice uses ds_add_f64: a row is owned by a
-// single lane and a wave's LDS operations execute in program order, so the
-// summation order of every entry is fixed (bitwise reproducible) while the
-// read-modify-write latency stays off the lane's dependency chain.
-// ABL != 0 only in diagnostic runs (AFEM_ASSEMBLY_ABLATION, results wrong):
-// 1 = no element arithmetic, 2 = no coordinate gathers, 3 = no LDS adds.
-template <int NV, bool USE_LDS, int ABL = 0>
-__global__ __launch_bounds__(256) void k_assemble_p1(int64_t n_rows, int64_t seg_cap,
-                                                     const int64_t* __restrict__ row_ptr,
-                                                     const int32_t* __restrict__ cols,
-                                                     const uint32_t* __restrict__ inc,
-                                                     const int64_t* __restrict__ slice_ptr,
-                                                     const int32_t* __restrict__ slice_k,
-                                                     const double* __restrict__ coords, double s_coef,
-                                                     double f_meas, double* __restrict__ vals,
-                                                     double* __restrict__ rhs)
+__host__ __device__ constexpr int64_t tile_bytes(int dimc, int nacc, int64_t u_cap, int64_t w_cap)
 {
-  // Wave-local: each wave owns one slice of 64 consecutive rows and its own
-  // LDS region (accumulators + the slice's columns).  No workgroup barrier:
-  // a wave's LDS operations execute in order, so its staging, accumulation
-  // and write-back need no synchronisation with the other waves, and the
-  // waves of a CU drift through the stage/compute/write phases independently.
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  unsigned char* wmem = smem + (size_t)wid * (size_t)lds_scalar_bytes(seg_cap);
-  double* acc = reinterpret_cast<double*>(wmem);                                // [seg_cap + 2]
-  int32_t* scol = reinterpret_cast<int32_t*>(wmem + lds_acc_bytes(seg_cap));  // [seg_cap + 8]
+  return tile_acc_bytes(nacc, w_cap) + tile_coord_bytes(dimc, u_cap) + 2 * 64 * w_cap + 4 * 128;
+}
+constexpr int kUcapBuckets[4] = { 257, 513, 1025, 2049 };
 
-  const int64_t n_slices = (n_rows + 63) >> 6;
-  const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int64_t sl = blk * (int64_t)(blockDim.x >> 6) + wid;
-  if (sl >= n_slices) return;  // whole wave: no barrier follows
-  const int64_t r0 = sl << 6;
-  const int64_t r1 = (r0 + 64 < n_rows) ? r0 + 64 : n_rows;
-  const int64_t r = r0 + lane;
-  const bool active = r < r1;
+template <int DIMC, int NACC, int UCAP>
+struct Tile {
+  double* acc;
+  double* cx;
+  uint16_t* li;
+  int32_t* offs;
+  int ucap;
 
-  // Per-lane prologue loads first, so their latency overlaps the staging.
-  const int64_t seg0 = row_ptr[r0];
-  const int64_t seg1 = row_ptr[r1];
-  const int64_t rb = active ? row_ptr[r] : seg0;
-  const int64_t re = active ? row_ptr[r + 1] : seg0;
-  const V3 xi = ld3(coords, active ? r : r0);
-  const uint4* ip = reinterpret_cast<const uint4*>(inc + slice_ptr[sl]) + lane;
-  const int ngroups = active ? (slice_k[sl] >> 2) : 0;
-  uint4 e4 = ngroups > 0 ? ip[0] : make_uint4(kPad, kPad, kPad, kPad);
+  __device__ Tile(unsigned char* smem, int u_cap, int w_cap)
+  {
+    ucap = UCAP > 0 ? UCAP : u_cap;
+    acc = reinterpret_cast<double*>(smem);
+    cx = reinterpret_cast<double*>(smem + tile_acc_bytes(NACC, w_cap));
+    li = reinterpret_cast<uint16_t*>(smem + tile_acc_bytes(NACC, w_cap) + tile_coord_bytes(DIMC, ucap));
+    offs = reinterpret_cast<int32_t*>(reinterpret_cast<unsigned char*>(li) + 2 * 64 * w_cap);
+  }
+  __device__ __forceinline__ int stride() const { return UCAP > 0 ? UCAP : ucap; }
 
-  // The slice's columns staged in LDS with 16-B loads from the 16-B aligned
-  // start (cols carries 4 ints of tail padding), all of a lane's loads issued
-  // before its LDS writes; accumulators zeroed with 16-B stores.
-  const int64_t q0 = seg0 >> 2;  // first uint4 of the segment
-  if (USE_LDS) {
-    const int64_t nq = ((seg1 + 3) >> 2) - q0;
-    const uint4* src = reinterpret_cast<const uint4*>(cols) + q0;
-    uint4* dst = reinterpret_cast<uint4*>(scol);
-    for (int64_t q = lane; q < nq; q += 256) {
-      const bool b1 = q + 64 < nq, b2 = q + 128 < nq, b3 = q + 192 < nq;
-      const uint4 v0 = src[q];
-      const uint4 v1 = b1 ? src[q + 64] : make_uint4(0, 0, 0, 0);
-      const uint4 v2 = b2 ? src[q + 128] : make_uint4(0, 0, 0, 0);
-      const uint4 v3 = b3 ? src[q + 192] : make_uint4(0, 0, 0, 0);
-      dst[q] = v0;
-      if (b1) dst[q + 64] = v1;
-      if (b2) dst[q + 128] = v2;
-      if (b3) dst[q + 192] = v3;
+  // Coordinates of the nu slice nodes, the slice's index table (16-B copies
+  // of W*128 bytes) and zeroed accumulators.  The index-table loads and the
+  // node ids are issued first, then all coordinates (four nodes per lane per
+  // round, one round for nu <= 256), then the LDS writes.  Lanes past an end
+  // redo the last element (same value to the same address), so every load
+  // and store is unconditional and none gets sunk behind an early wait.
+  __device__ void stage(int lane, int nu, const int32_t* __restrict__ nodes, const double* __restrict__ coords, int W,
+                        const uint16_t* __restrict__ lsrc)
+  {
+    const int st = stride();
+    const uint4* src = reinterpret_cast<const uint4*>(lsrc);
+    uint4* dst = reinterpret_cast<uint4*>(li);
+    const int nq = 8 * W;
+    const int q0 = min(lane, nq - 1), q1 = min(lane + 64, nq - 1);
+    const uint4 l0 = src[q0], l1 = src[q1];
+    for (int u = lane; u < nu; u += 256) {
+      int idx[4];
+      int64_t n[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        idx[k] = min(u + 64 * k, nu - 1);
+        n[k] = nodes[idx[k]];
+      }
+      double x[4], y[4], z[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        x[k] = coords[3 * n[k]];
+        y[k] = coords[3 * n[k] + 1];
+        z[k] = DIMC == 3 ? coords[3 * n[k] + 2] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        cx[idx[k]] = x[k];
+        cx[st + idx[k]] = y[k];
+        if (DIMC == 3) cx[2 * st + idx[k]] = z[k];
+      }
     }
-    const int64_t n2 = (seg1 - seg0 + 1) >> 1;
+    dst[q0] = l0;
+    dst[q1] = l1;
+    for (int q = lane + 128; q < nq; q += 64) dst[q] = src[q];
     double2* a2 = reinterpret_cast<double2*>(acc);
-    for (int64_t t = lane; t < n2; t += 64) a2[t] = make_double2(0.0, 0.0);
+    for (int q = lane; q < 32 * NACC * W; q += 64) a2[q] = make_double2(0.0, 0.0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
-  if (active) {
-    double* arow = USE_LDS ? acc + (rb - seg0) : vals + rb;
-    const int32_t* crow = USE_LDS ? scol + (rb - 4 * q0) : cols + rb;
-    if (!USE_LDS) {
-      for (int64_t t = 0; t < re - rb; ++t) arow[t] = 0.0;
-    }
-    double dacc = 0.0, macc = 0.0;
-    uint32_t dslot = 0xFFu;
-    // Branch-free groups of 4 incidences (padding entries become a zero
-    // contribution to slot 0), so every LDS read and coordinate gather of
-    // the group is issued before the first element row is computed; the
-    // next group's incidence word is prefetched one group ahead.
-    for (int g = 0; g < ngroups; ++g) {
-      const uint4 cur = e4;
-      if (cur.x == kPad) break;
-      if (g + 1 < ngroups) e4 = ip[(int64_t)(g + 1) * 64];
-      const uint32_t ev[4] = { cur.x, cur.y, cur.z, cur.w };
-      V3 xa[4], xb[4], xc[4];
-      uint32_t sa[4], sb[4], sc[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t e = ev[j] == kPad ? 0u : ev[j];
-        sa[j] = e & 0xFFu;
-        sb[j] = (e >> 8) & 0xFFu;
-        sc[j] = (NV == 4) ? (e >> 16) & 0xFFu : 0u;
-        if (ABL == 2) {
-          const double da = 1e-3 * (double)crow[sa[j]], db = 2e-3 * (double)crow[sb[j]],
-                       dc = 3e-3 * (double)crow[sc[j]];
-          xa[j] = V3{ xi.x + da, xi.y, xi.z };
-          xb[j] = V3{ xi.x, xi.y + db, xi.z };
-          xc[j] = V3{ xi.x, xi.y, xi.z + dc };
-        }
-        else {
-          xa[j] = ld3(coords, crow[sa[j]]);
-          xb[j] = ld3(coords, crow[sb[j]]);
-          if (NV == 4) xc[j] = ld3(coords, crow[sc[j]]);
-        }
-      }
-      dslot = (cur.x >> 24);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bool valid = ev[j] != kPad;
-        double k0, k1, k2, k3 = 0.0, meas;
-        if (ABL == 1) {
-          k0 = xa[j].x;
-          k1 = xa[j].y + xb[j].x;
-          k2 = xb[j].y + xc[j].x;
-          k3 = xc[j].y + xc[j].z;
-          meas = xa[j].z + xb[j].z;
-        }
-        else if (NV == 4)
-          meas = tet_row(xi, xa[j], xb[j], xc[j], s_coef, k0, k1, k2, k3);
-        else
-          meas = tri_row(xi, xa[j], xb[j], s_coef, k0, k1, k2);
-        if (!valid) k0 = k1 = k2 = k3 = meas = 0.0;
-        dacc += k0;
-        macc += meas;
-        if (ABL == 3) {
-          dacc += k1 + k2 + k3;
-        }
-        else if (USE_LDS) {
-          atomicAdd(arow + sa[j], k1);
-          atomicAdd(arow + sb[j], k2);
-          if (NV == 4) atomicAdd(arow + sc[j], k3);
-        }
-        else {
-          arow[sa[j]] += k1;
-          arow[sb[j]] += k2;
-          if (NV == 4) arow[sc[j]] += k3;
-        }
-      }
-    }
-    if (dslot != 0xFFu) arow[dslot] = dacc;
-    if (rhs) rhs[r] = f_meas * macc;
+
+  __device__ __forceinline__ V3 node(int lane, uint32_t slot) const
+  {
+    const int u = li[slot * 64 + lane];
+    const double* p = cx + u;
+    return V3{ p[0], p[stride()], DIMC == 3 ? p[2 * stride()] : 0.0 };
   }
-  if (USE_LDS) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    for (int64_t t = lane; t < seg1 - seg0; t += 64) vals[seg0 + t] = acc[t];
+  __device__ __forceinline__ double* at(int lane, uint32_t slot, int c) const { return acc + (slot * NACC + c) * 64 + lane; }
+};
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Coalesced write-back of a slice.  Lanes [j, j+run) hold consecutive rows
+// (idle lanes only at the end of a run), so the run's value segments form
+// one contiguous range [base_j, base_j + L_j): the wave writes it with
+// consecutive lanes on consecutive addresses, each position's value taken
+// from its row's accumulator column (owner found by a binary search over
+// the run's row offsets).  NACC values per (row, slot): per block
+// (slot*NACC + c) or, NACC = 4, per scalar row (i*2*len + 2*slot + j).
+template <int NACC, class TILE>
+__device__ __forceinline__ void write_back(const TILE& tile, int lane, int run, bool active, int64_t rb, int len,
+                                           bool per_block, double* __restrict__ vals)
+{
+  const int j0 = lane & ~(run - 1);
+  const int64_t base = __shfl(rb, j0);
+  const int off = active ? (int)(rb - base) : 0x7fffffff;
+  int end = active ? off + len : 0;
+  for (int o = 1; o < run; o <<= 1) end = max(end, __shfl_xor(end, o));
+  tile.offs[lane] = off;
+  tile.offs[64 + lane] = len;
+  wave_sync_lds();
+  for (int j = 0; j < 64; j += run) {
+    const int64_t bj = __shfl(base, j);
+    const int lj = __shfl(end, j);
+    for (int p = lane; p < NACC * lj; p += 64) {
+      const int pr = p / NACC;  // scalar position of the block
+      int q = 0;
+      for (int step = run >> 1; step > 0; step >>= 1)
+        if (tile.offs[j + q + step] <= pr) q += step;
+      const int o = tile.offs[j + q];
+      int slot, c;
+      if (NACC == 1 || per_block) {
+        slot = pr - o;
+        c = p - NACC * pr;
+      }
+      else {  // per scalar row: the row's 4*len values are [i][slot][jj]
+        const int w = p - NACC * o, rl2 = 2 * tile.offs[64 + j + q];
+        const int i = w >= rl2 ? 1 : 0;
+        const int rem = w - i * rl2;
+        slot = rem >> 1;
+        c = 2 * i + (rem & 1);
+      }
+      vals[NACC * bj + p] = *tile.at(j + q, slot, c);
+    }
   }
+}
+
+// ---------------------------------------------------------------- scalar P1
+// Incidence entry k of lane `lane` of slice `sl` lives at
+// inc[slice_ptr[sl] + (k/4)*256 + lane*4 + k%4]: one 16-B load per lane per 4
+// incidences, coalesced over the wave (1 KiB per load instruction).  A row
+// is owned by a single lane and a wave's LDS operations execute in program
+// order, so the summation order of every entry is fixed by the structure:
+// the assembled matrix is bitwise reproducible run to run.
+// The group loop is uniform over the wave (padding entries are computed as
+// degenerate cells whose scale is masked to 0) and the incidence words are
+// prefetched two groups ahead by unconditional loads (a conditional load
+// made the compiler wait for it right away).  The diagonal is not
+// accumulated: rows of the P1 Laplacian sum to zero (sum of the shape
+// function gradients), so K_ii = -sum_{j != i} K_ij, formed at write-back.
+// ABL != 0 only in diagnostic runs (AFEM_ASSEMBLY_ABLATION, results wrong):
+// 1 = no element arithmetic, 2 = no LDS coordinate reads, 3 = no LDS adds,
+// 4 = no staging (coordinates / indices / zeroing), 5 = no write-back.
+template <int NV, int UCAP, int ABL = 0>
+__global__ __launch_bounds__(64) void k_assemble_p1(int u_cap, int w_cap, int run, const int32_t* __restrict__ perm,
+                                                    const int64_t* __restrict__ row_ptr,
+                                                    const uint32_t* __restrict__ inc,
+                                                    const int64_t* __restrict__ slice_ptr,
+                                                    const int32_t* __restrict__ slice_k,
+                                                    const int32_t* __restrict__ slice_w,
+                                                    const int64_t* __restrict__ lidx_ptr,
+                                                    const uint16_t* __restrict__ lidx,
+                                                    const int64_t* __restrict__ snode_ptr,
+                                                    const int32_t* __restrict__ snode,
+                                                    const double* __restrict__ coords, double s_coef,
+                                                    double f_meas, double* __restrict__ vals,
+                                                    double* __restrict__ rhs)
+{
+  constexpr int DIMC = NV == 4 ? 3 : 2;
+  extern __shared__ __align__(16) unsigned char smem[];
+  Tile<DIMC, 1, UCAP> tile(smem, u_cap, w_cap);
+  const int lane = threadIdx.x;
+  const int64_t sl = xcd_swizzle(blockIdx.x, gridDim.x);
+
+  // per-lane prologue loads first, so their latency overlaps the staging
+  const int32_t row = perm[sl * 64 + lane];
+  const bool active = row >= 0;
+  const int64_t rb = active ? row_ptr[row] : 0;
+  const int len = active ? (int)(row_ptr[row + 1] - rb) : 0;
+  const V3 xi = ld3(coords, active ? row : 0);
+  const uint4* ip = reinterpret_cast<const uint4*>(inc + slice_ptr[sl]) + lane;
+  const int ngroups = slice_k[sl] >> 2;  // uniform over the wave
+  const int glast = ngroups > 0 ? ngroups - 1 : 0;
+  uint4 eA = ip[0];
+  uint4 eB = ip[(int64_t)(1 < glast ? 1 : glast) * 64];
+  if (ABL != 4) {
+    const int64_t u0 = snode_ptr[sl];
+    tile.stage(lane, (int)(snode_ptr[sl + 1] - u0), snode + u0, coords, slice_w[sl], lidx + lidx_ptr[sl]);
+  }
+  double macc = 0.0;
+  const uint32_t dslot = eA.x == kPad ? 0xFFu : (eA.x >> 24);
+
+  auto group = [&](const uint4 cur) {
+    const uint32_t ev[4] = { cur.x, cur.y, cur.z, cur.w };
+    V3 xa[4], xb[4], xc[4];
+    uint32_t sa[4], sb[4], sc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t e = ev[j] == kPad ? 0u : ev[j];
+      sa[j] = e & 0xFFu;
+      sb[j] = (e >> 8) & 0xFFu;
+      sc[j] = (NV == 4) ? (e >> 16) & 0xFFu : 0u;
+      if (ABL == 2) {
+        xa[j] = V3{ xi.x + 1e-3 * sa[j], xi.y, xi.z };
+        xb[j] = V3{ xi.x, xi.y + 1e-3 * sb[j], xi.z };
+        xc[j] = V3{ xi.x, xi.y, xi.z + 1e-3 * sc[j] };
+      }
+      else {
+        xa[j] = tile.node(lane, sa[j]);
+        xb[j] = tile.node(lane, sb[j]);
+        if (NV == 4) xc[j] = tile.node(lane, sc[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool pad = ev[j] == kPad;  // padding: degenerate cell (det 0), scale forced to 0
+      double k1, k2, k3 = 0.0, meas;
+      if (ABL == 1) {
+        k1 = xa[j].y + xb[j].x;
+        k2 = xb[j].y + xc[j].x;
+        k3 = xc[j].y + xc[j].z;
+        meas = xa[j].z + xb[j].z;
+      }
+      else if (NV == 4) {
+        const V3 e1 = sub(xa[j], xi), e2 = sub(xb[j], xi), e3 = sub(xc[j], xi);
+        const V3 c1 = cross(e2, e3), c2 = cross(e3, e1), c3 = cross(e1, e2);
+        const V3 c0 = V3{ -(c1.x + c2.x + c3.x), -(c1.y + c2.y + c3.y), -(c1.z + c2.z + c3.z) };
+        meas = fabs(dot(e1, c1));
+        const double s = pad ? 0.0 : s_coef * recip(meas);
+        k1 = dot(c0, c1) * s;
+        k2 = dot(c0, c2) * s;
+        k3 = dot(c0, c3) * s;
+      }
+      else {
+        const double e1x = xa[j].x - xi.x, e1y = xa[j].y - xi.y, e2x = xb[j].x - xi.x, e2y = xb[j].y - xi.y;
+        const double c1x = e2y, c1y = -e2x, c2x = -e1y, c2y = e1x;
+        const double c0x = -(c1x + c2x), c0y = -(c1y + c2y);
+        meas = fabs(e1x * e2y - e2x * e1y);
+        const double s = pad ? 0.0 : s_coef * recip(meas);
+        k1 = (c0x * c1x + c0y * c1y) * s;
+        k2 = (c0x * c2x + c0y * c2y) * s;
+      }
+      macc += meas;
+      if (ABL != 3) {
+        atomicAdd(tile.at(lane, sa[j], 0), k1);
+        atomicAdd(tile.at(lane, sb[j], 0), k2);
+        if (NV == 4) atomicAdd(tile.at(lane, sc[j], 0), k3);
+      }
+      else {
+        macc += k1 + k2 + k3;
+      }
+    }
+  };
+  // two-deep ring of incidence words, unrolled by 2 so that no register copy
+  // forces an early wait on a load
+  for (int g = 0; g < ngroups; g += 2) {
+    const uint4 a = eA;
+    eA = ip[(int64_t)(g + 2 < glast ? g + 2 : glast) * 64];
+    group(a);
+    if (g + 1 < ngroups) {
+      const uint4 b = eB;
+      eB = ip[(int64_t)(g + 3 < glast ? g + 3 : glast) * 64];
+      group(b);
+    }
+  }
+  if (rhs && active) rhs[row] = f_meas * macc;
+  wave_sync_lds();
+  if (active && dslot != 0xFFu) {
+    double sum = 0.0;
+    for (int t = 0; t < len; ++t)
+      if (t != (int)dslot) sum += *tile.at(lane, t, 0);
+    *tile.at(lane, dslot, 0) = -sum;
+  }
+  if (ABL != 5) write_back<1>(tile, lane, run, active, rb, len, true, vals);
+}
+
+// Global-memory variant for rows too long for the LDS tile: coordinates
+// gathered through the columns, accumulation in place (lane-owned rows).
+template <int NV>
+__global__ __launch_bounds__(64) void k_assemble_p1_global(const int32_t* __restrict__ perm,
+                                                           const int64_t* __restrict__ row_ptr,
+                                                           const int32_t* __restrict__ cols,
+                                                           const uint32_t* __restrict__ inc,
+                                                           const int64_t* __restrict__ slice_ptr,
+                                                           const int32_t* __restrict__ slice_k,
+                                                           const double* __restrict__ coords, double s_coef,
+                                                           double f_meas, double* __restrict__ vals,
+                                                           double* __restrict__ rhs)
+{
+  const int lane = threadIdx.x;
+  const int64_t sl = blockIdx.x;
+  const int32_t row = perm[sl * 64 + lane];
+  if (row < 0) return;
+  const int64_t rb = row_ptr[row];
+  const int len = (int)(row_ptr[row + 1] - rb);
+  const int32_t* crow = cols + rb;
+  double* arow = vals + rb;
+  for (int t = 0; t < len; ++t) arow[t] = 0.0;
+  const V3 xi = ld3(coords, row);
+  const uint32_t* ip = inc + slice_ptr[sl] + lane * 4;
+  const int kmax = slice_k[sl];
+  double dacc = 0.0, macc = 0.0;
+  uint32_t dslot = 0xFFu;
+  for (int k = 0; k < kmax; ++k) {
+    const uint32_t e = ip[(int64_t)(k >> 2) * 256 + (k & 3)];
+    if (e == kPad) break;
+    dslot = e >> 24;
+    const V3 xa = ld3(coords, crow[e & 0xFFu]), xb = ld3(coords, crow[(e >> 8) & 0xFFu]);
+    double k0, k1, k2, k3 = 0.0, meas;
+    if (NV == 4)
+      meas = tet_row(xi, xa, xb, ld3(coords, crow[(e >> 16) & 0xFFu]), s_coef, k0, k1, k2, k3);
+    else
+      meas = tri_row(xi, xa, xb, s_coef, k0, k1, k2);
+    dacc += k0;
+    macc += meas;
+    arow[e & 0xFFu] += k1;
+    arow[(e >> 8) & 0xFFu] += k2;
+    if (NV == 4) arow[(e >> 16) & 0xFFu] += k3;
+  }
+  if (dslot != 0xFFu) arow[dslot] = dacc;
+  if (rhs) rhs[row] = f_meas * macc;
 }
 
 // ---------------------------------------------------------------- block-2 elasticity (TRIA3)
@@ -283,43 +455,55 @@ __device__ __forceinline__ int64_t bidx2(bool per_block, int64_t rb4, int64_t nn
   return per_block ? rb4 + (int64_t)slot * 4 + i * 2 + j : rb4 + (int64_t)i * 2 * nnz_row + 2 * slot + j;
 }
 
-template <bool USE_LDS>
-__global__ __launch_bounds__(256) void k_assemble_elast_tri(int64_t n_rows, int64_t seg_cap, bool per_block,
-                                                            const int64_t* __restrict__ row_ptr,
-                                                            const int32_t* __restrict__ cols,
-                                                            const uint32_t* __restrict__ inc,
-                                                            const int64_t* __restrict__ slice_ptr,
-                                                            const int32_t* __restrict__ slice_k,
-                                                            const double* __restrict__ coords, double lambda,
-                                                            double mu2, double* __restrict__ vals)
+template <bool LDS>
+__global__ __launch_bounds__(64) void k_assemble_elast_tri(int u_cap, int w_cap, int run, bool per_block,
+                                                           const int32_t* __restrict__ perm,
+                                                           const int64_t* __restrict__ row_ptr,
+                                                           const int32_t* __restrict__ cols,
+                                                           const uint32_t* __restrict__ inc,
+                                                           const int64_t* __restrict__ slice_ptr,
+                                                           const int32_t* __restrict__ slice_k,
+                                                           const int32_t* __restrict__ slice_w,
+                                                           const int64_t* __restrict__ lidx_ptr,
+                                                           const uint16_t* __restrict__ lidx,
+                                                           const int64_t* __restrict__ snode_ptr,
+                                                           const int32_t* __restrict__ snode,
+                                                           const double* __restrict__ coords, double lambda,
+                                                           double mu2, double* __restrict__ vals)
 {
   extern __shared__ __align__(16) unsigned char smem[];
-  double* acc = reinterpret_cast<double*>(smem);
-  int32_t* scol = reinterpret_cast<int32_t*>(smem + 8 * 4 * seg_cap);
-  const int rpb = blockDim.x;
-  const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int64_t r0 = blk * rpb;
-  const int64_t r1 = (r0 + rpb < n_rows) ? r0 + rpb : n_rows;
-  const int64_t seg0 = row_ptr[r0];
-  const int64_t r = r0 + threadIdx.x;
-  double* out = USE_LDS ? acc : vals;
-  const int64_t base0 = USE_LDS ? seg0 * 4 : 0;
-  if (USE_LDS) {
-    const int64_t seglen = row_ptr[r1] - seg0;
-    for (int64_t t = threadIdx.x; t < seglen; t += rpb) scol[t] = cols[seg0 + t];
-    for (int64_t t = threadIdx.x; t < 4 * seglen; t += rpb) acc[t] = 0.0;
-    __syncthreads();
+  Tile<2, 4, 0> tile(smem, u_cap, w_cap);
+  const int lane = threadIdx.x;
+  const int64_t sl = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int32_t row = perm[sl * 64 + lane];
+  const bool active = row >= 0;
+  const int64_t rb = active ? row_ptr[row] : 0;
+  const int len = active ? (int)(row_ptr[row + 1] - rb) : 0;
+  const V3 x0 = ld3(coords, active ? row : 0);
+  const uint32_t* ip = inc + slice_ptr[sl] + lane * 4;
+  const int kmax = active ? slice_k[sl] : 0;
+  if (LDS) {
+    const int64_t u0 = snode_ptr[sl];
+    tile.stage(lane, (int)(snode_ptr[sl + 1] - u0), snode + u0, coords, slice_w[sl], lidx + lidx_ptr[sl]);
   }
-  if (r < r1) {
-    const int64_t rb = row_ptr[r];
-    const int64_t nnz_row = row_ptr[r + 1] - rb;
-    const int64_t rb4 = rb * 4 - base0;
-    if (!USE_LDS)
-      for (int64_t t = 0; t < 4 * nnz_row; ++t) vals[rb * 4 + t] = 0.0;
-    const V3 x0 = ld3(coords, r);
-    const int64_t sl = r >> 6;
-    const uint32_t* ip = inc + slice_ptr[sl] + (r & 63) * 4;
-    const int kmax = slice_k[sl];
+  else {
+    for (int t = 0; t < 4 * len; ++t) vals[4 * rb + t] = 0.0;
+  }
+  const int32_t* crow = cols + rb;
+  // accumulator of (slot, i, j): LDS tile, or the value array itself
+  auto add = [&](int slot, int i, int j, double v) {
+    if (LDS)
+      atomicAdd(tile.at(lane, slot, 2 * i + j), v);
+    else
+      vals[bidx2(per_block, 4 * rb, len, slot, i, j)] += v;
+  };
+  auto put = [&](int slot, int i, int j, double v) {
+    if (LDS)
+      *tile.at(lane, slot, 2 * i + j) = v;
+    else
+      vals[bidx2(per_block, 4 * rb, len, slot, i, j)] = v;
+  };
+  if (active) {
     double d00 = 0, d01 = 0, d10 = 0, d11 = 0;
     uint32_t dslot = 0xFFu;
     for (int k = 0; k < kmax; ++k) {
@@ -327,16 +511,13 @@ __global__ __launch_bounds__(256) void k_assemble_elast_tri(int64_t n_rows, int6
       if (e == kPad) break;
       const int s[2] = { (int)(e & 0xFFu), (int)((e >> 8) & 0xFFu) };
       dslot = e >> 24;
-      const int64_t cb = USE_LDS ? (rb - seg0) : rb;
-      const int32_t* cc = USE_LDS ? scol : cols;
-      const V3 x1 = ld3(coords, cc[cb + s[0]]), x2 = ld3(coords, cc[cb + s[1]]);
+      const V3 x1 = LDS ? tile.node(lane, s[0]) : ld3(coords, crow[s[0]]);
+      const V3 x2 = LDS ? tile.node(lane, s[1]) : ld3(coords, crow[s[1]]);
       // 2A * grad N: dPhi0 = (y1-y2, x2-x1), dPhi1 = (y2-y0, x0-x2), dPhi2 = (y0-y1, x1-x0)
-      const double p0x = x1.y - x2.y, p0y = x2.x - x1.x;
-      const double px[3] = { p0x, x2.y - x0.y, x0.y - x1.y };
-      const double py[3] = { p0y, x0.x - x2.x, x1.x - x0.x };
-      V3 a = sub(x1, x0), b = sub(x2, x0);
-      V3 cr = cross(a, b);
-      const double area = sqrt(dot(cr, cr)) / 2.0;
+      const double px[3] = { x1.y - x2.y, x2.y - x0.y, x0.y - x1.y };
+      const double py[3] = { x2.x - x1.x, x0.x - x2.x, x1.x - x0.x };
+      const double e1x = x1.x - x0.x, e1y = x1.y - x0.y, e2x = x2.x - x0.x, e2y = x2.y - x0.y;
+      const double area = fabs(e1x * e2y - e2x * e1y) / 2.0;
       const double sc = 1.0 / (4.0 * area);
       // row dof i of node 0, column dof j of node b:
       //  lam(i,j)  = (bx_i + by_i)(bx_j + by_j) over the interleaved B rows
@@ -344,25 +525,10 @@ __global__ __launch_bounds__(256) void k_assemble_elast_tri(int64_t n_rows, int6
       // with for dof (node a, comp 0): bx = px[a], by = 0, bs = py[a]
       //      for dof (node a, comp 1): bx = 0, by = py[a], bs = px[a]
       for (int nb = 0; nb < 3; ++nb) {
-        double K00, K01, K10, K11;
-        {
-          // i=0 (u1 of node 0), j=0 (u1 of node nb)
-          double lam = px[0] * px[nb];
-          double shr = px[0] * px[nb] + 0.5 * py[0] * py[nb];
-          K00 = (lambda * lam) * sc + (mu2 * shr) * sc;
-          // i=0, j=1 (u2 of node nb)
-          lam = px[0] * py[nb];
-          shr = 0.5 * py[0] * px[nb];
-          K01 = (lambda * lam) * sc + (mu2 * shr) * sc;
-          // i=1, j=0
-          lam = py[0] * px[nb];
-          shr = 0.5 * px[0] * py[nb];
-          K10 = (lambda * lam) * sc + (mu2 * shr) * sc;
-          // i=1, j=1
-          lam = py[0] * py[nb];
-          shr = py[0] * py[nb] + 0.5 * px[0] * px[nb];
-          K11 = (lambda * lam) * sc + (mu2 * shr) * sc;
-        }
+        const double K00 = (lambda * (px[0] * px[nb])) * sc + (mu2 * (px[0] * px[nb] + 0.5 * py[0] * py[nb])) * sc;
+        const double K01 = (lambda * (px[0] * py[nb])) * sc + (mu2 * (0.5 * py[0] * px[nb])) * sc;
+        const double K10 = (lambda * (py[0] * px[nb])) * sc + (mu2 * (0.5 * px[0] * py[nb])) * sc;
+        const double K11 = (lambda * (py[0] * py[nb])) * sc + (mu2 * (py[0] * py[nb] + 0.5 * px[0] * px[nb])) * sc;
         if (nb == 0) {
           d00 += K00;
           d01 += K01;
@@ -371,25 +537,21 @@ __global__ __launch_bounds__(256) void k_assemble_elast_tri(int64_t n_rows, int6
         }
         else {
           const int sl2 = s[nb - 1];
-          out[bidx2(per_block, rb4, nnz_row, sl2, 0, 0)] += K00;
-          out[bidx2(per_block, rb4, nnz_row, sl2, 0, 1)] += K01;
-          out[bidx2(per_block, rb4, nnz_row, sl2, 1, 0)] += K10;
-          out[bidx2(per_block, rb4, nnz_row, sl2, 1, 1)] += K11;
+          add(sl2, 0, 0, K00);
+          add(sl2, 0, 1, K01);
+          add(sl2, 1, 0, K10);
+          add(sl2, 1, 1, K11);
         }
       }
     }
     if (dslot != 0xFFu) {
-      out[bidx2(per_block, rb4, nnz_row, (int)dslot, 0, 0)] = d00;
-      out[bidx2(per_block, rb4, nnz_row, (int)dslot, 0, 1)] = d01;
-      out[bidx2(per_block, rb4, nnz_row, (int)dslot, 1, 0)] = d10;
-      out[bidx2(per_block, rb4, nnz_row, (int)dslot, 1, 1)] = d11;
+      put((int)dslot, 0, 0, d00);
+      put((int)dslot, 0, 1, d01);
+      put((int)dslot, 1, 0, d10);
+      put((int)dslot, 1, 1, d11);
     }
   }
-  if (USE_LDS) {
-    __syncthreads();
-    const int64_t seglen = row_ptr[r1] - seg0;
-    for (int64_t t = threadIdx.x; t < 4 * seglen; t += rpb) vals[seg0 * 4 + t] = acc[t];
-  }
+  if (LDS) write_back<4>(tile, lane, run, active, rb, len, per_block, vals);
 }
 
 // ---------------------------------------------------------------- point access / CSR expansion
@@ -497,44 +659,88 @@ void bsr_expand_scalar(Bsr& b, double* vals_out)
   AFEM_LAUNCHED();
 }
 
+namespace {
+// LDS tile budget per wave (one wave per workgroup): beyond it the global
+// accumulation variants run (rows of > ~90 non-zeros, not P1 meshes).
+constexpr int64_t kTileLdsMax = 64 * 1024;
+}  // namespace
+
 void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
 {
   Structure& s = b.s;
   Ctx& ctx = *b.mesh->ctx;
   const int nv = b.mesh->nv;
   AFEM_REQUIRE(b.nb_dof == 1, AFEM_ERR_ARG, "assembleBilinear(P1 Laplacian) needs NB_DOF = 1");
-  // wave-local kernel: 4 waves per workgroup, one LDS region per wave
-  const int64_t wave_lds = lds_scalar_bytes(s.max_wave_seg);
-  const bool lds = 4 * wave_lds <= 64 * 1024;
-  const int rpb = 256;
-  const unsigned nblk = lds ? (unsigned)((s.n_slices + 3) / 4) : (unsigned)((s.n_rows + rpb - 1) / rpb);
-  const size_t shm = lds ? (size_t)(4 * wave_lds) : 0;
+  const int dimc = nv == 4 ? 3 : 2;
+  int bucket = -1;
+  for (int i = 0; i < 4 && bucket < 0; ++i)
+    if (s.max_slice_nodes <= kUcapBuckets[i] && tile_bytes(dimc, 1, kUcapBuckets[i], s.max_slice_w) <= kTileLdsMax)
+      bucket = i;
   // K = coef * c0.cb / (6|det|) (tets) or / (2|A2|) (triangles);
   // RHS = f * |K| / nv = f*|det|/24 (tets) or f*|A2|/6 (triangles)
   const double s_coef = (nv == 4) ? coef / 6.0 : coef / 2.0;
   const double f_meas = (nv == 4) ? f / 24.0 : f / 6.0;
+  const dim3 grid((unsigned)s.n_slices), blk(64);
+  if (bucket < 0) {
+    if (nv == 4)
+      hipLaunchKernelGGL(k_assemble_p1_global<4>, grid, blk, 0, ctx.stream, s.perm.p, s.row_ptr.p, s.cols.p, s.inc.p,
+                         s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
+    else
+      hipLaunchKernelGGL(k_assemble_p1_global<3>, grid, blk, 0, ctx.stream, s.perm.p, s.row_ptr.p, s.cols.p, s.inc.p,
+                         s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
+    AFEM_LAUNCHED();
+    return;
+  }
+  const size_t shm = (size_t)tile_bytes(dimc, 1, kUcapBuckets[bucket], s.max_slice_w);
   static const int abl = [] {
     const char* e = getenv("AFEM_ASSEMBLY_ABLATION");
     return e ? atoi(e) : 0;
   }();
-#define AFEM_ASM_ARGS s.n_rows, s.max_wave_seg, s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p, \
+#define AFEM_ASM_ARGS s.max_slice_nodes, s.max_slice_w, s.run, s.perm.p, s.row_ptr.p, s.inc.p, s.inc_slice_ptr.p, \
+                      s.inc_slice_k.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p, s.snode.p,            \
                       b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs
-  if (nv == 4 && lds) {
+#define AFEM_ASM_LAUNCH(NV_, U_, A_) \
+  hipLaunchKernelGGL((k_assemble_p1<NV_, U_, A_>), grid, blk, shm, ctx.stream, AFEM_ASM_ARGS)
+  if (nv == 4 && bucket == 0 && abl != 0) {
     switch (abl) {
-      case 1: hipLaunchKernelGGL((k_assemble_p1<4, true, 1>), dim3(nblk), dim3(rpb), shm, ctx.stream, AFEM_ASM_ARGS); break;
-      case 2: hipLaunchKernelGGL((k_assemble_p1<4, true, 2>), dim3(nblk), dim3(rpb), shm, ctx.stream, AFEM_ASM_ARGS); break;
-      case 3: hipLaunchKernelGGL((k_assemble_p1<4, true, 3>), dim3(nblk), dim3(rpb), shm, ctx.stream, AFEM_ASM_ARGS); break;
-      default: hipLaunchKernelGGL((k_assemble_p1<4, true>), dim3(nblk), dim3(rpb), shm, ctx.stream, AFEM_ASM_ARGS);
+      case 1: AFEM_ASM_LAUNCH(4, 257, 1); break;
+      case 2: AFEM_ASM_LAUNCH(4, 257, 2); break;
+      case 3: AFEM_ASM_LAUNCH(4, 257, 3); break;
+      case 4: AFEM_ASM_LAUNCH(4, 257, 4); break;
+      default: AFEM_ASM_LAUNCH(4, 257, 5);
     }
   }
-  else if (nv == 4)
-    hipLaunchKernelGGL((k_assemble_p1<4, false>), dim3(nblk), dim3(rpb), 0, ctx.stream, AFEM_ASM_ARGS);
-  else if (lds)
-    hipLaunchKernelGGL((k_assemble_p1<3, true>), dim3(nblk), dim3(rpb), shm, ctx.stream, AFEM_ASM_ARGS);
-  else
-    hipLaunchKernelGGL((k_assemble_p1<3, false>), dim3(nblk), dim3(rpb), 0, ctx.stream, AFEM_ASM_ARGS);
+  else if (nv == 4) {
+    switch (bucket) {
+      case 0: AFEM_ASM_LAUNCH(4, 257, 0); break;
+      case 1: AFEM_ASM_LAUNCH(4, 513, 0); break;
+      case 2: AFEM_ASM_LAUNCH(4, 1025, 0); break;
+      default: AFEM_ASM_LAUNCH(4, 2049, 0);
+    }
+  }
+  else {
+    switch (bucket) {
+      case 0: AFEM_ASM_LAUNCH(3, 257, 0); break;
+      case 1: AFEM_ASM_LAUNCH(3, 513, 0); break;
+      case 2: AFEM_ASM_LAUNCH(3, 1025, 0); break;
+      default: AFEM_ASM_LAUNCH(3, 2049, 0);
+    }
+  }
+#undef AFEM_ASM_LAUNCH
 #undef AFEM_ASM_ARGS
   AFEM_LAUNCHED();
+}
+
+bool assembly_uses_lds(const Bsr& b)
+{
+  const int nacc = b.nb_dof * b.nb_dof;
+  const int dimc = b.mesh->nv == 4 ? 3 : 2;
+  if (nacc == 1) {
+    for (int u : kUcapBuckets)
+      if (b.s.max_slice_nodes <= u && tile_bytes(dimc, 1, u, b.s.max_slice_w) <= kTileLdsMax) return true;
+    return false;
+  }
+  return tile_bytes(dimc, nacc, b.s.max_slice_nodes, b.s.max_slice_w) <= kTileLdsMax;
 }
 
 void assemble_elasticity_tri(Bsr& b, double lambda, double mu2)
@@ -543,18 +749,17 @@ void assemble_elasticity_tri(Bsr& b, double lambda, double mu2)
   Ctx& ctx = *b.mesh->ctx;
   AFEM_REQUIRE(b.nb_dof == 2 && b.mesh->nv == 3, AFEM_ERR_NOT_IMPL,
                "P1 elasticity assembly is implemented for NB_DOF = 2 on triangles (the reference's elasticity module)");
-  const bool lds = s.rows_per_block > 0 && s.max_seg * 36 <= 64 * 1024;
-  const int rpb = lds ? s.rows_per_block : 256;
-  const unsigned nblk = (unsigned)((s.n_rows + rpb - 1) / rpb);
-  const size_t shm = lds ? (size_t)s.max_seg * 36 : 0;
+  const int64_t shm = tile_bytes(2, 4, s.max_slice_nodes, s.max_slice_w);
+  const bool lds = shm <= kTileLdsMax;
+  const dim3 grid((unsigned)s.n_slices), blk(64);
+#define AFEM_EL_ARGS s.max_slice_nodes, s.max_slice_w, s.run, b.order_per_block, s.perm.p, s.row_ptr.p, s.cols.p, s.inc.p, \
+                     s.inc_slice_ptr.p, s.inc_slice_k.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p,         \
+                     s.snode.p, b.mesh->coords.p, lambda, mu2, b.values.p
   if (lds)
-    hipLaunchKernelGGL(k_assemble_elast_tri<true>, dim3(nblk), dim3(rpb), shm, ctx.stream, s.n_rows, s.max_seg,
-                       b.order_per_block, s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p,
-                       b.mesh->coords.p, lambda, mu2, b.values.p);
+    hipLaunchKernelGGL(k_assemble_elast_tri<true>, grid, blk, (size_t)shm, ctx.stream, AFEM_EL_ARGS);
   else
-    hipLaunchKernelGGL(k_assemble_elast_tri<false>, dim3(nblk), dim3(rpb), 0, ctx.stream, s.n_rows, s.max_seg,
-                       b.order_per_block, s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p,
-                       b.mesh->coords.p, lambda, mu2, b.values.p);
+    hipLaunchKernelGGL(k_assemble_elast_tri<false>, grid, blk, 0, ctx.stream, AFEM_EL_ARGS);
+#undef AFEM_EL_ARGS
   AFEM_LAUNCHED();
 }
 

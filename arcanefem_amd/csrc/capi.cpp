@@ -446,8 +446,12 @@ int afem_bsr_get_stats(afem_bsr* b, afem_bsr_stats* st)
   st->n_incidences = b->s.n_incidences;
   st->inc_table_entries = (int64_t)b->s.inc.n;
   st->max_row_len = b->s.max_row_len;
-  st->rows_per_block = b->s.rows_per_block;
-  st->max_seg = b->s.max_seg;
+  st->rows_per_block = afem::assembly_uses_lds(*b) ? 64 : 0;
+  st->max_seg = b->s.max_wave_seg;
+  st->max_slice_nodes = b->s.max_slice_nodes;
+  st->max_slice_width = b->s.max_slice_w;
+  st->n_slices = b->s.n_slices;
+  st->brick_order = b->s.brick_order ? 1 : 0;
   API_END
 }
 

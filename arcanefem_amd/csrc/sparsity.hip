@@ -132,16 +132,43 @@ __global__ void k_check_len(int64_t n_rows, const int32_t* __restrict__ row_len,
   else atomicMax(&flags[1], l);
 }
 
-// Per slice of 64 rows: the max incidence count (ELL width) and its size.
-__global__ void k_slice_width(int64_t n_rows, int64_t n_slices, const int64_t* __restrict__ nc_ptr,
+// Processing order of a structured box of nodes (the owned nodes of a
+// generated mesh are numbered lexicographically, i fastest, in an
+// ax x ay x az box): bricks of 4x4x4 nodes (8x8 in 2D) in lexicographic
+// brick order, one brick per slice, lane = position in the brick.
+__global__ void k_perm_bricks(int64_t n_slices, int dim, int64_t ax, int64_t ay, int64_t az, int32_t* __restrict__ perm)
+{
+  int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_slices * 64) return;
+  const int64_t s = p >> 6;
+  const int lane = (int)(p & 63);
+  const int bx = dim == 3 ? 4 : 8, by = bx, bz = dim == 3 ? 4 : 1;
+  const int64_t nbx = (ax + bx - 1) / bx, nby = (ay + by - 1) / by;
+  const int64_t ib = s % nbx, jb = (s / nbx) % nby, kb = s / (nbx * nby);
+  const int64_t i = ib * bx + lane % bx;
+  const int64_t j = jb * by + (lane / bx) % by;
+  const int64_t k = kb * bz + lane / (bx * by);
+  perm[p] = (i < ax && j < ay && k < az) ? (int32_t)(i + ax * (j + ay * k)) : -1;
+}
+
+__global__ void k_perm_identity(int64_t n_pos, int64_t n_rows, int32_t* __restrict__ perm)
+{
+  int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_pos) perm[p] = p < n_rows ? (int32_t)p : -1;
+}
+
+// Per slice: the max incidence count (ELL width, rounded up to a multiple of
+// 4) and the table size.
+__global__ void k_slice_width(int64_t n_slices, const int32_t* __restrict__ perm, const int64_t* __restrict__ nc_ptr,
                               int32_t* __restrict__ slice_k, int64_t* __restrict__ slice_sz)
 {
   int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_slices) return;
-  int64_t r0 = s * 64, r1 = r0 + 64 < n_rows ? r0 + 64 : n_rows;
   int64_t w = 0;
-  for (int64_t r = r0; r < r1; ++r) {
-    int64_t c = nc_ptr[r + 1] - nc_ptr[r];
+  for (int l = 0; l < 64; ++l) {
+    const int32_t r = perm[s * 64 + l];
+    if (r < 0) continue;
+    const int64_t c = nc_ptr[r + 1] - nc_ptr[r];
     w = c > w ? c : w;
   }
   w = (w + 3) & ~(int64_t)3;  // groups of 4 incidences per lane (one 16-B load)
@@ -149,7 +176,7 @@ __global__ void k_slice_width(int64_t n_rows, int64_t n_slices, const int64_t* _
   slice_sz[s] = w * 64;
 }
 
-__device__ __forceinline__ int find_slot(const int32_t* __restrict__ c, int len, int32_t x)
+__device__ int find_slot(const int32_t* c, int len, int32_t x)
 {
   int lo = 0, hi = len;
   while (lo < hi) {
@@ -162,45 +189,131 @@ __device__ __forceinline__ int find_slot(const int32_t* __restrict__ c, int len,
   return lo;
 }
 
-__global__ void k_fill_inc(int64_t n_rows, int nv, const int32_t* __restrict__ cn, const int64_t* __restrict__ nc_ptr,
-                           const int32_t* __restrict__ nc, const int64_t* __restrict__ row_ptr,
-                           const int32_t* __restrict__ cols, const int64_t* __restrict__ slice_ptr,
-                           const int32_t* __restrict__ slice_k, uint32_t* __restrict__ inc)
+__global__ void k_fill_inc(int64_t n_pos, int nv, const int32_t* __restrict__ perm, const int32_t* __restrict__ cn,
+                           const int64_t* __restrict__ nc_ptr, const int32_t* __restrict__ nc,
+                           const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ cols,
+                           const int64_t* __restrict__ slice_ptr, const int32_t* __restrict__ slice_k,
+                           uint32_t* __restrict__ inc)
 {
-  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n_rows) return;
-  const int64_t s = r >> 6;
-  const int lane = (int)(r & 63);
-  const int32_t* c = cols + row_ptr[r];
-  const int len = (int)(row_ptr[r + 1] - row_ptr[r]);
-  const uint32_t dslot = (uint32_t)find_slot(c, len, (int32_t)r);
+  int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pos) return;
+  const int64_t s = p >> 6;
+  const int lane = (int)(p & 63);
   uint32_t* out = inc + slice_ptr[s] + lane * 4;  // entry k at (k/4)*256 + lane*4 + k%4
-  const int64_t b = nc_ptr[r];
-  const int cnt = (int)(nc_ptr[r + 1] - b);
-  for (int k = 0; k < cnt; ++k) {
-    const int32_t* nodes = cn + (int64_t)nc[b + k] * nv;
-    uint32_t packed = dslot << 24;
-    int o = 0;
-    for (int a = 0; a < nv; ++a) {
-      int32_t x = nodes[a];
-      if (x == (int32_t)r) continue;
-      packed |= (uint32_t)find_slot(c, len, x) << (8 * o);
-      ++o;
+  const int32_t r = perm[p];
+  int cnt = 0;
+  if (r >= 0) {
+    const int32_t* c = cols + row_ptr[r];
+    const int len = (int)(row_ptr[r + 1] - row_ptr[r]);
+    const uint32_t dslot = (uint32_t)find_slot(c, len, r);
+    const int64_t b = nc_ptr[r];
+    cnt = (int)(nc_ptr[r + 1] - b);
+    for (int k = 0; k < cnt; ++k) {
+      const int32_t* nodes = cn + (int64_t)nc[b + k] * nv;
+      uint32_t packed = dslot << 24;
+      int o = 0;
+      for (int a = 0; a < nv; ++a) {
+        int32_t x = nodes[a];
+        if (x == r) continue;
+        packed |= (uint32_t)find_slot(c, len, x) << (8 * o);
+        ++o;
+      }
+      if (nv == 3) packed |= 0xFFu << 16;  // unused third slot
+      out[(int64_t)(k >> 2) * 256 + (k & 3)] = packed;
     }
-    if (nv == 3) packed |= 0xFFu << 16;  // unused third slot
-    out[(int64_t)(k >> 2) * 256 + (k & 3)] = packed;
   }
   for (int k = cnt; k < slice_k[s]; ++k) out[(int64_t)(k >> 2) * 256 + (k & 3)] = kPad;
 }
 
-__global__ void k_block_seg(int64_t n_rows, int rpb, const int64_t* __restrict__ row_ptr, unsigned long long* out)
+// Slice node lists.  One wavefront per slice: the columns of the slice's
+// rows are bitonic-sorted in LDS and made unique (ballot compaction); the
+// WRITE pass stores the list and, for every (slot, lane), the column's
+// index in it.  Pass 1 (WRITE = false) only records the slice width and the
+// list length, for the prefix sums.
+template <bool WRITE>
+__global__ __launch_bounds__(64) void k_slice_nodes(const int32_t* __restrict__ perm, const int64_t* __restrict__ row_ptr,
+                                                    const int32_t* __restrict__ cols, int32_t* __restrict__ slice_w,
+                                                    int64_t* __restrict__ slice_nu, const int64_t* __restrict__ snode_ptr,
+                                                    int32_t* __restrict__ snode, const int64_t* __restrict__ lidx_ptr,
+                                                    uint16_t* __restrict__ lidx)
 {
-  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t r0 = b * rpb;
-  if (r0 >= n_rows) return;
-  int64_t r1 = r0 + rpb < n_rows ? r0 + rpb : n_rows;
-  unsigned long long seg = (unsigned long long)(row_ptr[r1] - row_ptr[r0]);
-  atomicMax(out, seg);
+  extern __shared__ int32_t buf[];
+  const int lane = threadIdx.x;
+  const int64_t s = blockIdx.x;
+  const int32_t r = perm[s * 64 + lane];
+  const int64_t rb = r >= 0 ? row_ptr[r] : 0;
+  const int len = r >= 0 ? (int)(row_ptr[r + 1] - rb) : 0;
+  int W = len;
+  for (int o = 32; o > 0; o >>= 1) W = max(W, __shfl_xor(W, o));
+  int M = 64;
+  while (M < 64 * W) M <<= 1;
+  for (int t = 0; t < (M >> 6); ++t) buf[t * 64 + lane] = t < len ? cols[rb + t] : INT_MAX;
+  __syncthreads();
+  for (int k = 2; k <= M; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = lane; i < M; i += 64) {
+        const int q = i ^ j;
+        if (q > i) {
+          const int a = buf[i], b = buf[q];
+          if ((a > b) == ((i & k) == 0)) {
+            buf[i] = b;
+            buf[q] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  int cnt = 0, carry = -1;
+  for (int base = 0; base < 64 * W; base += 64) {
+    const int v = buf[base + lane];
+    int prev = __shfl_up(v, 1);
+    if (lane == 0) prev = carry;
+    carry = __shfl(v, 63);
+    const bool f = v != INT_MAX && v != prev;
+    const unsigned long long m = __ballot(f);
+    const int pos = cnt + __popcll(m & ((1ull << lane) - 1ull));
+    __syncthreads();
+    if (f) buf[pos] = v;  // pos <= base + lane: later chunks are untouched
+    cnt += __popcll(m);
+    __syncthreads();
+  }
+  if (!WRITE) {
+    if (lane == 0) {
+      slice_w[s] = W;
+      slice_nu[s] = cnt;
+    }
+    return;
+  }
+  const int64_t u0 = snode_ptr[s];
+  for (int u = lane; u < cnt; u += 64) snode[u0 + u] = buf[u];
+  const int64_t l0 = lidx_ptr[s];
+  for (int t = 0; t < W; ++t) {
+    uint16_t v = 0;
+    if (t < len) v = (uint16_t)find_slot(buf, cnt, cols[rb + t]);
+    lidx[l0 + (int64_t)t * 64 + lane] = v;
+  }
+}
+
+__global__ void k_times64(int64_t n, const int32_t* __restrict__ w, int64_t* __restrict__ out)
+{
+  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) out[s] = 64 * (int64_t)w[s];
+}
+
+__global__ void k_slice_max(int64_t n_slices, const int32_t* __restrict__ perm, const int64_t* __restrict__ row_ptr,
+                            const int32_t* __restrict__ slice_w, const int64_t* __restrict__ slice_nu,
+                            unsigned long long* __restrict__ out)
+{
+  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_slices) return;
+  unsigned long long seg = 0;
+  for (int l = 0; l < 64; ++l) {
+    const int32_t r = perm[s * 64 + l];
+    if (r >= 0) seg += (unsigned long long)(row_ptr[r + 1] - row_ptr[r]);
+  }
+  atomicMax(&out[0], seg);
+  atomicMax(&out[1], (unsigned long long)slice_w[s]);
+  atomicMax(&out[2], (unsigned long long)slice_nu[s]);
 }
 
 }  // namespace
@@ -268,53 +381,86 @@ void build_structure(Mesh& m, Structure& s)
                      n_rows, nv, m.cell_node.p, nc_ptr.p, nc.p, nullptr, s.row_ptr.p, s.cols.p, s.diag_pos.p);
   AFEM_LAUNCHED();
 
-  // 3. sliced-ELL row-local incidence table
-  s.n_slices = (n_rows + 63) / 64;
+  // 3. processing order (slices of 64 rows)
+  const StructuredInfo& st = m.st;
+  if (st.valid && (st.dim == 3 || st.dim == 2)) {
+    const int64_t ax = st.n + 1;
+    const int64_t own_layers = st.k1 - st.k0;
+    const int64_t ay = st.dim == 3 ? (int64_t)st.n + 1 : own_layers;
+    const int64_t az = st.dim == 3 ? own_layers : 1;
+    AFEM_REQUIRE(ax * ay * az == n_rows, AFEM_ERR_STATE, "structured mesh: owned node box does not match n_own");
+    const int bx = st.dim == 3 ? 4 : 8, bz = st.dim == 3 ? 4 : 1;
+    s.n_slices = ((ax + bx - 1) / bx) * ((ay + bx - 1) / bx) * ((az + bz - 1) / bz);
+    s.perm.alloc(s.n_slices * 64);
+    hipLaunchKernelGGL(k_perm_bricks, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream, s.n_slices,
+                       st.dim, ax, ay, az, s.perm.p);
+    AFEM_LAUNCHED();
+    s.brick_order = true;
+    s.run = st.dim == 3 ? 4 : 8;
+  }
+  else {
+    s.n_slices = (n_rows + 63) / 64;
+    s.perm.alloc(s.n_slices * 64);
+    hipLaunchKernelGGL(k_perm_identity, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream,
+                       s.n_slices * 64, n_rows, s.perm.p);
+    AFEM_LAUNCHED();
+    s.brick_order = false;
+    s.run = 64;
+  }
+  const int64_t n_pos = s.n_slices * 64;
+
+  // 4. sliced-ELL row-local incidence table in processing order
   s.inc_slice_k.alloc(s.n_slices);
   DevBuf<int64_t> slice_sz;
   slice_sz.alloc(s.n_slices);
-  hipLaunchKernelGGL(k_slice_width, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, n_rows, s.n_slices,
+  hipLaunchKernelGGL(k_slice_width, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, s.n_slices, s.perm.p,
                      nc_ptr.p, s.inc_slice_k.p, slice_sz.p);
   AFEM_LAUNCHED();
   s.inc_slice_ptr.alloc(s.n_slices + 1);
   exclusive_scan_i64(ctx, slice_sz.p, s.inc_slice_ptr.p, s.n_slices);
   const int64_t inc_total = read_i64(ctx, s.inc_slice_ptr.p + s.n_slices);
   s.inc.alloc(inc_total > 0 ? inc_total : 1);
-  hipLaunchKernelGGL(k_fill_inc, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, nv, m.cell_node.p,
-                     nc_ptr.p, nc.p, s.row_ptr.p, s.cols.p, s.inc_slice_ptr.p, s.inc_slice_k.p, s.inc.p);
+  hipLaunchKernelGGL(k_fill_inc, dim3(grid_for(n_pos, 256)), dim3(256), 0, ctx.stream, n_pos, nv, s.perm.p,
+                     m.cell_node.p, nc_ptr.p, nc.p, s.row_ptr.p, s.cols.p, s.inc_slice_ptr.p, s.inc_slice_k.p, s.inc.p);
   AFEM_LAUNCHED();
 
-  // 4. rows per assembly block: the largest of 256/128/64 whose LDS segment
-  //    (4 B column + 8 B accumulator per non-zero) fits 64 KiB; 0 = use the
-  //    global-memory accumulation variant.
-  DevBuf<unsigned long long> mx;
-  mx.alloc(1);
-  s.rows_per_block = 0;
-  s.max_seg = 0;
-  for (int rpb : { 256, 128, 64 }) {
-    AFEM_HIP(hipMemsetAsync(mx.p, 0, mx.bytes(), ctx.stream));
-    int64_t nb = (n_rows + rpb - 1) / rpb;
-    hipLaunchKernelGGL(k_block_seg, dim3(grid_for(nb, 256)), dim3(256), 0, ctx.stream, n_rows, rpb, s.row_ptr.p, mx.p);
-    AFEM_LAUNCHED();
-    unsigned long long hm = 0;
-    AFEM_HIP(hipMemcpyAsync(&hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
-    ctx.sync();
-    if (hm * 12ull + 128ull <= 64ull * 1024ull) {
-      s.rows_per_block = rpb;
-      s.max_seg = (int64_t)hm;
-      break;
-    }
-  }
-  // per-wave (slice of 64 rows) maximum segment, for the wave-local kernels
+  // 5. slice node lists + local column indices
+  int m_cap = 64;
+  while (m_cap < 64 * s.max_row_len) m_cap <<= 1;
+  s.slice_w.alloc(s.n_slices);
+  DevBuf<int64_t> slice_nu;
+  slice_nu.alloc(s.n_slices);
+  hipLaunchKernelGGL(k_slice_nodes<false>, dim3((unsigned)s.n_slices), dim3(64), (size_t)m_cap * 4, ctx.stream,
+                     s.perm.p, s.row_ptr.p, s.cols.p, s.slice_w.p, slice_nu.p, nullptr, nullptr, nullptr, nullptr);
+  AFEM_LAUNCHED();
+  s.snode_ptr.alloc(s.n_slices + 1);
+  exclusive_scan_i64(ctx, slice_nu.p, s.snode_ptr.p, s.n_slices);
+  const int64_t n_snode = read_i64(ctx, s.snode_ptr.p + s.n_slices);
+  hipLaunchKernelGGL(k_times64, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, s.n_slices, s.slice_w.p,
+                     slice_sz.p);
+  AFEM_LAUNCHED();
+  s.lidx_ptr.alloc(s.n_slices + 1);
+  exclusive_scan_i64(ctx, slice_sz.p, s.lidx_ptr.p, s.n_slices);
+  const int64_t n_lidx = read_i64(ctx, s.lidx_ptr.p + s.n_slices);
+  s.snode.alloc(n_snode > 0 ? n_snode : 1);
+  s.lidx.alloc(n_lidx + 8);  // tail: the assembly stages the table with 16-B loads
+  hipLaunchKernelGGL(k_slice_nodes<true>, dim3((unsigned)s.n_slices), dim3(64), (size_t)m_cap * 4, ctx.stream,
+                     s.perm.p, s.row_ptr.p, s.cols.p, nullptr, nullptr, s.snode_ptr.p, s.snode.p, s.lidx_ptr.p,
+                     s.lidx.p);
+  AFEM_LAUNCHED();
   {
+    DevBuf<unsigned long long> mx;
+    mx.alloc(3);
     AFEM_HIP(hipMemsetAsync(mx.p, 0, mx.bytes(), ctx.stream));
-    hipLaunchKernelGGL(k_block_seg, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, n_rows, 64, s.row_ptr.p,
-                       mx.p);
+    hipLaunchKernelGGL(k_slice_max, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, s.n_slices, s.perm.p,
+                       s.row_ptr.p, s.slice_w.p, slice_nu.p, mx.p);
     AFEM_LAUNCHED();
-    unsigned long long hm = 0;
-    AFEM_HIP(hipMemcpyAsync(&hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
+    unsigned long long hm[3] = { 0, 0, 0 };
+    AFEM_HIP(hipMemcpyAsync(hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
     ctx.sync();
-    s.max_wave_seg = (int64_t)hm;
+    s.max_wave_seg = (int64_t)hm[0];
+    s.max_slice_w = (int)hm[1];
+    s.max_slice_nodes = (int)hm[2];
   }
   ctx.sync();
 }

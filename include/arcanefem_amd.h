@@ -164,8 +164,13 @@ typedef struct afem_bsr_stats {
   int64_t n_incidences;     /* (owned row, incident cell) pairs = entries of the incidence table */
   int64_t inc_table_entries;/* incidence table size including sliced-ELL padding */
   int32_t max_row_len;      /* max non-zero blocks in a row */
-  int32_t rows_per_block;   /* assembly workgroup rows (0: global-memory accumulation variant) */
-  int64_t max_seg;          /* max non-zeros of one workgroup's row block */
+  int32_t rows_per_block;   /* rows per assembly wavefront (64: LDS slice tiles; 0: global-memory accumulation variant) */
+  int64_t max_seg;          /* max non-zero blocks of one slice (64 rows in processing order) */
+  int32_t max_slice_nodes;  /* max distinct nodes one slice couples to (LDS coordinate cache) */
+  int32_t max_slice_width;  /* max row length within one slice */
+  int64_t n_slices;         /* assembly slices (wavefronts per launch) */
+  int32_t brick_order;      /* 1: slices are 4x4x4 (3D) / 8x8 (2D) node bricks, 0: node order */
+  int32_t reserved;
 } afem_bsr_stats;
 int afem_bsr_get_stats(afem_bsr* bsr, afem_bsr_stats* stats);
 /* Copies the scalar CSR expansion to host in the reference's CSRFormatView

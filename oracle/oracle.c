@@ -266,6 +266,44 @@ void orc_element_elasticity_tri3(const double* xyz, double lambda, double mu2, d
     }
 }
 
+/* Global block-2 elasticity assembly on triangles, values "ordered per block"
+ * (femutils/BSRFormat.h:786-850, assembleBilinearOrderedPerBlock: for every
+ * cell, every owned row node a and every node b of the cell, the 2x2 block
+ * K[2a+i][2b+j] is added at block_index*4 + i*2 + j).  Returns the number of
+ * (row,col) blocks not found in the structure. */
+int64_t orc_assemble_elasticity_tri(int64_t n_rows, int64_t n_cells, const int32_t* cell_node, const double* coords,
+                                    const int64_t* row_ptr, const int32_t* cols, double lambda, double mu2,
+                                    double* vals)
+{
+  int64_t missing = 0;
+  double xyz[9], K[36];
+  for (int64_t c = 0; c < n_cells; ++c) {
+    const int32_t* n = cell_node + 3 * c;
+    for (int a = 0; a < 3; ++a)
+      for (int d = 0; d < 3; ++d)
+        xyz[3 * a + d] = coords[3 * (int64_t)n[a] + d];
+    orc_element_elasticity_tri3(xyz, lambda, mu2, K);
+    for (int a = 0; a < 3; ++a) {
+      int32_t row = n[a];
+      if (row >= n_rows)
+        continue;
+      for (int b = 0; b < 3; ++b) {
+        int64_t k = row_ptr[row], end = row_ptr[row + 1];
+        while (k < end && cols[k] != n[b])
+          ++k;
+        if (k == end) {
+          ++missing;
+          continue;
+        }
+        for (int i = 0; i < 2; ++i)
+          for (int j = 0; j < 2; ++j)
+            vals[4 * k + 2 * i + j] += K[6 * (2 * a + i) + 2 * b + j];
+      }
+    }
+  }
+  return missing;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Dirichlet via penalty: femutils/ArcaneFemFunctionsGpu.h:434-456 (forced    */
 /* info/value, rhs = P*g) then femutils/HypreDoFLinearSystem.cc:356-382       */

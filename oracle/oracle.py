@@ -56,6 +56,9 @@ def lib():
         L.orc_assemble_poisson.restype = ctypes.c_int64
         L.orc_assemble_poisson.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _i32p, _f64p, _i64p, _i32p,
                                            _f64p, ctypes.c_double, ctypes.c_void_p]
+        L.orc_assemble_elasticity_tri.restype = ctypes.c_int64
+        L.orc_assemble_elasticity_tri.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _f64p, _i64p, _i32p,
+                                                  ctypes.c_double, ctypes.c_double, _f64p]
         L.orc_dirichlet_penalty.argtypes = [ctypes.c_int64, _i32p, ctypes.c_double, ctypes.c_double, _i64p, _i32p,
                                             _f64p, _f64p]
         L.orc_row_elimination.argtypes = [ctypes.c_int64, _i32p, ctypes.c_double, _i64p, _i32p, _f64p, _f64p]
@@ -121,6 +124,30 @@ def assemble_poisson(n_rows, cells, coords, row_ptr, cols, f=0.0, with_rhs=True)
     if missing:
         raise RuntimeError(f"{missing} (row,col) pairs missing from the structure")
     return vals, rhs
+
+
+def assemble_elasticity_tri(n_rows, cells, coords, row_ptr, cols, lam, mu2):
+    """Block-2 P1 elasticity values, ordered per block (block*4 + i*2 + j)."""
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    coords = np.ascontiguousarray(coords, dtype=np.float64).reshape(-1, 3)
+    vals = np.zeros(4 * cols.shape[0], dtype=np.float64)
+    missing = lib().orc_assemble_elasticity_tri(n_rows, cells.shape[0], cells.ravel(), coords.ravel(), row_ptr, cols,
+                                                lam, mu2, vals)
+    if missing:
+        raise RuntimeError(f"{missing} (row,col) blocks missing from the structure")
+    return vals
+
+
+def blocks_to_row_order(row_ptr, vals4):
+    """Per-block 2x2 values -> the per-scalar-row (CSR / Hypre) layout
+    rb*4 + i*2*len + 2*slot + j (femutils/BSRFormat.h:877-887)."""
+    out = np.empty_like(vals4)
+    for r in range(row_ptr.shape[0] - 1):
+        rb, re = int(row_ptr[r]), int(row_ptr[r + 1])
+        ln = re - rb
+        blk = vals4[4 * rb:4 * re].reshape(ln, 2, 2)
+        out[4 * rb:4 * re] = blk.transpose(1, 0, 2).reshape(-1)
+    return out
 
 
 def dirichlet_penalty(dofs, value, penalty, row_ptr, cols, vals, rhs):

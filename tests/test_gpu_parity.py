@@ -128,6 +128,53 @@ def test_ghost_rows_are_not_materialised(ctx):
     assert np.abs(ls.rhs_host() - orhs).max() <= VAL_TOL * np.abs(orhs).max()
 
 
+@pytest.mark.parametrize("dim,n,nz,nranks,rank", [(3, 9, 13, 3, 1), (3, 7, 10, 2, 0), (2, 21, None, 2, 1),
+                                                   (2, 30, None, 3, 2)])
+def test_slab_assembly_parity(ctx, dim, n, nz, nranks, rank):
+    # brick-ordered slices over slabs whose owned layer count is not a
+    # multiple of the brick height (partial bricks, idle lanes)
+    mesh = af.Mesh.structured(ctx, dim, n, nz=nz, nranks=nranks, rank=rank)
+    bsr, ls = _assemble_gpu(ctx, mesh, 3.0)
+    st = bsr.stats()
+    assert st["brick_order"] == 1 and st["rows_per_block"] == 64
+    rows, cols, vals = bsr.download()
+    cells, coords, _ = mesh.download()
+    orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+    ovals, orhs = O.assemble_poisson(mesh.n_own_nodes, cells, coords, orp, ocols, 3.0)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    _check_values(vals, ovals)
+    assert np.abs(ls.rhs_host() - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+
+
+def _elasticity_meshes(ctx, which):
+    if which == "bar":
+        gm = read_gmsh(path("bar.msh"))
+        return af.Mesh.from_arrays(ctx, 2, gm.cells, gm.coords)
+    if which == "box":
+        return af.Mesh.structured(ctx, 2, 37)
+    return af.Mesh.structured(ctx, 2, 19, nranks=3, rank=1)
+
+
+@pytest.mark.parametrize("which", ["bar", "box", "slab"])
+@pytest.mark.parametrize("use_csr", [False, True])
+def test_elasticity_assembly_parity(ctx, which, use_csr):
+    # block-2 P1 elasticity (modules/elasticity/FemModule.h:112-140) in both
+    # value layouts of BSRFormat: per block and per scalar row (Hypre CSR)
+    mesh = _elasticity_meshes(ctx, which)
+    lam, mu2 = 1.2e5, 2 * 8.1e4
+    bsr = af.BSRFormat(mesh, 2).initialize(use_csr)
+    bsr.computeSparsity()
+    bsr.assembleElasticityP1(lam, mu2)
+    rows, cols, vals = bsr.download()
+    cells, coords, _ = mesh.download()
+    orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+    ovals = O.assemble_elasticity_tri(mesh.n_own_nodes, cells, coords, orp, ocols, lam, mu2)
+    if use_csr:
+        ovals = O.blocks_to_row_order(orp, ovals)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    _check_values(vals, ovals)
+
+
 def test_row_sums_vanish_at_scale(ctx):
     # size-independent property on a ~1.1M DoF mesh: constants are in the
     # kernel of the Laplacian (rows sum to 0 up to rounding) and K is symmetric

@@ -62,6 +62,31 @@ def test_elasticity_element_rigid_modes():
         assert np.abs(K @ mode).max() < 1e-12 * np.abs(K).max()
 
 
+def test_global_elasticity_rigid_modes_and_layouts():
+    # the assembled block-2 matrix on the reference's bar mesh: symmetric, the
+    # three planar rigid-body modes in its kernel, and the per-row (Hypre CSR)
+    # layout a permutation of the per-block one
+    m = read_gmsh(path("bar.msh"))
+    rp, cols = O.sparsity(m.n_nodes, m.n_nodes, m.cells)
+    v = O.assemble_elasticity_tri(m.n_nodes, m.cells, m.coords, rp, cols, 1.2e5, 1.6e5)
+    n = m.n_nodes
+    A = np.zeros((2 * n, 2 * n))
+    for r in range(n):
+        for k in range(rp[r], rp[r + 1]):
+            A[2 * r:2 * r + 2, 2 * cols[k]:2 * cols[k] + 2] = v[4 * k:4 * k + 4].reshape(2, 2)
+    scale = np.abs(A).max()
+    assert np.abs(A - A.T).max() <= 1e-12 * scale
+    x, y = m.coords[:, 0], m.coords[:, 1]
+    for mode in (np.ravel(np.c_[np.ones(n), np.zeros(n)]), np.ravel(np.c_[np.zeros(n), np.ones(n)]),
+                 np.ravel(np.c_[-y, x])):
+        assert np.abs(A @ mode).max() <= 1e-10 * scale * max(1.0, np.abs(mode).max())
+    w = O.blocks_to_row_order(rp, v)
+    assert np.array_equal(np.sort(w), np.sort(v))
+    r = 5
+    ln = rp[r + 1] - rp[r]
+    assert w[4 * rp[r] + 2 * ln] == v[4 * rp[r] + 2]  # (i=1, slot 0, j=0)
+
+
 def test_sparsity_is_edge_graph():
     m = O.structured_mesh(3, 4)
     rp, cols = O.sparsity(m["n_local"], m["n_own"], m["cells"])
