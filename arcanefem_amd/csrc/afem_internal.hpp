@@ -124,6 +124,7 @@ struct Structure {
   DevBuf<uint32_t> inc;
   DevBuf<int64_t> inc_slice_ptr;  // [n_slices+1]
   DevBuf<int32_t> inc_slice_k;    // [n_slices] max incidences in the slice
+  int64_t inc_pad_off = 0;        // 256 padding entries at the end (slices without incidences)
   // Per slice: the sorted unique nodes its rows couple to (snode, the
   // coordinate cache the assembly stages in LDS) and, for every (slot t,
   // lane), the index of column cols[row_ptr[row]+t] in that list:
@@ -133,7 +134,17 @@ struct Structure {
   DevBuf<uint16_t> lidx;
   DevBuf<int64_t> snode_ptr;   // [n_slices+1]
   DevBuf<int32_t> snode;
-  int max_slice_nodes = 0, max_slice_w = 0;
+  int max_slice_nodes = 0, max_slice_w = 0, max_slice_k = 0;
+  // Row strips (sparsity.hip, "row strips"): per slice, 16-step chunks of one
+  // byte per step per lane at strip_ptr[s] + chunk*1024 + lane*16 + step%16;
+  // dslot = diagonal slot of each position's row.
+  bool strip_ok = false;
+  int max_strip_c = 0;
+  DevBuf<uint8_t> strip;
+  DevBuf<int64_t> strip_ptr;
+  DevBuf<int32_t> strip_c;  // 16-step chunks per slice
+  DevBuf<int32_t> strip_n;  // steps per slice (longest row stream)
+  DevBuf<uint8_t> dslot;
   int64_t n_slices = 0;
   int64_t n_incidences = 0;  // real (non-padding) entries
   int max_row_len = 0;

@@ -49,6 +49,15 @@ __device__ __forceinline__ V3 ld3(const double* __restrict__ c, int64_t n)
 {
   return V3{ c[3 * n + 0], c[3 * n + 1], c[3 * n + 2] };
 }
+// 1/a for the strip kernel: hardware estimate + ONE Newton step (relative
+// error <= eps_rcp^2, below 2^-46 even for a 2^-23 estimate: far inside the
+// 1e-12 parity bar; 3 VALU ops instead of 5)
+__device__ __forceinline__ double recip1(double a)
+{
+  const double r = __builtin_amdgcn_rcp(a);
+  return fma(r, fma(-a, r, 1.0), r);
+}
+
 __device__ __forceinline__ V3 sub(V3 a, V3 b) { return V3{ a.x - b.x, a.y - b.y, a.z - b.z }; }
 __device__ __forceinline__ V3 cross(V3 a, V3 b)
 {
@@ -265,17 +274,54 @@ __device__ __forceinline__ void write_back(const TILE& tile, int lane, int run, 
 // is owned by a single lane and a wave's LDS operations execute in program
 // order, so the summation order of every entry is fixed by the structure:
 // the assembled matrix is bitwise reproducible run to run.
+//
+// Persistent, software-pipelined waves: a wave walks a contiguous chunk of
+// slices (adjacent bricks: their coordinate footprints overlap in L1/L2).
+// While it computes slice i, the loads of slice i+1 are in flight into
+// registers (SlicePre): level 1 at the top of slice i (row ids, node ids,
+// local column table, first incidence words), level 2 after the first
+// incidence group (row offsets, row coordinates, node coordinates: they need
+// the level-1 values).  Slice i+1 is then staged into LDS from registers with
+// no memory wait, so the only exposed latency per slice is LDS latency.
+// The write-back of slice i is a flat copy of its value segment (one
+// contiguous range per x-run of rows) through a (position -> slot, lane) map
+// built in the then-free column-table region; its stores retire under the
+// next slice's arithmetic.
+//
 // The group loop is uniform over the wave (padding entries are computed as
-// degenerate cells whose scale is masked to 0) and the incidence words are
-// prefetched two groups ahead by unconditional loads (a conditional load
-// made the compiler wait for it right away).  The diagonal is not
+// degenerate cells whose scale is masked to 0).  The diagonal is not
 // accumulated: rows of the P1 Laplacian sum to zero (sum of the shape
-// function gradients), so K_ii = -sum_{j != i} K_ij, formed at write-back.
+// function gradients), so K_ii = -sum_{j != i} K_ij, formed before write-back.
 // ABL != 0 only in diagnostic runs (AFEM_ASSEMBLY_ABLATION, results wrong):
 // 1 = no element arithmetic, 2 = no LDS coordinate reads, 3 = no LDS adds,
-// 4 = no staging (coordinates / indices / zeroing), 5 = no write-back.
-template <int NV, int UCAP, int ABL = 0>
-__global__ __launch_bounds__(64) void k_assemble_p1(int u_cap, int w_cap, int run, const int32_t* __restrict__ perm,
+// 4 = no LDS staging (coordinates / indices / zeroing), 5 = no write-back.
+// native 4 x u32 vector: plain registers (HIP's uint4 is a union-based class
+// that keeps a struct copy of it in scratch)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Registers of one slice while it is in flight.  MAXG = incidence groups of 4
+// held per lane (the whole incidence table row of the slice).
+template <int MAXG>
+struct SlicePre {
+  int32_t row;
+  int32_t len;
+  int64_t rb;
+  V3 xi;
+  int32_t nid[4];
+  u32x4 l0, l1;
+  u32x4 wd[MAXG];
+  double x[4], y[4], z[4];
+};
+
+// Every vector-memory operation of the steady state has a compile-time count
+// (unrolled group loop, all incidence words prefetched, fixed-count
+// unconditional write-back stores, clamped duplicate addresses instead of
+// predication): the waitcnt pass can then wait for a load without draining
+// the younger write-back stores (vmcnt retires in issue order).
+// MAXW = max row length (slots) the fixed write-back covers.
+template <int NV, int UCAP, int MAXG, int MAXW, int ABL = 0>
+__global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t chunk, int u_cap, int w_cap,
+                                                    int64_t pad_off, const int32_t* __restrict__ perm,
                                                     const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ inc,
                                                     const int64_t* __restrict__ slice_ptr,
@@ -293,108 +339,571 @@ __global__ __launch_bounds__(64) void k_assemble_p1(int u_cap, int w_cap, int ru
   extern __shared__ __align__(16) unsigned char smem[];
   Tile<DIMC, 1, UCAP> tile(smem, u_cap, w_cap);
   const int lane = threadIdx.x;
-  const int64_t sl = xcd_swizzle(blockIdx.x, gridDim.x);
+  int64_t sl = xcd_swizzle(blockIdx.x, gridDim.x) * chunk;
+  const int64_t s_end = min(sl + chunk, n_slices);
+  if (sl >= s_end) return;
 
-  // per-lane prologue loads first, so their latency overlaps the staging
-  const int32_t row = perm[sl * 64 + lane];
-  const bool active = row >= 0;
-  const int64_t rb = active ? row_ptr[row] : 0;
-  const int len = active ? (int)(row_ptr[row + 1] - rb) : 0;
-  const V3 xi = ld3(coords, active ? row : 0);
-  const uint4* ip = reinterpret_cast<const uint4*>(inc + slice_ptr[sl]) + lane;
-  const int ngroups = slice_k[sl] >> 2;  // uniform over the wave
-  const int glast = ngroups > 0 ? ngroups - 1 : 0;
-  uint4 eA = ip[0];
-  uint4 eB = ip[(int64_t)(1 < glast ? 1 : glast) * 64];
-  if (ABL != 4) {
-    const int64_t u0 = snode_ptr[sl];
-    tile.stage(lane, (int)(snode_ptr[sl + 1] - u0), snode + u0, coords, slice_w[sl], lidx + lidx_ptr[sl]);
-  }
-  double macc = 0.0;
-  const uint32_t dslot = eA.x == kPad ? 0xFFu : (eA.x >> 24);
-
-  auto group = [&](const uint4 cur) {
-    const uint32_t ev[4] = { cur.x, cur.y, cur.z, cur.w };
-    V3 xa[4], xb[4], xc[4];
-    uint32_t sa[4], sb[4], sc[4];
+  // level 1: everything addressed by slice scalars only
+  auto level1 = [&](int64_t s, SlicePre<MAXG>& p) {
+    p.row = perm[s * 64 + lane];
+    const int nq = 8 * slice_w[s];
+    const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + lidx_ptr[s]);
+    p.l0 = ls[max(min(lane, nq - 1), 0)];
+    p.l1 = ls[max(min(lane + 64, nq - 1), 0)];
+    const int64_t u0 = snode_ptr[s];
+    const int nu = (int)(snode_ptr[s + 1] - u0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t e = ev[j] == kPad ? 0u : ev[j];
-      sa[j] = e & 0xFFu;
-      sb[j] = (e >> 8) & 0xFFu;
-      sc[j] = (NV == 4) ? (e >> 16) & 0xFFu : 0u;
-      if (ABL == 2) {
-        xa[j] = V3{ xi.x + 1e-3 * sa[j], xi.y, xi.z };
-        xb[j] = V3{ xi.x, xi.y + 1e-3 * sb[j], xi.z };
-        xc[j] = V3{ xi.x, xi.y, xi.z + 1e-3 * sc[j] };
-      }
-      else {
-        xa[j] = tile.node(lane, sa[j]);
-        xb[j] = tile.node(lane, sb[j]);
-        if (NV == 4) xc[j] = tile.node(lane, sc[j]);
-      }
-    }
+    for (int k = 0; k < 4; ++k) p.nid[k] = snode[u0 + max(min(lane + 64 * k, nu - 1), 0)];
+    const int ng = slice_k[s] >> 2;
+    const int gl = ng > 0 ? ng - 1 : 0;
+    const u32x4* ip = reinterpret_cast<const u32x4*>(inc + (ng > 0 ? slice_ptr[s] : pad_off)) + lane;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool pad = ev[j] == kPad;  // padding: degenerate cell (det 0), scale forced to 0
-      double k1, k2, k3 = 0.0, meas;
-      if (ABL == 1) {
-        k1 = xa[j].y + xb[j].x;
-        k2 = xb[j].y + xc[j].x;
-        k3 = xc[j].y + xc[j].z;
-        meas = xa[j].z + xb[j].z;
-      }
-      else if (NV == 4) {
-        const V3 e1 = sub(xa[j], xi), e2 = sub(xb[j], xi), e3 = sub(xc[j], xi);
-        const V3 c1 = cross(e2, e3), c2 = cross(e3, e1), c3 = cross(e1, e2);
-        const V3 c0 = V3{ -(c1.x + c2.x + c3.x), -(c1.y + c2.y + c3.y), -(c1.z + c2.z + c3.z) };
-        meas = fabs(dot(e1, c1));
-        const double s = pad ? 0.0 : s_coef * recip(meas);
-        k1 = dot(c0, c1) * s;
-        k2 = dot(c0, c2) * s;
-        k3 = dot(c0, c3) * s;
-      }
-      else {
-        const double e1x = xa[j].x - xi.x, e1y = xa[j].y - xi.y, e2x = xb[j].x - xi.x, e2y = xb[j].y - xi.y;
-        const double c1x = e2y, c1y = -e2x, c2x = -e1y, c2y = e1x;
-        const double c0x = -(c1x + c2x), c0y = -(c1y + c2y);
-        meas = fabs(e1x * e2y - e2x * e1y);
-        const double s = pad ? 0.0 : s_coef * recip(meas);
-        k1 = (c0x * c1x + c0y * c1y) * s;
-        k2 = (c0x * c2x + c0y * c2y) * s;
-      }
-      macc += meas;
-      if (ABL != 3) {
-        atomicAdd(tile.at(lane, sa[j], 0), k1);
-        atomicAdd(tile.at(lane, sb[j], 0), k2);
-        if (NV == 4) atomicAdd(tile.at(lane, sc[j], 0), k3);
-      }
-      else {
-        macc += k1 + k2 + k3;
-      }
+    for (int g = 0; g < MAXG; ++g) p.wd[g] = ip[(int64_t)min(g, gl) * 64];
+  };
+  // level 2: addressed by level-1 values
+  auto level2 = [&](SlicePre<MAXG>& p) {
+    const bool act = p.row >= 0;
+    const int32_t r = act ? p.row : 0;
+    const int64_t b = row_ptr[r];
+    const int64_t e = row_ptr[r + 1];
+    p.rb = act ? b : 0;
+    p.len = act ? (int)(e - b) : 0;
+    p.xi = ld3(coords, r);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      p.x[k] = coords[3 * (int64_t)p.nid[k]];
+      p.y[k] = coords[3 * (int64_t)p.nid[k] + 1];
+      p.z[k] = DIMC == 3 ? coords[3 * (int64_t)p.nid[k] + 2] : 0.0;
     }
   };
-  // two-deep ring of incidence words, unrolled by 2 so that no register copy
-  // forces an early wait on a load
-  for (int g = 0; g < ngroups; g += 2) {
-    const uint4 a = eA;
-    eA = ip[(int64_t)(g + 2 < glast ? g + 2 : glast) * 64];
-    group(a);
-    if (g + 1 < ngroups) {
-      const uint4 b = eB;
-      eB = ip[(int64_t)(g + 3 < glast ? g + 3 : glast) * 64];
-      group(b);
+
+  SlicePre<MAXG> cur, nxt;
+  level1(sl, cur);
+  level2(cur);
+  for (; sl < s_end; ++sl) {
+    // the last slice of the chunk prefetches itself again (L2 hits): keeps
+    // every load and the register hand-over unconditional
+    const int64_t sn = sl + 1 < s_end ? sl + 1 : sl;
+    const int ngroups = slice_k[sl] >> 2;  // uniform over the wave
+    const int W = slice_w[sl];
+    const int64_t u0 = snode_ptr[sl];
+    const int nu = (int)(snode_ptr[sl + 1] - u0);
+
+    // ---- stage slice sl from registers (+ the rare overflow beyond 256 nodes / 16 slots)
+    if (ABL != 4) {
+      const int st = tile.stride();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int idx = max(min(lane + 64 * k, nu - 1), 0);
+        tile.cx[idx] = cur.x[k];
+        tile.cx[st + idx] = cur.y[k];
+        if (DIMC == 3) tile.cx[2 * st + idx] = cur.z[k];
+      }
+      if (nu > 256) {
+        for (int u = lane + 256; u < nu; u += 64) {
+          const int64_t n = snode[u0 + u];
+          tile.cx[u] = coords[3 * n];
+          tile.cx[st + u] = coords[3 * n + 1];
+          if (DIMC == 3) tile.cx[2 * st + u] = coords[3 * n + 2];
+        }
+      }
+      const int nq = 8 * W;
+      u32x4* dst = reinterpret_cast<u32x4*>(tile.li);
+      dst[max(min(lane, nq - 1), 0)] = cur.l0;
+      dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
+      if (nq > 128) {
+        const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + lidx_ptr[sl]);
+        for (int q = lane + 128; q < nq; q += 64) dst[q] = ls[q];
+      }
+      double2* a2 = reinterpret_cast<double2*>(tile.acc);
+      for (int q = lane; q < 32 * W; q += 64) a2[q] = make_double2(0.0, 0.0);
     }
+    wave_sync_lds();
+    level1(sn, nxt);
+
+    const int32_t row = cur.row;
+    const bool active = row >= 0;
+    const int64_t rb = cur.rb;
+    const int len = cur.len;
+    const V3 xi = cur.xi;
+    const uint32_t dslot = (ngroups == 0 || cur.wd[0].x == kPad) ? 0xFFu : (cur.wd[0].x >> 24);
+    double macc = 0.0;
+
+    auto group = [&](const u32x4 w) {
+      const uint32_t ev[4] = { w.x, w.y, w.z, w.w };
+      V3 xa[4], xb[4], xc[4];
+      uint32_t sa[4], sb[4], sc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t e = ev[j] == kPad ? 0u : ev[j];
+        sa[j] = e & 0xFFu;
+        sb[j] = (e >> 8) & 0xFFu;
+        sc[j] = (NV == 4) ? (e >> 16) & 0xFFu : 0u;
+        if (ABL == 2) {
+          xa[j] = V3{ xi.x + 1e-3 * sa[j], xi.y, xi.z };
+          xb[j] = V3{ xi.x, xi.y + 1e-3 * sb[j], xi.z };
+          xc[j] = V3{ xi.x, xi.y, xi.z + 1e-3 * sc[j] };
+        }
+        else {
+          xa[j] = tile.node(lane, sa[j]);
+          xb[j] = tile.node(lane, sb[j]);
+          if (NV == 4) xc[j] = tile.node(lane, sc[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool pad = ev[j] == kPad;  // padding: degenerate cell (det 0), scale forced to 0
+        double k1, k2, k3 = 0.0, meas;
+        if (ABL == 1) {
+          k1 = xa[j].y + xb[j].x;
+          k2 = xb[j].y + xc[j].x;
+          k3 = xc[j].y + xc[j].z;
+          meas = xa[j].z + xb[j].z;
+        }
+        else if (NV == 4) {
+          const V3 e1 = sub(xa[j], xi), e2 = sub(xb[j], xi), e3 = sub(xc[j], xi);
+          const V3 c1 = cross(e2, e3), c2 = cross(e3, e1), c3 = cross(e1, e2);
+          const V3 c0 = V3{ -(c1.x + c2.x + c3.x), -(c1.y + c2.y + c3.y), -(c1.z + c2.z + c3.z) };
+          meas = fabs(dot(e1, c1));
+          const double s = pad ? 0.0 : s_coef * recip(meas);
+          k1 = dot(c0, c1) * s;
+          k2 = dot(c0, c2) * s;
+          k3 = dot(c0, c3) * s;
+        }
+        else {
+          const double e1x = xa[j].x - xi.x, e1y = xa[j].y - xi.y, e2x = xb[j].x - xi.x, e2y = xb[j].y - xi.y;
+          const double c1x = e2y, c1y = -e2x, c2x = -e1y, c2y = e1x;
+          const double c0x = -(c1x + c2x), c0y = -(c1y + c2y);
+          meas = fabs(e1x * e2y - e2x * e1y);
+          const double s = pad ? 0.0 : s_coef * recip(meas);
+          k1 = (c0x * c1x + c0y * c1y) * s;
+          k2 = (c0x * c2x + c0y * c2y) * s;
+        }
+        macc += meas;
+        if (ABL != 3) {
+          atomicAdd(tile.at(lane, sa[j], 0), k1);
+          atomicAdd(tile.at(lane, sb[j], 0), k2);
+          if (NV == 4) atomicAdd(tile.at(lane, sc[j], 0), k3);
+        }
+        else {
+          macc += k1 + k2 + k3;
+        }
+      }
+    };
+    // unrolled over the compile-time group count (uniform skips past the
+    // slice's width); the next slice's level-2 loads go out after group 1,
+    // when its level-1 loads (issued a whole slice earlier) have landed
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g) {
+      if (g < ngroups) group(cur.wd[g]);
+      if (g == 1) level2(nxt);
+    }
+    if (MAXG < 2) level2(nxt);
+
+    // ---- RHS (unconditional store: idle lanes repeat an active lane's store)
+    {
+      const unsigned long long am = __ballot(active);
+      const int src = active ? lane : (int)__ffsll((long long)am) - 1;
+      const double rv = __shfl(f_meas * macc, src);
+      const int32_t rr = __shfl(row, src);
+      if (rhs) rhs[rr] = rv;
+    }
+    wave_sync_lds();
+
+    // ---- diagonal + write-back.  Each lane pulls its row out of the
+    // [slot][lane] accumulators into registers (conflict-free: a lane always
+    // hits its own bank pair), forms the diagonal, and stores the row back in
+    // CSR order at its flat offset (rows of one x-run of lanes are
+    // consecutive, so the flat image of a slice is a few contiguous value
+    // ranges).  Then consecutive lanes copy consecutive flat positions to
+    // HBM: conflict-free LDS reads, coalesced stores.  The flat image reuses
+    // the accumulator region, the (position -> slot, lane) map the
+    // column-table region.
+    int fp = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(fp, o);
+      if (lane >= o) fp += t;
+    }
+    const int total = __shfl(fp, 63);
+    fp -= len;
+    uint16_t* map = tile.li;
+    int64_t* rbs = reinterpret_cast<int64_t*>(tile.offs);
+    if (W <= MAXW) {
+      double rv[MAXW];
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t) rv[t] = *tile.at(lane, min(t, W - 1), 0);
+      double sum = 0.0;
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t)
+        if (t < len && t != (int)dslot) sum += rv[t];
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t)
+        if (t == (int)dslot) rv[t] = -sum;
+      wave_sync_lds();  // every lane's reads before the overlapping flat writes
+      const int64_t rb_base = __shfl(rb, 0);
+      if (ABL != 5) {
+#pragma unroll
+        for (int t = 0; t < MAXW; ++t)
+          if (t < len) {
+            tile.acc[fp + t] = rv[t];
+            map[fp + t] = (uint16_t)(t * 64 + lane);
+          }
+        rbs[lane] = rb;
+        wave_sync_lds();
+        if (ABL == 6) {  // LDS side of the copy only: results folded into one store
+          double acc6 = 0.0;
+#pragma unroll
+          for (int k = 0; k < MAXW; ++k) {
+            const int P = min(64 * k + lane, total - 1);
+            const int m = map[P];
+            acc6 += tile.acc[P] + (double)(rbs[m & 63] + (m >> 6));
+          }
+          if (acc6 == 12345.678) vals[0] = acc6;
+        }
+        else if (ABL == 7) {  // stores only: coalesced stores of a register value
+#pragma unroll
+          for (int k = 0; k < MAXW; ++k) {
+            const int P = min(64 * k + lane, total - 1);
+            vals[rb_base + P] = rv[k];
+          }
+        }
+        else {
+#pragma unroll
+          for (int k = 0; k < MAXW; ++k) {
+            const int P = min(64 * k + lane, total - 1);
+            const double v = tile.acc[P];
+            const int m = map[P];
+            vals[rbs[m & 63] + (m >> 6)] = v;
+          }
+        }
+      }
+    }
+    else {  // rows longer than MAXW (not on the host-selected variants)
+      if (active && dslot != 0xFFu) {
+        double sum = 0.0;
+        for (int t = 0; t < len; ++t)
+          if (t != (int)dslot) sum += *tile.at(lane, t, 0);
+        *tile.at(lane, dslot, 0) = -sum;
+      }
+      for (int t = 0; t < len; ++t) map[fp + t] = (uint16_t)(t * 64 + lane);
+      rbs[lane] = rb;
+      wave_sync_lds();
+      for (int p = lane; p < total; p += 64) {
+        const int ix = map[p];
+        vals[rbs[ix & 63] + (ix >> 6)] = tile.acc[ix];
+      }
+    }
+    wave_sync_lds();
+    cur = nxt;
   }
-  if (rhs && active) rhs[row] = f_meas * macc;
-  wave_sync_lds();
-  if (active && dslot != 0xFFu) {
-    double sum = 0.0;
-    for (int t = 0; t < len; ++t)
-      if (t != (int)dslot) sum += *tile.at(lane, t, 0);
-    *tile.at(lane, dslot, 0) = -sum;
+}
+
+// ---------------------------------------------------------------- scalar P1, row strips
+// Same slice tiles and software pipeline as k_assemble_p1, but each lane walks
+// its row's strip (sparsity.hip "row strips"): one stream byte per cell gives
+// the ONE new node of the window (slot + shift/swap kind).  Per cell: one
+// coordinate gather (3 LDS reads instead of 9), one index read (instead of 3),
+// two new cofactors (the third is the previous cell's, up to sign), ~42 FP64
+// ops instead of 55; the stream is 1 B per step instead of 4 B per cell.
+//   window (P,Q,R) + node D:  shift -> (Q,R,D),  swap -> (P,R,D)
+//   cofactors c_P = e_Q x e_R, c_Q = e_R x e_P, c_R = e_P x e_Q (e = x - x_row):
+//   c_R' = shift ? c_P : -c_Q (old window), c_P' = e_R x e_D, c_Q' = e_D x e_P'
+//   K_row,b = coef (c_row . c_b) / (6 |det|), c_row = -(c_P + c_Q + c_R), det = e_P . c_P
+// Triangles: window (P,Q) + D: shift -> (Q,D), swap -> (P,D).
+template <int MAXC>
+struct StripPre {
+  int32_t row;
+  int32_t len;
+  int64_t rb;
+  V3 xi;
+  int32_t nid[4];
+  u32x4 l0, l1;
+  u32x4 ch[MAXC];
+  uint32_t dslot;
+  double x[4], y[4], z[4];
+};
+
+// LDS image of a strip slice: accumulators [slot][lane] (as Tile), the
+// slice's node coordinates AoS (DIMC doubles per node: one address per
+// gather, components at immediate offsets), the u16 column-index table
+// [slot][lane], 512 B of write-back scratch.
+// (the coordinate region doubles as the write-back map: at least 2 B per value)
+__host__ __device__ constexpr int64_t strip_coord_bytes(int dimc, int64_t u_cap, int64_t w_cap)
+{
+  return ((8 * (int64_t)dimc * u_cap > 128 * w_cap ? 8 * (int64_t)dimc * u_cap : 128 * w_cap) + 15) & ~int64_t(15);
+}
+__host__ __device__ constexpr int64_t strip_tile_bytes(int dimc, int64_t u_cap, int64_t w_cap)
+{
+  return 8 * 64 * w_cap + strip_coord_bytes(dimc, u_cap, w_cap) + 2 * 64 * w_cap + 512;
+}
+
+template <int NV, int MAXC, int MAXW>
+__global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, int64_t chunk, int u_cap, int w_cap,
+                                                          const int32_t* __restrict__ perm,
+                                                          const int64_t* __restrict__ row_ptr,
+                                                          const uint8_t* __restrict__ strip,
+                                                          const int64_t* __restrict__ strip_ptr,
+                                                          const int32_t* __restrict__ strip_n,
+                                                          const uint8_t* __restrict__ dslots,
+                                                          const int32_t* __restrict__ slice_w,
+                                                          const int64_t* __restrict__ lidx_ptr,
+                                                          const uint16_t* __restrict__ lidx,
+                                                          const int64_t* __restrict__ snode_ptr,
+                                                          const int32_t* __restrict__ snode,
+                                                          const double* __restrict__ coords, double s_coef,
+                                                          double f_meas, double* __restrict__ vals,
+                                                          double* __restrict__ rhs)
+{
+  constexpr int DIMC = NV == 4 ? 3 : 2;
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* acc = reinterpret_cast<double*>(smem);
+  double* cxyz = reinterpret_cast<double*>(smem + 8 * 64 * (int64_t)w_cap);
+  uint16_t* li = reinterpret_cast<uint16_t*>(smem + 8 * 64 * (int64_t)w_cap + strip_coord_bytes(DIMC, u_cap, w_cap));
+  int64_t* rbs = reinterpret_cast<int64_t*>(reinterpret_cast<unsigned char*>(li) + 2 * 64 * (int64_t)w_cap);
+  const int lane = threadIdx.x;
+  int64_t sl = xcd_swizzle(blockIdx.x, gridDim.x) * chunk;
+  const int64_t s_end = min(sl + chunk, n_slices);
+  if (sl >= s_end) return;
+
+  auto level1 = [&](int64_t s, StripPre<MAXC>& p) {
+    p.row = perm[s * 64 + lane];
+    p.dslot = dslots[s * 64 + lane];
+    const int nq = 8 * slice_w[s];
+    const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + lidx_ptr[s]);
+    p.l0 = ls[max(min(lane, nq - 1), 0)];
+    p.l1 = ls[max(min(lane + 64, nq - 1), 0)];
+    const int64_t u0 = snode_ptr[s];
+    const int nu = (int)(snode_ptr[s + 1] - u0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p.nid[k] = snode[u0 + max(min(lane + 64 * k, nu - 1), 0)];
+    const int nc = (strip_n[s] + 15) >> 4;
+    const u32x4* sp = reinterpret_cast<const u32x4*>(strip + strip_ptr[s]) + lane;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
+  };
+  auto level2 = [&](StripPre<MAXC>& p) {
+    const bool act = p.row >= 0;
+    const int32_t r = act ? p.row : 0;
+    const int64_t b = row_ptr[r];
+    const int64_t e = row_ptr[r + 1];
+    p.rb = act ? b : 0;
+    p.len = act ? (int)(e - b) : 0;
+    p.xi = ld3(coords, r);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      p.x[k] = coords[3 * (int64_t)p.nid[k]];
+      p.y[k] = coords[3 * (int64_t)p.nid[k] + 1];
+      p.z[k] = DIMC == 3 ? coords[3 * (int64_t)p.nid[k] + 2] : 0.0;
+    }
+  };
+
+  StripPre<MAXC> cur, nxt;
+  level1(sl, cur);
+  level2(cur);
+  for (; sl < s_end; ++sl) {
+    const int64_t sn = sl + 1 < s_end ? sl + 1 : sl;
+    const int nsteps = strip_n[sl];  // uniform over the wave
+    const int W = slice_w[sl];
+    const int64_t u0 = snode_ptr[sl];
+    const int nu = (int)(snode_ptr[sl + 1] - u0);
+
+    // ---- stage slice sl from registers (+ the rare overflow beyond 256 nodes / 16 slots)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = max(min(lane + 64 * k, nu - 1), 0);
+      cxyz[DIMC * idx] = cur.x[k];
+      cxyz[DIMC * idx + 1] = cur.y[k];
+      if (DIMC == 3) cxyz[DIMC * idx + 2] = cur.z[k];
+    }
+    if (nu > 256) {
+      for (int u = lane + 256; u < nu; u += 64) {
+        const int64_t n = snode[u0 + u];
+        cxyz[DIMC * u] = coords[3 * n];
+        cxyz[DIMC * u + 1] = coords[3 * n + 1];
+        if (DIMC == 3) cxyz[DIMC * u + 2] = coords[3 * n + 2];
+      }
+    }
+    {
+      const int nq = 8 * W;
+      u32x4* dst = reinterpret_cast<u32x4*>(li);
+      dst[max(min(lane, nq - 1), 0)] = cur.l0;
+      dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
+      if (nq > 128) {
+        const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + lidx_ptr[sl]);
+        for (int q = lane + 128; q < nq; q += 64) dst[q] = ls[q];
+      }
+      double2* a2 = reinterpret_cast<double2*>(acc);
+      for (int q = lane; q < 32 * W; q += 64) a2[q] = make_double2(0.0, 0.0);
+    }
+    wave_sync_lds();
+    level1(sn, nxt);
+
+    const int32_t row = cur.row;
+    const bool active = row >= 0;
+    const int64_t rb = cur.rb;
+    const int len = cur.len;
+    const V3 xi = cur.xi;
+    const uint32_t dslot = cur.dslot;
+    double macc = 0.0;
+    // window state (zero vectors: finite arithmetic on priming / padding
+    // steps); cN = e_P x e_R = -c_Q is kept instead of c_Q (no negations)
+    V3 eP{ 0.0, 0.0, 0.0 }, eQ{ 0.0, 0.0, 0.0 }, eR{ 0.0, 0.0, 0.0 };
+    V3 cP{ 0.0, 0.0, 0.0 }, cN{ 0.0, 0.0, 0.0 };
+    double* const acc_lane = acc + lane;
+    double* aP = acc_lane + 64 * dslot;  // accumulator addresses of the window nodes
+    double* aQ = aP;
+    double* aR = aP;
+    const uint16_t* lrow = li + lane;
+
+    auto lidx_of = [&](uint32_t byte) { return (int)lrow[(byte & 63u) * 64]; };
+    auto coord = [&](int u) {
+      const double* q = cxyz + DIMC * u;
+      return V3{ q[0], q[1], DIMC == 3 ? q[2] : 0.0 };
+    };
+    auto sel = [](bool c, V3 a, V3 b) { return V3{ c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z }; };
+    // x if the step emits a cell, +0.0 otherwise: a bit mask, not a select
+    // (the compiler turns a select of a reciprocal into a branch)
+    auto keep = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
+    auto step = [&](uint32_t byte, V3 xd) {
+      const bool swap = (byte & 0xC0u) == 0x40u;
+      const uint64_t em = (uint64_t)0 - (uint64_t)(byte < 0x80u);
+      double* const aD = acc_lane + 64 * (byte & 63u);
+      const V3 eD = sub(xd, xi);
+      double kP, kQ, kR = 0.0, meas;
+      if (NV == 4) {
+        const V3 cRn = sel(swap, cN, cP);  // c_R of the new window (shift: old c_P, swap: -old c_Q)
+        eP = sel(swap, eP, eQ);
+        aP = swap ? aP : aQ;
+        eQ = eR;
+        aQ = aR;
+        eR = eD;
+        aR = aD;
+        cP = cross(eQ, eR);
+        cN = cross(eP, eR);
+        // -c_row = c_P + c_Q + c_R = c_P - cN + cRn
+        const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
+        meas = fabs(dot(eP, cP));
+        const double s = keep(em, -s_coef * recip1(meas));  // carries the sign of c_row = -m
+        kP = dot(m, cP) * s;
+        kQ = -dot(m, cN) * s;
+        kR = dot(m, cRn) * s;
+      }
+      else {
+        eP = sel(swap, eP, eQ);
+        aP = swap ? aP : aQ;
+        eQ = eD;
+        aQ = aD;
+        // triangle (row, P, Q): c_P = (eQ.y, -eQ.x), c_Q = (-eP.y, eP.x), c_row = -(c_P + c_Q)
+        const double cpx = eQ.y, cpy = -eQ.x, cqx = -eP.y, cqy = eP.x;
+        const double crx = -(cpx + cqx), cry = -(cpy + cqy);
+        meas = fabs(eP.x * eQ.y - eQ.x * eP.y);
+        const double s = keep(em, s_coef * recip1(meas));
+        kP = (crx * cpx + cry * cpy) * s;
+        kQ = (crx * cqx + cry * cqy) * s;
+      }
+      macc += keep(em, meas);
+      atomicAdd(aP, kP);
+      atomicAdd(aQ, kQ);
+      if (NV == 4) atomicAdd(aR, kR);
+    };
+
+    // steps: byte j of the stream = byte j%16 of chunk j/16; uniform guard per
+    // 4-step word, padding steps are no-ops.  Two-deep LDS pipeline: at step
+    // j the column-index read of step j+2 and the coordinate reads of step
+    // j+1 are issued before step j's arithmetic and accumulator adds (no
+    // alias hazard: coordinates and indices are not written in the loop).
+    auto byte_at = [&](int j) -> uint32_t {
+      const u32x4 w = cur.ch[j >> 4];
+      const int q = (j >> 2) & 3;
+      const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
+      return (wq >> (8 * (j & 3))) & 0xFFu;
+    };
+    constexpr int NSTEP = 16 * MAXC;
+    int u1 = lidx_of(byte_at(0));
+    V3 xc = coord(u1);
+    u1 = lidx_of(byte_at(1));
+#pragma unroll
+    for (int j = 0; j < NSTEP; ++j) {
+      if ((j & 3) == 0 && j >= nsteps) break;
+      const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
+      const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
+      step(byte_at(j), xc);
+      xc = xn;
+      u1 = u2;
+      // next slice's level-2 loads: ~12 steps after its level-1 loads were issued
+      if (j == 11) level2(nxt);
+    }
+    if (nsteps <= 8) level2(nxt);  // the loop ended before step 11
+
+    // ---- RHS (unconditional store: idle lanes repeat an active lane's store)
+    {
+      const unsigned long long am = __ballot(active);
+      const int src = active ? lane : (int)__ffsll((long long)am) - 1;
+      const double rv = __shfl(f_meas * macc, src);
+      const int32_t rr = __shfl(row, src);
+      if (rhs) rhs[rr] = rv;
+    }
+    wave_sync_lds();
+
+    // ---- diagonal + write-back (as k_assemble_p1; the map overlays the coordinates)
+    int fp = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(fp, o);
+      if (lane >= o) fp += t;
+    }
+    const int total = __shfl(fp, 63);
+    fp -= len;
+    uint16_t* map = reinterpret_cast<uint16_t*>(cxyz);
+    const uint32_t dsl = active ? dslot : 0xFFu;
+    if (W <= MAXW) {
+      double rv[MAXW];
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t) rv[t] = acc_lane[64 * min(t, W - 1)];
+      double sum = 0.0;
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t)
+        if (t < len && t != (int)dsl) sum += rv[t];
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t)
+        if (t == (int)dsl) rv[t] = -sum;
+      wave_sync_lds();  // every lane's reads before the overlapping flat writes
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t)
+        if (t < len) {
+          acc[fp + t] = rv[t];
+          map[fp + t] = (uint16_t)(t * 64 + lane);
+        }
+      rbs[lane] = rb;
+      wave_sync_lds();
+#pragma unroll
+      for (int k = 0; k < MAXW; ++k) {
+        const int P = min(64 * k + lane, total - 1);
+        const double v = acc[P];
+        const int m = map[P];
+        vals[rbs[m & 63] + (m >> 6)] = v;
+      }
+    }
+    else {
+      if (dsl != 0xFFu) {
+        double sum = 0.0;
+        for (int t = 0; t < len; ++t)
+          if (t != (int)dsl) sum += acc_lane[64 * t];
+        acc_lane[64 * dsl] = -sum;
+      }
+      wave_sync_lds();
+      for (int t = 0; t < len; ++t) map[fp + t] = (uint16_t)(t * 64 + lane);
+      rbs[lane] = rb;
+      wave_sync_lds();
+      for (int p = lane; p < total; p += 64) {
+        const int ix = map[p];
+        vals[rbs[ix & 63] + (ix >> 6)] = acc[ix];
+      }
+    }
+    wave_sync_lds();
+    cur = nxt;
   }
-  if (ABL != 5) write_back<1>(tile, lane, run, active, rb, len, true, vals);
 }
 
 // Global-memory variant for rows too long for the LDS tile: coordinates
@@ -663,6 +1172,15 @@ namespace {
 // LDS tile budget per wave (one wave per workgroup): beyond it the global
 // accumulation variants run (rows of > ~90 non-zeros, not P1 meshes).
 constexpr int64_t kTileLdsMax = 64 * 1024;
+// AFEM_ASSEMBLY_WAVES_PER_CU: diagnostic override of the persistent grid size
+int occ_override()
+{
+  static const int v = [] {
+    const char* e = getenv("AFEM_ASSEMBLY_WAVES_PER_CU");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 }  // namespace
 
 void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
@@ -680,8 +1198,51 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
   // RHS = f * |K| / nv = f*|det|/24 (tets) or f*|A2|/6 (triangles)
   const double s_coef = (nv == 4) ? coef / 6.0 : coef / 2.0;
   const double f_meas = (nv == 4) ? f / 24.0 : f / 6.0;
+  // row strips: the default path (AFEM_ASSEMBLY_STRIPS=0 selects the
+  // per-cell incidence kernel, a diagnostic)
+  static const bool strips_env = [] {
+    const char* e = getenv("AFEM_ASSEMBLY_STRIPS");
+    return !(e && atoi(e) == 0);
+  }();
+  if (strips_env && s.strip_ok && s.max_strip_c <= 4 &&
+      strip_tile_bytes(dimc, s.max_slice_nodes, s.max_slice_w) <= kTileLdsMax) {
+    const size_t shm_s = (size_t)strip_tile_bytes(dimc, s.max_slice_nodes, s.max_slice_w);
+    static std::map<std::pair<const void*, size_t>, int> occ_s;
+    auto launch_s = [&](const void* fn, auto kern) {
+      auto it = occ_s.find({ fn, shm_s });
+      if (it == occ_s.end()) {
+        int q = 0;
+        AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, fn, 64, shm_s));
+        it = occ_s.emplace(std::make_pair(fn, shm_s), q < 1 ? 1 : q).first;
+      }
+      const int per_cu = occ_override() > 0 ? occ_override() : it->second;
+      const int64_t waves = (int64_t)ctx.n_cu * per_cu;
+      const int64_t chunk = (s.n_slices + waves - 1) / waves;
+      const int64_t nblk = (s.n_slices + chunk - 1) / chunk;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, ctx.stream, s.n_slices, chunk,
+                         s.max_slice_nodes, s.max_slice_w, s.perm.p, s.row_ptr.p, s.strip.p, s.strip_ptr.p,
+                         s.strip_n.p, s.dslot.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p, s.snode.p,
+                         b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
+    };
+#define AFEM_STRIP_K(NV_, C_, W_) launch_s(reinterpret_cast<const void*>(&k_assemble_strip<NV_, C_, W_>), k_assemble_strip<NV_, C_, W_>)
+    const bool small = s.max_strip_c <= 2 && s.max_slice_w <= 16;
+    if (nv == 4) {
+      if (small) AFEM_STRIP_K(4, 2, 16);
+      else AFEM_STRIP_K(4, 4, 32);
+    }
+    else {
+      if (small) AFEM_STRIP_K(3, 2, 16);
+      else AFEM_STRIP_K(3, 4, 32);
+    }
+#undef AFEM_STRIP_K
+    AFEM_LAUNCHED();
+    return;
+  }
+  // register-resident incidence groups per lane / fixed write-back width
+  const int max_groups = s.max_slice_k >> 2;
+  const int prof = (max_groups <= 6 && s.max_slice_w <= 16) ? 0 : (max_groups <= 16 ? 1 : -1);
   const dim3 grid((unsigned)s.n_slices), blk(64);
-  if (bucket < 0) {
+  if (bucket < 0 || prof < 0) {
     if (nv == 4)
       hipLaunchKernelGGL(k_assemble_p1_global<4>, grid, blk, 0, ctx.stream, s.perm.p, s.row_ptr.p, s.cols.p, s.inc.p,
                          s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
@@ -696,18 +1257,41 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
     const char* e = getenv("AFEM_ASSEMBLY_ABLATION");
     return e ? atoi(e) : 0;
   }();
-#define AFEM_ASM_ARGS s.max_slice_nodes, s.max_slice_w, s.run, s.perm.p, s.row_ptr.p, s.inc.p, s.inc_slice_ptr.p, \
-                      s.inc_slice_k.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p, s.snode.p,            \
-                      b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs
-#define AFEM_ASM_LAUNCH(NV_, U_, A_) \
-  hipLaunchKernelGGL((k_assemble_p1<NV_, U_, A_>), grid, blk, shm, ctx.stream, AFEM_ASM_ARGS)
-  if (nv == 4 && bucket == 0 && abl != 0) {
+  // persistent grid: as many single-wave workgroups as the LDS tile and the
+  // registers let reside at once, each walking a contiguous chunk of slices
+  // (occupancy queried once per (kernel, LDS size); kept off the launch path)
+  static std::map<std::pair<const void*, size_t>, int> occ;
+  auto launch = [&](const void* fn, auto kern) {
+    auto it = occ.find({ fn, shm });
+    if (it == occ.end()) {
+      int q = 0;
+      AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, fn, 64, shm));
+      it = occ.emplace(std::make_pair(fn, shm), q < 1 ? 1 : q).first;
+    }
+    const int per_cu = occ_override() > 0 ? occ_override() : it->second;
+    const int64_t waves = (int64_t)ctx.n_cu * per_cu;
+    const int64_t chunk = (s.n_slices + waves - 1) / waves;
+    const int64_t nblk = (s.n_slices + chunk - 1) / chunk;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm, ctx.stream, s.n_slices, chunk,
+                       s.max_slice_nodes, s.max_slice_w, s.inc_pad_off, s.perm.p, s.row_ptr.p, s.inc.p,
+                       s.inc_slice_ptr.p, s.inc_slice_k.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p,
+                       s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
+  };
+#define AFEM_ASM_K(NV_, U_, G_, W_, A_) launch(reinterpret_cast<const void*>(&k_assemble_p1<NV_, U_, G_, W_, A_>), k_assemble_p1<NV_, U_, G_, W_, A_>)
+#define AFEM_ASM_LAUNCH(NV_, U_, A_)            \
+  do {                                          \
+    if (prof == 0) AFEM_ASM_K(NV_, U_, 6, 16, A_); \
+    else AFEM_ASM_K(NV_, U_, 16, 32, A_);          \
+  } while (0)
+  if (nv == 4 && bucket == 0 && abl != 0 && prof == 0) {
     switch (abl) {
-      case 1: AFEM_ASM_LAUNCH(4, 257, 1); break;
-      case 2: AFEM_ASM_LAUNCH(4, 257, 2); break;
-      case 3: AFEM_ASM_LAUNCH(4, 257, 3); break;
-      case 4: AFEM_ASM_LAUNCH(4, 257, 4); break;
-      default: AFEM_ASM_LAUNCH(4, 257, 5);
+      case 1: AFEM_ASM_K(4, 257, 6, 16, 1); break;
+      case 2: AFEM_ASM_K(4, 257, 6, 16, 2); break;
+      case 3: AFEM_ASM_K(4, 257, 6, 16, 3); break;
+      case 4: AFEM_ASM_K(4, 257, 6, 16, 4); break;
+      case 5: AFEM_ASM_K(4, 257, 6, 16, 5); break;
+      case 6: AFEM_ASM_K(4, 257, 6, 16, 6); break;
+      default: AFEM_ASM_K(4, 257, 6, 16, 7);
     }
   }
   else if (nv == 4) {
@@ -726,8 +1310,8 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
       default: AFEM_ASM_LAUNCH(3, 2049, 0);
     }
   }
+#undef AFEM_ASM_K
 #undef AFEM_ASM_LAUNCH
-#undef AFEM_ASM_ARGS
   AFEM_LAUNCHED();
 }
 

@@ -302,7 +302,7 @@ __global__ void k_times64(int64_t n, const int32_t* __restrict__ w, int64_t* __r
 
 __global__ void k_slice_max(int64_t n_slices, const int32_t* __restrict__ perm, const int64_t* __restrict__ row_ptr,
                             const int32_t* __restrict__ slice_w, const int64_t* __restrict__ slice_nu,
-                            unsigned long long* __restrict__ out)
+                            const int32_t* __restrict__ slice_k, unsigned long long* __restrict__ out)
 {
   int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_slices) return;
@@ -314,6 +314,206 @@ __global__ void k_slice_max(int64_t n_slices, const int32_t* __restrict__ perm, 
   atomicMax(&out[0], seg);
   atomicMax(&out[1], (unsigned long long)slice_w[s]);
   atomicMax(&out[2], (unsigned long long)slice_nu[s]);
+  atomicMax(&out[3], (unsigned long long)slice_k[s]);
+}
+
+// ---------------------------------------------------------------- row strips
+// Around a row node r the incident cells form a star; its link is a
+// triangulated surface (tets: triangles of the other three nodes) or a path /
+// cycle (triangles: edges of the other two nodes).  A strip orders cells so
+// that consecutive ones share a face through r: the window of the last NV-1
+// other nodes advances by ONE new node per cell, either dropping its oldest
+// node ("shift", kind 0) or its middle one ("swap", kind 1).  The assembly
+// kernel then gathers one node per cell instead of NV-1 and reuses one
+// cofactor (cross product) of the previous cell.  Stream byte = slot (6 bits,
+// position of the node in the row's columns) | kind << 6; kind 2 = priming
+// node (window fill at a strip start, no cell), kind 3 = padding (slot = the
+// row's diagonal: a zero vector, no cell).
+// Greedy cover (deterministic): start at the unvisited link triangle with the
+// fewest unvisited neighbours, try the NV-1 choices of the "newest" node,
+// extend with the candidate having the fewest unvisited neighbours (shift
+// before swap), keep the longest extension.  Kuhn boxes: one strip per row
+// (steps = cells + 2); unstructured golden meshes: 1.1-1.25 steps per cell.
+constexpr int kStripMaxCells = 64;  // link elements per row (64-bit masks)
+constexpr int kStripMaxSlots = 64;  // 6-bit slots
+
+struct StripScratch {
+  uint64_t mask[kStripMaxCells];  // slots of each link element
+  uint64_t adj[kStripMaxCells];   // link elements sharing NV-2 slots (an edge / a node)
+  uint8_t sl[kStripMaxCells][3];
+};
+
+// greedy extension from window (w0,w1,w2) [tets] / (w1,w2) [triangles] over `unv`;
+// returns the number of cells appended; emits bytes if out != nullptr
+__device__ int strip_extend(const StripScratch& S, int k, int cur, uint64_t unv, int w0, int w1, int w2,
+                            uint8_t* out, uint64_t* unv_out)
+{
+  int n = 0;
+  for (;;) {
+    uint64_t cand = S.adj[cur] & unv;
+    int best = -1, best_kind = 0, best_key = 1 << 30;
+    while (cand) {
+      const int u = __ffsll((long long)cand) - 1;
+      cand &= cand - 1;
+      const uint64_t mu = S.mask[u];
+      int kind = -1;
+      if (k == 3) {
+        if ((mu >> w1 & 1) && (mu >> w2 & 1)) kind = 0;
+        else if ((mu >> w0 & 1) && (mu >> w2 & 1)) kind = 1;
+      }
+      else {
+        if (mu >> w2 & 1) kind = 0;
+        else if (mu >> w1 & 1) kind = 1;
+      }
+      if (kind < 0) continue;
+      const int key = (__popcll(S.adj[u] & unv & ~(1ull << u)) << 3) | (kind << 2);
+      if (key < best_key) {
+        best_key = key;
+        best = u;
+        best_kind = kind;
+      }
+    }
+    if (best < 0) break;
+    unv &= ~(1ull << best);
+    // the new node: the element's slot not in the kept part of the window
+    int d = -1;
+    for (int a = 0; a < k; ++a) {
+      const int x = S.sl[best][a];
+      const bool kept = (k == 3) ? (best_kind == 0 ? (x == w1 || x == w2) : (x == w0 || x == w2))
+                                 : (best_kind == 0 ? x == w2 : x == w1);
+      if (!kept) d = x;
+    }
+    if (out) out[n] = (uint8_t)(d | (best_kind << 6));
+    ++n;
+    if (k == 3) {
+      if (best_kind == 0) w0 = w1;
+      w1 = w2;
+      w2 = d;
+    }
+    else {
+      if (best_kind == 0) w1 = w2;
+      w2 = d;
+    }
+    cur = best;
+  }
+  if (unv_out) *unv_out = unv;
+  return n;
+}
+
+// One thread per processing position.  WRITE = false: stream length (or -1
+// when the row does not fit the 6-bit slot / 64-cell limits); WRITE = true:
+// the stream into the sliced layout (16 steps per 16-B chunk per lane) and
+// the row's diagonal slot.
+template <bool WRITE>
+__global__ __launch_bounds__(64) void k_strip_rows(int64_t n_pos, int nv, const int32_t* __restrict__ perm,
+                                                   const int32_t* __restrict__ cn, const int64_t* __restrict__ nc_ptr,
+                                                   const int32_t* __restrict__ nc, const int64_t* __restrict__ row_ptr,
+                                                   const int32_t* __restrict__ cols, int32_t* __restrict__ strip_len,
+                                                   const int64_t* __restrict__ strip_ptr,
+                                                   const int32_t* __restrict__ strip_c, uint8_t* __restrict__ strip,
+                                                   uint8_t* __restrict__ dslot_out)
+{
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pos) return;
+  const int64_t sl = p >> 6;
+  const int lane = (int)(p & 63);
+  const int32_t r = perm[p];
+  const int k = nv - 1;
+  int total = 0;
+  int dslot = 0;
+  uint8_t buf[2 * kStripMaxCells + 16];
+  if (r >= 0) {
+    const int32_t* c = cols + row_ptr[r];
+    const int len = (int)(row_ptr[r + 1] - row_ptr[r]);
+    const int64_t b = nc_ptr[r];
+    const int T = (int)(nc_ptr[r + 1] - b);
+    dslot = find_slot(c, len, r);
+    if (len > kStripMaxSlots || T > kStripMaxCells) {
+      if (!WRITE) strip_len[p] = -1;
+      return;
+    }
+    StripScratch S;
+    for (int t = 0; t < T; ++t) {
+      const int32_t* nodes = cn + (int64_t)nc[b + t] * nv;
+      uint64_t m = 0;
+      int o = 0;
+      for (int a = 0; a < nv; ++a) {
+        const int32_t x = nodes[a];
+        if (x == r) continue;
+        const int sx = find_slot(c, len, x);
+        S.sl[t][o++] = (uint8_t)sx;
+        m |= 1ull << sx;
+      }
+      S.mask[t] = m;
+    }
+    for (int t = 0; t < T; ++t) {
+      uint64_t a = 0;
+      for (int u = 0; u < T; ++u)
+        if (u != t && __popcll(S.mask[t] & S.mask[u]) == k - 1) a |= 1ull << u;
+      S.adj[t] = a;
+    }
+    uint64_t unv = T == 64 ? ~0ull : ((1ull << T) - 1);
+    while (unv) {
+      // start: fewest unvisited neighbours
+      int t0 = -1, bk = 1 << 30;
+      for (uint64_t q = unv; q; q &= q - 1) {
+        const int t = __ffsll((long long)q) - 1;
+        const int key = __popcll(S.adj[t] & unv);
+        if (key < bk) {
+          bk = key;
+          t0 = t;
+        }
+      }
+      unv &= ~(1ull << t0);
+      // orientation: which node is the newest (must be in the next shared face)
+      int best_rot = 0, best_n = -1;
+      for (int rot = 0; rot < k; ++rot) {
+        int w[3];
+        for (int a = 0; a < k; ++a) w[a] = S.sl[t0][(a + rot) % k];
+        const int n = k == 3 ? strip_extend(S, k, t0, unv, w[0], w[1], w[2], nullptr, nullptr)
+                             : strip_extend(S, k, t0, unv, 0, w[0], w[1], nullptr, nullptr);
+        if (n > best_n) {
+          best_n = n;
+          best_rot = rot;
+        }
+      }
+      int w[3];
+      for (int a = 0; a < k; ++a) w[a] = S.sl[t0][(a + best_rot) % k];
+      // priming nodes (kind 2) then the start cell (kind 0: shift, emit)
+      for (int a = 0; a < k - 1; ++a) buf[total++] = (uint8_t)(w[a] | (2 << 6));
+      buf[total++] = (uint8_t)w[k - 1];
+      const int n = k == 3 ? strip_extend(S, k, t0, unv, w[0], w[1], w[2], buf + total, &unv)
+                           : strip_extend(S, k, t0, unv, 0, w[0], w[1], buf + total, &unv);
+      total += n;
+    }
+  }
+  if (!WRITE) {
+    strip_len[p] = total;
+    return;
+  }
+  dslot_out[p] = (uint8_t)dslot;
+  uint8_t* out = strip + strip_ptr[sl] + lane * 16;
+  const int steps = 16 * strip_c[sl];
+  for (int j = 0; j < steps; ++j) out[(int64_t)(j >> 4) * 1024 + (j & 15)] = j < total ? buf[j] : (uint8_t)(dslot | (3 << 6));
+}
+
+// per slice: 16-step chunks (max stream length over its lanes) and bytes
+__global__ void k_strip_width(int64_t n_slices, const int32_t* __restrict__ strip_len, int32_t* __restrict__ strip_c,
+                              int32_t* __restrict__ strip_n, int64_t* __restrict__ sz, int32_t* __restrict__ flags)
+{
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_slices) return;
+  int w = 0;
+  for (int l = 0; l < 64; ++l) {
+    const int v = strip_len[s * 64 + l];
+    if (v < 0) atomicOr(&flags[0], 1);
+    w = v > w ? v : w;
+  }
+  const int c = (w + 15) >> 4;
+  strip_c[s] = c;
+  strip_n[s] = w;
+  sz[s] = (int64_t)c * 1024;
+  atomicMax(&flags[1], c);
 }
 
 }  // namespace
@@ -419,7 +619,9 @@ void build_structure(Mesh& m, Structure& s)
   s.inc_slice_ptr.alloc(s.n_slices + 1);
   exclusive_scan_i64(ctx, slice_sz.p, s.inc_slice_ptr.p, s.n_slices);
   const int64_t inc_total = read_i64(ctx, s.inc_slice_ptr.p + s.n_slices);
-  s.inc.alloc(inc_total > 0 ? inc_total : 1);
+  s.inc.alloc(inc_total + 256);
+  s.inc_pad_off = inc_total;
+  AFEM_HIP(hipMemsetAsync(s.inc.p + inc_total, 0xFF, 256 * sizeof(uint32_t), ctx.stream));
   hipLaunchKernelGGL(k_fill_inc, dim3(grid_for(n_pos, 256)), dim3(256), 0, ctx.stream, n_pos, nv, s.perm.p,
                      m.cell_node.p, nc_ptr.p, nc.p, s.row_ptr.p, s.cols.p, s.inc_slice_ptr.p, s.inc_slice_k.p, s.inc.p);
   AFEM_LAUNCHED();
@@ -450,17 +652,58 @@ void build_structure(Mesh& m, Structure& s)
   AFEM_LAUNCHED();
   {
     DevBuf<unsigned long long> mx;
-    mx.alloc(3);
+    mx.alloc(4);
     AFEM_HIP(hipMemsetAsync(mx.p, 0, mx.bytes(), ctx.stream));
     hipLaunchKernelGGL(k_slice_max, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, s.n_slices, s.perm.p,
-                       s.row_ptr.p, s.slice_w.p, slice_nu.p, mx.p);
+                       s.row_ptr.p, s.slice_w.p, slice_nu.p, s.inc_slice_k.p, mx.p);
     AFEM_LAUNCHED();
-    unsigned long long hm[3] = { 0, 0, 0 };
+    unsigned long long hm[4] = { 0, 0, 0, 0 };
     AFEM_HIP(hipMemcpyAsync(hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
     ctx.sync();
     s.max_wave_seg = (int64_t)hm[0];
     s.max_slice_w = (int)hm[1];
     s.max_slice_nodes = (int)hm[2];
+    s.max_slice_k = (int)hm[3];
+  }
+
+  // 6. row strips (the scalar assembly's cell order and node stream)
+  {
+    DevBuf<int32_t> slen;
+    slen.alloc(n_pos);
+    hipLaunchKernelGGL(k_strip_rows<false>, dim3(grid_for(n_pos, 64)), dim3(64), 0, ctx.stream, n_pos, nv, s.perm.p,
+                       m.cell_node.p, nc_ptr.p, nc.p, s.row_ptr.p, s.cols.p, slen.p, nullptr, nullptr, nullptr,
+                       nullptr);
+    AFEM_LAUNCHED();
+    s.strip_c.alloc(s.n_slices);
+    s.strip_n.alloc(s.n_slices);
+    DevBuf<int64_t> ssz;
+    ssz.alloc(s.n_slices);
+    DevBuf<int32_t> sflags;
+    sflags.alloc(2);
+    AFEM_HIP(hipMemsetAsync(sflags.p, 0, sflags.bytes(), ctx.stream));
+    hipLaunchKernelGGL(k_strip_width, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, s.n_slices, slen.p,
+                       s.strip_c.p, s.strip_n.p, ssz.p, sflags.p);
+    AFEM_LAUNCHED();
+    int32_t hf[2] = { 0, 0 };
+    AFEM_HIP(hipMemcpyAsync(hf, sflags.p, sizeof(hf), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    s.strip_ok = hf[0] == 0;
+    s.max_strip_c = hf[1];
+    if (s.strip_ok) {
+      s.strip_ptr.alloc(s.n_slices + 1);
+      exclusive_scan_i64(ctx, ssz.p, s.strip_ptr.p, s.n_slices);
+      const int64_t nbytes = read_i64(ctx, s.strip_ptr.p + s.n_slices);
+      s.strip.alloc(nbytes + 1024);
+      s.dslot.alloc(n_pos);
+      hipLaunchKernelGGL(k_strip_rows<true>, dim3(grid_for(n_pos, 64)), dim3(64), 0, ctx.stream, n_pos, nv,
+                         s.perm.p, m.cell_node.p, nc_ptr.p, nc.p, s.row_ptr.p, s.cols.p, nullptr, s.strip_ptr.p,
+                         s.strip_c.p, s.strip.p, s.dslot.p);
+      AFEM_LAUNCHED();
+    }
+    else {
+      s.strip_c.reset();
+      s.strip_n.reset();
+    }
   }
   ctx.sync();
 }

@@ -219,7 +219,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_assemble_p1<4,true>",
+                "kernel": "k_assemble_strip<4,2,16>",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
