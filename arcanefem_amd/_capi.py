@@ -86,6 +86,9 @@ SIGNATURES = {
     "afem_bsr_compute_sparsity": [P],
     "afem_bsr_assemble_poisson_p1": [P, D, D, P],
     "afem_bsr_assemble_elasticity_p1": [P, D, D],
+    "afem_bsr_assemble_elasticity_p1_ex": [P, D, D, D, P, P],
+    "afem_vec_lincomb": [P, I64, D, P, D, P, D, P, P],
+    "afem_newmark_update": [P, I64, D, D, D, P, P, P, P],
     "afem_bsr_reset_values": [P],
     "afem_bsr_set_value": [P, I32, I32, D],
     "afem_bsr_get_value": [P, I32, I32, ctypes.POINTER(D)],

@@ -177,6 +177,17 @@ class BSRFormat:
     def assembleElasticityP1(self, lam: float, mu2: float):
         call("afem_bsr_assemble_elasticity_p1", self.h, lam, mu2)
 
+    def assembleElasticityP1Ex(self, lam: float, mu2: float, mass_coef: float = 0.0, body_force=None,
+                               rhs_dptr: int | None = None):
+        """Block-3 tetrahedra: lambda/mu2 stiffness + mass_coef * consistent mass
+        (Newmark LHS c0 M + K) and, with body_force (3 floats), the vectorial
+        constant source into rhs_dptr (3 per owned node)."""
+        f = None
+        if body_force is not None:
+            f = (ctypes.c_double * 3)(*[float(x) for x in body_force])
+        call("afem_bsr_assemble_elasticity_p1_ex", self.h, lam, mu2, mass_coef, f,
+             ctypes.c_void_p(rhs_dptr) if rhs_dptr else None)
+
     def resetMatrixValues(self):
         call("afem_bsr_reset_values", self.h)
 

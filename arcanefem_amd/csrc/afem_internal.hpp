@@ -216,6 +216,7 @@ int64_t read_i64(Ctx& ctx, const int64_t* d);
 void build_structure(Mesh& m, Structure& s);
 void assemble_scalar(Bsr& b, double coef, double f, double* rhs);
 void assemble_elasticity_tri(Bsr& b, double lambda, double mu2);
+void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const double* f, double* rhs);
 bool assembly_uses_lds(const Bsr& b);  // slice tile fits the LDS budget
 
 void ls_apply_bcs(LinearSystem& ls);
@@ -240,6 +241,11 @@ bool bsr_point(Bsr& b, int32_t row, int32_t col, int op, double v, double* out);
 // per-row layout is already CSR order, the per-block one is permuted into
 // `vals_out` (device, nnz*k^2).
 void bsr_expand_scalar(Bsr& b, double* vals_out);
+
+void vec_lincomb(Ctx& ctx, int64_t n, double a, const double* x, double b, const double* y, double c, const double* z,
+                 double* out);
+void newmark_update(Ctx& ctx, int64_t n, double dt, double beta, double gamma, const double* un, double* u, double* v,
+                    double* a);
 
 void comm_unique_id(uint8_t* out);
 Comm* comm_create(Ctx& ctx, const uint8_t* id, int nranks, int rank);

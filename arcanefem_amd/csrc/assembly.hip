@@ -906,6 +906,143 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, int6
   }
 }
 
+// ---------------------------------------------------------------- block-3 elasticity (TETRA4), row strips
+// K_rb^{ij} = [lambda c_r,i c_b,j + mu (c_r,j c_b,i + delta_ij c_r.c_b)] / (6|det|)
+// (+ c0 |det|/120 delta_ij, the consistent mass V/20 (1 + delta_rb) for b != r):
+// the 3D form of computeElementMatrixTRIA3Base (modules/elasticity/FemModule.h:112-140),
+// restated in oracle/oracle.c orc_element_elasticity_tet4.  One wave per
+// (slice, component row i): it walks the slice's row strips exactly like the
+// scalar kernel and accumulates the three entries (i, j=0..2) of every
+// block of its 64 rows in LDS [slot][j][lane].  Diagonal blocks: rigid
+// translations are in the nullspace, so K_rr = -sum_{b != r} K_rb; the mass
+// part (row sum V/4, diagonal V/10) is restored from the row's measure sum.
+// Body force f (vectorial constant source, femutils/ArcaneFemFunctionsGpu.h:514-586):
+// rhs[3r+i] = f_i |K|/4, fused.
+template <int MAXW>
+__global__ __launch_bounds__(64) void k_assemble_elast_tet(int u_cap, int w_cap, bool per_block,
+                                                           const int32_t* __restrict__ perm,
+                                                           const int64_t* __restrict__ row_ptr,
+                                                           const uint8_t* __restrict__ strip,
+                                                           const int64_t* __restrict__ strip_ptr,
+                                                           const int32_t* __restrict__ strip_n,
+                                                           const uint8_t* __restrict__ dslots,
+                                                           const int32_t* __restrict__ slice_w,
+                                                           const int64_t* __restrict__ lidx_ptr,
+                                                           const uint16_t* __restrict__ lidx,
+                                                           const int64_t* __restrict__ snode_ptr,
+                                                           const int32_t* __restrict__ snode,
+                                                           const double* __restrict__ coords, double lambda, double mu,
+                                                           double c0, double fx, double fy, double fz,
+                                                           double* __restrict__ vals, double* __restrict__ rhs)
+{
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* acc = reinterpret_cast<double*>(smem);  // [slot][j][lane]
+  double* cxyz = reinterpret_cast<double*>(smem + 3 * 8 * 64 * (int64_t)w_cap);
+  uint16_t* li = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(cxyz) +
+                                             ((24 * (int64_t)u_cap + 15) & ~int64_t(15)));
+  const int lane = threadIdx.x;
+  const int64_t sl = blockIdx.x / 3;
+  const int ci = (int)(blockIdx.x % 3);  // component row of this wave (uniform)
+  const int32_t row = perm[sl * 64 + lane];
+  const bool active = row >= 0;
+  const int64_t rb = active ? row_ptr[row] : 0;
+  const int len = active ? (int)(row_ptr[row + 1] - rb) : 0;
+  const V3 xi = ld3(coords, active ? row : 0);
+  const uint32_t dslot = dslots[sl * 64 + lane];
+  const int W = slice_w[sl];
+  const int nsteps = strip_n[sl];
+  // stage coordinates (AoS), column-index table, zero accumulators
+  {
+    const int64_t u0 = snode_ptr[sl];
+    const int nu = (int)(snode_ptr[sl + 1] - u0);
+    for (int u = lane; u < nu; u += 64) {
+      const int64_t n = snode[u0 + u];
+      cxyz[3 * u] = coords[3 * n];
+      cxyz[3 * u + 1] = coords[3 * n + 1];
+      cxyz[3 * u + 2] = coords[3 * n + 2];
+    }
+    const int nq = 8 * W;
+    const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + lidx_ptr[sl]);
+    u32x4* dst = reinterpret_cast<u32x4*>(li);
+    for (int q = lane; q < nq; q += 64) dst[q] = ls[q];
+    double2* a2 = reinterpret_cast<double2*>(acc);
+    for (int q = lane; q < 96 * W; q += 64) a2[q] = make_double2(0.0, 0.0);
+  }
+  wave_sync_lds();
+
+  const double* comp_sel = nullptr;
+  (void)comp_sel;
+  double macc = 0.0;
+  V3 eP{ 0.0, 0.0, 0.0 }, eQ{ 0.0, 0.0, 0.0 }, eR{ 0.0, 0.0, 0.0 };
+  V3 cP{ 0.0, 0.0, 0.0 }, cN{ 0.0, 0.0, 0.0 };
+  double* const acc_lane = acc + lane;
+  double* aP = acc_lane + 192 * dslot;
+  double* aQ = aP;
+  double* aR = aP;
+  const uint16_t* lrow = li + lane;
+  const u32x4* sp = reinterpret_cast<const u32x4*>(strip + strip_ptr[sl]) + lane;
+  auto comp = [ci](V3 v) { return ci == 0 ? v.x : (ci == 1 ? v.y : v.z); };
+  auto sel = [](bool c, V3 a, V3 b) { return V3{ c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z }; };
+  auto keep = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
+  auto block = [&](double* a, V3 m, V3 cb, double s, double mass) {
+    // entries (ci, j) of K_rb with c_r = -m (sign folded into s < 0)
+    const double t = dot(m, cb);
+    const double A = lambda * comp(m), B = mu * comp(cb);
+    double v0 = (A * cb.x + B * m.x) * s, v1 = (A * cb.y + B * m.y) * s, v2 = (A * cb.z + B * m.z) * s;
+    const double dg = mu * t * s + mass;
+    if (ci == 0) v0 += dg;
+    else if (ci == 1) v1 += dg;
+    else v2 += dg;
+    atomicAdd(a, v0);
+    atomicAdd(a + 64, v1);
+    atomicAdd(a + 128, v2);
+  };
+  for (int c = 0; 16 * c < nsteps; ++c) {
+    const u32x4 w = sp[(int64_t)c * 64];
+    const uint32_t wv[4] = { w.x, w.y, w.z, w.w };
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t byte = (wv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      const bool swap = (byte & 0xC0u) == 0x40u;
+      const uint64_t em = (uint64_t)0 - (uint64_t)(byte < 0x80u);
+      double* const aD = acc_lane + 192 * (byte & 63u);
+      const double* q = cxyz + 3 * (int)lrow[(byte & 63u) * 64];
+      const V3 eD = sub(V3{ q[0], q[1], q[2] }, xi);
+      const V3 cRn = sel(swap, cN, cP);
+      eP = sel(swap, eP, eQ);
+      aP = swap ? aP : aQ;
+      eQ = eR;
+      aQ = aR;
+      eR = eD;
+      aR = aD;
+      cP = cross(eQ, eR);
+      cN = cross(eP, eR);
+      const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
+      const double meas = fabs(dot(eP, cP));
+      const double s = keep(em, -recip1(6.0 * meas));
+      const double mass = keep(em, c0 * meas * (1.0 / 120.0));
+      macc += keep(em, meas);
+      block(aP, m, cP, s, mass);
+      block(aQ, m, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+      block(aR, m, cRn, s, mass);
+    }
+  }
+  if (rhs && active) rhs[3 * (int64_t)row + ci] = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
+  wave_sync_lds();
+  // diagonal block row ci, then the row's 3*len values
+  if (active) {
+    double sum[3] = { 0.0, 0.0, 0.0 };
+    for (int t = 0; t < len; ++t)
+      if (t != (int)dslot)
+        for (int jj = 0; jj < 3; ++jj) sum[jj] += acc_lane[192 * t + 64 * jj];
+    for (int jj = 0; jj < 3; ++jj)
+      acc_lane[192 * dslot + 64 * jj] = -sum[jj] + (jj == ci ? c0 * macc * (1.0 / 24.0) : 0.0);
+    for (int t = 0; t < len; ++t)
+      for (int jj = 0; jj < 3; ++jj)
+        vals[per_block ? (rb + t) * 9 + 3 * ci + jj : rb * 9 + (int64_t)ci * 3 * len + 3 * t + jj] =
+          acc_lane[192 * t + 64 * jj];
+  }
+}
+
 // Global-memory variant for rows too long for the LDS tile: coordinates
 // gathered through the columns, accumulation in place (lane-owned rows).
 template <int NV>
@@ -1325,6 +1462,25 @@ bool assembly_uses_lds(const Bsr& b)
     return false;
   }
   return tile_bytes(dimc, nacc, b.s.max_slice_nodes, b.s.max_slice_w) <= kTileLdsMax;
+}
+
+void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const double* f, double* rhs)
+{
+  Structure& s = b.s;
+  Ctx& ctx = *b.mesh->ctx;
+  AFEM_REQUIRE(b.nb_dof == 3 && b.mesh->nv == 4, AFEM_ERR_NOT_IMPL,
+               "block-3 P1 elasticity assembly needs NB_DOF = 3 on tetrahedra");
+  AFEM_REQUIRE(s.strip_ok, AFEM_ERR_NOT_IMPL,
+               "block-3 elasticity assembly needs row strips (rows of at most 64 blocks and 64 incident cells)");
+  const int64_t shm = 3 * 8 * 64 * (int64_t)s.max_slice_w + ((24 * (int64_t)s.max_slice_nodes + 15) & ~int64_t(15)) +
+                      2 * 64 * (int64_t)s.max_slice_w;
+  AFEM_REQUIRE(shm <= 160 * 1024, AFEM_ERR_LIMIT, "block-3 slice tile exceeds the LDS of a CU");
+  const double fx = f ? f[0] : 0.0, fy = f ? f[1] : 0.0, fz = f ? f[2] : 0.0;
+  hipLaunchKernelGGL(k_assemble_elast_tet<16>, dim3((unsigned)(3 * s.n_slices)), dim3(64), (size_t)shm, ctx.stream,
+                     s.max_slice_nodes, s.max_slice_w, b.order_per_block, s.perm.p, s.row_ptr.p, s.strip.p,
+                     s.strip_ptr.p, s.strip_n.p, s.dslot.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p,
+                     s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr);
+  AFEM_LAUNCHED();
 }
 
 void assemble_elasticity_tri(Bsr& b, double lambda, double mu2)

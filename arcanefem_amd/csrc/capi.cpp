@@ -389,7 +389,24 @@ int afem_bsr_assemble_elasticity_p1(afem_bsr* b, double lambda, double mu2)
   NOT_NULL(b);
   AFEM_REQUIRE(b->has_sparsity, AFEM_ERR_STATE, "assembleBilinear called before computeSparsity");
   b->mesh->ctx->set_device();
-  assemble_elasticity_tri(*b, lambda, mu2);
+  if (b->mesh->nv == 4)
+    assemble_elasticity_tet(*b, lambda, mu2, 0.0, nullptr, nullptr);
+  else
+    assemble_elasticity_tri(*b, lambda, mu2);
+  API_END
+}
+
+int afem_bsr_assemble_elasticity_p1_ex(afem_bsr* b, double lambda, double mu2, double mass_coef, const double* body_force,
+                                       double* rhs)
+{
+  API_BEGIN
+  NOT_NULL(b);
+  AFEM_REQUIRE(b->has_sparsity, AFEM_ERR_STATE, "assembleBilinear called before computeSparsity");
+  AFEM_REQUIRE(b->mesh->nv == 4 && b->nb_dof == 3, AFEM_ERR_NOT_IMPL,
+               "the mass / body-force form is implemented for NB_DOF = 3 on tetrahedra");
+  AFEM_REQUIRE(!body_force || rhs, AFEM_ERR_ARG, "body_force given without an rhs array");
+  b->mesh->ctx->set_device();
+  assemble_elasticity_tet(*b, lambda, mu2, mass_coef, body_force, rhs);
   API_END
 }
 
@@ -843,6 +860,29 @@ int afem_ls_spmv(afem_ls* ls, const double* x, double* y)
   NOT_NULL(y);
   ls->ctx->set_device();
   ls_spmv(*ls, x, y);
+  API_END
+}
+
+int afem_vec_lincomb(afem_ctx* ctx, int64_t n, double a, const double* x, double b, const double* y, double c,
+                     const double* z, double* out)
+{
+  API_BEGIN
+  NOT_NULL(ctx);
+  AFEM_REQUIRE(n == 0 || (x && y && out), AFEM_ERR_ARG, "afem_vec_lincomb: x, y and out must not be NULL");
+  ctx->set_device();
+  vec_lincomb(*ctx, n, a, x, b, y, c, z, out);
+  API_END
+}
+
+int afem_newmark_update(afem_ctx* ctx, int64_t n, double dt, double beta, double gamma, const double* u_new, double* u,
+                        double* v, double* a)
+{
+  API_BEGIN
+  NOT_NULL(ctx);
+  AFEM_REQUIRE(n == 0 || (u_new && u && v && a), AFEM_ERR_ARG, "afem_newmark_update: NULL state array");
+  AFEM_REQUIRE(dt > 0.0 && beta > 0.0, AFEM_ERR_ARG, "afem_newmark_update: dt and beta must be positive");
+  ctx->set_device();
+  newmark_update(*ctx, n, dt, beta, gamma, u_new, u, v, a);
   API_END
 }
 

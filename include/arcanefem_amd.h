@@ -155,6 +155,16 @@ int afem_bsr_assemble_poisson_p1(afem_bsr* bsr, double coef, double f, double* r
 /* Block-2 P1 elasticity on triangles (modules/elasticity/FemModule.h:112-140),
  * mu2 = 2*mu, lambda as in modules/elasticity/FemModule.cc:130-134. */
 int afem_bsr_assemble_elasticity_p1(afem_bsr* bsr, double lambda, double mu2);
+/* Block-3 P1 elasticity on tetrahedra (the 3D form of the same bilinear form;
+ * no reference module) plus mass_coef * consistent mass (the
+ * c0 term of the Newmark / generalized-alpha LHS,
+ * modules/elastodynamics/FemModule.cc:259,1285-1340) and, if body_force
+ * (3 doubles, host) is given, the vectorial constant source
+ * rhs[3n+i] = f_i |K| / 4 on owned nodes (femutils/ArcaneFemFunctionsGpu.h:514-586;
+ * rhs: device, 3*n_own). afem_bsr_assemble_elasticity_p1 on a tetrahedral
+ * block-3 matrix is this call with mass_coef = 0 and no body force. */
+int afem_bsr_assemble_elasticity_p1_ex(afem_bsr* bsr, double lambda, double mu2, double mass_coef,
+                                       const double* body_force, double* rhs);
 int afem_bsr_reset_values(afem_bsr* bsr);                       /* resetMatrixValues */
 int afem_bsr_set_value(afem_bsr* bsr, int32_t row, int32_t col, double v); /* BSRMatrix::setValue */
 int afem_bsr_get_value(afem_bsr* bsr, int32_t row, int32_t col, double* v); /* BSRMatrix::getValue */
@@ -264,6 +274,18 @@ int afem_ls_solve(afem_ls* ls, afem_solve_stats* stats);
  * a communicator is attached).  Device pointers. */
 int afem_ls_spmv(afem_ls* ls, const double* x, double* y);
 int afem_ls_destroy(afem_ls* ls);
+
+/* ---- time stepping (callers of the path: modules/elastodynamics, modules/passmo) */
+/* out = a*x + b*y + c*z on device arrays of n doubles (z may be NULL): the
+ * Newmark right-hand side operand c0 U + c3 V + c4 A
+ * (modules/elastodynamics/FemModule.cc:842-862 with etam = etak = 0). */
+int afem_vec_lincomb(afem_ctx* ctx, int64_t n, double a, const double* x, double b, const double* y, double c,
+                     const double* z, double* out);
+/* Newmark-beta state update of modules/elastodynamics/FemModule.cc:429-455
+ * (_updateVariables) on device arrays: a' = (u_new-u-dt v)/(beta dt^2) -
+ * (1-2beta)/(2beta) a, v += dt((1-gamma)a + gamma a'), a = a', u = u_new. */
+int afem_newmark_update(afem_ctx* ctx, int64_t n, double dt, double beta, double gamma, const double* u_new, double* u,
+                        double* v, double* a);
 
 /* ---------------------------------------------------------------- communicator */
 #define AFEM_UNIQUE_ID_BYTES 128

@@ -304,6 +304,103 @@ int64_t orc_assemble_elasticity_tri(int64_t n_rows, int64_t n_cells, const int32
   return missing;
 }
 
+/* Block-3 P1 elasticity on tetrahedra (NB_DOF = 3).  No reference module has
+ * it (the elasticity module is 2D TRIA3); this is the 3D
+ * restatement of computeElementMatrixTRIA3Base (modules/elasticity/FemModule.h:112-140):
+ * the same bilinear form lambda*div(u)div(v) + mu2*(eps(u):eps(v)) written with
+ * the B matrix of the three normal strains and the three engineering shears
+ * (the 2D code's dx/dy rows and its 0.5*shear term), integrated exactly on the
+ * P1 tet: K = V * B^T D B with grad N_a = c_a / det, det = 6V signed.
+ * Optional consistent mass term (modules/elastodynamics/FemModule.cc:1285-1340,
+ * the TRIA3 u1v1/u2v2 blocks: area/12*(1+delta_ab); tetrahedron: V/20*(1+delta_ab))
+ * scaled by c0 (rho/(beta dt^2) in the Newmark LHS, :259).  Interleaved dofs
+ * [u1x,u1y,u1z,u2x,...], 12x12 row-major. */
+void orc_element_elasticity_tet4(const double* xyz, double lambda, double mu2, double c0, double* K /* [144] */)
+{
+  const double *m0 = xyz, *m1 = xyz + 3, *m2 = xyz + 6, *m3 = xyz + 9;
+  double e[3][3];
+  for (int d = 0; d < 3; ++d) {
+    e[0][d] = m1[d] - m0[d];
+    e[1][d] = m2[d] - m0[d];
+    e[2][d] = m3[d] - m0[d];
+  }
+  /* cofactors: c1 = e2 x e3, c2 = e3 x e1, c3 = e1 x e2, c0 = -(c1+c2+c3); det = e1.c1 */
+  double c[4][3];
+  const int A[3] = { 1, 2, 0 }, B[3] = { 2, 0, 1 };
+  for (int d = 0; d < 3; ++d) {
+    c[1][d] = e[1][A[d]] * e[2][B[d]] - e[1][B[d]] * e[2][A[d]];
+    c[2][d] = e[2][A[d]] * e[0][B[d]] - e[2][B[d]] * e[0][A[d]];
+    c[3][d] = e[0][A[d]] * e[1][B[d]] - e[0][B[d]] * e[1][A[d]];
+    c[0][d] = -(c[1][d] + c[2][d] + c[3][d]);
+  }
+  const double det = e[0][0] * c[1][0] + e[0][1] * c[1][1] + e[0][2] * c[1][2];
+  const double vol = fabs(det) / 6.0;
+  double g[4][3];
+  for (int a = 0; a < 4; ++a)
+    for (int d = 0; d < 3; ++d)
+      g[a][d] = c[a][d] / det;
+  /* B: 6 strain rows (xx, yy, zz, xy, yz, zx engineering) x 12 dofs */
+  double Bm[6][12];
+  for (int a = 0; a < 4; ++a) {
+    const double gx = g[a][0], gy = g[a][1], gz = g[a][2];
+    const double col[3][6] = { { gx, 0., 0., gy, 0., gz }, { 0., gy, 0., gx, gz, 0. }, { 0., 0., gz, 0., gy, gx } };
+    for (int i = 0; i < 3; ++i)
+      for (int r = 0; r < 6; ++r)
+        Bm[r][3 * a + i] = col[i][r];
+  }
+  for (int p = 0; p < 12; ++p)
+    for (int q = 0; q < 12; ++q) {
+      const double lam = (Bm[0][p] + Bm[1][p] + Bm[2][p]) * (Bm[0][q] + Bm[1][q] + Bm[2][q]);
+      const double shr = Bm[0][p] * Bm[0][q] + Bm[1][p] * Bm[1][q] + Bm[2][p] * Bm[2][q] +
+                         0.5 * (Bm[3][p] * Bm[3][q] + Bm[4][p] * Bm[4][q] + Bm[5][p] * Bm[5][q]);
+      double v = vol * (lambda * lam + mu2 * shr);
+      if (c0 != 0.0 && (p % 3) == (q % 3))
+        v += c0 * vol / 20.0 * ((p / 3) == (q / 3) ? 2.0 : 1.0);
+      K[12 * p + q] = v;
+    }
+}
+
+/* Global block-3 assembly on tetrahedra (assembleBilinearOrderedPerBlock,
+ * femutils/BSRFormat.h:786-837, with NB_DOF = 3: block_index*9 + i*3 + j) and
+ * the vectorial constant source (femutils/ArcaneFemFunctionsGpu.h:514-586:
+ * rhs[3n+i] += f_i * V / 4 on owned nodes; f may be NULL). */
+int64_t orc_assemble_elasticity_tet(int64_t n_rows, int64_t n_cells, const int32_t* cell_node, const double* coords,
+                                    const int64_t* row_ptr, const int32_t* cols, double lambda, double mu2, double c0,
+                                    const double* f, double* vals, double* rhs)
+{
+  int64_t missing = 0;
+  double xyz[12], K[144];
+  for (int64_t cc = 0; cc < n_cells; ++cc) {
+    const int32_t* n = cell_node + 4 * cc;
+    for (int a = 0; a < 4; ++a)
+      for (int d = 0; d < 3; ++d)
+        xyz[3 * a + d] = coords[3 * (int64_t)n[a] + d];
+    orc_element_elasticity_tet4(xyz, lambda, mu2, c0, K);
+    const double vol = tet_volume(xyz, xyz + 3, xyz + 6, xyz + 9);
+    for (int a = 0; a < 4; ++a) {
+      const int32_t row = n[a];
+      if (row >= n_rows)
+        continue;
+      if (f && rhs)
+        for (int i = 0; i < 3; ++i)
+          rhs[3 * (int64_t)row + i] += f[i] * vol / 4.0;
+      for (int b = 0; b < 4; ++b) {
+        int64_t k = row_ptr[row], end = row_ptr[row + 1];
+        while (k < end && cols[k] != n[b])
+          ++k;
+        if (k == end) {
+          ++missing;
+          continue;
+        }
+        for (int i = 0; i < 3; ++i)
+          for (int j = 0; j < 3; ++j)
+            vals[9 * k + 3 * i + j] += K[12 * (3 * a + i) + 3 * b + j];
+      }
+    }
+  }
+  return missing;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Dirichlet via penalty: femutils/ArcaneFemFunctionsGpu.h:434-456 (forced    */
 /* info/value, rhs = P*g) then femutils/HypreDoFLinearSystem.cc:356-382       */

@@ -50,6 +50,11 @@ def lib():
         L.orc_element_tet4.argtypes = [_f64p, _f64p, ctypes.POINTER(ctypes.c_double)]
         L.orc_element_tri3.argtypes = [_f64p, _f64p, ctypes.POINTER(ctypes.c_double)]
         L.orc_element_elasticity_tri3.argtypes = [_f64p, ctypes.c_double, ctypes.c_double, _f64p]
+        L.orc_element_elasticity_tet4.argtypes = [_f64p, ctypes.c_double, ctypes.c_double, ctypes.c_double, _f64p]
+        L.orc_assemble_elasticity_tet.restype = ctypes.c_int64
+        L.orc_assemble_elasticity_tet.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _f64p, _i64p, _i32p,
+                                                  ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p,
+                                                  _f64p, ctypes.c_void_p]
         L.orc_sparsity.restype = ctypes.c_int64
         L.orc_sparsity.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _i32p, _i64p,
                                    ctypes.c_void_p]
@@ -97,6 +102,14 @@ def element_elasticity_tri3(xyz, lam, mu2):
     return K.reshape(6, 6)
 
 
+def element_elasticity_tet4(xyz, lam, mu2, c0=0.0):
+    """12x12 block-3 elasticity (+ c0 * consistent mass) of one tetrahedron."""
+    xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(4, 3)
+    K = np.zeros(144)
+    lib().orc_element_elasticity_tet4(xyz.ravel(), lam, mu2, c0, K)
+    return K.reshape(12, 12)
+
+
 # --------------------------------------------------------------------------
 # sparsity / assembly / BC / solve
 # --------------------------------------------------------------------------
@@ -136,6 +149,35 @@ def assemble_elasticity_tri(n_rows, cells, coords, row_ptr, cols, lam, mu2):
     if missing:
         raise RuntimeError(f"{missing} (row,col) blocks missing from the structure")
     return vals
+
+
+def assemble_elasticity_tet(n_rows, cells, coords, row_ptr, cols, lam, mu2, c0=0.0, f=None):
+    """Block-3 P1 elasticity (+ c0 mass) values ordered per block
+    (block*9 + i*3 + j) and the body-force RHS (3 per owned node)."""
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    coords = np.ascontiguousarray(coords, dtype=np.float64).reshape(-1, 3)
+    vals = np.zeros(9 * cols.shape[0], dtype=np.float64)
+    rhs = np.zeros(3 * n_rows, dtype=np.float64)
+    fa = None if f is None else np.ascontiguousarray(f, dtype=np.float64)
+    missing = lib().orc_assemble_elasticity_tet(n_rows, cells.shape[0], cells.ravel(), coords.ravel(), row_ptr, cols,
+                                                lam, mu2, c0, None if fa is None else fa.ctypes.data_as(ctypes.c_void_p),
+                                                vals, None if fa is None else rhs.ctypes.data_as(ctypes.c_void_p))
+    if missing:
+        raise RuntimeError(f"{missing} (row,col) blocks missing from the structure")
+    return vals, rhs
+
+
+def blocks_to_row_order_k(row_ptr, vals, k):
+    """Per-block k x k values -> the per-scalar-row (CSR / Hypre) layout
+    rb*k^2 + i*k*len + k*slot + j."""
+    out = np.empty_like(vals)
+    kk = k * k
+    for r in range(row_ptr.shape[0] - 1):
+        rb, re = int(row_ptr[r]), int(row_ptr[r + 1])
+        ln = re - rb
+        blk = vals[kk * rb:kk * re].reshape(ln, k, k)
+        out[kk * rb:kk * re] = blk.transpose(1, 0, 2).reshape(-1)
+    return out
 
 
 def blocks_to_row_order(row_ptr, vals4):
@@ -335,3 +377,42 @@ def check_node_result(values_by_uid: dict, golden: dict, eps: float, min_value: 
         if not is_nearly_equal(ref, v, eps):
             nb_error += 1
     return nb_error, max_rel
+
+
+def newmark_elastodynamics(n_nodes, cells, coords, E, nu, rho, dt, n_steps, body_force, fixed_nodes, penalty=1e30):
+    """CPU restatement of the 3D elastodynamics time loop (per-step
+    re-assembly, Newmark-beta, modules/elastodynamics/FemModule.cc:255-264
+    coefficients, :842-862 RHS with etam = etak = 0, :429-455 update) on the
+    oracle's block-3 assembly, penalty Dirichlet (diagonal set to P, rhs = P*0)
+    and a dense direct solve.  Returns U, V, A (3 per node) after n_steps."""
+    lam = E * nu / ((1 + nu) * (1 - 2 * nu))
+    mu2 = 2.0 * E / (2 * (1 + nu))
+    gamma = 0.5
+    beta = 0.25 * (gamma + 0.5) ** 2
+    c0, c3, c4 = rho / (beta * dt * dt), rho / beta / dt, rho * ((1.0 - 2.0 * beta) / 2.0 / beta)
+    rp, cols = sparsity(n_nodes, n_nodes, cells)
+    m_vals, _ = assemble_elasticity_tet(n_nodes, cells, coords, rp, cols, 0.0, 0.0, 1.0)
+    n = 3 * n_nodes
+
+    def dense(vals):
+        A = np.zeros((n, n))
+        for r in range(n_nodes):
+            for k in range(int(rp[r]), int(rp[r + 1])):
+                A[3 * r:3 * r + 3, 3 * cols[k]:3 * cols[k] + 3] += vals[9 * k:9 * k + 9].reshape(3, 3)
+        return A
+
+    M = dense(m_vals)
+    fixed = (3 * np.asarray(fixed_nodes)[:, None] + np.arange(3)[None, :]).ravel()
+    U, V, A = np.zeros(n), np.zeros(n), np.zeros(n)
+    for _ in range(n_steps):
+        k_vals, f_rhs = assemble_elasticity_tet(n_nodes, cells, coords, rp, cols, lam, mu2, c0, body_force)
+        L = dense(k_vals)
+        b = f_rhs + M @ (c0 * U + c3 * V + c4 * A)
+        L[fixed, fixed] = penalty
+        b[fixed] = penalty * 0.0
+        Un = np.linalg.solve(L, b)
+        an = (Un - U - dt * V) / beta / (dt * dt) - (1.0 - 2.0 * beta) / 2.0 / beta * A
+        V = V + dt * ((1.0 - gamma) * A + gamma * an)
+        A = an
+        U = Un
+    return U, V, A

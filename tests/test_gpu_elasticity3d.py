@@ -1,0 +1,141 @@
+"""Block-3 P1 elasticity on tetrahedra (BASELINE config C3) and its Newmark
+LHS form c0*M + K (config C5): the HIP kernel through the C ABI against the
+oracle's restatement (oracle/oracle.c orc_assemble_elasticity_tet).
+
+No reference module assembles 3D elasticity, so parity is
+against the oracle restatement of the reference's 2D element
+(modules/elasticity/FemModule.h:112-140) lifted to 3D; the restatement itself
+is pinned by known answers in tests/test_oracle_elasticity3d.py.
+Tolerance: |gpu - oracle| <= 1e-12 * max|oracle| per entry.
+"""
+import numpy as np
+import pytest
+
+import arcanefem_amd as af
+from arcanefem_amd.gmsh import read_gmsh
+from oracle import oracle as O
+
+from golden_cases import path
+
+pytestmark = pytest.mark.gpu
+
+VAL_TOL = 1e-12
+E, NU = 21e5, 0.28
+LAM = E * NU / ((1 + NU) * (1 - 2 * NU))
+MU2 = 2 * E / (2 * (1 + NU))
+
+
+def _mesh(ctx, which):
+    if which == "box":
+        return af.Mesh.structured(ctx, 3, 6)
+    if which == "sphere":
+        gm = read_gmsh(path("sphere_cut.msh"))
+        return af.Mesh.from_arrays(ctx, 3, gm.cells, gm.coords)
+    if which == "lshape":
+        gm = read_gmsh(path("L-shape-3D.msh"))
+        return af.Mesh.from_arrays(ctx, 3, gm.cells, gm.coords)
+    return af.Mesh.structured(ctx, 3, 5, nz=9, nranks=3, rank=1)
+
+
+@pytest.mark.parametrize("which", ["box", "sphere", "lshape", "slab"])
+@pytest.mark.parametrize("use_csr", [False, True])
+@pytest.mark.parametrize("c0,force", [(0.0, None), (3.7e6, (0.5, -1.0, 2.0))])
+def test_elasticity3d_assembly_parity(ctx, which, use_csr, c0, force):
+    mesh = _mesh(ctx, which)
+    bsr = af.BSRFormat(mesh, 3).initialize(use_csr)
+    bsr.computeSparsity()
+    n3 = 3 * mesh.n_own_nodes
+    drhs = ctx.malloc(8 * n3)
+    ctx.to_device(drhs, np.zeros(n3))
+    bsr.assembleElasticityP1Ex(LAM, MU2, c0, force, drhs if force else None)
+    rows, cols, vals = bsr.download()
+    rhs = ctx.to_host(drhs, n3, np.float64)
+    ctx.free(drhs)
+    cells, coords, _ = mesh.download()
+    orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+    ovals, orhs = O.assemble_elasticity_tet(mesh.n_own_nodes, cells, coords, orp, ocols, LAM, MU2, c0, force)
+    if use_csr:
+        ovals = O.blocks_to_row_order_k(orp, ovals, 3)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    err = np.abs(vals - ovals).max() / np.abs(ovals).max()
+    assert err <= VAL_TOL, f"block-3 values differ from the oracle: {err:.3e}"
+    if force:
+        assert np.abs(rhs - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+
+
+def test_elasticity3d_plain_entry_point_equals_ex(ctx):
+    mesh = af.Mesh.structured(ctx, 3, 4)
+    b1 = af.BSRFormat(mesh, 3).initialize(False)
+    b1.computeSparsity()
+    b1.assembleElasticityP1(LAM, MU2)
+    b2 = af.BSRFormat(mesh, 3).initialize(False)
+    b2.computeSparsity()
+    b2.assembleElasticityP1Ex(LAM, MU2, 0.0, None, None)
+    assert np.array_equal(b1.download()[2], b2.download()[2])
+
+
+def test_elasticity3d_rigid_modes_at_scale(ctx):
+    # size-independent property (~330k DoF): the 6 rigid-body modes are in the
+    # nullspace of the unconstrained stiffness; with the mass term, a rigid
+    # translation gives M*1 whose sum is c0 * total volume
+    mesh = af.Mesh.structured(ctx, 3, 47)
+    bsr = af.BSRFormat(mesh, 3).initialize(False)
+    bsr.computeSparsity()
+    bsr.assembleElasticityP1(LAM, MU2)
+    rows, cols, vals = bsr.download()
+    cells, coords, _ = mesh.download()
+    nb = rows.shape[0] - 1
+    rid = np.repeat(np.arange(nb), np.diff(rows))
+    blk = vals.reshape(-1, 3, 3)
+    x = coords[:nb]
+    scale = np.abs(vals).max()
+    modes = []
+    for d in range(3):
+        u = np.zeros((x.shape[0], 3))
+        u[:, d] = 1.0
+        modes.append(u)
+    for ax in range(3):
+        w = np.zeros(3)
+        w[ax] = 1.0
+        modes.append(np.cross(w, x))
+    for u in modes:
+        r = np.zeros((nb, 3))
+        np.add.at(r, rid, np.einsum("kij,kj->ki", blk, u[cols]))
+        assert np.abs(r).max() <= 1e-10 * scale * np.abs(u).max()
+    # symmetry of the block matrix: K[a,b] == K[b,a]^T
+    key = rid.astype(np.int64) * nb + cols
+    keyT = cols.astype(np.int64) * nb + rid
+    order = np.argsort(key)
+    posT = np.searchsorted(key[order], keyT)
+    assert np.abs(blk - blk[order][posT].transpose(0, 2, 1)).max() <= 1e-13 * scale
+    # mass: sum of M over all blocks of component 0 = c0 * volume (jittered box)
+    b2 = af.BSRFormat(mesh, 3).initialize(False)
+    b2.computeSparsity()
+    b2.assembleElasticityP1Ex(0.0, 0.0, 2.0, None, None)
+    m = b2.download()[2].reshape(-1, 3, 3)
+    xc = coords[cells]
+    vol = np.abs(np.linalg.det(np.stack([xc[:, 1] - xc[:, 0], xc[:, 2] - xc[:, 0], xc[:, 3] - xc[:, 0]], 1))).sum() / 6
+    assert abs(m[:, 0, 0].sum() - 2.0 * vol) <= 1e-12 * vol
+    assert np.abs(m[:, 0, 1]).max() == 0.0
+
+
+def test_elastodynamics_newmark_parity(ctx):
+    # config C5 semantics on a small box: 6 Newmark steps with per-step
+    # re-assembly of c0 M + K, clamped x=0 face, gravity-like body force
+    from arcanefem_amd.elastodynamics import Elastodynamics3D
+
+    mesh = af.Mesh.structured(ctx, 3, 3)
+    cells, coords, _ = mesh.download()
+    fixed = np.nonzero(coords[:, 0] < 0.5 / 3)[0]  # the x = 0 node layer (jitter < h/2)
+    assert fixed.size == 16
+    E_, nu_, rho, dt = 21e5, 0.28, 1.0, 1e-3
+    f = (0.0, -9.81, 1.0)
+    sim = Elastodynamics3D(ctx, mesh, E_, nu_, rho, dt, body_force=f, fixed_nodes=fixed, rtol=1e-14)
+    for _ in range(6):
+        st = sim.step()
+        assert st["converged"]
+    U, V, A = sim.state_host()
+    Uo, Vo, Ao = O.newmark_elastodynamics(mesh.n_nodes, cells, coords, E_, nu_, rho, dt, 6, f, fixed)
+    for g, o in ((U, Uo), (V, Vo), (A, Ao)):
+        assert np.abs(g - o).max() <= 1e-8 * np.abs(o).max(), np.abs(g - o).max() / np.abs(o).max()
+    sim.close()
