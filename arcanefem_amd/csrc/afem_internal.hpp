@@ -145,6 +145,7 @@ struct Structure {
   DevBuf<int32_t> strip_c;  // 16-step chunks per slice
   DevBuf<int32_t> strip_n;  // steps per slice (longest row stream)
   DevBuf<uint8_t> dslot;
+  DevBuf<unsigned long long> tickets;  // dynamic slice claiming (assembly), 8 XCD counters
   int64_t n_slices = 0;
   int64_t n_incidences = 0;  // real (non-padding) entries
   int max_row_len = 0;

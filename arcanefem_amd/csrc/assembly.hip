@@ -639,7 +639,8 @@ __host__ __device__ constexpr int64_t strip_tile_bytes(int dimc, int64_t u_cap, 
 }
 
 template <int NV, int MAXC, int MAXW>
-__global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, int64_t chunk, int u_cap, int w_cap,
+__global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsigned long long* __restrict__ tickets,
+                                                          int u_cap, int w_cap,
                                                           const int32_t* __restrict__ perm,
                                                           const int64_t* __restrict__ row_ptr,
                                                           const uint8_t* __restrict__ strip,
@@ -662,9 +663,24 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, int6
   uint16_t* li = reinterpret_cast<uint16_t*>(smem + 8 * 64 * (int64_t)w_cap + strip_coord_bytes(DIMC, u_cap, w_cap));
   int64_t* rbs = reinterpret_cast<int64_t*>(reinterpret_cast<unsigned char*>(li) + 2 * 64 * (int64_t)w_cap);
   const int lane = threadIdx.x;
-  int64_t sl = xcd_swizzle(blockIdx.x, gridDim.x) * chunk;
-  const int64_t s_end = min(sl + chunk, n_slices);
-  if (sl >= s_end) return;
+  // Dynamic slice claiming, one ticket counter per XCD (workgroups are dealt
+  // to the 8 XCDs round-robin): XCD x walks the contiguous x-th eighth of the
+  // slices, so neighbouring bricks stay in one L2; a wave claims two slices
+  // ahead so the atomic's latency hides under a whole slice of work.
+  const int xcd = (int)(blockIdx.x & 7);
+  const int64_t r0 = n_slices * xcd / 8, r1 = n_slices * (xcd + 1) / 8;
+  auto claim = [&]() -> int64_t {
+    unsigned long long t = 0;
+    if (lane == 0) t = atomicAdd(tickets + 16 * xcd, 1ull);
+    // readfirstlane: the slice index is provably wave-uniform (scalar loads,
+    // scalar branches on the slice's sizes)
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)t);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(t >> 32));
+    return r0 + (int64_t)(((uint64_t)hi << 32) | lo);
+  };
+  int64_t sl = claim();
+  if (sl >= r1) return;
+  int64_t sn = claim();
 
   auto level1 = [&](int64_t s, StripPre<MAXC>& p) {
     p.row = perm[s * 64 + lane];
@@ -701,8 +717,9 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, int6
   StripPre<MAXC> cur, nxt;
   level1(sl, cur);
   level2(cur);
-  for (; sl < s_end; ++sl) {
-    const int64_t sn = sl + 1 < s_end ? sl + 1 : sl;
+  for (;;) {
+    const int64_t sn2 = claim();              // used by the next iteration
+    const int64_t snx = sn < r1 ? sn : sl;     // prefetch target (itself when done)
     const int nsteps = strip_n[sl];  // uniform over the wave
     const int W = slice_w[sl];
     const int64_t u0 = snode_ptr[sl];
@@ -737,7 +754,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, int6
       for (int q = lane; q < 32 * W; q += 64) a2[q] = make_double2(0.0, 0.0);
     }
     wave_sync_lds();
-    level1(sn, nxt);
+    level1(snx, nxt);
 
     const int32_t row = cur.row;
     const bool active = row >= 0;
@@ -902,6 +919,9 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, int6
       }
     }
     wave_sync_lds();
+    if (sn >= r1) break;
+    sl = sn;
+    sn = sn2;
     cur = nxt;
   }
 }
@@ -1353,10 +1373,11 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
         it = occ_s.emplace(std::make_pair(fn, shm_s), q < 1 ? 1 : q).first;
       }
       const int per_cu = occ_override() > 0 ? occ_override() : it->second;
-      const int64_t waves = (int64_t)ctx.n_cu * per_cu;
-      const int64_t chunk = (s.n_slices + waves - 1) / waves;
-      const int64_t nblk = (s.n_slices + chunk - 1) / chunk;
-      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, ctx.stream, s.n_slices, chunk,
+      int64_t nblk = (int64_t)ctx.n_cu * per_cu;
+      if (nblk > s.n_slices) nblk = s.n_slices < 8 ? 8 : s.n_slices;
+      if (!s.tickets.p) s.tickets.alloc(8 * 16);  // one counter per XCD, 128-B apart
+      AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, ctx.stream, s.n_slices, s.tickets.p,
                          s.max_slice_nodes, s.max_slice_w, s.perm.p, s.row_ptr.p, s.strip.p, s.strip_ptr.p,
                          s.strip_n.p, s.dslot.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p, s.snode.p,
                          b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);

@@ -19,7 +19,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def counters(d, kernel="k_assemble_p1"):
+def counters(d, kernel="k_assemble_strip"):
     acc = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True):
         for x in csv.DictReader(open(f)):
@@ -39,7 +39,7 @@ def main():
     c = {}
     for sub in ("pmc_sq", "pmc_fetch", "pmc_write", "pmc_lds"):
         c.update(counters(os.path.join(prof, sub)))
-    lines = [f"# {tag}: mean per dispatch of k_assemble_p1 (rocprofv3 --pmc, separate passes)"]
+    lines = [f"# {tag}: mean per dispatch of k_assemble_strip (rocprofv3 --pmc, separate passes)"]
     for k in sorted(c):
         lines.append(f"{k:32s} {c[k]:.6g}")
     fetch = c.get("FETCH_SIZE")
