@@ -6,6 +6,9 @@
 // (Aleph semantics, femutils/AlephDoFLinearSystem.cc:192-223,501-583).
 #include "afem_internal.hpp"
 
+#include <cstdlib>
+#include <string>
+
 #include <cmath>
 #include <cstring>
 
@@ -165,6 +168,135 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream(int64_t n_rows, const 
   }
 }
 
+// CSR-stream with 16-B loads: the block's value/column segment is read as
+// aligned groups of 4 non-zeros (one dwordx4 of columns and two dwordx4 of
+// values per lane: 0.75 vector-memory address ops per non-zero instead of 2),
+// the 4 gathers of x are issued together, products go to LDS; then one lane
+// per row sums its run (as k_spmv_stream).  Needs 16-B aligned cols/vals
+// bases (checked by the planner); the group past nnz is loaded element by
+// element.
+template <bool DOT>
+__global__ __launch_bounds__(kThreads) void k_spmv_stream4(int64_t n_rows, int64_t nnz,
+                                                           const int64_t* __restrict__ rows,
+                                                           const int32_t* __restrict__ cols,
+                                                           const double* __restrict__ vals,
+                                                           const double* __restrict__ x, double* __restrict__ y,
+                                                           double* __restrict__ partial)
+{
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* prod = reinterpret_cast<double*>(smem);
+  const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t r0 = blk * kThreads;
+  const int64_t r1 = (r0 + kThreads < n_rows) ? r0 + kThreads : n_rows;
+  const int64_t a = rows[r0], b = rows[r1];
+  for (int64_t q = (a & ~int64_t(3)) + 4 * (int64_t)threadIdx.x; q < b; q += 4 * kThreads) {
+    int c[4];
+    double v[4];
+    if (q + 4 <= nnz) {
+      const int4 c4 = *reinterpret_cast<const int4*>(cols + q);
+      const double2 v01 = *reinterpret_cast<const double2*>(vals + q);
+      const double2 v23 = *reinterpret_cast<const double2*>(vals + q + 2);
+      c[0] = c4.x;
+      c[1] = c4.y;
+      c[2] = c4.z;
+      c[3] = c4.w;
+      v[0] = v01.x;
+      v[1] = v01.y;
+      v[2] = v23.x;
+      v[3] = v23.y;
+    }
+    else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = q + j < nnz ? cols[q + j] : 0;
+        v[j] = q + j < nnz ? vals[q + j] : 0.0;
+      }
+    }
+    double xv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] = x[c[j]];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (q + j >= a && q + j < b) prod[q + j - a] = v[j] * xv[j];
+  }
+  __syncthreads();
+  const int64_t r = r0 + threadIdx.x;
+  double d = 0.0;
+  if (r < r1) {
+    double s = 0.0;
+    for (int64_t k = rows[r] - a, e = rows[r + 1] - a; k < e; ++k) s += prod[k];
+    y[r] = s;
+    if (DOT) d = x[r] * s;
+  }
+  if (DOT) {
+    double bs = block_sum(d);
+    if (threadIdx.x == 0) partial[blockIdx.x] = bs;
+  }
+}
+
+// Vector CSR SpMV: a 16-lane group per row, RPG rows per group with all of
+// their loads issued before any use (memory-level parallelism without LDS or
+// barriers).  Lane k of a row loads non-zero k (coalesced: a wave's 4 groups
+// read ~4*RPG consecutive rows' segments), gathers x, and the row sum is a
+// 16-lane shuffle reduction.  Rows longer than 16 loop in 16-wide chunks.
+// DOT: block partial of x[r] * y[r] (the CG's p.q).
+constexpr int kSpmvRpg = 4;
+template <bool DOT>
+__global__ __launch_bounds__(256) void k_spmv_v16(int64_t n_rows, const int64_t* __restrict__ rows,
+                                                  const int32_t* __restrict__ cols, const double* __restrict__ vals,
+                                                  const double* __restrict__ x, double* __restrict__ y,
+                                                  double* __restrict__ partial)
+{
+  const int l16 = threadIdx.x & 15;
+  const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int64_t r0 = g * kSpmvRpg;
+  int64_t rb[kSpmvRpg], re[kSpmvRpg];
+#pragma unroll
+  for (int i = 0; i < kSpmvRpg; ++i) {
+    const int64_t r = r0 + i < n_rows ? r0 + i : n_rows - 1;
+    rb[i] = rows[r];
+    re[i] = r0 + i < n_rows ? rows[r + 1] : rb[i];
+  }
+  double s[kSpmvRpg];
+  int32_t c[kSpmvRpg];
+  double v[kSpmvRpg];
+#pragma unroll
+  for (int i = 0; i < kSpmvRpg; ++i) {
+    const int64_t k = rb[i] + l16;
+    const bool in = k < re[i];
+    const int64_t kk = in ? k : rb[i];
+    c[i] = cols[kk];
+    v[i] = in ? vals[kk] : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < kSpmvRpg; ++i) s[i] = v[i] * x[c[i]];
+#pragma unroll
+  for (int i = 0; i < kSpmvRpg; ++i)
+    for (int64_t k = rb[i] + 16 + l16; k < re[i]; k += 16) s[i] += vals[k] * x[cols[k]];
+#pragma unroll
+  for (int i = 0; i < kSpmvRpg; ++i) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) s[i] += __shfl_xor(s[i], o, 16);
+  }
+  double d = 0.0;
+  if (l16 < kSpmvRpg) {
+    // lane i of the group writes row r0+i (4 consecutive rows: one 32-B store)
+    double si = s[0];
+#pragma unroll
+    for (int i = 1; i < kSpmvRpg; ++i)
+      if (l16 == i) si = s[i];
+    const int64_t r = r0 + l16;
+    if (r < n_rows) {
+      y[r] = si;
+      if (DOT) d = x[r] * si;
+    }
+  }
+  if (DOT) {
+    double bs = block_sum(d);
+    if (threadIdx.x == 0) partial[blockIdx.x] = bs;
+  }
+}
+
 // Fallback for segments that do not fit LDS: one lane per row.
 template <bool DOT>
 __global__ __launch_bounds__(kThreads) void k_spmv_row(int64_t n_rows, const int64_t* __restrict__ rows,
@@ -313,7 +445,8 @@ __global__ __launch_bounds__(kThreads) void k_dot(int64_t n, const double* __res
 
 // ---------------------------------------------------------------- helpers
 struct SpmvPlan {
-  int rpb = 0;          // rows per block (0: row kernel)
+  int rpb = 0;          // rows per block (0: row kernel, -1: vector CSR)
+  bool wide = false;    // 16-B loads of the segment (aligned bases)
   int64_t max_seg = 0;
   int64_t nblocks = 0;
 };
@@ -327,7 +460,8 @@ __global__ void k_block_seg(int64_t n_rows, int rpb, const int64_t* __restrict__
   atomicMax(out, (unsigned long long)(row_ptr[r1] - row_ptr[r0]));
 }
 
-SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows)
+SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows, const int32_t* cols = nullptr,
+                   const double* vals = nullptr)
 {
   SpmvPlan pl;
   DevBuf<unsigned long long> mx;
@@ -340,18 +474,45 @@ SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows)
   AFEM_HIP(hipMemcpyAsync(&hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
   ctx.sync();
   pl.nblocks = nb;
-  if (hm * 8ull <= 64ull * 1024ull) {
+  // AFEM_SPMV=stream (scalar-load stream) / v16 (16 lanes per row): diagnostics
+  static const int mode = [] {
+    const char* e = getenv("AFEM_SPMV");
+    if (e && std::string(e) == "stream") return 1;
+    if (e && std::string(e) == "v16") return 2;
+    return 0;
+  }();
+  if (mode == 2) {
+    pl.rpb = -1;
+    pl.nblocks = (n_rows + 16 * kSpmvRpg - 1) / (16 * kSpmvRpg);
+  }
+  else if (hm * 8ull <= 64ull * 1024ull) {
     pl.rpb = kThreads;
     pl.max_seg = (int64_t)hm;
+    pl.wide = mode == 0 && cols && vals && ((uintptr_t)cols & 15) == 0 && ((uintptr_t)vals & 15) == 0;
   }
   return pl;
 }
 
 void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* rows, const int32_t* cols,
-                 const double* vals, const double* x, double* y, double* partial)
+                 const double* vals, const double* x, double* y, double* partial, int64_t nnz = 0)
 {
   const unsigned nb = (unsigned)pl.nblocks;
-  if (pl.rpb) {
+  if (pl.rpb < 0) {
+    if (partial)
+      hipLaunchKernelGGL(k_spmv_v16<true>, dim3(nb), dim3(256), 0, ctx.stream, n_rows, rows, cols, vals, x, y, partial);
+    else
+      hipLaunchKernelGGL(k_spmv_v16<false>, dim3(nb), dim3(256), 0, ctx.stream, n_rows, rows, cols, vals, x, y,
+                         partial);
+  }
+  else if (pl.rpb && pl.wide) {
+    if (partial)
+      hipLaunchKernelGGL(k_spmv_stream4<true>, dim3(nb), dim3(kThreads), (size_t)pl.max_seg * 8, ctx.stream, n_rows,
+                         nnz, rows, cols, vals, x, y, partial);
+    else
+      hipLaunchKernelGGL(k_spmv_stream4<false>, dim3(nb), dim3(kThreads), (size_t)pl.max_seg * 8, ctx.stream, n_rows,
+                         nnz, rows, cols, vals, x, y, partial);
+  }
+  else if (pl.rpb) {
     if (partial)
       hipLaunchKernelGGL(k_spmv_stream<true>, dim3(nb), dim3(kThreads), (size_t)pl.max_seg * 8, ctx.stream, n_rows,
                          rows, cols, vals, x, y, partial);
@@ -488,8 +649,8 @@ void ls_spmv(LinearSystem& ls, const double* x, double* y)
   Ctx& ctx = *ls.ctx;
   require_csr(ls);
   if (ls.halo) halo_exchange(*ls.halo, ctx, const_cast<double*>(x));
-  SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, ls.n_rows);
-  launch_spmv(ctx, pl, ls.n_rows, ls.csr_rows, ls.csr_cols, ls.csr_vals, x, y, nullptr);
+  SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, ls.n_rows, ls.csr_cols, ls.csr_vals);
+  launch_spmv(ctx, pl, ls.n_rows, ls.csr_rows, ls.csr_cols, ls.csr_vals, x, y, nullptr, ls.csr_nnz);
 }
 
 void ls_solve(LinearSystem& ls, afem_solve_stats* st)
@@ -511,7 +672,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     ls.p.alloc(ls.n_cols);
     AFEM_HIP(hipMemsetAsync(ls.p.p, 0, ls.p.bytes(), ctx.stream));
   }
-  SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, n);
+  SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, n, ls.csr_cols, ls.csr_vals);
   const int64_t n_part = 2 * std::max<int64_t>(pl.nblocks, kVecBlocks);
   if (ls.partial.n < (size_t)n_part) ls.partial.alloc(n_part);
   if (ls.cons.n != (size_t)n) ls.cons.alloc(n);
@@ -527,7 +688,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
                      ls.p.p);
   AFEM_LAUNCHED();
   if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
-  launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, nullptr);
+  launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, nullptr, ls.csr_nnz);
   hipLaunchKernelGGL(k_cg_init, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.q.p, ls.r.p, ls.z.p, ls.p.p,
                      ls.dinv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
   AFEM_LAUNCHED();
@@ -555,7 +716,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   while (!converged && it < max_it) {
     const int par = it & 1;
     if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
-    launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p);
+    launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p, ls.csr_nnz);
     reduce_to(ctx, ls.partial.p, pl.nblocks, scal + 2);
     if (comm) comm_allreduce(comm, ctx, scal + 2, 1);
     hipLaunchKernelGGL(k_cg_update, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p, ls.r.p,
