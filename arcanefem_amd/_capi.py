@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libafem.so")
+LIB_PATH = os.environ.get("AFEM_LIB") or os.path.join(_HERE, "libafem.so")  # AFEM_LIB: diagnostic builds
 
 AFEM_OK = 0
 AFEM_MEM_HOST = 0
@@ -41,7 +41,7 @@ class BsrStats(ctypes.Structure):
     _fields_ = [("n_incidences", ctypes.c_int64), ("inc_table_entries", ctypes.c_int64),
                 ("max_row_len", ctypes.c_int32), ("rows_per_block", ctypes.c_int32), ("max_seg", ctypes.c_int64),
                 ("max_slice_nodes", ctypes.c_int32), ("max_slice_width", ctypes.c_int32),
-                ("n_slices", ctypes.c_int64), ("brick_order", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("n_slices", ctypes.c_int64), ("brick_order", ctypes.c_int32), ("uniform_slices", ctypes.c_int32)]
 
 
 class SolverOpts(ctypes.Structure):

@@ -145,7 +145,14 @@ struct Structure {
   DevBuf<int32_t> strip_c;  // 16-step chunks per slice
   DevBuf<int32_t> strip_n;  // steps per slice (longest row stream)
   DevBuf<uint8_t> dslot;
-  DevBuf<unsigned long long> tickets;  // dynamic slice claiming (assembly), 8 XCD counters
+  // Slices whose 64 rows share one strip topology (one strip, same length,
+  // same shift/swap bits spat[s]) run the uniform-control assembly variant;
+  // slist_u / slist_m list the uniform / other slices in processing order.
+  DevBuf<uint64_t> spat;
+  DevBuf<int32_t> slist_u, slist_m;
+  int64_t n_uni = 0, n_mix = 0;
+  DevBuf<int32_t> slist_all;  // identity list (general variant over every slice)
+  DevBuf<unsigned long long> tickets;  // dynamic slice claiming (assembly), 2 x 8 XCD counters
   int64_t n_slices = 0;
   int64_t n_incidences = 0;  // real (non-padding) entries
   int max_row_len = 0;

@@ -24,6 +24,11 @@
 #include "afem_internal.hpp"
 
 #include <cstdlib>
+#include <type_traits>
+
+#ifndef AFEM_ABL
+#define AFEM_ABL 0  // diagnostic ablations of the uniform strip kernel (tools/ablate_strip.sh)
+#endif
 
 
 namespace afem {
@@ -214,6 +219,11 @@ struct Tile {
     return V3{ p[0], p[stride()], DIMC == 3 ? p[2 * stride()] : 0.0 };
   }
   __device__ __forceinline__ double* at(int lane, uint32_t slot, int c) const { return acc + (slot * NACC + c) * 64 + lane; }
+};
+
+// two doubles stored with one 16-B access at an 8-B aligned address
+struct __attribute__((packed, aligned(8))) DPair {
+  double a, b;
 };
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -638,8 +648,17 @@ __host__ __device__ constexpr int64_t strip_tile_bytes(int dimc, int64_t u_cap, 
   return 8 * 64 * w_cap + strip_coord_bytes(dimc, u_cap, w_cap) + 2 * 64 * w_cap + 512;
 }
 
-template <int NV, int MAXC, int MAXW>
-__global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsigned long long* __restrict__ tickets,
+// UNI = true: the slices of `slist` whose 64 rows share one strip topology
+// (same length, one strip, same shift/swap sequence `spat`: every interior
+// brick of a structured mesh).  The shift/swap decision is then wave-uniform:
+// a scalar branch instead of 13 per-lane selects per step, the two priming
+// steps only load the window, and no step needs an emit mask (≈45 instead of
+// ≈72 VALU ops per cell).  Same formulas in the same order as the general
+// path, so both give the same bits.
+template <int NV, int MAXC, int MAXW, int UMODE>
+__global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, const int32_t* __restrict__ slist,
+                                                          const uint64_t* __restrict__ spat,
+                                                          unsigned long long* __restrict__ tickets,
                                                           int u_cap, int w_cap,
                                                           const int32_t* __restrict__ perm,
                                                           const int64_t* __restrict__ row_ptr,
@@ -654,8 +673,9 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsi
                                                           const int32_t* __restrict__ snode,
                                                           const double* __restrict__ coords, double s_coef,
                                                           double f_meas, double* __restrict__ vals,
-                                                          double* __restrict__ rhs)
+                                                          double* __restrict__ rhs, int wb_flat)
 {
+  constexpr bool UNI = UMODE != 0;  // 1: scalar shift/swap branches, 2: selects on the uniform bit
   constexpr int DIMC = NV == 4 ? 3 : 2;
   extern __shared__ __align__(16) unsigned char smem[];
   double* acc = reinterpret_cast<double*>(smem);
@@ -669,18 +689,25 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsi
   // ahead so the atomic's latency hides under a whole slice of work.
   const int xcd = (int)(blockIdx.x & 7);
   const int64_t r0 = n_slices * xcd / 8, r1 = n_slices * (xcd + 1) / 8;
-  auto claim = [&]() -> int64_t {
+  // issue: the atomic's result stays in a VGPR; get: readfirstlane (the slice
+  // index is provably wave-uniform: scalar loads, scalar branches).  In the
+  // loop a claim is read one whole slice after it was issued, behind that
+  // slice's stores, so the wave never waits on the atomic (or the stores).
+  auto claim_issue = [&]() -> unsigned long long {
     unsigned long long t = 0;
     if (lane == 0) t = atomicAdd(tickets + 16 * xcd, 1ull);
-    // readfirstlane: the slice index is provably wave-uniform (scalar loads,
-    // scalar branches on the slice's sizes)
+    return t;
+  };
+  auto claim_get = [&](unsigned long long t) -> int64_t {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)t);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(t >> 32));
     return r0 + (int64_t)(((uint64_t)hi << 32) | lo);
   };
-  int64_t sl = claim();
-  if (sl >= r1) return;
-  int64_t sn = claim();
+  // claimed values are positions in `slist` (the slice ids of this launch)
+  int64_t il = claim_get(claim_issue());
+  if (il >= r1) return;
+  int64_t in = claim_get(claim_issue());
+  int64_t sl = slist[il];
 
   auto level1 = [&](int64_t s, StripPre<MAXC>& p) {
     p.row = perm[s * 64 + lane];
@@ -699,6 +726,14 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsi
     for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
   };
   auto level2 = [&](StripPre<MAXC>& p) {
+#if AFEM_ABL == 6  // ablation: no dependent (second-level) loads; rows not stored (len 0; diagonals land in vals[0..63])
+    p.rb = 0;
+    p.len = 0;
+    p.xi = V3{ 0.5, 0.5, 0.5 };
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p.x[k] = p.y[k] = p.z[k] = (double)p.nid[k] * 1e-7;
+    return;
+#endif
     const bool act = p.row >= 0;
     const int32_t r = act ? p.row : 0;
     const int64_t b = row_ptr[r];
@@ -717,9 +752,13 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsi
   StripPre<MAXC> cur, nxt;
   level1(sl, cur);
   level2(cur);
+  // drain the prologue loads: the loop header then inherits only the
+  // back-edge's pending ops (loads a slice old, the stores), so the staging
+  // waits count past the stores instead of on them
+  __builtin_amdgcn_s_waitcnt(0);
   for (;;) {
-    const int64_t sn2 = claim();              // used by the next iteration
-    const int64_t snx = sn < r1 ? sn : sl;     // prefetch target (itself when done)
+    const unsigned long long t2 = claim_issue();   // read at the end of this iteration
+    const int64_t snx = in < r1 ? slist[in] : sl;  // prefetch target (itself when done)
     const int nsteps = strip_n[sl];  // uniform over the wave
     const int W = slice_w[sl];
     const int64_t u0 = snode_ptr[sl];
@@ -733,7 +772,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsi
       cxyz[DIMC * idx + 1] = cur.y[k];
       if (DIMC == 3) cxyz[DIMC * idx + 2] = cur.z[k];
     }
-    if (nu > 256) {
+    if (!UNI && nu > 256) {  // uniform slices: <= 256 nodes, <= 16 slots (k_strip_classify)
       for (int u = lane + 256; u < nu; u += 64) {
         const int64_t n = snode[u0 + u];
         cxyz[DIMC * u] = coords[3 * n];
@@ -746,7 +785,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsi
       u32x4* dst = reinterpret_cast<u32x4*>(li);
       dst[max(min(lane, nq - 1), 0)] = cur.l0;
       dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
-      if (nq > 128) {
+      if (!UNI && nq > 128) {
         const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + lidx_ptr[sl]);
         for (int q = lane + 128; q < nq; q += 64) dst[q] = ls[q];
       }
@@ -837,21 +876,116 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsi
       return (wq >> (8 * (j & 3))) & 0xFFu;
     };
     constexpr int NSTEP = 16 * MAXC;
-    int u1 = lidx_of(byte_at(0));
-    V3 xc = coord(u1);
-    u1 = lidx_of(byte_at(1));
+    if constexpr (UNI && NV == 4) {
+      // uniform strip: steps 0,1 prime the window (no cell), every later step
+      // emits; the shift/swap bit is a scalar (one branch per step, both arms
+      // straight-line code; only the kept node's registers move on a shift)
+      const uint64_t pat = spat[sl];
+      auto ustep = [&](auto swap_c, uint32_t byte, V3 xd, bool swp) {
+        constexpr int SWAP = decltype(swap_c)::value;  // 1 swap, 0 shift, -1 select on swp
+        double* const aD = acc_lane + 64 * (byte & 63u);
+        const V3 eD = sub(xd, xi);
+        V3 cRn;
+        if constexpr (SWAP == 1) {
+          cRn = cN;
+        }
+        else if constexpr (SWAP == 0) {
+          cRn = cP;
+          eP = eQ;
+          aP = aQ;
+        }
+        else {
+          cRn = sel(swp, cN, cP);
+          eP = sel(swp, eP, eQ);
+          aP = swp ? aP : aQ;
+        }
+        eQ = eR;
+        aQ = aR;
+        eR = eD;
+        aR = aD;
+#if AFEM_ABL == 3  // ablation: no element arithmetic
+        cP = eR;
+        cN = eQ;
+        macc += eD.x;
+        atomicAdd(aP, eD.x);
+        atomicAdd(aQ, eD.y);
+        atomicAdd(aR, eD.z);
+        (void)cRn;
+        return;
+#endif
+        cP = cross(eQ, eR);
+        cN = cross(eP, eR);
+        const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
+        // a padding step (odd lengths: the guard is every 2 steps) has a zero edge: meas = 0, all
+        // k but the diagonal's (aR) exactly 0 with the finite 1/tiny
+        const double meas = fabs(dot(eP, cP));
+        const double s = -s_coef * recip1(fmax(meas, 1e-300));
+        const double kP = dot(m, cP) * s;
+        const double kQ = -dot(m, cN) * s;
+        const double kR = dot(m, cRn) * s;
+        macc += meas;
+#if AFEM_ABL == 1  // ablation: plain LDS writes instead of LDS atomics
+        *aP = kP;
+        *aQ = kQ;
+        *aR = kR;
+#elif AFEM_ABL == 2  // ablation: no LDS accumulation
+        macc += kP + kQ + kR;
+        (void)aP;
+#else
+        atomicAdd(aP, kP);
+        atomicAdd(aQ, kQ);
+        atomicAdd(aR, kR);
+#endif
+      };
+      {
+        const uint32_t b0 = byte_at(0), b1 = byte_at(1);
+        eQ = sub(coord(lidx_of(b0)), xi);
+        eR = sub(coord(lidx_of(b1)), xi);
+        aQ = acc_lane + 64 * (b0 & 63u);
+        aR = acc_lane + 64 * (b1 & 63u);
+        cP = cross(eQ, eR);
+      }
+      int u1 = lidx_of(byte_at(2));
+      V3 xc = coord(u1);
+      u1 = lidx_of(byte_at(3));
 #pragma unroll
-    for (int j = 0; j < NSTEP; ++j) {
-      if ((j & 3) == 0 && j >= nsteps) break;
-      const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
-      const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
-      step(byte_at(j), xc);
-      xc = xn;
-      u1 = u2;
-      // next slice's level-2 loads: ~12 steps after its level-1 loads were issued
-      if (j == 11) level2(nxt);
+      for (int j = 2; j < NSTEP; ++j) {
+        if ((j & (UMODE == 1 ? 1 : 3)) == 0 && j >= nsteps) break;
+#if AFEM_ABL == 5  // ablation: no LDS index / coordinate reads in the step loop
+        const int u2 = 0;
+        const double fb = (double)(byte_at(j + 1 < NSTEP ? j + 1 : j) & 63u);
+        const V3 xn = V3{ xi.x + fb, xi.y - fb, xi.z + 2 * fb };
+#else
+        const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
+        const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
+#endif
+        const bool swp = (pat >> j) & 1u;
+        if constexpr (UMODE == 2) ustep(std::integral_constant<int, -1>{}, byte_at(j), xc, swp);
+        else if (swp) ustep(std::integral_constant<int, 1>{}, byte_at(j), xc, true);
+        else ustep(std::integral_constant<int, 0>{}, byte_at(j), xc, false);
+        xc = xn;
+        u1 = u2;
+        if (j == 11) level2(nxt);
+      }
+      if (nsteps <= (UMODE == 1 ? 10 : 8)) level2(nxt);  // the loop ended before step 11
     }
-    if (nsteps <= 8) level2(nxt);  // the loop ended before step 11
+    else {
+      int u1 = lidx_of(byte_at(0));
+      V3 xc = coord(u1);
+      u1 = lidx_of(byte_at(1));
+#pragma unroll
+      for (int j = 0; j < NSTEP; ++j) {
+        if ((j & 3) == 0 && j >= nsteps) break;
+        const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
+        const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
+        step(byte_at(j), xc);
+        xc = xn;
+        u1 = u2;
+        // next slice's level-2 loads: ~12 steps after its level-1 loads were issued
+        if (j == 11) level2(nxt);
+      }
+      if (nsteps <= 8) level2(nxt);  // the loop ended before step 11
+    }
 
     // ---- RHS (unconditional store: idle lanes repeat an active lane's store)
     {
@@ -863,7 +997,44 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsi
     }
     wave_sync_lds();
 
-    // ---- diagonal + write-back (as k_assemble_p1; the map overlays the coordinates)
+    // ---- diagonal + write-back, direct: each lane stores its own row from
+    // registers, two values per 16-B store (dword-aligned stores are legal);
+    // the rows of a slice lie in a few contiguous runs, so the lines are
+    // completed in L2 within the slice and leave as full lines.  The diagonal
+    // slot is zeroed first so the row sum needs no per-slot test (the slots
+    // past the row's end stay 0), then rewritten with -sum.
+    if ((UNI || W <= MAXW) && !wb_flat) {
+      const uint32_t dsl = active ? dslot : 0xFFu;
+      if (dsl != 0xFFu) acc_lane[64 * dsl] = 0.0;
+      double rv[MAXW];
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t) rv[t] = acc_lane[64 * min(t, W - 1)];
+      double sum = 0.0;
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t)
+        if (t < W) sum += rv[t];  // uniform bound
+      double* const rowp = vals + rb;
+#if AFEM_ABL == 4  // ablation: no value stores
+      if (sum == 12345.678) rowp[0] = sum;
+      if (false)
+#endif
+#pragma unroll
+      for (int t = 0; t < MAXW; t += 2) {
+        if (t < W) {  // uniform
+          if (t + 1 < len) *reinterpret_cast<DPair*>(rowp + t) = DPair{ rv[t], rv[t + 1] };
+          else if (t < len) rowp[t] = rv[t];
+        }
+      }
+      if (dsl != 0xFFu) rowp[dsl] = -sum;
+      wave_sync_lds();
+      if (in >= r1) break;
+      sl = snx;
+      in = claim_get(t2);
+      cur = nxt;
+      continue;
+    }
+    // ---- diagonal + write-back through a flat LDS image (default; as
+    // k_assemble_p1; the map overlays the coordinates)
     int fp = len;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -874,7 +1045,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsi
     fp -= len;
     uint16_t* map = reinterpret_cast<uint16_t*>(cxyz);
     const uint32_t dsl = active ? dslot : 0xFFu;
-    if (W <= MAXW) {
+    if (UNI || W <= MAXW) {
       double rv[MAXW];
 #pragma unroll
       for (int t = 0; t < MAXW; ++t) rv[t] = acc_lane[64 * min(t, W - 1)];
@@ -919,9 +1090,9 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, unsi
       }
     }
     wave_sync_lds();
-    if (sn >= r1) break;
-    sl = sn;
-    sn = sn2;
+    if (in >= r1) break;
+    sl = snx;
+    in = claim_get(t2);
     cur = nxt;
   }
 }
@@ -1365,7 +1536,19 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
       strip_tile_bytes(dimc, s.max_slice_nodes, s.max_slice_w) <= kTileLdsMax) {
     const size_t shm_s = (size_t)strip_tile_bytes(dimc, s.max_slice_nodes, s.max_slice_w);
     static std::map<std::pair<const void*, size_t>, int> occ_s;
-    auto launch_s = [&](const void* fn, auto kern) {
+    // AFEM_ASSEMBLY_UNIFORM=0: every slice through the general variant (diagnostic)
+    const char* ue = getenv("AFEM_ASSEMBLY_UNIFORM");  // read per call: the parity test toggles it
+    const int umode = ue ? atoi(ue) : 1;               // 0 off, 1 branches, 2 selects
+    const bool uni_env = umode != 0;
+    const bool use_uni = uni_env && s.n_uni > 0;
+    // AFEM_ASSEMBLY_WB=direct: per-lane 16-B stores from registers (diagnostic;
+    // the default writes through the flat LDS image, ~2% faster on C2)
+    const char* we = getenv("AFEM_ASSEMBLY_WB");
+    const int wb_flat = (we && std::string(we) == "direct") ? 0 : 1;
+    const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;
+    if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);  // one counter per XCD, 128-B apart, per launch
+    AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
+    auto launch_s = [&](const void* fn, auto kern, int64_t n_list, const int32_t* list, unsigned long long* tk) {
       auto it = occ_s.find({ fn, shm_s });
       if (it == occ_s.end()) {
         int q = 0;
@@ -1374,23 +1557,31 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
       }
       const int per_cu = occ_override() > 0 ? occ_override() : it->second;
       int64_t nblk = (int64_t)ctx.n_cu * per_cu;
-      if (nblk > s.n_slices) nblk = s.n_slices < 8 ? 8 : s.n_slices;
-      if (!s.tickets.p) s.tickets.alloc(8 * 16);  // one counter per XCD, 128-B apart
-      AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
-      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, ctx.stream, s.n_slices, s.tickets.p,
+      if (nblk > n_list) nblk = n_list < 8 ? 8 : n_list;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, ctx.stream, n_list, list, s.spat.p, tk,
                          s.max_slice_nodes, s.max_slice_w, s.perm.p, s.row_ptr.p, s.strip.p, s.strip_ptr.p,
                          s.strip_n.p, s.dslot.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p, s.snode.p,
-                         b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
+                         b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, wb_flat);
     };
-#define AFEM_STRIP_K(NV_, C_, W_) launch_s(reinterpret_cast<const void*>(&k_assemble_strip<NV_, C_, W_>), k_assemble_strip<NV_, C_, W_>)
+    const int32_t* list_m = use_uni ? s.slist_m.p : s.slist_all.p;
+#define AFEM_STRIP_K(NV_, C_, W_, U_, N_, L_, T_)                                                                      \
+  launch_s(reinterpret_cast<const void*>(&k_assemble_strip<NV_, C_, W_, U_>), k_assemble_strip<NV_, C_, W_, U_>, N_, \
+           L_, T_)
     const bool small = s.max_strip_c <= 2 && s.max_slice_w <= 16;
     if (nv == 4) {
-      if (small) AFEM_STRIP_K(4, 2, 16);
-      else AFEM_STRIP_K(4, 4, 32);
+      if (small) {
+        if (use_uni && umode == 2) AFEM_STRIP_K(4, 2, 16, 2, s.n_uni, s.slist_u.p, s.tickets.p);
+        else if (use_uni) AFEM_STRIP_K(4, 2, 16, 1, s.n_uni, s.slist_u.p, s.tickets.p);
+        if (n_mix > 0) AFEM_STRIP_K(4, 2, 16, 0, n_mix, list_m, s.tickets.p + 128);
+      }
+      else {
+        if (use_uni) AFEM_STRIP_K(4, 4, 32, 1, s.n_uni, s.slist_u.p, s.tickets.p);
+        if (n_mix > 0) AFEM_STRIP_K(4, 4, 32, 0, n_mix, list_m, s.tickets.p + 128);
+      }
     }
     else {
-      if (small) AFEM_STRIP_K(3, 2, 16);
-      else AFEM_STRIP_K(3, 4, 32);
+      if (small) AFEM_STRIP_K(3, 2, 16, 0, s.n_slices, s.slist_all.p, s.tickets.p + 128);
+      else AFEM_STRIP_K(3, 4, 32, 0, s.n_slices, s.slist_all.p, s.tickets.p + 128);
     }
 #undef AFEM_STRIP_K
     AFEM_LAUNCHED();

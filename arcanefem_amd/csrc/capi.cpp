@@ -469,6 +469,7 @@ int afem_bsr_get_stats(afem_bsr* b, afem_bsr_stats* st)
   st->max_slice_width = b->s.max_slice_w;
   st->n_slices = b->s.n_slices;
   st->brick_order = b->s.brick_order ? 1 : 0;
+  st->uniform_slices = (int32_t)b->s.n_uni;
   API_END
 }
 

@@ -497,6 +497,41 @@ __global__ __launch_bounds__(64) void k_strip_rows(int64_t n_pos, int nv, const 
   for (int j = 0; j < steps; ++j) out[(int64_t)(j >> 4) * 1024 + (j & 15)] = j < total ? buf[j] : (uint8_t)(dslot | (3 << 6));
 }
 
+// per slice: does every lane run the same strip topology?  Uniform = all 64
+// rows active, one strip (kinds 2,2 then 0/1 only), the same length, the same
+// shift/swap sequence.  Out: flag (1 = uniform) and the swap bits (bit j = step
+// j is a swap).  One wave per slice.
+__global__ __launch_bounds__(64) void k_strip_classify(int64_t n_slices, const int32_t* __restrict__ perm,
+                                                       const uint8_t* __restrict__ strip,
+                                                       const int64_t* __restrict__ strip_ptr,
+                                                       const int32_t* __restrict__ strip_n,
+                                                       const int64_t* __restrict__ snode_ptr,
+                                                       const int32_t* __restrict__ slice_w, uint8_t* __restrict__ uflag,
+                                                       uint64_t* __restrict__ spat)
+{
+  const int64_t sl = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (sl >= n_slices) return;
+  const int n = strip_n[sl];
+  const uint8_t* st = strip + strip_ptr[sl] + lane * 16;
+  // the uniform kernel also drops the overflow paths (> 256 slice nodes, > 16 slots)
+  bool ok = perm[sl * 64 + lane] >= 0 && n >= 3 && n <= 64 && snode_ptr[sl + 1] - snode_ptr[sl] <= 256 &&
+            slice_w[sl] <= 16;
+  uint64_t pat = 0;
+  for (int j = 0; j < n && ok; ++j) {
+    const uint32_t kind = st[(int64_t)(j >> 4) * 1024 + (j & 15)] >> 6;
+    if (j < 2) ok = kind == 2;
+    else if (kind > 1) ok = false;
+    else pat |= (uint64_t)kind << j;
+  }
+  const uint64_t p0 = __shfl(pat, 0);
+  const bool all = __all(ok && pat == p0);
+  if (lane == 0) {
+    uflag[sl] = all ? 1 : 0;
+    spat[sl] = all ? p0 : 0;
+  }
+}
+
 // per slice: 16-step chunks (max stream length over its lanes) and bytes
 __global__ void k_strip_width(int64_t n_slices, const int32_t* __restrict__ strip_len, int32_t* __restrict__ strip_c,
                               int32_t* __restrict__ strip_n, int64_t* __restrict__ sz, int32_t* __restrict__ flags)
@@ -699,6 +734,31 @@ void build_structure(Mesh& m, Structure& s)
                          s.perm.p, m.cell_node.p, nc_ptr.p, nc.p, s.row_ptr.p, s.cols.p, nullptr, s.strip_ptr.p,
                          s.strip_c.p, s.strip.p, s.dslot.p);
       AFEM_LAUNCHED();
+      // uniform / mixed slice lists (tets; triangles use the general path)
+      DevBuf<uint8_t> uflag;
+      uflag.alloc(s.n_slices);
+      s.spat.alloc(s.n_slices);
+      hipLaunchKernelGGL(k_strip_classify, dim3((unsigned)s.n_slices), dim3(64), 0, ctx.stream, s.n_slices, s.perm.p,
+                         s.strip.p, s.strip_ptr.p, s.strip_n.p, s.snode_ptr.p, s.slice_w.p, uflag.p, s.spat.p);
+      AFEM_LAUNCHED();
+      std::vector<uint8_t> hu((size_t)s.n_slices);
+      AFEM_HIP(hipMemcpyAsync(hu.data(), uflag.p, hu.size(), hipMemcpyDeviceToHost, ctx.stream));
+      ctx.sync();
+      std::vector<int32_t> lu, lm;
+      for (int64_t i = 0; i < s.n_slices; ++i) (hu[(size_t)i] && nv == 4 ? lu : lm).push_back((int32_t)i);
+      s.n_uni = (int64_t)lu.size();
+      s.n_mix = (int64_t)lm.size();
+      s.slist_all.alloc(s.n_slices);
+      hipLaunchKernelGGL(k_perm_identity, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, s.n_slices,
+                         s.n_slices, s.slist_all.p);
+      AFEM_LAUNCHED();
+      s.slist_u.alloc(s.n_uni > 0 ? s.n_uni : 1);
+      s.slist_m.alloc(s.n_mix > 0 ? s.n_mix : 1);
+      if (s.n_uni > 0)
+        AFEM_HIP(hipMemcpyAsync(s.slist_u.p, lu.data(), lu.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+      if (s.n_mix > 0)
+        AFEM_HIP(hipMemcpyAsync(s.slist_m.p, lm.data(), lm.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+      ctx.sync();
     }
     else {
       s.strip_c.reset();

@@ -219,7 +219,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_assemble_strip<4,2,16>",
+                "kernel": "k_assemble_strip<4,2,16,uniform> + k_assemble_strip<4,2,16,general>",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -228,6 +228,7 @@ def main():
                 "algorithmic_bytes_per_launch": int(ab),
                 "kernel_ms": round(kmean, 4),
                 "inc_padding": round(bst["inc_table_entries"] / max(n_inc, 1) - 1.0, 4),
+                "uniform_slice_frac": round(bst["uniform_slices"] / max(bst["n_slices"], 1), 4),
             },
             "cpu_baseline": cpu,
             "cg_iter_per_s": round(cg_iter_per_s, 2),

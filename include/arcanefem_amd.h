@@ -180,7 +180,7 @@ typedef struct afem_bsr_stats {
   int32_t max_slice_width;  /* max row length within one slice */
   int64_t n_slices;         /* assembly slices (wavefronts per launch) */
   int32_t brick_order;      /* 1: slices are 4x4x4 (3D) / 8x8 (2D) node bricks, 0: node order */
-  int32_t reserved;
+  int32_t uniform_slices;   /* slices whose 64 rows share one strip topology (uniform-control assembly variant) */
 } afem_bsr_stats;
 int afem_bsr_get_stats(afem_bsr* bsr, afem_bsr_stats* stats);
 /* Copies the scalar CSR expansion to host in the reference's CSRFormatView

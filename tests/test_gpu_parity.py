@@ -98,6 +98,33 @@ def test_assembly_bitwise_reproducible(ctx):
         assert np.array_equal(r1, ls.rhs_host())
 
 
+def test_uniform_strip_variant(ctx, monkeypatch):
+    # interior 4x4x4 bricks of a structured box share one strip topology and
+    # run the uniform-control kernel; it must give the general kernel's bits
+    # and match the oracle
+    mesh = af.Mesh.structured(ctx, 3, 23, seed=11)
+    bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+    st = bsr.stats()
+    assert st["brick_order"] == 1 and 0 < st["uniform_slices"] < st["n_slices"]
+    _, _, v_uni = bsr.download()
+    r_uni = ls.rhs_host()
+    monkeypatch.setenv("AFEM_ASSEMBLY_UNIFORM", "0")
+    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable())
+    rows, cols, v_gen = bsr.download()
+    assert np.array_equal(v_uni, v_gen), "uniform and general strip kernels differ"
+    assert np.array_equal(r_uni, ls.rhs_host())
+    monkeypatch.setenv("AFEM_ASSEMBLY_WB", "direct")  # per-lane stores from registers
+    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable())
+    _, _, v_flat = bsr.download()
+    assert np.array_equal(v_uni, v_flat), "flat and direct write-back differ"
+    cells, coords, _ = mesh.download()
+    orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+    ovals, orhs = O.assemble_poisson(mesh.n_own_nodes, cells, coords, orp, ocols, 5.5)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    _check_values(v_uni, ovals)
+    assert np.abs(r_uni - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+
+
 def test_isolated_node_and_ragged_rows(ctx):
     # two tets sharing a face + one node touched by no cell (empty row apart
     # from the diagonal the reference always inserts, BSRFormat.h:679)
