@@ -102,6 +102,19 @@ struct Mesh {
 };
 
 // ------------------------------------------------------------------ sparsity
+// Per-slice record of the strip assembly, one 32-B scalar load per slice
+// (in the order of the slice lists the kernel walks).
+struct alignas(16) SliceRec {
+  uint32_t sl;         // slice id (positions 64*sl .. 64*sl+63)
+  uint32_t lidx_off;   // lidx_ptr[sl]
+  uint32_t strip_off;  // strip_ptr[sl] / 1024
+  uint32_t snode_off;  // snode_ptr[sl]
+  uint32_t meta;       // slice nodes | width (max row length) << 16 | strip steps << 24
+  uint32_t pad;        // (dword fields only: the kernel reads records with scalar loads)
+  uint64_t pat;        // uniform slices: shift/swap bits
+};
+static_assert(sizeof(SliceRec) == 32, "SliceRec is one s_load_dwordx8");
+
 // Scalar (node-node) structure shared by every NB_DOF: rows = owned nodes.
 struct Structure {
   int64_t n_rows = 0, n_cols = 0, nnz = 0;
@@ -147,11 +160,13 @@ struct Structure {
   DevBuf<uint8_t> dslot;
   // Slices whose 64 rows share one strip topology (one strip, same length,
   // same shift/swap bits spat[s]) run the uniform-control assembly variant;
-  // slist_u / slist_m list the uniform / other slices in processing order.
+  // rec_u / rec_m list the uniform / other slices in processing order.
   DevBuf<uint64_t> spat;
-  DevBuf<int32_t> slist_u, slist_m;
+  DevBuf<SliceRec> rec_u, rec_m, rec_all;  // uniform / other / every slice, in processing order
   int64_t n_uni = 0, n_mix = 0;
-  DevBuf<int32_t> slist_all;  // identity list (general variant over every slice)
+  bool rec_ok = false;                     // offsets fit the 32-bit record fields
+  DevBuf<int64_t> pos_rb;                  // [n_slices*64] row_ptr of each position's row (0: idle)
+  DevBuf<uint32_t> pos_dl;                 // [n_slices*64] diagonal slot | row length << 8
   DevBuf<unsigned long long> tickets;  // dynamic slice claiming (assembly), 2 x 8 XCD counters
   int64_t n_slices = 0;
   int64_t n_incidences = 0;  // real (non-padding) entries

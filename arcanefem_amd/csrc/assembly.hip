@@ -26,8 +26,11 @@
 #include <cstdlib>
 #include <type_traits>
 
+#ifndef AFEM_WB
+#define AFEM_WB 0  // strip kernel write-back: 0 flat LDS image (default), 1 per-lane stores (diagnostic)
+#endif
 #ifndef AFEM_ABL
-#define AFEM_ABL 0  // diagnostic ablations of the uniform strip kernel (tools/ablate_strip.sh)
+#define AFEM_ABL 0  // diagnostic ablations of the uniform strip kernel (build_abl/, tools/ab.sh)
 #endif
 
 
@@ -219,11 +222,6 @@ struct Tile {
     return V3{ p[0], p[stride()], DIMC == 3 ? p[2 * stride()] : 0.0 };
   }
   __device__ __forceinline__ double* at(int lane, uint32_t slot, int c) const { return acc + (slot * NACC + c) * 64 + lane; }
-};
-
-// two doubles stored with one 16-B access at an 8-B aligned address
-struct __attribute__((packed, aligned(8))) DPair {
-  double a, b;
 };
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -624,13 +622,10 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
 template <int MAXC>
 struct StripPre {
   int32_t row;
-  int32_t len;
+  uint32_t dl;  // diagonal slot | row length << 8
   int64_t rb;
-  V3 xi;
-  int32_t nid[4];
   u32x4 l0, l1;
   u32x4 ch[MAXC];
-  uint32_t dslot;
   double x[4], y[4], z[4];
 };
 
@@ -638,17 +633,17 @@ struct StripPre {
 // slice's node coordinates AoS (DIMC doubles per node: one address per
 // gather, components at immediate offsets), the u16 column-index table
 // [slot][lane], 512 B of write-back scratch.
-// (the coordinate region doubles as the write-back map: at least 2 B per value)
+// (the coordinate region doubles as the write-back map: at least 4 B per value)
 __host__ __device__ constexpr int64_t strip_coord_bytes(int dimc, int64_t u_cap, int64_t w_cap)
 {
-  return ((8 * (int64_t)dimc * u_cap > 128 * w_cap ? 8 * (int64_t)dimc * u_cap : 128 * w_cap) + 15) & ~int64_t(15);
+  return ((8 * (int64_t)dimc * u_cap > 256 * w_cap ? 8 * (int64_t)dimc * u_cap : 256 * w_cap) + 15) & ~int64_t(15);
 }
 __host__ __device__ constexpr int64_t strip_tile_bytes(int dimc, int64_t u_cap, int64_t w_cap)
 {
   return 8 * 64 * w_cap + strip_coord_bytes(dimc, u_cap, w_cap) + 2 * 64 * w_cap + 512;
 }
 
-// UNI = true: the slices of `slist` whose 64 rows share one strip topology
+// UNI = true: the slices of `recs` (the uniform list) whose 64 rows share one strip topology
 // (same length, one strip, same shift/swap sequence `spat`: every interior
 // brick of a structured mesh).  The shift/swap decision is then wave-uniform:
 // a scalar branch instead of 13 per-lane selects per step, the two priming
@@ -656,24 +651,18 @@ __host__ __device__ constexpr int64_t strip_tile_bytes(int dimc, int64_t u_cap, 
 // ≈72 VALU ops per cell).  Same formulas in the same order as the general
 // path, so both give the same bits.
 template <int NV, int MAXC, int MAXW, int UMODE>
-__global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, const int32_t* __restrict__ slist,
-                                                          const uint64_t* __restrict__ spat,
+__global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, const SliceRec* __restrict__ recs,
                                                           unsigned long long* __restrict__ tickets,
                                                           int u_cap, int w_cap,
                                                           const int32_t* __restrict__ perm,
-                                                          const int64_t* __restrict__ row_ptr,
+                                                          const int64_t* __restrict__ pos_rb,
+                                                          const uint32_t* __restrict__ pos_dl,
                                                           const uint8_t* __restrict__ strip,
-                                                          const int64_t* __restrict__ strip_ptr,
-                                                          const int32_t* __restrict__ strip_n,
-                                                          const uint8_t* __restrict__ dslots,
-                                                          const int32_t* __restrict__ slice_w,
-                                                          const int64_t* __restrict__ lidx_ptr,
                                                           const uint16_t* __restrict__ lidx,
-                                                          const int64_t* __restrict__ snode_ptr,
                                                           const int32_t* __restrict__ snode,
                                                           const double* __restrict__ coords, double s_coef,
                                                           double f_meas, double* __restrict__ vals,
-                                                          double* __restrict__ rhs, int wb_flat)
+                                                          double* __restrict__ rhs)
 {
   constexpr bool UNI = UMODE != 0;  // 1: scalar shift/swap branches, 2: selects on the uniform bit
   constexpr int DIMC = NV == 4 ? 3 : 2;
@@ -685,13 +674,12 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
   const int lane = threadIdx.x;
   // Dynamic slice claiming, one ticket counter per XCD (workgroups are dealt
   // to the 8 XCDs round-robin): XCD x walks the contiguous x-th eighth of the
-  // slices, so neighbouring bricks stay in one L2; a wave claims two slices
-  // ahead so the atomic's latency hides under a whole slice of work.
+  // list, so neighbouring bricks stay in one L2.
   const int xcd = (int)(blockIdx.x & 7);
   const int64_t r0 = n_slices * xcd / 8, r1 = n_slices * (xcd + 1) / 8;
-  // issue: the atomic's result stays in a VGPR; get: readfirstlane (the slice
-  // index is provably wave-uniform: scalar loads, scalar branches).  In the
-  // loop a claim is read one whole slice after it was issued, behind that
+  // issue: the atomic's result stays in a VGPR; get: readfirstlane (the list
+  // position is provably wave-uniform: scalar loads, scalar branches).  In
+  // the loop a claim is read one whole slice after it was issued, behind that
   // slice's stores, so the wave never waits on the atomic (or the stores).
   auto claim_issue = [&]() -> unsigned long long {
     unsigned long long t = 0;
@@ -703,68 +691,71 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(t >> 32));
     return r0 + (int64_t)(((uint64_t)hi << 32) | lo);
   };
-  // claimed values are positions in `slist` (the slice ids of this launch)
-  int64_t il = claim_get(claim_issue());
-  if (il >= r1) return;
-  int64_t in = claim_get(claim_issue());
-  int64_t sl = slist[il];
+  // Four-stage software pipeline over the claimed list positions p0..p3:
+  // while slice p0 is processed out of LDS, the row data, strip, column
+  // indices and node coordinates of p1 are in flight, the node ids of p2
+  // (the addresses of its coordinate gather), and the 32-B record of p3 (the
+  // addresses of everything else).  Every dependent load thus has a whole
+  // slice of work to land; positions past the end re-fetch p0 (never used).
+  int64_t p0 = claim_get(claim_issue());
+  if (p0 >= r1) return;
+  int64_t p1 = claim_get(claim_issue());
+  int64_t p2 = claim_get(claim_issue());
+  int64_t p3 = claim_get(claim_issue());
+  SliceRec R0 = recs[p0];
+  SliceRec R1 = recs[p1 < r1 ? p1 : p0];
+  SliceRec R2 = recs[p2 < r1 ? p2 : p0];
 
-  auto level1 = [&](int64_t s, StripPre<MAXC>& p) {
-    p.row = perm[s * 64 + lane];
-    p.dslot = dslots[s * 64 + lane];
-    const int nq = 8 * slice_w[s];
-    const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + lidx_ptr[s]);
+  auto load_nid = [&](const SliceRec& R, int32_t(&nid)[4]) {
+    const int nu = (int)(R.meta & 0xFFFFu);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nid[k] = snode[(int64_t)R.snode_off + max(min(lane + 64 * k, nu - 1), 0)];
+  };
+  auto load_rows = [&](const SliceRec& R, StripPre<MAXC>& p) {
+    const int64_t q = (int64_t)R.sl * 64 + lane;
+    p.row = perm[q];
+    p.dl = pos_dl[q];
+    p.rb = pos_rb[q];
+    const int nq = 8 * (int)((R.meta >> 16) & 0xFFu);
+    const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R.lidx_off);
     p.l0 = ls[max(min(lane, nq - 1), 0)];
     p.l1 = ls[max(min(lane + 64, nq - 1), 0)];
-    const int64_t u0 = snode_ptr[s];
-    const int nu = (int)(snode_ptr[s + 1] - u0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) p.nid[k] = snode[u0 + max(min(lane + 64 * k, nu - 1), 0)];
-    const int nc = (strip_n[s] + 15) >> 4;
-    const u32x4* sp = reinterpret_cast<const u32x4*>(strip + strip_ptr[s]) + lane;
+    const int nc = (int)((R.meta >> 24) + 15) >> 4;
+    const u32x4* sp = reinterpret_cast<const u32x4*>(strip + (int64_t)R.strip_off * 1024) + lane;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
   };
-  auto level2 = [&](StripPre<MAXC>& p) {
-#if AFEM_ABL == 6  // ablation: no dependent (second-level) loads; rows not stored (len 0; diagonals land in vals[0..63])
-    p.rb = 0;
-    p.len = 0;
-    p.xi = V3{ 0.5, 0.5, 0.5 };
-#pragma unroll
-    for (int k = 0; k < 4; ++k) p.x[k] = p.y[k] = p.z[k] = (double)p.nid[k] * 1e-7;
-    return;
-#endif
-    const bool act = p.row >= 0;
-    const int32_t r = act ? p.row : 0;
-    const int64_t b = row_ptr[r];
-    const int64_t e = row_ptr[r + 1];
-    p.rb = act ? b : 0;
-    p.len = act ? (int)(e - b) : 0;
-    p.xi = ld3(coords, r);
+  auto gather = [&](const int32_t(&nid)[4], StripPre<MAXC>& p) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      p.x[k] = coords[3 * (int64_t)p.nid[k]];
-      p.y[k] = coords[3 * (int64_t)p.nid[k] + 1];
-      p.z[k] = DIMC == 3 ? coords[3 * (int64_t)p.nid[k] + 2] : 0.0;
+      p.x[k] = coords[3 * (int64_t)nid[k]];
+      p.y[k] = coords[3 * (int64_t)nid[k] + 1];
+      p.z[k] = DIMC == 3 ? coords[3 * (int64_t)nid[k] + 2] : 0.0;
     }
   };
 
   StripPre<MAXC> cur, nxt;
-  level1(sl, cur);
-  level2(cur);
+  int32_t nid1[4], nid2[4];
+  {
+    int32_t nid0[4];
+    load_nid(R0, nid0);
+    load_rows(R0, cur);
+    gather(nid0, cur);
+    load_nid(R1, nid1);
+  }
   // drain the prologue loads: the loop header then inherits only the
   // back-edge's pending ops (loads a slice old, the stores), so the staging
   // waits count past the stores instead of on them
   __builtin_amdgcn_s_waitcnt(0);
   for (;;) {
-    const unsigned long long t2 = claim_issue();   // read at the end of this iteration
-    const int64_t snx = in < r1 ? slist[in] : sl;  // prefetch target (itself when done)
-    const int nsteps = strip_n[sl];  // uniform over the wave
-    const int W = slice_w[sl];
-    const int64_t u0 = snode_ptr[sl];
-    const int nu = (int)(snode_ptr[sl + 1] - u0);
+    const unsigned long long t4 = claim_issue();    // read at the end of this iteration
+    const SliceRec R3 = recs[p3 < r1 ? p3 : p0];    // scalar load, used two iterations later
+    const int nsteps = (int)(R0.meta >> 24);  // uniform over the wave
+    const int W = (int)((R0.meta >> 16) & 0xFFu);
+    const int64_t u0 = R0.snode_off;
+    const int nu = (int)(R0.meta & 0xFFFFu);
 
-    // ---- stage slice sl from registers (+ the rare overflow beyond 256 nodes / 16 slots)
+    // ---- stage slice p0 from registers (+ the rare overflow beyond 256 nodes / 16 slots)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int idx = max(min(lane + 64 * k, nu - 1), 0);
@@ -786,21 +777,27 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
       dst[max(min(lane, nq - 1), 0)] = cur.l0;
       dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
       if (!UNI && nq > 128) {
-        const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + lidx_ptr[sl]);
+        const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R0.lidx_off);
         for (int q = lane + 128; q < nq; q += 64) dst[q] = ls[q];
       }
       double2* a2 = reinterpret_cast<double2*>(acc);
       for (int q = lane; q < 32 * W; q += 64) a2[q] = make_double2(0.0, 0.0);
     }
     wave_sync_lds();
-    level1(snx, nxt);
+    load_rows(R1, nxt);
+    gather(nid1, nxt);
+    load_nid(R2, nid2);
 
     const int32_t row = cur.row;
     const bool active = row >= 0;
     const int64_t rb = cur.rb;
-    const int len = cur.len;
-    const V3 xi = cur.xi;
-    const uint32_t dslot = cur.dslot;
+    const int len = (int)(cur.dl >> 8);
+    const uint32_t dslot = cur.dl & 0xFFu;
+    // the row's own coordinates: its diagonal column is one of the slice's nodes
+    const V3 xi = [&] {
+      const double* q = cxyz + DIMC * (int)li[dslot * 64 + lane];
+      return V3{ q[0], q[1], DIMC == 3 ? q[2] : 0.0 };
+    }();
     double macc = 0.0;
     // window state (zero vectors: finite arithmetic on priming / padding
     // steps); cN = e_P x e_R = -c_Q is kept instead of c_Q (no negations)
@@ -880,7 +877,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
       // uniform strip: steps 0,1 prime the window (no cell), every later step
       // emits; the shift/swap bit is a scalar (one branch per step, both arms
       // straight-line code; only the kept node's registers move on a shift)
-      const uint64_t pat = spat[sl];
+      const uint64_t pat = R0.pat;
       auto ustep = [&](auto swap_c, uint32_t byte, V3 xd, bool swp) {
         constexpr int SWAP = decltype(swap_c)::value;  // 1 swap, 0 shift, -1 select on swp
         double* const aD = acc_lane + 64 * (byte & 63u);
@@ -965,9 +962,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
         else ustep(std::integral_constant<int, 0>{}, byte_at(j), xc, false);
         xc = xn;
         u1 = u2;
-        if (j == 11) level2(nxt);
       }
-      if (nsteps <= (UMODE == 1 ? 10 : 8)) level2(nxt);  // the loop ended before step 11
     }
     else {
       int u1 = lidx_of(byte_at(0));
@@ -981,10 +976,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
         step(byte_at(j), xc);
         xc = xn;
         u1 = u2;
-        // next slice's level-2 loads: ~12 steps after its level-1 loads were issued
-        if (j == 11) level2(nxt);
       }
-      if (nsteps <= 8) level2(nxt);  // the loop ended before step 11
     }
 
     // ---- RHS (unconditional store: idle lanes repeat an active lane's store)
@@ -997,44 +989,25 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
     }
     wave_sync_lds();
 
-    // ---- diagonal + write-back, direct: each lane stores its own row from
-    // registers, two values per 16-B store (dword-aligned stores are legal);
-    // the rows of a slice lie in a few contiguous runs, so the lines are
-    // completed in L2 within the slice and leave as full lines.  The diagonal
-    // slot is zeroed first so the row sum needs no per-slot test (the slots
-    // past the row's end stay 0), then rewritten with -sum.
-    if ((UNI || W <= MAXW) && !wb_flat) {
-      const uint32_t dsl = active ? dslot : 0xFFu;
-      if (dsl != 0xFFu) acc_lane[64 * dsl] = 0.0;
-      double rv[MAXW];
+    // ---- diagonal + write-back through a flat LDS image (as k_assemble_p1;
+    // the map overlays the coordinates).  (Per-lane 16-B stores straight from
+    // registers measured ~2% slower on C2.)
+#if AFEM_ABL == 8  // ablation: no value write-back (LDS image and stores)
+    if (acc_lane[0] == 12345.678) vals[rb] = acc_lane[64];
+    wave_sync_lds();
+    if (p1 >= r1) break;
+    p0 = p1;
+    p1 = p2;
+    p2 = p3;
+    p3 = claim_get(t4);
+    R0 = R1;
+    R1 = R2;
+    R2 = R3;
+    cur = nxt;
 #pragma unroll
-      for (int t = 0; t < MAXW; ++t) rv[t] = acc_lane[64 * min(t, W - 1)];
-      double sum = 0.0;
-#pragma unroll
-      for (int t = 0; t < MAXW; ++t)
-        if (t < W) sum += rv[t];  // uniform bound
-      double* const rowp = vals + rb;
-#if AFEM_ABL == 4  // ablation: no value stores
-      if (sum == 12345.678) rowp[0] = sum;
-      if (false)
+    for (int k = 0; k < 4; ++k) nid1[k] = nid2[k];
+    continue;
 #endif
-#pragma unroll
-      for (int t = 0; t < MAXW; t += 2) {
-        if (t < W) {  // uniform
-          if (t + 1 < len) *reinterpret_cast<DPair*>(rowp + t) = DPair{ rv[t], rv[t + 1] };
-          else if (t < len) rowp[t] = rv[t];
-        }
-      }
-      if (dsl != 0xFFu) rowp[dsl] = -sum;
-      wave_sync_lds();
-      if (in >= r1) break;
-      sl = snx;
-      in = claim_get(t2);
-      cur = nxt;
-      continue;
-    }
-    // ---- diagonal + write-back through a flat LDS image (default; as
-    // k_assemble_p1; the map overlays the coordinates)
     int fp = len;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1046,32 +1019,52 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
     uint16_t* map = reinterpret_cast<uint16_t*>(cxyz);
     const uint32_t dsl = active ? dslot : 0xFFu;
     if (UNI || W <= MAXW) {
+      // The diagonal accumulator is zeroed first (on the uniform path it holds
+      // the padding steps' sink values): the row sum then runs over all W
+      // slots with no per-slot test (slots past the row's end stay 0, and
+      // adding +0 changes no bits), and the diagonal (-sum) is written after
+      // the row's other values.  The map gives every flat position its value
+      // index in `vals` (32 bits: nnz < 2^32, checked on the host).
+      if (active) acc_lane[64 * dslot] = 0.0;
       double rv[MAXW];
 #pragma unroll
       for (int t = 0; t < MAXW; ++t) rv[t] = acc_lane[64 * min(t, W - 1)];
       double sum = 0.0;
 #pragma unroll
       for (int t = 0; t < MAXW; ++t)
-        if (t < len && t != (int)dsl) sum += rv[t];
+        if (t < W) sum += rv[t];  // uniform bound
+#if AFEM_WB == 1  // diagnostic: per-lane 16-B stores straight from registers
+      double* const rowp = vals + rb;
 #pragma unroll
-      for (int t = 0; t < MAXW; ++t)
-        if (t == (int)dsl) rv[t] = -sum;
+      for (int t = 0; t < MAXW; t += 2) {
+        if (t < W) {
+          if (t + 1 < len) {
+            rowp[t] = rv[t];
+            rowp[t + 1] = rv[t + 1];
+          }
+          else if (t < len) rowp[t] = rv[t];
+        }
+      }
+      if (active) rowp[dslot] = -sum;
+      (void)fp;
+      (void)total;
+#else
+      uint32_t* const map32 = reinterpret_cast<uint32_t*>(cxyz);
       wave_sync_lds();  // every lane's reads before the overlapping flat writes
 #pragma unroll
       for (int t = 0; t < MAXW; ++t)
         if (t < len) {
           acc[fp + t] = rv[t];
-          map[fp + t] = (uint16_t)(t * 64 + lane);
+          map32[fp + t] = (uint32_t)(rb + t);
         }
-      rbs[lane] = rb;
+      if (active) acc[fp + dslot] = -sum;
       wave_sync_lds();
 #pragma unroll
       for (int k = 0; k < MAXW; ++k) {
         const int P = min(64 * k + lane, total - 1);
-        const double v = acc[P];
-        const int m = map[P];
-        vals[rbs[m & 63] + (m >> 6)] = v;
+        vals[map32[P]] = acc[P];
       }
+#endif
     }
     else {
       if (dsl != 0xFFu) {
@@ -1090,10 +1083,17 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
       }
     }
     wave_sync_lds();
-    if (in >= r1) break;
-    sl = snx;
-    in = claim_get(t2);
+    if (p1 >= r1) break;
+    p0 = p1;
+    p1 = p2;
+    p2 = p3;
+    p3 = claim_get(t4);
+    R0 = R1;
+    R1 = R2;
+    R2 = R3;
     cur = nxt;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nid1[k] = nid2[k];
   }
 }
 
@@ -1532,7 +1532,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
     const char* e = getenv("AFEM_ASSEMBLY_STRIPS");
     return !(e && atoi(e) == 0);
   }();
-  if (strips_env && s.strip_ok && s.max_strip_c <= 4 &&
+  if (strips_env && s.strip_ok && s.rec_ok && s.nnz < (int64_t(1) << 32) && s.max_strip_c <= 4 &&
       strip_tile_bytes(dimc, s.max_slice_nodes, s.max_slice_w) <= kTileLdsMax) {
     const size_t shm_s = (size_t)strip_tile_bytes(dimc, s.max_slice_nodes, s.max_slice_w);
     static std::map<std::pair<const void*, size_t>, int> occ_s;
@@ -1541,14 +1541,10 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
     const int umode = ue ? atoi(ue) : 1;               // 0 off, 1 branches, 2 selects
     const bool uni_env = umode != 0;
     const bool use_uni = uni_env && s.n_uni > 0;
-    // AFEM_ASSEMBLY_WB=direct: per-lane 16-B stores from registers (diagnostic;
-    // the default writes through the flat LDS image, ~2% faster on C2)
-    const char* we = getenv("AFEM_ASSEMBLY_WB");
-    const int wb_flat = (we && std::string(we) == "direct") ? 0 : 1;
     const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;
     if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);  // one counter per XCD, 128-B apart, per launch
     AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
-    auto launch_s = [&](const void* fn, auto kern, int64_t n_list, const int32_t* list, unsigned long long* tk) {
+    auto launch_s = [&](const void* fn, auto kern, int64_t n_list, const SliceRec* list, unsigned long long* tk) {
       auto it = occ_s.find({ fn, shm_s });
       if (it == occ_s.end()) {
         int q = 0;
@@ -1558,30 +1554,29 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
       const int per_cu = occ_override() > 0 ? occ_override() : it->second;
       int64_t nblk = (int64_t)ctx.n_cu * per_cu;
       if (nblk > n_list) nblk = n_list < 8 ? 8 : n_list;
-      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, ctx.stream, n_list, list, s.spat.p, tk,
-                         s.max_slice_nodes, s.max_slice_w, s.perm.p, s.row_ptr.p, s.strip.p, s.strip_ptr.p,
-                         s.strip_n.p, s.dslot.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p, s.snode.p,
-                         b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, wb_flat);
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, ctx.stream, n_list, list, tk,
+                         s.max_slice_nodes, s.max_slice_w, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p,
+                         s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
     };
-    const int32_t* list_m = use_uni ? s.slist_m.p : s.slist_all.p;
+    const SliceRec* list_m = use_uni ? s.rec_m.p : s.rec_all.p;
 #define AFEM_STRIP_K(NV_, C_, W_, U_, N_, L_, T_)                                                                      \
   launch_s(reinterpret_cast<const void*>(&k_assemble_strip<NV_, C_, W_, U_>), k_assemble_strip<NV_, C_, W_, U_>, N_, \
            L_, T_)
     const bool small = s.max_strip_c <= 2 && s.max_slice_w <= 16;
     if (nv == 4) {
       if (small) {
-        if (use_uni && umode == 2) AFEM_STRIP_K(4, 2, 16, 2, s.n_uni, s.slist_u.p, s.tickets.p);
-        else if (use_uni) AFEM_STRIP_K(4, 2, 16, 1, s.n_uni, s.slist_u.p, s.tickets.p);
+        if (use_uni && umode == 2) AFEM_STRIP_K(4, 2, 16, 2, s.n_uni, s.rec_u.p, s.tickets.p);
+        else if (use_uni) AFEM_STRIP_K(4, 2, 16, 1, s.n_uni, s.rec_u.p, s.tickets.p);
         if (n_mix > 0) AFEM_STRIP_K(4, 2, 16, 0, n_mix, list_m, s.tickets.p + 128);
       }
       else {
-        if (use_uni) AFEM_STRIP_K(4, 4, 32, 1, s.n_uni, s.slist_u.p, s.tickets.p);
+        if (use_uni) AFEM_STRIP_K(4, 4, 32, 1, s.n_uni, s.rec_u.p, s.tickets.p);
         if (n_mix > 0) AFEM_STRIP_K(4, 4, 32, 0, n_mix, list_m, s.tickets.p + 128);
       }
     }
     else {
-      if (small) AFEM_STRIP_K(3, 2, 16, 0, s.n_slices, s.slist_all.p, s.tickets.p + 128);
-      else AFEM_STRIP_K(3, 4, 32, 0, s.n_slices, s.slist_all.p, s.tickets.p + 128);
+      if (small) AFEM_STRIP_K(3, 2, 16, 0, s.n_slices, s.rec_all.p, s.tickets.p + 128);
+      else AFEM_STRIP_K(3, 4, 32, 0, s.n_slices, s.rec_all.p, s.tickets.p + 128);
     }
 #undef AFEM_STRIP_K
     AFEM_LAUNCHED();

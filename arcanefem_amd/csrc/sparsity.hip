@@ -497,6 +497,20 @@ __global__ __launch_bounds__(64) void k_strip_rows(int64_t n_pos, int nv, const 
   for (int j = 0; j < steps; ++j) out[(int64_t)(j >> 4) * 1024 + (j & 15)] = j < total ? buf[j] : (uint8_t)(dslot | (3 << 6));
 }
 
+// per position: the row's CSR offset, and its diagonal slot | length << 8
+__global__ void k_pos_rows(int64_t n_pos, const int32_t* __restrict__ perm, const int64_t* __restrict__ row_ptr,
+                           const uint8_t* __restrict__ dslot, int64_t* __restrict__ pos_rb,
+                           uint32_t* __restrict__ pos_dl)
+{
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pos) return;
+  const int32_t r = perm[p];
+  const int64_t b = r >= 0 ? row_ptr[r] : 0;
+  const int64_t len = r >= 0 ? row_ptr[r + 1] - b : 0;
+  pos_rb[p] = b;
+  pos_dl[p] = (uint32_t)dslot[p] | (uint32_t)len << 8;
+}
+
 // per slice: does every lane run the same strip topology?  Uniform = all 64
 // rows active, one strip (kinds 2,2 then 0/1 only), the same length, the same
 // shift/swap sequence.  Out: flag (1 = uniform) and the swap bits (bit j = step
@@ -734,6 +748,12 @@ void build_structure(Mesh& m, Structure& s)
                          s.perm.p, m.cell_node.p, nc_ptr.p, nc.p, s.row_ptr.p, s.cols.p, nullptr, s.strip_ptr.p,
                          s.strip_c.p, s.strip.p, s.dslot.p);
       AFEM_LAUNCHED();
+      // per-position row data of the strip assembly
+      s.pos_rb.alloc(n_pos);
+      s.pos_dl.alloc(n_pos);
+      hipLaunchKernelGGL(k_pos_rows, dim3(grid_for(n_pos, 256)), dim3(256), 0, ctx.stream, n_pos, s.perm.p,
+                         s.row_ptr.p, s.dslot.p, s.pos_rb.p, s.pos_dl.p);
+      AFEM_LAUNCHED();
       // uniform / mixed slice lists (tets; triangles use the general path)
       DevBuf<uint8_t> uflag;
       uflag.alloc(s.n_slices);
@@ -741,23 +761,44 @@ void build_structure(Mesh& m, Structure& s)
       hipLaunchKernelGGL(k_strip_classify, dim3((unsigned)s.n_slices), dim3(64), 0, ctx.stream, s.n_slices, s.perm.p,
                          s.strip.p, s.strip_ptr.p, s.strip_n.p, s.snode_ptr.p, s.slice_w.p, uflag.p, s.spat.p);
       AFEM_LAUNCHED();
-      std::vector<uint8_t> hu((size_t)s.n_slices);
-      AFEM_HIP(hipMemcpyAsync(hu.data(), uflag.p, hu.size(), hipMemcpyDeviceToHost, ctx.stream));
+      const size_t ns = (size_t)s.n_slices;
+      std::vector<uint8_t> hu(ns);
+      std::vector<int32_t> hw(ns), hn(ns);
+      std::vector<int64_t> hl(ns + 1), hs(ns + 1), hsn(ns + 1);
+      std::vector<uint64_t> hp(ns);
+      AFEM_HIP(hipMemcpyAsync(hu.data(), uflag.p, ns, hipMemcpyDeviceToHost, ctx.stream));
+      AFEM_HIP(hipMemcpyAsync(hw.data(), s.slice_w.p, ns * 4, hipMemcpyDeviceToHost, ctx.stream));
+      AFEM_HIP(hipMemcpyAsync(hn.data(), s.strip_n.p, ns * 4, hipMemcpyDeviceToHost, ctx.stream));
+      AFEM_HIP(hipMemcpyAsync(hl.data(), s.lidx_ptr.p, (ns + 1) * 8, hipMemcpyDeviceToHost, ctx.stream));
+      AFEM_HIP(hipMemcpyAsync(hs.data(), s.strip_ptr.p, (ns + 1) * 8, hipMemcpyDeviceToHost, ctx.stream));
+      AFEM_HIP(hipMemcpyAsync(hsn.data(), s.snode_ptr.p, (ns + 1) * 8, hipMemcpyDeviceToHost, ctx.stream));
+      AFEM_HIP(hipMemcpyAsync(hp.data(), s.spat.p, ns * 8, hipMemcpyDeviceToHost, ctx.stream));
       ctx.sync();
-      std::vector<int32_t> lu, lm;
-      for (int64_t i = 0; i < s.n_slices; ++i) (hu[(size_t)i] && nv == 4 ? lu : lm).push_back((int32_t)i);
-      s.n_uni = (int64_t)lu.size();
-      s.n_mix = (int64_t)lm.size();
-      s.slist_all.alloc(s.n_slices);
-      hipLaunchKernelGGL(k_perm_identity, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, s.n_slices,
-                         s.n_slices, s.slist_all.p);
-      AFEM_LAUNCHED();
-      s.slist_u.alloc(s.n_uni > 0 ? s.n_uni : 1);
-      s.slist_m.alloc(s.n_mix > 0 ? s.n_mix : 1);
-      if (s.n_uni > 0)
-        AFEM_HIP(hipMemcpyAsync(s.slist_u.p, lu.data(), lu.size() * 4, hipMemcpyHostToDevice, ctx.stream));
-      if (s.n_mix > 0)
-        AFEM_HIP(hipMemcpyAsync(s.slist_m.p, lm.data(), lm.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+      s.rec_ok = hl[ns] < (int64_t(1) << 32) && hs[ns] / 1024 < (int64_t(1) << 32) && hsn[ns] < (int64_t(1) << 32);
+      std::vector<SliceRec> ru, rm, ra;
+      for (size_t i = 0; i < ns && s.rec_ok; ++i) {
+        SliceRec r{};
+        r.sl = (uint32_t)i;
+        r.lidx_off = (uint32_t)hl[i];
+        r.strip_off = (uint32_t)(hs[i] / 1024);
+        r.snode_off = (uint32_t)hsn[i];
+        const int64_t nu = hsn[i + 1] - hsn[i];
+        if (nu > 65535 || hw[i] > 255 || hn[i] > 255) s.rec_ok = false;
+        r.meta = (uint32_t)nu | (uint32_t)hw[i] << 16 | (uint32_t)hn[i] << 24;
+        r.pat = hp[i];
+        ra.push_back(r);
+        (hu[i] && nv == 4 ? ru : rm).push_back(r);
+      }
+      s.n_uni = (int64_t)ru.size();
+      s.n_mix = (int64_t)rm.size();
+      auto upload = [&](DevBuf<SliceRec>& d, const std::vector<SliceRec>& h) {
+        d.alloc(h.empty() ? 1 : h.size());
+        if (!h.empty())
+          AFEM_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(SliceRec), hipMemcpyHostToDevice, ctx.stream));
+      };
+      upload(s.rec_u, ru);
+      upload(s.rec_m, rm);
+      upload(s.rec_all, ra);
       ctx.sync();
     }
     else {

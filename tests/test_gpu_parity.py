@@ -113,10 +113,6 @@ def test_uniform_strip_variant(ctx, monkeypatch):
     rows, cols, v_gen = bsr.download()
     assert np.array_equal(v_uni, v_gen), "uniform and general strip kernels differ"
     assert np.array_equal(r_uni, ls.rhs_host())
-    monkeypatch.setenv("AFEM_ASSEMBLY_WB", "direct")  # per-lane stores from registers
-    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable())
-    _, _, v_flat = bsr.download()
-    assert np.array_equal(v_uni, v_flat), "flat and direct write-back differ"
     cells, coords, _ = mesh.download()
     orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
     ovals, orhs = O.assemble_poisson(mesh.n_own_nodes, cells, coords, orp, ocols, 5.5)
