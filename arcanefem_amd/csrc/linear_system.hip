@@ -490,6 +490,12 @@ SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows, const int32_t*
     pl.max_seg = (int64_t)hm;
     pl.wide = mode == 0 && cols && vals && ((uintptr_t)cols & 15) == 0 && ((uintptr_t)vals & 15) == 0;
   }
+  else if (mode == 0 && hm >= 16ull * (unsigned long long)kThreads) {
+    // long rows (block-3 elasticity: 45 non-zeros per scalar row): segments do
+    // not fit LDS; 16 lanes per row keep the column/value reads coalesced
+    pl.rpb = -1;
+    pl.nblocks = (n_rows + 16 * kSpmvRpg - 1) / (16 * kSpmvRpg);
+  }
   return pl;
 }
 

@@ -42,7 +42,85 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_assembly_C2.json"))
+    ap.add_argument("--no-extras", action="store_true", help="skip the C3 / C5 side measurements")
+    ap.add_argument("--c3-n", type=int, default=170, help="C3 block-3 elasticity box (170 -> 5.0M nodes)")
+    ap.add_argument("--c5-n", type=int, default=100, help="C5 elastodynamics box (100 -> 1.03M nodes)")
+    ap.add_argument("--c5-steps", type=int, default=5)
     return ap.parse_args()
+
+
+def elasticity_c3(ctx, af, n, reps=10, warmup=2):
+    """BASELINE config C3: block-3 P1 elasticity on tetrahedra (BSR, ordered per
+    block), stiffness + body force fused, on fixed sparsity; kernel time from
+    HIP events around each launch.  Algorithmic bytes per launch: incidence
+    table 4*nv*Ncell, coordinates 24 N, row offsets 8 (N+1), block columns
+    4 nnz_b, block values 72 nnz_b, RHS 24 N."""
+    E, nu = 21.0e5, 0.28
+    lam = E * nu / ((1 + nu) * (1 - 2 * nu))
+    mu2 = E / (1 + nu)
+    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+    bsr = af.BSRFormat(mesh, 3).initialize(False)
+    t0 = time.perf_counter()
+    bsr.computeSparsity()
+    ctx.synchronize()
+    sp_ms = (time.perf_counter() - t0) * 1e3
+    rhs = ctx.malloc(8 * 3 * mesh.n_own_nodes)
+    f = (0.0, 0.0, -1.0)
+    for _ in range(warmup):
+        bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs)
+    ctx.synchronize()
+    for i in range(reps):
+        ctx.event_record(200 + 2 * i)
+        bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs)
+        ctx.event_record(201 + 2 * i)
+    ctx.synchronize()
+    kms = float(np.mean([ctx.event_elapsed(200 + 2 * i, 201 + 2 * i) for i in range(reps)]))
+    st = bsr.stats()
+    v = bsr.view()
+    nnz_b = v.nnz_blocks
+    n_own, n_loc = mesh.n_own_nodes, mesh.n_nodes
+    ab = 4 * int(st["n_incidences"]) + 24 * n_loc + 8 * (n_own + 1) + 76 * nnz_b + 24 * n_own
+    out = {"config": f"C3 elasticity block-3 P1 tets, Kuhn box n={n} ({n_own} nodes, {3 * n_own} DoF, "
+                     f"{mesh.n_cells} tets), BSR per-block, stiffness + body force",
+           "value": round(3 * n_own / (kms * 1e-3) / 1e6, 1), "unit": "MDoF/s", "kernel_ms": round(kms, 4),
+           "kernel": "k_assemble_elast_tet",
+           "roofline": {"bound": "hbm", "achieved": round(ab / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ab / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "algorithmic_bytes_per_launch": int(ab)},
+           "sparsity_ms": round(sp_ms, 1)}
+    ctx.free(rhs)
+    bsr.close()
+    mesh.close()
+    return out
+
+
+def elastodynamics_c5(ctx, af, n, steps):
+    """BASELINE config C5 on one GPU: 3D Newmark elastodynamics, every step
+    re-assembles c0 M + K and the body-force RHS on the fixed block-3
+    structure, adds M (c0 U + c3 V + c4 A), clamps x = 0 by penalty, solves by
+    Jacobi-PCG (rtol 1e-8) and updates U, V, A on the device."""
+    from arcanefem_amd.elastodynamics import Elastodynamics3D
+
+    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+    _, coords, _ = mesh.download()
+    fixed = np.nonzero(coords[: mesh.n_own_nodes, 0] == 0.0)[0]
+    dyn = Elastodynamics3D(ctx, mesh, E=21.0e5, nu=0.28, rho=1.0, dt=1.0e-3, body_force=(0.0, 0.0, -1.0),
+                           fixed_nodes=fixed, rtol=1e-8)
+    dyn.step()
+    ctx.synchronize()
+    iters = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        iters.append(int(dyn.step()["iterations"]))
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    out = {"config": f"C5 elastodynamics 3D Newmark, Kuhn box n={n} ({mesh.n_own_nodes} nodes, "
+                     f"{3 * mesh.n_own_nodes} DoF), reassembly every step + Jacobi-PCG rtol 1e-8",
+           "steps_per_s": round(1.0 / dt, 2), "ms_per_step": round(dt * 1e3, 2),
+           "cg_iterations_per_step": float(np.mean(iters))}
+    dyn.close()
+    mesh.close()
+    return out
 
 
 def algorithmic_bytes(n_inc, n_local, n_own, nnz):
@@ -195,6 +273,10 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.cpu_baseline_n, args.cpu_baseline_seconds)
+        extras = {}
+        if not args.no_extras and world == 1:
+            extras["c3"] = elasticity_c3(ctx, af, args.c3_n)
+            extras["c5"] = elastodynamics_c5(ctx, af, args.c5_n, args.c5_steps)
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -237,6 +319,7 @@ def main():
             "cg_device_ms": round(st["solve_ms"], 3),
             "sparsity_ms": round(sparsity_ms, 1),
             "setup_s": round(setup_s, 2),
+            **extras,
         }
         print(json.dumps(out), flush=True)
     ctx.free(dbottom)

@@ -3,7 +3,7 @@
 # time per environment setting given as arguments ("VAR=val VAR2=val ...").
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-B="bench.py --steps 20 --warmup 3 --cg-iters 2 --no-cpu-baseline"
+B="bench.py --steps 20 --warmup 3 --cg-iters 2 --no-cpu-baseline --no-extras"
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 gpurun_out/tests.log; exit 1; }
 tail -1 gpurun_out/tests.log
 for cfg in "$@"; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Memory-side counters of the assembly kernel for ablation modes 0 and 1.
 OUT=${1:-gpurun_out/pmem}
-B="bench.py --steps 6 --warmup 1 --cg-iters 2 --no-cpu-baseline"
+B="bench.py --steps 6 --warmup 1 --cg-iters 2 --no-cpu-baseline --no-extras"
 K='k_assemble_p1'
 mkdir -p $OUT
 pass() {  # name, counters...

@@ -5,7 +5,7 @@
 # Summarise with: python tools/pmc_summary.py <out_dir> <kernel_regex>
 OUT=${1:-gpurun_out/pmc}
 K=${2:-k_assemble_p1}
-B="bench.py --steps 6 --warmup 1 --cg-iters 2 --no-cpu-baseline"
+B="bench.py --steps 6 --warmup 1 --cg-iters 2 --no-cpu-baseline --no-extras"
 export TMPDIR=/tmp
 mkdir -p $OUT
 pass() {  # name, counters...
