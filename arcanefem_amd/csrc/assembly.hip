@@ -642,6 +642,16 @@ __host__ __device__ constexpr int64_t strip_tile_bytes(int dimc, int64_t u_cap, 
 {
   return 8 * 64 * w_cap + strip_coord_bytes(dimc, u_cap, w_cap) + 2 * 64 * w_cap + 512;
 }
+// block-3 tile: accumulators [slot][3][lane], coordinates (doubling as the
+// u16 write-back map: 3 values per slot), column indices, per-lane value bases
+__host__ __device__ constexpr int64_t elast_coord_bytes(int64_t u_cap, int64_t w_cap)
+{
+  return ((24 * u_cap > 6 * 64 * w_cap ? 24 * u_cap : 6 * 64 * w_cap) + 15) & ~int64_t(15);
+}
+__host__ __device__ constexpr int64_t elast_tile_bytes(int64_t u_cap, int64_t w_cap)
+{
+  return 3 * 8 * 64 * w_cap + elast_coord_bytes(u_cap, w_cap) + 2 * 64 * w_cap + 512;
+}
 
 // UNI = true: the slices of `recs` (the uniform list) whose 64 rows share one strip topology
 // (same length, one strip, same shift/swap sequence `spat`: every interior
@@ -1097,6 +1107,281 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
   }
 }
 
+// ---------------------------------------------------------------- block-3 elasticity, persistent strips
+// k_assemble_elast_tet restructured like k_assemble_strip: persistent waves
+// claim work items (slice, component row ci) per XCD (the three items of a
+// slice are adjacent: one L2 serves their shared coordinates), the same
+// four-stage prefetch pipeline over 32-B slice records, and a write-back
+// through a flat LDS image (per-row layout: the 3*len values of (row, ci)
+// are contiguous; per-block layout: runs of 3).  The wave works in a frame
+// whose axes are cyclically rotated by ci (coordinates staged as
+// (x_ci, x_ci+1, x_ci+2)): its component row is always "x", no per-step
+// component selects; value (t, k) of the rotated frame is column
+// (ci + k) % 3 of the block.  A cyclic axis permutation is a rotation, the
+// material isotropic: the entries are the same numbers (up to the order of
+// the three products in a dot product).
+template <int MAXC, int MAXW>
+__global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, const SliceRec* __restrict__ recs,
+                                                             unsigned long long* __restrict__ tickets, int u_cap,
+                                                             int w_cap, bool per_block,
+                                                             const int32_t* __restrict__ perm,
+                                                             const int64_t* __restrict__ pos_rb,
+                                                             const uint32_t* __restrict__ pos_dl,
+                                                             const uint8_t* __restrict__ strip,
+                                                             const uint16_t* __restrict__ lidx,
+                                                             const int32_t* __restrict__ snode,
+                                                             const double* __restrict__ coords, double lambda,
+                                                             double mu, double c0, double fx, double fy, double fz,
+                                                             double* __restrict__ vals, double* __restrict__ rhs)
+{
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* acc = reinterpret_cast<double*>(smem);  // [slot][k][lane]
+  double* cxyz = reinterpret_cast<double*>(smem + 3 * 8 * 64 * (int64_t)w_cap);
+  const int64_t cbytes = elast_coord_bytes(u_cap, w_cap);
+  uint16_t* li = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(cxyz) + cbytes);
+  int64_t* rbs = reinterpret_cast<int64_t*>(reinterpret_cast<unsigned char*>(li) + 2 * 64 * (int64_t)w_cap);
+  const int lane = threadIdx.x;
+  const int xcd = (int)(blockIdx.x & 7);
+  const int64_t r0 = n_items * xcd / 8, r1 = n_items * (xcd + 1) / 8;
+  auto claim_issue = [&]() -> unsigned long long {
+    unsigned long long t = 0;
+    if (lane == 0) t = atomicAdd(tickets + 16 * xcd, 1ull);
+    return t;
+  };
+  auto claim_get = [&](unsigned long long t) -> int64_t {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)t);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(t >> 32));
+    return r0 + (int64_t)(((uint64_t)hi << 32) | lo);
+  };
+  int64_t p0 = claim_get(claim_issue());
+  if (p0 >= r1) return;
+  int64_t p1 = claim_get(claim_issue());
+  int64_t p2 = claim_get(claim_issue());
+  int64_t p3 = claim_get(claim_issue());
+  SliceRec R0 = recs[p0 / 3];
+  SliceRec R1 = recs[(p1 < r1 ? p1 : p0) / 3];
+  SliceRec R2 = recs[(p2 < r1 ? p2 : p0) / 3];
+
+  auto load_nid = [&](const SliceRec& R, int32_t(&nid)[4]) {
+    const int nu = (int)(R.meta & 0xFFFFu);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nid[k] = snode[(int64_t)R.snode_off + max(min(lane + 64 * k, nu - 1), 0)];
+  };
+  auto load_rows = [&](const SliceRec& R, StripPre<MAXC>& p) {
+    const int64_t q = (int64_t)R.sl * 64 + lane;
+    p.row = perm[q];
+    p.dl = pos_dl[q];
+    p.rb = pos_rb[q];
+    const int nq = 8 * (int)((R.meta >> 16) & 0xFFu);
+    const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R.lidx_off);
+    p.l0 = ls[max(min(lane, nq - 1), 0)];
+    p.l1 = ls[max(min(lane + 64, nq - 1), 0)];
+    const int nc = (int)((R.meta >> 24) + 15) >> 4;
+    const u32x4* sp = reinterpret_cast<const u32x4*>(strip + (int64_t)R.strip_off * 1024) + lane;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
+  };
+  auto gather = [&](const int32_t(&nid)[4], StripPre<MAXC>& p) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      p.x[k] = coords[3 * (int64_t)nid[k]];
+      p.y[k] = coords[3 * (int64_t)nid[k] + 1];
+      p.z[k] = coords[3 * (int64_t)nid[k] + 2];
+    }
+  };
+  StripPre<MAXC> cur, nxt;
+  int32_t nid1[4], nid2[4];
+  {
+    int32_t nid0[4];
+    load_nid(R0, nid0);
+    load_rows(R0, cur);
+    gather(nid0, cur);
+    load_nid(R1, nid1);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  for (;;) {
+    const unsigned long long t4 = claim_issue();
+    const SliceRec R3 = recs[(p3 < r1 ? p3 : p0) / 3];
+    const int ci = (int)(p0 % 3);  // component row (uniform)
+    const int nsteps = (int)(R0.meta >> 24);
+    const int W = (int)((R0.meta >> 16) & 0xFFu);
+    const int nu = (int)(R0.meta & 0xFFFFu);
+    // ---- stage: coordinates in the rotated frame, column indices, zero accumulators
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = max(min(lane + 64 * k, nu - 1), 0);
+      const double a = cur.x[k], b = cur.y[k], c = cur.z[k];
+      cxyz[3 * idx] = ci == 0 ? a : (ci == 1 ? b : c);
+      cxyz[3 * idx + 1] = ci == 0 ? b : (ci == 1 ? c : a);
+      cxyz[3 * idx + 2] = ci == 0 ? c : (ci == 1 ? a : b);
+    }
+    {
+      const int nq = 8 * W;
+      u32x4* dst = reinterpret_cast<u32x4*>(li);
+      dst[max(min(lane, nq - 1), 0)] = cur.l0;
+      dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
+      double2* a2 = reinterpret_cast<double2*>(acc);
+      for (int q = lane; q < 96 * W; q += 64) a2[q] = make_double2(0.0, 0.0);
+    }
+    wave_sync_lds();
+    load_rows(R1, nxt);
+    gather(nid1, nxt);
+    load_nid(R2, nid2);
+
+    const int32_t row = cur.row;
+    const bool active = row >= 0;
+    const int64_t rb = cur.rb;
+    const int len = (int)(cur.dl >> 8);
+    const uint32_t dslot = cur.dl & 0xFFu;
+    const uint16_t* lrow = li + lane;
+    const V3 xi = [&] {
+      const double* q = cxyz + 3 * (int)lrow[dslot * 64];
+      return V3{ q[0], q[1], q[2] };
+    }();
+    double macc = 0.0;
+    V3 eP{ 0.0, 0.0, 0.0 }, eQ{ 0.0, 0.0, 0.0 }, eR{ 0.0, 0.0, 0.0 };
+    V3 cP{ 0.0, 0.0, 0.0 }, cN{ 0.0, 0.0, 0.0 };
+    double* const acc_lane = acc + lane;
+    double* aP = acc_lane + 192 * dslot;
+    double* aQ = aP;
+    double* aR = aP;
+    auto lidx_of = [&](uint32_t byte) { return (int)lrow[(byte & 63u) * 64]; };
+    auto coord = [&](int u) {
+      const double* q = cxyz + 3 * u;
+      return V3{ q[0], q[1], q[2] };
+    };
+    auto sel = [](bool c, V3 a, V3 b) { return V3{ c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z }; };
+    auto keep = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
+    // entries (0, k) of K_rb in the rotated frame, c_r = -m (sign folded into s < 0)
+    auto block = [&](double* a, V3 m, V3 cb, double s, double mass) {
+      const double t = dot(m, cb);
+      const double A = lambda * m.x, B = mu * cb.x;
+      const double v0 = (A * cb.x + B * m.x) * s + (mu * t * s + mass);
+      const double v1 = (A * cb.y + B * m.y) * s;
+      const double v2 = (A * cb.z + B * m.z) * s;
+      atomicAdd(a, v0);
+      atomicAdd(a + 64, v1);
+      atomicAdd(a + 128, v2);
+    };
+    auto step = [&](uint32_t byte, V3 xd) {
+      const bool swap = (byte & 0xC0u) == 0x40u;
+      const uint64_t em = (uint64_t)0 - (uint64_t)(byte < 0x80u);
+      double* const aD = acc_lane + 192 * (byte & 63u);
+      const V3 eD = sub(xd, xi);
+      const V3 cRn = sel(swap, cN, cP);
+      eP = sel(swap, eP, eQ);
+      aP = swap ? aP : aQ;
+      eQ = eR;
+      aQ = aR;
+      eR = eD;
+      aR = aD;
+      cP = cross(eQ, eR);
+      cN = cross(eP, eR);
+      const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
+      const double meas = fabs(dot(eP, cP));
+      const double s = keep(em, -recip1(6.0 * meas));
+      const double mass = keep(em, c0 * meas * (1.0 / 120.0));
+      macc += keep(em, meas);
+      block(aP, m, cP, s, mass);
+      block(aQ, m, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+      block(aR, m, cRn, s, mass);
+    };
+    auto byte_at = [&](int j) -> uint32_t {
+      const u32x4 w = cur.ch[j >> 4];
+      const int q = (j >> 2) & 3;
+      const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
+      return (wq >> (8 * (j & 3))) & 0xFFu;
+    };
+    constexpr int NSTEP = 16 * MAXC;
+    {
+      int u1 = lidx_of(byte_at(0));
+      V3 xc = coord(u1);
+      u1 = lidx_of(byte_at(1));
+#pragma unroll
+      for (int j = 0; j < NSTEP; ++j) {
+        if ((j & 3) == 0 && j >= nsteps) break;
+        const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
+        const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
+        step(byte_at(j), xc);
+        xc = xn;
+        u1 = u2;
+      }
+    }
+    if (rhs && active) rhs[3 * (int64_t)row + ci] = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
+    wave_sync_lds();
+
+    // ---- diagonal block row + write-back through a flat LDS image
+    // (3*len values per lane; map: position -> lane | offset << 6 with the
+    // value index = rbs[lane] + offset: per block 9 rb + 3 ci + (9 t + j),
+    // per row 9 rb + 3 ci len + (3 t + j))
+    const int n3 = 3 * len;
+    int fp = n3;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(fp, o);
+      if (lane >= o) fp += t;
+    }
+    const int total = __shfl(fp, 63);
+    fp -= n3;
+    if (active) {
+      acc_lane[192 * dslot] = 0.0;
+      acc_lane[192 * dslot + 64] = 0.0;
+      acc_lane[192 * dslot + 128] = 0.0;
+    }
+    double rv[3 * MAXW];
+#pragma unroll
+    for (int t = 0; t < MAXW; ++t)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) rv[3 * t + k] = acc_lane[192 * min(t, W - 1) + 64 * k];
+    double sum[3] = { 0.0, 0.0, 0.0 };
+#pragma unroll
+    for (int t = 0; t < MAXW; ++t)
+      if (t < W)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sum[k] += rv[3 * t + k];
+    uint16_t* map = reinterpret_cast<uint16_t*>(cxyz);
+    wave_sync_lds();  // every lane's reads before the overlapping flat writes
+#pragma unroll
+    for (int t = 0; t < MAXW; ++t)
+      if (t < len) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          // value (t, k) of the rotated frame = block column (ci + k) % 3
+          const int j = k + ci < 3 ? k + ci : k + ci - 3;
+          acc[fp + 3 * t + j] = rv[3 * t + k];
+          map[fp + 3 * t + j] = (uint16_t)(lane | (per_block ? 9 * t + j : 3 * t + j) << 6);
+        }
+      }
+    if (active) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int j = k + ci < 3 ? k + ci : k + ci - 3;
+        acc[fp + 3 * (int)dslot + j] = -sum[k] + (k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0);
+      }
+    }
+    rbs[lane] = 9 * rb + 3 * ci * (per_block ? 1 : (int64_t)len);
+    wave_sync_lds();
+    for (int k = 0; k < 3 * MAXW; ++k) {
+      if (64 * k >= total) break;  // uniform
+      const int Pc = min(64 * k + lane, total - 1);
+      const int m = map[Pc];
+      vals[rbs[m & 63] + (m >> 6)] = acc[Pc];
+    }
+    wave_sync_lds();
+    if (p1 >= r1) break;
+    p0 = p1;
+    p1 = p2;
+    p2 = p3;
+    p3 = claim_get(t4);
+    R0 = R1;
+    R1 = R2;
+    R2 = R3;
+    cur = nxt;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nid1[k] = nid2[k];
+  }
+}
+
 // ---------------------------------------------------------------- block-3 elasticity (TETRA4), row strips
 // K_rb^{ij} = [lambda c_r,i c_b,j + mu (c_r,j c_b,i + delta_ij c_r.c_b)] / (6|det|)
 // (+ c0 |det|/120 delta_ij, the consistent mass V/20 (1 + delta_rb) for b != r):
@@ -1188,7 +1473,11 @@ __global__ __launch_bounds__(64) void k_assemble_elast_tet(int u_cap, int w_cap,
     atomicAdd(a + 64, v1);
     atomicAdd(a + 128, v2);
   };
+#if AFEM_ABL == 10  // ablation (block-3): staging and write-back only
+  for (int c = 0; 16 * c < 0 * nsteps; ++c) {
+#else
   for (int c = 0; 16 * c < nsteps; ++c) {
+#endif
     const u32x4 w = sp[(int64_t)c * 64];
     const uint32_t wv[4] = { w.x, w.y, w.z, w.w };
     for (int j = 0; j < 16; ++j) {
@@ -1227,6 +1516,9 @@ __global__ __launch_bounds__(64) void k_assemble_elast_tet(int u_cap, int w_cap,
         for (int jj = 0; jj < 3; ++jj) sum[jj] += acc_lane[192 * t + 64 * jj];
     for (int jj = 0; jj < 3; ++jj)
       acc_lane[192 * dslot + 64 * jj] = -sum[jj] + (jj == ci ? c0 * macc * (1.0 / 24.0) : 0.0);
+#if AFEM_ABL == 9  // ablation (block-3): no value stores
+    if (acc_lane[0] == 12345.678)
+#endif
     for (int t = 0; t < len; ++t)
       for (int jj = 0; jj < 3; ++jj)
         vals[per_block ? (rb + t) * 9 + 3 * ci + jj : rb * 9 + (int64_t)ci * 3 * len + 3 * t + jj] =
@@ -1679,10 +1971,36 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
                "block-3 P1 elasticity assembly needs NB_DOF = 3 on tetrahedra");
   AFEM_REQUIRE(s.strip_ok, AFEM_ERR_NOT_IMPL,
                "block-3 elasticity assembly needs row strips (rows of at most 64 blocks and 64 incident cells)");
+  const double fx = f ? f[0] : 0.0, fy = f ? f[1] : 0.0, fz = f ? f[2] : 0.0;
+  // persistent pipelined kernel (AFEM_ELAST_STRIP=0: the one-wave-per-item kernel, diagnostic)
+  const char* ee = getenv("AFEM_ELAST_STRIP");
+  const bool use_new = !(ee && atoi(ee) == 0);
+  if (use_new && s.rec_ok && s.max_strip_c <= 2 && s.max_slice_w <= 16 && s.max_slice_nodes <= 256 &&
+      s.nnz * 9 < (int64_t(1) << 40)) {
+    const size_t shm2 = (size_t)elast_tile_bytes(s.max_slice_nodes, s.max_slice_w);
+    static std::map<size_t, int> occ;
+    auto it = occ.find(shm2);
+    if (it == occ.end()) {
+      int q = 0;
+      AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &q, reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16>), 64, shm2));
+      it = occ.emplace(shm2, q < 1 ? 1 : q).first;
+    }
+    const int64_t n_items = 3 * s.n_slices;
+    int64_t nblk = (int64_t)ctx.n_cu * it->second;
+    if (nblk > n_items) nblk = n_items < 8 ? 8 : n_items;
+    if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);
+    AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, 8 * 16 * sizeof(unsigned long long), ctx.stream));
+    hipLaunchKernelGGL((k_assemble_elast_strip<2, 16>), dim3((unsigned)nblk), dim3(64), shm2, ctx.stream, n_items,
+                       s.rec_all.p, s.tickets.p, s.max_slice_nodes, s.max_slice_w, b.order_per_block, s.perm.p,
+                       s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p, s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0,
+                       fx, fy, fz, b.values.p, f ? rhs : nullptr);
+    AFEM_LAUNCHED();
+    return;
+  }
   const int64_t shm = 3 * 8 * 64 * (int64_t)s.max_slice_w + ((24 * (int64_t)s.max_slice_nodes + 15) & ~int64_t(15)) +
                       2 * 64 * (int64_t)s.max_slice_w;
   AFEM_REQUIRE(shm <= 160 * 1024, AFEM_ERR_LIMIT, "block-3 slice tile exceeds the LDS of a CU");
-  const double fx = f ? f[0] : 0.0, fy = f ? f[1] : 0.0, fz = f ? f[2] : 0.0;
   hipLaunchKernelGGL(k_assemble_elast_tet<16>, dim3((unsigned)(3 * s.n_slices)), dim3(64), (size_t)shm, ctx.stream,
                      s.max_slice_nodes, s.max_slice_w, b.order_per_block, s.perm.p, s.row_ptr.p, s.strip.p,
                      s.strip_ptr.p, s.strip_n.p, s.dslot.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p,
