@@ -1120,7 +1120,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
 // (ci + k) % 3 of the block.  A cyclic axis permutation is a rotation, the
 // material isotropic: the entries are the same numbers (up to the order of
 // the three products in a dot product).
-template <int MAXC, int MAXW>
+template <int MAXC, int MAXW, int UMODE>
 __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, const SliceRec* __restrict__ recs,
                                                              unsigned long long* __restrict__ tickets, int u_cap,
                                                              int w_cap, bool per_block,
@@ -1293,7 +1293,62 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
       return (wq >> (8 * (j & 3))) & 0xFFu;
     };
     constexpr int NSTEP = 16 * MAXC;
-    {
+    if constexpr (UMODE == 1) {
+      // uniform slice (as k_assemble_strip<.., 1>): priming steps only load
+      // the window, scalar shift/swap branches, no emit masks; a padding step
+      // (odd lengths) has a zero edge and only feeds the diagonal slot
+      const uint64_t pat = R0.pat;
+      auto ustep = [&](auto swap_c, uint32_t byte, V3 xd) {
+        constexpr bool SWAP = decltype(swap_c)::value;
+        double* const aD = acc_lane + 192 * (byte & 63u);
+        const V3 eD = sub(xd, xi);
+        V3 cRn;
+        if constexpr (SWAP) {
+          cRn = cN;
+        }
+        else {
+          cRn = cP;
+          eP = eQ;
+          aP = aQ;
+        }
+        eQ = eR;
+        aQ = aR;
+        eR = eD;
+        aR = aD;
+        cP = cross(eQ, eR);
+        cN = cross(eP, eR);
+        const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
+        const double meas = fabs(dot(eP, cP));
+        const double s = -recip1(6.0 * fmax(meas, 1e-300));
+        const double mass = c0 * meas * (1.0 / 120.0);
+        macc += meas;
+        block(aP, m, cP, s, mass);
+        block(aQ, m, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+        block(aR, m, cRn, s, mass);
+      };
+      {
+        const uint32_t b0 = byte_at(0), b1 = byte_at(1);
+        eQ = sub(coord(lidx_of(b0)), xi);
+        eR = sub(coord(lidx_of(b1)), xi);
+        aQ = acc_lane + 192 * (b0 & 63u);
+        aR = acc_lane + 192 * (b1 & 63u);
+        cP = cross(eQ, eR);
+      }
+      int u1 = lidx_of(byte_at(2));
+      V3 xc = coord(u1);
+      u1 = lidx_of(byte_at(3));
+#pragma unroll
+      for (int j = 2; j < NSTEP; ++j) {
+        if ((j & 1) == 0 && j >= nsteps) break;
+        const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
+        const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
+        if ((pat >> j) & 1u) ustep(std::true_type{}, byte_at(j), xc);
+        else ustep(std::false_type{}, byte_at(j), xc);
+        xc = xn;
+        u1 = u2;
+      }
+    }
+    else {
       int u1 = lidx_of(byte_at(0));
       V3 xc = coord(u1);
       u1 = lidx_of(byte_at(1));
@@ -1978,24 +2033,33 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
   if (use_new && s.rec_ok && s.max_strip_c <= 2 && s.max_slice_w <= 16 && s.max_slice_nodes <= 256 &&
       s.nnz * 9 < (int64_t(1) << 40)) {
     const size_t shm2 = (size_t)elast_tile_bytes(s.max_slice_nodes, s.max_slice_w);
-    static std::map<size_t, int> occ;
-    auto it = occ.find(shm2);
-    if (it == occ.end()) {
-      int q = 0;
-      AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &q, reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16>), 64, shm2));
-      it = occ.emplace(shm2, q < 1 ? 1 : q).first;
-    }
-    const int64_t n_items = 3 * s.n_slices;
-    int64_t nblk = (int64_t)ctx.n_cu * it->second;
-    if (nblk > n_items) nblk = n_items < 8 ? 8 : n_items;
+    static std::map<std::pair<const void*, size_t>, int> occ;
+    // AFEM_ASSEMBLY_UNIFORM=0: every slice through the general instance (diagnostic)
+    const char* ue = getenv("AFEM_ASSEMBLY_UNIFORM");
+    const bool use_uni = !(ue && atoi(ue) == 0) && s.n_uni > 0;
     if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);
-    AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, 8 * 16 * sizeof(unsigned long long), ctx.stream));
-    hipLaunchKernelGGL((k_assemble_elast_strip<2, 16>), dim3((unsigned)nblk), dim3(64), shm2, ctx.stream, n_items,
-                       s.rec_all.p, s.tickets.p, s.max_slice_nodes, s.max_slice_w, b.order_per_block, s.perm.p,
-                       s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p, s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0,
-                       fx, fy, fz, b.values.p, f ? rhs : nullptr);
-    AFEM_LAUNCHED();
+    AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
+    auto launch = [&](const void* fn, auto kern, int64_t n_items, const SliceRec* list, unsigned long long* tk) {
+      auto it = occ.find({ fn, shm2 });
+      if (it == occ.end()) {
+        int q = 0;
+        AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, fn, 64, shm2));
+        it = occ.emplace(std::make_pair(fn, shm2), q < 1 ? 1 : q).first;
+      }
+      int64_t nblk = (int64_t)ctx.n_cu * it->second;
+      if (nblk > n_items) nblk = n_items < 8 ? 8 : n_items;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm2, ctx.stream, n_items, list, tk, s.max_slice_nodes,
+                         s.max_slice_w, b.order_per_block, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p,
+                         s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr);
+      AFEM_LAUNCHED();
+    };
+    if (use_uni)
+      launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16, 1>), k_assemble_elast_strip<2, 16, 1>,
+             3 * s.n_uni, s.rec_u.p, s.tickets.p);
+    const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;
+    if (n_mix > 0)
+      launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16, 0>), k_assemble_elast_strip<2, 16, 0>,
+             3 * n_mix, use_uni ? s.rec_m.p : s.rec_all.p, s.tickets.p + 128);
     return;
   }
   const int64_t shm = 3 * 8 * 64 * (int64_t)s.max_slice_w + ((24 * (int64_t)s.max_slice_nodes + 15) & ~int64_t(15)) +

@@ -28,6 +28,8 @@ MU2 = 2 * E / (2 * (1 + NU))
 def _mesh(ctx, which):
     if which == "box":
         return af.Mesh.structured(ctx, 3, 6)
+    if which == "bigbox":  # interior 4x4x4 bricks: the uniform-strip instance runs
+        return af.Mesh.structured(ctx, 3, 13, seed=5)
     if which == "sphere":
         gm = read_gmsh(path("sphere_cut.msh"))
         return af.Mesh.from_arrays(ctx, 3, gm.cells, gm.coords)
@@ -37,7 +39,7 @@ def _mesh(ctx, which):
     return af.Mesh.structured(ctx, 3, 5, nz=9, nranks=3, rank=1)
 
 
-@pytest.mark.parametrize("which", ["box", "sphere", "lshape", "slab"])
+@pytest.mark.parametrize("which", ["box", "bigbox", "sphere", "lshape", "slab"])
 @pytest.mark.parametrize("use_csr", [False, True])
 @pytest.mark.parametrize("c0,force", [(0.0, None), (3.7e6, (0.5, -1.0, 2.0))])
 def test_elasticity3d_assembly_parity(ctx, which, use_csr, c0, force):
@@ -61,6 +63,24 @@ def test_elasticity3d_assembly_parity(ctx, which, use_csr, c0, force):
     assert err <= VAL_TOL, f"block-3 values differ from the oracle: {err:.3e}"
     if force:
         assert np.abs(rhs - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+
+
+@pytest.mark.parametrize("use_csr", [False, True])
+def test_elasticity3d_uniform_variant_bitwise(ctx, monkeypatch, use_csr):
+    mesh = _mesh(ctx, "bigbox")
+    bsr = af.BSRFormat(mesh, 3).initialize(use_csr)
+    bsr.computeSparsity()
+    assert bsr.stats()["uniform_slices"] > 0
+    n3 = 3 * mesh.n_own_nodes
+    drhs = ctx.malloc(8 * n3)
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs)
+    v_uni, r_uni = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
+    monkeypatch.setenv("AFEM_ASSEMBLY_UNIFORM", "0")
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs)
+    v_gen, r_gen = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
+    ctx.free(drhs)
+    assert np.array_equal(v_uni, v_gen), "uniform and general block-3 instances differ"
+    assert np.array_equal(r_uni, r_gen)
 
 
 def test_elasticity3d_plain_entry_point_equals_ex(ctx):
