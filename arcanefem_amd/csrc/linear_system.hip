@@ -16,6 +16,9 @@ namespace afem {
 namespace {
 
 constexpr int kThreads = 256;
+#ifndef AFEM_SPMV_NT
+#define AFEM_SPMV_NT 0
+#endif
 inline unsigned grid_for(int64_t n, int threads) { return (unsigned)((n + threads - 1) / threads); }
 constexpr uint8_t kElimRow = 1, kElimRowCol = 2;
 
@@ -193,9 +196,20 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream4(int64_t n_rows, int64
     int c[4];
     double v[4];
     if (q + 4 <= nnz) {
+#if AFEM_SPMV_NT  // diagnostic: streaming (non-temporal) column / value loads
+      typedef int nt_i4 __attribute__((ext_vector_type(4)));
+      typedef double nt_d2 __attribute__((ext_vector_type(2)));
+      const nt_i4 ci4 = __builtin_nontemporal_load(reinterpret_cast<const nt_i4*>(cols + q));
+      const nt_d2 va = __builtin_nontemporal_load(reinterpret_cast<const nt_d2*>(vals + q));
+      const nt_d2 vb = __builtin_nontemporal_load(reinterpret_cast<const nt_d2*>(vals + q + 2));
+      const int4 c4 = make_int4(ci4.x, ci4.y, ci4.z, ci4.w);
+      const double2 v01 = make_double2(va.x, va.y);
+      const double2 v23 = make_double2(vb.x, vb.y);
+#else
       const int4 c4 = *reinterpret_cast<const int4*>(cols + q);
       const double2 v01 = *reinterpret_cast<const double2*>(vals + q);
       const double2 v23 = *reinterpret_cast<const double2*>(vals + q + 2);
+#endif
       c[0] = c4.x;
       c[1] = c4.y;
       c[2] = c4.z;
