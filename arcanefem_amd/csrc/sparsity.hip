@@ -19,6 +19,9 @@
 //      1-KiB line (a 16-B load per lane) per 4 incidence steps.
 #include "afem_internal.hpp"
 
+#include <cstdlib>
+#include <string>
+
 namespace afem {
 namespace {
 
@@ -149,6 +152,80 @@ __global__ void k_perm_bricks(int64_t n_slices, int dim, int64_t ax, int64_t ay,
   const int64_t j = jb * by + (lane / bx) % by;
   const int64_t k = kb * bz + lane / (bx * by);
   perm[p] = (i < ax && j < ay && k < az) ? (int32_t)(i + ax * (j + ay * k)) : -1;
+}
+
+// 3D structured boxes, boundary-aware: the interior nodes [1, a-2]^3 in 4x4x4
+// bricks (partial bricks at the upper end: idle lanes), then the six
+// boundary faces (k planes, j planes without the k rows, i planes without
+// both) in 8x8 tiles.  Interior bricks then share one strip topology (the
+// uniform assembly instance), and the boundary rows no longer spoil it for
+// the interior rows of their brick.
+struct FaceTiles {
+  int64_t n_core, nbx, nby;
+  int64_t start[7];  // first slice of face f (start[6] = n_slices)
+  int64_t U[6], V[6], tu[6];
+};
+
+__host__ __device__ inline FaceTiles face_tiles(int64_t ax, int64_t ay, int64_t az)
+{
+  FaceTiles F{};
+  const int64_t cx = ax > 2 ? ax - 2 : 0, cy = ay > 2 ? ay - 2 : 0, cz = az > 2 ? az - 2 : 0;
+  F.nbx = (cx + 3) / 4;
+  F.nby = (cy + 3) / 4;
+  F.n_core = F.nbx * F.nby * ((cz + 3) / 4);
+  const int64_t U[6] = { ax, az > 1 ? ax : 0, ax, ay > 1 ? ax : 0, cy, ax > 1 ? cy : 0 };
+  const int64_t V[6] = { ay, ay, cz, cz, cz, cz };
+  int64_t acc = F.n_core;
+  for (int f = 0; f < 6; ++f) {
+    F.U[f] = U[f];
+    F.V[f] = V[f];
+    F.tu[f] = (U[f] + 7) / 8;
+    F.start[f] = acc;
+    acc += (U[f] > 0 && V[f] > 0) ? F.tu[f] * ((V[f] + 7) / 8) : 0;
+  }
+  F.start[6] = acc;
+  return F;
+}
+
+__global__ void k_perm_bricks_bd(int64_t n_slices, int64_t ax, int64_t ay, int64_t az, FaceTiles F,
+                                 int32_t* __restrict__ perm)
+{
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_slices * 64) return;
+  const int64_t s = p >> 6;
+  const int lane = (int)(p & 63);
+  int64_t i = -1, j = -1, k = -1;
+  if (s < F.n_core) {
+    const int64_t ib = s % F.nbx, jb = (s / F.nbx) % F.nby, kb = s / (F.nbx * F.nby);
+    i = 1 + 4 * ib + (lane & 3);
+    j = 1 + 4 * jb + ((lane >> 2) & 3);
+    k = 1 + 4 * kb + (lane >> 4);
+    if (i > ax - 2 || j > ay - 2 || k > az - 2) i = -1;
+  }
+  else {
+    int f = 0;
+    while (f < 5 && s >= F.start[f + 1]) ++f;
+    const int64_t t = s - F.start[f];
+    const int64_t u = 8 * (t % F.tu[f]) + (lane & 7), v = 8 * (t / F.tu[f]) + (lane >> 3);
+    if (u < F.U[f] && v < F.V[f]) {
+      switch (f) {
+        case 0: i = u; j = v; k = 0; break;
+        case 1: i = u; j = v; k = az - 1; break;
+        case 2: i = u; j = 0; k = 1 + v; break;
+        case 3: i = u; j = ay - 1; k = 1 + v; break;
+        case 4: i = 0; j = 1 + u; k = 1 + v; break;
+        default: i = ax - 1; j = 1 + u; k = 1 + v; break;
+      }
+    }
+  }
+  perm[p] = i >= 0 ? (int32_t)(i + ax * (j + ay * k)) : -1;
+}
+
+__global__ void k_count_valid(int64_t n, const int32_t* __restrict__ perm, unsigned long long* __restrict__ out)
+{
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long b = __ballot(p < n && perm[p] >= 0);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (unsigned long long)__popcll(b));
 }
 
 __global__ void k_perm_identity(int64_t n_pos, int64_t n_rows, int32_t* __restrict__ perm)
@@ -528,18 +605,22 @@ __global__ __launch_bounds__(64) void k_strip_classify(int64_t n_slices, const i
   if (sl >= n_slices) return;
   const int n = strip_n[sl];
   const uint8_t* st = strip + strip_ptr[sl] + lane * 16;
-  // the uniform kernel also drops the overflow paths (> 256 slice nodes, > 16 slots)
-  bool ok = perm[sl * 64 + lane] >= 0 && n >= 3 && n <= 64 && snode_ptr[sl + 1] - snode_ptr[sl] <= 256 &&
-            slice_w[sl] <= 16;
+  // the uniform kernel also drops the overflow paths (> 256 slice nodes, > 16 slots).
+  // Idle lanes (no row, all-padding stream: slot 0 = a zero edge) are allowed:
+  // in the uniform kernel they only add zeros to their own accumulators.
+  const bool idle = perm[sl * 64 + lane] < 0;
+  bool ok = n >= 3 && n <= 64 && snode_ptr[sl + 1] - snode_ptr[sl] <= 256 && slice_w[sl] <= 16;
   uint64_t pat = 0;
-  for (int j = 0; j < n && ok; ++j) {
+  for (int j = 0; j < n && ok && !idle; ++j) {
     const uint32_t kind = st[(int64_t)(j >> 4) * 1024 + (j & 15)] >> 6;
     if (j < 2) ok = kind == 2;
     else if (kind > 1) ok = false;
     else pat |= (uint64_t)kind << j;
   }
-  const uint64_t p0 = __shfl(pat, 0);
-  const bool all = __all(ok && pat == p0);
+  const unsigned long long act = __ballot(!idle);
+  const int first = act ? __ffsll((long long)act) - 1 : 0;
+  const uint64_t p0 = __shfl(pat, first);
+  const bool all = act != 0 && __all(ok && (idle || pat == p0));
   if (lane == 0) {
     uflag[sl] = all ? 1 : 0;
     spat[sl] = all ? p0 : 0;
@@ -639,13 +720,37 @@ void build_structure(Mesh& m, Structure& s)
     const int64_t az = st.dim == 3 ? own_layers : 1;
     AFEM_REQUIRE(ax * ay * az == n_rows, AFEM_ERR_STATE, "structured mesh: owned node box does not match n_own");
     const int bx = st.dim == 3 ? 4 : 8, bz = st.dim == 3 ? 4 : 1;
-    s.n_slices = ((ax + bx - 1) / bx) * ((ay + bx - 1) / bx) * ((az + bz - 1) / bz);
-    s.perm.alloc(s.n_slices * 64);
-    hipLaunchKernelGGL(k_perm_bricks, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream, s.n_slices,
-                       st.dim, ax, ay, az, s.perm.p);
-    AFEM_LAUNCHED();
+    // AFEM_BRICKS=plain: the plain 4x4x4 brick grid over the whole box (diagnostic)
+    const char* be = getenv("AFEM_BRICKS");
+    const bool boundary_aware = st.dim == 3 && !(be && std::string(be) == "plain");
+    if (boundary_aware) {
+      const FaceTiles F = face_tiles(ax, ay, az);
+      s.n_slices = F.start[6];
+      s.perm.alloc(s.n_slices * 64);
+      hipLaunchKernelGGL(k_perm_bricks_bd, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream,
+                         s.n_slices, ax, ay, az, F, s.perm.p);
+      AFEM_LAUNCHED();
+      DevBuf<unsigned long long> cnt;
+      cnt.alloc(1);
+      AFEM_HIP(hipMemsetAsync(cnt.p, 0, cnt.bytes(), ctx.stream));
+      hipLaunchKernelGGL(k_count_valid, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream,
+                         s.n_slices * 64, s.perm.p, cnt.p);
+      AFEM_LAUNCHED();
+      unsigned long long hc = 0;
+      AFEM_HIP(hipMemcpyAsync(&hc, cnt.p, sizeof(hc), hipMemcpyDeviceToHost, ctx.stream));
+      ctx.sync();
+      AFEM_REQUIRE((int64_t)hc == n_rows, AFEM_ERR_STATE, "boundary-aware brick order does not cover the owned nodes");
+      s.run = 1;  // face tiles of the i planes do not hold consecutive rows
+    }
+    else {
+      s.n_slices = ((ax + bx - 1) / bx) * ((ay + bx - 1) / bx) * ((az + bz - 1) / bz);
+      s.perm.alloc(s.n_slices * 64);
+      hipLaunchKernelGGL(k_perm_bricks, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream, s.n_slices,
+                         st.dim, ax, ay, az, s.perm.p);
+      AFEM_LAUNCHED();
+      s.run = st.dim == 3 ? 4 : 8;
+    }
     s.brick_order = true;
-    s.run = st.dim == 3 ? 4 : 8;
   }
   else {
     s.n_slices = (n_rows + 63) / 64;
