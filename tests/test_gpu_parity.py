@@ -356,3 +356,37 @@ def test_spmv_matches_oracle(ctx):
     assert np.abs(y - yo).max() <= 1e-13 * np.abs(yo).max()
     ctx.free(dx)
     ctx.free(dy)
+
+
+@pytest.mark.parametrize("dim,n", [(3, 12), (2, 40)])
+def test_random_node_permutation(ctx, dim, n):
+    # SURVEY §8d robustness variant: the structured mesh with a seeded random
+    # node and cell numbering (node-order slices, no bricks, scattered strips);
+    # the assembled matrix must be the permuted matrix of the unpermuted box
+    ref = O.structured_mesh(dim, n, jitter=0.2, seed=20250220)
+    rng = np.random.default_rng(1234)
+    nn = ref["n_local"]
+    p = rng.permutation(nn)              # new id of old node i is p[i]
+    cells = p[ref["cells"]].astype(np.int32)[rng.permutation(ref["cells"].shape[0])]
+    coords = np.empty_like(ref["coords"])
+    coords[p] = ref["coords"]
+    mesh = af.Mesh.from_arrays(ctx, dim, cells, coords)
+    bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+    rows, cols, vals = bsr.download()
+    orp, ocols = O.sparsity(nn, nn, cells)
+    ovals, orhs = O.assemble_poisson(nn, cells, coords, orp, ocols, 5.5)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    _check_values(vals, ovals)
+    assert np.abs(ls.rhs_host() - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+    # against the unpermuted box: A_perm[p[i], p[j]] == A[i, j]
+    m0 = af.Mesh.structured(ctx, dim, n, jitter=0.2, seed=20250220)
+    b0, _ = _assemble_gpu(ctx, m0, 5.5)
+    r0, c0, v0 = b0.download()
+    A0 = {}
+    for i in range(nn):
+        for k in range(r0[i], r0[i + 1]):
+            A0[(p[i], p[c0[k]])] = v0[k]
+    scale = np.abs(v0).max()
+    for i in range(nn):
+        for k in range(rows[i], rows[i + 1]):
+            assert abs(vals[k] - A0[(i, cols[k])]) <= VAL_TOL * scale
