@@ -968,7 +968,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
 #endif
         const bool swp = (pat >> j) & 1u;
         if constexpr (UMODE == 2) ustep(std::integral_constant<int, -1>{}, byte_at(j), xc, swp);
-        else if (swp) ustep(std::integral_constant<int, 1>{}, byte_at(j), xc, true);
+        else if (__builtin_expect(swp, 0)) ustep(std::integral_constant<int, 1>{}, byte_at(j), xc, true);
         else ustep(std::integral_constant<int, 0>{}, byte_at(j), xc, false);
         xc = xn;
         u1 = u2;
@@ -1342,7 +1342,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
         if ((j & 1) == 0 && j >= nsteps) break;
         const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
         const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
-        if ((pat >> j) & 1u) ustep(std::true_type{}, byte_at(j), xc);
+        if (__builtin_expect((pat >> j) & 1u, 0)) ustep(std::true_type{}, byte_at(j), xc);
         else ustep(std::false_type{}, byte_at(j), xc);
         xc = xn;
         u1 = u2;

@@ -19,6 +19,7 @@
 //      1-KiB line (a 16-B load per lane) per 4 incidence steps.
 #include "afem_internal.hpp"
 
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 
@@ -904,6 +905,13 @@ void build_structure(Mesh& m, Structure& s)
       upload(s.rec_u, ru);
       upload(s.rec_m, rm);
       upload(s.rec_all, ra);
+      if (getenv("AFEM_DEBUG_PATTERNS")) {  // diagnostic: strip patterns of the uniform slices
+        std::map<std::pair<uint64_t, int>, int64_t> h;
+        for (const SliceRec& r : ru) ++h[{ r.pat, (int)(r.meta >> 24) }];
+        for (auto& kv : h)
+          fprintf(stderr, "afem pattern 0x%016llx steps %d slices %lld\n", (unsigned long long)kv.first.first,
+                  kv.first.second, (long long)kv.second);
+      }
       ctx.sync();
     }
     else {
