@@ -390,3 +390,32 @@ def test_random_node_permutation(ctx, dim, n):
     for i in range(nn):
         for k in range(rows[i], rows[i + 1]):
             assert abs(vals[k] - A0[(i, cols[k])]) <= VAL_TOL * scale
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_mesh_without_cells(ctx, dim):
+    # nodes but no cells: every row is its diagonal alone (BSRFormat.h:679 always
+    # inserts it), all values and the RHS are zero
+    coords = np.random.default_rng(3).random((70, 3))
+    if dim == 2:
+        coords[:, 2] = 0.0
+    cells = np.zeros((0, dim + 1), dtype=np.int32)
+    mesh = af.Mesh.from_arrays(ctx, dim, cells, coords)
+    bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+    rows, cols, vals = bsr.download()
+    assert np.array_equal(rows, np.arange(71)) and np.array_equal(cols, np.arange(70))
+    assert not vals.any() and not ls.rhs_host().any()
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_single_cell(ctx, dim):
+    coords = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [0.2, 0.3, 1.1]], dtype=np.float64)[: dim + 1]
+    cells = np.arange(dim + 1, dtype=np.int32)[None, :]
+    mesh = af.Mesh.from_arrays(ctx, dim, cells, coords)
+    bsr, ls = _assemble_gpu(ctx, mesh, 2.0)
+    rows, cols, vals = bsr.download()
+    orp, ocols = O.sparsity(dim + 1, dim + 1, cells)
+    ovals, orhs = O.assemble_poisson(dim + 1, cells, coords, orp, ocols, 2.0)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    _check_values(vals, ovals)
+    assert np.abs(ls.rhs_host() - orhs).max() <= VAL_TOL * np.abs(orhs).max()
