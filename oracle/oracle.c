@@ -16,6 +16,9 @@
  * -ffp-contract=off so that no FMA contraction changes the rounding of the
  * restated expressions.
  */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -231,6 +234,66 @@ int64_t orc_assemble_poisson(int64_t n_rows, int64_t n_cells, int nv, const int3
       }
       if (rhs)
         rhs[row] += f * meas / nv;
+    }
+  }
+  return missing;
+}
+
+/* The same cell loop run on all host threads, as the reference runs it on a
+ * multi-core host (the RUNCOMMAND cell loop of BSRFormat::assembleBilinearAtomic,
+ * femutils/BSRFormat.h:786-837, with Accelerator::doAtomic adds): cells split
+ * over OpenMP threads, every add atomic.  Used only for bench.py's multi-core
+ * CPU baseline (summation order is run-dependent, as in the reference). */
+int orc_omp_threads(int n)
+{
+#ifdef _OPENMP
+  if (n > 0)
+    omp_set_num_threads(n);
+  return omp_get_max_threads();
+#else
+  (void)n;
+  return 1;
+#endif
+}
+
+int64_t orc_assemble_poisson_omp(int64_t n_rows, int64_t n_cells, int nv, const int32_t* cell_node,
+                                 const double* coords, const int64_t* row_ptr, const int32_t* cols, double* vals,
+                                 double f, double* rhs)
+{
+  int64_t missing = 0;
+#pragma omp parallel for schedule(static) reduction(+ : missing)
+  for (int64_t c = 0; c < n_cells; ++c) {
+    double xyz[12], K[16], meas;
+    const int32_t* n = cell_node + c * nv;
+    for (int a = 0; a < nv; ++a) {
+      xyz[3 * a + 0] = coords[3 * (int64_t)n[a] + 0];
+      xyz[3 * a + 1] = coords[3 * (int64_t)n[a] + 1];
+      xyz[3 * a + 2] = coords[3 * (int64_t)n[a] + 2];
+    }
+    if (nv == 4)
+      orc_element_tet4(xyz, K, &meas);
+    else
+      orc_element_tri3(xyz, K, &meas);
+    for (int a = 0; a < nv; ++a) {
+      int32_t row = n[a];
+      if (row >= n_rows)
+        continue;
+      for (int b = 0; b < nv; ++b) {
+        int32_t col = n[b];
+        int64_t k = row_ptr[row], end = row_ptr[row + 1];
+        while (k < end && cols[k] != col)
+          ++k;
+        if (k == end) {
+          ++missing;
+          continue;
+        }
+#pragma omp atomic
+        vals[k] += K[nv * a + b];
+      }
+      if (rhs) {
+#pragma omp atomic
+        rhs[row] += f * meas / nv;
+      }
     }
   }
   return missing;

@@ -61,6 +61,10 @@ def lib():
         L.orc_assemble_poisson.restype = ctypes.c_int64
         L.orc_assemble_poisson.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _i32p, _f64p, _i64p, _i32p,
                                            _f64p, ctypes.c_double, ctypes.c_void_p]
+        L.orc_assemble_poisson_omp.restype = ctypes.c_int64
+        L.orc_assemble_poisson_omp.argtypes = L.orc_assemble_poisson.argtypes
+        L.orc_omp_threads.restype = ctypes.c_int
+        L.orc_omp_threads.argtypes = [ctypes.c_int]
         L.orc_assemble_elasticity_tri.restype = ctypes.c_int64
         L.orc_assemble_elasticity_tri.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _f64p, _i64p, _i32p,
                                                   ctypes.c_double, ctypes.c_double, _f64p]
@@ -134,6 +138,25 @@ def assemble_poisson(n_rows, cells, coords, row_ptr, cols, f=0.0, with_rhs=True)
     missing = lib().orc_assemble_poisson(n_rows, cells.shape[0], cells.shape[1], cells.ravel(), coords.ravel(),
                                          row_ptr, cols, vals, f,
                                          rhs.ctypes.data_as(ctypes.c_void_p) if with_rhs else None)
+    if missing:
+        raise RuntimeError(f"{missing} (row,col) pairs missing from the structure")
+    return vals, rhs
+
+
+def omp_threads(n=0):
+    """Set (n > 0) and return the OpenMP thread count of the multi-core oracle loop."""
+    return lib().orc_omp_threads(n)
+
+
+def assemble_poisson_omp(n_rows, cells, coords, row_ptr, cols, f=0.0):
+    """assemble_poisson on all OpenMP threads (atomic adds, the reference's
+    multi-core cell loop); bench.py's multi-core CPU baseline only."""
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    coords = np.ascontiguousarray(coords, dtype=np.float64).reshape(-1, 3)
+    vals = np.zeros(cols.shape[0], dtype=np.float64)
+    rhs = np.zeros(n_rows, dtype=np.float64)
+    missing = lib().orc_assemble_poisson_omp(n_rows, cells.shape[0], cells.shape[1], cells.ravel(), coords.ravel(),
+                                             row_ptr, cols, vals, f, rhs.ctypes.data_as(ctypes.c_void_p))
     if missing:
         raise RuntimeError(f"{missing} (row,col) pairs missing from the structure")
     return vals, rhs
