@@ -57,3 +57,16 @@ def test_structured_halo_plan_matches_mesh_spec(dim, n, nz, nranks):
             sent_g = meshes[q]["local_to_global"][qsi[qoff[kk]:qoff[kk + 1]]]
             assert np.array_equal(recv_g, sent_g)
             assert np.all(qsi[qoff[kk]:qoff[kk + 1]] < meshes[q]["n_own"])
+
+
+def test_c_driver_builds_against_the_header():
+    # examples/poisson3d.c uses only include/arcanefem_amd.h and links libafem.so
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "examples")], check=True)
+    exe = os.path.join(root, "examples", "poisson3d")
+    assert os.path.exists(exe)
+    out = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "libafem.so" in out and "not found" not in out.split("libafem.so")[1].splitlines()[0]

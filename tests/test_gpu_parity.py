@@ -419,3 +419,32 @@ def test_single_cell(ctx, dim):
     assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
     _check_values(vals, ovals)
     assert np.abs(ls.rhs_host() - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+
+
+def test_c_driver_through_the_c_abi(ctx, tmp_path):
+    # examples/poisson3d.c runs the Poisson module's sequence through the C ABI
+    # alone; its solution equals the one of the same calls made from Python
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "poisson3d")
+    assert os.path.exists(exe), "examples/poisson3d not built (make -C examples)"
+    out = tmp_path / "u.bin"
+    res = subprocess.run([exe, "8", str(out)], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    assert "converged=1" in res.stdout, res.stdout
+    u_c = np.fromfile(out, dtype=np.float64)
+    mesh = af.Mesh.structured(ctx, 3, 8, jitter=0.2, seed=20250220)
+    bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+    ls.applyDirichletViaPenalty(mesh.bottom_nodes(), 0.5, 1e30)
+    ls.setSolverOptions(rtol=1e-13)
+    ls.solve()
+    u_py = ls.solution_host()[: mesh.n_own_nodes]
+    assert u_c.shape == u_py.shape
+    assert np.abs(u_c - u_py).max() <= 1e-12 * np.abs(u_py).max()
+    cells, coords, _ = mesh.download()
+    orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+    ovals, orhs = O.assemble_poisson(mesh.n_own_nodes, cells, coords, orp, ocols, 5.5)
+    O.dirichlet_penalty(mesh.bottom_nodes(), 0.5, 1e30, orp, ocols, ovals, orhs)
+    xo = np.linalg.solve(O.csr_to_dense(orp, ocols, ovals), orhs)
+    assert np.abs(u_c - xo).max() <= SOL_TOL * np.abs(xo).max()
