@@ -448,3 +448,29 @@ def test_c_driver_through_the_c_abi(ctx, tmp_path):
     O.dirichlet_penalty(mesh.bottom_nodes(), 0.5, 1e30, orp, ocols, ovals, orhs)
     xo = np.linalg.solve(O.csr_to_dense(orp, ocols, ovals), orhs)
     assert np.abs(u_c - xo).max() <= SOL_TOL * np.abs(xo).max()
+
+
+def test_rccl_communicator_single_rank(ctx):
+    # the RCCL data path of bench.py --gpus N at N = 1: communicator bootstrap
+    # (ncclGetUniqueId / ncclCommInitRank), halo plan of the slab layout, solve
+    # with the halo attached (exchange and all-reduce are identities on one
+    # rank) equals the solve without it.  N > 1 needs one GPU per rank (RCCL
+    # refuses two ranks on one device); its decomposition logic is covered on
+    # CPU by tests/test_distributed_gloo.py.
+    mesh = af.Mesh.structured(ctx, 3, 10, jitter=0.2, seed=20250220)
+    uid = af.Communicator.unique_id()
+    comm = af.Communicator(ctx, 1, 0, uid)
+    try:
+        sols = []
+        for with_halo in (False, True):
+            bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+            if with_halo:
+                ls.set_halo_structured(comm, mesh)
+            ls.applyDirichletViaPenalty(mesh.bottom_nodes(), 0.5, 1e30)
+            ls.setSolverOptions(rtol=1e-12)
+            st = ls.solve()
+            assert st["converged"]
+            sols.append(ls.solution_host()[: mesh.n_own_nodes])
+        assert np.array_equal(sols[0], sols[1])
+    finally:
+        comm.close()
