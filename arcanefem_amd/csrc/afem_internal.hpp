@@ -154,6 +154,7 @@ struct Structure {
   bool strip_ok = false;
   int max_strip_c = 0;
   DevBuf<uint8_t> strip;
+  DevBuf<uint8_t> strip_u;  // per step byte: local index of its node in the slice's node list (u8)
   DevBuf<int64_t> strip_ptr;
   DevBuf<int32_t> strip_c;  // 16-step chunks per slice
   DevBuf<int32_t> strip_n;  // steps per slice (longest row stream)

@@ -626,6 +626,7 @@ struct StripPre {
   int64_t rb;
   u32x4 l0, l1;
   u32x4 ch[MAXC];
+  u32x4 cu[MAXC];  // uniform scalar instance: local node index of every step (strip_u)
   double x[4], y[4], z[4];
 };
 
@@ -668,6 +669,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
                                                           const int64_t* __restrict__ pos_rb,
                                                           const uint32_t* __restrict__ pos_dl,
                                                           const uint8_t* __restrict__ strip,
+                                                          const uint8_t* __restrict__ strip_u,
                                                           const uint16_t* __restrict__ lidx,
                                                           const int32_t* __restrict__ snode,
                                                           const double* __restrict__ coords, double s_coef,
@@ -675,6 +677,9 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
                                                           double* __restrict__ rhs)
 {
   constexpr bool UNI = UMODE != 0;  // 1: scalar shift/swap branches, 2: selects on the uniform bit
+  // uniform tet instances address coordinates by the local-index stream (no
+  // column-index table in LDS, no dependent LDS read per step)
+  constexpr bool ULOC = UNI && NV == 4;
   constexpr int DIMC = NV == 4 ? 3 : 2;
   extern __shared__ __align__(16) unsigned char smem[];
   double* acc = reinterpret_cast<double*>(smem);
@@ -726,14 +731,21 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
     p.row = perm[q];
     p.dl = pos_dl[q];
     p.rb = pos_rb[q];
-    const int nq = 8 * (int)((R.meta >> 16) & 0xFFu);
-    const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R.lidx_off);
-    p.l0 = ls[max(min(lane, nq - 1), 0)];
-    p.l1 = ls[max(min(lane + 64, nq - 1), 0)];
     const int nc = (int)((R.meta >> 24) + 15) >> 4;
     const u32x4* sp = reinterpret_cast<const u32x4*>(strip + (int64_t)R.strip_off * 1024) + lane;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
+    if constexpr (ULOC) {  // the steps' local node indices instead of the column-index table
+      const u32x4* su = reinterpret_cast<const u32x4*>(strip_u + (int64_t)R.strip_off * 1024) + lane;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) p.cu[c] = su[(int64_t)max(min(c, nc - 1), 0) * 64];
+    }
+    else {
+      const int nq = 8 * (int)((R.meta >> 16) & 0xFFu);
+      const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R.lidx_off);
+      p.l0 = ls[max(min(lane, nq - 1), 0)];
+      p.l1 = ls[max(min(lane + 64, nq - 1), 0)];
+    }
   };
   auto gather = [&](const int32_t(&nid)[4], StripPre<MAXC>& p) {
 #pragma unroll
@@ -784,8 +796,10 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
     {
       const int nq = 8 * W;
       u32x4* dst = reinterpret_cast<u32x4*>(li);
-      dst[max(min(lane, nq - 1), 0)] = cur.l0;
-      dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
+      if constexpr (!ULOC) {
+        dst[max(min(lane, nq - 1), 0)] = cur.l0;
+        dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
+      }
       if (!UNI && nq > 128) {
         const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R0.lidx_off);
         for (int q = lane + 128; q < nq; q += 64) dst[q] = ls[q];
@@ -801,11 +815,11 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
     const int32_t row = cur.row;
     const bool active = row >= 0;
     const int64_t rb = cur.rb;
-    const int len = (int)(cur.dl >> 8);
+    const int len = (int)((cur.dl >> 8) & 0xFFu);
     const uint32_t dslot = cur.dl & 0xFFu;
     // the row's own coordinates: its diagonal column is one of the slice's nodes
     const V3 xi = [&] {
-      const double* q = cxyz + DIMC * (int)li[dslot * 64 + lane];
+      const double* q = cxyz + DIMC * (ULOC ? (int)(cur.dl >> 16) : (int)li[dslot * 64 + lane]);
       return V3{ q[0], q[1], DIMC == 3 ? q[2] : 0.0 };
     }();
     double macc = 0.0;
@@ -882,6 +896,12 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
       const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
       return (wq >> (8 * (j & 3))) & 0xFFu;
     };
+    auto uloc_at = [&](int j) -> int {  // local node index of step j (ULOC)
+      const u32x4 w = cur.cu[j >> 4];
+      const int q = (j >> 2) & 3;
+      const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
+      return (int)((wq >> (8 * (j & 3))) & 0xFFu);
+    };
     constexpr int NSTEP = 16 * MAXC;
     if constexpr (UNI && NV == 4) {
       // uniform strip: steps 0,1 prime the window (no cell), every later step
@@ -946,32 +966,27 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
       };
       {
         const uint32_t b0 = byte_at(0), b1 = byte_at(1);
-        eQ = sub(coord(lidx_of(b0)), xi);
-        eR = sub(coord(lidx_of(b1)), xi);
+        eQ = sub(coord(uloc_at(0)), xi);
+        eR = sub(coord(uloc_at(1)), xi);
         aQ = acc_lane + 64 * (b0 & 63u);
         aR = acc_lane + 64 * (b1 & 63u);
         cP = cross(eQ, eR);
       }
-      int u1 = lidx_of(byte_at(2));
-      V3 xc = coord(u1);
-      u1 = lidx_of(byte_at(3));
+      V3 xc = coord(uloc_at(2));
 #pragma unroll
       for (int j = 2; j < NSTEP; ++j) {
         if ((j & (UMODE == 1 ? 1 : 3)) == 0 && j >= nsteps) break;
 #if AFEM_ABL == 5  // ablation: no LDS index / coordinate reads in the step loop
-        const int u2 = 0;
         const double fb = (double)(byte_at(j + 1 < NSTEP ? j + 1 : j) & 63u);
         const V3 xn = V3{ xi.x + fb, xi.y - fb, xi.z + 2 * fb };
 #else
-        const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
-        const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
+        const V3 xn = j + 1 < NSTEP ? coord(uloc_at(j + 1)) : xc;
 #endif
         const bool swp = (pat >> j) & 1u;
         if constexpr (UMODE == 2) ustep(std::integral_constant<int, -1>{}, byte_at(j), xc, swp);
         else if (__builtin_expect(swp, 0)) ustep(std::integral_constant<int, 1>{}, byte_at(j), xc, true);
         else ustep(std::integral_constant<int, 0>{}, byte_at(j), xc, false);
         xc = xn;
-        u1 = u2;
       }
     }
     else {
@@ -1231,7 +1246,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
     const int32_t row = cur.row;
     const bool active = row >= 0;
     const int64_t rb = cur.rb;
-    const int len = (int)(cur.dl >> 8);
+    const int len = (int)((cur.dl >> 8) & 0xFFu);
     const uint32_t dslot = cur.dl & 0xFFu;
     const uint16_t* lrow = li + lane;
     const V3 xi = [&] {
@@ -1902,8 +1917,8 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
       int64_t nblk = (int64_t)ctx.n_cu * per_cu;
       if (nblk > n_list) nblk = n_list < 8 ? 8 : n_list;
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, ctx.stream, n_list, list, tk,
-                         s.max_slice_nodes, s.max_slice_w, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p,
-                         s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
+                         s.max_slice_nodes, s.max_slice_w, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.strip_u.p,
+                         s.lidx.p, s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
     };
     const SliceRec* list_m = use_uni ? s.rec_m.p : s.rec_all.p;
 #define AFEM_STRIP_K(NV_, C_, W_, U_, N_, L_, T_)                                                                      \

@@ -575,9 +575,11 @@ __global__ __launch_bounds__(64) void k_strip_rows(int64_t n_pos, int nv, const 
   for (int j = 0; j < steps; ++j) out[(int64_t)(j >> 4) * 1024 + (j & 15)] = j < total ? buf[j] : (uint8_t)(dslot | (3 << 6));
 }
 
-// per position: the row's CSR offset, and its diagonal slot | length << 8
+// per position: the row's CSR offset, and its diagonal slot | length << 8 |
+// local index of the row node in the slice's node list << 16
 __global__ void k_pos_rows(int64_t n_pos, const int32_t* __restrict__ perm, const int64_t* __restrict__ row_ptr,
-                           const uint8_t* __restrict__ dslot, int64_t* __restrict__ pos_rb,
+                           const uint8_t* __restrict__ dslot, const int64_t* __restrict__ lidx_ptr,
+                           const uint16_t* __restrict__ lidx, int64_t* __restrict__ pos_rb,
                            uint32_t* __restrict__ pos_dl)
 {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -585,8 +587,29 @@ __global__ void k_pos_rows(int64_t n_pos, const int32_t* __restrict__ perm, cons
   const int32_t r = perm[p];
   const int64_t b = r >= 0 ? row_ptr[r] : 0;
   const int64_t len = r >= 0 ? row_ptr[r + 1] - b : 0;
+  const uint32_t ds = dslot[p];
+  const uint32_t u = lidx[lidx_ptr[p >> 6] + 64 * (int64_t)ds + (p & 63)];
   pos_rb[p] = b;
-  pos_dl[p] = (uint32_t)dslot[p] | (uint32_t)len << 8;
+  pos_dl[p] = ds | (uint32_t)len << 8 | (u & 0xFFFFu) << 16;
+}
+
+// Companion of the strip stream: for every step byte, the local index (in the
+// slice's node list) of the node its slot names, same layout (u8: streams of
+// slices with more than 256 nodes are not used by the scalar strip kernels).
+__global__ void k_strip_local(int64_t n_pos, const uint8_t* __restrict__ strip, const int64_t* __restrict__ strip_ptr,
+                              const int32_t* __restrict__ strip_c, const int64_t* __restrict__ lidx_ptr,
+                              const uint16_t* __restrict__ lidx, uint8_t* __restrict__ strip_u)
+{
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pos) return;
+  const int64_t sl = p >> 6;
+  const int lane = (int)(p & 63);
+  const int64_t base = strip_ptr[sl] + lane * 16, l0 = lidx_ptr[sl] + lane;
+  const int steps = 16 * strip_c[sl];
+  for (int j = 0; j < steps; ++j) {
+    const int64_t o = base + (int64_t)(j >> 4) * 1024 + (j & 15);
+    strip_u[o] = (uint8_t)lidx[l0 + 64 * (int64_t)(strip[o] & 63u)];
+  }
 }
 
 // per slice: does every lane run the same strip topology?  Uniform = all 64
@@ -858,7 +881,11 @@ void build_structure(Mesh& m, Structure& s)
       s.pos_rb.alloc(n_pos);
       s.pos_dl.alloc(n_pos);
       hipLaunchKernelGGL(k_pos_rows, dim3(grid_for(n_pos, 256)), dim3(256), 0, ctx.stream, n_pos, s.perm.p,
-                         s.row_ptr.p, s.dslot.p, s.pos_rb.p, s.pos_dl.p);
+                         s.row_ptr.p, s.dslot.p, s.lidx_ptr.p, s.lidx.p, s.pos_rb.p, s.pos_dl.p);
+      AFEM_LAUNCHED();
+      s.strip_u.alloc(s.strip.n);
+      hipLaunchKernelGGL(k_strip_local, dim3(grid_for(n_pos, 256)), dim3(256), 0, ctx.stream, n_pos, s.strip.p,
+                         s.strip_ptr.p, s.strip_c.p, s.lidx_ptr.p, s.lidx.p, s.strip_u.p);
       AFEM_LAUNCHED();
       // uniform / mixed slice lists (tets; triangles use the general path)
       DevBuf<uint8_t> uflag;
