@@ -19,6 +19,8 @@
 //      1-KiB line (a 16-B load per lane) per 4 incidence steps.
 #include "afem_internal.hpp"
 
+#include <hipcub/hipcub.hpp>
+
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -227,6 +229,66 @@ __global__ void k_count_valid(int64_t n, const int32_t* __restrict__ perm, unsig
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const unsigned long long b = __ballot(p < n && perm[p] >= 0);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (unsigned long long)__popcll(b));
+}
+
+// Meshes without a structured numbering: the processing order sorts the
+// owned nodes along a Morton (Z-order) curve of their coordinates, so the 64
+// rows of a slice are spatial neighbours (few distinct coupled nodes: the LDS
+// coordinate cache stays small, gathers stay in L2) whatever the caller's
+// numbering.  The matrix itself stays in the caller's node order.
+__device__ __forceinline__ unsigned long long ordered_bits(double v)
+{
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double from_ordered_bits(unsigned long long u)
+{
+  return __longlong_as_double((long long)((u >> 63) ? (u & 0x7fffffffffffffffull) : ~u));
+}
+__global__ void k_bbox(int64_t n, const double* __restrict__ coords, unsigned long long* __restrict__ box)
+{
+  unsigned long long mn[3] = { ~0ull, ~0ull, ~0ull }, mx[3] = { 0ull, 0ull, 0ull };
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    for (int a = 0; a < 3; ++a) {
+      const unsigned long long u = ordered_bits(coords[3 * i + a]);
+      mn[a] = u < mn[a] ? u : mn[a];
+      mx[a] = u > mx[a] ? u : mx[a];
+    }
+  for (int a = 0; a < 3; ++a) {
+    atomicMin(box + a, mn[a]);
+    atomicMax(box + 3 + a, mx[a]);
+  }
+}
+__device__ __forceinline__ uint64_t spread3(uint64_t v)  // 21 bits -> every third bit
+{
+  v &= 0x1fffffull;
+  v = (v | v << 32) & 0x1f00000000ffffull;
+  v = (v | v << 16) & 0x1f0000ff0000ffull;
+  v = (v | v << 8) & 0x100f00f00f00f00full;
+  v = (v | v << 4) & 0x10c30c30c30c30c3ull;
+  v = (v | v << 2) & 0x1249249249249249ull;
+  return v;
+}
+__global__ void k_morton_keys(int64_t n, const double* __restrict__ coords, const unsigned long long* __restrict__ box,
+                              uint64_t* __restrict__ keys, int32_t* __restrict__ ids)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t k = 0;
+  for (int a = 0; a < 3; ++a) {
+    const double lo = from_ordered_bits(box[a]), hi = from_ordered_bits(box[3 + a]);
+    const double t = hi > lo ? (coords[3 * i + a] - lo) / (hi - lo) : 0.0;
+    const uint64_t q = (uint64_t)fmin(fmax(t * 2097151.0, 0.0), 2097151.0);
+    k |= spread3(q) << a;
+  }
+  keys[i] = k;
+  ids[i] = (int32_t)i;
+}
+__global__ void k_perm_from_sorted(int64_t n_pos, int64_t n_rows, const int32_t* __restrict__ sorted,
+                                   int32_t* __restrict__ perm)
+{
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_pos) perm[p] = p < n_rows ? sorted[p] : -1;
 }
 
 __global__ void k_perm_identity(int64_t n_pos, int64_t n_rows, int32_t* __restrict__ perm)
@@ -779,11 +841,45 @@ void build_structure(Mesh& m, Structure& s)
   else {
     s.n_slices = (n_rows + 63) / 64;
     s.perm.alloc(s.n_slices * 64);
-    hipLaunchKernelGGL(k_perm_identity, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream,
-                       s.n_slices * 64, n_rows, s.perm.p);
-    AFEM_LAUNCHED();
+    // AFEM_ORDER=node: the caller's node order (diagnostic)
+    const char* oe = getenv("AFEM_ORDER");
+    const bool node_order = (oe && std::string(oe) == "node") || n_rows < 2;
+    if (node_order) {
+      hipLaunchKernelGGL(k_perm_identity, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream,
+                         s.n_slices * 64, n_rows, s.perm.p);
+      AFEM_LAUNCHED();
+      s.run = 64;
+    }
+    else {
+      DevBuf<unsigned long long> box;
+      box.alloc(6);
+      const unsigned long long init[6] = { ~0ull, ~0ull, ~0ull, 0ull, 0ull, 0ull };
+      AFEM_HIP(hipMemcpyAsync(box.p, init, sizeof(init), hipMemcpyHostToDevice, ctx.stream));
+      hipLaunchKernelGGL(k_bbox, dim3(1024), dim3(256), 0, ctx.stream, n_rows, m.coords.p, box.p);
+      AFEM_LAUNCHED();
+      DevBuf<uint64_t> keys, keys_out;
+      DevBuf<int32_t> ids, ids_out;
+      keys.alloc(n_rows);
+      keys_out.alloc(n_rows);
+      ids.alloc(n_rows);
+      ids_out.alloc(n_rows);
+      hipLaunchKernelGGL(k_morton_keys, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, m.coords.p,
+                         box.p, keys.p, ids.p);
+      AFEM_LAUNCHED();
+      size_t tmp_bytes = 0;
+      AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys.p, keys_out.p, ids.p, ids_out.p,
+                                                  (int)n_rows, 0, 64, ctx.stream));
+      DevBuf<unsigned char> tmp;
+      tmp.alloc(tmp_bytes > 0 ? tmp_bytes : 1);
+      AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tmp_bytes, keys.p, keys_out.p, ids.p, ids_out.p,
+                                                  (int)n_rows, 0, 64, ctx.stream));
+      hipLaunchKernelGGL(k_perm_from_sorted, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream,
+                         s.n_slices * 64, n_rows, ids_out.p, s.perm.p);
+      AFEM_LAUNCHED();
+      ctx.sync();
+      s.run = 1;  // a slice's rows are spatial neighbours, not consecutive rows
+    }
     s.brick_order = false;
-    s.run = 64;
   }
   const int64_t n_pos = s.n_slices * 64;
 
