@@ -300,9 +300,6 @@ __device__ __forceinline__ void write_back(const TILE& tile, int lane, int run, 
 // degenerate cells whose scale is masked to 0).  The diagonal is not
 // accumulated: rows of the P1 Laplacian sum to zero (sum of the shape
 // function gradients), so K_ii = -sum_{j != i} K_ij, formed before write-back.
-// ABL != 0 only in diagnostic runs (AFEM_ASSEMBLY_ABLATION, results wrong):
-// 1 = no element arithmetic, 2 = no LDS coordinate reads, 3 = no LDS adds,
-// 4 = no LDS staging (coordinates / indices / zeroing), 5 = no write-back.
 // native 4 x u32 vector: plain registers (HIP's uint4 is a union-based class
 // that keeps a struct copy of it in scratch)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -327,7 +324,7 @@ struct SlicePre {
 // predication): the waitcnt pass can then wait for a load without draining
 // the younger write-back stores (vmcnt retires in issue order).
 // MAXW = max row length (slots) the fixed write-back covers.
-template <int NV, int UCAP, int MAXG, int MAXW, int ABL = 0>
+template <int NV, int UCAP, int MAXG, int MAXW>
 __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t chunk, int u_cap, int w_cap,
                                                     int64_t pad_off, const int32_t* __restrict__ perm,
                                                     const int64_t* __restrict__ row_ptr,
@@ -398,7 +395,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
     const int nu = (int)(snode_ptr[sl + 1] - u0);
 
     // ---- stage slice sl from registers (+ the rare overflow beyond 256 nodes / 16 slots)
-    if (ABL != 4) {
+    {
       const int st = tile.stride();
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -447,28 +444,15 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
         sa[j] = e & 0xFFu;
         sb[j] = (e >> 8) & 0xFFu;
         sc[j] = (NV == 4) ? (e >> 16) & 0xFFu : 0u;
-        if (ABL == 2) {
-          xa[j] = V3{ xi.x + 1e-3 * sa[j], xi.y, xi.z };
-          xb[j] = V3{ xi.x, xi.y + 1e-3 * sb[j], xi.z };
-          xc[j] = V3{ xi.x, xi.y, xi.z + 1e-3 * sc[j] };
-        }
-        else {
-          xa[j] = tile.node(lane, sa[j]);
-          xb[j] = tile.node(lane, sb[j]);
-          if (NV == 4) xc[j] = tile.node(lane, sc[j]);
-        }
+        xa[j] = tile.node(lane, sa[j]);
+        xb[j] = tile.node(lane, sb[j]);
+        if (NV == 4) xc[j] = tile.node(lane, sc[j]);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bool pad = ev[j] == kPad;  // padding: degenerate cell (det 0), scale forced to 0
         double k1, k2, k3 = 0.0, meas;
-        if (ABL == 1) {
-          k1 = xa[j].y + xb[j].x;
-          k2 = xb[j].y + xc[j].x;
-          k3 = xc[j].y + xc[j].z;
-          meas = xa[j].z + xb[j].z;
-        }
-        else if (NV == 4) {
+        if (NV == 4) {
           const V3 e1 = sub(xa[j], xi), e2 = sub(xb[j], xi), e3 = sub(xc[j], xi);
           const V3 c1 = cross(e2, e3), c2 = cross(e3, e1), c3 = cross(e1, e2);
           const V3 c0 = V3{ -(c1.x + c2.x + c3.x), -(c1.y + c2.y + c3.y), -(c1.z + c2.z + c3.z) };
@@ -488,14 +472,9 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
           k2 = (c0x * c2x + c0y * c2y) * s;
         }
         macc += meas;
-        if (ABL != 3) {
-          atomicAdd(tile.at(lane, sa[j], 0), k1);
-          atomicAdd(tile.at(lane, sb[j], 0), k2);
-          if (NV == 4) atomicAdd(tile.at(lane, sc[j], 0), k3);
-        }
-        else {
-          macc += k1 + k2 + k3;
-        }
+        atomicAdd(tile.at(lane, sa[j], 0), k1);
+        atomicAdd(tile.at(lane, sb[j], 0), k2);
+        if (NV == 4) atomicAdd(tile.at(lane, sc[j], 0), k3);
       }
     };
     // unrolled over the compile-time group count (uniform skips past the
@@ -549,42 +528,20 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
       for (int t = 0; t < MAXW; ++t)
         if (t == (int)dslot) rv[t] = -sum;
       wave_sync_lds();  // every lane's reads before the overlapping flat writes
-      const int64_t rb_base = __shfl(rb, 0);
-      if (ABL != 5) {
 #pragma unroll
-        for (int t = 0; t < MAXW; ++t)
-          if (t < len) {
-            tile.acc[fp + t] = rv[t];
-            map[fp + t] = (uint16_t)(t * 64 + lane);
-          }
-        rbs[lane] = rb;
-        wave_sync_lds();
-        if (ABL == 6) {  // LDS side of the copy only: results folded into one store
-          double acc6 = 0.0;
-#pragma unroll
-          for (int k = 0; k < MAXW; ++k) {
-            const int P = min(64 * k + lane, total - 1);
-            const int m = map[P];
-            acc6 += tile.acc[P] + (double)(rbs[m & 63] + (m >> 6));
-          }
-          if (acc6 == 12345.678) vals[0] = acc6;
+      for (int t = 0; t < MAXW; ++t)
+        if (t < len) {
+          tile.acc[fp + t] = rv[t];
+          map[fp + t] = (uint16_t)(t * 64 + lane);
         }
-        else if (ABL == 7) {  // stores only: coalesced stores of a register value
+      rbs[lane] = rb;
+      wave_sync_lds();
 #pragma unroll
-          for (int k = 0; k < MAXW; ++k) {
-            const int P = min(64 * k + lane, total - 1);
-            vals[rb_base + P] = rv[k];
-          }
-        }
-        else {
-#pragma unroll
-          for (int k = 0; k < MAXW; ++k) {
-            const int P = min(64 * k + lane, total - 1);
-            const double v = tile.acc[P];
-            const int m = map[P];
-            vals[rbs[m & 63] + (m >> 6)] = v;
-          }
-        }
+      for (int k = 0; k < MAXW; ++k) {
+        const int P = min(64 * k + lane, total - 1);
+        const double v = tile.acc[P];
+        const int m = map[P];
+        vals[rbs[m & 63] + (m >> 6)] = v;
       }
     }
     else {  // rows longer than MAXW (not on the host-selected variants)
@@ -1959,10 +1916,6 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
     return;
   }
   const size_t shm = (size_t)tile_bytes(dimc, 1, kUcapBuckets[bucket], s.max_slice_w);
-  static const int abl = [] {
-    const char* e = getenv("AFEM_ASSEMBLY_ABLATION");
-    return e ? atoi(e) : 0;
-  }();
   // persistent grid: as many single-wave workgroups as the LDS tile and the
   // registers let reside at once, each walking a contiguous chunk of slices
   // (occupancy queried once per (kernel, LDS size); kept off the launch path)
@@ -1983,37 +1936,26 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
                        s.inc_slice_ptr.p, s.inc_slice_k.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p,
                        s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
   };
-#define AFEM_ASM_K(NV_, U_, G_, W_, A_) launch(reinterpret_cast<const void*>(&k_assemble_p1<NV_, U_, G_, W_, A_>), k_assemble_p1<NV_, U_, G_, W_, A_>)
-#define AFEM_ASM_LAUNCH(NV_, U_, A_)            \
+#define AFEM_ASM_K(NV_, U_, G_, W_) launch(reinterpret_cast<const void*>(&k_assemble_p1<NV_, U_, G_, W_>), k_assemble_p1<NV_, U_, G_, W_>)
+#define AFEM_ASM_LAUNCH(NV_, U_)                \
   do {                                          \
-    if (prof == 0) AFEM_ASM_K(NV_, U_, 6, 16, A_); \
-    else AFEM_ASM_K(NV_, U_, 16, 32, A_);          \
+    if (prof == 0) AFEM_ASM_K(NV_, U_, 6, 16);  \
+    else AFEM_ASM_K(NV_, U_, 16, 32);           \
   } while (0)
-  if (nv == 4 && bucket == 0 && abl != 0 && prof == 0) {
-    switch (abl) {
-      case 1: AFEM_ASM_K(4, 257, 6, 16, 1); break;
-      case 2: AFEM_ASM_K(4, 257, 6, 16, 2); break;
-      case 3: AFEM_ASM_K(4, 257, 6, 16, 3); break;
-      case 4: AFEM_ASM_K(4, 257, 6, 16, 4); break;
-      case 5: AFEM_ASM_K(4, 257, 6, 16, 5); break;
-      case 6: AFEM_ASM_K(4, 257, 6, 16, 6); break;
-      default: AFEM_ASM_K(4, 257, 6, 16, 7);
-    }
-  }
-  else if (nv == 4) {
+  if (nv == 4) {
     switch (bucket) {
-      case 0: AFEM_ASM_LAUNCH(4, 257, 0); break;
-      case 1: AFEM_ASM_LAUNCH(4, 513, 0); break;
-      case 2: AFEM_ASM_LAUNCH(4, 1025, 0); break;
-      default: AFEM_ASM_LAUNCH(4, 2049, 0);
+      case 0: AFEM_ASM_LAUNCH(4, 257); break;
+      case 1: AFEM_ASM_LAUNCH(4, 513); break;
+      case 2: AFEM_ASM_LAUNCH(4, 1025); break;
+      default: AFEM_ASM_LAUNCH(4, 2049);
     }
   }
   else {
     switch (bucket) {
-      case 0: AFEM_ASM_LAUNCH(3, 257, 0); break;
-      case 1: AFEM_ASM_LAUNCH(3, 513, 0); break;
-      case 2: AFEM_ASM_LAUNCH(3, 1025, 0); break;
-      default: AFEM_ASM_LAUNCH(3, 2049, 0);
+      case 0: AFEM_ASM_LAUNCH(3, 257); break;
+      case 1: AFEM_ASM_LAUNCH(3, 513); break;
+      case 2: AFEM_ASM_LAUNCH(3, 1025); break;
+      default: AFEM_ASM_LAUNCH(3, 2049);
     }
   }
 #undef AFEM_ASM_K
