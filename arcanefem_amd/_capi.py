@@ -15,6 +15,14 @@ LIB_PATH = os.environ.get("AFEM_LIB") or os.path.join(_HERE, "libafem.so")  # AF
 AFEM_OK = 0
 AFEM_MEM_HOST = 0
 AFEM_MEM_DEVICE = 1
+AFEM_RHS_ADD = 0
+AFEM_RHS_SET = 1
+AFEM_SOLVER_AUTO = 0
+AFEM_SOLVER_PCG = 1
+AFEM_SOLVER_DIRECT = 2
+AFEM_NEUMANN_VALUE = 0
+AFEM_NEUMANN_NORMAL = 1
+AFEM_NEUMANN_TRACTION = 2
 UNIQUE_ID_BYTES = 128
 ERRORS = {1: "ArgumentException", 2: "HipError", 3: "NotImplementedException", 4: "StateError",
           5: "NotFound", 6: "CommError", 7: "LimitExceeded"}
@@ -41,7 +49,8 @@ class BsrStats(ctypes.Structure):
     _fields_ = [("n_incidences", ctypes.c_int64), ("inc_table_entries", ctypes.c_int64),
                 ("max_row_len", ctypes.c_int32), ("rows_per_block", ctypes.c_int32), ("max_seg", ctypes.c_int64),
                 ("max_slice_nodes", ctypes.c_int32), ("max_slice_width", ctypes.c_int32),
-                ("n_slices", ctypes.c_int64), ("brick_order", ctypes.c_int32), ("uniform_slices", ctypes.c_int32)]
+                ("n_slices", ctypes.c_int64), ("brick_order", ctypes.c_int32), ("uniform_slices", ctypes.c_int32),
+                ("last_kernel", ctypes.c_int32)]
 
 
 class SolverOpts(ctypes.Structure):
@@ -85,8 +94,10 @@ SIGNATURES = {
     "afem_bsr_create": [P, INT, INT, PP],
     "afem_bsr_compute_sparsity": [P],
     "afem_bsr_assemble_poisson_p1": [P, D, D, P],
+    "afem_bsr_assemble_poisson_p1_ex": [P, D, D, P, INT],
     "afem_bsr_assemble_elasticity_p1": [P, D, D],
-    "afem_bsr_assemble_elasticity_p1_ex": [P, D, D, D, P, P],
+    "afem_bsr_assemble_elasticity_p1_ex": [P, D, D, D, P, P, INT],
+    "afem_apply_neumann": [P, INT, INT, P, I64, P, P, INT, P],
     "afem_vec_lincomb": [P, I64, D, P, D, P, D, P, P],
     "afem_newmark_update": [P, I64, D, D, D, P, P, P, P],
     "afem_bsr_reset_values": [P],

@@ -23,11 +23,37 @@ from . import _capi as C
 from ._capi import AfemError, call
 
 __all__ = ["AfemError", "Context", "Mesh", "BSRFormat", "DoFLinearSystem", "HipDoFLinearSystemFactory",
-           "device_count", "structured_halo_plan"]
+           "applyNeumannToRhs", "device_count", "structured_halo_plan"]
 
 
 def _ptr(a: np.ndarray):
     return ctypes.c_void_p(a.ctypes.data)
+
+
+def _rhs_mode(mode: str) -> int:
+    if mode not in ("add", "set"):
+        raise ValueError(f"rhs_mode must be 'add' or 'set', got {mode!r}")
+    return C.AFEM_RHS_ADD if mode == "add" else C.AFEM_RHS_SET
+
+
+NEUMANN_MODES = {"value": C.AFEM_NEUMANN_VALUE, "normal": C.AFEM_NEUMANN_NORMAL, "traction": C.AFEM_NEUMANN_TRACTION}
+
+
+def applyNeumannToRhs(mesh: "Mesh", rhs_dptr: int, faces, value, mode: str = "normal", nb_dof: int = 1,
+                      face_cells=None):
+    """BoundaryConditions{2D,3D}::applyNeumannToRhs (femutils/ArcaneFemFunctionsGpu.h:612-766)
+    and the elasticity traction term (modules/elasticity/FemModule.cc:244-273):
+    adds the boundary-face term of `faces` (host int32 [n_faces, dim] local
+    node ids) to the device RHS.  mode "value": scalar g; "normal": (v . n)
+    with the outward normal (oriented by `face_cells`); "traction": vector t,
+    one component per DoF."""
+    faces = np.ascontiguousarray(faces, dtype=np.int32).reshape(-1, mesh.dim)
+    v = np.zeros(3)
+    vv = np.atleast_1d(np.asarray(value, dtype=np.float64))
+    v[:vv.shape[0]] = vv
+    fc = None if face_cells is None else np.ascontiguousarray(face_cells, dtype=np.int32)
+    call("afem_apply_neumann", mesh.h, nb_dof, NEUMANN_MODES[mode], _ptr(v), faces.shape[0], _ptr(faces),
+         None if fc is None else _ptr(fc), C.AFEM_MEM_HOST, ctypes.c_void_p(rhs_dptr))
 
 
 def device_count() -> int:
@@ -168,25 +194,28 @@ class BSRFormat:
     def computeSparsity(self):
         call("afem_bsr_compute_sparsity", self.h)
 
-    def assemblePoissonP1(self, coef: float = 1.0, f: float | None = None, rhs_dptr: int | None = None):
+    def assemblePoissonP1(self, coef: float = 1.0, f: float | None = None, rhs_dptr: int | None = None,
+                          rhs_mode: str = "add"):
         """assembleBilinear(_computeElementMatrix{Tria3,Tetra4}Gpu) fused with
-        applyConstantSourceToRhs(f) into rhs_dptr when given."""
-        call("afem_bsr_assemble_poisson_p1", self.h, coef, 0.0 if f is None else f,
-             ctypes.c_void_p(rhs_dptr) if rhs_dptr else None)
+        applyConstantSourceToRhs(f) into rhs_dptr when given.  rhs_mode "add"
+        accumulates (the reference's atomic adds); "set" overwrites (the
+        module's rhs.fill(0) + source in one pass)."""
+        call("afem_bsr_assemble_poisson_p1_ex", self.h, coef, 0.0 if f is None else f,
+             ctypes.c_void_p(rhs_dptr) if rhs_dptr else None, _rhs_mode(rhs_mode))
 
     def assembleElasticityP1(self, lam: float, mu2: float):
         call("afem_bsr_assemble_elasticity_p1", self.h, lam, mu2)
 
     def assembleElasticityP1Ex(self, lam: float, mu2: float, mass_coef: float = 0.0, body_force=None,
-                               rhs_dptr: int | None = None):
+                               rhs_dptr: int | None = None, rhs_mode: str = "add"):
         """Block-3 tetrahedra: lambda/mu2 stiffness + mass_coef * consistent mass
         (Newmark LHS c0 M + K) and, with body_force (3 floats), the vectorial
-        constant source into rhs_dptr (3 per owned node)."""
+        constant source into rhs_dptr (3 per owned node; rhs_mode as above)."""
         f = None
         if body_force is not None:
             f = (ctypes.c_double * 3)(*[float(x) for x in body_force])
         call("afem_bsr_assemble_elasticity_p1_ex", self.h, lam, mu2, mass_coef, f,
-             ctypes.c_void_p(rhs_dptr) if rhs_dptr else None)
+             ctypes.c_void_p(rhs_dptr) if rhs_dptr else None, _rhs_mode(rhs_mode))
 
     def resetMatrixValues(self):
         call("afem_bsr_reset_values", self.h)
@@ -358,9 +387,14 @@ class DoFLinearSystem:
     def applyBoundaryConditions(self):
         call("afem_ls_apply_boundary_conditions", self.impl)
 
-    def setSolverOptions(self, rtol=None, atol=None, max_iter=None, check_every=None, fixed_iterations=None):
+    SOLVERS = {"auto": C.AFEM_SOLVER_AUTO, "pcg": C.AFEM_SOLVER_PCG, "direct": C.AFEM_SOLVER_DIRECT}
+
+    def setSolverOptions(self, rtol=None, atol=None, max_iter=None, check_every=None, fixed_iterations=None,
+                         method=None):
         o = C.SolverOpts()
         call("afem_ls_get_solver_options", self.impl, ctypes.byref(o))
+        if method is not None:
+            o.method = self.SOLVERS[method]
         if rtol is not None:
             o.rtol = rtol
         if atol is not None:

@@ -185,6 +185,7 @@ struct Bsr {
   bool has_sparsity = false;
   Structure s;
   DevBuf<double> values;       // [nnz * nb_dof^2]
+  int last_kernel = 0;         // AFEM_KERNEL_* of the last assembly launch (afem_bsr_stats)
   // scalar CSR expansion for NB_DOF>1 (built on demand)
   DevBuf<int64_t> csr_rows;
   DevBuf<int32_t> csr_cols;
@@ -221,12 +222,17 @@ struct LinearSystem {
   double* csr_vals = nullptr;
   DevBuf<int64_t> own_rows;   // when the view came in the reference int32 layout
   DevBuf<int32_t> own_cols;
-  DevBuf<double> own_vals;    // COO-built matrix
+  DevBuf<double> own_vals;    // host-uploaded or COO-built matrix
+  // the CSR was rebuilt from the host COO maps (matrixAddValue without a
+  // view): later adds/sets go to the maps again; any other CSR view (device,
+  // host-uploaded, BSR) is updated in place
+  bool csr_from_coo = false;
   // host COO (Aleph semantics)
   std::map<std::pair<int32_t, int32_t>, double> add_map, set_map;
   std::map<int32_t, std::pair<uint8_t, double>> host_elim;
   // solver work
   DevBuf<double> r, z, p, q, dinv, partial, scal;
+  DevBuf<double> dense;  // direct solver: augmented n x (n+1) matrix
   DevBuf<uint8_t> cons;  // constraint-row flags of the stopping test
   double* pinned = nullptr;
   std::unique_ptr<Halo> halo;
@@ -236,11 +242,15 @@ struct LinearSystem {
 void exclusive_scan_i64(Ctx& ctx, const int64_t* in, int64_t* out, int64_t n, DevBuf<int64_t>* tmp_pool = nullptr);
 void exclusive_scan_i32_to_i64(Ctx& ctx, const int32_t* in, int64_t* out, int64_t n);
 int64_t read_i64(Ctx& ctx, const int64_t* d);
+void device_minmax_i32(Ctx& ctx, const int32_t* a, int64_t n, int32_t* lo, int32_t* hi);
 
 void build_structure(Mesh& m, Structure& s);
-void assemble_scalar(Bsr& b, double coef, double f, double* rhs);
+// rhs_add: 1 accumulate into rhs (applyConstantSourceToRhs), 0 overwrite
+void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add);
 void assemble_elasticity_tri(Bsr& b, double lambda, double mu2);
-void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const double* f, double* rhs);
+void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const double* f, double* rhs, int rhs_add);
+void apply_neumann(Mesh& m, int k, int mode, const double* v, int64_t n_faces, const int32_t* face_nodes,
+                   const int32_t* face_cells, int mem, double* rhs);
 bool assembly_uses_lds(const Bsr& b);  // slice tile fits the LDS budget
 
 void ls_apply_bcs(LinearSystem& ls);

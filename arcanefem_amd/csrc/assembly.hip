@@ -26,12 +26,6 @@
 #include <cstdlib>
 #include <type_traits>
 
-#ifndef AFEM_WB
-#define AFEM_WB 0  // strip kernel write-back: 0 flat LDS image (default), 1 per-lane stores (diagnostic)
-#endif
-#ifndef AFEM_ABL
-#define AFEM_ABL 0  // diagnostic ablations of the uniform strip kernel (build_abl/, tools/ab.sh)
-#endif
 
 
 namespace afem {
@@ -338,7 +332,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
                                                     const int32_t* __restrict__ snode,
                                                     const double* __restrict__ coords, double s_coef,
                                                     double f_meas, double* __restrict__ vals,
-                                                    double* __restrict__ rhs)
+                                                    double* __restrict__ rhs, int rhs_add)
 {
   constexpr int DIMC = NV == 4 ? 3 : 2;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -493,7 +487,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
       const int src = active ? lane : (int)__ffsll((long long)am) - 1;
       const double rv = __shfl(f_meas * macc, src);
       const int32_t rr = __shfl(row, src);
-      if (rhs) rhs[rr] = rv;
+      if (rhs) rhs[rr] = rhs_add ? rhs[rr] + rv : rv;
     }
     wave_sync_lds();
 
@@ -631,7 +625,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
                                                           const int32_t* __restrict__ snode,
                                                           const double* __restrict__ coords, double s_coef,
                                                           double f_meas, double* __restrict__ vals,
-                                                          double* __restrict__ rhs)
+                                                          double* __restrict__ rhs, int rhs_add)
 {
   constexpr bool UNI = UMODE != 0;  // 1: scalar shift/swap branches, 2: selects on the uniform bit
   // uniform tet instances address coordinates by the local-index stream (no
@@ -887,16 +881,6 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
         aQ = aR;
         eR = eD;
         aR = aD;
-#if AFEM_ABL == 3  // ablation: no element arithmetic
-        cP = eR;
-        cN = eQ;
-        macc += eD.x;
-        atomicAdd(aP, eD.x);
-        atomicAdd(aQ, eD.y);
-        atomicAdd(aR, eD.z);
-        (void)cRn;
-        return;
-#endif
         cP = cross(eQ, eR);
         cN = cross(eP, eR);
         const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
@@ -908,18 +892,9 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
         const double kQ = -dot(m, cN) * s;
         const double kR = dot(m, cRn) * s;
         macc += meas;
-#if AFEM_ABL == 1  // ablation: plain LDS writes instead of LDS atomics
-        *aP = kP;
-        *aQ = kQ;
-        *aR = kR;
-#elif AFEM_ABL == 2  // ablation: no LDS accumulation
-        macc += kP + kQ + kR;
-        (void)aP;
-#else
         atomicAdd(aP, kP);
         atomicAdd(aQ, kQ);
         atomicAdd(aR, kR);
-#endif
       };
       {
         const uint32_t b0 = byte_at(0), b1 = byte_at(1);
@@ -933,12 +908,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
 #pragma unroll
       for (int j = 2; j < NSTEP; ++j) {
         if ((j & (UMODE == 1 ? 1 : 3)) == 0 && j >= nsteps) break;
-#if AFEM_ABL == 5  // ablation: no LDS index / coordinate reads in the step loop
-        const double fb = (double)(byte_at(j + 1 < NSTEP ? j + 1 : j) & 63u);
-        const V3 xn = V3{ xi.x + fb, xi.y - fb, xi.z + 2 * fb };
-#else
         const V3 xn = j + 1 < NSTEP ? coord(uloc_at(j + 1)) : xc;
-#endif
         const bool swp = (pat >> j) & 1u;
         if constexpr (UMODE == 2) ustep(std::integral_constant<int, -1>{}, byte_at(j), xc, swp);
         else if (__builtin_expect(swp, 0)) ustep(std::integral_constant<int, 1>{}, byte_at(j), xc, true);
@@ -967,29 +937,13 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
       const int src = active ? lane : (int)__ffsll((long long)am) - 1;
       const double rv = __shfl(f_meas * macc, src);
       const int32_t rr = __shfl(row, src);
-      if (rhs) rhs[rr] = rv;
+      if (rhs) rhs[rr] = rhs_add ? rhs[rr] + rv : rv;
     }
     wave_sync_lds();
 
     // ---- diagonal + write-back through a flat LDS image (as k_assemble_p1;
     // the map overlays the coordinates).  (Per-lane 16-B stores straight from
     // registers measured ~2% slower on C2.)
-#if AFEM_ABL == 8  // ablation: no value write-back (LDS image and stores)
-    if (acc_lane[0] == 12345.678) vals[rb] = acc_lane[64];
-    wave_sync_lds();
-    if (p1 >= r1) break;
-    p0 = p1;
-    p1 = p2;
-    p2 = p3;
-    p3 = claim_get(t4);
-    R0 = R1;
-    R1 = R2;
-    R2 = R3;
-    cur = nxt;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) nid1[k] = nid2[k];
-    continue;
-#endif
     int fp = len;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1015,22 +969,6 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
 #pragma unroll
       for (int t = 0; t < MAXW; ++t)
         if (t < W) sum += rv[t];  // uniform bound
-#if AFEM_WB == 1  // diagnostic: per-lane 16-B stores straight from registers
-      double* const rowp = vals + rb;
-#pragma unroll
-      for (int t = 0; t < MAXW; t += 2) {
-        if (t < W) {
-          if (t + 1 < len) {
-            rowp[t] = rv[t];
-            rowp[t + 1] = rv[t + 1];
-          }
-          else if (t < len) rowp[t] = rv[t];
-        }
-      }
-      if (active) rowp[dslot] = -sum;
-      (void)fp;
-      (void)total;
-#else
       uint32_t* const map32 = reinterpret_cast<uint32_t*>(cxyz);
       wave_sync_lds();  // every lane's reads before the overlapping flat writes
 #pragma unroll
@@ -1046,7 +984,6 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
         const int P = min(64 * k + lane, total - 1);
         vals[map32[P]] = acc[P];
       }
-#endif
     }
     else {
       if (dsl != 0xFFu) {
@@ -1104,7 +1041,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
                                                              const int32_t* __restrict__ snode,
                                                              const double* __restrict__ coords, double lambda,
                                                              double mu, double c0, double fx, double fy, double fz,
-                                                             double* __restrict__ vals, double* __restrict__ rhs)
+                                                             double* __restrict__ vals, double* __restrict__ rhs, int rhs_add)
 {
   extern __shared__ __align__(16) unsigned char smem[];
   double* acc = reinterpret_cast<double*>(smem);  // [slot][k][lane]
@@ -1334,7 +1271,10 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
         u1 = u2;
       }
     }
-    if (rhs && active) rhs[3 * (int64_t)row + ci] = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
+    if (rhs && active) {
+    const double rv = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
+    rhs[3 * (int64_t)row + ci] = rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv;
+  }
     wave_sync_lds();
 
     // ---- diagonal block row + write-back through a flat LDS image
@@ -1436,7 +1376,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_tet(int u_cap, int w_cap,
                                                            const int32_t* __restrict__ snode,
                                                            const double* __restrict__ coords, double lambda, double mu,
                                                            double c0, double fx, double fy, double fz,
-                                                           double* __restrict__ vals, double* __restrict__ rhs)
+                                                           double* __restrict__ vals, double* __restrict__ rhs, int rhs_add)
 {
   extern __shared__ __align__(16) unsigned char smem[];
   double* acc = reinterpret_cast<double*>(smem);  // [slot][j][lane]
@@ -1500,11 +1440,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_tet(int u_cap, int w_cap,
     atomicAdd(a + 64, v1);
     atomicAdd(a + 128, v2);
   };
-#if AFEM_ABL == 10  // ablation (block-3): staging and write-back only
-  for (int c = 0; 16 * c < 0 * nsteps; ++c) {
-#else
   for (int c = 0; 16 * c < nsteps; ++c) {
-#endif
     const u32x4 w = sp[(int64_t)c * 64];
     const uint32_t wv[4] = { w.x, w.y, w.z, w.w };
     for (int j = 0; j < 16; ++j) {
@@ -1533,7 +1469,10 @@ __global__ __launch_bounds__(64) void k_assemble_elast_tet(int u_cap, int w_cap,
       block(aR, m, cRn, s, mass);
     }
   }
-  if (rhs && active) rhs[3 * (int64_t)row + ci] = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
+  if (rhs && active) {
+    const double rv = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
+    rhs[3 * (int64_t)row + ci] = rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv;
+  }
   wave_sync_lds();
   // diagonal block row ci, then the row's 3*len values
   if (active) {
@@ -1543,9 +1482,6 @@ __global__ __launch_bounds__(64) void k_assemble_elast_tet(int u_cap, int w_cap,
         for (int jj = 0; jj < 3; ++jj) sum[jj] += acc_lane[192 * t + 64 * jj];
     for (int jj = 0; jj < 3; ++jj)
       acc_lane[192 * dslot + 64 * jj] = -sum[jj] + (jj == ci ? c0 * macc * (1.0 / 24.0) : 0.0);
-#if AFEM_ABL == 9  // ablation (block-3): no value stores
-    if (acc_lane[0] == 12345.678)
-#endif
     for (int t = 0; t < len; ++t)
       for (int jj = 0; jj < 3; ++jj)
         vals[per_block ? (rb + t) * 9 + 3 * ci + jj : rb * 9 + (int64_t)ci * 3 * len + 3 * t + jj] =
@@ -1564,7 +1500,7 @@ __global__ __launch_bounds__(64) void k_assemble_p1_global(const int32_t* __rest
                                                            const int32_t* __restrict__ slice_k,
                                                            const double* __restrict__ coords, double s_coef,
                                                            double f_meas, double* __restrict__ vals,
-                                                           double* __restrict__ rhs)
+                                                           double* __restrict__ rhs, int rhs_add)
 {
   const int lane = threadIdx.x;
   const int64_t sl = blockIdx.x;
@@ -1597,7 +1533,67 @@ __global__ __launch_bounds__(64) void k_assemble_p1_global(const int32_t* __rest
     if (NV == 4) arow[(e >> 16) & 0xFFu] += k3;
   }
   if (dslot != 0xFFu) arow[dslot] = dacc;
-  if (rhs) rhs[row] = f_meas * macc;
+  if (rhs) rhs[row] = rhs_add ? rhs[row] + f_meas * macc : f_meas * macc;
+}
+
+// Block-3 global-memory variant for meshes without row strips (a node with
+// more than 64 incident cells, rows of more than 64 blocks): one wave per
+// (slice, component row ci), lane-owned rows, the incidence table gives the
+// row-slots of each incident cell's other nodes, coordinates gathered through
+// the columns, entries accumulated in place (each value has one writer).
+// Same element matrix as the strip kernels (orc_element_elasticity_tet4):
+// K_rb^{ij} = [lambda c_r,i c_b,j + mu (c_r,j c_b,i + d_ij c_r.c_b)] / (6|det|)
+// + c0 |det|/120 (1 + d_rb) d_ij, c the cofactors (gradients x det).
+__global__ __launch_bounds__(64) void k_assemble_elast_tet_global(
+    bool per_block, const int32_t* __restrict__ perm, const int64_t* __restrict__ row_ptr,
+    const int32_t* __restrict__ cols, const uint32_t* __restrict__ inc, const int64_t* __restrict__ slice_ptr,
+    const int32_t* __restrict__ slice_k, const double* __restrict__ coords, double lambda, double mu, double c0,
+    double fx, double fy, double fz, double* __restrict__ vals, double* __restrict__ rhs, int rhs_add)
+{
+  const int lane = threadIdx.x;
+  const int64_t sl = blockIdx.x / 3;
+  const int ci = (int)(blockIdx.x % 3);
+  const int32_t row = perm[sl * 64 + lane];
+  if (row < 0) return;
+  const int64_t rb = row_ptr[row];
+  const int len = (int)(row_ptr[row + 1] - rb);
+  auto vidx = [&](int t, int j) -> int64_t {
+    return per_block ? (rb + t) * 9 + 3 * ci + j : rb * 9 + (int64_t)ci * 3 * len + 3 * t + j;
+  };
+  for (int t = 0; t < len; ++t)
+    for (int j = 0; j < 3; ++j) vals[vidx(t, j)] = 0.0;
+  const int32_t* crow = cols + rb;
+  const V3 xi = ld3(coords, row);
+  const uint32_t* ip = inc + slice_ptr[sl] + lane * 4;
+  const int kmax = slice_k[sl];
+  auto comp = [](V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); };
+  double macc = 0.0;
+  for (int k = 0; k < kmax; ++k) {
+    const uint32_t e = ip[(int64_t)(k >> 2) * 256 + (k & 3)];
+    if (e == kPad) break;
+    const int slot[4] = { (int)(e >> 24), (int)(e & 0xFFu), (int)((e >> 8) & 0xFFu), (int)((e >> 16) & 0xFFu) };
+    const V3 e1 = sub(ld3(coords, crow[slot[1]]), xi), e2 = sub(ld3(coords, crow[slot[2]]), xi),
+             e3 = sub(ld3(coords, crow[slot[3]]), xi);
+    const V3 c1 = cross(e2, e3), c2 = cross(e3, e1), c3 = cross(e1, e2);
+    const V3 cr = V3{ -(c1.x + c2.x + c3.x), -(c1.y + c2.y + c3.y), -(c1.z + c2.z + c3.z) };
+    const double meas = fabs(dot(e1, c1));
+    const double s = 1.0 / (6.0 * meas);
+    const double mass = c0 * meas * (1.0 / 120.0);
+    macc += meas;
+    const V3 cb[4] = { cr, c1, c2, c3 };
+    for (int b = 0; b < 4; ++b) {
+      const double t = dot(cr, cb[b]);
+      for (int j = 0; j < 3; ++j) {
+        double v = (lambda * comp(cr, ci) * comp(cb[b], j) + mu * (comp(cr, j) * comp(cb[b], ci) + (ci == j ? t : 0.0))) * s;
+        if (ci == j) v += b == 0 ? 2.0 * mass : mass;
+        vals[vidx(slot[b], j)] += v;
+      }
+    }
+  }
+  if (rhs) {
+    const double rv = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
+    rhs[3 * (int64_t)row + ci] = rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv;
+  }
 }
 
 // ---------------------------------------------------------------- block-2 elasticity (TRIA3)
@@ -1830,7 +1826,7 @@ int occ_override()
 }
 }  // namespace
 
-void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
+void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
 {
   Structure& s = b.s;
   Ctx& ctx = *b.mesh->ctx;
@@ -1875,7 +1871,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
       if (nblk > n_list) nblk = n_list < 8 ? 8 : n_list;
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, ctx.stream, n_list, list, tk,
                          s.max_slice_nodes, s.max_slice_w, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.strip_u.p,
-                         s.lidx.p, s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
+                         s.lidx.p, s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add);
     };
     const SliceRec* list_m = use_uni ? s.rec_m.p : s.rec_all.p;
 #define AFEM_STRIP_K(NV_, C_, W_, U_, N_, L_, T_)                                                                      \
@@ -1899,6 +1895,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
     }
 #undef AFEM_STRIP_K
     AFEM_LAUNCHED();
+    b.last_kernel = AFEM_KERNEL_STRIP;
     return;
   }
   // register-resident incidence groups per lane / fixed write-back width
@@ -1908,11 +1905,12 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
   if (bucket < 0 || prof < 0) {
     if (nv == 4)
       hipLaunchKernelGGL(k_assemble_p1_global<4>, grid, blk, 0, ctx.stream, s.perm.p, s.row_ptr.p, s.cols.p, s.inc.p,
-                         s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
+                         s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add);
     else
       hipLaunchKernelGGL(k_assemble_p1_global<3>, grid, blk, 0, ctx.stream, s.perm.p, s.row_ptr.p, s.cols.p, s.inc.p,
-                         s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
+                         s.inc_slice_ptr.p, s.inc_slice_k.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add);
     AFEM_LAUNCHED();
+    b.last_kernel = AFEM_KERNEL_GLOBAL;
     return;
   }
   const size_t shm = (size_t)tile_bytes(dimc, 1, kUcapBuckets[bucket], s.max_slice_w);
@@ -1934,7 +1932,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
     hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm, ctx.stream, s.n_slices, chunk,
                        s.max_slice_nodes, s.max_slice_w, s.inc_pad_off, s.perm.p, s.row_ptr.p, s.inc.p,
                        s.inc_slice_ptr.p, s.inc_slice_k.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p,
-                       s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs);
+                       s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add);
   };
 #define AFEM_ASM_K(NV_, U_, G_, W_) launch(reinterpret_cast<const void*>(&k_assemble_p1<NV_, U_, G_, W_>), k_assemble_p1<NV_, U_, G_, W_>)
 #define AFEM_ASM_LAUNCH(NV_, U_)                \
@@ -1961,6 +1959,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs)
 #undef AFEM_ASM_K
 #undef AFEM_ASM_LAUNCH
   AFEM_LAUNCHED();
+  b.last_kernel = AFEM_KERNEL_SLICE_TILE;
 }
 
 bool assembly_uses_lds(const Bsr& b)
@@ -1975,15 +1974,24 @@ bool assembly_uses_lds(const Bsr& b)
   return tile_bytes(dimc, nacc, b.s.max_slice_nodes, b.s.max_slice_w) <= kTileLdsMax;
 }
 
-void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const double* f, double* rhs)
+void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const double* f, double* rhs, int rhs_add)
 {
   Structure& s = b.s;
   Ctx& ctx = *b.mesh->ctx;
   AFEM_REQUIRE(b.nb_dof == 3 && b.mesh->nv == 4, AFEM_ERR_NOT_IMPL,
                "block-3 P1 elasticity assembly needs NB_DOF = 3 on tetrahedra");
-  AFEM_REQUIRE(s.strip_ok, AFEM_ERR_NOT_IMPL,
-               "block-3 elasticity assembly needs row strips (rows of at most 64 blocks and 64 incident cells)");
   const double fx = f ? f[0] : 0.0, fy = f ? f[1] : 0.0, fz = f ? f[2] : 0.0;
+  const int64_t shm_old = 3 * 8 * 64 * (int64_t)s.max_slice_w + ((24 * (int64_t)s.max_slice_nodes + 15) & ~int64_t(15)) +
+                          2 * 64 * (int64_t)s.max_slice_w;
+  if (!s.strip_ok || s.max_slice_w > 16 || shm_old > 160 * 1024) {
+    // no row strips (high-valence nodes) or rows too long for the LDS tile
+    hipLaunchKernelGGL(k_assemble_elast_tet_global, dim3((unsigned)(3 * s.n_slices)), dim3(64), 0, ctx.stream,
+                       b.order_per_block, s.perm.p, s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p,
+                       b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr, rhs_add);
+    AFEM_LAUNCHED();
+    b.last_kernel = AFEM_KERNEL_ELAST3_GLOBAL;
+    return;
+  }
   // persistent pipelined kernel (AFEM_ELAST_STRIP=0: the one-wave-per-item kernel, diagnostic)
   const char* ee = getenv("AFEM_ELAST_STRIP");
   const bool use_new = !(ee && atoi(ee) == 0);
@@ -2007,7 +2015,7 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
       if (nblk > n_items) nblk = n_items < 8 ? 8 : n_items;
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm2, ctx.stream, n_items, list, tk, s.max_slice_nodes,
                          s.max_slice_w, b.order_per_block, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p,
-                         s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr);
+                         s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr, rhs_add);
       AFEM_LAUNCHED();
     };
     if (use_uni)
@@ -2017,16 +2025,15 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
     if (n_mix > 0)
       launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16, 0>), k_assemble_elast_strip<2, 16, 0>,
              3 * n_mix, use_uni ? s.rec_m.p : s.rec_all.p, s.tickets.p + 128);
+    b.last_kernel = AFEM_KERNEL_ELAST3_STRIP;
     return;
   }
-  const int64_t shm = 3 * 8 * 64 * (int64_t)s.max_slice_w + ((24 * (int64_t)s.max_slice_nodes + 15) & ~int64_t(15)) +
-                      2 * 64 * (int64_t)s.max_slice_w;
-  AFEM_REQUIRE(shm <= 160 * 1024, AFEM_ERR_LIMIT, "block-3 slice tile exceeds the LDS of a CU");
-  hipLaunchKernelGGL(k_assemble_elast_tet<16>, dim3((unsigned)(3 * s.n_slices)), dim3(64), (size_t)shm, ctx.stream,
+  hipLaunchKernelGGL(k_assemble_elast_tet<16>, dim3((unsigned)(3 * s.n_slices)), dim3(64), (size_t)shm_old, ctx.stream,
                      s.max_slice_nodes, s.max_slice_w, b.order_per_block, s.perm.p, s.row_ptr.p, s.strip.p,
                      s.strip_ptr.p, s.strip_n.p, s.dslot.p, s.slice_w.p, s.lidx_ptr.p, s.lidx.p, s.snode_ptr.p,
-                     s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr);
+                     s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr, rhs_add);
   AFEM_LAUNCHED();
+  b.last_kernel = AFEM_KERNEL_ELAST3_ITEM;
 }
 
 void assemble_elasticity_tri(Bsr& b, double lambda, double mu2)
@@ -2047,6 +2054,7 @@ void assemble_elasticity_tri(Bsr& b, double lambda, double mu2)
     hipLaunchKernelGGL(k_assemble_elast_tri<false>, grid, blk, 0, ctx.stream, AFEM_EL_ARGS);
 #undef AFEM_EL_ARGS
   AFEM_LAUNCHED();
+  b.last_kernel = AFEM_KERNEL_ELAST2;
 }
 
 }  // namespace afem

@@ -379,7 +379,18 @@ int afem_bsr_assemble_poisson_p1(afem_bsr* b, double coef, double f, double* rhs
   NOT_NULL(b);
   AFEM_REQUIRE(b->has_sparsity, AFEM_ERR_STATE, "assembleBilinear called before computeSparsity");
   b->mesh->ctx->set_device();
-  assemble_scalar(*b, coef, f, rhs);
+  assemble_scalar(*b, coef, f, rhs, 1);
+  API_END
+}
+
+int afem_bsr_assemble_poisson_p1_ex(afem_bsr* b, double coef, double f, double* rhs, int rhs_mode)
+{
+  API_BEGIN
+  NOT_NULL(b);
+  AFEM_REQUIRE(b->has_sparsity, AFEM_ERR_STATE, "assembleBilinear called before computeSparsity");
+  AFEM_REQUIRE(rhs_mode == AFEM_RHS_ADD || rhs_mode == AFEM_RHS_SET, AFEM_ERR_ARG, "unknown rhs_mode");
+  b->mesh->ctx->set_device();
+  assemble_scalar(*b, coef, f, rhs, rhs_mode == AFEM_RHS_ADD ? 1 : 0);
   API_END
 }
 
@@ -390,14 +401,14 @@ int afem_bsr_assemble_elasticity_p1(afem_bsr* b, double lambda, double mu2)
   AFEM_REQUIRE(b->has_sparsity, AFEM_ERR_STATE, "assembleBilinear called before computeSparsity");
   b->mesh->ctx->set_device();
   if (b->mesh->nv == 4)
-    assemble_elasticity_tet(*b, lambda, mu2, 0.0, nullptr, nullptr);
+    assemble_elasticity_tet(*b, lambda, mu2, 0.0, nullptr, nullptr, 1);
   else
     assemble_elasticity_tri(*b, lambda, mu2);
   API_END
 }
 
 int afem_bsr_assemble_elasticity_p1_ex(afem_bsr* b, double lambda, double mu2, double mass_coef, const double* body_force,
-                                       double* rhs)
+                                       double* rhs, int rhs_mode)
 {
   API_BEGIN
   NOT_NULL(b);
@@ -405,8 +416,9 @@ int afem_bsr_assemble_elasticity_p1_ex(afem_bsr* b, double lambda, double mu2, d
   AFEM_REQUIRE(b->mesh->nv == 4 && b->nb_dof == 3, AFEM_ERR_NOT_IMPL,
                "the mass / body-force form is implemented for NB_DOF = 3 on tetrahedra");
   AFEM_REQUIRE(!body_force || rhs, AFEM_ERR_ARG, "body_force given without an rhs array");
+  AFEM_REQUIRE(rhs_mode == AFEM_RHS_ADD || rhs_mode == AFEM_RHS_SET, AFEM_ERR_ARG, "unknown rhs_mode");
   b->mesh->ctx->set_device();
-  assemble_elasticity_tet(*b, lambda, mu2, mass_coef, body_force, rhs);
+  assemble_elasticity_tet(*b, lambda, mu2, mass_coef, body_force, rhs, rhs_mode == AFEM_RHS_ADD ? 1 : 0);
   API_END
 }
 
@@ -470,6 +482,7 @@ int afem_bsr_get_stats(afem_bsr* b, afem_bsr_stats* st)
   st->n_slices = b->s.n_slices;
   st->brick_order = b->s.brick_order ? 1 : 0;
   st->uniform_slices = (int32_t)b->s.n_uni;
+  st->last_kernel = b->last_kernel;
   API_END
 }
 
@@ -543,6 +556,9 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
   const int k = b->nb_dof;
   AFEM_REQUIRE(ls->n_rows == b->s.n_rows * k, AFEM_ERR_ARG,
                "BSRFormat(toLinearSystem): linear system size differs from the matrix rows");
+  AFEM_REQUIRE(ls->n_cols >= b->mesh->n_nodes * k, AFEM_ERR_ARG,
+               "BSRFormat(toLinearSystem): the linear system's column space (n_cols_local) is smaller than the "
+               "matrix columns (owned + ghost nodes x NB_DOF)");
   b->mesh->ctx->set_device();
   if (k == 1) {
     ls->csr_rows = b->s.row_ptr.p;
@@ -557,6 +573,7 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
     ls->csr_vals = b->order_per_block ? b->csr_vals.p : b->values.p;
   }
   ls->has_csr = true;
+  ls->csr_from_coo = false;
   ls->csr_n = b->s.n_rows * k;
   ls->csr_nnz = b->s.nnz * k * k;
   API_END
@@ -622,8 +639,8 @@ int afem_ls_set_solver_options(afem_ls* ls, const afem_solver_opts* o)
   API_BEGIN
   NOT_NULL(ls);
   NOT_NULL(o);
-  AFEM_REQUIRE(o->method == AFEM_SOLVER_AUTO || o->method == AFEM_SOLVER_PCG, AFEM_ERR_NOT_IMPL,
-               "unknown solver method");
+  AFEM_REQUIRE(o->method == AFEM_SOLVER_AUTO || o->method == AFEM_SOLVER_PCG || o->method == AFEM_SOLVER_DIRECT,
+               AFEM_ERR_NOT_IMPL, "unknown solver method");
   AFEM_REQUIRE(o->max_iter >= 0 && o->rtol >= 0 && o->atol >= 0, AFEM_ERR_ARG, "bad solver options");
   ls->opts = *o;
   API_END
@@ -638,7 +655,11 @@ int afem_ls_get_solver_options(afem_ls* ls, afem_solver_opts* o)
   API_END
 }
 
-static bool ls_uses_device_view(afem_ls* ls) { return ls->has_csr && ls->own_vals.p != ls->csr_vals; }
+// With a CSR view (from the BSR, setCSRValues on host or device memory) the
+// point updates go into it, as HypreDoFLinearSystemImpl::matrixAddValue does
+// (femutils/HypreDoFLinearSystem.cc:148-156); a CSR rebuilt from the host COO
+// maps is a derived copy, so further adds go to the maps.
+static bool ls_uses_device_view(afem_ls* ls) { return ls->has_csr && !ls->csr_from_coo; }
 
 int afem_ls_matrix_add_value(afem_ls* ls, int32_t row, int32_t col, double v)
 {
@@ -653,6 +674,7 @@ int afem_ls_matrix_add_value(afem_ls* ls, int32_t row, int32_t col, double v)
   else {
     if (v == 0.0) return AFEM_OK;  // femutils/AlephDoFLinearSystem.cc:198-199
     ls->has_csr = false;           // rebuilt from the maps at solve
+    ls->csr_from_coo = false;
     ls->add_map[{ row, col }] += v;
   }
   API_END
@@ -670,6 +692,7 @@ int afem_ls_matrix_set_value(afem_ls* ls, int32_t row, int32_t col, double v)
   }
   else {
     ls->has_csr = false;
+    ls->csr_from_coo = false;
     ls->set_map[{ row, col }] = v;
   }
   API_END
@@ -723,6 +746,18 @@ int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows
   r64[nb_row] = nb_nz;
   for (int32_t i = 0; i < nb_row; ++i)
     AFEM_REQUIRE(r64[i] <= r64[i + 1], AFEM_ERR_ARG, "setCSRValues: rows are not non-decreasing");
+  AFEM_REQUIRE(nb_row == 0 || r64[0] == 0, AFEM_ERR_ARG, "setCSRValues: rows[0] must be 0");
+  if (mem == AFEM_MEM_HOST) {
+    for (int32_t t = 0; t < nb_nz; ++t)
+      AFEM_REQUIRE(columns[t] >= 0 && columns[t] < ls->n_cols, AFEM_ERR_ARG,
+                   "setCSRValues: column index outside the linear system's column space");
+  }
+  else {
+    int32_t lo = 0, hi = 0;
+    device_minmax_i32(ctx, columns, nb_nz, &lo, &hi);
+    AFEM_REQUIRE(nb_nz == 0 || (lo >= 0 && hi < ls->n_cols), AFEM_ERR_ARG,
+                 "setCSRValues: column index outside the linear system's column space");
+  }
   ls->own_rows.alloc(nb_row + 1);
   AFEM_HIP(hipMemcpyAsync(ls->own_rows.p, r64.data(), ls->own_rows.bytes(), hipMemcpyHostToDevice, ctx.stream));
   if (mem == AFEM_MEM_DEVICE) {
@@ -745,6 +780,7 @@ int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows
   ls->csr_n = nb_row;
   ls->csr_nnz = nb_nz;
   ls->has_csr = true;
+  ls->csr_from_coo = false;
   if (mem == AFEM_MEM_HOST) {
     // host view: values now live on the device copy; keep the COO maps empty
     ls->add_map.clear();
@@ -815,6 +851,27 @@ int afem_ls_dirichlet_row_elimination(afem_ls* ls, const int32_t* dofs, int64_t 
   API_END
 }
 
+int afem_apply_neumann(afem_mesh* mesh, int nb_dof, int mode, const double value[3], int64_t n_faces,
+                       const int32_t* face_nodes, const int32_t* face_cells, int mem, double* rhs)
+{
+  API_BEGIN
+  NOT_NULL(mesh);
+  NOT_NULL(value);
+  AFEM_REQUIRE(mode == AFEM_NEUMANN_VALUE || mode == AFEM_NEUMANN_NORMAL || mode == AFEM_NEUMANN_TRACTION, AFEM_ERR_ARG,
+               "applyNeumannToRhs: unknown mode");
+  AFEM_REQUIRE(nb_dof >= 1 && nb_dof <= 3, AFEM_ERR_ARG, "applyNeumannToRhs: NB_DOF must be 1, 2 or 3");
+  AFEM_REQUIRE(mode == AFEM_NEUMANN_TRACTION || nb_dof == 1, AFEM_ERR_ARG,
+               "applyNeumannToRhs: the scalar modes need NB_DOF = 1 (vector data: AFEM_NEUMANN_TRACTION)");
+  AFEM_REQUIRE(n_faces >= 0, AFEM_ERR_ARG, "negative face count");
+  if (n_faces > 0) {
+    NOT_NULL(face_nodes);
+    NOT_NULL(rhs);
+  }
+  mesh->ctx->set_device();
+  apply_neumann(*mesh, nb_dof, mode, value, n_faces, face_nodes, face_cells, mem, rhs);
+  API_END
+}
+
 int afem_ls_apply_boundary_conditions(afem_ls* ls)
 {
   API_BEGIN
@@ -832,6 +889,7 @@ int afem_ls_clear_values(afem_ls* ls)
   Ctx& ctx = *ls->ctx;
   ctx.set_device();
   ls->has_csr = false;
+  ls->csr_from_coo = false;
   ls->csr_rows = nullptr;
   ls->csr_cols = nullptr;
   ls->csr_vals = nullptr;

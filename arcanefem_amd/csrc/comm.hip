@@ -117,16 +117,28 @@ void halo_exchange(Halo& h, Ctx& ctx, double* x)
                        h.send_buf.p);
     AFEM_LAUNCHED();
   }
+  // the group is always closed, even after a failed send/recv: an open group
+  // would swallow every later collective on the communicator (the CG
+  // all-reduces) and hang; the first error is reported after ncclGroupEnd
   AFEM_NCCL(ncclGroupStart());
-  for (size_t i = 0; i < h.nbr.size(); ++i) {
-    if (h.send_cnt[i])
-      AFEM_NCCL(ncclSend(h.send_buf.p + h.send_off[i], (size_t)h.send_cnt[i], ncclDouble, h.nbr[i], h.comm->comm,
-                         ctx.stream));
-    if (h.recv_cnt[i])
-      AFEM_NCCL(ncclRecv(h.recv_buf.p + h.recv_off[i], (size_t)h.recv_cnt[i], ncclDouble, h.nbr[i], h.comm->comm,
-                         ctx.stream));
+  ncclResult_t first = ncclSuccess;
+  const char* what = "";
+  for (size_t i = 0; i < h.nbr.size() && first == ncclSuccess; ++i) {
+    if (h.send_cnt[i]) {
+      first = ncclSend(h.send_buf.p + h.send_off[i], (size_t)h.send_cnt[i], ncclDouble, h.nbr[i], h.comm->comm,
+                       ctx.stream);
+      what = "ncclSend";
+    }
+    if (first == ncclSuccess && h.recv_cnt[i]) {
+      first = ncclRecv(h.recv_buf.p + h.recv_off[i], (size_t)h.recv_cnt[i], ncclDouble, h.nbr[i], h.comm->comm,
+                       ctx.stream);
+      what = "ncclRecv";
+    }
   }
-  AFEM_NCCL(ncclGroupEnd());
+  const ncclResult_t end = ncclGroupEnd();
+  if (first != ncclSuccess)
+    throw Error(AFEM_ERR_COMM, std::string("halo exchange: ") + what + " failed: " + ncclGetErrorString(first));
+  if (end != ncclSuccess) throw Error(AFEM_ERR_COMM, std::string("ncclGroupEnd failed: ") + ncclGetErrorString(end));
   if (h.n_recv) {
     hipLaunchKernelGGL(k_scatter, dim3(grid_for(h.n_recv, 256)), dim3(256), 0, ctx.stream, h.n_recv, h.recv_ids.p,
                        h.recv_buf.p, x);

@@ -16,9 +16,6 @@ namespace afem {
 namespace {
 
 constexpr int kThreads = 256;
-#ifndef AFEM_SPMV_NT
-#define AFEM_SPMV_NT 0
-#endif
 inline unsigned grid_for(int64_t n, int threads) { return (unsigned)((n + threads - 1) / threads); }
 constexpr uint8_t kElimRow = 1, kElimRowCol = 2;
 
@@ -44,9 +41,15 @@ __global__ void k_set_list(int64_t n, const int32_t* __restrict__ ids, int kind,
   }
 }
 
-// Row+column elimination, phase 1: rhs_j -= A[j,i] * g_i for every eliminated
-// column i != j of a non-eliminated row j, and A[j,i] = 0 (Aleph _fillMatrix,
-// femutils/AlephDoFLinearSystem.cc:539-565).
+// Row+column elimination, phase 1 (Aleph _fillMatrix,
+// femutils/AlephDoFLinearSystem.cc:539-565): for every row+column eliminated
+// DoF i and every owned column j != i of row i, rhs_j -= A[i,j] * g_i (the
+// eliminated ROW's entry), and the column entries A[j,i] of the other rows
+// are dropped.  Gathered per row j (no atomics, fixed summation order): the
+// eliminated rows coupled to j are the RC-eliminated columns of row j (the
+// P1 structure is symmetric), A[i,j] is looked up in row i.  Eliminated rows
+// are skipped (their rhs is overwritten by g in phase 2) and not modified
+// here, so the lookups read final values.
 __global__ void k_elim_columns(int64_t n_rows, const int64_t* __restrict__ rows, const int32_t* __restrict__ cols,
                                double* __restrict__ vals, const uint8_t* __restrict__ elim_info,
                                const double* __restrict__ elim_value, double* __restrict__ rhs)
@@ -58,7 +61,13 @@ __global__ void k_elim_columns(int64_t n_rows, const int64_t* __restrict__ rows,
   for (int64_t k = rows[j]; k < rows[j + 1]; ++k) {
     int32_t i = cols[k];
     if (i != (int32_t)j && i < n_rows && elim_info[i] == kElimRowCol) {
-      acc += vals[k] * elim_value[i];
+      double a_ij = 0.0;
+      for (int64_t t = rows[i]; t < rows[i + 1]; ++t)
+        if (cols[t] == (int32_t)j) {
+          a_ij = vals[t];
+          break;
+        }
+      acc += a_ij * elim_value[i];
       vals[k] = 0.0;
     }
   }
@@ -196,20 +205,9 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream4(int64_t n_rows, int64
     int c[4];
     double v[4];
     if (q + 4 <= nnz) {
-#if AFEM_SPMV_NT  // diagnostic: streaming (non-temporal) column / value loads
-      typedef int nt_i4 __attribute__((ext_vector_type(4)));
-      typedef double nt_d2 __attribute__((ext_vector_type(2)));
-      const nt_i4 ci4 = __builtin_nontemporal_load(reinterpret_cast<const nt_i4*>(cols + q));
-      const nt_d2 va = __builtin_nontemporal_load(reinterpret_cast<const nt_d2*>(vals + q));
-      const nt_d2 vb = __builtin_nontemporal_load(reinterpret_cast<const nt_d2*>(vals + q + 2));
-      const int4 c4 = make_int4(ci4.x, ci4.y, ci4.z, ci4.w);
-      const double2 v01 = make_double2(va.x, va.y);
-      const double2 v23 = make_double2(vb.x, vb.y);
-#else
       const int4 c4 = *reinterpret_cast<const int4*>(cols + q);
       const double2 v01 = *reinterpret_cast<const double2*>(vals + q);
       const double2 v23 = *reinterpret_cast<const double2*>(vals + q + 2);
-#endif
       c[0] = c4.x;
       c[1] = c4.y;
       c[2] = c4.z;
@@ -457,6 +455,122 @@ __global__ __launch_bounds__(kThreads) void k_dot(int64_t n, const double* __res
   if (threadIdx.x == 0) partial[blockIdx.x] = bs;
 }
 
+// ---------------------------------------------------------------- direct solver
+// The direct branch of SequentialDoFLinearSystemImpl::solve (N < 500,
+// femutils/DoFLinearSystem.cc:127-136; Arcane MatVec::DirectSolver is external,
+// so its pivoting is unpinned): dense Gaussian elimination with partial
+// pivoting on the augmented n x (n+1) matrix [A | b], row-major in HBM, by
+// one 1024-lane workgroup (n <= 4096: at most 128 MiB and a few ms), then
+// column-oriented back substitution.  Ghost columns (>= n) are dropped: on
+// one rank their values are not unknowns of this system.
+constexpr int kDirectThreads = 1024;
+
+__global__ void k_csr_to_dense(int64_t n, const int64_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                               const double* __restrict__ vals, const double* __restrict__ b, double* __restrict__ a)
+{
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  double* ar = a + r * (n + 1);
+  for (int64_t j = 0; j <= n; ++j) ar[j] = 0.0;
+  for (int64_t k = rows[r]; k < rows[r + 1]; ++k)
+    if (cols[k] < n) ar[cols[k]] += vals[k];
+  ar[n] = b[r];
+}
+
+__global__ __launch_bounds__(kDirectThreads) void k_dense_gauss(int n, double* __restrict__ a, double* __restrict__ x,
+                                                                int* __restrict__ singular)
+{
+  __shared__ double sv[kDirectThreads / 64];
+  __shared__ int si[kDirectThreads / 64];
+  __shared__ int piv;
+  const int ld = n + 1, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) *singular = 0;
+  for (int k = 0; k < n; ++k) {
+    // pivot: argmax_i>=k |a_ik| (lowest row index on ties)
+    double bv = -1.0;
+    int bi = k;
+    for (int i = k + t; i < n; i += kDirectThreads) {
+      const double v = fabs(a[(int64_t)i * ld + k]);
+      if (v > bv) {
+        bv = v;
+        bi = i;
+      }
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+      const double ov = __shfl_xor(bv, d, 64);
+      const int oi = __shfl_xor(bi, d, 64);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      sv[w] = bv;
+      si[w] = bi;
+    }
+    __syncthreads();
+    if (t == 0) {
+      double v = sv[0];
+      int i0 = si[0];
+      for (int q = 1; q < kDirectThreads / 64; ++q)
+        if (sv[q] > v || (sv[q] == v && si[q] < i0)) {
+          v = sv[q];
+          i0 = si[q];
+        }
+      piv = i0;
+      if (!(v > 0.0)) *singular = 1;
+    }
+    __syncthreads();
+    const int p = piv;
+    if (p != k)
+      for (int j = k + t; j <= n; j += kDirectThreads) {
+        const double tmp = a[(int64_t)k * ld + j];
+        a[(int64_t)k * ld + j] = a[(int64_t)p * ld + j];
+        a[(int64_t)p * ld + j] = tmp;
+      }
+    __syncthreads();
+    const double inv = 1.0 / a[(int64_t)k * ld + k];
+    const int wdt = n - k;  // columns k+1..n
+    const int64_t tot = (int64_t)(n - k - 1) * wdt;
+    for (int64_t e = t; e < tot; e += kDirectThreads) {
+      const int i = k + 1 + (int)(e / wdt), j = k + 1 + (int)(e % wdt);
+      const double l = a[(int64_t)i * ld + k] * inv;
+      a[(int64_t)i * ld + j] -= l * a[(int64_t)k * ld + j];
+    }
+    __syncthreads();
+  }
+  // back substitution, column oriented: x_j = c_j / u_jj, c_i -= u_ij x_j (i < j)
+  for (int j = n - 1; j >= 0; --j) {
+    const double xj = a[(int64_t)j * ld + n] / a[(int64_t)j * ld + j];
+    for (int i = t; i < j; i += kDirectThreads) a[(int64_t)i * ld + n] -= a[(int64_t)i * ld + j] * xj;
+    if (t == 0) x[j] = xj;
+    __syncthreads();
+  }
+}
+
+// r = b - A x (owned rows), partial sums of r.r and b.b
+__global__ __launch_bounds__(256) void k_residual(int64_t n, const int64_t* __restrict__ rows,
+                                                  const int32_t* __restrict__ cols, const double* __restrict__ vals,
+                                                  const double* __restrict__ x, const double* __restrict__ b,
+                                                  double* __restrict__ partial)
+{
+  double rr = 0.0, bb = 0.0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int64_t k = rows[r]; k < rows[r + 1]; ++k)
+      if (cols[k] < n) s += vals[k] * x[cols[k]];
+    const double ri = b[r] - s;
+    rr += ri * ri;
+    bb += b[r] * b[r];
+  }
+  const double a = block_sum(rr);
+  const double c = block_sum(bb);
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = a;
+    partial[2 * blockIdx.x + 1] = c;
+  }
+}
+
 // ---------------------------------------------------------------- helpers
 struct SpmvPlan {
   int rpb = 0;          // rows per block (0: row kernel, -1: vector CSR)
@@ -638,6 +752,7 @@ void ls_build_from_host_coo(LinearSystem& ls)
   }
   ctx.sync();
   ls.has_csr = true;
+  ls.csr_from_coo = true;
   ls.csr_n = ls.n_rows;
   ls.csr_nnz = (int64_t)cols.size();
   ls.csr_rows = ls.own_rows.p;
@@ -673,6 +788,50 @@ void ls_spmv(LinearSystem& ls, const double* x, double* y)
   launch_spmv(ctx, pl, ls.n_rows, ls.csr_rows, ls.csr_cols, ls.csr_vals, x, y, nullptr, ls.csr_nnz);
 }
 
+namespace {
+void ls_solve_direct(LinearSystem& ls, afem_solve_stats* st)
+{
+  Ctx& ctx = *ls.ctx;
+  const int64_t n = ls.n_rows;
+  AFEM_REQUIRE(n <= 4096, AFEM_ERR_LIMIT, "direct solver: more than 4096 rows (use the PCG)");
+  ls.dense.alloc((size_t)n * (n + 1));
+  if (ls.partial.n < 2 * 64) ls.partial.alloc(2 * 64);
+  DevBuf<int> sing;
+  sing.alloc(1);
+  AFEM_HIP(hipEventRecord(ctx.ev0, ctx.stream));
+  hipLaunchKernelGGL(k_csr_to_dense, dim3(grid_for(n, 256)), dim3(256), 0, ctx.stream, n, ls.csr_rows, ls.csr_cols,
+                     ls.csr_vals, ls.rhs.p, ls.dense.p);
+  AFEM_LAUNCHED();
+  hipLaunchKernelGGL(k_dense_gauss, dim3(1), dim3(kDirectThreads), 0, ctx.stream, (int)n, ls.dense.p, ls.sol.p, sing.p);
+  AFEM_LAUNCHED();
+  AFEM_HIP(hipEventRecord(ctx.ev1, ctx.stream));
+  hipLaunchKernelGGL(k_residual, dim3(64), dim3(256), 0, ctx.stream, n, ls.csr_rows, ls.csr_cols, ls.csr_vals,
+                     ls.sol.p, ls.rhs.p, ls.partial.p);
+  AFEM_LAUNCHED();
+  double h[128];
+  int hs = 0;
+  AFEM_HIP(hipMemcpyAsync(h, ls.partial.p, sizeof(h), hipMemcpyDeviceToHost, ctx.stream));
+  AFEM_HIP(hipMemcpyAsync(&hs, sing.p, sizeof(hs), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  ls.dense.reset();
+  AFEM_REQUIRE(!hs, AFEM_ERR_ARG, "direct solver: the matrix is singular");
+  double rr = 0.0, bb = 0.0;
+  for (int i = 0; i < 64; ++i) {
+    rr += h[2 * i];
+    bb += h[2 * i + 1];
+  }
+  float ms = 0.f;
+  AFEM_HIP(hipEventElapsedTime(&ms, ctx.ev0, ctx.ev1));
+  if (st) {
+    st->iterations = 0;
+    st->converged = 1;
+    st->rel_residual = bb > 0 ? std::sqrt(rr / bb) : 0.0;
+    st->residual_norm = std::sqrt(rr);
+    st->solve_ms = ms;
+  }
+}
+}  // namespace
+
 void ls_solve(LinearSystem& ls, afem_solve_stats* st)
 {
   Ctx& ctx = *ls.ctx;
@@ -682,6 +841,16 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   require_csr(ls);
   AFEM_REQUIRE(ls.csr_n == ls.n_rows, AFEM_ERR_ARG, "CSR view row count differs from the linear system size");
   ls_apply_bcs(ls);
+  const bool multi = ls.halo && ls.halo->comm && comm_nranks(ls.halo->comm) > 1;
+  int method = ls.opts.method;
+  if (method == AFEM_SOLVER_AUTO)  // femutils/DoFLinearSystem.cc:127-136: direct below 500 rows
+    method = (!multi && ls.n_rows < 500 && ls.opts.fixed_iterations <= 0) ? AFEM_SOLVER_DIRECT : AFEM_SOLVER_PCG;
+  if (method == AFEM_SOLVER_DIRECT) {
+    AFEM_REQUIRE(!multi, AFEM_ERR_NOT_IMPL, "the direct solver runs on one rank (the reference's Sequential "
+                                            "solver refuses parallel runs, femutils/DoFLinearSystem.cc:562-564)");
+    ls_solve_direct(ls, st);
+    return;
+  }
 
   const int64_t n = ls.n_rows;
   if (ls.r.n != (size_t)n) {

@@ -3,6 +3,8 @@
 // node->cell offsets, incidence-slice offsets), not by the timed assembly.
 #include "afem_internal.hpp"
 
+#include <algorithm>
+#include <climits>
 #include <cstdio>
 
 namespace afem {
@@ -120,7 +122,43 @@ void scan_impl(Ctx& ctx, const In* in, int64_t* out, int64_t n)
   ctx.sync();
 }
 
+__global__ void k_minmax_i32(const int32_t* __restrict__ a, int64_t n, int* __restrict__ out)
+{
+  int lo = INT32_MAX, hi = INT32_MIN;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    lo = min(lo, a[i]);
+    hi = max(hi, a[i]);
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    lo = min(lo, __shfl_xor(lo, d, 64));
+    hi = max(hi, __shfl_xor(hi, d, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(out, lo);
+    atomicMax(out + 1, hi);
+  }
+}
+
 }  // namespace
+
+void device_minmax_i32(Ctx& ctx, const int32_t* a, int64_t n, int32_t* lo, int32_t* hi)
+{
+  *lo = 0;
+  *hi = 0;
+  if (n <= 0) return;
+  DevBuf<int> d;
+  d.alloc(2);
+  const int init[2] = { INT32_MAX, INT32_MIN };
+  AFEM_HIP(hipMemcpyAsync(d.p, init, sizeof(init), hipMemcpyHostToDevice, ctx.stream));
+  const unsigned nb = (unsigned)std::min<int64_t>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(k_minmax_i32, dim3(nb), dim3(256), 0, ctx.stream, a, n, d.p);
+  AFEM_LAUNCHED();
+  int h[2];
+  AFEM_HIP(hipMemcpyAsync(h, d.p, sizeof(h), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  *lo = h[0];
+  *hi = h[1];
+}
 
 void exclusive_scan_i64(Ctx& ctx, const int64_t* in, int64_t* out, int64_t n, DevBuf<int64_t>*)
 {

@@ -88,7 +88,7 @@ class Elastodynamics3D:
         ctx, ls = self.ctx, self.ls
         rhs = ls.rhsVariable()
         # LHS c0 M + K and body-force RHS, re-assembled on the fixed structure
-        self.K.assembleElasticityP1Ex(self.lam, self.mu2, self.c0, self.f, rhs)
+        self.K.assembleElasticityP1Ex(self.lam, self.mu2, self.c0, self.f, rhs, rhs_mode="set")
         # RHS += M (c0 U + c3 V + c4 A)
         call("afem_vec_lincomb", ctx.h, self.n, self.c0, ctypes.c_void_p(self.U), self.c3, ctypes.c_void_p(self.V),
              self.c4, ctypes.c_void_p(self.A), ctypes.c_void_p(self.W))

@@ -37,6 +37,9 @@ class GmshMesh:
     coords: np.ndarray           # float64 [n_nodes, 3]
     cells: np.ndarray            # int32 [n_cells, nv]  0-based node indices
     groups: dict                 # name -> (dim, int32 sorted unique node indices)
+    face_groups: dict = dataclasses.field(default_factory=dict)
+    # name -> int32 [n_faces, dim] node indices of the group's boundary faces
+    # (edges in 2D, triangles in 3D), as stored in the file
 
     @property
     def n_nodes(self) -> int:
@@ -45,6 +48,16 @@ class GmshMesh:
     @property
     def n_cells(self) -> int:
         return int(self.cells.shape[0])
+
+    def group_faces(self, name: str) -> np.ndarray:
+        if name not in self.face_groups:
+            raise KeyError(f"no face group named {name!r}; have {sorted(self.face_groups)}")
+        return self.face_groups[name]
+
+    def face_cells(self, faces: np.ndarray) -> np.ndarray:
+        """For each boundary face, the cell it bounds (Arcane's face->cell
+        connectivity, which the reference uses to orient boundary normals)."""
+        return boundary_face_cells(self.cells, faces)
 
     def group_nodes(self, name: str) -> np.ndarray:
         if name not in self.groups:
@@ -214,7 +227,32 @@ def read_gmsh(path: str) -> GmshMesh:
             groups_acc.setdefault(name, (edim, []))[1].append(tag_to_idx[conn].ravel())
     groups = {name: (gd, np.unique(np.concatenate(lst)).astype(np.int32))
               for name, (gd, lst) in groups_acc.items()}
-    return GmshMesh(dim=mesh_dim, node_tags=node_tags, coords=coords, cells=cells, groups=groups)
+    faces_acc: dict = {}
+    for edim, etag, etype, conn in elem_blocks:
+        if edim != mesh_dim - 1 or _NODES_PER_TYPE[etype] != mesh_dim:
+            continue
+        for ptag in entity_phys.get((edim, etag), []):
+            name = phys_names.get((edim, ptag))
+            if name is not None:
+                faces_acc.setdefault(name, []).append(tag_to_idx[conn])
+    face_groups = {name: np.concatenate(lst).astype(np.int32) for name, lst in faces_acc.items()}
+    return GmshMesh(dim=mesh_dim, node_tags=node_tags, coords=coords, cells=cells, groups=groups,
+                    face_groups=face_groups)
+
+
+def boundary_face_cells(cells: np.ndarray, faces: np.ndarray) -> np.ndarray:
+    """Cell owning each face (the faces of a P1 simplex are its nv choose dim
+    node subsets); -1 when no cell has the face."""
+    cells = np.asarray(cells)
+    nv = cells.shape[1]
+    dim = nv - 1
+    lookup = {}
+    for a in range(nv):
+        sub = np.sort(np.delete(cells, a, axis=1), axis=1)
+        for c, key in enumerate(map(tuple, sub)):
+            lookup.setdefault(key, c)
+    fs = np.sort(np.asarray(faces).reshape(-1, dim), axis=1)
+    return np.array([lookup.get(tuple(f), -1) for f in fs], dtype=np.int32)
 
 
 def read_node_result_file(path: str) -> dict:

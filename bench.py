@@ -67,11 +67,11 @@ def elasticity_c3(ctx, af, n, reps=10, warmup=2):
     rhs = ctx.malloc(8 * 3 * mesh.n_own_nodes)
     f = (0.0, 0.0, -1.0)
     for _ in range(warmup):
-        bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs)
+        bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs, rhs_mode="set")
     ctx.synchronize()
     for i in range(reps):
         ctx.event_record(200 + 2 * i)
-        bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs)
+        bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs, rhs_mode="set")
         ctx.event_record(201 + 2 * i)
     ctx.synchronize()
     kms = float(np.mean([ctx.event_elapsed(200 + 2 * i, 201 + 2 * i) for i in range(reps)]))
@@ -209,7 +209,7 @@ def main():
     def step(ev=None):
         if ev is not None:
             ctx.event_record(ev)
-        bsr.assemblePoissonP1(1.0, 5.5, rhs)
+        bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set")  # rhs.fill(0) + source, fused
         if ev is not None:
             ctx.event_record(ev + 1)
         ls.applyDirichletViaPenaltyDevice(dbottom, bottom.size, 0.5, 1.0e30)

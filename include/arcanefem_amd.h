@@ -148,10 +148,16 @@ int afem_bsr_compute_sparsity(afem_bsr* bsr);
 /* BSRFormat::assembleBilinear with the P1 Laplacian element of
  * modules/poisson/FemModule.h:139-186, scaled by `coef`, fused with
  * applyConstantSourceToRhs (femutils/ArcaneFemFunctionsGpu.h:401-429) when
- * rhs != NULL: rhs[dof] = sum f*|K|/nv over cells of own node dof (rhs is
- * overwritten, not accumulated; device pointer of length n_own_nodes).
- * Every matrix value of the structure is written (no separate zeroing). */
+ * rhs != NULL: rhs[dof] += sum f*|K|/nv over the cells of own node dof
+ * (accumulated, as the reference's doAtomic<Add> at :419-428; device pointer
+ * of length n_own_nodes).  Every matrix value of the structure is written (no
+ * separate zeroing). */
 int afem_bsr_assemble_poisson_p1(afem_bsr* bsr, double coef, double f, double* rhs);
+/* RHS modes of the fused source term */
+#define AFEM_RHS_ADD 0 /* rhs += source (applyConstantSourceToRhs) */
+#define AFEM_RHS_SET 1 /* rhs  = source: the module's rhs_values.fill(0.0) +
+                          applyConstantSourceToRhs (modules/poisson/FemModule.cc:163-169) in one pass */
+int afem_bsr_assemble_poisson_p1_ex(afem_bsr* bsr, double coef, double f, double* rhs, int rhs_mode);
 /* Block-2 P1 elasticity on triangles (modules/elasticity/FemModule.h:112-140),
  * mu2 = 2*mu, lambda as in modules/elasticity/FemModule.cc:130-134. */
 int afem_bsr_assemble_elasticity_p1(afem_bsr* bsr, double lambda, double mu2);
@@ -161,10 +167,11 @@ int afem_bsr_assemble_elasticity_p1(afem_bsr* bsr, double lambda, double mu2);
  * modules/elastodynamics/FemModule.cc:259,1285-1340) and, if body_force
  * (3 doubles, host) is given, the vectorial constant source
  * rhs[3n+i] = f_i |K| / 4 on owned nodes (femutils/ArcaneFemFunctionsGpu.h:514-586;
- * rhs: device, 3*n_own). afem_bsr_assemble_elasticity_p1 on a tetrahedral
+ * rhs: device, 3*n_own; rhs_mode AFEM_RHS_ADD / AFEM_RHS_SET as for the Poisson
+ * source). afem_bsr_assemble_elasticity_p1 on a tetrahedral
  * block-3 matrix is this call with mass_coef = 0 and no body force. */
 int afem_bsr_assemble_elasticity_p1_ex(afem_bsr* bsr, double lambda, double mu2, double mass_coef,
-                                       const double* body_force, double* rhs);
+                                       const double* body_force, double* rhs, int rhs_mode);
 int afem_bsr_reset_values(afem_bsr* bsr);                       /* resetMatrixValues */
 int afem_bsr_set_value(afem_bsr* bsr, int32_t row, int32_t col, double v); /* BSRMatrix::setValue */
 int afem_bsr_get_value(afem_bsr* bsr, int32_t row, int32_t col, double* v); /* BSRMatrix::getValue */
@@ -179,9 +186,21 @@ typedef struct afem_bsr_stats {
   int32_t max_slice_nodes;  /* max distinct nodes one slice couples to (LDS coordinate cache) */
   int32_t max_slice_width;  /* max row length within one slice */
   int64_t n_slices;         /* assembly slices (wavefronts per launch) */
-  int32_t brick_order;      /* 1: slices are 4x4x4 (3D) / 8x8 (2D) node bricks, 0: node order */
+  int32_t brick_order;      /* 1: slices are node bricks of a structured box: 4x4x4 interior bricks
+                               (8x8 in 2D) and 8x8 tiles of the boundary faces; 0: slices follow a
+                               Morton-curve order of the node coordinates (plain node order under
+                               AFEM_ORDER=node) */
   int32_t uniform_slices;   /* slices whose 64 rows share one strip topology (uniform-control assembly variant) */
+  int32_t last_kernel;      /* AFEM_KERNEL_* that ran the last assembly of this matrix */
 } afem_bsr_stats;
+#define AFEM_KERNEL_NONE 0
+#define AFEM_KERNEL_STRIP 1          /* scalar row-strip kernel (uniform + general instances) */
+#define AFEM_KERNEL_SLICE_TILE 2     /* scalar incidence-table kernel with the LDS slice tile */
+#define AFEM_KERNEL_GLOBAL 3         /* scalar global-memory kernel (no strips, rows beyond the LDS tile) */
+#define AFEM_KERNEL_ELAST3_STRIP 4   /* block-3 persistent strip kernel */
+#define AFEM_KERNEL_ELAST3_ITEM 5    /* block-3 one-wave-per-item strip kernel */
+#define AFEM_KERNEL_ELAST3_GLOBAL 6  /* block-3 global-memory kernel (no strips) */
+#define AFEM_KERNEL_ELAST2 7         /* block-2 triangle kernel */
 int afem_bsr_get_stats(afem_bsr* bsr, afem_bsr_stats* stats);
 /* Copies the scalar CSR expansion to host in the reference's CSRFormatView
  * layout (BSRMatrix::toCsr, femutils/BSRFormat.h:194-256): rows[n] without
@@ -197,8 +216,10 @@ int afem_bsr_to_linear_system(afem_bsr* bsr, afem_ls* ls);
 int afem_bsr_destroy(afem_bsr* bsr);
 
 /* ---------------------------------------------------------------- linear system */
-#define AFEM_SOLVER_AUTO 0   /* Jacobi-PCG (the reference's Auto picks a direct solver below 500 rows) */
+#define AFEM_SOLVER_AUTO 0   /* direct below 500 rows on one rank, Jacobi-PCG otherwise
+                                (SequentialDoFLinearSystemImpl::solve, femutils/DoFLinearSystem.cc:127-151) */
 #define AFEM_SOLVER_PCG 1    /* Jacobi (diagonal) preconditioned CG */
+#define AFEM_SOLVER_DIRECT 2 /* dense LU with partial pivoting on the device (one rank, n_rows <= 4096) */
 
 typedef struct afem_solver_opts {
   int32_t method;       /* AFEM_SOLVER_* */
@@ -259,16 +280,35 @@ int afem_ls_elimination_value(afem_ls* ls, double** dptr);
 int afem_ls_dirichlet_penalty(afem_ls* ls, const int32_t* dofs, int64_t n, double value, double penalty, int mem);
 /* ...ViaRowElimination (femutils/ArcaneFemFunctionsGpu.h:461-482): elimination_info = 1, value. */
 int afem_ls_dirichlet_row_elimination(afem_ls* ls, const int32_t* dofs, int64_t n, double value, int mem);
+/* Neumann / traction right-hand side on boundary faces (K15):
+ * BoundaryConditions{2D,3D}::applyNeumannToRhs (femutils/ArcaneFemFunctionsGpu.h:612-674,
+ * 703-766) and the elasticity traction term (modules/elasticity/FemModule.cc:244-273).
+ *   AFEM_NEUMANN_VALUE    rhs[k n]     += value[0] |F| / nf
+ *   AFEM_NEUMANN_NORMAL   rhs[k n]     += (value . N) |F| / nf, N the outward unit normal
+ *   AFEM_NEUMANN_TRACTION rhs[k n + i] += value[i] |F| / nf, i < nb_dof
+ * |F| = edge length (2D, nf = 2 nodes per face) or triangle area (3D, nf = 3);
+ * only owned nodes receive a share.  face_nodes[n_faces*nf] are local node ids;
+ * face_cells[n_faces] (may be NULL) the cell each face bounds: the normal is
+ * oriented away from it, which is what the reference's
+ * isSubDomainBoundaryOutside() swap achieves (without it the node order of the
+ * face defines the normal).  Arrays in `mem`; rhs: device, nb_dof*n_own_nodes.
+ * Accumulated with f64 atomics (summation order not fixed). */
+#define AFEM_NEUMANN_VALUE 0
+#define AFEM_NEUMANN_NORMAL 1
+#define AFEM_NEUMANN_TRACTION 2
+int afem_apply_neumann(afem_mesh* mesh, int nb_dof, int mode, const double value[3], int64_t n_faces,
+                       const int32_t* face_nodes, const int32_t* face_cells, int mem, double* rhs);
 /* _applyRowElimination + _applyForcedValuesToLhs (femutils/HypreDoFLinearSystem.cc:
  * 319-382) on the CSR view; afem_ls_solve calls it, it is exposed so the
  * assembly step can be timed with it. */
 int afem_ls_apply_boundary_conditions(afem_ls* ls);
 /* clearValues (femutils/HypreDoFLinearSystem.cc:180-187) */
 int afem_ls_clear_values(afem_ls* ls);
-/* solve: BCs into the CSR, then Jacobi-PCG from x0 = 0 (SequentialDoFLinearSystemImpl
- * iterative branch, femutils/DoFLinearSystem.cc:137-151).  With a communicator
- * attached the SpMV exchanges ghost values and the dot products are summed
- * over ranks (RCCL). */
+/* solve: BCs into the CSR, then (SequentialDoFLinearSystemImpl::solve,
+ * femutils/DoFLinearSystem.cc:106-164) a direct dense LU below 500 rows or the
+ * Jacobi-PCG whose initial guess lifts the constraint rows.
+ * With a communicator attached the SpMV exchanges ghost values and the dot
+ * products are summed over ranks (RCCL). */
 int afem_ls_solve(afem_ls* ls, afem_solve_stats* stats);
 /* y[0:n_rows] = A x (x of length n_cols_local, ghost part exchanged first when
  * a communicator is attached).  Device pointers. */

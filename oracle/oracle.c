@@ -603,3 +603,224 @@ int orc_pcg_jacobi(int64_t n, const int64_t* row_ptr, const int32_t* cols, const
   free(dinv);
   return it;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Neumann / traction right-hand side on boundary faces (K15).               */
+/*   mode 0 (value):    rhs[k n]   += g |F| / nf                             */
+/*                      femutils/ArcaneFemFunctionsGpu.h:636-650 (2D, length/2)*/
+/*                      and :731-743 (3D, area/3)                            */
+/*   mode 1 (normal):   rhs[k n]   += (v . N) |F| / nf, N outward unit normal */
+/*                      :652-672 (2D computeNormalFace, :145-160) and        */
+/*                      :745-766 (3D computeNormalTriangle, :172-196)        */
+/*   mode 2 (traction): rhs[k n+i] += t_i |F| / nf, i < k                    */
+/*                      modules/elasticity/FemModule.cc:244-273              */
+/* |F|: 2D edge length in the xy plane (computeLengthFace, :130-137), 3D     */
+/* triangle area |cross|/2 (computeAreaTria, :88-96).  Only owned nodes      */
+/* (node < n_own) receive a contribution (nodes_infos.isOwn).                */
+/* Orientation: the reference swaps the face's first two nodes when the face  */
+/* is not isSubDomainBoundaryOutside(), i.e. it uses the outward normal of   */
+/* the boundary face; here the outward side is the one away from the         */
+/* centroid of the face's cell face_cells[f] (node order as given when       */
+/* face_cells is NULL).                                                      */
+/* ------------------------------------------------------------------------ */
+void orc_neumann(int dim, int64_t n_own, int k, int mode, const double* v, int64_t n_faces, const int32_t* face_nodes,
+                 const int32_t* face_cells, int nv, const int32_t* cell_node, const double* coords, double* rhs)
+{
+  const int nf = dim; /* nodes per face: 2 (edge) or 3 (triangle) */
+  for (int64_t f = 0; f < n_faces; ++f) {
+    const int32_t* fn = face_nodes + (int64_t)nf * f;
+    const double* m0 = coords + 3 * (int64_t)fn[0];
+    const double* m1 = coords + 3 * (int64_t)fn[1];
+    double meas, N[3] = { 0.0, 0.0, 0.0 };
+    if (dim == 2) {
+      meas = sqrt((m1[0] - m0[0]) * (m1[0] - m0[0]) + (m1[1] - m0[1]) * (m1[1] - m0[1]));
+      N[0] = (m1[1] - m0[1]) / meas;
+      N[1] = (m0[0] - m1[0]) / meas;
+    }
+    else {
+      const double* m2 = coords + 3 * (int64_t)fn[2];
+      double e1[3] = { m1[0] - m0[0], m1[1] - m0[1], m1[2] - m0[2] };
+      double e2[3] = { m2[0] - m0[0], m2[1] - m0[1], m2[2] - m0[2] };
+      double c[3] = { e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0] };
+      double nrm = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+      meas = nrm / 2.0;
+      N[0] = c[0] / nrm;
+      N[1] = c[1] / nrm;
+      N[2] = c[2] / nrm;
+    }
+    if (mode == 1 && face_cells) {
+      /* outward: N . (face centroid - cell centroid) > 0 */
+      const int32_t* cn = cell_node + (int64_t)nv * face_cells[f];
+      double s = 0.0;
+      for (int d = 0; d < dim; ++d) {
+        double fc = 0.0, cc = 0.0;
+        for (int a = 0; a < nf; ++a)
+          fc += coords[3 * (int64_t)fn[a] + d];
+        for (int a = 0; a < nv; ++a)
+          cc += coords[3 * (int64_t)cn[a] + d];
+        s += N[d] * (fc / nf - cc / nv);
+      }
+      if (s < 0.0) {
+        N[0] = -N[0];
+        N[1] = -N[1];
+        N[2] = -N[2];
+      }
+    }
+    for (int a = 0; a < nf; ++a) {
+      const int32_t node = fn[a];
+      if (node >= n_own)
+        continue;
+      if (mode == 0)
+        rhs[(int64_t)k * node] += v[0] * meas / nf;
+      else if (mode == 1) {
+        double vn = dim == 2 ? N[0] * v[0] + N[1] * v[1] : N[0] * v[0] + N[1] * v[1] + N[2] * v[2];
+        rhs[(int64_t)k * node] += vn * meas / nf;
+      }
+      else {
+        for (int i = 0; i < k; ++i)
+          rhs[(int64_t)k * node + i] += v[i] * meas / nf;
+      }
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Row / row+column elimination with Aleph semantics:                        */
+/* femutils/AlephDoFLinearSystem.cc:501-583 (_fillMatrix).                   */
+/*   info[d] = 1 (ELIMINATE_ROW) or 2 (ELIMINATE_ROW_COLUMN), value[d] = g.   */
+/* Phase 1: for a row+column eliminated row r, every owned column c != r:     */
+/*          rhs[c] -= A[r,c] * g_r; entries of row+column eliminated columns  */
+/*          are dropped from the other rows.                                  */
+/* Phase 2: eliminated rows become identity rows with rhs = g.               */
+/* ------------------------------------------------------------------------ */
+void orc_eliminate(int64_t n_rows, const uint8_t* info, const double* value, const int64_t* row_ptr,
+                   const int32_t* cols, double* vals, double* rhs)
+{
+  for (int64_t r = 0; r < n_rows; ++r) {
+    if (info[r] != 2)
+      continue;
+    for (int64_t k = row_ptr[r]; k < row_ptr[r + 1]; ++k) {
+      int32_t c = cols[k];
+      if (c == r || c >= n_rows)
+        continue;
+      rhs[c] = rhs[c] - vals[k] * value[r];
+    }
+  }
+  for (int64_t j = 0; j < n_rows; ++j) {
+    if (info[j] != 0)
+      continue;
+    for (int64_t k = row_ptr[j]; k < row_ptr[j + 1]; ++k)
+      if (cols[k] != j && cols[k] < n_rows && info[cols[k]] == 2)
+        vals[k] = 0.0;
+  }
+  for (int64_t d = 0; d < n_rows; ++d) {
+    if (info[d] == 0)
+      continue;
+    for (int64_t k = row_ptr[d]; k < row_ptr[d + 1]; ++k)
+      vals[k] = cols[k] == d ? 1.0 : 0.0;
+    rhs[d] = value[d];
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* OpenMP variant of orc_pcg_jacobi (same iteration, same stopping rule;     */
+/* parallel loops with reductions, so the summation order of the dot          */
+/* products differs from the serial one).  The BASELINE.md §4 CPU baseline   */
+/* "Jacobi-PCG restatement with OpenMP, fixed 50 iterations" and the         */
+/* solution-parity reference at >= 1e7 DoF.                                   */
+/* ------------------------------------------------------------------------ */
+static double dot_omp(int64_t n, const double* a, const double* b)
+{
+  double s = 0.0;
+#pragma omp parallel for reduction(+ : s) schedule(static)
+  for (int64_t i = 0; i < n; ++i)
+    s += a[i] * b[i];
+  return s;
+}
+
+static void spmv_omp(int64_t n_rows, const int64_t* row_ptr, const int32_t* cols, const double* vals, const double* x,
+                     double* y)
+{
+#pragma omp parallel for schedule(static)
+  for (int64_t r = 0; r < n_rows; ++r) {
+    double s = 0.0;
+    for (int64_t k = row_ptr[r]; k < row_ptr[r + 1]; ++k)
+      s += vals[k] * x[cols[k]];
+    y[r] = s;
+  }
+}
+
+int orc_pcg_jacobi_omp(int64_t n, const int64_t* row_ptr, const int32_t* cols, const double* vals, const double* b,
+                       double* x, double rtol, double atol, int max_iter, double* res_out, double* rnorm_out)
+{
+  int fixed = max_iter < 0;
+  if (fixed)
+    max_iter = -max_iter;
+  double* r = (double*)malloc(sizeof(double) * (size_t)n);
+  double* z = (double*)malloc(sizeof(double) * (size_t)n);
+  double* p = (double*)malloc(sizeof(double) * (size_t)n);
+  double* q = (double*)malloc(sizeof(double) * (size_t)n);
+  double* dinv = (double*)malloc(sizeof(double) * (size_t)n);
+  unsigned char* constraint = (unsigned char*)malloc((size_t)n);
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {
+    double d = 0.0, off = 0.0;
+    for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k)
+      if (cols[k] == i)
+        d = vals[k];
+      else
+        off += fabs(vals[k]);
+    dinv[i] = d != 0.0 ? 1.0 / d : 0.0;
+    constraint[i] = fabs(d) > 1e10 * off;
+    x[i] = constraint[i] ? b[i] * dinv[i] : 0.0;
+  }
+  spmv_omp(n, row_ptr, cols, vals, x, q);
+  double rz0 = 0.0, rz = 0.0;
+#pragma omp parallel for reduction(+ : rz0, rz) schedule(static)
+  for (int64_t i = 0; i < n; ++i) {
+    r[i] = b[i] - q[i];
+    z[i] = r[i] * dinv[i];
+    p[i] = z[i];
+    rz += r[i] * z[i];
+    if (!constraint[i])
+      rz0 += r[i] * z[i];
+  }
+  if (rz0 == 0.0)
+    rz0 = rz;
+  free(constraint);
+  int it = 0;
+  while (it < max_iter) {
+    if (!fixed) {
+      if (rz0 == 0.0 || sqrt(fabs(rz / rz0)) <= rtol)
+        break;
+      if (atol > 0 && sqrt(dot_omp(n, r, r)) <= atol)
+        break;
+    }
+    spmv_omp(n, row_ptr, cols, vals, p, q);
+    const double alpha = rz / dot_omp(n, p, q);
+    double rz_new = 0.0;
+#pragma omp parallel for reduction(+ : rz_new) schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+      x[i] += alpha * p[i];
+      r[i] -= alpha * q[i];
+      z[i] = r[i] * dinv[i];
+      rz_new += r[i] * z[i];
+    }
+    const double beta = rz_new / rz;
+    rz = rz_new;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i)
+      p[i] = z[i] + beta * p[i];
+    ++it;
+  }
+  if (res_out)
+    *res_out = rz0 > 0 ? sqrt(fabs(rz / rz0)) : 0.0;
+  if (rnorm_out)
+    *rnorm_out = sqrt(dot_omp(n, r, r));
+  free(r);
+  free(z);
+  free(p);
+  free(q);
+  free(dinv);
+  return it;
+}

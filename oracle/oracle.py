@@ -76,6 +76,12 @@ def lib():
         L.orc_pcg_jacobi.argtypes = [ctypes.c_int64, _i64p, _i32p, _f64p, _f64p, _f64p, ctypes.c_double,
                                      ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double)]
+        L.orc_neumann.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _f64p, ctypes.c_int64,
+                                  _i32p, ctypes.c_void_p, ctypes.c_int, _i32p, _f64p, _f64p]
+        L.orc_eliminate.argtypes = [ctypes.c_int64, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS"), _f64p,
+                                    _i64p, _i32p, _f64p, _f64p]
+        L.orc_pcg_jacobi_omp.restype = ctypes.c_int
+        L.orc_pcg_jacobi_omp.argtypes = L.orc_pcg_jacobi.argtypes
         _lib = L
     return _lib
 
@@ -215,6 +221,24 @@ def blocks_to_row_order(row_ptr, vals4):
     return out
 
 
+NEUMANN_VALUE, NEUMANN_NORMAL, NEUMANN_TRACTION = 0, 1, 2
+
+
+def neumann(dim, n_own, k, mode, value, faces, face_cells, cells, coords, rhs):
+    """Adds the Neumann / traction term of the boundary faces to rhs in place
+    (oracle.c::orc_neumann)."""
+    v = np.zeros(3)
+    v[:len(np.atleast_1d(value))] = np.atleast_1d(value)
+    faces = np.ascontiguousarray(faces, dtype=np.int32)
+    fc = None if face_cells is None else np.ascontiguousarray(face_cells, dtype=np.int32)
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    coords = np.ascontiguousarray(coords, dtype=np.float64).reshape(-1, 3)
+    lib().orc_neumann(dim, n_own, k, mode, v, faces.shape[0], faces.ravel(),
+                      None if fc is None else fc.ctypes.data_as(ctypes.c_void_p), cells.shape[1], cells.ravel(),
+                      coords.ravel(), rhs)
+    return rhs
+
+
 def dirichlet_penalty(dofs, value, penalty, row_ptr, cols, vals, rhs):
     dofs = np.ascontiguousarray(dofs, dtype=np.int32)
     lib().orc_dirichlet_penalty(dofs.shape[0], dofs, value, penalty, row_ptr, cols, vals, rhs)
@@ -223,6 +247,14 @@ def dirichlet_penalty(dofs, value, penalty, row_ptr, cols, vals, rhs):
 def row_elimination(dofs, value, row_ptr, cols, vals, rhs):
     dofs = np.ascontiguousarray(dofs, dtype=np.int32)
     lib().orc_row_elimination(dofs.shape[0], dofs, value, row_ptr, cols, vals, rhs)
+
+
+def eliminate(info, value, row_ptr, cols, vals, rhs):
+    """Aleph row / row+column elimination (oracle.c::orc_eliminate); info 1 =
+    eliminateRow, 2 = eliminateRowColumn; arrays updated in place."""
+    n = row_ptr.shape[0] - 1
+    lib().orc_eliminate(n, np.ascontiguousarray(info, dtype=np.uint8), np.ascontiguousarray(value, dtype=np.float64),
+                        row_ptr, cols, vals, rhs)
 
 
 def spmv(row_ptr, cols, vals, x):
@@ -239,6 +271,18 @@ def pcg_jacobi(row_ptr, cols, vals, b, rtol=1e-12, atol=0.0, max_iter=10000, x0=
     rn = ctypes.c_double()
     it = lib().orc_pcg_jacobi(n, row_ptr, cols, vals, np.ascontiguousarray(b, dtype=np.float64), x, rtol, atol,
                               max_iter, ctypes.byref(res), ctypes.byref(rn))
+    return x, it, res.value, rn.value
+
+
+def pcg_jacobi_omp(row_ptr, cols, vals, b, rtol=1e-12, atol=0.0, max_iter=10000):
+    """orc_pcg_jacobi on all the OpenMP threads (omp_threads); max_iter < 0: exactly
+    -max_iter iterations."""
+    n = row_ptr.shape[0] - 1
+    x = np.zeros(n)
+    res = ctypes.c_double()
+    rn = ctypes.c_double()
+    it = lib().orc_pcg_jacobi_omp(n, row_ptr, cols, vals, np.ascontiguousarray(b, dtype=np.float64), x, rtol, atol,
+                                  max_iter, ctypes.byref(res), ctypes.byref(rn))
     return x, it, res.value, rn.value
 
 

@@ -36,3 +36,30 @@ GOLDEN_TOL = {"circle_2D": 1e-8, "sphere_3D": 1e-8, "L-shape_2D": 1e-12, "L-shap
 
 def path(name):
     return os.path.join(GOLDEN, name)
+
+
+# Neumann / traction cases (K15), same meshes:
+#   circle_neumann_2D  modules/poisson/inputs/circle.neumann.2D.arc     check/poisson_test_ref_circle_neumann_2D.txt
+#   sphere_neumann_3D  modules/poisson/inputs/sphere.neumann.3D.arc     check/poisson_test_ref_sphere_neumann_3D.txt
+# name: (mesh, f, [(dirichlet group, value)], [(neumann face group, (vx, vy[, vz]))], golden, penalty)
+NEUMANN_CASES = {
+    "circle_neumann_2D": ("circle_cut.msh", 5.5, [("horizontal", 0.5)], [("curved", (-0.35, 1.65))],
+                          "poisson_test_ref_circle_neumann_2D.txt", 1.0e30),
+    "sphere_neumann_3D": ("sphere_cut.msh", 5.5, [("horizontal", 0.5)], [("curved", (0.35, 1.65, 3.75))],
+                          "poisson_test_ref_sphere_neumann_3D.txt", 1.0e30),
+}
+
+# Block-2 elasticity with traction (modules/elasticity/inputs/bar.2D.traction.bsr.arc:22-35):
+# E = 21e5, nu = 0.28, `left` clamped (u = 0, both components) by penalty 1e30
+# (modules/elasticity/Fem.axl:32-41), traction (1, NULL) on `right`; golden
+# modules/elasticity/check/elasticity_traction_bar_test_ref.txt, checked by the
+# reference at epsilon 1e-3, min value 1e-16 (modules/elasticity/FemModule.cc:547-553).
+ELASTICITY_BAR = dict(mesh="bar.msh", E=21.0e5, nu=0.28, clamp="left", traction_group="right",
+                      traction=(1.0, 0.0), golden="elasticity_traction_bar_test_ref.txt", penalty=1.0e30)
+
+
+def lame(E, nu):
+    """modules/elasticity/FemModule.cc:132-133."""
+    mu2 = (E / (2 * (1 + nu))) * 2
+    lam = E * nu / ((1 + nu) * (1 - 2 * nu))
+    return lam, mu2

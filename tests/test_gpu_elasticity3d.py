@@ -73,10 +73,10 @@ def test_elasticity3d_uniform_variant_bitwise(ctx, monkeypatch, use_csr):
     assert bsr.stats()["uniform_slices"] > 0
     n3 = 3 * mesh.n_own_nodes
     drhs = ctx.malloc(8 * n3)
-    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs)
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
     v_uni, r_uni = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
     monkeypatch.setenv("AFEM_ASSEMBLY_UNIFORM", "0")
-    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs)
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
     v_gen, r_gen = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
     ctx.free(drhs)
     assert np.array_equal(v_uni, v_gen), "uniform and general block-3 instances differ"

@@ -92,7 +92,7 @@ def test_assembly_bitwise_reproducible(ctx):
     _, _, v1 = bsr.download()
     r1 = ls.rhs_host()
     for _ in range(2):
-        bsr.assemblePoissonP1(1.0, 2.0, ls.rhsVariable())
+        bsr.assemblePoissonP1(1.0, 2.0, ls.rhsVariable(), rhs_mode="set")
         _, _, v2 = bsr.download()
         assert np.array_equal(v1, v2)
         assert np.array_equal(r1, ls.rhs_host())
@@ -109,7 +109,7 @@ def test_uniform_strip_variant(ctx, monkeypatch):
     _, _, v_uni = bsr.download()
     r_uni = ls.rhs_host()
     monkeypatch.setenv("AFEM_ASSEMBLY_UNIFORM", "0")
-    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable())
+    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
     rows, cols, v_gen = bsr.download()
     assert np.array_equal(v_uni, v_gen), "uniform and general strip kernels differ"
     assert np.array_equal(r_uni, ls.rhs_host())
@@ -230,7 +230,8 @@ def _oracle_system(gm_cells, coords, n_own, n_nodes, f, bcs, P):
 
 
 @pytest.mark.parametrize("case", list(CASES))
-def test_golden_solve(ctx, case):
+@pytest.mark.parametrize("method", ["auto", "pcg"])
+def test_golden_solve(ctx, case, method):
     mfile, f, bcs, gfile, P = CASES[case]
     gm = read_gmsh(path(mfile))
     mesh = af.Mesh.from_arrays(ctx, gm.dim, gm.cells, gm.coords)
@@ -238,7 +239,7 @@ def test_golden_solve(ctx, case):
     groups = [(gm.group_nodes(g), v) for g, v in bcs]
     for ids, v in groups:
         ls.applyDirichletViaPenalty(ids, v, P)
-    ls.setSolverOptions(rtol=1e-14, max_iter=20000)
+    ls.setSolverOptions(rtol=1e-14, max_iter=20000, method=method)
     st = ls.solve()
     assert st["converged"], st
     x = ls.solution_host()
@@ -359,10 +360,13 @@ def test_spmv_matches_oracle(ctx):
 
 
 @pytest.mark.parametrize("dim,n", [(3, 12), (2, 40)])
-def test_random_node_permutation(ctx, dim, n):
+@pytest.mark.parametrize("order", ["morton", "node"])
+def test_random_node_permutation(ctx, monkeypatch, dim, n, order):
     # SURVEY §8d robustness variant: the structured mesh with a seeded random
-    # node and cell numbering (node-order slices, no bricks, scattered strips);
-    # the assembled matrix must be the permuted matrix of the unpermuted box
+    # node and cell numbering; slices follow a Morton curve of the node
+    # coordinates (default) or the caller's node order (AFEM_ORDER=node, read
+    # at every computeSparsity); the assembled matrix must be the permuted
+    # matrix of the unpermuted box either way
     ref = O.structured_mesh(dim, n, jitter=0.2, seed=20250220)
     rng = np.random.default_rng(1234)
     nn = ref["n_local"]
@@ -371,7 +375,21 @@ def test_random_node_permutation(ctx, dim, n):
     coords = np.empty_like(ref["coords"])
     coords[p] = ref["coords"]
     mesh = af.Mesh.from_arrays(ctx, dim, cells, coords)
+    if order == "node":
+        monkeypatch.setenv("AFEM_ORDER", "node")
     bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+    st = bsr.stats()
+    assert st["brick_order"] == 0
+    if order == "node":
+        monkeypatch.delenv("AFEM_ORDER")
+    else:
+        # the Morton sort ran: a slice's rows are spatial neighbours, so it
+        # couples to far fewer distinct nodes than 64 random rows would
+        m2 = af.Mesh.from_arrays(ctx, dim, cells, coords)
+        monkeypatch.setenv("AFEM_ORDER", "node")
+        b2, _ = _assemble_gpu(ctx, m2, 5.5)
+        monkeypatch.delenv("AFEM_ORDER")
+        assert st["max_slice_nodes"] < 0.6 * b2.stats()["max_slice_nodes"]
     rows, cols, vals = bsr.download()
     orp, ocols = O.sparsity(nn, nn, cells)
     ovals, orhs = O.assemble_poisson(nn, cells, coords, orp, ocols, 5.5)

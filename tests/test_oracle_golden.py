@@ -147,3 +147,75 @@ def test_pcg_dirichlet_driven_and_row_elimination():
     xd = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
     assert res <= 1e-14 and np.abs(x - xd).max() / np.abs(xd).max() < 1e-12
     assert np.all(x[ids] == 0.5)
+
+
+# ---------------------------------------------------------------- Neumann / traction (K15)
+from golden_cases import ELASTICITY_BAR, NEUMANN_CASES, lame  # noqa: E402
+
+
+def oracle_neumann_system(m, f, dirichlet, neumann, P):
+    rp, cols = O.sparsity(m.n_nodes, m.n_nodes, m.cells)
+    vals, rhs = O.assemble_poisson(m.n_nodes, m.cells, m.coords, rp, cols, f)
+    for g, v in neumann:
+        faces = m.group_faces(g)
+        O.neumann(m.dim, m.n_nodes, 1, O.NEUMANN_NORMAL, v, faces, m.face_cells(faces), m.cells, m.coords, rhs)
+    for g, v in dirichlet:
+        O.dirichlet_penalty(m.group_nodes(g), v, P, rp, cols, vals, rhs)
+    return rp, cols, vals, rhs
+
+
+@pytest.mark.parametrize("case", list(NEUMANN_CASES))
+def test_oracle_neumann_reproduces_reference_golden(case):
+    mfile, f, dirichlet, neumann, gfile, P = NEUMANN_CASES[case]
+    m = read_gmsh(path(mfile))
+    rp, cols, vals, rhs = oracle_neumann_system(m, f, dirichlet, neumann, P)
+    x = O.sequential_dense_solve(O.csr_to_dense(rp, cols, vals), rhs)
+    gold = read_node_result_file(path(gfile))
+    nerr, mx = O.check_node_result({int(t): x[i] for i, t in enumerate(m.node_tags)}, gold, 1e-4)
+    print(f"{case}: max rel error vs reference golden {mx:.3e}")
+    assert nerr == 0 and mx <= 1e-8, f"max rel error {mx:.3e}"
+
+
+def oracle_elasticity_bar():
+    c = ELASTICITY_BAR
+    m = read_gmsh(path(c["mesh"]))
+    lam, mu2 = lame(c["E"], c["nu"])
+    n = m.n_nodes
+    rp, cols = O.sparsity(n, n, m.cells)
+    v = O.assemble_elasticity_tri(n, m.cells, m.coords, rp, cols, lam, mu2)
+    A = np.zeros((2 * n, 2 * n))
+    for r in range(n):
+        for k in range(rp[r], rp[r + 1]):
+            A[2 * r:2 * r + 2, 2 * cols[k]:2 * cols[k] + 2] = v[4 * k:4 * k + 4].reshape(2, 2)
+    b = np.zeros(2 * n)
+    faces = m.group_faces(c["traction_group"])
+    O.neumann(2, n, 2, O.NEUMANN_TRACTION, c["traction"], faces, None, m.cells, m.coords, b)
+    clamp = m.group_nodes(c["clamp"])
+    for i in range(2):
+        d = 2 * clamp + i
+        A[d, d] = c["penalty"]   # matrixSetValue(dof, dof, P) (modules/elasticity/FemModule.cc:300-306)
+        b[d] = c["penalty"] * 0.0
+    return m, A, b, rp, cols, v
+
+
+def check_vector_golden(m, u, gfile, eps=1e-3, min_value=1e-16):
+    gold = read_node_result_file(path(gfile))
+    worst = 0.0
+    nerr = 0
+    for comp in range(2):
+        g = {uid: val[comp] for uid, val in gold.items()}
+        e, mx = O.check_node_result({int(t): u[2 * i + comp] for i, t in enumerate(m.node_tags)}, g, eps,
+                                    min_value)
+        nerr += e
+        worst = max(worst, mx)
+    return nerr, worst
+
+
+def test_oracle_elasticity_traction_reproduces_reference_golden():
+    """Pins the block-2 restatement (element matrix, traction RHS, penalty
+    clamp) with the reference's own elasticity golden."""
+    m, A, b, _, _, _ = oracle_elasticity_bar()
+    u = O.sequential_dense_solve(A, b)
+    nerr, mx = check_vector_golden(m, u, ELASTICITY_BAR["golden"])
+    print(f"elasticity bar traction: max rel error vs reference golden {mx:.3e}")
+    assert nerr == 0 and mx <= 1e-10, f"max rel error {mx:.3e}"

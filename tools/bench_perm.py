@@ -32,11 +32,11 @@ ctx.synchronize()
 print(f"sparsity {1e3 * (time.time() - t0):.1f} ms; stats {bsr.stats()}", flush=True)
 ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes, mesh.n_nodes)
 for _ in range(2):
-    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable())
+    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
 ctx.synchronize()
 for i in range(reps):
     ctx.event_record(2 * i)
-    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable())
+    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
     ctx.event_record(2 * i + 1)
 ctx.synchronize()
 ms = float(np.mean([ctx.event_elapsed(2 * i, 2 * i + 1) for i in range(reps)]))
