@@ -63,6 +63,22 @@ class SolveStats(ctypes.Structure):
                 ("residual_norm", ctypes.c_double), ("solve_ms", ctypes.c_double)]
 
 
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64)
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
+                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
+                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64))
+
+
+class HostTransport(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("allreduce_sum", ALLREDUCE_FN), ("exchange", EXCHANGE_FN)]
+
+
+class NewmarkParams(ctypes.Structure):
+    _fields_ = [("E", ctypes.c_double), ("nu", ctypes.c_double), ("rho", ctypes.c_double), ("dt", ctypes.c_double),
+                ("body_force", ctypes.c_double * 3), ("penalty", ctypes.c_double), ("gamma", ctypes.c_double),
+                ("beta", ctypes.c_double)]
+
+
 P = ctypes.c_void_p
 PP = ctypes.POINTER(ctypes.c_void_p)
 I32 = ctypes.c_int32
@@ -135,6 +151,12 @@ SIGNATURES = {
     "afem_ls_destroy": [P],
     "afem_comm_unique_id": [P],
     "afem_comm_create": [P, P, INT, INT, PP],
+    "afem_comm_create_host": [P, INT, INT, ctypes.POINTER(HostTransport), PP],
+    "afem_elastodynamics_create": [P, P, ctypes.POINTER(NewmarkParams), P, I64, INT, PP],
+    "afem_elastodynamics_set_solver_options": [P, ctypes.POINTER(SolverOpts)],
+    "afem_elastodynamics_step": [P, ctypes.POINTER(SolveStats)],
+    "afem_elastodynamics_state": [P, PP, PP, PP],
+    "afem_elastodynamics_destroy": [P],
     "afem_comm_destroy": [P],
     "afem_comm_allreduce_sum": [P, P, I64],
     "afem_ls_set_halo": [P, P, INT, P, P, P, P, P],

@@ -267,6 +267,9 @@ void structured_halo_lists(int dim, int n, int nz, int nranks, int rank, std::ve
                            std::vector<int64_t>& send_cnt, std::vector<int64_t>& recv_cnt,
                            std::vector<int32_t>& send_ids, std::vector<int32_t>& recv_ids);
 
+void expand_dof_lists(int k, std::vector<int64_t>& sc, std::vector<int64_t>& rc, std::vector<int32_t>& si,
+                      std::vector<int32_t>& ri);
+
 // op: 0 get, 1 set, 2 add on the (scalar DoF row, scalar DoF col) entry of a BSR
 // matrix; returns false when the entry is not in the structure.
 bool bsr_point(Bsr& b, int32_t row, int32_t col, int op, double v, double* out);
@@ -276,6 +279,26 @@ bool bsr_point(Bsr& b, int32_t row, int32_t col, int op, double v, double* out);
 // `vals_out` (device, nnz*k^2).
 void bsr_expand_scalar(Bsr& b, double* vals_out);
 
+// ------------------------------------------------------------------ time stepping (elastodynamics.cpp)
+struct Elastodynamics {
+  Mesh* mesh = nullptr;
+  Ctx* ctx = nullptr;
+  Comm* comm = nullptr;
+  afem_newmark_params p{};
+  double lambda = 0, mu2 = 0, gamma = 0.5, beta = 0.25, c0 = 0, c3 = 0, c4 = 0;
+  Bsr K;                  // block-3, per-row (CSR) layout: values = c0 M + K
+  DevBuf<double> mvals;   // consistent mass on K's structure (CSR order)
+  LinearSystem ls, lsm;   // the solve, and the mass operator's SpMV
+  DevBuf<double> U, V, A, W, MW;
+  DevBuf<int32_t> fixed;  // clamped DoFs
+  int64_t n = 0, n_cols = 0;
+  afem_solve_stats last{};
+};
+Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* prm, const int32_t* fixed_nodes,
+                           int64_t n_fixed, int mem);
+void dyn_step(Elastodynamics* d, afem_solve_stats* st);
+void dyn_destroy(Elastodynamics* d);
+
 void vec_lincomb(Ctx& ctx, int64_t n, double a, const double* x, double b, const double* y, double c, const double* z,
                  double* out);
 void newmark_update(Ctx& ctx, int64_t n, double dt, double beta, double gamma, const double* un, double* u, double* v,
@@ -283,6 +306,7 @@ void newmark_update(Ctx& ctx, int64_t n, double dt, double beta, double gamma, c
 
 void comm_unique_id(uint8_t* out);
 Comm* comm_create(Ctx& ctx, const uint8_t* id, int nranks, int rank);
+Comm* comm_create_host(int nranks, int rank, const afem_host_transport* t);
 void comm_destroy(Comm* c);
 int comm_nranks(Comm* c);
 int comm_rank(Comm* c);
@@ -299,4 +323,7 @@ struct afem_ls : afem::LinearSystem {};
 struct afem_comm {
   afem::Comm* c = nullptr;
   afem::Ctx* ctx = nullptr;
+};
+struct afem_elastodynamics {
+  afem::Elastodynamics* d = nullptr;
 };

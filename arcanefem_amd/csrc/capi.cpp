@@ -41,6 +41,23 @@ static hipMemcpyKind kind_of(int dst_mem, int src_mem)
 }
 
 namespace afem {
+// node halo lists -> DoF halo lists (DoF lid = node lid * k + i)
+void expand_dof_lists(int k, std::vector<int64_t>& sc, std::vector<int64_t>& rc, std::vector<int32_t>& si,
+                      std::vector<int32_t>& ri)
+{
+  auto expand = [k](std::vector<int32_t>& v) {
+    std::vector<int32_t> o;
+    o.reserve(v.size() * k);
+    for (int32_t x : v)
+      for (int i = 0; i < k; ++i) o.push_back(x * k + i);
+    v.swap(o);
+  };
+  expand(si);
+  expand(ri);
+  for (auto& c : sc) c *= k;
+  for (auto& c : rc) c *= k;
+}
+
 void structured_halo_lists(int dim, int n, int nz, int nranks, int rank, std::vector<int>& nbr,
                            std::vector<int64_t>& send_cnt, std::vector<int64_t>& recv_cnt,
                            std::vector<int32_t>& send_ids, std::vector<int32_t>& recv_ids)
@@ -945,6 +962,66 @@ int afem_newmark_update(afem_ctx* ctx, int64_t n, double dt, double beta, double
   API_END
 }
 
+int afem_elastodynamics_create(afem_mesh* mesh, afem_comm* comm, const afem_newmark_params* p,
+                               const int32_t* fixed_nodes, int64_t n_fixed, int mem, afem_elastodynamics** out)
+{
+  API_BEGIN
+  NOT_NULL(mesh);
+  NOT_NULL(p);
+  NOT_NULL(out);
+  *out = nullptr;
+  auto* h = new afem_elastodynamics();
+  try {
+    h->d = dyn_create(mesh, comm ? comm->c : nullptr, p, fixed_nodes, n_fixed, mem);
+  }
+  catch (...) {
+    delete h;
+    throw;
+  }
+  *out = h;
+  API_END
+}
+
+int afem_elastodynamics_set_solver_options(afem_elastodynamics* h, const afem_solver_opts* o)
+{
+  API_BEGIN
+  NOT_NULL(h);
+  NOT_NULL(o);
+  AFEM_REQUIRE(o->method != AFEM_SOLVER_DIRECT, AFEM_ERR_NOT_IMPL, "elastodynamics solves with the Jacobi-PCG");
+  AFEM_REQUIRE(o->max_iter >= 0 && o->rtol >= 0 && o->atol >= 0, AFEM_ERR_ARG, "bad solver options");
+  h->d->ls.opts = *o;
+  h->d->ls.opts.method = AFEM_SOLVER_PCG;
+  API_END
+}
+
+int afem_elastodynamics_step(afem_elastodynamics* h, afem_solve_stats* st)
+{
+  API_BEGIN
+  NOT_NULL(h);
+  dyn_step(h->d, st);
+  API_END
+}
+
+int afem_elastodynamics_state(afem_elastodynamics* h, double** u, double** v, double** a)
+{
+  API_BEGIN
+  NOT_NULL(h);
+  if (u) *u = h->d->U.p;
+  if (v) *v = h->d->V.p;
+  if (a) *a = h->d->A.p;
+  API_END
+}
+
+int afem_elastodynamics_destroy(afem_elastodynamics* h)
+{
+  API_BEGIN
+  if (h) {
+    dyn_destroy(h->d);
+    delete h;
+  }
+  API_END
+}
+
 int afem_ls_destroy(afem_ls* ls)
 {
   API_BEGIN
@@ -976,6 +1053,26 @@ int afem_comm_create(afem_ctx* ctx, const uint8_t id[AFEM_UNIQUE_ID_BYTES], int 
   auto* c = new afem_comm();
   try {
     c->c = comm_create(*ctx, id, nranks, rank);
+    c->ctx = ctx;
+  }
+  catch (...) {
+    delete c;
+    throw;
+  }
+  *out = c;
+  API_END
+}
+
+int afem_comm_create_host(afem_ctx* ctx, int nranks, int rank, const afem_host_transport* t, afem_comm** out)
+{
+  API_BEGIN
+  NOT_NULL(ctx);
+  NOT_NULL(t);
+  NOT_NULL(out);
+  *out = nullptr;
+  auto* c = new afem_comm();
+  try {
+    c->c = comm_create_host(nranks, rank, t);
     c->ctx = ctx;
   }
   catch (...) {
@@ -1066,6 +1163,12 @@ int afem_ls_set_halo_structured(afem_ls* ls, afem_comm* comm, afem_mesh* mesh)
   std::vector<int32_t> si, ri;
   structured_halo_lists(st.dim, st.n, st.nz, st.nranks, st.rank, nb, sc, rc, si, ri);
   std::vector<int32_t> nb32(nb.begin(), nb.end());
+  AFEM_REQUIRE(mesh->n_own > 0 && ls->n_rows % mesh->n_own == 0, AFEM_ERR_ARG,
+               "linear system rows are not a multiple of the mesh's owned nodes");
+  const int k = (int)(ls->n_rows / mesh->n_own);
+  AFEM_REQUIRE(k >= 1 && k <= 3 && ls->n_cols >= k * mesh->n_nodes, AFEM_ERR_ARG,
+               "linear system does not span NB_DOF x (owned + ghost) nodes");
+  if (k > 1) expand_dof_lists(k, sc, rc, si, ri);
   ls->ctx->set_device();
   ls->halo.reset(new Halo());
   halo_setup(*ls->halo, *ls->ctx, comm->c, (int)nb.size(), nb32.data(), sc.data(), si.data(), rc.data(), ri.data());

@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <vector>
 
 #include "afem_internal.hpp"
 
@@ -16,6 +17,22 @@ namespace afem {
 struct Comm {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  // host transport (afem_comm_create_host): the caller's IParallelMng-like
+  // callbacks move the halo and the dot-product sums through host memory
+  bool host = false;
+  afem_host_transport ht{};
+  double* pin = nullptr;  // pinned staging buffer (allreduce / halo)
+  size_t pin_n = 0;
+  double* stage(size_t n)
+  {
+    if (n > pin_n) {
+      if (pin) (void)hipHostFree(pin);
+      pin = nullptr;
+      AFEM_HIP(hipHostMalloc(reinterpret_cast<void**>(&pin), n * sizeof(double), hipHostMallocDefault));
+      pin_n = n;
+    }
+    return pin;
+  }
 };
 
 #define AFEM_NCCL(x)                                                                                  \
@@ -67,16 +84,38 @@ Comm* comm_create(Ctx& ctx, const uint8_t* idb, int nranks, int rank)
   return c;
 }
 
+Comm* comm_create_host(int nranks, int rank, const afem_host_transport* t)
+{
+  AFEM_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, AFEM_ERR_ARG, "afem_comm_create_host: bad rank/nranks");
+  AFEM_REQUIRE(t && t->allreduce_sum && t->exchange, AFEM_ERR_ARG, "afem_comm_create_host: missing callbacks");
+  auto* c = new Comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->host = true;
+  c->ht = *t;
+  return c;
+}
+
 void comm_destroy(Comm* c)
 {
   if (!c) return;
   if (c->comm) ncclCommDestroy(c->comm);
+  if (c->pin) (void)hipHostFree(c->pin);
   delete c;
 }
 
 void comm_allreduce(Comm* c, Ctx& ctx, double* d, int64_t n)
 {
-  if (!c || c->nranks == 1) return;
+  if (!c || c->nranks == 1 || n <= 0) return;
+  if (c->host) {
+    double* h = c->stage((size_t)n);
+    AFEM_HIP(hipMemcpyAsync(h, d, n * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    AFEM_REQUIRE(c->ht.allreduce_sum(c->ht.user, h, n) == 0, AFEM_ERR_COMM, "host transport: allreduce_sum failed");
+    AFEM_HIP(hipMemcpyAsync(d, h, n * sizeof(double), hipMemcpyHostToDevice, ctx.stream));
+    ctx.sync();
+    return;
+  }
   AFEM_NCCL(ncclAllReduce(d, d, (size_t)n, ncclDouble, ncclSum, c->comm, ctx.stream));
 }
 
@@ -116,6 +155,27 @@ void halo_exchange(Halo& h, Ctx& ctx, double* x)
     hipLaunchKernelGGL(k_gather, dim3(grid_for(h.n_send, 256)), dim3(256), 0, ctx.stream, h.n_send, h.send_ids.p, x,
                        h.send_buf.p);
     AFEM_LAUNCHED();
+  }
+  if (h.comm->host) {
+    Comm* c = h.comm;
+    double* hb = c->stage((size_t)(h.n_send + h.n_recv));
+    if (h.n_send)
+      AFEM_HIP(hipMemcpyAsync(hb, h.send_buf.p, h.n_send * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    std::vector<int32_t> nb(h.nbr.begin(), h.nbr.end());
+    AFEM_REQUIRE(c->ht.exchange(c->ht.user, (int)nb.size(), nb.data(), hb, h.send_cnt.data(), hb + h.n_send,
+                                h.recv_cnt.data()) == 0,
+                 AFEM_ERR_COMM, "host transport: exchange failed");
+    if (h.n_recv)
+      AFEM_HIP(hipMemcpyAsync(h.recv_buf.p, hb + h.n_send, h.n_recv * sizeof(double), hipMemcpyHostToDevice,
+                              ctx.stream));
+    if (h.n_recv) {
+      hipLaunchKernelGGL(k_scatter, dim3(grid_for(h.n_recv, 256)), dim3(256), 0, ctx.stream, h.n_recv, h.recv_ids.p,
+                         h.recv_buf.p, x);
+      AFEM_LAUNCHED();
+    }
+    ctx.sync();
+    return;
   }
   // the group is always closed, even after a failed send/recv: an open group
   // would swallow every later collective on the communicator (the CG

@@ -1,0 +1,183 @@
+// 3D elastodynamics time stepping on the assembly + CG path (BASELINE config
+// C5), native behind the C ABI.  Mirrors the reference's time-stepping callers:
+//   modules/elastodynamics/FemModule.cc  Newmark-beta constants (:255-270),
+//     RHS M (c0 U + c3 V + c4 A) + body force (:842-862), state update
+//     _updateVariables (:429-455), the matrix re-assembled every step (:149-153);
+//   modules/passmo/ElastodynamicModule.cc  3D, re-assembly every step on a
+//     fixed structure (:469-536).
+// Per step: the fused block-3 kernel re-assembles c0 M + K and the body-force
+// RHS (rhs_mode SET), the device lincomb + mass SpMV (the mass values share
+// the stiffness structure, assembled once) add M (c0 U + c3 V + c4 A), the
+// clamped DoFs are imposed by penalty, the Jacobi-PCG solves (halo exchange
+// and dot-product sums over ranks when a communicator is attached) and the
+// Newmark update runs on the device.  Rayleigh damping (etam, etak) and the
+// generalized-alpha variant are not implemented.
+#include <cmath>
+#include <vector>
+
+#include "afem_internal.hpp"
+
+namespace afem {
+
+namespace {
+
+void halo_for(LinearSystem& ls, Comm* comm, Mesh& m)
+{
+  if (!comm || comm_nranks(comm) == 1) return;
+  AFEM_REQUIRE(m.st.valid, AFEM_ERR_NOT_IMPL,
+               "distributed elastodynamics: the halo plan is built for structured slab meshes "
+               "(afem_ls_set_halo for others)");
+  std::vector<int> nb;
+  std::vector<int64_t> sc, rc;
+  std::vector<int32_t> si, ri;
+  structured_halo_lists(m.st.dim, m.st.n, m.st.nz, m.st.nranks, m.st.rank, nb, sc, rc, si, ri);
+  expand_dof_lists(3, sc, rc, si, ri);
+  std::vector<int32_t> nb32(nb.begin(), nb.end());
+  ls.halo.reset(new Halo());
+  halo_setup(*ls.halo, *ls.ctx, comm, (int)nb.size(), nb32.data(), sc.data(), si.data(), rc.data(), ri.data());
+}
+
+void init_ls(LinearSystem& ls, Ctx* ctx, int64_t n, int64_t n_cols)
+{
+  ls.ctx = ctx;
+  ls.n_rows = n;
+  ls.n_cols = n_cols;
+  ls.opts.method = AFEM_SOLVER_PCG;
+  ls.opts.max_iter = 20000;
+  ls.opts.rtol = 1e-8;
+  ls.opts.atol = 0.0;
+  ls.opts.check_every = 8;
+  ls.opts.fixed_iterations = 0;
+  ls.rhs.alloc(n);
+  ls.sol.alloc(n_cols);
+  ls.forced_info.alloc(n);
+  ls.elim_info.alloc(n);
+  ls.forced_value.alloc(n);
+  ls.elim_value.alloc(n);
+  for (auto* b : { (void*)ls.rhs.p, (void*)ls.forced_value.p, (void*)ls.elim_value.p })
+    AFEM_HIP(hipMemsetAsync(b, 0, n * sizeof(double), ctx->stream));
+  AFEM_HIP(hipMemsetAsync(ls.sol.p, 0, n_cols * sizeof(double), ctx->stream));
+  AFEM_HIP(hipMemsetAsync(ls.forced_info.p, 0, n, ctx->stream));
+  AFEM_HIP(hipMemsetAsync(ls.elim_info.p, 0, n, ctx->stream));
+}
+}  // namespace
+
+Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* prm, const int32_t* fixed_nodes,
+                           int64_t n_fixed, int mem)
+{
+  {
+    AFEM_REQUIRE(mesh->nv == 4 && mesh->dim == 3, AFEM_ERR_NOT_IMPL, "elastodynamics needs a tetrahedral mesh");
+    AFEM_REQUIRE(prm->dt > 0 && prm->E > 0 && prm->nu > -1.0 && prm->nu < 0.5 && prm->rho >= 0, AFEM_ERR_ARG,
+                 "elastodynamics: bad material or time step");
+    AFEM_REQUIRE(n_fixed == 0 || fixed_nodes, AFEM_ERR_ARG, "fixed_nodes is NULL");
+    if (comm)
+      AFEM_REQUIRE(comm_nranks(comm) == 1 || (mesh->st.valid && mesh->st.nranks == comm_nranks(comm) &&
+                                              mesh->st.rank == comm_rank(comm)),
+                   AFEM_ERR_ARG, "the mesh's slab rank/nranks differ from the communicator");
+    mesh->ctx->set_device();
+    auto* d = new Elastodynamics();
+    try {
+      Ctx& ctx = *mesh->ctx;
+      d->mesh = mesh;
+      d->ctx = &ctx;
+      d->comm = comm;
+      d->p = *prm;
+      if (!(d->p.penalty > 0)) d->p.penalty = 1.0e30;  // modules/elasticity/Fem.axl:37-41
+      // modules/elastodynamics/FemModule.cc:130-134 (Lame) and :255-270 (Newmark, etam = etak = 0)
+      d->mu2 = (prm->E / (2 * (1 + prm->nu))) * 2;
+      d->lambda = prm->E * prm->nu / ((1 + prm->nu) * (1 - 2 * prm->nu));
+      d->gamma = prm->gamma > 0 ? prm->gamma : 0.5;
+      d->beta = prm->beta > 0 ? prm->beta : 0.25 * (d->gamma + 0.5) * (d->gamma + 0.5);
+      d->c0 = prm->rho / (d->beta * prm->dt * prm->dt);
+      d->c3 = prm->rho / d->beta / prm->dt;
+      d->c4 = prm->rho * ((1.0 - 2.0 * d->beta) / 2.0 / d->beta);
+      d->n = 3 * mesh->n_own;
+      d->n_cols = 3 * mesh->n_nodes;
+      // structure once; stiffness and mass share it
+      d->K.mesh = mesh;
+      d->K.nb_dof = 3;
+      d->K.order_per_block = false;
+      build_structure(*mesh, d->K.s);
+      d->K.values.alloc((size_t)d->K.s.nnz * 9);
+      d->K.has_sparsity = true;
+      d->mvals.alloc((size_t)d->K.s.nnz * 9);
+      std::swap(d->K.values, d->mvals);
+      assemble_elasticity_tet(d->K, 0.0, 0.0, 1.0, nullptr, nullptr, 0);  // M (c0 = 1)
+      std::swap(d->K.values, d->mvals);
+      bsr_expand_scalar(d->K, nullptr);  // scalar rows / columns of the block-3 CSR (shared)
+      init_ls(d->ls, &ctx, d->n, d->n_cols);
+      init_ls(d->lsm, &ctx, d->n, d->n_cols);
+      for (LinearSystem* l : { &d->ls, &d->lsm }) {
+        l->has_csr = true;
+        l->csr_n = d->n;
+        l->csr_nnz = d->K.s.nnz * 9;
+        l->csr_rows = d->K.csr_rows.p;
+        l->csr_cols = d->K.csr_cols.p;
+      }
+      d->ls.csr_vals = d->K.values.p;
+      d->lsm.csr_vals = d->mvals.p;
+      halo_for(d->ls, d->comm, *mesh);
+      halo_for(d->lsm, d->comm, *mesh);
+      for (auto* b : { &d->U, &d->V, &d->A, &d->MW }) {
+        b->alloc(d->n);
+        AFEM_HIP(hipMemsetAsync(b->p, 0, b->bytes(), ctx.stream));
+      }
+      d->W.alloc(d->n_cols);  // ghost part filled by the mass SpMV's halo exchange
+      AFEM_HIP(hipMemsetAsync(d->W.p, 0, d->W.bytes(), ctx.stream));
+      std::vector<int32_t> hn(n_fixed);
+      if (n_fixed) {
+        AFEM_HIP(hipMemcpyAsync(hn.data(), fixed_nodes, n_fixed * 4,
+                                mem == AFEM_MEM_HOST ? hipMemcpyHostToHost : hipMemcpyDeviceToHost, ctx.stream));
+        ctx.sync();
+      }
+      std::vector<int32_t> dofs;
+      for (int32_t nd : hn) {
+        AFEM_REQUIRE(nd >= 0 && nd < mesh->n_nodes, AFEM_ERR_ARG, "fixed node id out of range");
+        if (nd < mesh->n_own)
+          for (int i = 0; i < 3; ++i) dofs.push_back(3 * nd + i);
+      }
+      d->fixed.alloc(dofs.size());
+      if (!dofs.empty())
+        AFEM_HIP(hipMemcpyAsync(d->fixed.p, dofs.data(), dofs.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+      ctx.sync();
+    }
+    catch (...) {
+      delete d;
+      throw;
+    }
+    return d;
+  }
+}
+
+void dyn_step(Elastodynamics* d, afem_solve_stats* st)
+{
+  {
+    Ctx& ctx = *d->ctx;
+    ctx.set_device();
+    const double f[3] = { d->p.body_force[0], d->p.body_force[1], d->p.body_force[2] };
+    // LHS c0 M + K and the body force (rhs = f |K|/4), re-assembled on the fixed structure
+    assemble_elasticity_tet(d->K, d->lambda, d->mu2, d->c0, f, d->ls.rhs.p, 0);
+    // rhs += M (c0 U + c3 V + c4 A)
+    vec_lincomb(ctx, d->n, d->c0, d->U.p, d->c3, d->V.p, d->c4, d->A.p, d->W.p);
+    ls_spmv(d->lsm, d->W.p, d->MW.p);
+    vec_lincomb(ctx, d->n, 1.0, d->ls.rhs.p, 1.0, d->MW.p, 0.0, nullptr, d->ls.rhs.p);
+    // clamped DoFs by penalty (the reference's default Dirichlet treatment)
+    if (d->fixed.n) ls_set_list(d->ls, d->fixed.p, (int64_t)d->fixed.n, AFEM_MEM_DEVICE, 0, 0.0, d->p.penalty);
+    ls_solve(d->ls, &d->last);
+    newmark_update(ctx, d->n, d->p.dt, d->beta, d->gamma, d->ls.sol.p, d->U.p, d->V.p, d->A.p);
+    ctx.sync();
+    if (st) *st = d->last;
+  }
+}
+
+void dyn_destroy(Elastodynamics* d)
+{
+  if (!d) return;
+  d->ctx->set_device();
+  (void)hipStreamSynchronize(d->ctx->stream);
+  if (d->ls.pinned) (void)hipHostFree(d->ls.pinned);
+  if (d->lsm.pinned) (void)hipHostFree(d->lsm.pinned);
+  delete d;
+}
+
+}  // namespace afem

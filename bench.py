@@ -1,18 +1,31 @@
 """Benchmark of the MI355X FEM assembly + CG path (BASELINE.json metric).
 
 A step = one numeric assembly of the Poisson-3D P1 system on a fixed sparsity:
-matrix values + constant-source RHS (one fused kernel), the penalty Dirichlet
-list (forced info/value, rhs = P g) and the forced values written into the
-CSR (the reference's K14/K8/K16/K19 sequence).  Inputs (mesh, structure) are
-resident in HBM before the timed region.  Afterwards a fixed number of
-Jacobi-PCG iterations on the assembled CSR is timed for the CG iter/s half of
-the metric.
+matrix values + constant-source RHS (one fused kernel; the module's
+rhs.fill(0) + applyConstantSourceToRhs, modules/poisson/FemModule.cc:163-169),
+the penalty Dirichlet list (forced info/value, rhs = P g) and the forced
+values written into the CSR (the reference's K14/K8/K16/K19 sequence).
+Inputs (mesh, structure) are resident in HBM before the timed region.
+Afterwards a fixed number of Jacobi-PCG iterations on the assembled CSR is
+timed for the CG iter/s half of the metric.
+
+Timing: `value` = DoF assembled per second over the K timed steps (wall clock
+between barriers, max over ranks).  The roofline of the assembly kernels uses
+the MEDIAN of the per-step kernel durations (HIP events recorded on the
+context stream around each assembly launch; BASELINE.md §4 asks for medians);
+the committed rocprofv3 kernel-stats summary of the same command is in
+profiles/.
 
 Multi-GPU (torchrun): one process per GPU; the mesh is a z-slab per rank with
 one ghost layer and the same per-rank size (weak scaling); assembly needs no
 communication, the CG exchanges ghost values and sums dot products through
 RCCL (libafem's own communicator; torch.distributed/gloo is only the control
 plane: bootstrap of the RCCL id, barriers, max-over-ranks of the timings).
+
+Side measurements at N=1 (rank 0): C4 (Poisson-3D at 10^8 DoF on one GPU:
+assembly + CG), C3 (block-3 elasticity), C5 (elastodynamics step), and the
+CPU baselines of BASELINE.md §4 (assembly cell loop, OpenMP Jacobi-PCG over 50
+fixed iterations, the C1 dense SequentialBasic end to end).
 """
 from __future__ import annotations
 
@@ -29,6 +42,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MDoF/s assembly + CG iter/s, Poisson-3D P1 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ASM_KERNEL = "k_assemble_strip<4,2,16,uniform> + k_assemble_strip<4,2,16,general>"
 
 
 def parse():
@@ -42,17 +56,115 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_assembly_C2.json"))
-    ap.add_argument("--no-extras", action="store_true", help="skip the C3 / C5 side measurements")
+    ap.add_argument("--no-extras", action="store_true", help="skip the C3 / C4 / C5 side measurements")
     ap.add_argument("--c3-n", type=int, default=170, help="C3 block-3 elasticity box (170 -> 5.0M nodes)")
+    ap.add_argument("--c4-n", type=int, default=463, help="C4 Poisson box on one GPU (463 -> 99.9M DoF); 0: skip")
     ap.add_argument("--c5-n", type=int, default=100, help="C5 elastodynamics box (100 -> 1.03M nodes)")
     ap.add_argument("--c5-steps", type=int, default=5)
     return ap.parse_args()
 
 
+def algorithmic_bytes(n_inc, n_local, n_own, nnz):
+    """Per assembly launch: incidence table 4 B per (owned
+    row, incident cell) = the connectivity bytes 4*nv*Ncell, node coordinates
+    24 B, row offsets 8 B, columns 4 B + values 8 B per non-zero, RHS 8 B per
+    owned DoF (written once: the fused fill(0) + source)."""
+    return 4 * n_inc + 24 * n_local + 8 * (n_own + 1) + 12 * nnz + 8 * n_own
+
+
+def cg_bytes(nnz, n_own):
+    """Per Jacobi-PCG iteration of this implementation's kernel sequence
+    (DESIGN.md §3.3): SpMV 12 nnz + 8 (N+1) + 8 N gathers + 8 N store; update
+    64 N; direction 24 N."""
+    return 12 * nnz + 8 * (n_own + 1) + 104 * n_own
+
+
+def poisson_setup(ctx, af, n, nz, world, rank):
+    mesh = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=20250220, nranks=world, rank=rank)
+    bsr = af.BSRFormat(mesh, 1).initialize(True)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    bsr.computeSparsity()
+    ctx.synchronize()
+    sparsity_ms = (time.perf_counter() - t0) * 1e3
+    ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes, mesh.n_nodes)
+    bsr.toLinearSystem(ls)
+    bottom = mesh.bottom_nodes()
+    dbottom = ctx.malloc(max(4 * bottom.size, 4))
+    ctx.to_device(dbottom, bottom)
+    return mesh, bsr, ls, bottom, dbottom, sparsity_ms
+
+
+def make_step(ctx, bsr, ls, bottom, dbottom):
+    rhs = ls.rhsVariable()
+
+    def step(ev=None):
+        if ev is not None:
+            ctx.event_record(ev)
+        bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set")  # rhs.fill(0) + applyConstantSourceToRhs, fused
+        if ev is not None:
+            ctx.event_record(ev + 1)
+        ls.applyDirichletViaPenaltyDevice(dbottom, bottom.size, 0.5, 1.0e30)
+        ls.applyBoundaryConditions()
+
+    return step
+
+
+def roofline(bsr, mesh, kernel_ms):
+    st = bsr.stats()
+    nnz = bsr.view().nnz_blocks
+    ab = algorithmic_bytes(int(st["n_incidences"]), mesh.n_nodes, mesh.n_own_nodes, nnz)
+    achieved = ab / (kernel_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": ASM_KERNEL, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(ab),
+            "kernel_ms": round(kernel_ms, 4),
+            "inc_padding": round(st["inc_table_entries"] / max(int(st["n_incidences"]), 1) - 1.0, 4),
+            "uniform_slice_frac": round(st["uniform_slices"] / max(st["n_slices"], 1), 4)}
+
+
+def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50):
+    """BASELINE config C4's problem (Poisson-3D at ~10^8 DoF) on ONE GPU: the
+    north-star size.  Assembly kernel time = median of `reps` launches after
+    `warmup` (HIP events), CG = `cg_iters` fixed Jacobi-PCG iterations."""
+    mesh, bsr, ls, bottom, dbottom, sp_ms = poisson_setup(ctx, af, n, None, 1, 0)
+    step = make_step(ctx, bsr, ls, bottom, dbottom)
+    for _ in range(warmup):
+        step()
+    ctx.synchronize()
+    for i in range(reps):
+        step(210 + 2 * i)
+    ctx.synchronize()
+    ks = [ctx.event_elapsed(210 + 2 * i, 211 + 2 * i) for i in range(reps)]
+    kms = float(np.median(ks))
+    nnz = bsr.view().nnz_blocks
+    ls.setSolverOptions(fixed_iterations=cg_iters)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    st = ls.solve()
+    ctx.synchronize()
+    cg_s = time.perf_counter() - t0
+    ips = cg_iters / cg_s
+    out = {"config": f"C4 problem on 1 GPU: Poisson-3D P1 jittered Kuhn box n={n} ({mesh.n_own_nodes} DoF, "
+                     f"{mesh.n_cells} tets, {nnz} nnz), CSR assembly + penalty Dirichlet; CG = {cg_iters} fixed "
+                     f"Jacobi-PCG iterations",
+           "dof": int(mesh.n_own_nodes), "nnz": int(nnz),
+           "value": round(mesh.n_own_nodes / (kms * 1e-3) / 1e6, 1), "unit": "MDoF/s (assembly kernels)",
+           "kernel_ms_median": round(kms, 4), "kernel_ms_all": [round(x, 4) for x in ks],
+           "roofline": roofline(bsr, mesh, kms),
+           "cg_iter_per_s": round(ips, 2), "cg_roofline_frac": round(cg_bytes(nnz, mesh.n_own_nodes) * ips / 1e9
+                                                                       / HBM_PEAK_GBS, 4),
+           "cg_device_ms": round(st["solve_ms"], 2), "sparsity_ms": round(sp_ms, 1)}
+    ctx.free(dbottom)
+    ls.reset()
+    bsr.close()
+    mesh.close()
+    return out
+
+
 def elasticity_c3(ctx, af, n, reps=10, warmup=2):
     """BASELINE config C3: block-3 P1 elasticity on tetrahedra (BSR, ordered per
-    block), stiffness + body force fused, on fixed sparsity; kernel time from
-    HIP events around each launch.  Algorithmic bytes per launch: incidence
+    block), stiffness + body force fused, on fixed sparsity; kernel time = median
+    of HIP-event launch times.  Algorithmic bytes per launch: incidence
     table 4*nv*Ncell, coordinates 24 N, row offsets 8 (N+1), block columns
     4 nnz_b, block values 72 nnz_b, RHS 24 N."""
     E, nu = 21.0e5, 0.28
@@ -70,11 +182,11 @@ def elasticity_c3(ctx, af, n, reps=10, warmup=2):
         bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs, rhs_mode="set")
     ctx.synchronize()
     for i in range(reps):
-        ctx.event_record(200 + 2 * i)
+        ctx.event_record(230 + 2 * i)
         bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs, rhs_mode="set")
-        ctx.event_record(201 + 2 * i)
+        ctx.event_record(231 + 2 * i)
     ctx.synchronize()
-    kms = float(np.mean([ctx.event_elapsed(200 + 2 * i, 201 + 2 * i) for i in range(reps)]))
+    kms = float(np.median([ctx.event_elapsed(230 + 2 * i, 231 + 2 * i) for i in range(reps)]))
     st = bsr.stats()
     v = bsr.view()
     nnz_b = v.nnz_blocks
@@ -83,7 +195,7 @@ def elasticity_c3(ctx, af, n, reps=10, warmup=2):
     out = {"config": f"C3 elasticity block-3 P1 tets, Kuhn box n={n} ({n_own} nodes, {3 * n_own} DoF, "
                      f"{mesh.n_cells} tets), BSR per-block, stiffness + body force",
            "value": round(3 * n_own / (kms * 1e-3) / 1e6, 1), "unit": "MDoF/s", "kernel_ms": round(kms, 4),
-           "kernel": "k_assemble_elast_tet",
+           "kernel": "k_assemble_elast_strip",
            "roofline": {"bound": "hbm", "achieved": round(ab / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(ab / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "algorithmic_bytes_per_launch": int(ab)},
@@ -123,12 +235,8 @@ def elastodynamics_c5(ctx, af, n, steps):
     return out
 
 
-def algorithmic_bytes(n_inc, n_local, n_own, nnz):
-    """Per assembly launch: incidence table 4 B per
-    (owned row, incident cell) = the connectivity bytes 4*nv*Ncell, node
-    coordinates 24 B, row offsets 8 B, columns 4 B + values 8 B per non-zero,
-    RHS 8 B per owned DoF."""
-    return 4 * n_inc + 24 * n_local + 8 * (n_own + 1) + 12 * nnz + 8 * n_own
+def _threads():
+    return min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1))
 
 
 def cpu_baseline(n, seconds):
@@ -154,13 +262,67 @@ def cpu_baseline(n, seconds):
         return reps, t
 
     r1, t1 = run(O.assemble_poisson, 0.4 * seconds)
-    threads = O.omp_threads(min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
+    threads = O.omp_threads(_threads())
     O.assemble_poisson_omp(n_own, cells, coords, rp, cols, 5.5)  # thread pool warm-up
     rm, tm = run(O.assemble_poisson_omp, 0.6 * seconds)
     return {"value": n_own * rm / tm / 1e6, "unit": "MDoF/s", "cores": threads, "kind": "port",
             "sample": f"Poisson-3D P1 Kuhn box n={n} ({n_own} DoF, {cells.shape[0]} tets): {rm} assemblies in "
                       f"{tm:.1f} s on {threads} OpenMP threads (oracle/oracle.c cell loop, atomic adds, gcc -O2); "
                       f"single thread {n_own * r1 / t1 / 1e6:.2f} MDoF/s ({r1} assemblies in {t1:.1f} s)"}
+
+
+def cpu_baseline_cg(n, iters=50, runs=5):
+    """the oracle's Jacobi-PCG with OpenMP on the same CSR
+    kind, exactly `iters` iterations, median of `runs` after one warm-up."""
+    from oracle import oracle as O
+
+    m = O.structured_mesh(3, n)
+    rp, cols = O.sparsity(m["n_local"], m["n_own"], m["cells"])
+    vals, rhs = O.assemble_poisson(m["n_own"], m["cells"], m["coords"], rp, cols, 5.5)
+    O.dirichlet_penalty(m["dirichlet"], 0.5, 1e30, rp, cols, vals, rhs)
+    threads = O.omp_threads(_threads())
+    O.pcg_jacobi_omp(rp, cols, vals, rhs, max_iter=-iters)
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        O.pcg_jacobi_omp(rp, cols, vals, rhs, max_iter=-iters)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"value": round(iters / t, 2), "unit": "iter/s", "cores": threads, "kind": "port",
+            "sample": f"Jacobi-PCG (oracle/oracle.c orc_pcg_jacobi_omp) on the Poisson-3D Kuhn box n={n} "
+                      f"({m['n_own']} DoF, {int(rp[-1])} nnz): {iters} fixed iterations, median of {runs} runs "
+                      f"{t * 1e3:.1f} ms on {threads} OpenMP threads"}
+
+
+def cpu_baseline_c1(runs=3):
+    """config C1 end to end with the SequentialBasic
+    semantics (femutils/DoFLinearSystem.cc:83-164): dense N x N `+=` assembly,
+    penalty via matrixSetValue, dense -> CSR dropping zeros, PCG eps 1e-15.
+    Single-threaded numpy/C; median of `runs`."""
+    from oracle import oracle as O
+
+    m = O.structured_mesh(2, 99)
+    n = m["n_own"]
+    cells, coords = m["cells"], m["coords"]
+    ts, x = [], None
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        A = np.zeros((n, n))
+        b = np.zeros(n)
+        for c in cells:
+            K, area = O.element_tri3(coords[c])
+            A[np.ix_(c, c)] += K
+            b[c] += 5.5 * area / 3
+        for d in m["dirichlet"]:
+            A[d, d] = 1e30
+            b[d] = 1e30 * 0.5
+        x = O.sequential_dense_solve(A, b)
+        ts.append(time.perf_counter() - t0)
+        del A
+    t = float(np.median(ts))
+    return {"value": round(t * 1e3, 1), "unit": "ms (assembly + solve)", "cores": 1, "kind": "port",
+            "sample": f"C1: Poisson-2D P1 n=99 ({n} DoF, {cells.shape[0]} triangles), dense SequentialBasic "
+                      f"semantics end to end, median of {runs}; max|u| = {np.abs(x).max():.6g}"}
 
 
 def main():
@@ -183,21 +345,9 @@ def main():
     n = args.n
     nz = n * world
     t_setup = time.perf_counter()
-    mesh = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=20250220, nranks=world, rank=rank)
-    bsr = af.BSRFormat(mesh, 1).initialize(True)
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    bsr.computeSparsity()
-    ctx.synchronize()
-    sparsity_ms = (time.perf_counter() - t0) * 1e3
-    ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes, mesh.n_nodes)
-    bsr.toLinearSystem(ls)
-    rhs = ls.rhsVariable()
-    bottom = mesh.bottom_nodes()
-    dbottom = ctx.malloc(max(4 * bottom.size, 4))
-    ctx.to_device(dbottom, bottom)
-    view = bsr.view()
-    nnz = view.nnz_blocks
+    mesh, bsr, ls, bottom, dbottom, sparsity_ms = poisson_setup(ctx, af, n, nz, world, rank)
+    nnz = bsr.view().nnz_blocks
+    n_own, n_cells = mesh.n_own_nodes, mesh.n_cells
     comm = None
     if world > 1:
         uid = [af.Communicator.unique_id() if rank == 0 else None]
@@ -205,15 +355,7 @@ def main():
         comm = af.Communicator(ctx, world, rank, uid[0])
         ls.set_halo_structured(comm, mesh)
     setup_s = time.perf_counter() - t_setup
-
-    def step(ev=None):
-        if ev is not None:
-            ctx.event_record(ev)
-        bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set")  # rhs.fill(0) + source, fused
-        if ev is not None:
-            ctx.event_record(ev + 1)
-        ls.applyDirichletViaPenaltyDevice(dbottom, bottom.size, 0.5, 1.0e30)
-        ls.applyBoundaryConditions()
+    step = make_step(ctx, bsr, ls, bottom, dbottom)
 
     for _ in range(args.warmup):
         step()
@@ -236,11 +378,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
-        tot = torch.tensor([float(mesh.n_own_nodes)], dtype=torch.float64)
+        tot = torch.tensor([float(n_own)], dtype=torch.float64)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         total_dof = float(tot[0])
     else:
-        total_dof = float(mesh.n_own_nodes)
+        total_dof = float(n_own)
     ms_per_step = elapsed * 1e3 / args.steps
     value = total_dof * args.steps / elapsed / 1e6
 
@@ -262,32 +404,39 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         cg_s = float(t[0])
     cg_iter_per_s = args.cg_iters / cg_s
-    # CG bytes per iteration (minimal fused form of this implementation):
-    # SpMV 12 nnz + 8 (N+1) + 8 N gathers + 8 N store; update 64 N; direction 24 N
-    cg_bytes = 12 * nnz + 8 * (mesh.n_own_nodes + 1) + 104 * mesh.n_own_nodes
 
     if rank == 0:
-        kmean = float(np.mean(kernel_ms))
-        bst = bsr.stats()
-        n_inc = int(bst["n_incidences"])
-        ab = algorithmic_bytes(n_inc, mesh.n_nodes, mesh.n_own_nodes, nnz)
-        achieved = ab / (kmean * 1e-3) / 1e9
-        traffic = None
+        kmed = float(np.median(kernel_ms))
+        rf = roofline(bsr, mesh, kmed)
+        rf["kernel_ms_mean"] = round(float(np.mean(kernel_ms)), 4)
+        rf["traffic"] = None
         if os.path.exists(args.pmc_json):
             try:
                 with open(args.pmc_json) as f:
                     pm = json.load(f)
                 if pm.get("n") == n and pm.get("world") in (None, 1) and world == 1:
-                    traffic = pm.get("hbm_bytes_per_launch")
+                    rf["traffic"] = pm.get("hbm_bytes_per_launch")
+                    rf["traffic_profile"] = pm.get("tag")
             except Exception:
-                traffic = None
+                rf["traffic"] = None
+        extras = {}
+        if world == 1:
+            # free the headline's buffers before the large side legs
+            ctx.free(dbottom)
+            ls.reset()
+            bsr.close()
+            mesh.close()
+            dbottom = None
+        if not args.no_extras and world == 1:
+            if args.c4_n > 0:
+                extras["c4"] = poisson_c4(ctx, af, args.c4_n)
+            extras["c3"] = elasticity_c3(ctx, af, args.c3_n)
+            extras["c5"] = elastodynamics_c5(ctx, af, args.c5_n, args.c5_steps)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.cpu_baseline_n, args.cpu_baseline_seconds)
-        extras = {}
-        if not args.no_extras and world == 1:
-            extras["c3"] = elasticity_c3(ctx, af, args.c3_n)
-            extras["c5"] = elastodynamics_c5(ctx, af, args.c5_n, args.c5_steps)
+            extras["cpu_baseline_cg"] = cpu_baseline_cg(args.cpu_baseline_n)
+            extras["cpu_baseline_c1"] = cpu_baseline_c1()
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -303,37 +452,26 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": (f"C2 Poisson-3D P1, jittered Kuhn-tet box n={n} per GPU "
-                             f"({mesh.n_own_nodes} DoF, {mesh.n_cells} tets per GPU), CSR assembly "
+                             f"({n_own} DoF, {n_cells} tets per GPU), CSR assembly "
                              f"(matrix+RHS+penalty Dirichlet z=0) on fixed sparsity; CG = Jacobi-PCG on it"),
                 "n": n,
-                "dof_per_gpu": int(mesh.n_own_nodes),
+                "dof_per_gpu": int(n_own),
                 "nnz_per_gpu": int(nnz),
                 "parallelism": f"z-slab x{world}, RCCL halo + all-reduce in CG",
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_assemble_strip<4,2,16,uniform> + k_assemble_strip<4,2,16,general>",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": int(ab),
-                "kernel_ms": round(kmean, 4),
-                "inc_padding": round(bst["inc_table_entries"] / max(n_inc, 1) - 1.0, 4),
-                "uniform_slice_frac": round(bst["uniform_slices"] / max(bst["n_slices"], 1), 4),
-            },
+            "roofline": rf,
             "cpu_baseline": cpu,
             "cg_iter_per_s": round(cg_iter_per_s, 2),
             "cg_ms_per_iter": round(cg_s * 1e3 / args.cg_iters, 4),
-            "cg_roofline_frac": round(cg_bytes * cg_iter_per_s / 1e9 / HBM_PEAK_GBS, 4),
+            "cg_roofline_frac": round(cg_bytes(nnz, n_own) * cg_iter_per_s / 1e9 / HBM_PEAK_GBS, 4),
             "cg_device_ms": round(st["solve_ms"], 3),
             "sparsity_ms": round(sparsity_ms, 1),
             "setup_s": round(setup_s, 2),
             **extras,
         }
         print(json.dumps(out), flush=True)
-    ctx.free(dbottom)
+    if dbottom is not None:
+        ctx.free(dbottom)
     if comm:
         comm.close()
     if dist:

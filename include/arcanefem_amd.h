@@ -327,12 +327,56 @@ int afem_vec_lincomb(afem_ctx* ctx, int64_t n, double a, const double* x, double
 int afem_newmark_update(afem_ctx* ctx, int64_t n, double dt, double beta, double gamma, const double* u_new, double* u,
                         double* v, double* a);
 
+/* Native Newmark-beta elastodynamics time loop (BASELINE config C5): the
+ * callers of the path modules/elastodynamics/FemModule.cc (Newmark constants
+ * :255-270, RHS M (c0 U + c3 V + c4 A) + body force :842-862, update
+ * :429-455) and modules/passmo/ElastodynamicModule.cc (3D, re-assembly every
+ * step on a fixed structure, :469-536).  Per step: fused block-3 re-assembly
+ * of c0 M + K and the body force, mass operator (shares the structure),
+ * penalty clamp of the fixed nodes' DoFs, Jacobi-PCG (halo + all-reduces over
+ * `comm` when given: one ghosted z-slab per rank), device state update.
+ * Lame parameters as modules/elasticity/FemModule.cc:132-133. */
+typedef struct afem_elastodynamics afem_elastodynamics;
+typedef struct afem_newmark_params {
+  double E, nu, rho, dt;
+  double body_force[3];
+  double penalty; /* <= 0: 1e30 (modules/elasticity/Fem.axl:37-41) */
+  double gamma;   /* <= 0: 1/2 */
+  double beta;    /* <= 0: (gamma + 1/2)^2 / 4 */
+} afem_newmark_params;
+/* fixed_nodes: local node ids (in `mem`) whose 3 DoFs are clamped to 0; comm
+ * may be NULL (one subdomain). */
+int afem_elastodynamics_create(afem_mesh* mesh, afem_comm* comm, const afem_newmark_params* params,
+                               const int32_t* fixed_nodes, int64_t n_fixed, int mem, afem_elastodynamics** out);
+int afem_elastodynamics_set_solver_options(afem_elastodynamics* dyn, const afem_solver_opts* opts);
+int afem_elastodynamics_step(afem_elastodynamics* dyn, afem_solve_stats* stats);
+/* device arrays of 3*n_own_nodes doubles (DoF lid = 3 node + i) */
+int afem_elastodynamics_state(afem_elastodynamics* dyn, double** u, double** v, double** a);
+int afem_elastodynamics_destroy(afem_elastodynamics* dyn);
+
 /* ---------------------------------------------------------------- communicator */
 #define AFEM_UNIQUE_ID_BYTES 128
 /* ncclGetUniqueId on the root rank; the bytes are broadcast by the caller
  * (e.g. torch.distributed) and passed to afem_comm_create on every rank. */
 int afem_comm_unique_id(uint8_t id[AFEM_UNIQUE_ID_BYTES]);
 int afem_comm_create(afem_ctx* ctx, const uint8_t id[AFEM_UNIQUE_ID_BYTES], int nranks, int rank, afem_comm** out);
+/* Host transport: the communicator moves the halo and the dot-product sums
+ * through host memory with the caller's callbacks (the reference's
+ * IParallelMng::allReduce / sendRecv, or MPI, or torch.distributed gloo) --
+ * for hosts where RCCL cannot run (e.g. several ranks on one GPU) and for
+ * tests of the distributed path.  Callbacks return 0 on success.
+ *   allreduce_sum: in-place sum over all ranks of n doubles.
+ *   exchange: for every neighbour i (n_neighbors, in order), send
+ *     send_counts[i] doubles (consecutive in `send`) to neighbor_ranks[i] and
+ *     receive recv_counts[i] doubles (consecutive in `recv`) from it. */
+typedef struct afem_host_transport {
+  void* user;
+  int (*allreduce_sum)(void* user, double* buf, int64_t n);
+  int (*exchange)(void* user, int n_neighbors, const int32_t* neighbor_ranks, const double* send,
+                  const int64_t* send_counts, double* recv, const int64_t* recv_counts);
+} afem_host_transport;
+int afem_comm_create_host(afem_ctx* ctx, int nranks, int rank, const afem_host_transport* transport,
+                          afem_comm** out);
 int afem_comm_destroy(afem_comm* comm);
 /* In-place sum over ranks of n doubles (device pointer) on the context stream. */
 int afem_comm_allreduce_sum(afem_comm* comm, double* dbuf, int64_t n);
@@ -342,7 +386,9 @@ int afem_comm_allreduce_sum(afem_comm* comm, double* dbuf, int64_t n);
 int afem_ls_set_halo(afem_ls* ls, afem_comm* comm, int n_neighbors, const int32_t* neighbor_ranks,
                      const int64_t* send_counts, const int32_t* send_ids, const int64_t* recv_counts,
                      const int32_t* recv_ids);
-/* Halo plan of a structured slab mesh (neighbours rank-1 / rank+1). */
+/* Halo plan of a structured slab mesh (neighbours rank-1 / rank+1); the
+ * linear system may carry NB_DOF = n_rows / n_own_nodes DoFs per node (DoF
+ * lid = node lid * NB_DOF + i, femutils/FemDoFsOnNodes.cc:79-109). */
 int afem_ls_set_halo_structured(afem_ls* ls, afem_comm* comm, afem_mesh* mesh);
 /* Host-only (no GPU needed): the halo plan of a structured slab mesh, i.e.
  * the ghost synchronisation lists FemDoFsOnNodes::computeSynchronizeInfos

@@ -483,3 +483,53 @@ def newmark_elastodynamics(n_nodes, cells, coords, E, nu, rho, dt, n_steps, body
         A = an
         U = Un
     return U, V, A
+
+
+# --------------------------------------------------------------------------
+# extended-precision reference of the P1 Laplacian values (test infrastructure)
+# --------------------------------------------------------------------------
+def assemble_poisson_extended(n_rows, cells, coords, row_ptr, cols):
+    """The assembled P1 Laplacian values in x87 extended precision (numpy
+    longdouble, 64-bit mantissa) from edge vectors: K_ab = (c_a . c_b) /
+    (6 |det|) (tets; triangles (c_a . c_b) / (2 |A2|)), c the cofactors.  The
+    same bilinear form as the reference's element routines, computed ~2^11
+    times more precisely than any double restatement, so that the per-entry
+    error of a double implementation can be measured against it (entries that
+    nearly cancel are ill-conditioned in every double formula).  Returns
+    (values, magnitude) with magnitude = sum over the entry's terms of
+    |c_a||c_b| / (6|det|) (the entry's condition scale)."""
+    ld = np.longdouble
+    cells = np.asarray(cells, dtype=np.int64)
+    X = np.asarray(coords, dtype=np.float64).reshape(-1, 3).astype(ld)
+    nv = cells.shape[1]
+    P = X[cells]  # [nc, nv, 3]
+    if nv == 4:
+        e1, e2, e3 = P[:, 1] - P[:, 0], P[:, 2] - P[:, 0], P[:, 3] - P[:, 0]
+        c1, c2, c3 = np.cross(e2, e3), np.cross(e3, e1), np.cross(e1, e2)
+        c0 = -(c1 + c2 + c3)
+        det = np.abs(np.sum(e1 * c1, axis=1))
+        C = np.stack([c0, c1, c2, c3], 1)
+        scale = 1 / (6 * det)
+    else:
+        e1, e2 = P[:, 1] - P[:, 0], P[:, 2] - P[:, 0]
+        c1 = np.stack([e2[:, 1], -e2[:, 0]], 1)
+        c2 = np.stack([-e1[:, 1], e1[:, 0]], 1)
+        c0 = -(c1 + c2)
+        det = np.abs(e1[:, 0] * e2[:, 1] - e2[:, 0] * e1[:, 1])
+        C = np.stack([c0, c1, c2], 1)
+        scale = 1 / (2 * det)
+    K = np.einsum("cad,cbd->cab", C, C) * scale[:, None, None]
+    M = np.einsum("cad,cbd->cab", np.abs(C), np.abs(C)) * scale[:, None, None]
+    rows_idx = np.repeat(cells[:, :, None], nv, axis=2).ravel()
+    cols_idx = np.repeat(cells[:, None, :], nv, axis=1).ravel()
+    own = rows_idx < n_rows
+    n_cols = int(max(cols.max() if cols.size else 0, cells.max() if cells.size else 0)) + 1
+    keys = rows_idx[own] * n_cols + cols_idx[own]
+    rid = np.repeat(np.arange(n_rows, dtype=np.int64), np.diff(row_ptr))
+    ckeys = rid * n_cols + cols.astype(np.int64)
+    pos = np.searchsorted(ckeys, keys)
+    vals = np.zeros(cols.shape[0], dtype=ld)
+    mag = np.zeros(cols.shape[0], dtype=ld)
+    np.add.at(vals, pos, K.ravel()[own])
+    np.add.at(mag, pos, M.ravel()[own])
+    return vals, mag

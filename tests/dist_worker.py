@@ -1,0 +1,81 @@
+"""One rank of the distributed GPU tests (tests/test_gpu_distributed.py).
+
+Run as a child process per rank: python tests/dist_worker.py <case> <rank> <world> <port> <out.npz>.
+The rank runs the PRODUCT's distributed path on its own z-slab -- libafem's
+halo plan, halo packing/unpacking, distributed Jacobi-PCG and its reductions
+-- with the halo bytes and the dot-product sums moved by the host transport
+(arcanefem_amd.parallel.HostCommunicator over torch.distributed gloo), since
+RCCL does not run several ranks on one GPU.  Results go to out.npz.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# case parameters shared with the test
+POISSON = dict(n=5, nz=8)
+DYN = dict(n=3, nz=5, E=21e5, nu=0.28, rho=1.0, dt=1e-3, f=(0.0, -9.81, 1.0), steps=4)
+
+
+def main():
+    case, rank, world, port, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = port
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import arcanefem_amd as af
+    from arcanefem_amd.parallel import HostCommunicator
+
+    ctx = af.Context(0)
+    comm = HostCommunicator(ctx)
+    res = {}
+    if case == "poisson":
+        n, nz = POISSON["n"], POISSON["nz"]
+        mesh = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=20250220, nranks=world, rank=rank)
+        bsr = af.BSRFormat(mesh, 1).initialize(True)
+        bsr.computeSparsity()
+        ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes, mesh.n_nodes)
+        bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
+        bsr.toLinearSystem(ls)
+        ls.applyDirichletViaPenalty(mesh.bottom_nodes(), 0.5, 1e30)
+        ls.set_halo_structured(comm, mesh)
+        ls.setSolverOptions(rtol=1e-14, max_iter=20000)
+        st = ls.solve()
+        _, _, l2g = mesh.download()
+        res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
+                   converged=int(st["converged"]), rel=st["rel_residual"])
+        # CG iter/s with the halo attached (fixed iterations)
+        ls.setSolverOptions(fixed_iterations=20)
+        ls.solve()
+    elif case == "elastodynamics":
+        from arcanefem_amd.elastodynamics import Elastodynamics3D
+
+        p = DYN
+        mesh = af.Mesh.structured(ctx, 3, p["n"], nz=p["nz"], jitter=0.2, seed=20250220, nranks=world, rank=rank)
+        _, coords, l2g = mesh.download()
+        fixed = np.nonzero(coords[:, 0] < 0.5 / p["n"])[0].astype(np.int32)  # the x = 0 layer, ghosts included
+        sim = Elastodynamics3D(ctx, mesh, p["E"], p["nu"], p["rho"], p["dt"], body_force=p["f"], fixed_nodes=fixed,
+                               rtol=1e-14, comm=comm)
+        its = []
+        for _ in range(p["steps"]):
+            st = sim.step()
+            its.append(st["iterations"])
+            assert st["converged"], st
+        U, V, A = sim.state_host()
+        res = dict(l2g=l2g, n_own=mesh.n_own_nodes, U=U, V=V, A=A, iters=np.array(its))
+        sim.close()
+    else:
+        raise SystemExit(f"unknown case {case}")
+    assert not comm.errors, comm.errors
+    np.savez(out, **res)
+    dist.barrier()
+    comm.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

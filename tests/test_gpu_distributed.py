@@ -1,0 +1,103 @@
+"""GPU: the product's distributed path with more than one rank.
+
+Each rank is a child process (tests/dist_worker.py) with its own context on
+cuda:0, its own z-slab (owned nodes first, one ghost layer) and libafem's halo
+plan; the ranks talk through the host transport (afem_comm_create_host with
+torch.distributed gloo callbacks): only the transport differs from the RCCL
+path, the halo packing / unpacking, the distributed Jacobi-PCG (x0 lifting of
+the constraint rows, stopping reference over the free rows, dot products
+summed over ranks) and the per-step elastodynamics loop are libafem's.
+The gathered results must match the oracle's single-domain direct solve /
+time loop.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+import dist_worker as W
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(case, world, tmp_path):
+    port = str(_free_port())
+    outs = [str(tmp_path / f"{case}_{r}.npz") for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), case, str(r), str(world), port,
+                               outs[r]], stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(world)]
+    logs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        logs.append(out.decode(errors="replace"))
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    return [dict(np.load(o)) for o in outs]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_poisson_solve(world, tmp_path):
+    res = _run("poisson", world, tmp_path)
+    n, nz = W.POISSON["n"], W.POISSON["nz"]
+    g = O.structured_mesh(3, n, nz=nz)
+    grp, gcols = O.sparsity(g["n_local"], g["n_own"], g["cells"])
+    gvals, grhs = O.assemble_poisson(g["n_own"], g["cells"], g["coords"], grp, gcols, 5.5)
+    O.dirichlet_penalty(g["dirichlet"], 0.5, 1e30, grp, gcols, gvals, grhs)
+    xg = np.linalg.solve(O.csr_to_dense(grp, gcols, gvals), grhs)
+    x = np.full(g["n_own"], np.nan)
+    iters = set()
+    for r in res:
+        k = int(r["n_own"])
+        x[r["l2g"][:k]] = r["x"][:k]
+        # ghost values after the solve: the owners' (m_u.synchronize())
+        assert np.array_equal(r["x"][k:], np.zeros(0)) or np.all(np.isfinite(r["x"][k:]))
+        iters.add(int(r["iters"]))
+        assert r["converged"]
+    assert len(iters) == 1  # one iteration sequence (the reductions are global)
+    assert not np.isnan(x).any()
+    assert np.abs(x - xg).max() / np.abs(xg).max() <= 1e-10
+    for r in res:  # synchronised ghosts equal the owners' values
+        k = int(r["n_own"])
+        gid = r["l2g"][k:]
+        assert np.abs(r["x"][k:] - x[gid]).max() <= 1e-15 * np.abs(xg).max()
+
+
+def test_distributed_elastodynamics(tmp_path):
+    p = W.DYN
+    world = 2
+    res = _run("elastodynamics", world, tmp_path)
+    g = O.structured_mesh(3, p["n"], nz=p["nz"])
+    fixed = np.nonzero(g["coords"][:, 0] < 0.5 / p["n"])[0]
+    Uo, Vo, Ao = O.newmark_elastodynamics(g["n_own"], g["cells"], g["coords"], p["E"], p["nu"], p["rho"], p["dt"],
+                                          p["steps"], p["f"], fixed)
+    U = np.full(3 * g["n_own"], np.nan)
+    V = U.copy()
+    A = U.copy()
+    its = []
+    for r in res:
+        k = int(r["n_own"])
+        d = (3 * r["l2g"][:k][:, None] + np.arange(3)[None, :]).ravel()
+        U[d], V[d], A[d] = r["U"], r["V"], r["A"]
+        its.append(r["iters"])
+    assert np.array_equal(its[0], its[1])
+    for gpu, orc in ((U, Uo), (V, Vo), (A, Ao)):
+        assert not np.isnan(gpu).any()
+        assert np.abs(gpu - orc).max() <= 1e-8 * np.abs(orc).max(), np.abs(gpu - orc).max() / np.abs(orc).max()
