@@ -75,6 +75,19 @@ struct Ctx {
   bool own_stream = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> pool;  // AFEM_EVENT_SLOTS, created lazily
+  // side stream for a small kernel that runs beside a large one (fork/join
+  // through two events on the context stream), created lazily
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipStream_t side()
+  {
+    if (!aux) {
+      AFEM_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+      AFEM_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+      AFEM_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    }
+    return aux;
+  }
   int n_cu = 256;
   void set_device() const { AFEM_HIP(hipSetDevice(device)); }
   void sync() const { AFEM_HIP(hipStreamSynchronize(stream)); }
@@ -163,6 +176,7 @@ struct Structure {
   // same shift/swap bits spat[s]) run the uniform-control assembly variant;
   // rec_u / rec_m list the uniform / other slices in processing order.
   DevBuf<uint64_t> spat;
+  DevBuf<uint8_t> uslot;  // uniform list, in list order: the 32 common step bytes of each slice (scalar stream)
   DevBuf<SliceRec> rec_u, rec_m, rec_all;  // uniform / other / every slice, in processing order
   int64_t n_uni = 0, n_mix = 0;
   bool rec_ok = false;                     // offsets fit the 32-bit record fields

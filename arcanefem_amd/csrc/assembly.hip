@@ -570,6 +570,12 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
 //   c_R' = shift ? c_P : -c_Q (old window), c_P' = e_R x e_D, c_Q' = e_D x e_P'
 //   K_row,b = coef (c_row . c_b) / (6 |det|), c_row = -(c_P + c_Q + c_R), det = e_P . c_P
 // Triangles: window (P,Q) + D: shift -> (Q,D), swap -> (P,D).
+// common step bytes of a uniform slice (sparsity.hip k_strip_classify): one
+// s_load_dwordx8 per slice
+struct alignas(32) SlotRec {
+  uint32_t w[8];
+};
+
 template <int MAXC>
 struct StripPre {
   int32_t row;
@@ -613,7 +619,7 @@ __host__ __device__ constexpr int64_t elast_tile_bytes(int64_t u_cap, int64_t w_
 // ≈72 VALU ops per cell).  Same formulas in the same order as the general
 // path, so both give the same bits.
 template <int NV, int MAXC, int MAXW, int UMODE>
-__global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, const SliceRec* __restrict__ recs,
+__global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64_t n_slices, const SliceRec* __restrict__ recs,
                                                           unsigned long long* __restrict__ tickets,
                                                           int u_cap, int w_cap,
                                                           const int32_t* __restrict__ perm,
@@ -625,7 +631,8 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
                                                           const int32_t* __restrict__ snode,
                                                           const double* __restrict__ coords, double s_coef,
                                                           double f_meas, double* __restrict__ vals,
-                                                          double* __restrict__ rhs, int rhs_add)
+                                                          double* __restrict__ rhs, int rhs_add,
+                                                          const SlotRec* __restrict__ uslots)
 {
   constexpr bool UNI = UMODE != 0;  // 1: scalar shift/swap branches, 2: selects on the uniform bit
   // uniform tet instances address coordinates by the local-index stream (no
@@ -671,6 +678,14 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
   SliceRec R0 = recs[p0];
   SliceRec R1 = recs[p1 < r1 ? p1 : p0];
   SliceRec R2 = recs[p2 < r1 ? p2 : p0];
+  // uniform tet instances: the slot stream is common to the slice's rows (32
+  // bytes per list position, scalar loads riding with the records)
+  SlotRec S0{}, S1{}, S2{};
+  if constexpr (ULOC) {
+    S0 = uslots[p0];
+    S1 = uslots[p1 < r1 ? p1 : p0];
+    S2 = uslots[p2 < r1 ? p2 : p0];
+  }
 
   auto load_nid = [&](const SliceRec& R, int32_t(&nid)[4]) {
     const int nu = (int)(R.meta & 0xFFFFu);
@@ -683,9 +698,11 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
     p.dl = pos_dl[q];
     p.rb = pos_rb[q];
     const int nc = (int)((R.meta >> 24) + 15) >> 4;
-    const u32x4* sp = reinterpret_cast<const u32x4*>(strip + (int64_t)R.strip_off * 1024) + lane;
+    if constexpr (!ULOC) {  // uniform instances read the slots from the scalar stream
+      const u32x4* sp = reinterpret_cast<const u32x4*>(strip + (int64_t)R.strip_off * 1024) + lane;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
+      for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
+    }
     if constexpr (ULOC) {  // the steps' local node indices instead of the column-index table
       const u32x4* su = reinterpret_cast<const u32x4*>(strip_u + (int64_t)R.strip_off * 1024) + lane;
 #pragma unroll
@@ -723,6 +740,8 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
   for (;;) {
     const unsigned long long t4 = claim_issue();    // read at the end of this iteration
     const SliceRec R3 = recs[p3 < r1 ? p3 : p0];    // scalar load, used two iterations later
+    SlotRec S3{};
+    if constexpr (ULOC) S3 = uslots[p3 < r1 ? p3 : p0];
     const int nsteps = (int)(R0.meta >> 24);  // uniform over the wave
     const int W = (int)((R0.meta >> 16) & 0xFFu);
     const int64_t u0 = R0.snode_off;
@@ -842,10 +861,15 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
     // j+1 are issued before step j's arithmetic and accumulator adds (no
     // alias hazard: coordinates and indices are not written in the loop).
     auto byte_at = [&](int j) -> uint32_t {
-      const u32x4 w = cur.ch[j >> 4];
-      const int q = (j >> 2) & 3;
-      const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
-      return (wq >> (8 * (j & 3))) & 0xFFu;
+      if constexpr (ULOC) {  // scalar: the slice's common slot stream
+        return (S0.w[(j >> 2) & 7] >> (8 * (j & 3))) & 0xFFu;
+      }
+      else {
+        const u32x4 w = cur.ch[j >> 4];
+        const int q = (j >> 2) & 3;
+        const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
+        return (wq >> (8 * (j & 3))) & 0xFFu;
+      }
     };
     auto uloc_at = [&](int j) -> int {  // local node index of step j (ULOC)
       const u32x4 w = cur.cu[j >> 4];
@@ -1010,6 +1034,11 @@ __global__ __launch_bounds__(64, 2) void k_assemble_strip(int64_t n_slices, cons
     R0 = R1;
     R1 = R2;
     R2 = R3;
+    if constexpr (ULOC) {
+      S0 = S1;
+      S1 = S2;
+      S2 = S3;
+    }
     cur = nxt;
 #pragma unroll
     for (int k = 0; k < 4; ++k) nid1[k] = nid2[k];
@@ -1849,7 +1878,10 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   }();
   if (strips_env && s.strip_ok && s.rec_ok && s.nnz < (int64_t(1) << 32) && s.max_strip_c <= 4 &&
       strip_tile_bytes(dimc, s.max_slice_nodes, s.max_slice_w) <= kTileLdsMax) {
-    const size_t shm_s = (size_t)strip_tile_bytes(dimc, s.max_slice_nodes, s.max_slice_w);
+    const size_t shm_g = (size_t)strip_tile_bytes(dimc, s.max_slice_nodes, s.max_slice_w);
+    // the uniform tet instance needs neither the column-index table nor the
+    // overflow scratch: accumulators + coordinates (<= 13.6 KB: 12 waves per CU)
+    const size_t shm_u = (size_t)(8 * 64 * (int64_t)s.max_slice_w + strip_coord_bytes(dimc, s.max_slice_nodes, s.max_slice_w));
     static std::map<std::pair<const void*, size_t>, int> occ_s;
     // AFEM_ASSEMBLY_UNIFORM=0: every slice through the general variant (diagnostic)
     const char* ue = getenv("AFEM_ASSEMBLY_UNIFORM");  // read per call: the parity test toggles it
@@ -1859,7 +1891,8 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
     const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;
     if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);  // one counter per XCD, 128-B apart, per launch
     AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
-    auto launch_s = [&](const void* fn, auto kern, int64_t n_list, const SliceRec* list, unsigned long long* tk) {
+    auto launch_s = [&](const void* fn, auto kern, int64_t n_list, const SliceRec* list, unsigned long long* tk,
+                        size_t shm_s, hipStream_t stream) {
       auto it = occ_s.find({ fn, shm_s });
       if (it == occ_s.end()) {
         int q = 0;
@@ -1869,29 +1902,45 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       const int per_cu = occ_override() > 0 ? occ_override() : it->second;
       int64_t nblk = (int64_t)ctx.n_cu * per_cu;
       if (nblk > n_list) nblk = n_list < 8 ? 8 : n_list;
-      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, ctx.stream, n_list, list, tk,
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, stream, n_list, list, tk,
                          s.max_slice_nodes, s.max_slice_w, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.strip_u.p,
-                         s.lidx.p, s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add);
+                         s.lidx.p, s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add,
+                         reinterpret_cast<const SlotRec*>(s.uslot.p));
     };
     const SliceRec* list_m = use_uni ? s.rec_m.p : s.rec_all.p;
-#define AFEM_STRIP_K(NV_, C_, W_, U_, N_, L_, T_)                                                                      \
+#define AFEM_STRIP_K(NV_, C_, W_, U_, N_, L_, T_, SHM_, ST_)                                                           \
   launch_s(reinterpret_cast<const void*>(&k_assemble_strip<NV_, C_, W_, U_>), k_assemble_strip<NV_, C_, W_, U_>, N_, \
-           L_, T_)
+           L_, T_, SHM_, ST_)
     const bool small = s.max_strip_c <= 2 && s.max_slice_w <= 16;
     if (nv == 4) {
+      // the few mixed slices (domain edges, irregular rows) run on the side
+      // stream beside the uniform instance (fork / join through events): their
+      // launch and tail hide under the large kernel
+      const bool fork = use_uni && n_mix > 0;
+      hipStream_t ms = ctx.stream;
+      if (fork) {
+        ms = ctx.side();
+        AFEM_HIP(hipEventRecord(ctx.ev_fork, ctx.stream));
+        AFEM_HIP(hipStreamWaitEvent(ms, ctx.ev_fork, 0));
+      }
       if (small) {
-        if (use_uni && umode == 2) AFEM_STRIP_K(4, 2, 16, 2, s.n_uni, s.rec_u.p, s.tickets.p);
-        else if (use_uni) AFEM_STRIP_K(4, 2, 16, 1, s.n_uni, s.rec_u.p, s.tickets.p);
-        if (n_mix > 0) AFEM_STRIP_K(4, 2, 16, 0, n_mix, list_m, s.tickets.p + 128);
+        if (n_mix > 0) AFEM_STRIP_K(4, 2, 16, 0, n_mix, list_m, s.tickets.p + 128, shm_g, ms);
+        if (use_uni && umode == 2) AFEM_STRIP_K(4, 2, 16, 2, s.n_uni, s.rec_u.p, s.tickets.p, shm_u, ctx.stream);
+        else if (use_uni) AFEM_STRIP_K(4, 2, 16, 1, s.n_uni, s.rec_u.p, s.tickets.p, shm_u, ctx.stream);
       }
       else {
-        if (use_uni) AFEM_STRIP_K(4, 4, 32, 1, s.n_uni, s.rec_u.p, s.tickets.p);
-        if (n_mix > 0) AFEM_STRIP_K(4, 4, 32, 0, n_mix, list_m, s.tickets.p + 128);
+        if (n_mix > 0) AFEM_STRIP_K(4, 4, 32, 0, n_mix, list_m, s.tickets.p + 128, shm_g, ms);
+        if (use_uni) AFEM_STRIP_K(4, 4, 32, 1, s.n_uni, s.rec_u.p, s.tickets.p, shm_u, ctx.stream);
+      }
+      AFEM_LAUNCHED();
+      if (fork) {
+        AFEM_HIP(hipEventRecord(ctx.ev_join, ms));
+        AFEM_HIP(hipStreamWaitEvent(ctx.stream, ctx.ev_join, 0));
       }
     }
     else {
-      if (small) AFEM_STRIP_K(3, 2, 16, 0, s.n_slices, s.rec_all.p, s.tickets.p + 128);
-      else AFEM_STRIP_K(3, 4, 32, 0, s.n_slices, s.rec_all.p, s.tickets.p + 128);
+      if (small) AFEM_STRIP_K(3, 2, 16, 0, s.n_slices, s.rec_all.p, s.tickets.p + 128, shm_g, ctx.stream);
+      else AFEM_STRIP_K(3, 4, 32, 0, s.n_slices, s.rec_all.p, s.tickets.p + 128, shm_g, ctx.stream);
     }
 #undef AFEM_STRIP_K
     AFEM_LAUNCHED();

@@ -148,6 +148,12 @@ int afem_ctx_destroy(afem_ctx* ctx)
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
+  if (ctx->aux) {
+    (void)hipStreamSynchronize(ctx->aux);
+    (void)hipStreamDestroy(ctx->aux);
+    (void)hipEventDestroy(ctx->ev_fork);
+    (void)hipEventDestroy(ctx->ev_join);
+  }
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);

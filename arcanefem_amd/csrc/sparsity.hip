@@ -674,17 +674,22 @@ __global__ void k_strip_local(int64_t n_pos, const uint8_t* __restrict__ strip, 
   }
 }
 
-// per slice: does every lane run the same strip topology?  Uniform = all 64
-// rows active, one strip (kinds 2,2 then 0/1 only), the same length, the same
-// shift/swap sequence.  Out: flag (1 = uniform) and the swap bits (bit j = step
-// j is a swap).  One wave per slice.
+// per slice: does every lane run the same strip topology?  Uniform = one
+// strip (kinds 2,2 then 0/1 only), the same length, the same shift/swap
+// sequence and the same step bytes (slots) on every active row, and the same
+// diagonal slot: every interior brick / face tile of a structured mesh, whose
+// rows have the same sorted neighbour pattern.  Out: flag (1 = uniform), the
+// swap bits (bit j = step j is a swap) and the common step bytes (32: the
+// scalar slot stream of the uniform kernel; padding steps carry the diagonal
+// slot).  One wave per slice.
 __global__ __launch_bounds__(64) void k_strip_classify(int64_t n_slices, const int32_t* __restrict__ perm,
                                                        const uint8_t* __restrict__ strip,
                                                        const int64_t* __restrict__ strip_ptr,
                                                        const int32_t* __restrict__ strip_n,
                                                        const int64_t* __restrict__ snode_ptr,
-                                                       const int32_t* __restrict__ slice_w, uint8_t* __restrict__ uflag,
-                                                       uint64_t* __restrict__ spat)
+                                                       const int32_t* __restrict__ slice_w,
+                                                       const uint8_t* __restrict__ dslot, uint8_t* __restrict__ uflag,
+                                                       uint64_t* __restrict__ spat, uint8_t* __restrict__ sslot)
 {
   const int64_t sl = blockIdx.x;
   const int lane = threadIdx.x;
@@ -706,7 +711,17 @@ __global__ __launch_bounds__(64) void k_strip_classify(int64_t n_slices, const i
   const unsigned long long act = __ballot(!idle);
   const int first = act ? __ffsll((long long)act) - 1 : 0;
   const uint64_t p0 = __shfl(pat, first);
-  const bool all = act != 0 && __all(ok && (idle || pat == p0));
+  bool all = act != 0 && __all(ok && (idle || pat == p0));
+  // slot-uniform: the same byte at every step (and the same diagonal slot)
+  const uint32_t ds = dslot[sl * 64 + lane], ds0 = __shfl(ds, first);
+  bool same = idle || ds == ds0;
+  for (int j = 0; j < 32; ++j) {
+    const uint32_t b = j < n ? st[(int64_t)(j >> 4) * 1024 + (j & 15)] : (ds | (3u << 6));
+    const uint32_t b0 = __shfl(b, first);
+    if (!idle && b != b0) same = false;
+    if (lane == 0) sslot[sl * 32 + j] = (uint8_t)b0;
+  }
+  all = all && __all(same) && n <= 32;
   if (lane == 0) {
     uflag[sl] = all ? 1 : 0;
     spat[sl] = all ? p0 : 0;
@@ -987,14 +1002,19 @@ void build_structure(Mesh& m, Structure& s)
       DevBuf<uint8_t> uflag;
       uflag.alloc(s.n_slices);
       s.spat.alloc(s.n_slices);
+      DevBuf<uint8_t> sslot;
+      sslot.alloc(s.n_slices * 32);
       hipLaunchKernelGGL(k_strip_classify, dim3((unsigned)s.n_slices), dim3(64), 0, ctx.stream, s.n_slices, s.perm.p,
-                         s.strip.p, s.strip_ptr.p, s.strip_n.p, s.snode_ptr.p, s.slice_w.p, uflag.p, s.spat.p);
+                         s.strip.p, s.strip_ptr.p, s.strip_n.p, s.snode_ptr.p, s.slice_w.p, s.dslot.p, uflag.p,
+                         s.spat.p, sslot.p);
       AFEM_LAUNCHED();
       const size_t ns = (size_t)s.n_slices;
       std::vector<uint8_t> hu(ns);
       std::vector<int32_t> hw(ns), hn(ns);
       std::vector<int64_t> hl(ns + 1), hs(ns + 1), hsn(ns + 1);
       std::vector<uint64_t> hp(ns);
+      std::vector<uint8_t> hslot(ns * 32);
+      AFEM_HIP(hipMemcpyAsync(hslot.data(), sslot.p, ns * 32, hipMemcpyDeviceToHost, ctx.stream));
       AFEM_HIP(hipMemcpyAsync(hu.data(), uflag.p, ns, hipMemcpyDeviceToHost, ctx.stream));
       AFEM_HIP(hipMemcpyAsync(hw.data(), s.slice_w.p, ns * 4, hipMemcpyDeviceToHost, ctx.stream));
       AFEM_HIP(hipMemcpyAsync(hn.data(), s.strip_n.p, ns * 4, hipMemcpyDeviceToHost, ctx.stream));
@@ -1005,6 +1025,7 @@ void build_structure(Mesh& m, Structure& s)
       ctx.sync();
       s.rec_ok = hl[ns] < (int64_t(1) << 32) && hs[ns] / 1024 < (int64_t(1) << 32) && hsn[ns] < (int64_t(1) << 32);
       std::vector<SliceRec> ru, rm, ra;
+      std::vector<uint8_t> su;  // the uniform list's slot streams, in list order
       for (size_t i = 0; i < ns && s.rec_ok; ++i) {
         SliceRec r{};
         r.sl = (uint32_t)i;
@@ -1016,7 +1037,13 @@ void build_structure(Mesh& m, Structure& s)
         r.meta = (uint32_t)nu | (uint32_t)hw[i] << 16 | (uint32_t)hn[i] << 24;
         r.pat = hp[i];
         ra.push_back(r);
-        (hu[i] && nv == 4 ? ru : rm).push_back(r);
+        if (hu[i] && nv == 4) {
+          ru.push_back(r);
+          su.insert(su.end(), hslot.begin() + 32 * i, hslot.begin() + 32 * (i + 1));
+        }
+        else {
+          rm.push_back(r);
+        }
       }
       s.n_uni = (int64_t)ru.size();
       s.n_mix = (int64_t)rm.size();
@@ -1026,6 +1053,8 @@ void build_structure(Mesh& m, Structure& s)
           AFEM_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(SliceRec), hipMemcpyHostToDevice, ctx.stream));
       };
       upload(s.rec_u, ru);
+      s.uslot.alloc(su.empty() ? 32 : su.size());
+      if (!su.empty()) AFEM_HIP(hipMemcpyAsync(s.uslot.p, su.data(), su.size(), hipMemcpyHostToDevice, ctx.stream));
       upload(s.rec_m, rm);
       upload(s.rec_all, ra);
       if (getenv("AFEM_DEBUG_PATTERNS")) {  // diagnostic: strip patterns of the uniform slices
