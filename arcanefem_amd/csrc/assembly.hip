@@ -558,6 +558,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
   }
 }
 
+
 // ---------------------------------------------------------------- scalar P1, row strips
 // Same slice tiles and software pipeline as k_assemble_p1, but each lane walks
 // its row's strip (sparsity.hip "row strips"): one stream byte per cell gives
@@ -611,6 +612,21 @@ __host__ __device__ constexpr int64_t elast_tile_bytes(int64_t u_cap, int64_t w_
   return 3 * 8 * 64 * w_cap + elast_coord_bytes(u_cap, w_cap) + 2 * 64 * w_cap + 512;
 }
 
+#ifdef AFEM_WAVE_TIMES
+// diagnostic build only (make EXTRA=-DAFEM_WAVE_TIMES OUT=../libafem_wt.so
+// OBJDIR=build_wt; tools/wave_times.py): start / end realtime stamps and the
+// slice count of every workgroup of the uniform strip instance
+__device__ unsigned long long afem_wave_t[3 * 16384];
+extern "C" int afem_debug_wave_times(unsigned long long* out, int n)
+{
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(afem_wave_t), sizeof(unsigned long long) * (size_t)(3 * n));
+}
+#define AFEM_WT(i, v)                                                               \
+  if (UMODE == 1 && lane == 0 && blockIdx.x < 16384) afem_wave_t[3 * blockIdx.x + (i)] = (v)
+#else
+#define AFEM_WT(i, v) (void)0
+#endif
+
 // UNI = true: the slices of `recs` (the uniform list) whose 64 rows share one strip topology
 // (same length, one strip, same shift/swap sequence `spat`: every interior
 // brick of a structured mesh).  The shift/swap decision is then wave-uniform:
@@ -648,12 +664,18 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
   // Dynamic slice claiming, one ticket counter per XCD (workgroups are dealt
   // to the 8 XCDs round-robin): XCD x walks the contiguous x-th eighth of the
   // list, so neighbouring bricks stay in one L2.
-  const int xcd = (int)(blockIdx.x & 7);
-  const int64_t r0 = n_slices * xcd / 8, r1 = n_slices * (xcd + 1) / 8;
+  // Dynamic slice claiming, one ticket counter per XCD (workgroups are dealt
+  // to the 8 XCDs round-robin): XCD x walks the contiguous x-th eighth of the
+  // list, so neighbouring bricks stay in one L2.  (Cross-XCD stealing at the
+  // end of the eighths, tried with a blocking re-claim, broke the scalar
+  // record loads and the register budget of the pipeline; the XCDs finish
+  // within ~5-10% of each other, tools/wave_times.py.)
   // issue: the atomic's result stays in a VGPR; get: readfirstlane (the list
   // position is provably wave-uniform: scalar loads, scalar branches).  In
   // the loop a claim is read one whole slice after it was issued, behind that
   // slice's stores, so the wave never waits on the atomic (or the stores).
+  const int xcd = (int)(blockIdx.x & 7);
+  const int64_t r0 = n_slices * xcd / 8, r1 = n_slices * (xcd + 1) / 8;
   auto claim_issue = [&]() -> unsigned long long {
     unsigned long long t = 0;
     if (lane == 0) t = atomicAdd(tickets + 16 * xcd, 1ull);
@@ -664,12 +686,16 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(t >> 32));
     return r0 + (int64_t)(((uint64_t)hi << 32) | lo);
   };
+#ifdef AFEM_WAVE_TIMES
+  unsigned long long n_done = 0;
+#endif
   // Four-stage software pipeline over the claimed list positions p0..p3:
   // while slice p0 is processed out of LDS, the row data, strip, column
   // indices and node coordinates of p1 are in flight, the node ids of p2
   // (the addresses of its coordinate gather), and the 32-B record of p3 (the
   // addresses of everything else).  Every dependent load thus has a whole
   // slice of work to land; positions past the end re-fetch p0 (never used).
+  AFEM_WT(0, __builtin_amdgcn_s_memrealtime());
   int64_t p0 = claim_get(claim_issue());
   if (p0 >= r1) return;
   int64_t p1 = claim_get(claim_issue());
@@ -1026,6 +1052,9 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
       }
     }
     wave_sync_lds();
+#ifdef AFEM_WAVE_TIMES
+    AFEM_WT(2, ++n_done);
+#endif
     if (p1 >= r1) break;
     p0 = p1;
     p1 = p2;
@@ -1043,6 +1072,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
 #pragma unroll
     for (int k = 0; k < 4; ++k) nid1[k] = nid2[k];
   }
+  AFEM_WT(1, __builtin_amdgcn_s_memrealtime());
 }
 
 // ---------------------------------------------------------------- block-3 elasticity, persistent strips

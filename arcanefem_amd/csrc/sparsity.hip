@@ -674,6 +674,175 @@ __global__ void k_strip_local(int64_t n_pos, const uint8_t* __restrict__ strip, 
   }
 }
 
+// LDS-bank-aware placement of a uniform slice's node list (the strip
+// kernels' coordinate cache, 24 B per node at position q).  A step's
+// coordinate gather is one ds_read2_b64 (x, y: per access four groups of 16
+// lanes over 32 banks; 16 nodes at 6-dword stride are conflict-free when their
+// positions are distinct mod 16) and one ds_read_b64 (z: two groups of 32
+// lanes over 64 banks: distinct mod 32); bank model measured with
+// tools/lds_probe.hip.  In a uniform slice every row takes the same
+// stencil step at step j, so on a structured brick the node read by lane L at
+// step j is "L + d_j" in the brick's lane numbering: a node class
+// c(u) = (L + s_j) mod 32, consistent over every (lane, step) reading u, makes
+// every gather conflict-free.  This pass finds the shifts s_j (the row's own
+// node has shift 0) by propagation over the steps, checks consistency, and
+// places node u at q = c(u) + 32 m (m = rank within its class; at most 8 per
+// class fit the 256 positions, extra nodes fill free positions).  Slices that
+// are not uniform, not consistent or larger than 256 nodes keep their order
+// (identity).  Positions left free repeat the slice's first node.  Every
+// kernel addresses the cache through the remapped local indices, so the
+// values do not change.  One wavefront per slice.
+__global__ __launch_bounds__(64) void k_bank_place(int64_t n_slices, const uint8_t* __restrict__ uflag,
+                                                   const int32_t* __restrict__ perm,
+                                                   const int64_t* __restrict__ snode_ptr,
+                                                   const uint8_t* __restrict__ strip_u,
+                                                   const int64_t* __restrict__ strip_ptr,
+                                                   const int32_t* __restrict__ strip_n,
+                                                   const uint32_t* __restrict__ pos_dl, uint8_t* __restrict__ q_of_u,
+                                                   int32_t* __restrict__ nu_new)
+{
+  __shared__ int cls[256];
+  __shared__ int shift[32];
+  __shared__ int bad;
+  const int lane = threadIdx.x;
+  const int64_t sl = blockIdx.x;
+  if (sl >= n_slices) return;
+  const int nu = (int)(snode_ptr[sl + 1] - snode_ptr[sl]);
+  uint8_t* qo = q_of_u + sl * 256;
+  auto identity = [&]() {
+    for (int u = lane; u < 256; u += 64) qo[u] = (uint8_t)(u < nu ? u : 0);
+    if (lane == 0) nu_new[sl] = nu;
+  };
+  const int n = strip_n[sl];
+  if (!uflag[sl] || nu > 256 || n > 32) {
+    identity();
+    return;
+  }
+  const bool act = perm[sl * 64 + lane] >= 0;
+  const uint8_t* st = strip_u + strip_ptr[sl] + lane * 16;
+  const int own = (int)((pos_dl[sl * 64 + lane] >> 16) & 0xFFu);
+  for (int u = lane; u < 256; u += 64) cls[u] = -1;
+  if (lane < 32) shift[lane] = -1;
+  if (lane == 0) bad = 0;
+  __syncthreads();
+  if (act) cls[own] = lane & 31;
+  __syncthreads();
+  for (int pass = 0; pass < 32; ++pass) {
+    bool progress = false, open = false;
+    for (int j = 0; j < n; ++j) {
+      if (shift[j] >= 0) continue;
+      const int u = st[(j >> 4) * 1024 + (j & 15)];
+      const int c = act ? cls[u] : -1;
+      const unsigned long long b = __ballot(c >= 0);
+      if (!b) {
+        open = true;
+        continue;
+      }
+      const int f = __ffsll((long long)b) - 1;
+      const int sj = (__shfl(c, f) - f) & 31;
+      __syncthreads();
+      if (act) {
+        const int want = (lane + sj) & 31;
+        if (c < 0) cls[u] = want;
+      }
+      if (lane == 0) shift[j] = sj;
+      progress = true;
+      __syncthreads();
+    }
+    if (!open || !progress) break;
+  }
+  __syncthreads();
+  // consistency: every (lane, step) and every row's own node
+  bool ok = !act || cls[own] == (lane & 31);
+  for (int j = 0; j < n; ++j) {
+    const int u = st[(j >> 4) * 1024 + (j & 15)];
+    if (act && (shift[j] < 0 || cls[u] != ((lane + shift[j]) & 31))) ok = false;
+  }
+  if (!ok) atomicOr(&bad, 1);
+  __syncthreads();
+  if (bad) {
+    identity();
+    return;
+  }
+  if (lane == 0) {
+    uint8_t cnt[32];
+    uint32_t taken[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+    for (int c = 0; c < 32; ++c) cnt[c] = 0;
+    int maxq = -1;
+    for (int u = 0; u < nu; ++u) {
+      const int c = cls[u];
+      if (c >= 0 && cnt[c] < 8) {
+        const int q = c + 32 * cnt[c]++;
+        qo[u] = (uint8_t)q;
+        taken[q >> 5] |= 1u << (q & 31);
+        maxq = max(maxq, q);
+        cls[u] = 256;  // placed
+      }
+    }
+    int free_q = 0;
+    for (int u = 0; u < nu; ++u) {
+      if (cls[u] == 256) continue;
+      while (taken[free_q >> 5] >> (free_q & 31) & 1u) ++free_q;
+      qo[u] = (uint8_t)free_q;
+      taken[free_q >> 5] |= 1u << (free_q & 31);
+      maxq = max(maxq, free_q);
+    }
+    for (int u = nu; u < 256; ++u) qo[u] = qo[0];
+    nu_new[sl] = maxq + 1;
+  }
+}
+
+// new node lists (free positions repeat the slice's first node, never read by a lane)
+__global__ __launch_bounds__(64) void k_snode_place(int64_t n_slices, const int64_t* __restrict__ ptr_old,
+                                                    const int32_t* __restrict__ snode_old,
+                                                    const int64_t* __restrict__ ptr_new, int32_t* __restrict__ snode_new,
+                                                    const uint8_t* __restrict__ q_of_u)
+{
+  const int lane = threadIdx.x;
+  const int64_t sl = blockIdx.x;
+  if (sl >= n_slices) return;
+  const int64_t a = ptr_old[sl], nu = ptr_old[sl + 1] - a, b = ptr_new[sl], nn = ptr_new[sl + 1] - b;
+  if (nu > 256) {
+    for (int64_t u = lane; u < nu; u += 64) snode_new[b + u] = snode_old[a + u];
+    return;
+  }
+  const int32_t first = nu > 0 ? snode_old[a] : 0;
+  for (int64_t q = lane; q < nn; q += 64) snode_new[b + q] = first;
+  __syncthreads();
+  for (int64_t u = lane; u < nu; u += 64) snode_new[b + q_of_u[sl * 256 + u]] = snode_old[a + u];
+}
+
+// renumber the local node indices of the strips, the column-index table and the row positions
+__global__ void k_local_place(int64_t n_pos, const int64_t* __restrict__ snode_ptr_old,
+                              const uint8_t* __restrict__ q_of_u, uint8_t* __restrict__ strip_u,
+                              const int64_t* __restrict__ strip_ptr, const int32_t* __restrict__ strip_c,
+                              uint16_t* __restrict__ lidx, const int64_t* __restrict__ lidx_ptr,
+                              const int32_t* __restrict__ slice_w, uint32_t* __restrict__ pos_dl)
+{
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pos) return;
+  const int64_t sl = p >> 6;
+  const int lane = (int)(p & 63);
+  if (snode_ptr_old[sl + 1] - snode_ptr_old[sl] > 256) return;
+  const uint8_t* q = q_of_u + sl * 256;
+  uint8_t* su = strip_u + strip_ptr[sl] + lane * 16;
+  const int steps = 16 * strip_c[sl];
+  for (int j = 0; j < steps; ++j) {
+    uint8_t& b = su[(int64_t)(j >> 4) * 1024 + (j & 15)];
+    b = q[b];
+  }
+  uint16_t* li = lidx + lidx_ptr[sl] + lane;
+  for (int t = 0; t < slice_w[sl]; ++t) li[64 * t] = q[li[64 * t] & 0xFFu];
+  const uint32_t dl = pos_dl[p];
+  pos_dl[p] = (dl & 0xFFFFu) | ((uint32_t)q[(dl >> 16) & 0xFFu] << 16);
+}
+
+__global__ void k_max_i32(int64_t n, const int32_t* __restrict__ v, unsigned long long* __restrict__ out)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicMax(out, (unsigned long long)v[i]);
+}
+
 // per slice: does every lane run the same strip topology?  Uniform = one
 // strip (kinds 2,2 then 0/1 only), the same length, the same shift/swap
 // sequence and the same step bytes (slots) on every active row, and the same
@@ -1008,6 +1177,44 @@ void build_structure(Mesh& m, Structure& s)
                          s.strip.p, s.strip_ptr.p, s.strip_n.p, s.snode_ptr.p, s.slice_w.p, s.dslot.p, uflag.p,
                          s.spat.p, sslot.p);
       AFEM_LAUNCHED();
+      // LDS-bank-aware node placement of the uniform slices (AFEM_BANK_PLACE=0: sorted order, diagnostic)
+      const char* bpe = getenv("AFEM_BANK_PLACE");
+      if (!(bpe && atoi(bpe) == 0) && nv == 4) {
+        DevBuf<uint8_t> q_of_u;
+        q_of_u.alloc(s.n_slices * 256);
+        DevBuf<int32_t> nu_new;
+        nu_new.alloc(s.n_slices);
+        hipLaunchKernelGGL(k_bank_place, dim3((unsigned)s.n_slices), dim3(64), 0, ctx.stream, s.n_slices, uflag.p,
+                           s.perm.p, s.snode_ptr.p, s.strip_u.p, s.strip_ptr.p, s.strip_n.p, s.pos_dl.p, q_of_u.p,
+                           nu_new.p);
+        AFEM_LAUNCHED();
+        DevBuf<int64_t> ptr_new;
+        ptr_new.alloc(s.n_slices + 1);
+        exclusive_scan_i32_to_i64(ctx, nu_new.p, ptr_new.p, s.n_slices);
+        const int64_t n_new = read_i64(ctx, ptr_new.p + s.n_slices);
+        DevBuf<int32_t> snode_new;
+        snode_new.alloc(n_new > 0 ? n_new : 1);
+        hipLaunchKernelGGL(k_snode_place, dim3((unsigned)s.n_slices), dim3(64), 0, ctx.stream, s.n_slices,
+                           s.snode_ptr.p, s.snode.p, ptr_new.p, snode_new.p, q_of_u.p);
+        AFEM_LAUNCHED();
+        hipLaunchKernelGGL(k_local_place, dim3(grid_for(n_pos, 256)), dim3(256), 0, ctx.stream, n_pos, s.snode_ptr.p,
+                           q_of_u.p, s.strip_u.p, s.strip_ptr.p, s.strip_c.p, s.lidx.p, s.lidx_ptr.p, s.slice_w.p,
+                           s.pos_dl.p);
+        AFEM_LAUNCHED();
+        ctx.sync();
+        s.snode = std::move(snode_new);
+        s.snode_ptr = std::move(ptr_new);
+        DevBuf<unsigned long long> mx;
+        mx.alloc(1);
+        AFEM_HIP(hipMemsetAsync(mx.p, 0, mx.bytes(), ctx.stream));
+        hipLaunchKernelGGL(k_max_i32, dim3(grid_for(s.n_slices, 256)), dim3(256), 0, ctx.stream, s.n_slices, nu_new.p,
+                           mx.p);
+        AFEM_LAUNCHED();
+        unsigned long long hm = 0;
+        AFEM_HIP(hipMemcpyAsync(&hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
+        ctx.sync();
+        s.max_slice_nodes = (int)hm;
+      }
       const size_t ns = (size_t)s.n_slices;
       std::vector<uint8_t> hu(ns);
       std::vector<int32_t> hw(ns), hn(ns);
