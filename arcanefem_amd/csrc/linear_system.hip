@@ -246,6 +246,114 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream4(int64_t n_rows, int64
   }
 }
 
+// k_spmv_stream4 with the segment's first kSpmvU groups per lane issued
+// together (all column/value loads, then all gathers): kSpmvU round trips of
+// memory latency overlap instead of running back to back (a 256-row block of
+// 15-non-zero rows is ~4 groups per lane).  Longer segments finish in the
+// k_spmv_stream4 loop.
+constexpr int kSpmvU = 4;
+template <bool DOT>
+__global__ __launch_bounds__(kThreads) void k_spmv_stream4u(int64_t n_rows, int64_t nnz,
+                                                            const int64_t* __restrict__ rows,
+                                                            const int32_t* __restrict__ cols,
+                                                            const double* __restrict__ vals,
+                                                            const double* __restrict__ x, double* __restrict__ y,
+                                                            double* __restrict__ partial)
+{
+
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* prod = reinterpret_cast<double*>(smem);
+  const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t r0 = blk * kThreads;
+  const int64_t r1 = (r0 + kThreads < n_rows) ? r0 + kThreads : n_rows;
+  const int64_t a = rows[r0], b = rows[r1];
+  const int64_t q0 = (a & ~int64_t(3)) + 4 * (int64_t)threadIdx.x;
+  auto load4 = [&](int64_t q, int (&c)[4], double (&v)[4]) {
+    if (q + 4 <= nnz) {
+      const int4 c4 = *reinterpret_cast<const int4*>(cols + q);
+      const double2 v01 = *reinterpret_cast<const double2*>(vals + q);
+      const double2 v23 = *reinterpret_cast<const double2*>(vals + q + 2);
+      c[0] = c4.x;
+      c[1] = c4.y;
+      c[2] = c4.z;
+      c[3] = c4.w;
+      v[0] = v01.x;
+      v[1] = v01.y;
+      v[2] = v23.x;
+      v[3] = v23.y;
+    }
+    else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = q + j < nnz ? cols[q + j] : 0;
+        v[j] = q + j < nnz ? vals[q + j] : 0.0;
+      }
+    }
+  };
+  // products to LDS: a lane's 4 products are contiguous (32 B), so lanes
+  // l, l+8, l+16, l+24 hit the same banks; the t-th store of lane l writes
+  // product (t + l/8) mod 4 instead, which spreads them (conflict-free)
+  const int rot = (int)(threadIdx.x >> 3) & 3;
+  auto put4 = [&](int64_t q, const double (&v)[4], const double (&xv)[4]) {
+    double pr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pr[j] = v[j] * xv[j];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = (t + rot) & 3;
+      const double w = j == 0 ? pr[0] : (j == 1 ? pr[1] : (j == 2 ? pr[2] : pr[3]));
+      if (q + j >= a && q + j < b) prod[q + j - a] = w;
+    }
+  };
+  {
+    int c[kSpmvU][4];
+    double v[kSpmvU][4];
+#pragma unroll
+    for (int u = 0; u < kSpmvU; ++u) {
+      const int64_t q = q0 + (int64_t)u * 4 * kThreads;
+      if (q < b) {
+        load4(q, c[u], v[u]);
+      }
+      else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          c[u][j] = 0;
+          v[u][j] = 0.0;
+        }
+      }
+    }
+    double xv[kSpmvU][4];
+#pragma unroll
+    for (int u = 0; u < kSpmvU; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xv[u][j] = x[c[u][j]];
+#pragma unroll
+    for (int u = 0; u < kSpmvU; ++u) put4(q0 + (int64_t)u * 4 * kThreads, v[u], xv[u]);
+  }
+  for (int64_t q = q0 + (int64_t)kSpmvU * 4 * kThreads; q < b; q += 4 * kThreads) {
+    int c[4];
+    double v[4];
+    load4(q, c, v);
+    double xv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] = x[c[j]];
+    put4(q, v, xv);
+  }
+  __syncthreads();
+  const int64_t r = r0 + threadIdx.x;
+  double d = 0.0;
+  if (r < r1) {
+    double s = 0.0;
+    for (int64_t k = rows[r] - a, e = rows[r + 1] - a; k < e; ++k) s += prod[k];
+    y[r] = s;
+    if (DOT) d = x[r] * s;
+  }
+  if (DOT) {
+    double bs = block_sum(d);
+    if (threadIdx.x == 0) partial[blockIdx.x] = bs;
+  }
+}
+
 // Vector CSR SpMV: a 16-lane group per row, RPG rows per group with all of
 // their loads issued before any use (memory-level parallelism without LDS or
 // barriers).  Lane k of a row loads non-zero k (coalesced: a wave's 4 groups
@@ -575,6 +683,7 @@ __global__ __launch_bounds__(256) void k_residual(int64_t n, const int64_t* __re
 struct SpmvPlan {
   int rpb = 0;          // rows per block (0: row kernel, -1: vector CSR)
   bool wide = false;    // 16-B loads of the segment (aligned bases)
+  bool unroll = false;  // k_spmv_stream4u
   int64_t max_seg = 0;
   int64_t nblocks = 0;
 };
@@ -602,11 +711,12 @@ SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows, const int32_t*
   AFEM_HIP(hipMemcpyAsync(&hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
   ctx.sync();
   pl.nblocks = nb;
-  // AFEM_SPMV=stream (scalar-load stream) / v16 (16 lanes per row): diagnostics
-  static const int mode = [] {
+  // AFEM_SPMV=stream (scalar-load stream) / v16 (16 lanes per row) / s4 (no unrolling): diagnostics
+  const int mode = [] {  // read per plan (tools/cg_probe.py toggles it in one process)
     const char* e = getenv("AFEM_SPMV");
     if (e && std::string(e) == "stream") return 1;
     if (e && std::string(e) == "v16") return 2;
+    if (e && std::string(e) == "s4") return 3;
     return 0;
   }();
   if (mode == 2) {
@@ -616,7 +726,8 @@ SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows, const int32_t*
   else if (hm * 8ull <= 64ull * 1024ull) {
     pl.rpb = kThreads;
     pl.max_seg = (int64_t)hm;
-    pl.wide = mode == 0 && cols && vals && ((uintptr_t)cols & 15) == 0 && ((uintptr_t)vals & 15) == 0;
+    pl.wide = (mode == 0 || mode == 3) && cols && vals && ((uintptr_t)cols & 15) == 0 && ((uintptr_t)vals & 15) == 0;
+    pl.unroll = mode == 0;
   }
   else if (mode == 0 && hm >= 16ull * (unsigned long long)kThreads) {
     // long rows (block-3 elasticity: 45 non-zeros per scalar row): segments do
@@ -637,6 +748,14 @@ void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* ro
     else
       hipLaunchKernelGGL(k_spmv_v16<false>, dim3(nb), dim3(256), 0, ctx.stream, n_rows, rows, cols, vals, x, y,
                          partial);
+  }
+  else if (pl.rpb && pl.wide && pl.unroll) {
+    if (partial)
+      hipLaunchKernelGGL(k_spmv_stream4u<true>, dim3(nb), dim3(kThreads), (size_t)pl.max_seg * 8, ctx.stream, n_rows,
+                         nnz, rows, cols, vals, x, y, partial);
+    else
+      hipLaunchKernelGGL(k_spmv_stream4u<false>, dim3(nb), dim3(kThreads), (size_t)pl.max_seg * 8, ctx.stream, n_rows,
+                         nnz, rows, cols, vals, x, y, partial);
   }
   else if (pl.rpb && pl.wide) {
     if (partial)
