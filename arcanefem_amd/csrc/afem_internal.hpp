@@ -215,10 +215,29 @@ struct Halo {
   DevBuf<int32_t> send_ids, recv_ids;
   DevBuf<double> send_buf, recv_buf;
   int64_t n_send = 0, n_recv = 0;
+  // split exchange (halo_begin / halo_end): the RCCL send/recv run on their
+  // own stream while the context stream computes (created lazily)
+  hipStream_t cs = nullptr;
+  hipEvent_t ev_packed = nullptr, ev_done = nullptr;
+  Halo() = default;
+  Halo(const Halo&) = delete;
+  Halo& operator=(const Halo&) = delete;
+  ~Halo()
+  {
+    if (ev_packed) (void)hipEventDestroy(ev_packed);
+    if (ev_done) (void)hipEventDestroy(ev_done);
+    if (cs) (void)hipStreamDestroy(cs);
+  }
 };
 
 void halo_exchange(Halo& h, Ctx& ctx, double* x);
+// halo_exchange in two halves: begin packs and posts the transfers (RCCL: on
+// the halo's stream, returns at once; host transport: the whole exchange),
+// end makes the context stream wait for them and scatters the ghosts
+void halo_begin(Halo& h, Ctx& ctx, double* x);
+void halo_end(Halo& h, Ctx& ctx, double* x);
 void comm_allreduce(Comm* c, Ctx& ctx, double* d, int64_t n);
+bool comm_is_host(Comm* c);  // host-transport communicator (synchronous exchanges)
 
 // ------------------------------------------------------------------ linear system
 struct LinearSystem {
@@ -246,6 +265,9 @@ struct LinearSystem {
   std::map<int32_t, std::pair<uint8_t, double>> host_elim;
   // solver work
   DevBuf<double> r, z, p, q, dinv, partial, scal;
+  DevBuf<int32_t> blist;  // multi-rank CG: SpMV row blocks, interior ones first
+  int64_t blist_nint = 0;
+  uint64_t blist_key = 0;
   DevBuf<double> dense;  // direct solver: augmented n x (n+1) matrix
   DevBuf<uint8_t> cons;  // constraint-row flags of the stopping test
   double* pinned = nullptr;

@@ -120,6 +120,7 @@ void comm_allreduce(Comm* c, Ctx& ctx, double* d, int64_t n)
 }
 
 int comm_nranks(Comm* c) { return c ? c->nranks : 1; }
+bool comm_is_host(Comm* c) { return c && c->host; }
 int comm_rank(Comm* c) { return c ? c->rank : 0; }
 
 void halo_setup(Halo& h, Ctx& ctx, Comm* comm, int n_nbr, const int32_t* nbr, const int64_t* send_cnt,
@@ -146,6 +147,67 @@ void halo_setup(Halo& h, Ctx& ctx, Comm* comm, int n_nbr, const int32_t* nbr, co
   if (h.n_recv)
     AFEM_HIP(hipMemcpyAsync(h.recv_ids.p, recv_ids, h.recv_ids.bytes(), hipMemcpyHostToDevice, ctx.stream));
   ctx.sync();
+}
+
+namespace {
+// the RCCL send/recv of the packed buffers on `st`; the group is always
+// closed, even after a failed send/recv: an open group would swallow every
+// later collective on the communicator (the CG all-reduces) and hang; the
+// first error is reported after ncclGroupEnd
+void post_sendrecv(Halo& h, hipStream_t st)
+{
+  AFEM_NCCL(ncclGroupStart());
+  ncclResult_t first = ncclSuccess;
+  const char* what = "";
+  for (size_t i = 0; i < h.nbr.size() && first == ncclSuccess; ++i) {
+    if (h.send_cnt[i]) {
+      first = ncclSend(h.send_buf.p + h.send_off[i], (size_t)h.send_cnt[i], ncclDouble, h.nbr[i], h.comm->comm, st);
+      what = "ncclSend";
+    }
+    if (first == ncclSuccess && h.recv_cnt[i]) {
+      first = ncclRecv(h.recv_buf.p + h.recv_off[i], (size_t)h.recv_cnt[i], ncclDouble, h.nbr[i], h.comm->comm, st);
+      what = "ncclRecv";
+    }
+  }
+  const ncclResult_t end = ncclGroupEnd();
+  if (first != ncclSuccess)
+    throw Error(AFEM_ERR_COMM, std::string("halo exchange: ") + what + " failed: " + ncclGetErrorString(first));
+  if (end != ncclSuccess) throw Error(AFEM_ERR_COMM, std::string("ncclGroupEnd failed: ") + ncclGetErrorString(end));
+}
+}  // namespace
+
+void halo_begin(Halo& h, Ctx& ctx, double* x)
+{
+  if (!h.comm || h.comm->nranks == 1 || h.nbr.empty()) return;
+  if (h.comm->host) {  // host transport: synchronous anyway
+    halo_exchange(h, ctx, x);
+    return;
+  }
+  if (!h.cs) {
+    AFEM_HIP(hipStreamCreateWithFlags(&h.cs, hipStreamNonBlocking));
+    AFEM_HIP(hipEventCreateWithFlags(&h.ev_packed, hipEventDisableTiming));
+    AFEM_HIP(hipEventCreateWithFlags(&h.ev_done, hipEventDisableTiming));
+  }
+  if (h.n_send) {
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(h.n_send, 256)), dim3(256), 0, ctx.stream, h.n_send, h.send_ids.p, x,
+                       h.send_buf.p);
+    AFEM_LAUNCHED();
+  }
+  AFEM_HIP(hipEventRecord(h.ev_packed, ctx.stream));
+  AFEM_HIP(hipStreamWaitEvent(h.cs, h.ev_packed, 0));
+  post_sendrecv(h, h.cs);
+  AFEM_HIP(hipEventRecord(h.ev_done, h.cs));
+}
+
+void halo_end(Halo& h, Ctx& ctx, double* x)
+{
+  if (!h.comm || h.comm->nranks == 1 || h.nbr.empty() || h.comm->host) return;
+  AFEM_HIP(hipStreamWaitEvent(ctx.stream, h.ev_done, 0));
+  if (h.n_recv) {
+    hipLaunchKernelGGL(k_scatter, dim3(grid_for(h.n_recv, 256)), dim3(256), 0, ctx.stream, h.n_recv, h.recv_ids.p,
+                       h.recv_buf.p, x);
+    AFEM_LAUNCHED();
+  }
 }
 
 void halo_exchange(Halo& h, Ctx& ctx, double* x)
@@ -177,28 +239,7 @@ void halo_exchange(Halo& h, Ctx& ctx, double* x)
     ctx.sync();
     return;
   }
-  // the group is always closed, even after a failed send/recv: an open group
-  // would swallow every later collective on the communicator (the CG
-  // all-reduces) and hang; the first error is reported after ncclGroupEnd
-  AFEM_NCCL(ncclGroupStart());
-  ncclResult_t first = ncclSuccess;
-  const char* what = "";
-  for (size_t i = 0; i < h.nbr.size() && first == ncclSuccess; ++i) {
-    if (h.send_cnt[i]) {
-      first = ncclSend(h.send_buf.p + h.send_off[i], (size_t)h.send_cnt[i], ncclDouble, h.nbr[i], h.comm->comm,
-                       ctx.stream);
-      what = "ncclSend";
-    }
-    if (first == ncclSuccess && h.recv_cnt[i]) {
-      first = ncclRecv(h.recv_buf.p + h.recv_off[i], (size_t)h.recv_cnt[i], ncclDouble, h.nbr[i], h.comm->comm,
-                       ctx.stream);
-      what = "ncclRecv";
-    }
-  }
-  const ncclResult_t end = ncclGroupEnd();
-  if (first != ncclSuccess)
-    throw Error(AFEM_ERR_COMM, std::string("halo exchange: ") + what + " failed: " + ncclGetErrorString(first));
-  if (end != ncclSuccess) throw Error(AFEM_ERR_COMM, std::string("ncclGroupEnd failed: ") + ncclGetErrorString(end));
+  post_sendrecv(h, ctx.stream);
   if (h.n_recv) {
     hipLaunchKernelGGL(k_scatter, dim3(grid_for(h.n_recv, 256)), dim3(256), 0, ctx.stream, h.n_recv, h.recv_ids.p,
                        h.recv_buf.p, x);

@@ -258,12 +258,13 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream4u(int64_t n_rows, int6
                                                             const int32_t* __restrict__ cols,
                                                             const double* __restrict__ vals,
                                                             const double* __restrict__ x, double* __restrict__ y,
-                                                            double* __restrict__ partial)
+                                                            double* __restrict__ partial,
+                                                            const int32_t* __restrict__ blist = nullptr)
 {
-
   extern __shared__ __align__(16) unsigned char smem[];
   double* prod = reinterpret_cast<double*>(smem);
-  const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+  // blist: the row blocks of this launch (the CG's interior / halo-boundary split)
+  const int64_t blk = blist ? (int64_t)blist[blockIdx.x] : xcd_swizzle(blockIdx.x, gridDim.x);
   const int64_t r0 = blk * kThreads;
   const int64_t r1 = (r0 + kThreads < n_rows) ? r0 + kThreads : n_rows;
   const int64_t a = rows[r0], b = rows[r1];
@@ -680,6 +681,19 @@ __global__ __launch_bounds__(256) void k_residual(int64_t n, const int64_t* __re
 }
 
 // ---------------------------------------------------------------- helpers
+// 1 if a row block reads a ghost column (col >= n_rows): its SpMV must wait
+// for the halo exchange
+__global__ __launch_bounds__(256) void k_block_ghost(int64_t n_rows, int rpb, const int64_t* __restrict__ rows,
+                                                     const int32_t* __restrict__ cols, uint8_t* __restrict__ flag)
+{
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < n_rows ? r0 + rpb : n_rows;
+  int g = 0;
+  for (int64_t k = rows[r0] + threadIdx.x; k < rows[r1]; k += blockDim.x) g |= cols[k] >= n_rows ? 1 : 0;
+  g = __syncthreads_or(g);
+  if (threadIdx.x == 0) flag[blockIdx.x] = (uint8_t)g;
+}
+
 struct SpmvPlan {
   int rpb = 0;          // rows per block (0: row kernel, -1: vector CSR)
   bool wide = false;    // 16-B loads of the segment (aligned bases)
@@ -1021,10 +1035,67 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   double rel = rz0 > 0 ? std::sqrt(std::fabs(ls.pinned[0] / rz0)) : 0.0;
   int it = 0;
   bool converged = fixed ? false : (ls.pinned[0] == 0.0 || rel <= o.rtol);
+  // multi-rank: the row blocks that read no ghost column run while the halo
+  // of p is in flight (RCCL on the halo's stream), the rest after it lands
+  // (host transport: the exchange completes in halo_begin; same split, so the
+  // multi-rank GPU tests cover it)
+  const bool overlap = multi && pl.rpb > 0 && pl.wide && pl.unroll;
+  int64_t n_int = 0;
+  if (overlap) {
+    const uint64_t key = (uint64_t)(uintptr_t)ls.csr_rows ^ ((uint64_t)(uintptr_t)ls.csr_cols << 1) ^
+                         ((uint64_t)n << 40) ^ (uint64_t)ls.csr_nnz;
+    if (ls.blist_key != key) {
+      DevBuf<uint8_t> fl;
+      fl.alloc(pl.nblocks);
+      hipLaunchKernelGGL(k_block_ghost, dim3((unsigned)pl.nblocks), dim3(256), 0, ctx.stream, n, kThreads,
+                         ls.csr_rows, ls.csr_cols, fl.p);
+      AFEM_LAUNCHED();
+      std::vector<uint8_t> hf(pl.nblocks);
+      AFEM_HIP(hipMemcpyAsync(hf.data(), fl.p, pl.nblocks, hipMemcpyDeviceToHost, ctx.stream));
+      ctx.sync();
+      std::vector<int32_t> in, bd;
+      for (int64_t b = 0; b < pl.nblocks; ++b) (hf[b] ? bd : in).push_back((int32_t)b);
+      // launch position i of a list runs on XCD i % 8: deal each list's
+      // contiguous eighths to the XCDs (neighbouring blocks share one L2)
+      std::vector<int32_t> lst;
+      for (auto* v : { &in, &bd }) {
+        const int64_t m = (int64_t)v->size();
+        std::vector<int32_t> sw(m);
+        for (int64_t i = 0; i < m; ++i) {
+          const int64_t q = m >> 3, rem = m & 7, x = i & 7, j = i >> 3;
+          sw[i] = (*v)[x * q + (x < rem ? x : rem) + j];
+        }
+        lst.insert(lst.end(), sw.begin(), sw.end());
+      }
+      ls.blist.alloc(lst.size() ? lst.size() : 1);
+      if (!lst.empty())
+        AFEM_HIP(hipMemcpyAsync(ls.blist.p, lst.data(), lst.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+      ls.blist_nint = (int64_t)in.size();
+      ls.blist_key = key;
+    }
+    n_int = ls.blist_nint;
+  }
   while (!converged && it < max_it) {
     const int par = it & 1;
-    if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
-    launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p, ls.csr_nnz);
+    if (overlap) {
+      const int64_t n_bd = pl.nblocks - n_int;
+      halo_begin(*ls.halo, ctx, ls.p.p);
+      if (n_int > 0)
+        hipLaunchKernelGGL(k_spmv_stream4u<true>, dim3((unsigned)n_int), dim3(kThreads), (size_t)pl.max_seg * 8,
+                           ctx.stream, n, ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p,
+                           ls.partial.p, ls.blist.p);
+      halo_end(*ls.halo, ctx, ls.p.p);
+      if (n_bd > 0)
+        hipLaunchKernelGGL(k_spmv_stream4u<true>, dim3((unsigned)n_bd), dim3(kThreads), (size_t)pl.max_seg * 8,
+                           ctx.stream, n, ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p,
+                           ls.partial.p + n_int, ls.blist.p + n_int);
+      AFEM_LAUNCHED();
+    }
+    else {
+      if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
+      launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p, ls.csr_nnz);
+    }
+
     reduce_to(ctx, ls.partial.p, pl.nblocks, scal + 2);
     if (comm) comm_allreduce(comm, ctx, scal + 2, 1);
     hipLaunchKernelGGL(k_cg_update, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p, ls.r.p,
