@@ -39,6 +39,11 @@ class MeshInfo(ctypes.Structure):
                 ("n_own_nodes", ctypes.c_int64), ("n_cells", ctypes.c_int64)]
 
 
+class SubdomainInfo(ctypes.Structure):
+    _fields_ = [("n_own_nodes", ctypes.c_int64), ("n_nodes", ctypes.c_int64), ("n_cells", ctypes.c_int64),
+                ("n_neighbors", ctypes.c_int), ("n_send", ctypes.c_int64), ("n_recv", ctypes.c_int64)]
+
+
 class CsrView(ctypes.Structure):
     _fields_ = [("n_block_rows", ctypes.c_int64), ("n_block_cols", ctypes.c_int64), ("nnz_blocks", ctypes.c_int64),
                 ("block_size", ctypes.c_int32), ("ordered_per_block", ctypes.c_int32), ("rows", ctypes.c_void_p),
@@ -104,6 +109,9 @@ SIGNATURES = {
     "afem_mesh_create": [P, INT, INT, I64, I64, I64, P, P, INT, PP],
     "afem_mesh_create_structured": [P, INT, INT, INT, D, U64, INT, INT, PP],
     "afem_mesh_get_info": [P, ctypes.POINTER(MeshInfo)],
+    "afem_partition_rcb": [INT, I64, P, INT, P],
+    "afem_subdomain_plan": [INT, I64, I64, P, P, INT, INT, ctypes.POINTER(SubdomainInfo), P, P, P, P, P, P, P],
+    "afem_mesh_create_subdomain": [P, INT, INT, I64, I64, P, P, P, INT, INT, PP],
     "afem_mesh_download": [P, P, P, P],
     "afem_mesh_structured_bottom_nodes": [P, P, ctypes.POINTER(I64)],
     "afem_mesh_destroy": [P],
@@ -161,6 +169,7 @@ SIGNATURES = {
     "afem_comm_allreduce_sum": [P, P, I64],
     "afem_ls_set_halo": [P, P, INT, P, P, P, P, P],
     "afem_ls_set_halo_structured": [P, P, P],
+    "afem_ls_set_halo_mesh": [P, P, P],
     "afem_structured_halo_plan": [INT, INT, INT, INT, INT, ctypes.POINTER(INT), P, P, P, P, P],
     "afem_ls_synchronize": [P, P],
 }

@@ -123,6 +123,39 @@ class Context:
             pass
 
 
+def partition_rcb(dim: int, coords: np.ndarray, n_parts: int) -> np.ndarray:
+    """Node partition by recursive coordinate bisection (afem_partition_rcb,
+    host C++): the partitioner Arcane runs before the FEM module."""
+    coords = np.ascontiguousarray(coords, dtype=np.float64).reshape(-1, 3)
+    part = np.empty(coords.shape[0], dtype=np.int32)
+    call("afem_partition_rcb", dim, coords.shape[0], _ptr(coords), n_parts, _ptr(part))
+    return part
+
+
+def subdomain_plan(cells: np.ndarray, node_part: np.ndarray, nranks: int, rank: int) -> dict:
+    """Host-side subdomain plan (afem_subdomain_plan): local_to_global (owned
+    then ghost nodes), cells (global ids of the local cells), neighbors and the
+    send / recv lists (local node ids, split per neighbour)."""
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    part = np.ascontiguousarray(node_part, dtype=np.int32)
+    info = C.SubdomainInfo()
+    args = (cells.shape[1], part.shape[0], cells.shape[0], _ptr(cells), _ptr(part), nranks, rank, ctypes.byref(info))
+    call("afem_subdomain_plan", *args, None, None, None, None, None, None, None)
+    l2g = np.empty(info.n_nodes, dtype=np.int64)
+    lc = np.empty(info.n_cells, dtype=np.int64)
+    nbr = np.empty(info.n_neighbors, dtype=np.int32)
+    sc = np.empty(info.n_neighbors, dtype=np.int64)
+    rc = np.empty(info.n_neighbors, dtype=np.int64)
+    si = np.empty(info.n_send, dtype=np.int32)
+    ri = np.empty(info.n_recv, dtype=np.int32)
+    call("afem_subdomain_plan", *args, _ptr(l2g), _ptr(lc), _ptr(nbr), _ptr(sc), _ptr(si), _ptr(rc), _ptr(ri))
+    so = np.concatenate([[0], np.cumsum(sc)]).astype(np.int64)
+    ro = np.concatenate([[0], np.cumsum(rc)]).astype(np.int64)
+    return dict(n_own=int(info.n_own_nodes), local_to_global=l2g, cells=lc, neighbors=nbr,
+                send={int(nbr[i]): si[so[i]:so[i + 1]] for i in range(len(nbr))},
+                recv={int(nbr[i]): ri[ro[i]:ro[i + 1]] for i in range(len(nbr))})
+
+
 class Mesh:
     """Device-resident P1 mesh: owned nodes [0, n_own) first, then ghosts."""
 
@@ -153,6 +186,21 @@ class Mesh:
         h = ctypes.c_void_p()
         call("afem_mesh_create_structured", ctx.h, dim, n, 0 if nz is None else nz, jitter, seed, nranks, rank,
              ctypes.byref(h))
+        return cls(ctx, h)
+
+    @classmethod
+    def subdomain(cls, ctx: Context, dim: int, cells: np.ndarray, coords: np.ndarray, node_part: np.ndarray,
+                  nranks: int, rank: int):
+        """The ghosted subdomain of `rank` of a global mesh under a node
+        partition (afem_mesh_create_subdomain): owned nodes first, then one
+        layer of ghosts; carries its halo plan (DoFLinearSystem.set_halo_mesh)
+        and its local-to-global node ids (download())."""
+        cells = np.ascontiguousarray(cells, dtype=np.int32)
+        coords = np.ascontiguousarray(coords, dtype=np.float64).reshape(-1, 3)
+        part = np.ascontiguousarray(node_part, dtype=np.int32)
+        h = ctypes.c_void_p()
+        call("afem_mesh_create_subdomain", ctx.h, dim, cells.shape[1], coords.shape[0], cells.shape[0], _ptr(cells),
+             _ptr(coords), _ptr(part), nranks, rank, ctypes.byref(h))
         return cls(ctx, h)
 
     def download(self):
@@ -423,6 +471,10 @@ class DoFLinearSystem:
 
     def set_halo_structured(self, comm, mesh: Mesh):
         call("afem_ls_set_halo_structured", self.impl, comm.h, mesh.h)
+
+    def set_halo_mesh(self, comm, mesh: Mesh):
+        """Halo plan of a structured slab or a partitioned subdomain (NB_DOF-aware)."""
+        call("afem_ls_set_halo_mesh", self.impl, comm.h, mesh.h)
 
     def synchronize(self, x_dptr: int):
         call("afem_ls_synchronize", self.impl, ctypes.c_void_p(x_dptr))

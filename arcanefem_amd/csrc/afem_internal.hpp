@@ -104,6 +104,24 @@ struct StructuredInfo {
   uint64_t seed = 0;
 };
 
+// Subdomain of a partitioned general mesh (partition.cpp): local numbering
+// (owned nodes first, then ghosts; l2g = global node ids), local cells
+// (global ids) and their local connectivity, halo lists per neighbour rank
+// (local node ids; send = owned nodes, receive = ghosts).
+struct SubdomainPlan {
+  bool valid = false;
+  int nranks = 1, rank = 0;
+  int64_t n_own = 0;
+  std::vector<int64_t> l2g, cells;
+  std::vector<int32_t> cell_node;
+  std::vector<int> nbr;
+  std::vector<int64_t> send_cnt, recv_cnt;
+  std::vector<int32_t> send_ids, recv_ids;
+};
+void partition_rcb(int dim, int64_t n, const double* xyz, int nparts, int32_t* part);
+void subdomain_plan(int nv, int64_t n_nodes, int64_t n_cells, const int32_t* cell_node, const int32_t* part,
+                    int nranks, int rank, SubdomainPlan& P);
+
 struct Mesh {
   Ctx* ctx = nullptr;
   int dim = 3;
@@ -112,6 +130,7 @@ struct Mesh {
   DevBuf<int32_t> cell_node;  // [n_cells*nv]
   DevBuf<double> coords;      // [n_nodes*3]  AoS x,y,z (VariableNodeReal3 layout)
   StructuredInfo st;
+  SubdomainPlan part;  // meshes from afem_mesh_create_subdomain
 };
 
 // ------------------------------------------------------------------ sparsity

@@ -315,6 +315,78 @@ int afem_mesh_create_structured(afem_ctx* ctx, int dim, int n, int nz, double ji
   API_END
 }
 
+int afem_partition_rcb(int dim, int64_t n_nodes, const double* coords, int n_parts, int32_t* node_part)
+{
+  API_BEGIN
+  AFEM_REQUIRE(n_nodes >= 0, AFEM_ERR_ARG, "bad node count");
+  if (n_nodes) {
+    NOT_NULL(coords);
+    NOT_NULL(node_part);
+  }
+  partition_rcb(dim, n_nodes, coords, n_parts, node_part);
+  API_END
+}
+
+int afem_subdomain_plan(int nv, int64_t n_nodes, int64_t n_cells, const int32_t* cell_node, const int32_t* node_part,
+                        int nranks, int rank, afem_subdomain_info* info, int64_t* local_to_global, int64_t* cells,
+                        int32_t* neighbor_ranks, int64_t* send_counts, int32_t* send_ids, int64_t* recv_counts,
+                        int32_t* recv_ids)
+{
+  API_BEGIN
+  NOT_NULL(info);
+  AFEM_REQUIRE(nv >= 2 && n_nodes >= 0 && n_cells >= 0, AFEM_ERR_ARG, "bad mesh sizes");
+  if (n_cells) NOT_NULL(cell_node);
+  if (n_nodes) NOT_NULL(node_part);
+  SubdomainPlan P;
+  subdomain_plan(nv, n_nodes, n_cells, cell_node, node_part, nranks, rank, P);
+  info->n_own_nodes = P.n_own;
+  info->n_nodes = (int64_t)P.l2g.size();
+  info->n_cells = (int64_t)P.cells.size();
+  info->n_neighbors = (int)P.nbr.size();
+  info->n_send = (int64_t)P.send_ids.size();
+  info->n_recv = (int64_t)P.recv_ids.size();
+  if (local_to_global) std::copy(P.l2g.begin(), P.l2g.end(), local_to_global);
+  if (cells) std::copy(P.cells.begin(), P.cells.end(), cells);
+  if (neighbor_ranks) std::copy(P.nbr.begin(), P.nbr.end(), neighbor_ranks);
+  if (send_counts) std::copy(P.send_cnt.begin(), P.send_cnt.end(), send_counts);
+  if (recv_counts) std::copy(P.recv_cnt.begin(), P.recv_cnt.end(), recv_counts);
+  if (send_ids) std::copy(P.send_ids.begin(), P.send_ids.end(), send_ids);
+  if (recv_ids) std::copy(P.recv_ids.begin(), P.recv_ids.end(), recv_ids);
+  API_END
+}
+
+int afem_mesh_create_subdomain(afem_ctx* ctx, int dim, int nv, int64_t n_nodes, int64_t n_cells,
+                               const int32_t* cell_node, const double* coords, const int32_t* node_part, int nranks,
+                               int rank, afem_mesh** out)
+{
+  API_BEGIN
+  NOT_NULL(ctx);
+  NOT_NULL(out);
+  *out = nullptr;
+  AFEM_REQUIRE(dim == 2 || dim == 3, AFEM_ERR_ARG, "mesh dimension must be 2 or 3");
+  AFEM_REQUIRE(nv == dim + 1, AFEM_ERR_NOT_IMPL, "only P1 simplices (TRIA3 in 2D, TETRA4 in 3D) are supported");
+  AFEM_REQUIRE(n_nodes >= 0 && n_cells >= 0, AFEM_ERR_ARG, "bad mesh sizes");
+  if (n_cells) NOT_NULL(cell_node);
+  if (n_nodes) {
+    NOT_NULL(coords);
+    NOT_NULL(node_part);
+  }
+  SubdomainPlan P;
+  subdomain_plan(nv, n_nodes, n_cells, cell_node, node_part, nranks, rank, P);
+  std::vector<double> xyz(P.l2g.size() * 3);
+  for (size_t l = 0; l < P.l2g.size(); ++l)
+    for (int d = 0; d < 3; ++d) xyz[3 * l + d] = coords[3 * P.l2g[l] + d];
+  afem_mesh* m = nullptr;
+  const int rc = afem_mesh_create(ctx, dim, nv, (int64_t)P.l2g.size(), P.n_own, (int64_t)P.cells.size(),
+                                  P.cell_node.data(), xyz.data(), AFEM_MEM_HOST, &m);
+  if (rc != AFEM_OK) return rc;
+  P.cell_node.clear();
+  P.cell_node.shrink_to_fit();
+  m->part = std::move(P);
+  *out = m;
+  API_END
+}
+
 int afem_mesh_get_info(const afem_mesh* m, afem_mesh_info* info)
 {
   API_BEGIN
@@ -1160,14 +1232,26 @@ int afem_ls_set_halo_structured(afem_ls* ls, afem_comm* comm, afem_mesh* mesh)
   NOT_NULL(ls);
   NOT_NULL(comm);
   NOT_NULL(mesh);
-  AFEM_REQUIRE(mesh->st.valid, AFEM_ERR_ARG, "mesh is not a structured slab mesh");
-  const StructuredInfo& st = mesh->st;
-  AFEM_REQUIRE(st.nranks == comm_nranks(comm->c) && st.rank == comm_rank(comm->c), AFEM_ERR_ARG,
-               "mesh slab rank/nranks differ from the communicator");
   std::vector<int> nb;
   std::vector<int64_t> sc, rc;
   std::vector<int32_t> si, ri;
-  structured_halo_lists(st.dim, st.n, st.nz, st.nranks, st.rank, nb, sc, rc, si, ri);
+  if (mesh->part.valid) {  // afem_mesh_create_subdomain
+    const SubdomainPlan& P = mesh->part;
+    AFEM_REQUIRE(P.nranks == comm_nranks(comm->c) && P.rank == comm_rank(comm->c), AFEM_ERR_ARG,
+                 "subdomain rank/nranks differ from the communicator");
+    nb = P.nbr;
+    sc = P.send_cnt;
+    rc = P.recv_cnt;
+    si = P.send_ids;
+    ri = P.recv_ids;
+  }
+  else {
+    AFEM_REQUIRE(mesh->st.valid, AFEM_ERR_ARG, "mesh is neither a structured slab nor a partitioned subdomain");
+    const StructuredInfo& st = mesh->st;
+    AFEM_REQUIRE(st.nranks == comm_nranks(comm->c) && st.rank == comm_rank(comm->c), AFEM_ERR_ARG,
+                 "mesh slab rank/nranks differ from the communicator");
+    structured_halo_lists(st.dim, st.n, st.nz, st.nranks, st.rank, nb, sc, rc, si, ri);
+  }
   std::vector<int32_t> nb32(nb.begin(), nb.end());
   AFEM_REQUIRE(mesh->n_own > 0 && ls->n_rows % mesh->n_own == 0, AFEM_ERR_ARG,
                "linear system rows are not a multiple of the mesh's owned nodes");
@@ -1179,6 +1263,11 @@ int afem_ls_set_halo_structured(afem_ls* ls, afem_comm* comm, afem_mesh* mesh)
   ls->halo.reset(new Halo());
   halo_setup(*ls->halo, *ls->ctx, comm->c, (int)nb.size(), nb32.data(), sc.data(), si.data(), rc.data(), ri.data());
   API_END
+}
+
+int afem_ls_set_halo_mesh(afem_ls* ls, afem_comm* comm, afem_mesh* mesh)
+{
+  return afem_ls_set_halo_structured(ls, comm, mesh);
 }
 
 int afem_ls_synchronize(afem_ls* ls, double* x)

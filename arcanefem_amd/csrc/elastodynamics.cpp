@@ -24,13 +24,22 @@ namespace {
 void halo_for(LinearSystem& ls, Comm* comm, Mesh& m)
 {
   if (!comm || comm_nranks(comm) == 1) return;
-  AFEM_REQUIRE(m.st.valid, AFEM_ERR_NOT_IMPL,
-               "distributed elastodynamics: the halo plan is built for structured slab meshes "
-               "(afem_ls_set_halo for others)");
   std::vector<int> nb;
   std::vector<int64_t> sc, rc;
   std::vector<int32_t> si, ri;
-  structured_halo_lists(m.st.dim, m.st.n, m.st.nz, m.st.nranks, m.st.rank, nb, sc, rc, si, ri);
+  if (m.part.valid) {  // partitioned general mesh (afem_mesh_create_subdomain)
+    nb = m.part.nbr;
+    sc = m.part.send_cnt;
+    rc = m.part.recv_cnt;
+    si = m.part.send_ids;
+    ri = m.part.recv_ids;
+  }
+  else {
+    AFEM_REQUIRE(m.st.valid, AFEM_ERR_NOT_IMPL,
+                 "distributed elastodynamics: the mesh carries no halo plan (structured slab or "
+                 "afem_mesh_create_subdomain)");
+    structured_halo_lists(m.st.dim, m.st.n, m.st.nz, m.st.nranks, m.st.rank, nb, sc, rc, si, ri);
+  }
   expand_dof_lists(3, sc, rc, si, ri);
   std::vector<int32_t> nb32(nb.begin(), nb.end());
   ls.halo.reset(new Halo());
@@ -71,9 +80,11 @@ Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* pr
                  "elastodynamics: bad material or time step");
     AFEM_REQUIRE(n_fixed == 0 || fixed_nodes, AFEM_ERR_ARG, "fixed_nodes is NULL");
     if (comm)
-      AFEM_REQUIRE(comm_nranks(comm) == 1 || (mesh->st.valid && mesh->st.nranks == comm_nranks(comm) &&
-                                              mesh->st.rank == comm_rank(comm)),
-                   AFEM_ERR_ARG, "the mesh's slab rank/nranks differ from the communicator");
+      AFEM_REQUIRE(comm_nranks(comm) == 1 ||
+                       (mesh->st.valid && mesh->st.nranks == comm_nranks(comm) && mesh->st.rank == comm_rank(comm)) ||
+                       (mesh->part.valid && mesh->part.nranks == comm_nranks(comm) &&
+                        mesh->part.rank == comm_rank(comm)),
+                   AFEM_ERR_ARG, "the mesh's slab / subdomain rank and nranks differ from the communicator");
     mesh->ctx->set_device();
     auto* d = new Elastodynamics();
     try {

@@ -1,3 +1,4 @@
+#include <algorithm>
 // Device-resident P1 meshes: upload of caller arrays and the synthetic
 // jittered structured generator (the benchmark input, DESIGN.md "Synthetic
 // inputs").  The generator runs on the GPU so a 1e8-node mesh never crosses
@@ -199,6 +200,10 @@ void mesh_structured(Ctx& ctx, Mesh& m, int dim, int n, int nz, double jitter, u
 void mesh_local_to_global(Mesh& m, int64_t* host_out)
 {
   Ctx& ctx = *m.ctx;
+  if (m.part.valid) {
+    std::copy(m.part.l2g.begin(), m.part.l2g.end(), host_out);
+    return;
+  }
   if (!m.st.valid) {
     for (int64_t i = 0; i < m.n_nodes; ++i) host_out[i] = i;
     return;

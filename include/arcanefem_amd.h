@@ -110,6 +110,35 @@ int afem_mesh_create(afem_ctx* ctx, int dim, int nb_node_per_cell, int64_t n_nod
  * `rank` with one ghost node/cell layer (nranks = 1: the whole mesh). */
 int afem_mesh_create_structured(afem_ctx* ctx, int dim, int n, int nz, double jitter, uint64_t seed, int nranks,
                                 int rank, afem_mesh** out);
+/* ---- partitioned general meshes (Gmsh): what Arcane does before the FEM
+ * module sees the mesh (partitioner + one ghost layer) and what
+ * femutils/FemDoFsOnNodes.cc:71-128 does after it (DoF owner = node owner,
+ * computeSynchronizeInfos: the send / receive lists).  Host-side, C++. */
+/* Recursive coordinate bisection of the nodes into n_parts parts (node counts
+ * proportional, compact, deterministic).  coords[n_nodes*3]; node_part out. */
+int afem_partition_rcb(int dim, int64_t n_nodes, const double* coords, int n_parts, int32_t* node_part);
+typedef struct afem_subdomain_info {
+  int64_t n_own_nodes, n_nodes, n_cells; /* local: owned nodes first, then ghosts */
+  int n_neighbors;
+  int64_t n_send, n_recv;
+} afem_subdomain_info;
+/* The subdomain of `rank` for a node partition of a global mesh (host arrays):
+ * owned nodes (node_part == rank) then the ghost nodes (the other nodes of
+ * every cell with an owned node), each in global order; the local cells
+ * (every cell with an owned node, global order); per neighbour rank
+ * (ascending) the owned nodes that are ghosts there (send) and the ghosts it
+ * owns (receive), local ids in global order: rank r's send list to s is rank
+ * s's receive list from r.  Output arrays may be NULL (sizes in *info). */
+int afem_subdomain_plan(int nb_node_per_cell, int64_t n_nodes, int64_t n_cells, const int32_t* cell_node,
+                        const int32_t* node_part, int nranks, int rank, afem_subdomain_info* info,
+                        int64_t* local_to_global, int64_t* cells, int32_t* neighbor_ranks, int64_t* send_counts,
+                        int32_t* send_ids, int64_t* recv_counts, int32_t* recv_ids);
+/* The local mesh of that subdomain (afem_mesh_create on the local arrays); it
+ * keeps its halo plan (afem_ls_set_halo_mesh) and local_to_global
+ * (afem_mesh_download). */
+int afem_mesh_create_subdomain(afem_ctx* ctx, int dim, int nb_node_per_cell, int64_t n_nodes, int64_t n_cells,
+                               const int32_t* cell_node, const double* coords, const int32_t* node_part, int nranks,
+                               int rank, afem_mesh** out);
 int afem_mesh_get_info(const afem_mesh* mesh, afem_mesh_info* info);
 /* Copies to host: cell_node[n_cells*nv], coords[n_nodes*3], local_to_global[n_nodes]
  * (any pointer may be NULL). local_to_global is the identity for meshes from
@@ -390,6 +419,9 @@ int afem_ls_set_halo(afem_ls* ls, afem_comm* comm, int n_neighbors, const int32_
  * linear system may carry NB_DOF = n_rows / n_own_nodes DoFs per node (DoF
  * lid = node lid * NB_DOF + i, femutils/FemDoFsOnNodes.cc:79-109). */
 int afem_ls_set_halo_structured(afem_ls* ls, afem_comm* comm, afem_mesh* mesh);
+/* The same from any mesh that carries a halo plan: a structured slab or an
+ * afem_mesh_create_subdomain subdomain (NB_DOF-aware as above). */
+int afem_ls_set_halo_mesh(afem_ls* ls, afem_comm* comm, afem_mesh* mesh);
 /* Host-only (no GPU needed): the halo plan of a structured slab mesh, i.e.
  * the ghost synchronisation lists FemDoFsOnNodes::computeSynchronizeInfos
  * builds (femutils/FemDoFsOnNodes.cc:125-126).  Neighbours are rank-1 and

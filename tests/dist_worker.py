@@ -14,6 +14,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 # case parameters shared with the test
 POISSON = dict(n=5, nz=8)
@@ -51,6 +52,35 @@ def main():
         # CG iter/s with the halo attached (fixed iterations)
         ls.setSolverOptions(fixed_iterations=20)
         ls.solve()
+    elif case.startswith("gmsh:"):
+        # a reference Gmsh mesh partitioned by libafem's RCB into `world`
+        # ghosted subdomains (afem_mesh_create_subdomain), Poisson + penalty
+        # Dirichlet as the golden case, halo plan from the subdomain
+        from golden_cases import CASES
+        from arcanefem_amd.gmsh import read_gmsh
+
+        mfile, f, bcs, _, P = CASES[case[5:]]
+        gm = read_gmsh(os.path.join(ROOT, "tests", "golden", mfile))
+        part = af.partition_rcb(gm.dim, gm.coords, world)
+        mesh = af.Mesh.subdomain(ctx, gm.dim, gm.cells, gm.coords, part, world, rank)
+        _, _, l2g = mesh.download()
+        g2l = np.full(gm.n_nodes, -1, dtype=np.int64)
+        g2l[l2g] = np.arange(l2g.size)
+        bsr = af.BSRFormat(mesh, 1).initialize(True)
+        bsr.computeSparsity()
+        ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes, mesh.n_nodes)
+        bsr.assemblePoissonP1(1.0, f, ls.rhsVariable(), rhs_mode="set")
+        bsr.toLinearSystem(ls)
+        for g, v in bcs:
+            loc = g2l[gm.group_nodes(g)]
+            own = loc[(loc >= 0) & (loc < mesh.n_own_nodes)].astype(np.int32)
+            if own.size:
+                ls.applyDirichletViaPenalty(own, v, P)
+        ls.set_halo_mesh(comm, mesh)
+        ls.setSolverOptions(rtol=1e-14, max_iter=20000)
+        st = ls.solve()
+        res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
+                   converged=int(st["converged"]), rel=st["rel_residual"], part=part)
     elif case == "elastodynamics":
         from arcanefem_amd.elastodynamics import Elastodynamics3D
 

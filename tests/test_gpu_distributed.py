@@ -101,3 +101,39 @@ def test_distributed_elastodynamics(tmp_path):
     for gpu, orc in ((U, Uo), (V, Vo), (A, Ao)):
         assert not np.isnan(gpu).any()
         assert np.abs(gpu - orc).max() <= 1e-8 * np.abs(orc).max(), np.abs(gpu - orc).max() / np.abs(orc).max()
+
+
+@pytest.mark.parametrize("case,world", [("sphere_3D", 2), ("sphere_3D", 3), ("L-shape_2D", 3), ("L-shape_3D", 4)])
+def test_distributed_gmsh_subdomains(case, world, tmp_path):
+    """A reference Gmsh mesh cut by libafem's RCB partitioner into ghosted
+    subdomains (afem_mesh_create_subdomain, the plan of
+    femutils/FemDoFsOnNodes.cc:71-128): the gathered distributed solve equals
+    the oracle's single-domain direct solve and passes the reference golden."""
+    from golden_cases import CASES, GOLDEN_TOL
+    from arcanefem_amd.gmsh import read_gmsh, read_node_result_file
+
+    res = _run("gmsh:" + case, world, tmp_path)
+    mfile, f, bcs, gfile, P = CASES[case]
+    gm = read_gmsh(os.path.join(HERE, "golden", mfile))
+    rp, cols = O.sparsity(gm.n_nodes, gm.n_nodes, gm.cells)
+    vals, rhs = O.assemble_poisson(gm.n_nodes, gm.cells, gm.coords, rp, cols, f)
+    for g, v in bcs:
+        O.dirichlet_penalty(gm.group_nodes(g), v, P, rp, cols, vals, rhs)
+    xo = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
+    x = np.full(gm.n_nodes, np.nan)
+    owners = np.zeros(gm.n_nodes, dtype=np.int64)
+    for r in res:
+        k = int(r["n_own"])
+        x[r["l2g"][:k]] = r["x"][:k]
+        owners[r["l2g"][:k]] += 1
+        assert r["converged"]
+    assert np.all(owners == 1)  # the subdomains' owned nodes tile the mesh
+    assert len({int(r["iters"]) for r in res}) == 1
+    assert np.abs(x - xo).max() / np.abs(xo).max() <= 1e-10
+    for r in res:  # synchronised ghosts equal the owners' values
+        k = int(r["n_own"])
+        assert np.abs(r["x"][k:] - x[r["l2g"][k:]]).max() <= 1e-14 * np.abs(xo).max()
+    gold = read_node_result_file(os.path.join(HERE, "golden", gfile))
+    nerr, mx = O.check_node_result({int(t): x[i] for i, t in enumerate(gm.node_tags)}, gold, 1e-4)
+    assert nerr == 0
+    assert mx <= GOLDEN_TOL[case] * 1.5
