@@ -438,7 +438,9 @@ class DoFLinearSystem:
     SOLVERS = {"auto": C.AFEM_SOLVER_AUTO, "pcg": C.AFEM_SOLVER_PCG, "direct": C.AFEM_SOLVER_DIRECT}
 
     def setSolverOptions(self, rtol=None, atol=None, max_iter=None, check_every=None, fixed_iterations=None,
-                         method=None):
+                         method=None, initial_guess=None):
+        """initial_guess: "zero" (default) or "current" (start the PCG from the
+        solution vector's values)."""
         o = C.SolverOpts()
         call("afem_ls_get_solver_options", self.impl, ctypes.byref(o))
         if method is not None:
@@ -453,6 +455,8 @@ class DoFLinearSystem:
             o.check_every = check_every
         if fixed_iterations is not None:
             o.fixed_iterations = fixed_iterations
+        if initial_guess is not None:
+            o.initial_guess = {"zero": 0, "current": 1}[initial_guess]
         call("afem_ls_set_solver_options", self.impl, ctypes.byref(o))
 
     def solve(self) -> dict:

@@ -706,6 +706,7 @@ int afem_ls_create(afem_ctx* ctx, int64_t n_rows, int64_t n_cols_local, afem_ls*
     ls->opts.atol = 0.0;
     ls->opts.check_every = 8;
     ls->opts.fixed_iterations = 0;
+    ls->opts.initial_guess = 0;
     ls->rhs.alloc(n_rows);
     ls->sol.alloc(n_cols_local);
     ls->forced_info.alloc(n_rows);
@@ -737,6 +738,7 @@ int afem_ls_set_solver_options(afem_ls* ls, const afem_solver_opts* o)
   AFEM_REQUIRE(o->method == AFEM_SOLVER_AUTO || o->method == AFEM_SOLVER_PCG || o->method == AFEM_SOLVER_DIRECT,
                AFEM_ERR_NOT_IMPL, "unknown solver method");
   AFEM_REQUIRE(o->max_iter >= 0 && o->rtol >= 0 && o->atol >= 0, AFEM_ERR_ARG, "bad solver options");
+  AFEM_REQUIRE(o->initial_guess == 0 || o->initial_guess == 1, AFEM_ERR_ARG, "initial_guess must be 0 or 1");
   ls->opts = *o;
   API_END
 }

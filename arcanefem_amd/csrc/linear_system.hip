@@ -496,6 +496,21 @@ __global__ __launch_bounds__(kThreads) void k_cg_x0(int64_t n, const double* __r
   }
 }
 
+// Initial guess from the caller (afem_solver_opts::initial_guess = 1): the
+// constraint rows lifted as in k_cg_x0, the free rows from g
+__global__ __launch_bounds__(kThreads) void k_cg_x0_guess(int64_t n, const double* __restrict__ b,
+                                                          const double* __restrict__ dinv,
+                                                          const uint8_t* __restrict__ cons,
+                                                          const double* __restrict__ g, double* __restrict__ x,
+                                                          double* __restrict__ p)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double xi = cons[i] ? b[i] * dinv[i] : g[i];
+    x[i] = xi;
+    p[i] = xi;
+  }
+}
+
 // r = b - A x0 (q), z = D^-1 r, p = z ; partials r.z (all rows) and r.z (free rows)
 __global__ __launch_bounds__(kThreads) void k_cg_init(int64_t n, const double* __restrict__ b,
                                                       const double* __restrict__ q, double* __restrict__ r,
@@ -1006,6 +1021,11 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   hipLaunchKernelGGL(k_inv_diag, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, ctx.stream, n, ls.csr_rows,
                      ls.csr_cols, ls.csr_vals, ls.dinv.p, ls.cons.p);
   AFEM_LAUNCHED();
+  const bool warm = ls.opts.initial_guess == 1;
+  if (warm) {  // keep the caller's guess (the cold pass below overwrites the solution)
+    if (ls.x0.n != (size_t)n) ls.x0.alloc(n);
+    AFEM_HIP(hipMemcpyAsync(ls.x0.p, ls.sol.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
+  }
   hipLaunchKernelGGL(k_cg_x0, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.dinv.p, ls.cons.p, ls.sol.p,
                      ls.p.p);
   AFEM_LAUNCHED();
@@ -1027,6 +1047,23 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   // reference value of the stopping test: r0.z0 over the free rows (all rows
   // if every row is a constraint)
   double rz0 = ls.pinned[3] > 0.0 ? ls.pinned[3] : ls.pinned[0];
+  if (warm) {
+    // start from the caller's guess; the stopping reference stays the one of
+    // the zero (lifted) guess above, so the stopping test asks for the same
+    // residual as a cold start
+    hipLaunchKernelGGL(k_cg_x0_guess, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.dinv.p, ls.cons.p,
+                       ls.x0.p, ls.sol.p, ls.p.p);
+    AFEM_LAUNCHED();
+    if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
+    launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, nullptr, ls.csr_nnz);
+    hipLaunchKernelGGL(k_cg_init, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.q.p, ls.r.p, ls.z.p,
+                       ls.p.p, ls.dinv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
+    AFEM_LAUNCHED();
+    reduce_to(ctx, ls.partial.p, vb, scal + 0);
+    if (comm) comm_allreduce(comm, ctx, scal + 0, 1);
+    AFEM_HIP(hipMemcpyAsync(ls.pinned, scal, sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+  }
 
   const afem_solver_opts& o = ls.opts;
   const bool fixed = o.fixed_iterations > 0;

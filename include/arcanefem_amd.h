@@ -257,6 +257,9 @@ typedef struct afem_solver_opts {
   double atol;          /* or when ||r||_2 <= atol (default 0 = off) */
   int32_t check_every;  /* iterations between host convergence checks (default 8) */
   int32_t fixed_iterations; /* >0: run exactly this many iterations, no test (benchmarking) */
+  int32_t initial_guess;    /* 0: zero (constraint rows lifted to their values, default); 1: start from the
+                               current solution vector (free rows; e.g. the previous time step's).  The
+                               stopping reference r0.z0 stays the zero guess's: same residual target. */
 } afem_solver_opts;
 
 typedef struct afem_solve_stats {

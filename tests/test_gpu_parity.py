@@ -492,3 +492,27 @@ def test_rccl_communicator_single_rank(ctx):
         assert np.array_equal(sols[0], sols[1])
     finally:
         comm.close()
+
+
+def test_initial_guess_current_solution(ctx):
+    """afem_solver_opts::initial_guess = 1 starts the PCG from the solution
+    vector: from the converged solution it stops at once with the same
+    answer; from a perturbed one it converges to the cold-start solution
+    (same stopping target: the zero guess's residual)."""
+    gm = read_gmsh(path("sphere_cut.msh"))
+    mesh = af.Mesh.from_arrays(ctx, gm.dim, gm.cells, gm.coords)
+    bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+    ls.applyDirichletViaPenalty(gm.group_nodes("horizontal"), 0.5, 1e30)
+    ls.setSolverOptions(rtol=1e-12, max_iter=20000, method="pcg", initial_guess="zero")
+    st0 = ls.solve()
+    x0 = ls.solution_host()
+    ls.setSolverOptions(initial_guess="current")
+    st1 = ls.solve()
+    assert st1["converged"] and st1["iterations"] <= 8
+    assert np.abs(ls.solution_host() - x0).max() <= 1e-12 * np.abs(x0).max()
+    pert = x0 * (1.0 + 1e-3 * np.sin(np.arange(x0.size)))
+    ctx.to_device(ls.solutionVariable(), pert)
+    st2 = ls.solve()
+    assert st2["converged"] and st2["iterations"] < st0["iterations"]
+    assert np.abs(ls.solution_host() - x0).max() <= 1e-9 * np.abs(x0).max()
+    ls.setSolverOptions(initial_guess="zero")
