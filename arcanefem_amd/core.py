@@ -438,9 +438,10 @@ class DoFLinearSystem:
     SOLVERS = {"auto": C.AFEM_SOLVER_AUTO, "pcg": C.AFEM_SOLVER_PCG, "direct": C.AFEM_SOLVER_DIRECT}
 
     def setSolverOptions(self, rtol=None, atol=None, max_iter=None, check_every=None, fixed_iterations=None,
-                         method=None, initial_guess=None):
+                         method=None, initial_guess=None, preconditioner=None):
         """initial_guess: "zero" (default) or "current" (start the PCG from the
-        solution vector's values)."""
+        solution vector's values); preconditioner: "jacobi" (default) or
+        "block3" (3x3 node-block Jacobi, NB_DOF = 3 systems)."""
         o = C.SolverOpts()
         call("afem_ls_get_solver_options", self.impl, ctypes.byref(o))
         if method is not None:
@@ -457,6 +458,8 @@ class DoFLinearSystem:
             o.fixed_iterations = fixed_iterations
         if initial_guess is not None:
             o.initial_guess = {"zero": 0, "current": 1}[initial_guess]
+        if preconditioner is not None:
+            o.precond_block = {"jacobi": 0, "block3": 3}[preconditioner]
         call("afem_ls_set_solver_options", self.impl, ctypes.byref(o))
 
     def solve(self) -> dict:

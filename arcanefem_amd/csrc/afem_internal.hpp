@@ -285,6 +285,7 @@ struct LinearSystem {
   // solver work
   DevBuf<double> r, z, p, q, dinv, partial, scal;
   DevBuf<double> x0;      // the caller's initial guess (opts.initial_guess = 1)
+  DevBuf<double> binv;    // block-Jacobi 3: inverse node blocks [n/3][9]
   DevBuf<int32_t> blist;  // multi-rank CG: SpMV row blocks, interior ones first
   int64_t blist_nint = 0;
   uint64_t blist_key = 0;

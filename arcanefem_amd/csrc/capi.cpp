@@ -707,6 +707,7 @@ int afem_ls_create(afem_ctx* ctx, int64_t n_rows, int64_t n_cols_local, afem_ls*
     ls->opts.check_every = 8;
     ls->opts.fixed_iterations = 0;
     ls->opts.initial_guess = 0;
+    ls->opts.precond_block = 0;
     ls->rhs.alloc(n_rows);
     ls->sol.alloc(n_cols_local);
     ls->forced_info.alloc(n_rows);
@@ -739,6 +740,8 @@ int afem_ls_set_solver_options(afem_ls* ls, const afem_solver_opts* o)
                AFEM_ERR_NOT_IMPL, "unknown solver method");
   AFEM_REQUIRE(o->max_iter >= 0 && o->rtol >= 0 && o->atol >= 0, AFEM_ERR_ARG, "bad solver options");
   AFEM_REQUIRE(o->initial_guess == 0 || o->initial_guess == 1, AFEM_ERR_ARG, "initial_guess must be 0 or 1");
+  AFEM_REQUIRE(o->precond_block == 0 || o->precond_block == 1 || o->precond_block == 3, AFEM_ERR_ARG,
+               "precond_block must be 0, 1 or 3");
   ls->opts = *o;
   API_END
 }
@@ -1069,6 +1072,8 @@ int afem_elastodynamics_set_solver_options(afem_elastodynamics* h, const afem_so
   NOT_NULL(o);
   AFEM_REQUIRE(o->method != AFEM_SOLVER_DIRECT, AFEM_ERR_NOT_IMPL, "elastodynamics solves with the Jacobi-PCG");
   AFEM_REQUIRE(o->max_iter >= 0 && o->rtol >= 0 && o->atol >= 0, AFEM_ERR_ARG, "bad solver options");
+  AFEM_REQUIRE(o->precond_block == 0 || o->precond_block == 1 || o->precond_block == 3, AFEM_ERR_ARG,
+               "precond_block must be 0, 1 or 3");
   h->d->ls.opts = *o;
   h->d->ls.opts.method = AFEM_SOLVER_PCG;
   API_END

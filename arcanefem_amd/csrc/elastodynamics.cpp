@@ -59,6 +59,7 @@ void init_ls(LinearSystem& ls, Ctx* ctx, int64_t n, int64_t n_cols)
   ls.opts.check_every = 8;
   ls.opts.fixed_iterations = 0;
   ls.opts.initial_guess = 0;
+  ls.opts.precond_block = 0;
   ls.rhs.alloc(n);
   ls.sol.alloc(n_cols);
   ls.forced_info.alloc(n);

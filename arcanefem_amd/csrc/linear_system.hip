@@ -537,6 +537,115 @@ __global__ __launch_bounds__(kThreads) void k_cg_init(int64_t n, const double* _
   }
 }
 
+// ---- block-Jacobi (3x3 node blocks, afem_solver_opts::precond_block = 3:
+// the NB_DOF = 3 systems of elasticity / elastodynamics).  The block of node
+// b is rows/cols 3b..3b+2 of the CSR; a constraint row (penalty / eliminated,
+// `cons`) is decoupled from its block mates before the inversion, so the
+// preconditioner is block-diag(1/a_ii, inverse of the free sub-block): SPD
+// when the free block is, and the constraint rows keep z_i = r_i / a_ii.
+__global__ void k_inv_block3(int64_t nb, const int64_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                             const double* __restrict__ vals, const uint8_t* __restrict__ cons,
+                             const double* __restrict__ dinv, double* __restrict__ binv)
+{
+  const int64_t ib = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ib >= nb) return;
+  double B[3][3] = { { 0, 0, 0 }, { 0, 0, 0 }, { 0, 0, 0 } };
+  bool c[3];
+  for (int a = 0; a < 3; ++a) {
+    const int64_t row = 3 * ib + a;
+    c[a] = cons[row] != 0;
+    for (int64_t k = rows[row]; k < rows[row + 1]; ++k) {
+      const int64_t d = (int64_t)cols[k] - 3 * ib;
+      if (d >= 0 && d < 3) B[a][d] = vals[k];
+    }
+  }
+  for (int a = 0; a < 3; ++a)
+    for (int d = 0; d < 3; ++d)
+      if (a != d && (c[a] || c[d])) B[a][d] = 0.0;
+  const double c00 = B[1][1] * B[2][2] - B[1][2] * B[2][1], c01 = B[1][2] * B[2][0] - B[1][0] * B[2][2],
+               c02 = B[1][0] * B[2][1] - B[1][1] * B[2][0];
+  const double det = B[0][0] * c00 + B[0][1] * c01 + B[0][2] * c02;
+  double* o = binv + 9 * ib;
+  if (det == 0.0 || !isfinite(det)) {  // singular block: point Jacobi
+    for (int a = 0; a < 3; ++a)
+      for (int d = 0; d < 3; ++d) o[3 * a + d] = a == d ? dinv[3 * ib + a] : 0.0;
+    return;
+  }
+  const double id = 1.0 / det;
+  o[0] = c00 * id;
+  o[1] = (B[0][2] * B[2][1] - B[0][1] * B[2][2]) * id;
+  o[2] = (B[0][1] * B[1][2] - B[0][2] * B[1][1]) * id;
+  o[3] = c01 * id;
+  o[4] = (B[0][0] * B[2][2] - B[0][2] * B[2][0]) * id;
+  o[5] = (B[0][2] * B[1][0] - B[0][0] * B[1][2]) * id;
+  o[6] = c02 * id;
+  o[7] = (B[0][1] * B[2][0] - B[0][0] * B[2][1]) * id;
+  o[8] = (B[0][0] * B[1][1] - B[0][1] * B[1][0]) * id;
+}
+
+__device__ __forceinline__ void apply_binv3(const double* __restrict__ m, const double (&r)[3], double (&z)[3])
+{
+  z[0] = m[0] * r[0] + m[1] * r[1] + m[2] * r[2];
+  z[1] = m[3] * r[0] + m[4] * r[1] + m[5] * r[2];
+  z[2] = m[6] * r[0] + m[7] * r[1] + m[8] * r[2];
+}
+
+// k_cg_init with z = Binv r per node block (nb = n / 3 blocks)
+__global__ __launch_bounds__(kThreads) void k_cg_init_b3(int64_t nb, const double* __restrict__ b,
+                                                         const double* __restrict__ q, double* __restrict__ r,
+                                                         double* __restrict__ z, double* __restrict__ p,
+                                                         const double* __restrict__ binv,
+                                                         const uint8_t* __restrict__ cons, double* __restrict__ partial,
+                                                         double* __restrict__ partial_free)
+{
+  double s = 0.0, sf = 0.0;
+  for (int64_t ib = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ib < nb; ib += (int64_t)gridDim.x * blockDim.x) {
+    double ri[3], zi[3];
+    for (int a = 0; a < 3; ++a) ri[a] = b[3 * ib + a] - q[3 * ib + a];
+    apply_binv3(binv + 9 * ib, ri, zi);
+    for (int a = 0; a < 3; ++a) {
+      r[3 * ib + a] = ri[a];
+      z[3 * ib + a] = zi[a];
+      p[3 * ib + a] = zi[a];
+      s += ri[a] * zi[a];
+      if (!cons[3 * ib + a]) sf += ri[a] * zi[a];
+    }
+  }
+  double bs = block_sum(s);
+  double bf = block_sum(sf);
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = bs;
+    partial_free[blockIdx.x] = bf;
+  }
+}
+
+// k_cg_update with z = Binv r per node block
+__global__ __launch_bounds__(kThreads) void k_cg_update_b3(int64_t nb, const double* __restrict__ scal, int par,
+                                                           double* __restrict__ x, const double* __restrict__ p,
+                                                           double* __restrict__ r, const double* __restrict__ q,
+                                                           double* __restrict__ z, const double* __restrict__ binv,
+                                                           double* __restrict__ partial)
+{
+  const double rz = scal[par], pq = scal[2];
+  const double alpha = (pq != 0.0) ? rz / pq : 0.0;
+  double s = 0.0;
+  for (int64_t ib = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ib < nb; ib += (int64_t)gridDim.x * blockDim.x) {
+    double ri[3], zi[3];
+    for (int a = 0; a < 3; ++a) {
+      x[3 * ib + a] += alpha * p[3 * ib + a];
+      ri[a] = r[3 * ib + a] - alpha * q[3 * ib + a];
+      r[3 * ib + a] = ri[a];
+    }
+    apply_binv3(binv + 9 * ib, ri, zi);
+    for (int a = 0; a < 3; ++a) {
+      z[3 * ib + a] = zi[a];
+      s += ri[a] * zi[a];
+    }
+  }
+  double bs = block_sum(s);
+  if (threadIdx.x == 0) partial[blockIdx.x] = bs;
+}
+
 // alpha = rz/pq ; x += alpha p ; r -= alpha q ; z = D^-1 r ; partial r.z (and r.r)
 __global__ __launch_bounds__(kThreads) void k_cg_update(int64_t n, const double* __restrict__ scal, int par,
                                                         double* __restrict__ x, const double* __restrict__ p,
@@ -1021,6 +1130,26 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   hipLaunchKernelGGL(k_inv_diag, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, ctx.stream, n, ls.csr_rows,
                      ls.csr_cols, ls.csr_vals, ls.dinv.p, ls.cons.p);
   AFEM_LAUNCHED();
+  const bool blk3 = ls.opts.precond_block == 3;
+  AFEM_REQUIRE(!blk3 || n % 3 == 0, AFEM_ERR_ARG, "block-Jacobi 3: the row count is not a multiple of 3");
+  const int64_t nb3 = n / 3;
+  const unsigned vb3 = (unsigned)std::min<int64_t>(kVecBlocks, std::max<int64_t>(1, (nb3 + kThreads - 1) / kThreads));
+  if (blk3) {
+    if (ls.binv.n != (size_t)(9 * nb3)) ls.binv.alloc(9 * nb3 > 0 ? 9 * nb3 : 1);
+    hipLaunchKernelGGL(k_inv_block3, dim3(grid_for(nb3, 256)), dim3(256), 0, ctx.stream, nb3, ls.csr_rows,
+                       ls.csr_cols, ls.csr_vals, ls.cons.p, ls.dinv.p, ls.binv.p);
+    AFEM_LAUNCHED();
+  }
+  // r = b - A x0, z = M^-1 r, p = z and the r.z partials (all rows, free rows)
+  auto cg_init = [&]() {
+    if (blk3)
+      hipLaunchKernelGGL(k_cg_init_b3, dim3(vb3), dim3(kThreads), 0, ctx.stream, nb3, ls.rhs.p, ls.q.p, ls.r.p,
+                         ls.z.p, ls.p.p, ls.binv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
+    else
+      hipLaunchKernelGGL(k_cg_init, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.q.p, ls.r.p, ls.z.p,
+                         ls.p.p, ls.dinv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
+    AFEM_LAUNCHED();
+  };
   const bool warm = ls.opts.initial_guess == 1;
   if (warm) {  // keep the caller's guess (the cold pass below overwrites the solution)
     if (ls.x0.n != (size_t)n) ls.x0.alloc(n);
@@ -1031,12 +1160,10 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   AFEM_LAUNCHED();
   if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
   launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, nullptr, ls.csr_nnz);
-  hipLaunchKernelGGL(k_cg_init, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.q.p, ls.r.p, ls.z.p, ls.p.p,
-                     ls.dinv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
-  AFEM_LAUNCHED();
+  cg_init();
   double* scal = ls.scal.p;  // [0],[1]: r.z ping-pong, [2]: p.q, [3]: r0.z0 over free rows, [4]: r.r
-  reduce_to(ctx, ls.partial.p, vb, scal + 0);
-  reduce_to(ctx, ls.partial.p + vb, vb, scal + 3);
+  reduce_to(ctx, ls.partial.p, blk3 ? vb3 : vb, scal + 0);
+  reduce_to(ctx, ls.partial.p + vb, blk3 ? vb3 : vb, scal + 3);
   Comm* comm = ls.halo ? ls.halo->comm : nullptr;
   if (comm) {
     comm_allreduce(comm, ctx, scal + 0, 1);
@@ -1056,10 +1183,8 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     AFEM_LAUNCHED();
     if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
     launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, nullptr, ls.csr_nnz);
-    hipLaunchKernelGGL(k_cg_init, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.q.p, ls.r.p, ls.z.p,
-                       ls.p.p, ls.dinv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
-    AFEM_LAUNCHED();
-    reduce_to(ctx, ls.partial.p, vb, scal + 0);
+    cg_init();
+    reduce_to(ctx, ls.partial.p, blk3 ? vb3 : vb, scal + 0);
     if (comm) comm_allreduce(comm, ctx, scal + 0, 1);
     AFEM_HIP(hipMemcpyAsync(ls.pinned, scal, sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
     ctx.sync();
@@ -1135,10 +1260,14 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
 
     reduce_to(ctx, ls.partial.p, pl.nblocks, scal + 2);
     if (comm) comm_allreduce(comm, ctx, scal + 2, 1);
-    hipLaunchKernelGGL(k_cg_update, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p, ls.r.p,
-                       ls.q.p, ls.z.p, ls.dinv.p, ls.partial.p);
+    if (blk3)
+      hipLaunchKernelGGL(k_cg_update_b3, dim3(vb3), dim3(kThreads), 0, ctx.stream, nb3, scal, par, ls.sol.p, ls.p.p,
+                         ls.r.p, ls.q.p, ls.z.p, ls.binv.p, ls.partial.p);
+    else
+      hipLaunchKernelGGL(k_cg_update, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p,
+                         ls.r.p, ls.q.p, ls.z.p, ls.dinv.p, ls.partial.p);
     AFEM_LAUNCHED();
-    reduce_to(ctx, ls.partial.p, vb, scal + (par ^ 1));
+    reduce_to(ctx, ls.partial.p, blk3 ? vb3 : vb, scal + (par ^ 1));
     if (comm) comm_allreduce(comm, ctx, scal + (par ^ 1), 1);
     hipLaunchKernelGGL(k_cg_dir, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.z.p, ls.p.p);
     AFEM_LAUNCHED();

@@ -19,7 +19,8 @@ subdomain or on one ghosted z-slab per rank (``comm``: RCCL ``Communicator`` or
 body-force RHS in one fused HIP kernel on the fixed sparsity, adds
 ``M (c0 U + c3 V + c4 A)`` (the mass operator shares the structure; its SpMV
 exchanges the ghost values of the operand), clamps the fixed nodes by
-penalty, solves with the Jacobi-PCG (halo + all-reduces over the ranks) and
+penalty, solves with the PCG (3x3 node-block Jacobi by default, warm started
+from the Newmark predictor; halo + all-reduces over the ranks) and
 applies the Newmark update on the device.
 """
 from __future__ import annotations
@@ -47,7 +48,7 @@ def newmark_coefficients(rho: float, dt: float):
 class Elastodynamics3D:
     def __init__(self, ctx: Context, mesh: Mesh, E: float, nu: float, rho: float, dt: float,
                  body_force=(0.0, 0.0, 0.0), fixed_nodes=None, penalty: float = 1.0e30, rtol: float = 1e-12,
-                 comm=None, max_iter: int = 20000):
+                 comm=None, max_iter: int = 20000, preconditioner: str = "jacobi"):
         if mesh.dim != 3:
             raise ValueError("Elastodynamics3D needs a tetrahedral mesh")
         self.ctx, self.mesh, self.dt = ctx, mesh, dt
@@ -60,7 +61,7 @@ class Elastodynamics3D:
              ctypes.c_void_p(fixed.ctypes.data) if fixed.size else None, fixed.size, C.AFEM_MEM_HOST,
              ctypes.byref(h))
         self.h = h
-        o = C.SolverOpts(C.AFEM_SOLVER_PCG, max_iter, rtol, 0.0, 8, 0)
+        o = C.SolverOpts(C.AFEM_SOLVER_PCG, max_iter, rtol, 0.0, 8, 0, 0, {"jacobi": 0, "block3": 3}[preconditioner])
         call("afem_elastodynamics_set_solver_options", self.h, ctypes.byref(o))
         self.t = 0.0
         self.last_stats = None

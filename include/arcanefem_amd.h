@@ -260,6 +260,8 @@ typedef struct afem_solver_opts {
   int32_t initial_guess;    /* 0: zero (constraint rows lifted to their values, default); 1: start from the
                                current solution vector (free rows; e.g. the previous time step's).  The
                                stopping reference r0.z0 stays the zero guess's: same residual target. */
+  int32_t precond_block;    /* 0 or 1: point Jacobi (default); 3: block Jacobi on 3x3 node blocks (NB_DOF = 3
+                               systems; constraint rows decoupled from their block mates) */
 } afem_solver_opts;
 
 typedef struct afem_solve_stats {
