@@ -686,8 +686,8 @@ __global__ void k_strip_local(int64_t n_pos, const uint8_t* __restrict__ strip, 
 // c(u) = (L + s_j) mod 32, consistent over every (lane, step) reading u, makes
 // every gather conflict-free.  This pass finds the shifts s_j (the row's own
 // node has shift 0) by propagation over the steps, checks consistency, and
-// places node u at q = c(u) + 32 m (m = rank within its class; at most 8 per
-// class fit the 256 positions, extra nodes fill free positions).  Slices that
+// places node u at q = c(u) + 32 m (m = rank within its class, q < maxq;
+// extra nodes fill free positions).  Slices that
 // are not uniform, not consistent or larger than 256 nodes keep their order
 // (identity).  Positions left free repeat the slice's first node.  Every
 // kernel addresses the cache through the remapped local indices, so the
@@ -699,7 +699,7 @@ __global__ __launch_bounds__(64) void k_bank_place(int64_t n_slices, const uint8
                                                    const int64_t* __restrict__ strip_ptr,
                                                    const int32_t* __restrict__ strip_n,
                                                    const uint32_t* __restrict__ pos_dl, uint8_t* __restrict__ q_of_u,
-                                                   int32_t* __restrict__ nu_new)
+                                                   int32_t* __restrict__ nu_new, int maxq)
 {
   __shared__ int cls[256];
   __shared__ int shift[32];
@@ -714,7 +714,7 @@ __global__ __launch_bounds__(64) void k_bank_place(int64_t n_slices, const uint8
     if (lane == 0) nu_new[sl] = nu;
   };
   const int n = strip_n[sl];
-  if (!uflag[sl] || nu > 256 || n > 32) {
+  if (!uflag[sl] || nu > maxq || n > 32) {
     identity();
     return;
   }
@@ -768,14 +768,14 @@ __global__ __launch_bounds__(64) void k_bank_place(int64_t n_slices, const uint8
     uint8_t cnt[32];
     uint32_t taken[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
     for (int c = 0; c < 32; ++c) cnt[c] = 0;
-    int maxq = -1;
+    int top = -1;
     for (int u = 0; u < nu; ++u) {
       const int c = cls[u];
-      if (c >= 0 && cnt[c] < 8) {
+      if (c >= 0 && c + 32 * cnt[c] < maxq) {
         const int q = c + 32 * cnt[c]++;
         qo[u] = (uint8_t)q;
         taken[q >> 5] |= 1u << (q & 31);
-        maxq = max(maxq, q);
+        top = max(top, q);
         cls[u] = 256;  // placed
       }
     }
@@ -785,10 +785,10 @@ __global__ __launch_bounds__(64) void k_bank_place(int64_t n_slices, const uint8
       while (taken[free_q >> 5] >> (free_q & 31) & 1u) ++free_q;
       qo[u] = (uint8_t)free_q;
       taken[free_q >> 5] |= 1u << (free_q & 31);
-      maxq = max(maxq, free_q);
+      top = max(top, free_q);
     }
     for (int u = nu; u < 256; ++u) qo[u] = qo[0];
-    nu_new[sl] = maxq + 1;
+    nu_new[sl] = top + 1;
   }
 }
 
@@ -1184,9 +1184,13 @@ void build_structure(Mesh& m, Structure& s)
         q_of_u.alloc(s.n_slices * 256);
         DevBuf<int32_t> nu_new;
         nu_new.alloc(s.n_slices);
+        // positions < maxq: 232 keeps the uniform instance's LDS image at 13.3 KB per wave
+        // (12 waves per CU with 15 slots); classes c < 8 get 8 positions, the others 7
+        const char* bpm = getenv("AFEM_BANK_PLACE_MAX");
+        const int maxq = bpm ? std::max(64, std::min(256, atoi(bpm))) : 232;
         hipLaunchKernelGGL(k_bank_place, dim3((unsigned)s.n_slices), dim3(64), 0, ctx.stream, s.n_slices, uflag.p,
                            s.perm.p, s.snode_ptr.p, s.strip_u.p, s.strip_ptr.p, s.strip_n.p, s.pos_dl.p, q_of_u.p,
-                           nu_new.p);
+                           nu_new.p, maxq);
         AFEM_LAUNCHED();
         DevBuf<int64_t> ptr_new;
         ptr_new.alloc(s.n_slices + 1);
