@@ -1408,6 +1408,361 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
   }
 }
 
+// ---------------------------------------------------------------- block-3 elasticity, one workgroup per slice
+// k_assemble_elast_strip with the three component rows of a slice in ONE
+// workgroup of three waves (wave i = component row i): the slice's node
+// coordinates (SoA, bank-aware positions) and column-index table are staged
+// once for the three waves (one global gather per slice instead of three),
+// and the write-back goes through one flat LDS image of the slice's
+// complete 3x3 blocks (per block 9 contiguous values, per row 9 len): the
+// workgroup stores whole blocks with consecutive threads (no 24-B pieces
+// of 72-B blocks from three different waves: WRITE_SIZE was 1.3x the
+// values).  LDS per workgroup: 3 x [slot][3][lane] accumulators (the flat
+// image overlays them) + coordinates + column indices: 2 workgroups = 6
+// waves per CU (the one-wave-per-item kernel: 5).  Coordinates are read in
+// the frame rotated by the wave's component row (three SoA reads at
+// rotated array offsets), so the element arithmetic is that of
+// k_assemble_elast_strip, entry for entry.
+__host__ __device__ constexpr int64_t elast_wg_bytes(int64_t u_cap, int64_t w_cap)
+{
+  return 3 * 3 * 8 * 64 * w_cap + 3 * 8 * u_cap + 2 * 64 * w_cap + 64 * 8 + 64 * 4 + 64 + ((64 * w_cap + 15) & ~15);
+}
+
+template <int MAXC, int MAXW, int UMODE>
+__global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, const SliceRec* __restrict__ recs,
+                                                           unsigned long long* __restrict__ tickets, int u_cap,
+                                                           int w_cap, bool per_block, const int32_t* __restrict__ perm,
+                                                           const int64_t* __restrict__ pos_rb,
+                                                           const uint32_t* __restrict__ pos_dl,
+                                                           const uint8_t* __restrict__ strip,
+                                                           const uint16_t* __restrict__ lidx,
+                                                           const int32_t* __restrict__ snode,
+                                                           const double* __restrict__ coords, double lambda, double mu,
+                                                           double c0, double fx, double fy, double fz,
+                                                           double* __restrict__ vals, double* __restrict__ rhs,
+                                                           int rhs_add)
+{
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int ci = __builtin_amdgcn_readfirstlane(tid >> 6);  // component row of this wave
+  const int64_t acc_stride = 3 * 64 * (int64_t)w_cap;   // doubles per wave region
+  double* const acc_all = reinterpret_cast<double*>(smem);
+  double* const acc = acc_all + ci * acc_stride;  // [slot][k][lane]
+  double* const cs = acc_all + 3 * acc_stride;    // SoA coordinates [3][u_cap]
+  uint16_t* const li = reinterpret_cast<uint16_t*>(cs + 3 * (int64_t)u_cap);
+  int64_t* const rbs = reinterpret_cast<int64_t*>(li + 64 * (int64_t)w_cap);
+  int32_t* const fps = reinterpret_cast<int32_t*>(rbs + 64);
+  unsigned long long* const claim = reinterpret_cast<unsigned long long*>(fps + 64);
+  uint8_t* const bown = reinterpret_cast<uint8_t*>(claim + 8);  // block -> owning row lane
+  const int xcd = (int)(blockIdx.x & 7);
+  const int64_t r0 = n_slices * xcd / 8, r1 = n_slices * (xcd + 1) / 8;
+  // workgroup claims: thread 0 takes a ticket, the workgroup reads it after a barrier
+  auto issue = [&]() -> unsigned long long { return tid == 0 ? atomicAdd(tickets + 16 * xcd, 1ull) : 0ull; };
+  auto uni = [&](unsigned long long t) -> int64_t {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)t);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(t >> 32));
+    return r0 + (int64_t)(((uint64_t)hi << 32) | lo);
+  };
+  auto bcast = [&](unsigned long long t) -> int64_t {
+    if (tid == 0) claim[0] = t;
+    __syncthreads();
+    const unsigned long long v = claim[0];
+    __syncthreads();
+    return uni(v);
+  };
+  int64_t p0 = bcast(issue());
+  if (p0 >= r1) return;
+  int64_t p1 = bcast(issue());
+  int64_t p2 = bcast(issue());
+  int64_t p3 = bcast(issue());
+  SliceRec R0 = recs[p0];
+  SliceRec R1 = recs[p1 < r1 ? p1 : p0];
+  SliceRec R2 = recs[p2 < r1 ? p2 : p0];
+
+  // staging share of a thread: nodes u = tid and tid + 192 (u_cap <= 256)
+  auto load_nid = [&](const SliceRec& R, int32_t(&nid)[2]) {
+    const int nu = (int)(R.meta & 0xFFFFu);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) nid[k] = snode[(int64_t)R.snode_off + max(min(tid + 192 * k, nu - 1), 0)];
+  };
+  struct Pre {
+    int32_t row;
+    uint32_t dl;
+    int64_t rb;
+    u32x4 l0, l1;
+    u32x4 ch[MAXC];
+    double x[2], y[2], z[2];
+  };
+  auto load_rows = [&](const SliceRec& R, Pre& p) {
+    const int64_t q = (int64_t)R.sl * 64 + lane;
+    p.row = perm[q];
+    p.dl = pos_dl[q];
+    p.rb = pos_rb[q];
+    if (ci == 0) {  // the column-index table (staged by wave 0)
+      const int nq = 8 * (int)((R.meta >> 16) & 0xFFu);
+      const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R.lidx_off);
+      p.l0 = ls[max(min(lane, nq - 1), 0)];
+      p.l1 = ls[max(min(lane + 64, nq - 1), 0)];
+    }
+    const int nc = (int)((R.meta >> 24) + 15) >> 4;
+    const u32x4* sp = reinterpret_cast<const u32x4*>(strip + (int64_t)R.strip_off * 1024) + lane;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
+  };
+  auto gather = [&](const int32_t(&nid)[2], Pre& p) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      p.x[k] = coords[3 * (int64_t)nid[k]];
+      p.y[k] = coords[3 * (int64_t)nid[k] + 1];
+      p.z[k] = coords[3 * (int64_t)nid[k] + 2];
+    }
+  };
+  Pre cur, nxt;
+  int32_t nid1[2], nid2[2];
+  {
+    int32_t nid0[2];
+    load_nid(R0, nid0);
+    load_rows(R0, cur);
+    gather(nid0, cur);
+    load_nid(R1, nid1);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  // rotated-frame component arrays of this wave: (x_ci, x_ci+1, x_ci+2)
+  const double* const ca = cs + (int64_t)u_cap * ci;
+  const double* const cb = cs + (int64_t)u_cap * (ci == 2 ? 0 : ci + 1);
+  const double* const cc = cs + (int64_t)u_cap * (ci == 0 ? 2 : ci - 1);
+  for (;;) {
+    const unsigned long long t4 = issue();  // read at the end of this iteration
+    const SliceRec R3 = recs[p3 < r1 ? p3 : p0];
+    const int nsteps = (int)(R0.meta >> 24);
+    const int W = (int)((R0.meta >> 16) & 0xFFu);
+    const int nu = (int)(R0.meta & 0xFFFFu);
+    // ---- stage: coordinates (SoA), column indices, zero accumulators
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int u = tid + 192 * k;
+      if (u < nu) {
+        cs[u] = cur.x[k];
+        cs[u_cap + u] = cur.y[k];
+        cs[2 * u_cap + u] = cur.z[k];
+      }
+    }
+    if (ci == 0) {
+      const int nq = 8 * W;
+      u32x4* dst = reinterpret_cast<u32x4*>(li);
+      dst[max(min(lane, nq - 1), 0)] = cur.l0;
+      dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
+    }
+    {
+      double2* a2 = reinterpret_cast<double2*>(acc);
+      for (int q = lane; q < 96 * W; q += 64) a2[q] = make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+    load_rows(R1, nxt);
+    gather(nid1, nxt);
+    load_nid(R2, nid2);
+
+    const int32_t row = cur.row;
+    const bool active = row >= 0;
+    const int64_t rb = cur.rb;
+    const int len = (int)((cur.dl >> 8) & 0xFFu);
+    const uint32_t dslot = cur.dl & 0xFFu;
+    const uint16_t* lrow = li + lane;
+    auto coord = [&](int u) { return V3{ ca[u], cb[u], cc[u] }; };
+    const V3 xi = coord((int)lrow[dslot * 64]);
+    double macc = 0.0;
+    V3 eP{ 0.0, 0.0, 0.0 }, eQ{ 0.0, 0.0, 0.0 }, eR{ 0.0, 0.0, 0.0 };
+    V3 cP{ 0.0, 0.0, 0.0 }, cN{ 0.0, 0.0, 0.0 };
+    double* const acc_lane = acc + lane;
+    double* aP = acc_lane + 192 * dslot;
+    double* aQ = aP;
+    double* aR = aP;
+    auto lidx_of = [&](uint32_t byte) { return (int)lrow[(byte & 63u) * 64]; };
+    auto sel = [](bool c, V3 a, V3 b) { return V3{ c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z }; };
+    auto keep = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
+    auto block = [&](double* a, V3 m, V3 cbv, double s, double mass) {
+      const double t = dot(m, cbv);
+      const double A = lambda * m.x, B = mu * cbv.x;
+      const double v0 = (A * cbv.x + B * m.x) * s + (mu * t * s + mass);
+      const double v1 = (A * cbv.y + B * m.y) * s;
+      const double v2 = (A * cbv.z + B * m.z) * s;
+      atomicAdd(a, v0);
+      atomicAdd(a + 64, v1);
+      atomicAdd(a + 128, v2);
+    };
+    auto byte_at = [&](int j) -> uint32_t {
+      const u32x4 w = cur.ch[j >> 4];
+      const int q = (j >> 2) & 3;
+      const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
+      return (wq >> (8 * (j & 3))) & 0xFFu;
+    };
+    constexpr int NSTEP = 16 * MAXC;
+    if constexpr (UMODE == 1) {
+      const uint64_t pat = R0.pat;
+      auto ustep = [&](auto swap_c, uint32_t byte, V3 xd) {
+        constexpr bool SWAP = decltype(swap_c)::value;
+        double* const aD = acc_lane + 192 * (byte & 63u);
+        const V3 eD = sub(xd, xi);
+        V3 cRn;
+        if constexpr (SWAP) {
+          cRn = cN;
+        }
+        else {
+          cRn = cP;
+          eP = eQ;
+          aP = aQ;
+        }
+        eQ = eR;
+        aQ = aR;
+        eR = eD;
+        aR = aD;
+        cP = cross(eQ, eR);
+        cN = cross(eP, eR);
+        const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
+        const double meas = fabs(dot(eP, cP));
+        const double s = -recip1(6.0 * fmax(meas, 1e-300));
+        const double mass = c0 * meas * (1.0 / 120.0);
+        macc += meas;
+        block(aP, m, cP, s, mass);
+        block(aQ, m, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+        block(aR, m, cRn, s, mass);
+      };
+      {
+        const uint32_t b0 = byte_at(0), b1 = byte_at(1);
+        eQ = sub(coord(lidx_of(b0)), xi);
+        eR = sub(coord(lidx_of(b1)), xi);
+        aQ = acc_lane + 192 * (b0 & 63u);
+        aR = acc_lane + 192 * (b1 & 63u);
+        cP = cross(eQ, eR);
+      }
+      int u1 = lidx_of(byte_at(2));
+      V3 xc = coord(u1);
+      u1 = lidx_of(byte_at(3));
+#pragma unroll
+      for (int j = 2; j < NSTEP; ++j) {
+        if ((j & 1) == 0 && j >= nsteps) break;
+        const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
+        const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
+        if (__builtin_expect((pat >> j) & 1u, 0)) ustep(std::true_type{}, byte_at(j), xc);
+        else ustep(std::false_type{}, byte_at(j), xc);
+        xc = xn;
+        u1 = u2;
+      }
+    }
+    else {
+      auto step = [&](uint32_t byte, V3 xd) {
+        const bool swap = (byte & 0xC0u) == 0x40u;
+        const uint64_t em = (uint64_t)0 - (uint64_t)(byte < 0x80u);
+        double* const aD = acc_lane + 192 * (byte & 63u);
+        const V3 eD = sub(xd, xi);
+        const V3 cRn = sel(swap, cN, cP);
+        eP = sel(swap, eP, eQ);
+        aP = swap ? aP : aQ;
+        eQ = eR;
+        aQ = aR;
+        eR = eD;
+        aR = aD;
+        cP = cross(eQ, eR);
+        cN = cross(eP, eR);
+        const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
+        const double meas = fabs(dot(eP, cP));
+        const double s = keep(em, -recip1(6.0 * meas));
+        const double mass = keep(em, c0 * meas * (1.0 / 120.0));
+        macc += keep(em, meas);
+        block(aP, m, cP, s, mass);
+        block(aQ, m, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+        block(aR, m, cRn, s, mass);
+      };
+      int u1 = lidx_of(byte_at(0));
+      V3 xc = coord(u1);
+      u1 = lidx_of(byte_at(1));
+#pragma unroll
+      for (int j = 0; j < NSTEP; ++j) {
+        if ((j & 3) == 0 && j >= nsteps) break;
+        const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
+        const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
+        step(byte_at(j), xc);
+        xc = xn;
+        u1 = u2;
+      }
+    }
+    if (rhs && active) {
+      const double rv = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
+      rhs[3 * (int64_t)row + ci] = rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv;
+    }
+    wave_sync_lds();
+
+    // ---- diagonal block row, then the slice's complete blocks through one flat image
+    int fp = len;  // block prefix over the lanes (the same in the three waves)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(fp, o);
+      if (lane >= o) fp += t;
+    }
+    const int total = __shfl(fp, 63);  // blocks of the slice
+    fp -= len;
+    if (active) {
+      acc_lane[192 * dslot] = 0.0;
+      acc_lane[192 * dslot + 64] = 0.0;
+      acc_lane[192 * dslot + 128] = 0.0;
+    }
+    double rv[3 * MAXW];
+#pragma unroll
+    for (int t = 0; t < MAXW; ++t)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) rv[3 * t + k] = acc_lane[192 * min(t, W - 1) + 64 * k];
+    double sum[3] = { 0.0, 0.0, 0.0 };
+#pragma unroll
+    for (int t = 0; t < MAXW; ++t)
+      if (t < W)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sum[k] += rv[3 * t + k];
+    if (ci == 0) {
+      fps[lane] = fp;
+      rbs[lane] = active ? rb : 0;
+      for (int t = 0; t < len; ++t) bown[fp + t] = (uint8_t)lane;
+    }
+    __syncthreads();  // every wave's accumulator reads before the flat image overwrites them
+    double* const flat = acc_all;
+    // value (t, k) of the rotated frame = block column j = (ci + k) % 3; the
+    // block (row, t) holds 9 values: per block [i][j] at 9 t + 3 i + j, per
+    // row (CSR order) at 3 len i + 3 t + j
+    if (active) {
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t)
+        if (t < len) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const int j = k + ci < 3 ? k + ci : k + ci - 3;
+            const double v = t == (int)dslot ? -sum[k] + (k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0) : rv[3 * t + k];
+            flat[9 * fp + (per_block ? 9 * t + 3 * ci + j : 3 * len * ci + 3 * t + j)] = v;
+          }
+        }
+    }
+    if (tid == 0) claim[0] = t4;
+    __syncthreads();
+    const int64_t pn = uni(claim[0]);
+    // store: flat position P is value P - 9 fps[L] of row lane L = bown[P / 9]
+    for (int P = tid; P < 9 * total; P += 192) {
+      const int L = bown[P / 9];
+      vals[9 * rbs[L] + (P - 9 * fps[L])] = flat[P];
+    }
+    __syncthreads();
+    if (p1 >= r1) break;
+    p0 = p1;
+    p1 = p2;
+    p2 = p3;
+    p3 = pn;
+    R0 = R1;
+    R1 = R2;
+    R2 = R3;
+    cur = nxt;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) nid1[k] = nid2[k];
+  }
+}
+
 // ---------------------------------------------------------------- block-3 elasticity (TETRA4), row strips
 // K_rb^{ij} = [lambda c_r,i c_b,j + mu (c_r,j c_b,i + delta_ij c_r.c_b)] / (6|det|)
 // (+ c0 |det|/120 delta_ij, the consistent mass V/20 (1 + delta_rb) for b != r):
@@ -2071,7 +2426,45 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
     b.last_kernel = AFEM_KERNEL_ELAST3_GLOBAL;
     return;
   }
-  // persistent pipelined kernel (AFEM_ELAST_STRIP=0: the one-wave-per-item kernel, diagnostic)
+  // one workgroup (three waves) per slice (AFEM_ELAST_WG=0: one wave per (slice, component), diagnostic)
+  const char* we = getenv("AFEM_ELAST_WG");
+  const bool use_wg = !(we && atoi(we) == 0);
+  const int64_t ucap2 = (s.max_slice_nodes + 1) & ~int64_t(1);  // 16-B aligned column-index table
+  if (use_wg && s.rec_ok && s.max_strip_c <= 2 && s.max_slice_w <= 16 && s.max_slice_nodes <= 256 &&
+      s.nnz * 9 < (int64_t(1) << 40) && elast_wg_bytes(ucap2, s.max_slice_w) <= 160 * 1024) {
+    const size_t shm = (size_t)elast_wg_bytes(ucap2, s.max_slice_w);
+    static std::map<std::pair<const void*, size_t>, int> occ_wg;
+    const char* ue = getenv("AFEM_ASSEMBLY_UNIFORM");
+    const bool use_uni = !(ue && atoi(ue) == 0) && s.n_uni > 0;
+    if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);
+    AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
+    auto launch = [&](const void* fn, auto kern, int64_t n_items, const SliceRec* list, unsigned long long* tk) {
+      auto it = occ_wg.find({ fn, shm });
+      if (it == occ_wg.end()) {
+        int q = 0;
+        AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, fn, 192, shm));
+        it = occ_wg.emplace(std::make_pair(fn, shm), q < 1 ? 1 : q).first;
+      }
+      int64_t nblk = (int64_t)ctx.n_cu * it->second;
+      if (nblk > n_items) nblk = n_items < 8 ? 8 : n_items;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(192), shm, ctx.stream, n_items, list, tk, (int)ucap2,
+                         s.max_slice_w, b.order_per_block, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p,
+                         s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr,
+                         rhs_add);
+      AFEM_LAUNCHED();
+    };
+    if (use_uni)
+      launch(reinterpret_cast<const void*>(&k_assemble_elast_wg<2, 16, 1>), k_assemble_elast_wg<2, 16, 1>, s.n_uni,
+             s.rec_u.p, s.tickets.p);
+    const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;
+    if (n_mix > 0)
+      launch(reinterpret_cast<const void*>(&k_assemble_elast_wg<2, 16, 0>), k_assemble_elast_wg<2, 16, 0>, n_mix,
+             use_uni ? s.rec_m.p : s.rec_all.p, s.tickets.p + 128);
+    b.last_kernel = AFEM_KERNEL_ELAST3_WG;
+    return;
+  }
+  // persistent pipelined kernel, one wave per (slice, component) (AFEM_ELAST_STRIP=0: the
+  // one-wave-per-item kernel, diagnostic)
   const char* ee = getenv("AFEM_ELAST_STRIP");
   const bool use_new = !(ee && atoi(ee) == 0);
   if (use_new && s.rec_ok && s.max_strip_c <= 2 && s.max_slice_w <= 16 && s.max_slice_nodes <= 256 &&

@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 
 VAL_TOL = 1e-12
 SOL_TOL = 1e-10
-K_STRIP, K_TILE, K_GLOBAL, K_E3_STRIP, K_E3_ITEM, K_E3_GLOBAL, K_E2 = 1, 2, 3, 4, 5, 6, 7
+K_STRIP, K_TILE, K_GLOBAL, K_E3_STRIP, K_E3_ITEM, K_E3_GLOBAL, K_E2, K_E3_WG = 1, 2, 3, 4, 5, 6, 7, 8
 
 
 def _close(a, b, tol=VAL_TOL):
@@ -429,9 +429,13 @@ def test_fan_mesh_scalar_fallbacks(ctx, dim, m, kern):
     _close(ls.rhs_host(), 2 * orhs)
 
 
-@pytest.mark.parametrize("m,kern", [(40, K_E3_GLOBAL), (31, K_E3_GLOBAL), (12, K_E3_STRIP)])
+@pytest.mark.parametrize("m,kern,env", [(40, K_E3_GLOBAL, None), (31, K_E3_GLOBAL, None), (12, K_E3_WG, None),
+                                        (12, K_E3_STRIP, "AFEM_ELAST_WG"), (12, K_E3_ITEM, "AFEM_ELAST_STRIP")])
 @pytest.mark.parametrize("use_csr", [False, True])
-def test_fan_mesh_block3_fallback(ctx, m, kern, use_csr):
+def test_fan_mesh_block3_fallback(ctx, monkeypatch, m, kern, env, use_csr):
+    if env:  # the alternative kernels, forced
+        monkeypatch.setenv("AFEM_ELAST_WG", "0")
+        monkeypatch.setenv(env, "0")
     cells, coords = fan_mesh_3d(m, seed=2)
     n = coords.shape[0]
     mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)

@@ -83,6 +83,32 @@ def test_elasticity3d_uniform_variant_bitwise(ctx, monkeypatch, use_csr):
     assert np.array_equal(r_uni, r_gen)
 
 
+@pytest.mark.parametrize("which", ["bigbox", "box"])
+@pytest.mark.parametrize("use_csr", [False, True])
+def test_elasticity3d_workgroup_kernel_bitwise(ctx, monkeypatch, which, use_csr):
+    """The three-wave-per-slice kernel (k_assemble_elast_wg) against the
+    one-wave-per-(slice, component) kernel: the same arithmetic per entry (up
+    to the compiler's FMA contraction: last-bit differences)."""
+    mesh = _mesh(ctx, which)
+    bsr = af.BSRFormat(mesh, 3).initialize(use_csr)
+    bsr.computeSparsity()
+    n3 = 3 * mesh.n_own_nodes
+    drhs = ctx.malloc(8 * n3)
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
+    assert bsr.stats()["last_kernel"] == 8
+    v_wg, r_wg = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
+    monkeypatch.setenv("AFEM_ELAST_WG", "0")
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
+    assert bsr.stats()["last_kernel"] == 4
+    v_st, r_st = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
+    ctx.free(drhs)
+    dv = np.abs(v_wg - v_st).max() / np.abs(v_st).max()
+    dr = np.abs(r_wg - r_st).max() / np.abs(r_st).max()
+    print(f"wg vs strip: values max rel {dv:.2e} ({np.count_nonzero(v_wg != v_st)} of {v_st.size} differ), rhs {dr:.2e}")
+    # the same formulas; the compiler's FMA contraction may differ by kernel (last-bit differences)
+    assert dv <= 1e-15 and dr <= 1e-15
+
+
 def test_elasticity3d_plain_entry_point_equals_ex(ctx):
     mesh = af.Mesh.structured(ctx, 3, 4)
     b1 = af.BSRFormat(mesh, 3).initialize(False)

@@ -2,7 +2,7 @@
 set -e
 export TMPDIR=/tmp
 O=${1:-gpurun_out/c3_prof}
-K=k_assemble_elast_strip
+K=${2:-k_assemble_elast}
 C="python3 tools/c3_probe.py 170 5"
 mkdir -p $O
 timeout -k 5 150 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- $C > $O/t.log 2>&1
