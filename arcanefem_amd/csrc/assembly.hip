@@ -1088,7 +1088,13 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
 // (ci + k) % 3 of the block.  A cyclic axis permutation is a rotation, the
 // material isotropic: the entries are the same numbers (up to the order of
 // the three products in a dot product).
-template <int MAXC, int MAXW, int UMODE>
+// BIG: unstructured meshes (rows up to 32 slots, slices of more than 256
+// nodes, strips up to 64 steps): the nodes past the first 256 and the
+// column-index entries past the first 128 words are staged straight from
+// memory, and the write-back stores each lane's values directly (two passes
+// over the accumulators: diagonal sums, then values) instead of holding 3 x
+// MAXW values in registers for the flat image.
+template <int MAXC, int MAXW, int UMODE, bool BIG = false>
 __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, const SliceRec* __restrict__ recs,
                                                              unsigned long long* __restrict__ tickets, int u_cap,
                                                              int w_cap, bool per_block,
@@ -1183,11 +1189,24 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
       cxyz[3 * idx + 1] = ci == 0 ? b : (ci == 1 ? c : a);
       cxyz[3 * idx + 2] = ci == 0 ? c : (ci == 1 ? a : b);
     }
+    if (BIG && nu > 256) {
+      for (int u = lane + 256; u < nu; u += 64) {
+        const int64_t nd = snode[(int64_t)R0.snode_off + u];
+        const double a = coords[3 * nd], b = coords[3 * nd + 1], c = coords[3 * nd + 2];
+        cxyz[3 * u] = ci == 0 ? a : (ci == 1 ? b : c);
+        cxyz[3 * u + 1] = ci == 0 ? b : (ci == 1 ? c : a);
+        cxyz[3 * u + 2] = ci == 0 ? c : (ci == 1 ? a : b);
+      }
+    }
     {
       const int nq = 8 * W;
       u32x4* dst = reinterpret_cast<u32x4*>(li);
       dst[max(min(lane, nq - 1), 0)] = cur.l0;
       dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
+      if (BIG && nq > 128) {
+        const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R0.lidx_off);
+        for (int q = lane + 128; q < nq; q += 64) dst[q] = ls[q];
+      }
       double2* a2 = reinterpret_cast<double2*>(acc);
       for (int q = lane; q < 96 * W; q += 64) a2[q] = make_double2(0.0, 0.0);
     }
@@ -1336,6 +1355,30 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
   }
     wave_sync_lds();
 
+    if constexpr (BIG) {
+      // ---- diagonal block row (sums over the row's slots), then direct stores
+      if (active) {
+        acc_lane[192 * dslot] = 0.0;
+        acc_lane[192 * dslot + 64] = 0.0;
+        acc_lane[192 * dslot + 128] = 0.0;
+      }
+      double sum[3] = { 0.0, 0.0, 0.0 };
+      for (int t = 0; t < W; ++t)  // slots past the row's end hold 0
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sum[k] += acc_lane[192 * t + 64 * k];
+      if (active) {
+        for (int t = 0; t < len; ++t) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const int j = k + ci < 3 ? k + ci : k + ci - 3;
+            const double v =
+                t == (int)dslot ? -sum[k] + (k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0) : acc_lane[192 * t + 64 * k];
+            vals[per_block ? 9 * (rb + t) + 3 * ci + j : 9 * rb + 3 * (int64_t)ci * len + 3 * t + j] = v;
+          }
+        }
+      }
+    }
+    else {
     // ---- diagonal block row + write-back through a flat LDS image
     // (3*len values per lane; map: position -> lane | offset << 6 with the
     // value index = rbs[lane] + offset: per block 9 rb + 3 ci + (9 t + j),
@@ -1392,6 +1435,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
       const int Pc = min(64 * k + lane, total - 1);
       const int m = map[Pc];
       vals[rbs[m & 63] + (m >> 6)] = acc[Pc];
+    }
     }
     wave_sync_lds();
     if (p1 >= r1) break;
@@ -2417,8 +2461,36 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
   const double fx = f ? f[0] : 0.0, fy = f ? f[1] : 0.0, fz = f ? f[2] : 0.0;
   const int64_t shm_old = 3 * 8 * 64 * (int64_t)s.max_slice_w + ((24 * (int64_t)s.max_slice_nodes + 15) & ~int64_t(15)) +
                           2 * 64 * (int64_t)s.max_slice_w;
-  if (!s.strip_ok || s.max_slice_w > 16 || shm_old > 160 * 1024) {
-    // no row strips (high-valence nodes) or rows too long for the LDS tile
+  // unstructured meshes: rows up to 32 slots, slices beyond 256 nodes, strips up to 64 steps
+  const size_t shm_big = (size_t)elast_tile_bytes(s.max_slice_nodes, s.max_slice_w);
+  const bool big_ok = s.strip_ok && s.rec_ok && s.max_strip_c <= 4 && s.max_slice_w <= 32 &&
+                      shm_big <= 160 * 1024 && s.nnz * 9 < (int64_t(1) << 40);
+  const bool fits_small = s.strip_ok && s.max_slice_w <= 16 && shm_old <= 160 * 1024;
+  const char* be = getenv("AFEM_ELAST_BIG");  // 0: the global kernel instead (diagnostic)
+  if (!fits_small && big_ok && !(be && atoi(be) == 0)) {
+    static std::map<size_t, int> occ_big;
+    auto it = occ_big.find(shm_big);
+    if (it == occ_big.end()) {
+      int q = 0;
+      AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &q, reinterpret_cast<const void*>(&k_assemble_elast_strip<4, 32, 0, true>), 64, shm_big));
+      it = occ_big.emplace(shm_big, q < 1 ? 1 : q).first;
+    }
+    if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);
+    AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
+    const int64_t n_items = 3 * s.n_slices;
+    int64_t nblk = (int64_t)ctx.n_cu * it->second;
+    if (nblk > n_items) nblk = n_items < 8 ? 8 : n_items;
+    hipLaunchKernelGGL((k_assemble_elast_strip<4, 32, 0, true>), dim3((unsigned)nblk), dim3(64), shm_big, ctx.stream,
+                       n_items, s.rec_all.p, s.tickets.p, s.max_slice_nodes, s.max_slice_w, b.order_per_block,
+                       s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p, s.snode.p, b.mesh->coords.p, lambda,
+                       0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr, rhs_add);
+    AFEM_LAUNCHED();
+    b.last_kernel = AFEM_KERNEL_ELAST3_BIG;
+    return;
+  }
+  if (!fits_small) {
+    // no row strips (high-valence nodes) or rows / slices too large for any LDS tile
     hipLaunchKernelGGL(k_assemble_elast_tet_global, dim3((unsigned)(3 * s.n_slices)), dim3(64), 0, ctx.stream,
                        b.order_per_block, s.perm.p, s.row_ptr.p, s.cols.p, s.inc.p, s.inc_slice_ptr.p, s.inc_slice_k.p,
                        b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr, rhs_add);

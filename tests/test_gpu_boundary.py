@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 
 VAL_TOL = 1e-12
 SOL_TOL = 1e-10
-K_STRIP, K_TILE, K_GLOBAL, K_E3_STRIP, K_E3_ITEM, K_E3_GLOBAL, K_E2, K_E3_WG = 1, 2, 3, 4, 5, 6, 7, 8
+K_STRIP, K_TILE, K_GLOBAL, K_E3_STRIP, K_E3_ITEM, K_E3_GLOBAL, K_E2, K_E3_WG, K_E3_BIG = 1, 2, 3, 4, 5, 6, 7, 8, 9
 
 
 def _close(a, b, tol=VAL_TOL):

@@ -109,6 +109,45 @@ def test_elasticity3d_workgroup_kernel_bitwise(ctx, monkeypatch, which, use_csr)
     assert dv <= 1e-15 and dr <= 1e-15
 
 
+@pytest.mark.parametrize("levels", [2, 3])
+@pytest.mark.parametrize("use_csr", [False, True])
+def test_elasticity3d_unstructured_refined(ctx, monkeypatch, levels, use_csr):
+    """An unstructured mesh (the reference's L-shape-3D refined `levels` times:
+    irregular valences, rows longer than 16, Morton slices beyond 256 nodes at
+    3 levels) through the block-3 kernel for such meshes (AFEM_KERNEL_ELAST3_BIG)
+    against the oracle, and against the global-memory kernel."""
+    import bench
+
+    gm = read_gmsh(path("L-shape-3D.msh"))
+    cells, coords = bench.refine_tets(gm.cells, gm.coords, levels, "cpu")
+    mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    bsr = af.BSRFormat(mesh, 3).initialize(use_csr)
+    bsr.computeSparsity()
+    n = mesh.n_own_nodes
+    drhs = ctx.malloc(8 * 3 * n)
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
+    st = bsr.stats()
+    print("max_slice_width", st["max_slice_width"], "max_slice_nodes", st["max_slice_nodes"], "kernel",
+          st["last_kernel"])
+    assert st["last_kernel"] in (8, 9)
+    rows, cols, vals = bsr.download()
+    rhs = ctx.to_host(drhs, 3 * n, np.float64)
+    orp, ocols = O.sparsity(n, n, cells)
+    ovals, orhs = O.assemble_elasticity_tet(n, cells, coords, orp, ocols, LAM, MU2, 3.7e6, (0.5, -1.0, 2.0))
+    if use_csr:
+        ovals = O.blocks_to_row_order_k(orp, ovals, 3)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    assert np.abs(vals - ovals).max() <= VAL_TOL * np.abs(ovals).max()
+    assert np.abs(rhs - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+    monkeypatch.setenv("AFEM_ELAST_BIG", "0")
+    monkeypatch.setenv("AFEM_ELAST_WG", "0")
+    monkeypatch.setenv("AFEM_ELAST_STRIP", "0")
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
+    _, _, gvals = bsr.download()
+    ctx.free(drhs)
+    assert np.abs(vals - gvals).max() <= 1e-13 * np.abs(ovals).max()
+
+
 def test_elasticity3d_plain_entry_point_equals_ex(ctx):
     mesh = af.Mesh.structured(ctx, 3, 4)
     b1 = af.BSRFormat(mesh, 3).initialize(False)
