@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--c4-n", type=int, default=463, help="C4 Poisson box on one GPU (463 -> 99.9M DoF); 0: skip")
     ap.add_argument("--c5-n", type=int, default=100, help="C5 elastodynamics box (100 -> 1.03M nodes)")
     ap.add_argument("--c5-steps", type=int, default=5)
+    ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
+                    help="N > 1: the CG's transport (host: gloo callbacks, for rehearsing several ranks on one GPU)")
     ap.add_argument("--unstructured-levels", type=int, default=6,
                     help="refinements of L-shape-3D.msh for the unstructured leg (6 -> 12 M DoF); 0: skip")
     return ap.parse_args()
@@ -423,9 +425,14 @@ def main():
     n_own, n_cells = mesh.n_own_nodes, mesh.n_cells
     comm = None
     if world > 1:
-        uid = [af.Communicator.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = af.Communicator(ctx, world, rank, uid[0])
+        if args.comm == "host":
+            from arcanefem_amd.parallel import HostCommunicator
+
+            comm = HostCommunicator(ctx)
+        else:
+            uid = [af.Communicator.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = af.Communicator(ctx, world, rank, uid[0])
         ls.set_halo_structured(comm, mesh)
     setup_s = time.perf_counter() - t_setup
     step = make_step(ctx, bsr, ls, bottom, dbottom)
@@ -532,7 +539,7 @@ def main():
                 "n": n,
                 "dof_per_gpu": int(n_own),
                 "nnz_per_gpu": int(nnz),
-                "parallelism": f"z-slab x{world}, RCCL halo + all-reduce in CG",
+                "parallelism": f"z-slab x{world}, {'RCCL' if args.comm == 'rccl' else 'host-transport'} halo + all-reduce in CG",
             },
             "roofline": rf,
             "cpu_baseline": cpu,
