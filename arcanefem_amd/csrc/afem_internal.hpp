@@ -198,6 +198,13 @@ struct Structure {
   DevBuf<uint8_t> uslot;  // uniform list, in list order: the 32 common step bytes of each slice (scalar stream)
   DevBuf<SliceRec> rec_u, rec_m, rec_all;  // uniform / other / every slice, in processing order
   int64_t n_uni = 0, n_mix = 0;
+  // the scalar kernel's split of the other (general-instance) slices: small
+  // = at most 16 slots, 32 steps and kSmallSliceNodes nodes (the compact LDS
+  // tile, higher occupancy), big = the rest
+  DevBuf<SliceRec> rec_ms, rec_mb;
+  int64_t n_ms = 0, n_mb = 0;
+  int ms_nodes = 0, mb_nodes = 0, mb_w = 0;
+  int u_nodes = 0, u_w = 0;  // maxima over the uniform list (its LDS tile)
   bool rec_ok = false;                     // offsets fit the 32-bit record fields
   DevBuf<int64_t> pos_rb;                  // [n_slices*64] row_ptr of each position's row (0: idle)
   DevBuf<uint32_t> pos_dl;                 // [n_slices*64] diagonal slot | row length << 8

@@ -2318,10 +2318,12 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
     const bool uni_env = umode != 0;
     const bool use_uni = uni_env && s.n_uni > 0;
     const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;
-    if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);  // one counter per XCD, 128-B apart, per launch
+    if (s.tickets.n < 3 * 8 * 16) s.tickets.alloc(3 * 8 * 16);  // one counter per XCD, 128-B apart, per launch
     AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
     auto launch_s = [&](const void* fn, auto kern, int64_t n_list, const SliceRec* list, unsigned long long* tk,
-                        size_t shm_s, hipStream_t stream) {
+                        size_t shm_s, hipStream_t stream, int ucap = -1, int wcap = -1) {
+      if (ucap < 0) ucap = s.max_slice_nodes;
+      if (wcap < 0) wcap = s.max_slice_w;
       auto it = occ_s.find({ fn, shm_s });
       if (it == occ_s.end()) {
         int q = 0;
@@ -2332,7 +2334,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       int64_t nblk = (int64_t)ctx.n_cu * per_cu;
       if (nblk > n_list) nblk = n_list < 8 ? 8 : n_list;
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, stream, n_list, list, tk,
-                         s.max_slice_nodes, s.max_slice_w, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.strip_u.p,
+                         ucap, wcap, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.strip_u.p,
                          s.lidx.p, s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add,
                          reinterpret_cast<const SlotRec*>(s.uslot.p));
     };
@@ -2341,10 +2343,51 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   launch_s(reinterpret_cast<const void*>(&k_assemble_strip<NV_, C_, W_, U_>), k_assemble_strip<NV_, C_, W_, U_>, N_, \
            L_, T_, SHM_, ST_)
     const bool small = s.max_strip_c <= 2 && s.max_slice_w <= 16;
-    if (nv == 4) {
-      // the few mixed slices (domain edges, irregular rows) run on the side
-      // stream beside the uniform instance (fork / join through events): their
-      // launch and tail hide under the large kernel
+    if (nv == 4 && uni_env) {
+      // uniform slices on the context stream; the general-instance slices in
+      // two lists (compact / big: sparsity.hip) with their own LDS tiles.  With
+      // uniform slices the general lists run on the side stream beside the
+      // uniform instance (fork / join through events): their launch and tail
+      // hide under the large kernel; without (unstructured meshes) the
+      // compact list runs on the context stream and the big one beside it.
+      const bool has_u = s.n_uni > 0;
+      const bool fork = (has_u && (s.n_ms > 0 || s.n_mb > 0)) || (!has_u && s.n_ms > 0 && s.n_mb > 0);
+      hipStream_t side = ctx.stream;
+      if (fork) {
+        side = ctx.side();
+        AFEM_HIP(hipEventRecord(ctx.ev_fork, ctx.stream));
+        AFEM_HIP(hipStreamWaitEvent(side, ctx.ev_fork, 0));
+      }
+      const int ms_w = 16;
+      const size_t shm_ms = (size_t)strip_tile_bytes(dimc, s.ms_nodes, ms_w);
+      const size_t shm_mb = (size_t)strip_tile_bytes(dimc, s.mb_nodes, s.mb_w);
+      const bool mb_ok = s.mb_w <= 32 && s.n_mb >= 0 && shm_mb <= kTileLdsMax;
+      AFEM_REQUIRE(s.n_mb == 0 || (mb_ok && s.max_strip_c <= 4), AFEM_ERR_STATE, "strip lists exceed the kernels");
+      hipStream_t s_ms = has_u ? side : ctx.stream;
+      hipStream_t s_mb = has_u ? side : (s.n_ms > 0 ? side : ctx.stream);
+      if (s.n_ms > 0)
+        launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 0>), k_assemble_strip<4, 2, 16, 0>, s.n_ms,
+                 s.rec_ms.p, s.tickets.p + 128, shm_ms, s_ms, s.ms_nodes, ms_w);
+      if (s.n_mb > 0)
+        launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 4, 32, 0>), k_assemble_strip<4, 4, 32, 0>, s.n_mb,
+                 s.rec_mb.p, s.tickets.p + 256, shm_mb, s_mb, s.mb_nodes, s.mb_w);
+      if (has_u) {
+        const size_t shm_uu = (size_t)(8 * 64 * (int64_t)s.u_w + strip_coord_bytes(dimc, s.u_nodes, s.u_w));
+        if (umode == 2)
+          launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 2>), k_assemble_strip<4, 2, 16, 2>,
+                   s.n_uni, s.rec_u.p, s.tickets.p, shm_uu, ctx.stream, s.u_nodes, s.u_w);
+        else
+          launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 1>), k_assemble_strip<4, 2, 16, 1>,
+                   s.n_uni, s.rec_u.p, s.tickets.p, shm_uu, ctx.stream, s.u_nodes, s.u_w);
+      }
+      AFEM_LAUNCHED();
+      if (fork) {
+        AFEM_HIP(hipEventRecord(ctx.ev_join, side));
+        AFEM_HIP(hipStreamWaitEvent(ctx.stream, ctx.ev_join, 0));
+      }
+    }
+    else if (nv == 4) {
+      // every slice through the general instance (AFEM_ASSEMBLY_UNIFORM=0, diagnostic)
       const bool fork = use_uni && n_mix > 0;
       hipStream_t ms = ctx.stream;
       if (fork) {

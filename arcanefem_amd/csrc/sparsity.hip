@@ -1258,6 +1258,40 @@ void build_structure(Mesh& m, Structure& s)
       }
       s.n_uni = (int64_t)ru.size();
       s.n_mix = (int64_t)rm.size();
+      {
+        // general-instance slices: the compact ones (<= 16 slots, <= 32 steps,
+        // <= 352 nodes: 90 % of a Morton-ordered unstructured mesh) in their
+        // own list, so the big ones do not size the LDS tile of all
+        constexpr int kSmallSliceNodes = 352;
+        std::vector<SliceRec> ms, mb;
+        s.ms_nodes = s.mb_nodes = s.mb_w = 0;
+        for (const SliceRec& r : rm) {
+          const int nu = (int)(r.meta & 0xFFFFu), w = (int)((r.meta >> 16) & 0xFFu), st = (int)(r.meta >> 24);
+          if (w <= 16 && st <= 32 && nu <= kSmallSliceNodes) {
+            ms.push_back(r);
+            s.ms_nodes = std::max(s.ms_nodes, nu);
+          }
+          else {
+            mb.push_back(r);
+            s.mb_nodes = std::max(s.mb_nodes, nu);
+            s.mb_w = std::max(s.mb_w, w);
+          }
+        }
+        s.u_nodes = s.u_w = 0;
+        for (const SliceRec& r : ru) {
+          s.u_nodes = std::max(s.u_nodes, (int)(r.meta & 0xFFFFu));
+          s.u_w = std::max(s.u_w, (int)((r.meta >> 16) & 0xFFu));
+        }
+        s.n_ms = (int64_t)ms.size();
+        s.n_mb = (int64_t)mb.size();
+        auto up = [&](DevBuf<SliceRec>& d, const std::vector<SliceRec>& h) {
+          d.alloc(h.empty() ? 1 : h.size());
+          if (!h.empty())
+            AFEM_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(SliceRec), hipMemcpyHostToDevice, ctx.stream));
+        };
+        up(s.rec_ms, ms);
+        up(s.rec_mb, mb);
+      }
       auto upload = [&](DevBuf<SliceRec>& d, const std::vector<SliceRec>& h) {
         d.alloc(h.empty() ? 1 : h.size());
         if (!h.empty())
@@ -1268,6 +1302,16 @@ void build_structure(Mesh& m, Structure& s)
       if (!su.empty()) AFEM_HIP(hipMemcpyAsync(s.uslot.p, su.data(), su.size(), hipMemcpyHostToDevice, ctx.stream));
       upload(s.rec_m, rm);
       upload(s.rec_all, ra);
+      if (getenv("AFEM_DEBUG_SLICES")) {  // diagnostic: slice node counts and widths
+        std::vector<int64_t> nus(ns);
+        for (size_t i = 0; i < ns; ++i) nus[i] = hsn[i + 1] - hsn[i];
+        std::sort(nus.begin(), nus.end());
+        std::vector<int32_t> ws(hw.begin(), hw.end());
+        std::sort(ws.begin(), ws.end());
+        auto q = [&](const auto& v, double f) { return (long long)v[(size_t)(f * (double)(v.size() - 1))]; };
+        fprintf(stderr, "afem slices %zu nodes p50 %lld p90 %lld p99 %lld max %lld | width p50 %lld p90 %lld max %lld\n",
+                ns, q(nus, 0.5), q(nus, 0.9), q(nus, 0.99), q(nus, 1.0), q(ws, 0.5), q(ws, 0.9), q(ws, 1.0));
+      }
       if (getenv("AFEM_DEBUG_PATTERNS")) {  // diagnostic: strip patterns of the uniform slices
         std::map<std::pair<uint64_t, int>, int64_t> h;
         for (const SliceRec& r : ru) ++h[{ r.pat, (int)(r.meta >> 24) }];
