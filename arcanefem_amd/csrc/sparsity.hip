@@ -232,7 +232,7 @@ __global__ void k_count_valid(int64_t n, const int32_t* __restrict__ perm, unsig
 }
 
 // Meshes without a structured numbering: the processing order sorts the
-// owned nodes along a Morton (Z-order) curve of their coordinates, so the 64
+// owned nodes along a Hilbert curve of their coordinates, so the 64
 // rows of a slice are spatial neighbours (few distinct coupled nodes: the LDS
 // coordinate cache stays small, gathers stay in L2) whatever the caller's
 // numbering.  The matrix itself stays in the caller's node order.
@@ -269,19 +269,49 @@ __device__ __forceinline__ uint64_t spread3(uint64_t v)  // 21 bits -> every thi
   v = (v | v << 2) & 0x1249249249249249ull;
   return v;
 }
-__global__ void k_morton_keys(int64_t n, const double* __restrict__ coords, const unsigned long long* __restrict__ box,
-                              uint64_t* __restrict__ keys, int32_t* __restrict__ ids)
+// Hilbert index of a point of the 2^21-grid (Skilling's transpose algorithm:
+// undo the excess work, Gray-encode, interleave the transposed bits): unlike
+// the Morton curve it has no jumps, so 64 consecutive nodes form a compact
+// cluster (fewer coupled nodes per slice).
+__device__ __forceinline__ uint64_t hilbert3(uint32_t x, uint32_t y, uint32_t z)
+{
+  uint32_t X[3] = { x, y, z };
+  const uint32_t M = 1u << 20;
+  for (uint32_t Q = M; Q > 1; Q >>= 1) {
+    const uint32_t P = Q - 1;
+    for (int i = 0; i < 3; ++i) {
+      if (X[i] & Q) {
+        X[0] ^= P;
+      }
+      else {
+        const uint32_t t = (X[0] ^ X[i]) & P;
+        X[0] ^= t;
+        X[i] ^= t;
+      }
+    }
+  }
+  X[1] ^= X[0];
+  X[2] ^= X[1];
+  uint32_t t = 0;
+  for (uint32_t Q = M; Q > 1; Q >>= 1)
+    if (X[2] & Q) t ^= Q - 1;
+  for (int i = 0; i < 3; ++i) X[i] ^= t;
+  return spread3(X[0]) << 2 | spread3(X[1]) << 1 | spread3(X[2]);
+}
+// curve keys of the owned nodes: HILBERT (default) or Morton (AFEM_ORDER=morton)
+template <bool HILBERT>
+__global__ void k_curve_keys(int64_t n, const double* __restrict__ coords, const unsigned long long* __restrict__ box,
+                             uint64_t* __restrict__ keys, int32_t* __restrict__ ids)
 {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint64_t k = 0;
+  uint32_t q[3];
   for (int a = 0; a < 3; ++a) {
     const double lo = from_ordered_bits(box[a]), hi = from_ordered_bits(box[3 + a]);
     const double t = hi > lo ? (coords[3 * i + a] - lo) / (hi - lo) : 0.0;
-    const uint64_t q = (uint64_t)fmin(fmax(t * 2097151.0, 0.0), 2097151.0);
-    k |= spread3(q) << a;
+    q[a] = (uint32_t)fmin(fmax(t * 2097151.0, 0.0), 2097151.0);
   }
-  keys[i] = k;
+  keys[i] = HILBERT ? hilbert3(q[0], q[1], q[2]) : (spread3(q[0]) | spread3(q[1]) << 1 | spread3(q[2]) << 2);
   ids[i] = (int32_t)i;
 }
 __global__ void k_perm_from_sorted(int64_t n_pos, int64_t n_rows, const int32_t* __restrict__ sorted,
@@ -1025,7 +1055,7 @@ void build_structure(Mesh& m, Structure& s)
   else {
     s.n_slices = (n_rows + 63) / 64;
     s.perm.alloc(s.n_slices * 64);
-    // AFEM_ORDER=node: the caller's node order (diagnostic)
+    // AFEM_ORDER=node: the caller's node order; =morton: Morton curve (diagnostics)
     const char* oe = getenv("AFEM_ORDER");
     const bool node_order = (oe && std::string(oe) == "node") || n_rows < 2;
     if (node_order) {
@@ -1047,8 +1077,12 @@ void build_structure(Mesh& m, Structure& s)
       keys_out.alloc(n_rows);
       ids.alloc(n_rows);
       ids_out.alloc(n_rows);
-      hipLaunchKernelGGL(k_morton_keys, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, m.coords.p,
-                         box.p, keys.p, ids.p);
+      if (oe && std::string(oe) == "morton")
+        hipLaunchKernelGGL(k_curve_keys<false>, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows,
+                           m.coords.p, box.p, keys.p, ids.p);
+      else
+        hipLaunchKernelGGL(k_curve_keys<true>, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows,
+                           m.coords.p, box.p, keys.p, ids.p);
       AFEM_LAUNCHED();
       size_t tmp_bytes = 0;
       AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys.p, keys_out.p, ids.p, ids_out.p,

@@ -243,7 +243,7 @@ def refine_tets(cells, coords, levels, device):
 def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2):
     """An unstructured mesh at the C2 scale: the reference's L-shape-3D Gmsh
     mesh refined `levels` times (levels = 6: 68 M tets, 12 M DoF).  No brick
-    order, no uniform slices: Morton-curve slices and the general strip
+    order, no uniform slices: Hilbert-curve slices and the general strip
     instance.  Poisson assembly (+ source) on fixed sparsity, median kernel
     time, roofline as C2's."""
     from arcanefem_amd.gmsh import read_gmsh
@@ -270,7 +270,7 @@ def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2):
     kms = float(np.median([ctx.event_elapsed(240 + 2 * i, 241 + 2 * i) for i in range(reps)]))
     st = bsr.stats()
     out = {"config": f"{mesh_file} refined {levels}x ({mesh.n_own_nodes} DoF, {mesh.n_cells} tets, "
-                     f"max row length {st['max_row_len']}), Morton-ordered slices, Poisson assembly + source",
+                     f"max row length {st['max_row_len']}), Hilbert-ordered slices, Poisson assembly + source",
            "dof": int(mesh.n_own_nodes), "value": round(mesh.n_own_nodes / (kms * 1e-3) / 1e6, 1),
            "unit": "MDoF/s (assembly kernels)", "kernel_ms": round(kms, 4), "roofline": roofline(bsr, mesh, kms),
            "last_kernel": int(st["last_kernel"]), "max_slice_nodes": int(st["max_slice_nodes"]),

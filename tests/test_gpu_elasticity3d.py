@@ -113,7 +113,7 @@ def test_elasticity3d_workgroup_kernel_bitwise(ctx, monkeypatch, which, use_csr)
 @pytest.mark.parametrize("use_csr", [False, True])
 def test_elasticity3d_unstructured_refined(ctx, monkeypatch, levels, use_csr):
     """An unstructured mesh (the reference's L-shape-3D refined `levels` times:
-    irregular valences, rows longer than 16, Morton slices beyond 256 nodes at
+    irregular valences, rows longer than 16, Hilbert slices beyond 256 nodes at
     3 levels) through the block-3 kernel for such meshes (AFEM_KERNEL_ELAST3_BIG)
     against the oracle, and against the global-memory kernel."""
     import bench

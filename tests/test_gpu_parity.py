@@ -360,12 +360,13 @@ def test_spmv_matches_oracle(ctx):
 
 
 @pytest.mark.parametrize("dim,n", [(3, 12), (2, 40)])
-@pytest.mark.parametrize("order", ["morton", "node"])
+@pytest.mark.parametrize("order", ["hilbert", "morton", "node"])
 def test_random_node_permutation(ctx, monkeypatch, dim, n, order):
     # SURVEY §8d robustness variant: the structured mesh with a seeded random
-    # node and cell numbering; slices follow a Morton curve of the node
-    # coordinates (default) or the caller's node order (AFEM_ORDER=node, read
-    # at every computeSparsity); the assembled matrix must be the permuted
+    # node and cell numbering; slices follow a Hilbert curve of the node
+    # coordinates (default), a Morton curve (AFEM_ORDER=morton) or the
+    # caller's node order (AFEM_ORDER=node, read at every computeSparsity);
+    # the assembled matrix must be the permuted
     # matrix of the unpermuted box either way
     ref = O.structured_mesh(dim, n, jitter=0.2, seed=20250220)
     rng = np.random.default_rng(1234)
@@ -375,15 +376,15 @@ def test_random_node_permutation(ctx, monkeypatch, dim, n, order):
     coords = np.empty_like(ref["coords"])
     coords[p] = ref["coords"]
     mesh = af.Mesh.from_arrays(ctx, dim, cells, coords)
-    if order == "node":
-        monkeypatch.setenv("AFEM_ORDER", "node")
+    if order != "hilbert":
+        monkeypatch.setenv("AFEM_ORDER", order)
     bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
     st = bsr.stats()
     assert st["brick_order"] == 0
-    if order == "node":
+    if order != "hilbert":
         monkeypatch.delenv("AFEM_ORDER")
-    else:
-        # the Morton sort ran: a slice's rows are spatial neighbours, so it
+    if order != "node":
+        # the curve sort ran: a slice's rows are spatial neighbours, so it
         # couples to far fewer distinct nodes than 64 random rows would
         m2 = af.Mesh.from_arrays(ctx, dim, cells, coords)
         monkeypatch.setenv("AFEM_ORDER", "node")

@@ -1,5 +1,5 @@
 """Unstructured-mesh legs (the reference's L-shape-3D Gmsh mesh refined
-`levels` times, Morton-ordered slices): bench.unstructured_leg (Poisson) and,
+`levels` times, Hilbert-ordered slices): bench.unstructured_leg (Poisson) and,
 with --elasticity, the block-3 assembly on the same mesh.
 usage: python tools/unstructured_probe.py [levels] [--elasticity]"""
 import json
