@@ -279,6 +279,12 @@ struct LinearSystem {
   const int64_t* csr_rows = nullptr;
   const int32_t* csr_cols = nullptr;
   double* csr_vals = nullptr;
+  // node-row structure of a view that came from a BSRFormat with NB_DOF = blk_k
+  // (2 or 3; 0: none): the SpMV's column source (k_spmv_blk)
+  int blk_k = 0;
+  int64_t blk_n = 0;
+  const int64_t* blk_rows = nullptr;
+  const int32_t* blk_cols = nullptr;
   DevBuf<int64_t> own_rows;   // when the view came in the reference int32 layout
   DevBuf<int32_t> own_cols;
   DevBuf<double> own_vals;    // host-uploaded or COO-built matrix

@@ -655,6 +655,7 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
                "BSRFormat(toLinearSystem): the linear system's column space (n_cols_local) is smaller than the "
                "matrix columns (owned + ghost nodes x NB_DOF)");
   b->mesh->ctx->set_device();
+  ls->blk_k = 0;
   if (k == 1) {
     ls->csr_rows = b->s.row_ptr.p;
     ls->csr_cols = b->s.cols.p;
@@ -666,6 +667,10 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
     ls->csr_rows = b->csr_rows.p;
     ls->csr_cols = b->csr_cols.p;
     ls->csr_vals = b->order_per_block ? b->csr_vals.p : b->values.p;
+    ls->blk_k = k;  // the SpMV reads the node-row structure instead of the scalar columns
+    ls->blk_n = b->s.n_rows;
+    ls->blk_rows = b->s.row_ptr.p;
+    ls->blk_cols = b->s.cols.p;
   }
   ls->has_csr = true;
   ls->csr_from_coo = false;
@@ -877,6 +882,7 @@ int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows
   }
   ctx.sync();
   ls->csr_rows = ls->own_rows.p;
+  ls->blk_k = 0;
   ls->csr_n = nb_row;
   ls->csr_nnz = nb_nz;
   ls->has_csr = true;
@@ -991,6 +997,7 @@ int afem_ls_clear_values(afem_ls* ls)
   ls->has_csr = false;
   ls->csr_from_coo = false;
   ls->csr_rows = nullptr;
+  ls->blk_k = 0;
   ls->csr_cols = nullptr;
   ls->csr_vals = nullptr;
   ls->add_map.clear();

@@ -127,6 +127,10 @@ Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* pr
         l->csr_nnz = d->K.s.nnz * 9;
         l->csr_rows = d->K.csr_rows.p;
         l->csr_cols = d->K.csr_cols.p;
+        l->blk_k = 3;
+        l->blk_n = d->K.s.n_rows;
+        l->blk_rows = d->K.s.row_ptr.p;
+        l->blk_cols = d->K.s.cols.p;
       }
       d->ls.csr_vals = d->K.values.p;
       d->lsm.csr_vals = d->mvals.p;

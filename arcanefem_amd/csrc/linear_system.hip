@@ -418,6 +418,99 @@ __global__ __launch_bounds__(256) void k_spmv_v16(int64_t n_rows, const int64_t*
   }
 }
 
+// Node-block SpMV of an NB_DOF = K system held in BSRFormat's CSR order
+// (femutils/BSRFormat.h:194-256: scalar row K r + i holds the node row's
+// K * len values as [block s][j]).  The node-row structure (block offsets bp,
+// node columns bc) replaces the scalar column indices: 4 B per block instead
+// of 4 K^2 B, so a block-3 SpMV reads 76 B per block instead of 108 B.
+// 16 lanes per node row (lane t: blocks t, t + 16, ...), kBlkRpg node rows
+// per group with every load of the first pass issued before any use; the K
+// values of (row i, block s) are contiguous.  The K * kBlkRpg sums leave a
+// 16-lane reduction in lanes 0 .. K*kBlkRpg-1, which hold consecutive scalar
+// rows (one contiguous store).  DOT: block partial of x[r] * y[r].
+constexpr int kBlkRpg = 2;
+template <int K, bool DOT>
+__global__ __launch_bounds__(256) void k_spmv_blk(int64_t n_brows, const int64_t* __restrict__ bp,
+                                                  const int32_t* __restrict__ bc, const double* __restrict__ vals,
+                                                  const double* __restrict__ x, double* __restrict__ y,
+                                                  double* __restrict__ partial)
+{
+  const int l16 = threadIdx.x & 15;
+  const int64_t r0 = (((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4) * kBlkRpg;
+  int64_t b0[kBlkRpg];
+  int len[kBlkRpg];
+#pragma unroll
+  for (int i = 0; i < kBlkRpg; ++i) {
+    const int64_t r = r0 + i < n_brows ? r0 + i : n_brows - 1;
+    b0[i] = bp[r];
+    len[i] = r0 + i < n_brows ? (int)(bp[r + 1] - b0[i]) : 0;
+  }
+  double s[kBlkRpg][K];
+  {
+    int32_t c[kBlkRpg];
+    double v[kBlkRpg][K][K];
+#pragma unroll
+    for (int i = 0; i < kBlkRpg; ++i) {
+      const bool in = l16 < len[i];
+      const int64_t kb = in ? b0[i] + l16 : b0[0];
+      c[i] = in ? bc[kb] : 0;
+      const double* vr = vals + (in ? K * K * b0[i] + K * l16 : 0);
+#pragma unroll
+      for (int a = 0; a < K; ++a)
+#pragma unroll
+        for (int j = 0; j < K; ++j) v[i][a][j] = in ? vr[K * a * len[i] + j] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kBlkRpg; ++i) {
+      double xv[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) xv[j] = x[K * (int64_t)c[i] + j];
+#pragma unroll
+      for (int a = 0; a < K; ++a) {
+        double t = v[i][a][0] * xv[0];
+#pragma unroll
+        for (int j = 1; j < K; ++j) t = fma(v[i][a][j], xv[j], t);
+        s[i][a] = t;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kBlkRpg; ++i)
+    for (int t = l16 + 16; t < len[i]; t += 16) {
+      const int64_t cb = K * (int64_t)bc[b0[i] + t];
+      const double* vr = vals + K * K * b0[i] + K * t;
+#pragma unroll
+      for (int a = 0; a < K; ++a) {
+        double u = s[i][a];
+#pragma unroll
+        for (int j = 0; j < K; ++j) u = fma(vr[K * a * len[i] + j], x[cb + j], u);
+        s[i][a] = u;
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < kBlkRpg; ++i)
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) s[i][a] += __shfl_xor(s[i][a], o, 16);
+  double d = 0.0;
+  if (l16 < K * kBlkRpg) {
+    double si = s[0][0];
+#pragma unroll
+    for (int q = 1; q < K * kBlkRpg; ++q)
+      if (l16 == q) si = s[q / K][q % K];
+    const int64_t r = K * r0 + l16;
+    if (r < K * n_brows) {
+      y[r] = si;
+      if (DOT) d = x[r] * si;
+    }
+  }
+  if (DOT) {
+    double bs = block_sum(d);
+    if (threadIdx.x == 0) partial[blockIdx.x] = bs;
+  }
+}
+
 // Fallback for segments that do not fit LDS: one lane per row.
 template <bool DOT>
 __global__ __launch_bounds__(kThreads) void k_spmv_row(int64_t n_rows, const int64_t* __restrict__ rows,
@@ -819,11 +912,16 @@ __global__ __launch_bounds__(256) void k_block_ghost(int64_t n_rows, int rpb, co
 }
 
 struct SpmvPlan {
-  int rpb = 0;          // rows per block (0: row kernel, -1: vector CSR)
+  int rpb = 0;          // rows per block (0: row kernel, -1: vector CSR, -2: node blocks)
   bool wide = false;    // 16-B loads of the segment (aligned bases)
   bool unroll = false;  // k_spmv_stream4u
   int64_t max_seg = 0;
   int64_t nblocks = 0;
+  // rpb = -2: k_spmv_blk over the node-row structure (NB_DOF = blk_k)
+  int blk_k = 0;
+  int64_t blk_n = 0;
+  const int64_t* blk_rows = nullptr;
+  const int32_t* blk_cols = nullptr;
 };
 
 __global__ void k_block_seg(int64_t n_rows, int rpb, const int64_t* __restrict__ row_ptr, unsigned long long* out)
@@ -876,11 +974,44 @@ SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows, const int32_t*
   return pl;
 }
 
+// the node-block SpMV when the system came from a BSRFormat with NB_DOF 2 or 3
+// (AFEM_SPMV=csr or any other diagnostic mode keeps the scalar CSR kernels)
+SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
+{
+  SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, ls.n_rows, ls.csr_cols, ls.csr_vals);
+  const char* e = getenv("AFEM_SPMV");
+  if ((ls.blk_k == 2 || ls.blk_k == 3) && ls.blk_rows && ls.blk_n * ls.blk_k == ls.n_rows && ls.blk_n > 0 && !e) {
+    pl.rpb = -2;
+    pl.blk_k = ls.blk_k;
+    pl.blk_n = ls.blk_n;
+    pl.blk_rows = ls.blk_rows;
+    pl.blk_cols = ls.blk_cols;
+    pl.nblocks = (ls.blk_n + 16 * kBlkRpg - 1) / (16 * kBlkRpg);
+  }
+  return pl;
+}
+
 void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* rows, const int32_t* cols,
                  const double* vals, const double* x, double* y, double* partial, int64_t nnz = 0)
 {
   const unsigned nb = (unsigned)pl.nblocks;
-  if (pl.rpb < 0) {
+  if (pl.rpb == -2) {
+#define AFEM_BLK(K_)                                                                                               \
+  if (partial)                                                                                                    \
+    hipLaunchKernelGGL((k_spmv_blk<K_, true>), dim3(nb), dim3(256), 0, ctx.stream, pl.blk_n, pl.blk_rows,         \
+                       pl.blk_cols, vals, x, y, partial);                                                         \
+  else                                                                                                            \
+    hipLaunchKernelGGL((k_spmv_blk<K_, false>), dim3(nb), dim3(256), 0, ctx.stream, pl.blk_n, pl.blk_rows,        \
+                       pl.blk_cols, vals, x, y, partial);
+    if (pl.blk_k == 3) {
+      AFEM_BLK(3)
+    }
+    else {
+      AFEM_BLK(2)
+    }
+#undef AFEM_BLK
+  }
+  else if (pl.rpb < 0) {
     if (partial)
       hipLaunchKernelGGL(k_spmv_v16<true>, dim3(nb), dim3(256), 0, ctx.stream, n_rows, rows, cols, vals, x, y, partial);
     else
@@ -1015,6 +1146,7 @@ void ls_build_from_host_coo(LinearSystem& ls)
   ls.csr_rows = ls.own_rows.p;
   ls.csr_cols = ls.own_cols.p;
   ls.csr_vals = ls.own_vals.p;
+  ls.blk_k = 0;
 }
 
 void ls_apply_bcs(LinearSystem& ls)
@@ -1041,7 +1173,7 @@ void ls_spmv(LinearSystem& ls, const double* x, double* y)
   Ctx& ctx = *ls.ctx;
   require_csr(ls);
   if (ls.halo) halo_exchange(*ls.halo, ctx, const_cast<double*>(x));
-  SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, ls.n_rows, ls.csr_cols, ls.csr_vals);
+  SpmvPlan pl = plan_spmv_ls(ctx, ls);
   launch_spmv(ctx, pl, ls.n_rows, ls.csr_rows, ls.csr_cols, ls.csr_vals, x, y, nullptr, ls.csr_nnz);
 }
 
@@ -1118,7 +1250,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     ls.p.alloc(ls.n_cols);
     AFEM_HIP(hipMemsetAsync(ls.p.p, 0, ls.p.bytes(), ctx.stream));
   }
-  SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, n, ls.csr_cols, ls.csr_vals);
+  SpmvPlan pl = plan_spmv_ls(ctx, ls);
   const int64_t n_part = 2 * std::max<int64_t>(pl.nblocks, kVecBlocks);
   if (ls.partial.n < (size_t)n_part) ls.partial.alloc(n_part);
   if (ls.cons.n != (size_t)n) ls.cons.alloc(n);

@@ -268,3 +268,50 @@ def test_block_jacobi3_static_solve(ctx, which):
     for pc in xs:
         assert np.abs(xs[pc] - xo).max() <= 1e-8 * np.abs(xo).max(), pc
     print("iterations", its)
+
+
+def _blocks(rows, vals, k, use_csr):
+    """[nnz_b, k, k] blocks of a BSR value array in either layout
+    (femutils/BSRFormat.h:194-256: CSR order = per node row [i][s][j])."""
+    if not use_csr:
+        return vals.reshape(-1, k, k)
+    out = np.empty((rows[-1], k, k))
+    for r in range(rows.shape[0] - 1):
+        a, b = rows[r], rows[r + 1]
+        out[a:b] = vals[k * k * a:k * k * b].reshape(k, b - a, k).transpose(1, 0, 2)
+    return out
+
+
+@pytest.mark.parametrize("which", ["box", "slab", "lshape", "tri"])
+@pytest.mark.parametrize("use_csr", [False, True])
+@pytest.mark.parametrize("spmv", ["blk", "csr"])
+def test_block_spmv_matches_block_product(ctx, monkeypatch, which, use_csr, spmv):
+    # the node-block SpMV (k_spmv_blk: node columns instead of scalar ones)
+    # and the scalar CSR kernels (AFEM_SPMV=v16) against the block product
+    if spmv == "csr":
+        monkeypatch.setenv("AFEM_SPMV", "v16")
+    k = 2 if which == "tri" else 3
+    mesh = af.Mesh.structured(ctx, 2, 21, seed=3) if which == "tri" else _mesh(ctx, which)
+    bsr = af.BSRFormat(mesh, k).initialize(use_csr)
+    bsr.computeSparsity()
+    if k == 3:
+        bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, None, None)
+    else:
+        bsr.assembleElasticityP1(LAM, MU2)
+    ls = af.DoFLinearSystem().initialize(ctx, k * mesh.n_own_nodes, k * mesh.n_nodes)
+    bsr.toLinearSystem(ls)
+    rows, cols, vals = bsr.download()
+    x = np.random.default_rng(7).standard_normal(k * mesh.n_nodes)
+    dx = ctx.malloc(x.nbytes)
+    dy = ctx.malloc(8 * k * mesh.n_own_nodes)
+    ctx.to_device(dx, x)
+    ls.spmv(dx, dy)
+    y = ctx.to_host(dy, k * mesh.n_own_nodes, np.float64)
+    ctx.free(dx)
+    ctx.free(dy)
+    B = _blocks(rows, vals, k, use_csr)
+    xb = x.reshape(-1, k)[cols]                          # [nnz_b, k]
+    prod = np.einsum("sij,sj->si", B, xb)
+    yo = np.zeros((rows.shape[0] - 1, k))
+    np.add.at(yo, np.repeat(np.arange(rows.shape[0] - 1), np.diff(rows)), prod)
+    assert np.abs(y - yo.ravel()).max() <= 1e-13 * np.abs(yo).max()
