@@ -433,10 +433,13 @@ template <int K, bool DOT>
 __global__ __launch_bounds__(256) void k_spmv_blk(int64_t n_brows, const int64_t* __restrict__ bp,
                                                   const int32_t* __restrict__ bc, const double* __restrict__ vals,
                                                   const double* __restrict__ x, double* __restrict__ y,
-                                                  double* __restrict__ partial)
+                                                  double* __restrict__ partial,
+                                                  const int32_t* __restrict__ blist = nullptr)
 {
   const int l16 = threadIdx.x & 15;
-  const int64_t r0 = (((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4) * kBlkRpg;
+  // blist: the row blocks of this launch (the CG's interior / halo-boundary split)
+  const int64_t blk = blist ? (int64_t)blist[blockIdx.x] : xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t r0 = ((blk * 256 + threadIdx.x) >> 4) * kBlkRpg;
   int64_t b0[kBlkRpg];
   int len[kBlkRpg];
 #pragma unroll
@@ -1333,15 +1336,17 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   // of p is in flight (RCCL on the halo's stream), the rest after it lands
   // (host transport: the exchange completes in halo_begin; same split, so the
   // multi-rank GPU tests cover it)
-  const bool overlap = multi && pl.rpb > 0 && pl.wide && pl.unroll;
+  const bool overlap = multi && ((pl.rpb > 0 && pl.wide && pl.unroll) || pl.rpb == -2);
   int64_t n_int = 0;
   if (overlap) {
+    // scalar rows per launch block: kThreads (CSR-stream) or K * 32 (node blocks)
+    const int rpb = pl.rpb == -2 ? pl.blk_k * 16 * kBlkRpg : kThreads;
     const uint64_t key = (uint64_t)(uintptr_t)ls.csr_rows ^ ((uint64_t)(uintptr_t)ls.csr_cols << 1) ^
-                         ((uint64_t)n << 40) ^ (uint64_t)ls.csr_nnz;
+                         ((uint64_t)n << 40) ^ (uint64_t)ls.csr_nnz ^ ((uint64_t)rpb << 52);
     if (ls.blist_key != key) {
       DevBuf<uint8_t> fl;
       fl.alloc(pl.nblocks);
-      hipLaunchKernelGGL(k_block_ghost, dim3((unsigned)pl.nblocks), dim3(256), 0, ctx.stream, n, kThreads,
+      hipLaunchKernelGGL(k_block_ghost, dim3((unsigned)pl.nblocks), dim3(256), 0, ctx.stream, n, rpb,
                          ls.csr_rows, ls.csr_cols, fl.p);
       AFEM_LAUNCHED();
       std::vector<uint8_t> hf(pl.nblocks);
@@ -1373,17 +1378,26 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     const int par = it & 1;
     if (overlap) {
       const int64_t n_bd = pl.nblocks - n_int;
+      auto part = [&](int64_t nbk, int64_t off) {
+        if (nbk <= 0) return;
+        if (pl.rpb != -2)
+          hipLaunchKernelGGL(k_spmv_stream4u<true>, dim3((unsigned)nbk), dim3(kThreads), (size_t)pl.max_seg * 8,
+                             ctx.stream, n, ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p,
+                             ls.partial.p + off, ls.blist.p + off);
+        else if (pl.blk_k == 3)
+          hipLaunchKernelGGL((k_spmv_blk<3, true>), dim3((unsigned)nbk), dim3(256), 0, ctx.stream, pl.blk_n,
+                             pl.blk_rows, pl.blk_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p + off,
+                             ls.blist.p + off);
+        else
+          hipLaunchKernelGGL((k_spmv_blk<2, true>), dim3((unsigned)nbk), dim3(256), 0, ctx.stream, pl.blk_n,
+                             pl.blk_rows, pl.blk_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p + off,
+                             ls.blist.p + off);
+        AFEM_LAUNCHED();
+      };
       halo_begin(*ls.halo, ctx, ls.p.p);
-      if (n_int > 0)
-        hipLaunchKernelGGL(k_spmv_stream4u<true>, dim3((unsigned)n_int), dim3(kThreads), (size_t)pl.max_seg * 8,
-                           ctx.stream, n, ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p,
-                           ls.partial.p, ls.blist.p);
+      part(n_int, 0);
       halo_end(*ls.halo, ctx, ls.p.p);
-      if (n_bd > 0)
-        hipLaunchKernelGGL(k_spmv_stream4u<true>, dim3((unsigned)n_bd), dim3(kThreads), (size_t)pl.max_seg * 8,
-                           ctx.stream, n, ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p,
-                           ls.partial.p + n_int, ls.blist.p + n_int);
-      AFEM_LAUNCHED();
+      part(n_bd, n_int);
     }
     else {
       if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
