@@ -1294,7 +1294,7 @@ void build_structure(Mesh& m, Structure& s)
       s.n_mix = (int64_t)rm.size();
       {
         // general-instance slices: the compact ones (<= 16 slots, <= 32 steps,
-        // <= 352 nodes: 90 % of a Morton-ordered unstructured mesh) in their
+        // <= 352 nodes: 90 % of a Hilbert-ordered unstructured mesh) in their
         // own list, so the big ones do not size the LDS tile of all
         constexpr int kSmallSliceNodes = 352;
         std::vector<SliceRec> ms, mb;

@@ -217,7 +217,7 @@ typedef struct afem_bsr_stats {
   int64_t n_slices;         /* assembly slices (wavefronts per launch) */
   int32_t brick_order;      /* 1: slices are node bricks of a structured box: 4x4x4 interior bricks
                                (8x8 in 2D) and 8x8 tiles of the boundary faces; 0: slices follow a
-                               Morton-curve order of the node coordinates (plain node order under
+                               Hilbert-curve order of the node coordinates (plain node order under
                                AFEM_ORDER=node) */
   int32_t uniform_slices;   /* slices whose 64 rows share one strip topology (uniform-control assembly variant) */
   int32_t last_kernel;      /* AFEM_KERNEL_* that ran the last assembly of this matrix */
