@@ -1348,10 +1348,28 @@ void build_structure(Mesh& m, Structure& s)
       }
       if (getenv("AFEM_DEBUG_PATTERNS")) {  // diagnostic: strip patterns of the uniform slices
         std::map<std::pair<uint64_t, int>, int64_t> h;
-        for (const SliceRec& r : ru) ++h[{ r.pat, (int)(r.meta >> 24) }];
+        std::map<std::string, int64_t> hs2;  // pattern + steps + slot stream
+        for (size_t i = 0; i < ru.size(); ++i) {
+          const SliceRec& r = ru[i];
+          ++h[{ r.pat, (int)(r.meta >> 24) }];
+          char b[32];
+          snprintf(b, sizeof(b), "%016llx/%d/", (unsigned long long)r.pat, (int)(r.meta >> 24));
+          std::string k(b);
+          for (int t = 0; t < 32; ++t) {
+            snprintf(b, sizeof(b), "%02x", su[32 * i + t]);
+            k += b;
+          }
+          ++hs2[k];
+        }
         for (auto& kv : h)
           fprintf(stderr, "afem pattern 0x%016llx steps %d slices %lld\n", (unsigned long long)kv.first.first,
                   kv.first.second, (long long)kv.second);
+        std::vector<std::pair<int64_t, std::string>> top;
+        for (auto& kv : hs2) top.push_back({ kv.second, kv.first });
+        std::sort(top.rbegin(), top.rend());
+        fprintf(stderr, "afem pattern+slots: %zu distinct\n", top.size());
+        for (size_t i = 0; i < top.size() && i < 8; ++i)
+          fprintf(stderr, "afem  %lld  %s\n", (long long)top[i].first, top[i].second.c_str());
       }
       ctx.sync();
     }

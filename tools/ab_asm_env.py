@@ -1,0 +1,33 @@
+"""A/B of an assembly-time environment toggle (read at every assembly) in ONE
+process: one structure, the assembly timed with VAR=valA / VAR=valB
+interleaved (HIP events, median).
+usage: python tools/ab_asm_env.py VAR valA valB [n] [reps]"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import arcanefem_amd as af  # noqa: E402
+
+var, va, vb = sys.argv[1], sys.argv[2], sys.argv[3]
+n = int(sys.argv[4]) if len(sys.argv) > 4 else 215
+reps = int(sys.argv[5]) if len(sys.argv) > 5 else 20
+ctx = af.Context(0)
+mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+bsr = af.BSRFormat(mesh, 1).initialize(True)
+bsr.computeSparsity()
+ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes)
+times = {va: [], vb: []}
+for r in range(reps):
+    for v in (va, vb):
+        os.environ[var] = v
+        ctx.event_record(0)
+        bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
+        ctx.event_record(1)
+        ctx.synchronize()
+        if r >= 2:
+            times[v].append(ctx.event_elapsed(0, 1))
+for v in times:
+    print(f"{var}={v}: median {np.median(times[v]):.4f} ms  min {np.min(times[v]):.4f}", flush=True)
