@@ -1075,6 +1075,34 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
   AFEM_WT(1, __builtin_amdgcn_s_memrealtime());
 }
 
+// Shared factors of a step's three window blocks (rotated frame: component
+// row x; c_row = -m, the sign folded into s < 0):
+//   K_rb^{0j} = s [lambda m_x c_j + mu (m_j c_x + delta_0j m.c)] + delta_0j mass
+// lm = lambda m_x, mm = mu m once per step; per block 3 + 3 + 3 FP64 ops and
+// the scale s applied last (a uniform padding step's huge s meets only
+// finite products: no inf * 0).
+struct ElastPre {
+  double lm, l0;
+  V3 mm;
+};
+__device__ __forceinline__ ElastPre elast_pre(V3 m, double lambda, double mu)
+{
+  ElastPre e;
+  e.lm = lambda * m.x;
+  e.mm = V3{ mu * m.x, mu * m.y, mu * m.z };
+  e.l0 = e.lm + e.mm.x;
+  return e;
+}
+__device__ __forceinline__ void elast_block(double* a, const ElastPre& e, V3 c, double s, double mass)
+{
+  // explicit fma: one rounding sequence whatever the instance (the uniform and
+  // general instances, and the one-wave and workgroup kernels, agree bit for bit)
+  const double t = fma(e.mm.z, c.z, fma(e.mm.y, c.y, e.mm.x * c.x));
+  atomicAdd(a, fma(fma(e.l0, c.x, t), s, mass));
+  atomicAdd(a + 64, fma(e.lm, c.y, e.mm.y * c.x) * s);
+  atomicAdd(a + 128, fma(e.lm, c.z, e.mm.z * c.x) * s);
+}
+
 // ---------------------------------------------------------------- block-3 elasticity, persistent strips
 // k_assemble_elast_tet restructured like k_assemble_strip: persistent waves
 // claim work items (slice, component row ci) per XCD (the three items of a
@@ -1240,16 +1268,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
     auto sel = [](bool c, V3 a, V3 b) { return V3{ c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z }; };
     auto keep = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
     // entries (0, k) of K_rb in the rotated frame, c_r = -m (sign folded into s < 0)
-    auto block = [&](double* a, V3 m, V3 cb, double s, double mass) {
-      const double t = dot(m, cb);
-      const double A = lambda * m.x, B = mu * cb.x;
-      const double v0 = (A * cb.x + B * m.x) * s + (mu * t * s + mass);
-      const double v1 = (A * cb.y + B * m.y) * s;
-      const double v2 = (A * cb.z + B * m.z) * s;
-      atomicAdd(a, v0);
-      atomicAdd(a + 64, v1);
-      atomicAdd(a + 128, v2);
-    };
+    auto block = [&](double* a, const ElastPre& e, V3 cb, double s, double mass) { elast_block(a, e, cb, s, mass); };
     auto step = [&](uint32_t byte, V3 xd) {
       const bool swap = (byte & 0xC0u) == 0x40u;
       const uint64_t em = (uint64_t)0 - (uint64_t)(byte < 0x80u);
@@ -1269,9 +1288,10 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
       const double s = keep(em, -recip1(6.0 * meas));
       const double mass = keep(em, c0 * meas * (1.0 / 120.0));
       macc += keep(em, meas);
-      block(aP, m, cP, s, mass);
-      block(aQ, m, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
-      block(aR, m, cRn, s, mass);
+      const ElastPre e = elast_pre(m, lambda, mu);
+      block(aP, e, cP, s, mass);
+      block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+      block(aR, e, cRn, s, mass);
     };
     auto byte_at = [&](int j) -> uint32_t {
       const u32x4 w = cur.ch[j >> 4];
@@ -1309,9 +1329,10 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
         const double s = -recip1(6.0 * fmax(meas, 1e-300));
         const double mass = c0 * meas * (1.0 / 120.0);
         macc += meas;
-        block(aP, m, cP, s, mass);
-        block(aQ, m, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
-        block(aR, m, cRn, s, mass);
+        const ElastPre e = elast_pre(m, lambda, mu);
+        block(aP, e, cP, s, mass);
+        block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+        block(aR, e, cRn, s, mass);
       };
       {
         const uint32_t b0 = byte_at(0), b1 = byte_at(1);
@@ -1625,16 +1646,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     auto lidx_of = [&](uint32_t byte) { return (int)lrow[(byte & 63u) * 64]; };
     auto sel = [](bool c, V3 a, V3 b) { return V3{ c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z }; };
     auto keep = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
-    auto block = [&](double* a, V3 m, V3 cbv, double s, double mass) {
-      const double t = dot(m, cbv);
-      const double A = lambda * m.x, B = mu * cbv.x;
-      const double v0 = (A * cbv.x + B * m.x) * s + (mu * t * s + mass);
-      const double v1 = (A * cbv.y + B * m.y) * s;
-      const double v2 = (A * cbv.z + B * m.z) * s;
-      atomicAdd(a, v0);
-      atomicAdd(a + 64, v1);
-      atomicAdd(a + 128, v2);
-    };
+    auto block = [&](double* a, const ElastPre& e, V3 cb, double s, double mass) { elast_block(a, e, cb, s, mass); };
     auto byte_at = [&](int j) -> uint32_t {
       const u32x4 w = cur.ch[j >> 4];
       const int q = (j >> 2) & 3;
@@ -1668,9 +1680,10 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         const double s = -recip1(6.0 * fmax(meas, 1e-300));
         const double mass = c0 * meas * (1.0 / 120.0);
         macc += meas;
-        block(aP, m, cP, s, mass);
-        block(aQ, m, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
-        block(aR, m, cRn, s, mass);
+        const ElastPre e = elast_pre(m, lambda, mu);
+        block(aP, e, cP, s, mass);
+        block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+        block(aR, e, cRn, s, mass);
       };
       {
         const uint32_t b0 = byte_at(0), b1 = byte_at(1);
@@ -1714,9 +1727,10 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         const double s = keep(em, -recip1(6.0 * meas));
         const double mass = keep(em, c0 * meas * (1.0 / 120.0));
         macc += keep(em, meas);
-        block(aP, m, cP, s, mass);
-        block(aQ, m, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
-        block(aR, m, cRn, s, mass);
+        const ElastPre e = elast_pre(m, lambda, mu);
+        block(aP, e, cP, s, mass);
+        block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+        block(aR, e, cRn, s, mass);
       };
       int u1 = lidx_of(byte_at(0));
       V3 xc = coord(u1);
