@@ -2525,24 +2525,60 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
   const bool fits_small = s.strip_ok && s.max_slice_w <= 16 && shm_old <= 160 * 1024;
   const char* be = getenv("AFEM_ELAST_BIG");  // 0: the global kernel instead (diagnostic)
   if (!fits_small && big_ok && !(be && atoi(be) == 0)) {
-    static std::map<size_t, int> occ_big;
-    auto it = occ_big.find(shm_big);
-    if (it == occ_big.end()) {
-      int q = 0;
-      AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &q, reinterpret_cast<const void*>(&k_assemble_elast_strip<4, 32, 0, true>), 64, shm_big));
-      it = occ_big.emplace(shm_big, q < 1 ? 1 : q).first;
-    }
-    if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);
+    // three lists (sparsity.hip): uniform and compact slices (<= 16 slots, <= 32
+    // steps, <= 352 nodes) through the <2, 16> instance with a tile sized by
+    // their own maxima, the big ones through <4, 32> beside them on the side
+    // stream: the few large slices no longer set the LDS tile (and the
+    // occupancy) of all
+    static std::map<std::pair<const void*, size_t>, int> occ_big;
+    if (s.tickets.n < 3 * 8 * 16) s.tickets.alloc(3 * 8 * 16);
     AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
-    const int64_t n_items = 3 * s.n_slices;
-    int64_t nblk = (int64_t)ctx.n_cu * it->second;
-    if (nblk > n_items) nblk = n_items < 8 ? 8 : n_items;
-    hipLaunchKernelGGL((k_assemble_elast_strip<4, 32, 0, true>), dim3((unsigned)nblk), dim3(64), shm_big, ctx.stream,
-                       n_items, s.rec_all.p, s.tickets.p, s.max_slice_nodes, s.max_slice_w, b.order_per_block,
-                       s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p, s.snode.p, b.mesh->coords.p, lambda,
-                       0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr, rhs_add);
-    AFEM_LAUNCHED();
+    auto launch = [&](const void* fn, auto kern, int64_t n_list, const SliceRec* list, unsigned long long* tk,
+                      int ucap, int wcap, hipStream_t st) {
+      const size_t shm = (size_t)elast_tile_bytes(ucap, wcap);
+      auto it = occ_big.find({ fn, shm });
+      if (it == occ_big.end()) {
+        int q = 0;
+        AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, fn, 64, shm));
+        it = occ_big.emplace(std::make_pair(fn, shm), q < 1 ? 1 : q).first;
+      }
+      const int64_t n_items = 3 * n_list;
+      int64_t nblk = (int64_t)ctx.n_cu * it->second;
+      if (nblk > n_items) nblk = n_items < 8 ? 8 : n_items;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm, st, n_items, list, tk, ucap, wcap,
+                         b.order_per_block, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p, s.snode.p,
+                         b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr, rhs_add);
+      AFEM_LAUNCHED();
+    };
+    const int c_nodes = std::max(s.u_nodes, s.ms_nodes);
+    const bool split = s.n_mb < s.n_slices && elast_tile_bytes(c_nodes, 16) <= 160 * 1024 &&
+                       elast_tile_bytes(s.mb_nodes, s.mb_w) <= 160 * 1024;
+    if (!split) {
+      launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<4, 32, 0, true>), k_assemble_elast_strip<4, 32, 0, true>,
+             s.n_slices, s.rec_all.p, s.tickets.p, s.max_slice_nodes, s.max_slice_w, ctx.stream);
+    }
+    else {
+      const bool fork = s.n_mb > 0;
+      hipStream_t side = ctx.stream;
+      if (fork) {
+        side = ctx.side();
+        AFEM_HIP(hipEventRecord(ctx.ev_fork, ctx.stream));
+        AFEM_HIP(hipStreamWaitEvent(side, ctx.ev_fork, 0));
+      }
+      if (s.n_mb > 0)
+        launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<4, 32, 0, true>),
+               k_assemble_elast_strip<4, 32, 0, true>, s.n_mb, s.rec_mb.p, s.tickets.p + 256, s.mb_nodes, s.mb_w, side);
+      if (s.n_ms > 0)
+        launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16, 0, true>),
+               k_assemble_elast_strip<2, 16, 0, true>, s.n_ms, s.rec_ms.p, s.tickets.p + 128, c_nodes, 16, ctx.stream);
+      if (s.n_uni > 0)
+        launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16, 0, true>),
+               k_assemble_elast_strip<2, 16, 0, true>, s.n_uni, s.rec_u.p, s.tickets.p, c_nodes, 16, ctx.stream);
+      if (fork) {
+        AFEM_HIP(hipEventRecord(ctx.ev_join, side));
+        AFEM_HIP(hipStreamWaitEvent(ctx.stream, ctx.ev_join, 0));
+      }
+    }
     b.last_kernel = AFEM_KERNEL_ELAST3_BIG;
     return;
   }
