@@ -42,8 +42,6 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MDoF/s assembly + CG iter/s, Poisson-3D P1 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-ASM_KERNEL = "k_assemble_strip<4,2,16,uniform> + k_assemble_strip<4,2,16,general>"
-
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -116,8 +114,13 @@ def make_step(ctx, bsr, ls, bottom, dbottom):
 
 def roofline(bsr, mesh, kernel_ms):
     st = bsr.stats()
-    small = st["max_slice_width"] <= 16
-    kname = ASM_KERNEL if small else ASM_KERNEL.replace("<4,2,16,", "<4,4,32,")
+    # the instances the assembly launches: uniform slices, compact general
+    # slices, big general slices (> 16 slots / > 352 nodes, assembly.hip)
+    names = ["k_assemble_strip<4,2,16,uniform>"] if st["uniform_slices"] > 0 else []
+    names.append("k_assemble_strip<4,2,16,general>")
+    if st["max_slice_width"] > 16 or st["max_slice_nodes"] > 352:
+        names.append("k_assemble_strip<4,4,32,general>")
+    kname = " + ".join(names)
     nnz = bsr.view().nnz_blocks
     ab = algorithmic_bytes(int(st["n_incidences"]), mesh.n_nodes, mesh.n_own_nodes, nnz)
     achieved = ab / (kernel_ms * 1e-3) / 1e9
