@@ -132,6 +132,19 @@ def roofline(bsr, mesh, kernel_ms):
             "uniform_slice_frac": round(st["uniform_slices"] / max(st["n_slices"], 1), 4)}
 
 
+def pmc_traffic(path, n):
+    """HBM bytes per assembly launch from a committed PMC summary
+    (tools/collect_profiles.py) when it was taken at this size on one GPU."""
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+        if pm.get("n") == n and pm.get("world") in (None, 1):
+            return pm.get("hbm_bytes_per_launch"), pm.get("tag")
+    except (OSError, ValueError):
+        pass
+    return None, None
+
+
 def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50):
     """BASELINE config C4's problem (Poisson-3D at ~10^8 DoF) on ONE GPU: the
     north-star size.  Assembly kernel time = median of `reps` launches after
@@ -164,6 +177,8 @@ def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50):
            "cg_iter_per_s": round(ips, 2), "cg_roofline_frac": round(cg_bytes(nnz, mesh.n_own_nodes) * ips / 1e9
                                                                        / HBM_PEAK_GBS, 4),
            "cg_device_ms": round(st["solve_ms"], 2), "sparsity_ms": round(sp_ms, 1)}
+    out["roofline"]["traffic"], out["roofline"]["traffic_profile"] = pmc_traffic(
+        os.path.join(ROOT, "profiles", f"pmc_assembly_n{n}.json"), n)
     ctx.free(dbottom)
     ls.reset()
     bsr.close()
@@ -494,15 +509,10 @@ def main():
         rf = roofline(bsr, mesh, kmed)
         rf["kernel_ms_mean"] = round(float(np.mean(kernel_ms)), 4)
         rf["traffic"] = None
-        if os.path.exists(args.pmc_json):
-            try:
-                with open(args.pmc_json) as f:
-                    pm = json.load(f)
-                if pm.get("n") == n and pm.get("world") in (None, 1) and world == 1:
-                    rf["traffic"] = pm.get("hbm_bytes_per_launch")
-                    rf["traffic_profile"] = pm.get("tag")
-            except Exception:
-                rf["traffic"] = None
+        if world == 1:
+            rf["traffic"], tag = pmc_traffic(args.pmc_json, n)
+            if tag:
+                rf["traffic_profile"] = tag
         extras = {}
         if world == 1:
             # free the headline's buffers before the large side legs

@@ -50,7 +50,8 @@ def main():
     if fetch is not None and write is not None:
         hbm = (2.0 * fetch + write) * 1024.0
         lines.append(f"hbm_bytes_per_launch (2*FETCH_SIZE + WRITE_SIZE) KiB*1024 = {hbm:.6g}")
-        with open(os.path.join(out, "pmc_assembly_C2.json"), "w") as f:
+        pj = "pmc_assembly_C2.json" if n == 215 else f"pmc_assembly_n{n}.json"
+        with open(os.path.join(out, pj), "w") as f:
             json.dump({"n": n, "world": 1, "tag": tag, "fetch_kib": fetch, "write_kib": write,
                        "hbm_bytes_per_launch": int(hbm),
                        "method": "2*FETCH_SIZE + WRITE_SIZE (KiB), MI355X_MICROARCH.md HBM section"}, f, indent=1)

@@ -8,7 +8,7 @@ set -e
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/prof}
 K=${2:-k_assemble_strip}
-B="bench.py --steps 10 --warmup 2 --cg-iters 20 --no-cpu-baseline --no-extras"
+B=${B:-"bench.py --steps 10 --warmup 2 --cg-iters 20 --no-cpu-baseline --no-extras"}
 mkdir -p $OUT
 timeout -k 5 200 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1
 timeout -k 5 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-include-regex $K -f csv -d $OUT/pmc_sq -o run -- python3 $B > $OUT/pmc_sq.log 2>&1
