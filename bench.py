@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the C3 / C4 / C5 side measurements")
     ap.add_argument("--c3-n", type=int, default=170, help="C3 block-3 elasticity box (170 -> 5.0M nodes)")
     ap.add_argument("--c4-n", type=int, default=463, help="C4 Poisson box on one GPU (463 -> 99.9M DoF); 0: skip")
-    ap.add_argument("--c5-n", type=int, default=100, help="C5 elastodynamics box (100 -> 1.03M nodes)")
+    ap.add_argument("--c5-n", type=int, default=126, help="C5 elastodynamics box (126 -> 2.05M nodes, the config's ~2e6 per GPU)")
     ap.add_argument("--c5-steps", type=int, default=5)
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
                     help="N > 1: the CG's transport (host: gloo callbacks, for rehearsing several ranks on one GPU)")
