@@ -61,7 +61,7 @@ class BsrStats(ctypes.Structure):
 class SolverOpts(ctypes.Structure):
     _fields_ = [("method", ctypes.c_int32), ("max_iter", ctypes.c_int32), ("rtol", ctypes.c_double),
                 ("atol", ctypes.c_double), ("check_every", ctypes.c_int32), ("fixed_iterations", ctypes.c_int32),
-                ("initial_guess", ctypes.c_int32), ("precond_block", ctypes.c_int32)]
+                ("initial_guess", ctypes.c_int32), ("precond_block", ctypes.c_int32), ("multigrid", ctypes.c_int32)]
 
 
 class SolveStats(ctypes.Structure):

@@ -440,8 +440,11 @@ class DoFLinearSystem:
     def setSolverOptions(self, rtol=None, atol=None, max_iter=None, check_every=None, fixed_iterations=None,
                          method=None, initial_guess=None, preconditioner=None):
         """initial_guess: "zero" (default) or "current" (start the PCG from the
-        solution vector's values); preconditioner: "jacobi" (default) or
-        "block3" (3x3 node-block Jacobi, NB_DOF = 3 systems)."""
+        solution vector's values); preconditioner: "jacobi" (default),
+        "block3" (3x3 node-block Jacobi, NB_DOF = 3 systems), "multigrid"
+        (geometric multigrid V-cycle on structured boxes, one rank; rebuilt
+        every solve) or "multigrid-reuse" (built once, reused while the
+        matrix structure is unchanged)."""
         o = C.SolverOpts()
         call("afem_ls_get_solver_options", self.impl, ctypes.byref(o))
         if method is not None:
@@ -459,7 +462,8 @@ class DoFLinearSystem:
         if initial_guess is not None:
             o.initial_guess = {"zero": 0, "current": 1}[initial_guess]
         if preconditioner is not None:
-            o.precond_block = {"jacobi": 0, "block3": 3}[preconditioner]
+            o.precond_block, o.multigrid = {"jacobi": (0, 0), "block3": (3, 0), "multigrid": (0, 1),
+                                            "multigrid-reuse": (0, 2)}[preconditioner]
         call("afem_ls_set_solver_options", self.impl, ctypes.byref(o))
 
     def solve(self) -> dict:

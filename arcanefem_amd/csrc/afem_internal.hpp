@@ -266,6 +266,10 @@ void comm_allreduce(Comm* c, Ctx& ctx, double* d, int64_t n);
 bool comm_is_host(Comm* c);  // host-transport communicator (synchronous exchanges)
 
 // ------------------------------------------------------------------ linear system
+struct Multigrid;
+struct MgDeleter {
+  void operator()(Multigrid* m) const;
+};
 struct LinearSystem {
   Ctx* ctx = nullptr;
   int64_t n_rows = 0, n_cols = 0;
@@ -306,6 +310,10 @@ struct LinearSystem {
   DevBuf<uint8_t> cons;  // constraint-row flags of the stopping test
   double* pinned = nullptr;
   std::unique_ptr<Halo> halo;
+  // structured Kuhn box on one rank (BSR from Mesh.structured): the geometric
+  // multigrid preconditioner's fine grid (multigrid.hip); mg_k = NB_DOF, 0: none
+  int mg_k = 0, mg_nx = 0, mg_nz = 0;
+  std::unique_ptr<Multigrid, MgDeleter> mg;
 };
 
 // ------------------------------------------------------------------ kernels (host launchers)
@@ -323,6 +331,15 @@ void apply_neumann(Mesh& m, int k, int mode, const double* v, int64_t n_faces, c
                    const int32_t* face_cells, int mem, double* rhs);
 bool assembly_uses_lds(const Bsr& b);  // slice tile fits the LDS budget
 
+// geometric multigrid preconditioner (multigrid.hip)
+bool mg_available(const LinearSystem& ls);
+void mg_setup(LinearSystem& ls);                              // (re)build the hierarchy from the current matrix
+void mg_apply(LinearSystem& ls, const double* r, double* z);  // z = M^-1 r (one V-cycle)
+int mg_levels(const LinearSystem& ls);
+// node-block SpMV with an epilogue (linear_system.hip): epi 0: y = A x; 1: y = x + omega dinv (b - A x)
+// (a damped-Jacobi sweep); 2: y = b - A x.  NB_DOF k = 1, 2 or 3, values in BSRFormat's CSR order.
+void spmv_blk_epi(Ctx& ctx, int k, int epi, int64_t n_brows, const int64_t* bp, const int32_t* bc, const double* vals,
+                  const double* x, double* y, const double* b, const double* dinv, double omega);
 void ls_apply_bcs(LinearSystem& ls);
 void ls_solve(LinearSystem& ls, afem_solve_stats* st);
 void ls_spmv(LinearSystem& ls, const double* x, double* y);

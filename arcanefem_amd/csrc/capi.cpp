@@ -672,6 +672,13 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
     ls->blk_rows = b->s.row_ptr.p;
     ls->blk_cols = b->s.cols.p;
   }
+  // structured box on one rank: the multigrid preconditioner's fine grid
+  const StructuredInfo& st = b->mesh->st;
+  const bool box = st.valid && st.dim == 3 && st.nranks == 1 && b->mesh->nv == 4 && !b->mesh->part.valid;
+  ls->mg_k = box ? k : 0;
+  ls->mg_nx = box ? st.n : 0;
+  ls->mg_nz = box ? st.nz : 0;
+  ls->mg.reset();
   ls->has_csr = true;
   ls->csr_from_coo = false;
   ls->csr_n = b->s.n_rows * k;
@@ -747,6 +754,10 @@ int afem_ls_set_solver_options(afem_ls* ls, const afem_solver_opts* o)
   AFEM_REQUIRE(o->initial_guess == 0 || o->initial_guess == 1, AFEM_ERR_ARG, "initial_guess must be 0 or 1");
   AFEM_REQUIRE(o->precond_block == 0 || o->precond_block == 1 || o->precond_block == 3, AFEM_ERR_ARG,
                "precond_block must be 0, 1 or 3");
+  AFEM_REQUIRE(o->multigrid >= 0 && o->multigrid <= 2, AFEM_ERR_ARG, "multigrid must be 0, 1 or 2");
+  AFEM_REQUIRE(!(o->multigrid && o->precond_block == 3), AFEM_ERR_ARG,
+               "multigrid and block Jacobi are alternative preconditioners");
+  if (o->multigrid != ls->opts.multigrid) ls->mg.reset();
   ls->opts = *o;
   API_END
 }
@@ -883,6 +894,8 @@ int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows
   ctx.sync();
   ls->csr_rows = ls->own_rows.p;
   ls->blk_k = 0;
+  ls->mg_k = 0;
+  ls->mg.reset();
   ls->csr_n = nb_row;
   ls->csr_nnz = nb_nz;
   ls->has_csr = true;
@@ -998,6 +1011,8 @@ int afem_ls_clear_values(afem_ls* ls)
   ls->csr_from_coo = false;
   ls->csr_rows = nullptr;
   ls->blk_k = 0;
+  ls->mg_k = 0;
+  ls->mg.reset();
   ls->csr_cols = nullptr;
   ls->csr_vals = nullptr;
   ls->add_map.clear();
@@ -1081,6 +1096,10 @@ int afem_elastodynamics_set_solver_options(afem_elastodynamics* h, const afem_so
   AFEM_REQUIRE(o->max_iter >= 0 && o->rtol >= 0 && o->atol >= 0, AFEM_ERR_ARG, "bad solver options");
   AFEM_REQUIRE(o->precond_block == 0 || o->precond_block == 1 || o->precond_block == 3, AFEM_ERR_ARG,
                "precond_block must be 0, 1 or 3");
+  AFEM_REQUIRE(o->multigrid >= 0 && o->multigrid <= 2, AFEM_ERR_ARG, "multigrid must be 0, 1 or 2");
+  AFEM_REQUIRE(!(o->multigrid && o->precond_block == 3), AFEM_ERR_ARG,
+               "multigrid and block Jacobi are alternative preconditioners");
+  h->d->ls.mg.reset();
   h->d->ls.opts = *o;
   h->d->ls.opts.method = AFEM_SOLVER_PCG;
   API_END

@@ -132,6 +132,14 @@ Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* pr
         l->blk_rows = d->K.s.row_ptr.p;
         l->blk_cols = d->K.s.cols.p;
       }
+      {  // structured box on one rank: the solve may use the multigrid preconditioner
+        const StructuredInfo& st = mesh->st;
+        if (st.valid && st.dim == 3 && st.nranks == 1 && !mesh->part.valid) {
+          d->ls.mg_k = 3;
+          d->ls.mg_nx = st.n;
+          d->ls.mg_nz = st.nz;
+        }
+      }
       d->ls.csr_vals = d->K.values.p;
       d->lsm.csr_vals = d->mvals.p;
       halo_for(d->ls, d->comm, *mesh);

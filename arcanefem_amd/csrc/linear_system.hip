@@ -428,13 +428,16 @@ __global__ __launch_bounds__(256) void k_spmv_v16(int64_t n_rows, const int64_t*
 // values of (row i, block s) are contiguous.  The K * kBlkRpg sums leave a
 // 16-lane reduction in lanes 0 .. K*kBlkRpg-1, which hold consecutive scalar
 // rows (one contiguous store).  DOT: block partial of x[r] * y[r].
+// EPI (multigrid smoothing, multigrid.hip): 0 y = A x; 1 y = x + omega dinv (b - A x); 2 y = b - A x.
 constexpr int kBlkRpg = 2;
-template <int K, bool DOT>
+template <int K, bool DOT, int EPI = 0>
 __global__ __launch_bounds__(256) void k_spmv_blk(int64_t n_brows, const int64_t* __restrict__ bp,
                                                   const int32_t* __restrict__ bc, const double* __restrict__ vals,
                                                   const double* __restrict__ x, double* __restrict__ y,
                                                   double* __restrict__ partial,
-                                                  const int32_t* __restrict__ blist = nullptr)
+                                                  const int32_t* __restrict__ blist = nullptr,
+                                                  const double* __restrict__ b = nullptr,
+                                                  const double* __restrict__ dinv = nullptr, double omega = 0.0)
 {
   const int l16 = threadIdx.x & 15;
   // blist: the row blocks of this launch (the CG's interior / halo-boundary split)
@@ -504,7 +507,9 @@ __global__ __launch_bounds__(256) void k_spmv_blk(int64_t n_brows, const int64_t
       if (l16 == q) si = s[q / K][q % K];
     const int64_t r = K * r0 + l16;
     if (r < K * n_brows) {
-      y[r] = si;
+      if constexpr (EPI == 1) y[r] = x[r] + omega * dinv[r] * (b[r] - si);
+      else if constexpr (EPI == 2) y[r] = b[r] - si;
+      else y[r] = si;
       if (DOT) d = x[r] * si;
     }
   }
@@ -765,6 +770,19 @@ __global__ __launch_bounds__(kThreads) void k_cg_update(int64_t n, const double*
 }
 
 // beta = rz_new / rz_old ; p = z + beta p
+// x += alpha p, r -= alpha q (the multigrid-preconditioned PCG forms z separately)
+__global__ __launch_bounds__(kThreads) void k_cg_xr(int64_t n, const double* __restrict__ scal, int par,
+                                                    double* __restrict__ x, const double* __restrict__ p,
+                                                    double* __restrict__ r, const double* __restrict__ q)
+{
+  const double rz = scal[par], pq = scal[2];
+  const double alpha = (pq != 0.0) ? rz / pq : 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    x[i] += alpha * p[i];
+    r[i] -= alpha * q[i];
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void k_cg_dir(int64_t n, const double* __restrict__ scal, int par,
                                                      const double* __restrict__ z, double* __restrict__ p)
 {
@@ -977,6 +995,39 @@ SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows, const int32_t*
   return pl;
 }
 
+}  // namespace
+
+void spmv_blk_epi(Ctx& ctx, int k, int epi, int64_t n_brows, const int64_t* bp, const int32_t* bc, const double* vals,
+                  const double* x, double* y, const double* b, const double* dinv, double omega)
+{
+  const unsigned nb = (unsigned)((n_brows + 16 * kBlkRpg - 1) / (16 * kBlkRpg));
+  if (nb == 0) return;
+#define AFEM_EPI(K_, E_)                                                                                           \
+  hipLaunchKernelGGL((k_spmv_blk<K_, false, E_>), dim3(nb), dim3(256), 0, ctx.stream, n_brows, bp, bc, vals, x, y, \
+                     nullptr, nullptr, b, dinv, omega)
+#define AFEM_EPI_K(K_)       \
+  if (epi == 1)              \
+    AFEM_EPI(K_, 1);         \
+  else if (epi == 2)         \
+    AFEM_EPI(K_, 2);         \
+  else                       \
+    AFEM_EPI(K_, 0);
+  if (k == 3) {
+    AFEM_EPI_K(3)
+  }
+  else if (k == 2) {
+    AFEM_EPI_K(2)
+  }
+  else {
+    AFEM_EPI_K(1)
+  }
+#undef AFEM_EPI_K
+#undef AFEM_EPI
+  AFEM_LAUNCHED();
+}
+
+namespace {
+
 // the node-block SpMV when the system came from a BSRFormat with NB_DOF 2 or 3
 // (AFEM_SPMV=csr or any other diagnostic mode keeps the scalar CSR kernels)
 SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
@@ -1150,6 +1201,8 @@ void ls_build_from_host_coo(LinearSystem& ls)
   ls.csr_cols = ls.own_cols.p;
   ls.csr_vals = ls.own_vals.p;
   ls.blk_k = 0;
+  ls.mg_k = 0;
+  ls.mg.reset();
 }
 
 void ls_apply_bcs(LinearSystem& ls)
@@ -1275,8 +1328,23 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
                        ls.csr_cols, ls.csr_vals, ls.cons.p, ls.dinv.p, ls.binv.p);
     AFEM_LAUNCHED();
   }
+  // geometric multigrid (structured box, one rank); other systems: point Jacobi
+  const bool use_mg = ls.opts.multigrid != 0 && !blk3 && !multi && mg_available(ls);
+  if (use_mg) mg_setup(ls);
   // r = b - A x0, z = M^-1 r, p = z and the r.z partials (all rows, free rows)
   auto cg_init = [&]() {
+    if (use_mg) {
+      hipLaunchKernelGGL(k_cg_init, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.q.p, ls.r.p, ls.z.p,
+                         ls.p.p, ls.dinv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
+      AFEM_LAUNCHED();
+      mg_apply(ls, ls.r.p, ls.z.p);
+      AFEM_HIP(hipMemcpyAsync(ls.p.p, ls.z.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
+      // r.z over all rows for both references (the constraint rows' z is r_i / a_ii: negligible)
+      hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.r.p, ls.z.p, ls.partial.p);
+      hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.r.p, ls.z.p, ls.partial.p + vb);
+      AFEM_LAUNCHED();
+      return;
+    }
     if (blk3)
       hipLaunchKernelGGL(k_cg_init_b3, dim3(vb3), dim3(kThreads), 0, ctx.stream, nb3, ls.rhs.p, ls.q.p, ls.r.p,
                          ls.z.p, ls.p.p, ls.binv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
@@ -1328,7 +1396,8 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   const afem_solver_opts& o = ls.opts;
   const bool fixed = o.fixed_iterations > 0;
   const int max_it = fixed ? o.fixed_iterations : o.max_iter;
-  const int check = o.check_every > 0 ? o.check_every : 8;
+  // a multigrid iteration costs ~5 SpMVs: test every 2 iterations (a host sync is ~20 us)
+  const int check = use_mg ? std::min(o.check_every > 0 ? o.check_every : 8, 2) : (o.check_every > 0 ? o.check_every : 8);
   double rel = rz0 > 0 ? std::sqrt(std::fabs(ls.pinned[0] / rz0)) : 0.0;
   int it = 0;
   bool converged = fixed ? false : (ls.pinned[0] == 0.0 || rel <= o.rtol);
@@ -1406,7 +1475,15 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
 
     reduce_to(ctx, ls.partial.p, pl.nblocks, scal + 2);
     if (comm) comm_allreduce(comm, ctx, scal + 2, 1);
-    if (blk3)
+    if (use_mg) {
+      hipLaunchKernelGGL(k_cg_xr, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p, ls.r.p,
+                         ls.q.p);
+      AFEM_LAUNCHED();
+      mg_apply(ls, ls.r.p, ls.z.p);
+      hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.r.p, ls.z.p, ls.partial.p);
+      AFEM_LAUNCHED();
+    }
+    else if (blk3)
       hipLaunchKernelGGL(k_cg_update_b3, dim3(vb3), dim3(kThreads), 0, ctx.stream, nb3, scal, par, ls.sol.p, ls.p.p,
                          ls.r.p, ls.q.p, ls.z.p, ls.binv.p, ls.partial.p);
     else

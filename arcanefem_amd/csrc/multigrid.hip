@@ -1,0 +1,583 @@
+// Geometric multigrid preconditioner for the PCG (afem_solver_opts.multigrid)
+// on systems assembled on a structured Kuhn box on one rank (Mesh.structured:
+// node (x, y, z) = x + (nx+1)(y + (ny+1) z), every cube split into the six
+// tetrahedra around its main diagonal).
+//
+// The reference's GPU solve is Hypre PCG + BoomerAMG (femutils/
+// HypreDoFLinearSystem.cc:387-762); this is the structured-grid counterpart,
+// built from the assembled matrix alone (no physics on the coarse levels):
+//  * hierarchy: the box with every other node, while the cell counts stay
+//    even; the Kuhn triangulation of the half grid is nested in the fine one,
+//    so the coarse hat function of node I is the fine-grid function with value
+//    1 at node 2I and 1/2 at the 14 fine nodes 2I +- e (e in {0,1}^3 \ 0, the
+//    midpoints of the coarse Kuhn edges at I) -- P is that interpolation in
+//    index space (exact P1 interpolation without jitter), R = P^T;
+//  * coarse operators A_c = P^T A P (Galerkin), formed by a deterministic
+//    per-coarse-row kernel on the coarse Kuhn stencil (15 node blocks per row,
+//    the exact sparsity of P^T A P for nested Kuhn grids); penalty rows carry
+//    over by themselves;
+//  * smoothing: damped Jacobi, omega = 4 / (3 lambda_max(D^-1 A)) from a power
+//    iteration per level, 2 sweeps before and 2 after (symmetric V-cycle);
+//  * coarsest level: dense inverse (<= kDenseMax DoF, symmetric scaling +
+//    Cholesky on the host at setup), else 16 Jacobi sweeps;
+//  * constraint rows (penalty / eliminated, the PCG's `cons` flags) are taken
+//    out of the cycle: z = F V(F r) + C D^-1 r (F free, C constraint masks), so
+//    the preconditioner stays SPD and eliminated rows keep a zero direction.
+#include "afem_internal.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+namespace afem {
+
+namespace {
+
+inline unsigned grid_for(int64_t n, int threads) { return (unsigned)((n + threads - 1) / threads); }
+
+constexpr int kDenseMax = 512;  // DoF of a coarsest level inverted densely
+constexpr int kSweeps = 2;       // pre- and post-smoothing sweeps
+constexpr int kCoarseSweeps = 16;
+constexpr int kPowerIts = 12;
+
+struct Dims {
+  int nx, ny, nz;  // cells per axis
+  __host__ __device__ int64_t nodes() const { return (int64_t)(nx + 1) * (ny + 1) * (nz + 1); }
+  __host__ __device__ int64_t id(int x, int y, int z) const { return x + (int64_t)(nx + 1) * (y + (int64_t)(ny + 1) * z); }
+  __host__ __device__ bool in(int x, int y, int z) const
+  {
+    return x >= 0 && y >= 0 && z >= 0 && x <= nx && y <= ny && z <= nz;
+  }
+};
+
+// self + the 14 Kuhn edge directions (monotone e in {0,1}^3 \ 0, both signs)
+__constant__ int c_st[15][3] = { { 0, 0, 0 },   { 1, 0, 0 },   { 0, 1, 0 },  { 0, 0, 1 },  { 1, 1, 0 },
+                                 { 1, 0, 1 },   { 0, 1, 1 },   { 1, 1, 1 },  { -1, 0, 0 }, { 0, -1, 0 },
+                                 { 0, 0, -1 },  { -1, -1, 0 }, { -1, 0, -1 }, { 0, -1, -1 }, { -1, -1, -1 } };
+const int h_st[15][3] = { { 0, 0, 0 },  { 1, 0, 0 },   { 0, 1, 0 },   { 0, 0, 1 },   { 1, 1, 0 },
+                          { 1, 0, 1 },  { 0, 1, 1 },   { 1, 1, 1 },   { -1, 0, 0 },  { 0, -1, 0 },
+                          { 0, 0, -1 }, { -1, -1, 0 }, { -1, 0, -1 }, { 0, -1, -1 }, { -1, -1, -1 } };
+
+__device__ __forceinline__ void decompose(const Dims& d, int64_t n, int& x, int& y, int& z)
+{
+  x = (int)(n % (d.nx + 1));
+  const int64_t q = n / (d.nx + 1);
+  y = (int)(q % (d.ny + 1));
+  z = (int)(q / (d.ny + 1));
+}
+
+// A_c = P^T A P, one thread per coarse node row (fixed loop order: deterministic)
+template <int K>
+__global__ void k_mg_galerkin(Dims fd, Dims cd, const int64_t* __restrict__ fbp, const int32_t* __restrict__ fbc,
+                              const double* __restrict__ fv, const int64_t* __restrict__ cbp,
+                              const int32_t* __restrict__ cbc, double* __restrict__ cv, int* __restrict__ err)
+{
+  const int64_t I = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (I >= cd.nodes()) return;
+  int cx, cy, cz;
+  decompose(cd, I, cx, cy, cz);
+  const int64_t c0 = cbp[I];
+  const int clen = (int)(cbp[I + 1] - c0);
+  for (int o = 0; o < 15; ++o) {
+    const int fx = 2 * cx + c_st[o][0], fy = 2 * cy + c_st[o][1], fz = 2 * cz + c_st[o][2];
+    if (!fd.in(fx, fy, fz)) continue;
+    const double wi = o == 0 ? 1.0 : 0.5;
+    const int64_t fi = fd.id(fx, fy, fz);
+    const int64_t f0 = fbp[fi];
+    const int flen = (int)(fbp[fi + 1] - f0);
+    for (int s = 0; s < flen; ++s) {
+      int jx, jy, jz;
+      decompose(fd, fbc[f0 + s], jx, jy, jz);
+      const int a = jx & 1, b = jy & 1, c = jz & 1;
+      const int px = jx >> 1, py = jy >> 1, pz = jz >> 1;
+      const int np = (a | b | c) ? 2 : 1;
+      const double w = wi * (np == 2 ? 0.5 : 1.0);
+      for (int p = 0; p < np; ++p) {
+        const int32_t J = (int32_t)cd.id(px + p * a, py + p * b, pz + p * c);
+        int t = -1;
+        for (int q = 0; q < clen; ++q)
+          if (cbc[c0 + q] == J) {
+            t = q;
+            break;
+          }
+        if (t < 0) {
+          *err = 1;
+          continue;
+        }
+        for (int u = 0; u < K; ++u)
+          for (int v = 0; v < K; ++v)
+            cv[K * K * c0 + K * u * clen + K * t + v] += w * fv[K * K * f0 + K * u * flen + K * s + v];
+      }
+    }
+  }
+}
+
+// r_c = P^T r_f
+template <int K>
+__global__ void k_mg_restrict(Dims fd, Dims cd, const double* __restrict__ rf, double* __restrict__ rc)
+{
+  const int64_t I = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (I >= cd.nodes()) return;
+  int cx, cy, cz;
+  decompose(cd, I, cx, cy, cz);
+  double acc[K];
+  for (int u = 0; u < K; ++u) acc[u] = 0.0;
+  for (int o = 0; o < 15; ++o) {
+    const int fx = 2 * cx + c_st[o][0], fy = 2 * cy + c_st[o][1], fz = 2 * cz + c_st[o][2];
+    if (!fd.in(fx, fy, fz)) continue;
+    const double w = o == 0 ? 1.0 : 0.5;
+    const int64_t fi = fd.id(fx, fy, fz);
+    for (int u = 0; u < K; ++u) acc[u] += w * rf[K * fi + u];
+  }
+  for (int u = 0; u < K; ++u) rc[K * I + u] = acc[u];
+}
+
+// x_f += P x_c
+template <int K>
+__global__ void k_mg_prolong(Dims fd, Dims cd, const double* __restrict__ xc, double* __restrict__ xf)
+{
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= fd.nodes()) return;
+  int x, y, z;
+  decompose(fd, f, x, y, z);
+  const int a = x & 1, b = y & 1, c = z & 1;
+  const int64_t P0 = cd.id(x >> 1, y >> 1, z >> 1);
+  if (a | b | c) {
+    const int64_t P1 = cd.id((x >> 1) + a, (y >> 1) + b, (z >> 1) + c);
+    for (int u = 0; u < K; ++u) xf[K * f + u] += 0.5 * (xc[K * P0 + u] + xc[K * P1 + u]);
+  }
+  else {
+    for (int u = 0; u < K; ++u) xf[K * f + u] += xc[K * P0 + u];
+  }
+}
+
+// point-Jacobi diagonal of a coarse level (its node-diagonal block's diagonal)
+template <int K>
+__global__ void k_mg_dinv(int64_t n_nodes, const int64_t* __restrict__ bp, const int32_t* __restrict__ bc,
+                          const double* __restrict__ v, double* __restrict__ dinv)
+{
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_nodes) return;
+  const int64_t b0 = bp[r];
+  const int len = (int)(bp[r + 1] - b0);
+  int s = 0;
+  for (int q = 0; q < len; ++q)
+    if (bc[b0 + q] == (int32_t)r) s = q;
+  for (int u = 0; u < K; ++u) {
+    const double d = v[K * K * b0 + K * u * len + K * s + u];
+    dinv[K * r + u] = d != 0.0 ? 1.0 / d : 0.0;
+  }
+}
+
+__global__ void k_mg_scale(int64_t n, double omega, const double* __restrict__ dinv, const double* __restrict__ b,
+                           double* __restrict__ x)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = omega * dinv[i] * b[i];
+}
+
+// F r (constraint rows zeroed)
+__global__ void k_mg_mask(int64_t n, const uint8_t* __restrict__ cons, const double* __restrict__ r,
+                          double* __restrict__ b)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    b[i] = cons[i] ? 0.0 : r[i];
+}
+
+// z = F z + C D^-1 r
+__global__ void k_mg_fix(int64_t n, const uint8_t* __restrict__ cons, const double* __restrict__ r,
+                         const double* __restrict__ dinv, double* __restrict__ z)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (cons[i]) z[i] = r[i] * dinv[i];
+}
+
+__global__ void k_mg_fill(int64_t n, double* __restrict__ v)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    v[i] = 0.5 + (double)(h & 0xFFFF) / 65536.0;
+  }
+}
+
+// w = dinv .* w, block partials of w.w
+__global__ void k_mg_dscale_dot(int64_t n, const double* __restrict__ dinv, double* __restrict__ w,
+                                double* __restrict__ partial)
+{
+  __shared__ double sh[256];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double t = dinv[i] * w[i];
+    w[i] = t;
+    s += t * t;
+  }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+// block partials of v.v
+__global__ void k_mg_norm2(int64_t n, const double* __restrict__ v, double* __restrict__ partial)
+{
+  __shared__ double sh[256];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    s += v[i] * v[i];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+__global__ void k_mg_mul(int64_t n, double a, double* __restrict__ v)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    v[i] *= a;
+}
+
+// x = Ainv b (dense, coarsest level)
+__global__ void k_mg_gemv(int n, const double* __restrict__ A, const double* __restrict__ b, double* __restrict__ x)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int j = 0; j < n; ++j) s += A[(int64_t)i * n + j] * b[j];
+  x[i] = s;
+}
+
+constexpr int kVec = 1024;  // grid of the vector kernels
+
+}  // namespace
+
+struct MgLevel {
+  Dims d{};
+  int64_t nn = 0, n = 0;  // nodes, scalar rows (k * nodes)
+  const int64_t* bp = nullptr;
+  const int32_t* bc = nullptr;
+  const double* v = nullptr;
+  const double* dinv = nullptr;
+  DevBuf<int64_t> own_bp;
+  DevBuf<int32_t> own_bc;
+  DevBuf<double> own_v, own_dinv;
+  DevBuf<double> x, t, b, r;  // iterate (ping-pong x / t), right-hand side, residual
+  double omega = 0.0;
+};
+
+struct Multigrid {
+  int k = 1;
+  std::vector<MgLevel> lv;
+  DevBuf<double> ainv;  // dense inverse of the coarsest level (n_dense x n_dense) or empty
+  int n_dense = 0;
+  DevBuf<double> partial;
+  // reuse key (multigrid = 2): the fine structure the hierarchy was built for
+  const void* key_rows = nullptr;
+  const void* key_vals = nullptr;
+  int64_t key_n = 0;
+};
+
+void MgDeleter::operator()(Multigrid* m) const { delete m; }
+
+bool mg_available(const LinearSystem& ls)
+{
+  if (ls.mg_k < 1 || ls.mg_k > 3 || ls.mg_nx < 2 || ls.mg_nz < 2) return false;
+  if (ls.mg_nx % 2 || ls.mg_nz % 2) return false;  // no coarse level
+  if (ls.halo) return false;                        // one rank
+  const Dims d{ ls.mg_nx, ls.mg_nx, ls.mg_nz };
+  if (d.nodes() * ls.mg_k != ls.n_rows) return false;
+  if (ls.mg_k == 1 ? !ls.csr_rows : (ls.blk_k != ls.mg_k || !ls.blk_rows)) return false;
+  return true;
+}
+
+int mg_levels(const LinearSystem& ls) { return ls.mg ? (int)ls.mg->lv.size() : 0; }
+
+namespace {
+
+template <class F>
+void dispatch_k(int k, F&& f)
+{
+  if (k == 3) f(std::integral_constant<int, 3>{});
+  else if (k == 2) f(std::integral_constant<int, 2>{});
+  else f(std::integral_constant<int, 1>{});
+}
+
+void coarse_structure(const Dims& d, std::vector<int64_t>& bp, std::vector<int32_t>& bc)
+{
+  const int64_t n = d.nodes();
+  bp.assign(n + 1, 0);
+  bc.clear();
+  bc.reserve(n * 15);
+  std::vector<int32_t> row;
+  for (int z = 0; z <= d.nz; ++z)
+    for (int y = 0; y <= d.ny; ++y)
+      for (int x = 0; x <= d.nx; ++x) {
+        row.clear();
+        for (int o = 0; o < 15; ++o) {
+          const int X = x + h_st[o][0], Y = y + h_st[o][1], Z = z + h_st[o][2];
+          if (d.in(X, Y, Z)) row.push_back((int32_t)d.id(X, Y, Z));
+        }
+        std::sort(row.begin(), row.end());
+        bc.insert(bc.end(), row.begin(), row.end());
+        bp[d.id(x, y, z) + 1] = (int64_t)bc.size();
+      }
+}
+
+double host_sum(Ctx& ctx, const DevBuf<double>& partial, int n)
+{
+  std::vector<double> h(n);
+  AFEM_HIP(hipMemcpyAsync(h.data(), partial.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  double s = 0.0;
+  for (double v : h) s += v;
+  return s;
+}
+
+// lambda_max(D^-1 A) by power iteration (x, t as work vectors)
+double power_lambda(Ctx& ctx, Multigrid& mg, MgLevel& L)
+{
+  const int k = mg.k;
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
+  hipLaunchKernelGGL(k_mg_fill, dim3(g), dim3(256), 0, ctx.stream, L.n, L.x.p);
+  AFEM_LAUNCHED();
+  double lam = 0.0, nv = 0.0;
+  hipLaunchKernelGGL(k_mg_norm2, dim3(g), dim3(256), 0, ctx.stream, L.n, L.x.p, mg.partial.p);
+  AFEM_LAUNCHED();
+  nv = std::sqrt(host_sum(ctx, mg.partial, (int)g));
+  for (int it = 0; it < kPowerIts; ++it) {
+    spmv_blk_epi(ctx, k, 0, L.nn, L.bp, L.bc, L.v, L.x.p, L.t.p, nullptr, nullptr, 0.0);
+    hipLaunchKernelGGL(k_mg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, L.dinv, L.t.p, mg.partial.p);
+    AFEM_LAUNCHED();
+    const double nw = std::sqrt(host_sum(ctx, mg.partial, (int)g));
+    lam = nv > 0 ? nw / nv : 0.0;
+    if (!(nw > 0)) break;
+    hipLaunchKernelGGL(k_mg_mul, dim3(g), dim3(256), 0, ctx.stream, L.n, 1.0 / nw, L.t.p);
+    AFEM_LAUNCHED();
+    std::swap(L.x, L.t);
+    nv = 1.0;
+  }
+  return lam;
+}
+
+// dense inverse of the coarsest operator: symmetric diagonal scaling, Cholesky,
+// inverse (host; <= kDenseMax DoF)
+bool dense_inverse(Ctx& ctx, Multigrid& mg, MgLevel& L)
+{
+  const int k = mg.k;
+  const int m = (int)L.n;
+  std::vector<int64_t> bp(L.nn + 1);
+  AFEM_HIP(hipMemcpyAsync(bp.data(), L.bp, (L.nn + 1) * 8, hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  const int64_t nb = bp[L.nn];
+  std::vector<int32_t> bc(nb);
+  std::vector<double> v((size_t)nb * k * k);
+  AFEM_HIP(hipMemcpyAsync(bc.data(), L.bc, nb * 4, hipMemcpyDeviceToHost, ctx.stream));
+  AFEM_HIP(hipMemcpyAsync(v.data(), L.v, v.size() * 8, hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  std::vector<double> A((size_t)m * m, 0.0);
+  for (int64_t r = 0; r < L.nn; ++r) {
+    const int len = (int)(bp[r + 1] - bp[r]);
+    for (int s = 0; s < len; ++s)
+      for (int u = 0; u < k; ++u)
+        for (int w = 0; w < k; ++w)
+          A[(size_t)(k * r + u) * m + k * bc[bp[r] + s] + w] = v[k * k * bp[r] + k * u * len + k * s + w];
+  }
+  std::vector<double> sc(m);
+  for (int i = 0; i < m; ++i) {
+    if (!(A[(size_t)i * m + i] > 0)) return false;
+    sc[i] = 1.0 / std::sqrt(A[(size_t)i * m + i]);
+  }
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < m; ++j) A[(size_t)i * m + j] *= sc[i] * sc[j];
+  // Cholesky A = L L^T (lower, in place)
+  for (int j = 0; j < m; ++j) {
+    double d = A[(size_t)j * m + j];
+    for (int q = 0; q < j; ++q) d -= A[(size_t)j * m + q] * A[(size_t)j * m + q];
+    if (!(d > 0)) return false;
+    d = std::sqrt(d);
+    A[(size_t)j * m + j] = d;
+    for (int i = j + 1; i < m; ++i) {
+      double s = A[(size_t)i * m + j];
+      for (int q = 0; q < j; ++q) s -= A[(size_t)i * m + q] * A[(size_t)j * m + q];
+      A[(size_t)i * m + j] = s / d;
+    }
+  }
+  // inverse column by column: solve L L^T x = e_c
+  std::vector<double> inv((size_t)m * m), y(m);
+  for (int c = 0; c < m; ++c) {
+    for (int i = 0; i < m; ++i) {
+      double s = i == c ? 1.0 : 0.0;
+      for (int q = 0; q < i; ++q) s -= A[(size_t)i * m + q] * y[q];
+      y[i] = s / A[(size_t)i * m + i];
+    }
+    for (int i = m - 1; i >= 0; --i) {
+      double s = y[i];
+      for (int q = i + 1; q < m; ++q) s -= A[(size_t)q * m + i] * y[q];
+      y[i] = s / A[(size_t)i * m + i];
+    }
+    for (int i = 0; i < m; ++i) inv[(size_t)i * m + c] = y[i] * sc[i] * sc[c];
+  }
+  mg.ainv.alloc((size_t)m * m);
+  AFEM_HIP(hipMemcpyAsync(mg.ainv.p, inv.data(), inv.size() * 8, hipMemcpyHostToDevice, ctx.stream));
+  ctx.sync();
+  mg.n_dense = m;
+  return true;
+}
+
+}  // namespace
+
+void mg_setup(LinearSystem& ls)
+{
+  Ctx& ctx = *ls.ctx;
+  AFEM_REQUIRE(mg_available(ls), AFEM_ERR_STATE, "multigrid: not a structured single-rank system");
+  const bool reuse = ls.opts.multigrid == 2;
+  const void* krows = ls.mg_k == 1 ? (const void*)ls.csr_rows : (const void*)ls.blk_rows;
+  if (reuse && ls.mg && ls.mg->key_rows == krows && ls.mg->key_vals == ls.csr_vals && ls.mg->key_n == ls.n_rows)
+    return;
+  auto mg = std::unique_ptr<Multigrid, MgDeleter>(new Multigrid());
+  const int k = ls.mg_k;
+  mg->k = k;
+  mg->partial.alloc(kVec);
+  {
+    MgLevel L;
+    L.d = Dims{ ls.mg_nx, ls.mg_nx, ls.mg_nz };
+    L.nn = L.d.nodes();
+    L.n = k * L.nn;
+    L.bp = k == 1 ? ls.csr_rows : ls.blk_rows;
+    L.bc = k == 1 ? ls.csr_cols : ls.blk_cols;
+    L.v = ls.csr_vals;
+    L.dinv = ls.dinv.p;  // computed by ls_solve (k_inv_diag) before the setup
+    mg->lv.push_back(std::move(L));
+  }
+  DevBuf<int> err;
+  err.alloc(1);
+  AFEM_HIP(hipMemsetAsync(err.p, 0, sizeof(int), ctx.stream));
+  while (true) {
+    const MgLevel& F = mg->lv.back();
+    if (F.n <= kDenseMax || F.d.nx % 2 || F.d.ny % 2 || F.d.nz % 2 || F.d.nx < 2 || F.d.nz < 2) break;
+    MgLevel C;
+    C.d = Dims{ F.d.nx / 2, F.d.ny / 2, F.d.nz / 2 };
+    C.nn = C.d.nodes();
+    C.n = k * C.nn;
+    std::vector<int64_t> hbp;
+    std::vector<int32_t> hbc;
+    coarse_structure(C.d, hbp, hbc);
+    C.own_bp.alloc(hbp.size());
+    C.own_bc.alloc(hbc.size());
+    AFEM_HIP(hipMemcpyAsync(C.own_bp.p, hbp.data(), hbp.size() * 8, hipMemcpyHostToDevice, ctx.stream));
+    AFEM_HIP(hipMemcpyAsync(C.own_bc.p, hbc.data(), hbc.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+    C.own_v.alloc(hbc.size() * k * k);
+    AFEM_HIP(hipMemsetAsync(C.own_v.p, 0, C.own_v.bytes(), ctx.stream));
+    C.own_dinv.alloc(C.n);
+    const unsigned g = (unsigned)grid_for(C.nn, 128);
+    dispatch_k(k, [&](auto kc) {
+      constexpr int K = decltype(kc)::value;
+      hipLaunchKernelGGL(k_mg_galerkin<K>, dim3(g), dim3(128), 0, ctx.stream, F.d, C.d, F.bp, F.bc, F.v, C.own_bp.p,
+                         C.own_bc.p, C.own_v.p, err.p);
+      AFEM_LAUNCHED();
+      hipLaunchKernelGGL(k_mg_dinv<K>, dim3(g), dim3(128), 0, ctx.stream, C.nn, C.own_bp.p, C.own_bc.p, C.own_v.p,
+                         C.own_dinv.p);
+      AFEM_LAUNCHED();
+    });
+    C.bp = C.own_bp.p;
+    C.bc = C.own_bc.p;
+    C.v = C.own_v.p;
+    C.dinv = C.own_dinv.p;
+    ctx.sync();  // the host structure vectors go out of scope
+    mg->lv.push_back(std::move(C));
+  }
+  int herr = 0;
+  AFEM_HIP(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  AFEM_REQUIRE(!herr, AFEM_ERR_STATE, "multigrid: Galerkin product outside the coarse Kuhn stencil");
+  for (MgLevel& L : mg->lv) {
+    L.x.alloc(L.n);
+    L.t.alloc(L.n);
+    L.b.alloc(L.n);
+    L.r.alloc(L.n);
+    const double lam = power_lambda(ctx, *mg, L);
+    L.omega = lam > 0 ? 4.0 / (3.0 * 1.05 * lam) : 0.6;
+  }
+  MgLevel& Lc = mg->lv.back();
+  if (mg->lv.size() > 1 && Lc.n <= kDenseMax) dense_inverse(ctx, *mg, Lc);
+  mg->key_rows = krows;
+  mg->key_vals = ls.csr_vals;
+  mg->key_n = ls.n_rows;
+  ls.mg = std::move(mg);
+}
+
+namespace {
+
+// `sweeps` damped-Jacobi sweeps on level L from x = 0 (first sweep: omega D^-1 b)
+// or from the current iterate; the result is left in L.x
+void smooth(Ctx& ctx, Multigrid& mg, MgLevel& L, const double* b, int sweeps, bool from_zero)
+{
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
+  int s = 0;
+  if (from_zero) {
+    hipLaunchKernelGGL(k_mg_scale, dim3(g), dim3(256), 0, ctx.stream, L.n, L.omega, L.dinv, b, L.x.p);
+    AFEM_LAUNCHED();
+    s = 1;
+  }
+  for (; s < sweeps; ++s) {
+    spmv_blk_epi(ctx, mg.k, 1, L.nn, L.bp, L.bc, L.v, L.x.p, L.t.p, b, L.dinv, L.omega);
+    std::swap(L.x, L.t);
+  }
+}
+
+void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
+{
+  MgLevel& L = mg.lv[l];
+  if (l + 1 == mg.lv.size()) {
+    if (mg.n_dense == L.n && l > 0) {
+      hipLaunchKernelGGL(k_mg_gemv, dim3((unsigned)((L.n + 127) / 128)), dim3(128), 0, ctx.stream, (int)L.n,
+                         mg.ainv.p, b, L.x.p);
+      AFEM_LAUNCHED();
+    }
+    else {
+      smooth(ctx, mg, L, b, l == 0 ? 2 * kSweeps : kCoarseSweeps, true);
+    }
+    return;
+  }
+  MgLevel& C = mg.lv[l + 1];
+  smooth(ctx, mg, L, b, kSweeps, true);
+  spmv_blk_epi(ctx, mg.k, 2, L.nn, L.bp, L.bc, L.v, L.x.p, L.r.p, b, nullptr, 0.0);
+  dispatch_k(mg.k, [&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    hipLaunchKernelGGL(k_mg_restrict<K>, dim3((unsigned)grid_for(C.nn, 256)), dim3(256), 0, ctx.stream, L.d, C.d,
+                       L.r.p, C.b.p);
+    AFEM_LAUNCHED();
+  });
+  vcycle(ctx, mg, l + 1, C.b.p);
+  dispatch_k(mg.k, [&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    hipLaunchKernelGGL(k_mg_prolong<K>, dim3((unsigned)grid_for(L.nn, 256)), dim3(256), 0, ctx.stream, L.d, C.d,
+                       C.x.p, L.x.p);
+    AFEM_LAUNCHED();
+  });
+  smooth(ctx, mg, L, b, kSweeps, false);
+}
+
+}  // namespace
+
+void mg_apply(LinearSystem& ls, const double* r, double* z)
+{
+  Ctx& ctx = *ls.ctx;
+  Multigrid& mg = *ls.mg;
+  MgLevel& L0 = mg.lv[0];
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L0.n + 255) / 256);
+  hipLaunchKernelGGL(k_mg_mask, dim3(g), dim3(256), 0, ctx.stream, L0.n, ls.cons.p, r, L0.b.p);
+  AFEM_LAUNCHED();
+  vcycle(ctx, mg, 0, L0.b.p);
+  AFEM_HIP(hipMemcpyAsync(z, L0.x.p, L0.n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
+  hipLaunchKernelGGL(k_mg_fix, dim3(g), dim3(256), 0, ctx.stream, L0.n, ls.cons.p, r, ls.dinv.p, z);
+  AFEM_LAUNCHED();
+}
+
+}  // namespace afem

@@ -264,6 +264,11 @@ typedef struct afem_solver_opts {
                                stopping reference r0.z0 stays the zero guess's: same residual target. */
   int32_t precond_block;    /* 0 or 1: point Jacobi (default); 3: block Jacobi on 3x3 node blocks (NB_DOF = 3
                                systems; constraint rows decoupled from their block mates) */
+  int32_t multigrid;        /* 0: off (default); 1: geometric multigrid V-cycle preconditioner (Galerkin coarse
+                               operators of the Kuhn-box hierarchy, damped-Jacobi smoothing) on systems from a
+                               structured box on one rank, rebuilt at every solve; 2: built at the first solve
+                               and reused while the matrix structure stays the same (time stepping with a
+                               constant operator).  Other systems fall back to point Jacobi. */
 } afem_solver_opts;
 
 typedef struct afem_solve_stats {

@@ -10,7 +10,7 @@ sys.path.insert(0, ROOT)
 import arcanefem_amd as af  # noqa: E402
 import bench  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 ctx = af.Context(0)
 out = bench.elastodynamics_c5(ctx, af, n, steps)
