@@ -17,7 +17,7 @@
 //    the exact sparsity of P^T A P for nested Kuhn grids); penalty rows carry
 //    over by themselves;
 //  * smoothing: damped Jacobi, omega = 4 / (3 lambda_max(D^-1 A)) from a power
-//    iteration per level, 2 sweeps before and 2 after (symmetric V-cycle);
+//    iteration per level, one sweep before and one after (symmetric V-cycle);
 //  * coarsest level: dense inverse (<= kDenseMax DoF, symmetric scaling +
 //    Cholesky on the host at setup), else 16 Jacobi sweeps;
 //  * constraint rows (penalty / eliminated, the PCG's `cons` flags) are taken
@@ -36,7 +36,8 @@ namespace {
 inline unsigned grid_for(int64_t n, int threads) { return (unsigned)((n + threads - 1) / threads); }
 
 constexpr int kDenseMax = 512;  // DoF of a coarsest level inverted densely
-constexpr int kSweeps = 2;       // pre- and post-smoothing sweeps
+constexpr int kSweeps = 1;       // pre- and post-smoothing sweeps (C5, n = 128: 1 -> 20 PCG iterations, 43 ms
+                                 // per step; 2 -> 16, 55 ms; 3 -> 13, 64 ms)
 constexpr int kCoarseSweeps = 16;
 constexpr int kPowerIts = 12;
 
@@ -243,14 +244,15 @@ __global__ void k_mg_mul(int64_t n, double a, double* __restrict__ v)
     v[i] *= a;
 }
 
-// x = Ainv b (dense, coarsest level)
-__global__ void k_mg_gemv(int n, const double* __restrict__ A, const double* __restrict__ b, double* __restrict__ x)
+// x = Ainv b (dense, coarsest level): one wavefront per row, coalesced row reads
+__global__ __launch_bounds__(64) void k_mg_gemv(int n, const double* __restrict__ A, const double* __restrict__ b,
+                                                double* __restrict__ x)
 {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const int i = blockIdx.x;
   double s = 0.0;
-  for (int j = 0; j < n; ++j) s += A[(int64_t)i * n + j] * b[j];
-  x[i] = s;
+  for (int j = threadIdx.x; j < n; j += 64) s += A[(int64_t)i * n + j] * b[j];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (threadIdx.x == 0) x[i] = s;
 }
 
 constexpr int kVec = 1024;  // grid of the vector kernels
@@ -273,6 +275,7 @@ struct MgLevel {
 
 struct Multigrid {
   int k = 1;
+  int sweeps = kSweeps;
   std::vector<MgLevel> lv;
   DevBuf<double> ainv;  // dense inverse of the coarsest level (n_dense x n_dense) or empty
   int n_dense = 0;
@@ -536,17 +539,16 @@ void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
   MgLevel& L = mg.lv[l];
   if (l + 1 == mg.lv.size()) {
     if (mg.n_dense == L.n && l > 0) {
-      hipLaunchKernelGGL(k_mg_gemv, dim3((unsigned)((L.n + 127) / 128)), dim3(128), 0, ctx.stream, (int)L.n,
-                         mg.ainv.p, b, L.x.p);
+      hipLaunchKernelGGL(k_mg_gemv, dim3((unsigned)L.n), dim3(64), 0, ctx.stream, (int)L.n, mg.ainv.p, b, L.x.p);
       AFEM_LAUNCHED();
     }
     else {
-      smooth(ctx, mg, L, b, l == 0 ? 2 * kSweeps : kCoarseSweeps, true);
+      smooth(ctx, mg, L, b, l == 0 ? 2 * mg.sweeps : kCoarseSweeps, true);
     }
     return;
   }
   MgLevel& C = mg.lv[l + 1];
-  smooth(ctx, mg, L, b, kSweeps, true);
+  smooth(ctx, mg, L, b, mg.sweeps, true);
   spmv_blk_epi(ctx, mg.k, 2, L.nn, L.bp, L.bc, L.v, L.x.p, L.r.p, b, nullptr, 0.0);
   dispatch_k(mg.k, [&](auto kc) {
     constexpr int K = decltype(kc)::value;
@@ -561,7 +563,7 @@ void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
                        C.x.p, L.x.p);
     AFEM_LAUNCHED();
   });
-  smooth(ctx, mg, L, b, kSweeps, false);
+  smooth(ctx, mg, L, b, mg.sweeps, false);
 }
 
 }  // namespace
