@@ -428,6 +428,9 @@ class AfemDoFLinearSystemFactoryService
     o.atol = options()->atol();
     o.check_every = options()->checkEvery();
     o.fixed_iterations = 0;
+    const String pc = options()->preconditioner();
+    o.precond_block = pc == "block3" ? 3 : 0;
+    o.multigrid = pc == "multigrid" ? 1 : (pc == "multigrid-reuse" ? 2 : 0);
     x->setSolverOptions(o);
     return x;
   }
