@@ -42,6 +42,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MDoF/s assembly + CG iter/s, Poisson-3D P1 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# block-3 assembly kernels by afem_bsr_stats.last_kernel (include/arcanefem_amd.h AFEM_KERNEL_*)
+ELAST3_KERNELS = {4: "k_assemble_elast_strip", 5: "k_assemble_elast_tet", 6: "k_assemble_elast_tet_global",
+                  8: "k_assemble_elast_wg", 9: "k_assemble_elast_strip<..,BIG>"}
 
 
 def parse():
@@ -221,7 +224,7 @@ def elasticity_c3(ctx, af, n, reps=10, warmup=2):
     out = {"config": f"C3 elasticity block-3 P1 tets, Kuhn box n={n} ({n_own} nodes, {3 * n_own} DoF, "
                      f"{mesh.n_cells} tets), BSR per-block, stiffness + body force",
            "value": round(3 * n_own / (kms * 1e-3) / 1e6, 1), "unit": "MDoF/s", "kernel_ms": round(kms, 4),
-           "kernel": "k_assemble_elast_strip",
+           "kernel": ELAST3_KERNELS.get(int(st["last_kernel"]), str(int(st["last_kernel"]))),
            "roofline": {"bound": "hbm", "achieved": round(ab / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(ab / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "algorithmic_bytes_per_launch": int(ab)},
