@@ -147,6 +147,17 @@ struct alignas(16) SliceRec {
 };
 static_assert(sizeof(SliceRec) == 32, "SliceRec is one s_load_dwordx8");
 
+// Strip signature of a stencil instance (assembly.hip k_assemble_stencil): the
+// steps (2 priming + cells), row length, diagonal slot, shift/swap bits and the
+// 32 step bytes of the uniform slot stream (k_strip_classify's layout).
+struct StencilSig {
+  int nsteps, w, dslot;
+  uint64_t pat;
+  uint8_t slot[32];
+};
+// index of the compiled-in stencil signature a uniform slice matches, or -1
+int stencil_match(uint64_t pat, int nsteps, int w, const uint8_t* slot32);
+
 // Scalar (node-node) structure shared by every NB_DOF: rows = owned nodes.
 struct Structure {
   int64_t n_rows = 0, n_cols = 0, nnz = 0;
@@ -205,6 +216,14 @@ struct Structure {
   int64_t n_ms = 0, n_mb = 0;
   int ms_nodes = 0, mb_nodes = 0, mb_w = 0;
   int u_nodes = 0, u_w = 0;  // maxima over the uniform list (its LDS tile)
+  // stencil split of the uniform list (scalar assembly): the slices of the
+  // dominant compiled-in signature (rec_k, signature sig_k) and the other
+  // uniform slices (rec_ur + their slot streams urslot); rec_u stays whole
+  // (block-3 uses it)
+  DevBuf<SliceRec> rec_k, rec_ur;
+  DevBuf<uint8_t> urslot;
+  int64_t n_k = 0, n_ur = 0;
+  int sig_k = -1, k_nodes = 0, ur_nodes = 0, ur_w = 0;
   bool rec_ok = false;                     // offsets fit the 32-bit record fields
   DevBuf<int64_t> pos_rb;                  // [n_slices*64] row_ptr of each position's row (0: idle)
   DevBuf<uint32_t> pos_dl;                 // [n_slices*64] diagonal slot | row length << 8

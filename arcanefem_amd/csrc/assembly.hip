@@ -21,6 +21,7 @@
 //   * HBM traffic ~= the algorithmic minimum: incidence table (4 B per
 //     (cell,node), the same bytes as the connectivity), row offsets, columns,
 //     values, RHS, coordinates once.
+#include <cstring>
 #include "afem_internal.hpp"
 
 #include <cstdlib>
@@ -61,11 +62,14 @@ __device__ __forceinline__ double recip1(double a)
 }
 
 __device__ __forceinline__ V3 sub(V3 a, V3 b) { return V3{ a.x - b.x, a.y - b.y, a.z - b.z }; }
+// cross / dot with explicit fma: the same rounding in every kernel instance
+// whatever the compiler's contraction choices (the strip instances agree bit
+// for bit, tests/test_gpu_parity.py)
 __device__ __forceinline__ V3 cross(V3 a, V3 b)
 {
-  return V3{ a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x };
+  return V3{ fma(a.y, b.z, -(a.z * b.y)), fma(a.z, b.x, -(a.x * b.z)), fma(a.x, b.y, -(a.y * b.x)) };
 }
-__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return fma(a.z, b.z, fma(a.y, b.y, a.x * b.x)); }
 
 // 1/a to full double precision: hardware reciprocal estimate + two Newton
 // steps (5 VALU ops instead of the ~10 of an IEEE division; within 1 ulp).
@@ -1075,6 +1079,241 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
   AFEM_WT(1, __builtin_amdgcn_s_memrealtime());
 }
 
+// ---------------------------------------------------------------- scalar P1, stencil instance
+// The uniform slices whose rows all follow ONE strip signature SIG known at
+// compile time (StencilSig: steps, shift/swap pattern, slot of every step, row
+// length, diagonal slot; matched byte for byte by the structure build,
+// stencil_match): the interior bricks of a structured box, 97.5 % of the C2
+// slices.  With the slots constant, the row's accumulators are REGISTERS
+// (acc[W], indexed by compile-time window slots): no LDS accumulators, no
+// ds_add_f64 in the step loop, no zero fill, no scalar shift/swap branches,
+// no slot stream; the LDS holds the slice's coordinates and, after the steps,
+// the write-back image (position P = lane * W + t: no map, the value index is
+// rbs[P / W] + P % W).  Arithmetic, entry by entry, in the uniform instance's
+// order (each accumulator starts at +0 and adds the steps' products in step
+// order, rounded like ds_add_f64: the adds are not contracted): the three
+// instances give the same bits.
+#include "stencil_sigs.inc"  // constexpr StencilSig kSig<name> (StencilSig: afem_internal.hpp)
+
+template <const StencilSig& S>
+struct StencilWin {  // slots of the window nodes P, Q, R after step j's rotation
+  int p[32] = {}, q[32] = {}, r[32] = {};
+  constexpr StencilWin()
+  {
+    int P = S.dslot, Q = S.slot[0] & 63, R = S.slot[1] & 63;
+    for (int j = 2; j < S.nsteps; ++j) {
+      if (!((S.pat >> j) & 1u)) P = Q;
+      Q = R;
+      R = S.slot[j] & 63;
+      p[j] = P;
+      q[j] = Q;
+      r[j] = R;
+    }
+  }
+};
+template <const StencilSig& S>
+inline constexpr StencilWin<S> kStencilWin{};
+
+__device__ __forceinline__ double add_nc(double a, double b)
+{
+#pragma clang fp contract(off)
+  return a + b;  // rounded on its own, as the LDS accumulator's ds_add_f64
+}
+
+__host__ __device__ constexpr int64_t stencil_tile_bytes(int64_t u_cap, int64_t w)
+{
+  // coordinates (24 B per node) overlaid by the write-back image (64 w values), + 64 row offsets
+  return ((24 * u_cap > 512 * w ? 24 * u_cap : 512 * w) + 15) / 16 * 16 + 512;
+}
+
+template <const StencilSig& S>
+__global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, const SliceRec* __restrict__ recs,
+                                                            unsigned long long* __restrict__ tickets, int u_cap,
+                                                            const int32_t* __restrict__ perm,
+                                                            const int64_t* __restrict__ pos_rb,
+                                                            const uint32_t* __restrict__ pos_dl,
+                                                            const uint8_t* __restrict__ strip_u,
+                                                            const int32_t* __restrict__ snode,
+                                                            const double* __restrict__ coords, double s_coef,
+                                                            double f_meas, double* __restrict__ vals,
+                                                            double* __restrict__ rhs, int rhs_add)
+{
+  constexpr int W = S.w, D = S.dslot, NS = S.nsteps;
+  constexpr int MAXC = (NS + 15) / 16;
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* const cxyz = reinterpret_cast<double*>(smem);
+  double* const flat = cxyz;  // the write-back image overlays the coordinates
+  int64_t* const rbs = reinterpret_cast<int64_t*>(smem + stencil_tile_bytes(u_cap, W) - 512);
+  const int lane = threadIdx.x;
+  // claiming and the four-stage pipeline of k_assemble_strip
+  const int xcd = (int)(blockIdx.x & 7);
+  const int64_t r0 = n_slices * xcd / 8, r1 = n_slices * (xcd + 1) / 8;
+  auto claim_issue = [&]() -> unsigned long long {
+    unsigned long long t = 0;
+    if (lane == 0) t = atomicAdd(tickets + 16 * xcd, 1ull);
+    return t;
+  };
+  auto claim_get = [&](unsigned long long t) -> int64_t {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)t);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(t >> 32));
+    return r0 + (int64_t)(((uint64_t)hi << 32) | lo);
+  };
+  int64_t p0 = claim_get(claim_issue());
+  if (p0 >= r1) return;
+  int64_t p1 = claim_get(claim_issue());
+  int64_t p2 = claim_get(claim_issue());
+  int64_t p3 = claim_get(claim_issue());
+  SliceRec R0 = recs[p0];
+  SliceRec R1 = recs[p1 < r1 ? p1 : p0];
+  SliceRec R2 = recs[p2 < r1 ? p2 : p0];
+  auto load_nid = [&](const SliceRec& R, int32_t(&nid)[4]) {
+    const int nu = (int)(R.meta & 0xFFFFu);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nid[k] = snode[(int64_t)R.snode_off + max(min(lane + 64 * k, nu - 1), 0)];
+  };
+  auto load_rows = [&](const SliceRec& R, StripPre<MAXC>& p) {
+    const int64_t q = (int64_t)R.sl * 64 + lane;
+    p.row = perm[q];
+    p.dl = pos_dl[q];
+    p.rb = pos_rb[q];
+    const u32x4* su = reinterpret_cast<const u32x4*>(strip_u + (int64_t)R.strip_off * 1024) + lane;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) p.cu[c] = su[(int64_t)c * 64];
+  };
+  auto gather = [&](const int32_t(&nid)[4], StripPre<MAXC>& p) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      p.x[k] = coords[3 * (int64_t)nid[k]];
+      p.y[k] = coords[3 * (int64_t)nid[k] + 1];
+      p.z[k] = coords[3 * (int64_t)nid[k] + 2];
+    }
+  };
+  StripPre<MAXC> cur, nxt;
+  int32_t nid1[4], nid2[4];
+  {
+    int32_t nid0[4];
+    load_nid(R0, nid0);
+    load_rows(R0, cur);
+    gather(nid0, cur);
+    load_nid(R1, nid1);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  for (;;) {
+    const unsigned long long t4 = claim_issue();
+    const SliceRec R3 = recs[p3 < r1 ? p3 : p0];
+    const int nu = (int)(R0.meta & 0xFFFFu);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = max(min(lane + 64 * k, nu - 1), 0);
+      cxyz[3 * idx] = cur.x[k];
+      cxyz[3 * idx + 1] = cur.y[k];
+      cxyz[3 * idx + 2] = cur.z[k];
+    }
+    wave_sync_lds();
+    load_rows(R1, nxt);
+    gather(nid1, nxt);
+    load_nid(R2, nid2);
+
+    const int32_t row = cur.row;
+    const bool active = row >= 0;
+    auto coord = [&](int u) {
+      const double* q = cxyz + 3 * u;
+      return V3{ q[0], q[1], q[2] };
+    };
+    auto uloc_at = [&](int j) -> int {
+      const u32x4 w = cur.cu[j >> 4];
+      const int q = (j >> 2) & 3;
+      const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
+      return (int)((wq >> (8 * (j & 3))) & 0xFFu);
+    };
+    const V3 xi = coord((int)(cur.dl >> 16));
+    double acc[W];
+#pragma unroll
+    for (int t = 0; t < W; ++t) acc[t] = 0.0;
+    double macc = 0.0;
+    V3 eP{ 0.0, 0.0, 0.0 }, eQ = sub(coord(uloc_at(0)), xi), eR = sub(coord(uloc_at(1)), xi);
+    V3 cP = cross(eQ, eR), cN{ 0.0, 0.0, 0.0 };
+    V3 xc = coord(uloc_at(2));
+    // the uniform instance's loop shape: a scalar guard every 2 steps (the
+    // slice's step count, NS for every slice of the list) keeps the steps in
+    // their own blocks, so the coordinate reads stay one step ahead instead of
+    // being hoisted all at once; after full unrolling the window slots and the
+    // shift/swap arms are constants
+    const int nsteps = (int)(R0.meta >> 24);
+#pragma unroll
+    for (int j = 2; j < NS; ++j) {
+      if ((j & 1) == 0 && j >= nsteps) break;
+      const V3 xn = j + 1 < NS ? coord(uloc_at(j + 1 < NS ? j + 1 : j)) : xc;
+      const V3 eD = sub(xc, xi);
+      V3 cRn;
+      if ((S.pat >> j) & 1u) {
+        cRn = cN;
+      }
+      else {
+        cRn = cP;
+        eP = eQ;
+      }
+      eQ = eR;
+      eR = eD;
+      cP = cross(eQ, eR);
+      cN = cross(eP, eR);
+      const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
+      const double meas = fabs(dot(eP, cP));
+      const double s = -s_coef * recip1(fmax(meas, 1e-300));
+      const double kP = dot(m, cP) * s;
+      const double kQ = -dot(m, cN) * s;
+      const double kR = dot(m, cRn) * s;
+      macc += meas;
+      const int iP = kStencilWin<S>.p[j], iQ = kStencilWin<S>.q[j], iR = kStencilWin<S>.r[j];
+      acc[iP] = add_nc(acc[iP], kP);
+      acc[iQ] = add_nc(acc[iQ], kQ);
+      acc[iR] = add_nc(acc[iR], kR);
+      // keep the adds in their step: an accumulator read only at the end would
+      // otherwise be summed there (machine sinking), with all 3 x 24 products live
+      asm volatile("" : "+v"(acc[iP]), "+v"(acc[iQ]), "+v"(acc[iR]));
+      xc = xn;
+    }
+
+    // ---- RHS (as k_assemble_strip)
+    {
+      const unsigned long long am = __ballot(active);
+      const int src = active ? lane : (int)__ffsll((long long)am) - 1;
+      const double rv = __shfl(f_meas * macc, src);
+      const int32_t rr = __shfl(row, src);
+      if (rhs) rhs[rr] = rhs_add ? rhs[rr] + rv : rv;
+    }
+    // ---- diagonal (-sum of the row's other entries, in slot order) + write-back image
+    double sum = 0.0;
+#pragma unroll
+    for (int t = 0; t < W; ++t)
+      if (t != D) sum += acc[t];
+    wave_sync_lds();  // every lane's coordinate reads before the image overwrites them
+#pragma unroll
+    for (int t = 0; t < W; ++t) flat[lane * W + t] = t == D ? -sum : acc[t];
+    rbs[lane] = active ? cur.rb : -1;
+    wave_sync_lds();
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const int P = 64 * k + lane;
+      const int L = P / W;
+      const int64_t r = rbs[L];
+      if (r >= 0) vals[r + (P - L * W)] = flat[P];
+    }
+    wave_sync_lds();
+    if (p1 >= r1) break;
+    p0 = p1;
+    p1 = p2;
+    p2 = p3;
+    p3 = claim_get(t4);
+    R0 = R1;
+    R1 = R2;
+    R2 = R3;
+    cur = nxt;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nid1[k] = nid2[k];
+  }
+}
+
 // Shared factors of a step's three window blocks (rotated frame: component
 // row x; c_row = -m, the sign folded into s < 0):
 //   K_rb^{0j} = s [lambda m_x c_j + mu (m_j c_x + delta_0j m.c)] + delta_0j mass
@@ -1101,6 +1340,22 @@ __device__ __forceinline__ void elast_block(double* a, const ElastPre& e, V3 c, 
   atomicAdd(a, fma(fma(e.l0, c.x, t), s, mass));
   atomicAdd(a + 64, fma(e.lm, c.y, e.mm.y * c.x) * s);
   atomicAdd(a + 128, fma(e.lm, c.z, e.mm.z * c.x) * s);
+}
+// the same three entries added to register partial sums g (register-window
+// accumulation); explicit fma throughout, so no instance is left to the
+// compiler's contraction choices (instances agree bit for bit)
+__device__ __forceinline__ V3 elast_acc(V3 g, const ElastPre& e, V3 c, double s, double mass)
+{
+  const double t = fma(e.mm.z, c.z, fma(e.mm.y, c.y, e.mm.x * c.x));
+  return V3{ fma(fma(e.l0, c.x, t), s, mass) + g.x, fma(fma(e.lm, c.y, e.mm.y * c.x), s, g.y),
+             fma(fma(e.lm, c.z, e.mm.z * c.x), s, g.z) };
+}
+// flush a window node's register partial sums into its LDS accumulators [k][lane] (stride 64)
+__device__ __forceinline__ void flush3(double* a, V3 g)
+{
+  atomicAdd(a, g.x);
+  atomicAdd(a + 64, g.y);
+  atomicAdd(a + 128, g.z);
 }
 
 // ---------------------------------------------------------------- block-3 elasticity, persistent strips
@@ -1643,10 +1898,16 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     double* aP = acc_lane + 192 * dslot;
     double* aQ = aP;
     double* aR = aP;
+    // Register window: the partial sums of the three window nodes' entries
+    // stay in registers (gP, gQ, gR) while the node is in the window; a node
+    // leaving it (one per step: P on a shift, Q on a swap) is flushed into its
+    // LDS accumulators.  3 ds_add_f64 per step instead of 9; the entry of a
+    // (row, column) is summed per window visit first, then over the visits
+    // (fixed order: still bitwise reproducible, the same in both instances).
+    V3 gP{ 0.0, 0.0, 0.0 }, gQ{ 0.0, 0.0, 0.0 }, gR{ 0.0, 0.0, 0.0 };
     auto lidx_of = [&](uint32_t byte) { return (int)lrow[(byte & 63u) * 64]; };
     auto sel = [](bool c, V3 a, V3 b) { return V3{ c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z }; };
     auto keep = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
-    auto block = [&](double* a, const ElastPre& e, V3 cb, double s, double mass) { elast_block(a, e, cb, s, mass); };
     auto byte_at = [&](int j) -> uint32_t {
       const u32x4 w = cur.ch[j >> 4];
       const int q = (j >> 2) & 3;
@@ -1663,14 +1924,18 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         V3 cRn;
         if constexpr (SWAP) {
           cRn = cN;
+          flush3(aQ, gQ);
         }
         else {
           cRn = cP;
           eP = eQ;
+          flush3(aP, gP);
           aP = aQ;
+          gP = gQ;
         }
         eQ = eR;
         aQ = aR;
+        gQ = gR;
         eR = eD;
         aR = aD;
         cP = cross(eQ, eR);
@@ -1681,9 +1946,9 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         const double mass = c0 * meas * (1.0 / 120.0);
         macc += meas;
         const ElastPre e = elast_pre(m, lambda, mu);
-        block(aP, e, cP, s, mass);
-        block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
-        block(aR, e, cRn, s, mass);
+        gP = elast_acc(gP, e, cP, s, mass);
+        gQ = elast_acc(gQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+        gR = elast_acc(V3{ 0.0, 0.0, 0.0 }, e, cRn, s, mass);
       };
       {
         const uint32_t b0 = byte_at(0), b1 = byte_at(1);
@@ -1715,9 +1980,12 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         const V3 eD = sub(xd, xi);
         const V3 cRn = sel(swap, cN, cP);
         eP = sel(swap, eP, eQ);
+        flush3(swap ? aQ : aP, sel(swap, gQ, gP));
+        gP = sel(swap, gP, gQ);
         aP = swap ? aP : aQ;
         eQ = eR;
         aQ = aR;
+        gQ = gR;
         eR = eD;
         aR = aD;
         cP = cross(eQ, eR);
@@ -1728,9 +1996,9 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         const double mass = keep(em, c0 * meas * (1.0 / 120.0));
         macc += keep(em, meas);
         const ElastPre e = elast_pre(m, lambda, mu);
-        block(aP, e, cP, s, mass);
-        block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
-        block(aR, e, cRn, s, mass);
+        gP = elast_acc(gP, e, cP, s, mass);
+        gQ = elast_acc(gQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
+        gR = elast_acc(V3{ 0.0, 0.0, 0.0 }, e, cRn, s, mass);
       };
       int u1 = lidx_of(byte_at(0));
       V3 xc = coord(u1);
@@ -1745,6 +2013,9 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         u1 = u2;
       }
     }
+    flush3(aP, gP);
+    flush3(aQ, gQ);
+    flush3(aR, gR);
     if (rhs && active) {
       const double rv = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
       rhs[3 * (int64_t)row + ci] = rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv;
@@ -2298,6 +2569,52 @@ int occ_override()
 }
 }  // namespace
 
+// the stencil instance of signature `sig` (stencil_sigs.inc) over s.rec_k
+void launch_stencil(int sig, const Structure& s, int n_cu, const double* coords, double s_coef, double f_meas,
+                    double* vals, double* rhs, int rhs_add, unsigned long long* tk, hipStream_t stream)
+{
+  static std::map<std::pair<const void*, size_t>, int> occ_k;
+  auto go = [&](const void* fn, auto kern, int w) {
+    const size_t shm = (size_t)stencil_tile_bytes(s.k_nodes, w);
+    auto it = occ_k.find({ fn, shm });
+    if (it == occ_k.end()) {
+      int q = 0;
+      AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, fn, 64, shm));
+      it = occ_k.emplace(std::make_pair(fn, shm), q < 1 ? 1 : q).first;
+    }
+    const int per_cu = occ_override() > 0 ? occ_override() : it->second;
+    int64_t nblk = (int64_t)n_cu * per_cu;
+    if (nblk > s.n_k) nblk = s.n_k < 8 ? 8 : s.n_k;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm, stream, s.n_k, s.rec_k.p, tk, s.k_nodes, s.perm.p,
+                       s.pos_rb.p, s.pos_dl.p, s.strip_u.p, s.snode.p, coords, s_coef, f_meas, vals, rhs, rhs_add);
+    AFEM_LAUNCHED();
+  };
+  switch (sig) {
+#define AFEM_STENCIL_CASE(ID_, SIG_)                                                              \
+  case ID_:                                                                                      \
+    go(reinterpret_cast<const void*>(&k_assemble_stencil<SIG_>), k_assemble_stencil<SIG_>, SIG_.w); \
+    break;
+    AFEM_STENCIL_SIGS(AFEM_STENCIL_CASE)
+#undef AFEM_STENCIL_CASE
+    default:
+      throw Error(AFEM_ERR_STATE, "unknown stencil signature");
+  }
+}
+
+int stencil_match(uint64_t pat, int nsteps, int w, const uint8_t* slot32)
+{
+  static const StencilSig* const table[] = {
+#define AFEM_STENCIL_PTR(ID_, SIG_) &SIG_,
+    AFEM_STENCIL_SIGS(AFEM_STENCIL_PTR)
+#undef AFEM_STENCIL_PTR
+  };
+  for (int i = 0; i < (int)(sizeof(table) / sizeof(table[0])); ++i) {
+    const StencilSig& g = *table[i];
+    if (g.pat == pat && g.nsteps == nsteps && g.w == w && memcmp(g.slot, slot32, 32) == 0) return i;
+  }
+  return -1;
+}
+
 void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
 {
   Structure& s = b.s;
@@ -2332,10 +2649,11 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
     const bool uni_env = umode != 0;
     const bool use_uni = uni_env && s.n_uni > 0;
     const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;
-    if (s.tickets.n < 3 * 8 * 16) s.tickets.alloc(3 * 8 * 16);  // one counter per XCD, 128-B apart, per launch
+    if (s.tickets.n < 4 * 8 * 16) s.tickets.alloc(4 * 8 * 16);  // one counter per XCD, 128-B apart, per launch
     AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
     auto launch_s = [&](const void* fn, auto kern, int64_t n_list, const SliceRec* list, unsigned long long* tk,
-                        size_t shm_s, hipStream_t stream, int ucap = -1, int wcap = -1) {
+                        size_t shm_s, hipStream_t stream, int ucap = -1, int wcap = -1,
+                        const uint8_t* slots = nullptr) {
       if (ucap < 0) ucap = s.max_slice_nodes;
       if (wcap < 0) wcap = s.max_slice_w;
       auto it = occ_s.find({ fn, shm_s });
@@ -2350,7 +2668,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, stream, n_list, list, tk,
                          ucap, wcap, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.strip_u.p,
                          s.lidx.p, s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add,
-                         reinterpret_cast<const SlotRec*>(s.uslot.p));
+                         reinterpret_cast<const SlotRec*>(slots ? slots : s.uslot.p));
     };
     const SliceRec* list_m = use_uni ? s.rec_m.p : s.rec_all.p;
 #define AFEM_STRIP_K(NV_, C_, W_, U_, N_, L_, T_, SHM_, ST_)                                                           \
@@ -2365,7 +2683,13 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       // hide under the large kernel; without (unstructured meshes) the
       // compact list runs on the context stream and the big one beside it.
       const bool has_u = s.n_uni > 0;
-      const bool fork = (has_u && (s.n_ms > 0 || s.n_mb > 0)) || (!has_u && s.n_ms > 0 && s.n_mb > 0);
+      // stencil split (AFEM_ASSEMBLY_STENCIL=0: the whole uniform list through the
+      // uniform instance, diagnostic): the signature's slices on the context
+      // stream, the other uniform slices through the uniform instance beside them
+      const char* ke = getenv("AFEM_ASSEMBLY_STENCIL");  // read per call: the parity test toggles it
+      const bool use_k = has_u && umode == 1 && s.n_k > 0 && !(ke && atoi(ke) == 0);
+      const bool fork = (has_u && (s.n_ms > 0 || s.n_mb > 0 || (use_k && s.n_ur > 0))) ||
+                        (!has_u && s.n_ms > 0 && s.n_mb > 0);
       hipStream_t side = ctx.stream;
       if (fork) {
         side = ctx.side();
@@ -2385,7 +2709,16 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       if (s.n_mb > 0)
         launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 4, 32, 0>), k_assemble_strip<4, 4, 32, 0>, s.n_mb,
                  s.rec_mb.p, s.tickets.p + 256, shm_mb, s_mb, s.mb_nodes, s.mb_w);
-      if (has_u) {
+      if (use_k) {
+        if (s.n_ur > 0) {
+          const size_t shm_ur = (size_t)(8 * 64 * (int64_t)s.ur_w + strip_coord_bytes(dimc, s.ur_nodes, s.ur_w));
+          launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 1>), k_assemble_strip<4, 2, 16, 1>,
+                   s.n_ur, s.rec_ur.p, s.tickets.p, shm_ur, side, s.ur_nodes, s.ur_w, s.urslot.p);
+        }
+        launch_stencil(s.sig_k, s, ctx.n_cu, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add,
+                       s.tickets.p + 384, ctx.stream);
+      }
+      else if (has_u) {
         const size_t shm_uu = (size_t)(8 * 64 * (int64_t)s.u_w + strip_coord_bytes(dimc, s.u_nodes, s.u_w));
         if (umode == 2)
           launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 2>), k_assemble_strip<4, 2, 16, 2>,

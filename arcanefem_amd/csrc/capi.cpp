@@ -577,6 +577,8 @@ int afem_bsr_get_stats(afem_bsr* b, afem_bsr_stats* st)
   st->n_slices = b->s.n_slices;
   st->brick_order = b->s.brick_order ? 1 : 0;
   st->uniform_slices = (int32_t)b->s.n_uni;
+  st->stencil_slices = (int32_t)b->s.n_k;
+  st->stencil_sig = b->s.sig_k;
   st->last_kernel = b->last_kernel;
   API_END
 }

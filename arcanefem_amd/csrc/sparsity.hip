@@ -1334,6 +1334,45 @@ void build_structure(Mesh& m, Structure& s)
       upload(s.rec_u, ru);
       s.uslot.alloc(su.empty() ? 32 : su.size());
       if (!su.empty()) AFEM_HIP(hipMemcpyAsync(s.uslot.p, su.data(), su.size(), hipMemcpyHostToDevice, ctx.stream));
+      {
+        // stencil split of the uniform list (scalar assembly): the slices of the
+        // most frequent compiled-in signature run k_assemble_stencil, the other
+        // uniform slices the uniform instance (rec_ur with their slot streams)
+        std::vector<int> sid(ru.size());
+        std::map<int, int64_t> cnt;
+        for (size_t i = 0; i < ru.size(); ++i) {
+          const SliceRec& r = ru[i];
+          sid[i] = stencil_match(r.pat, (int)(r.meta >> 24), (int)((r.meta >> 16) & 0xFFu), su.data() + 32 * i);
+          if (sid[i] >= 0) ++cnt[sid[i]];
+        }
+        int best = -1;
+        for (const auto& kv : cnt)
+          if (best < 0 || kv.second > cnt[best]) best = kv.first;
+        std::vector<SliceRec> rk, rur;
+        std::vector<uint8_t> sur;
+        s.k_nodes = s.ur_nodes = s.ur_w = 0;
+        for (size_t i = 0; i < ru.size(); ++i) {
+          const SliceRec& r = ru[i];
+          if (best >= 0 && sid[i] == best) {
+            rk.push_back(r);
+            s.k_nodes = std::max(s.k_nodes, (int)(r.meta & 0xFFFFu));
+          }
+          else {
+            rur.push_back(r);
+            sur.insert(sur.end(), su.begin() + 32 * i, su.begin() + 32 * (i + 1));
+            s.ur_nodes = std::max(s.ur_nodes, (int)(r.meta & 0xFFFFu));
+            s.ur_w = std::max(s.ur_w, (int)((r.meta >> 16) & 0xFFu));
+          }
+        }
+        s.sig_k = best;
+        s.n_k = (int64_t)rk.size();
+        s.n_ur = (int64_t)rur.size();
+        upload(s.rec_k, rk);
+        upload(s.rec_ur, rur);
+        s.urslot.alloc(sur.empty() ? 32 : sur.size());
+        if (!sur.empty())
+          AFEM_HIP(hipMemcpyAsync(s.urslot.p, sur.data(), sur.size(), hipMemcpyHostToDevice, ctx.stream));
+      }
       upload(s.rec_m, rm);
       upload(s.rec_all, ra);
       if (getenv("AFEM_DEBUG_SLICES")) {  // diagnostic: slice node counts and widths
@@ -1353,7 +1392,8 @@ void build_structure(Mesh& m, Structure& s)
           const SliceRec& r = ru[i];
           ++h[{ r.pat, (int)(r.meta >> 24) }];
           char b[32];
-          snprintf(b, sizeof(b), "%016llx/%d/", (unsigned long long)r.pat, (int)(r.meta >> 24));
+          snprintf(b, sizeof(b), "%016llx/%d/w%d/", (unsigned long long)r.pat, (int)(r.meta >> 24),
+                   (int)((r.meta >> 16) & 0xFFu));
           std::string k(b);
           for (int t = 0; t < 32; ++t) {
             snprintf(b, sizeof(b), "%02x", su[32 * i + t]);

@@ -221,6 +221,8 @@ typedef struct afem_bsr_stats {
                                AFEM_ORDER=node) */
   int32_t uniform_slices;   /* slices whose 64 rows share one strip topology (uniform-control assembly variant) */
   int32_t last_kernel;      /* AFEM_KERNEL_* that ran the last assembly of this matrix */
+  int32_t stencil_slices;   /* uniform slices of a compiled-in strip signature (scalar stencil instance) */
+  int32_t stencil_sig;      /* that signature's index (-1: none) */
 } afem_bsr_stats;
 #define AFEM_KERNEL_NONE 0
 #define AFEM_KERNEL_STRIP 1          /* scalar row-strip kernel (uniform + general instances) */

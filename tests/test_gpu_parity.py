@@ -121,6 +121,37 @@ def test_uniform_strip_variant(ctx, monkeypatch):
     assert np.abs(r_uni - orhs).max() <= VAL_TOL * np.abs(orhs).max()
 
 
+@pytest.mark.parametrize("n", [23, 40])
+def test_stencil_instance_bitwise(ctx, monkeypatch, n):
+    """Interior bricks of a Kuhn box match the compiled-in strip signature
+    (stencil_sigs.inc) and run k_assemble_stencil (register accumulators): the
+    same bits as the uniform instance (AFEM_ASSEMBLY_STENCIL=0) and the general
+    instance (AFEM_ASSEMBLY_UNIFORM=0), and the oracle's values."""
+    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=7)
+    bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+    st = bsr.stats()
+    print("slices", st["n_slices"], "uniform", st["uniform_slices"], "stencil", st["stencil_slices"])
+    assert st["stencil_sig"] == 0 and 0 < st["stencil_slices"] < st["uniform_slices"]
+    _, _, v_k = bsr.download()
+    r_k = ls.rhs_host()
+    monkeypatch.setenv("AFEM_ASSEMBLY_STENCIL", "0")
+    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
+    _, _, v_uni = bsr.download()
+    assert np.array_equal(v_k, v_uni), f"stencil and uniform instances differ in {np.count_nonzero(v_k != v_uni)} values"
+    assert np.array_equal(r_k, ls.rhs_host())
+    monkeypatch.setenv("AFEM_ASSEMBLY_UNIFORM", "0")
+    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
+    rows, cols, v_gen = bsr.download()
+    assert np.array_equal(v_k, v_gen)
+    assert np.array_equal(r_k, ls.rhs_host())
+    cells, coords, _ = mesh.download()
+    orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+    ovals, orhs = O.assemble_poisson(mesh.n_own_nodes, cells, coords, orp, ocols, 5.5)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    _check_values(v_k, ovals)
+    assert np.abs(r_k - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+
+
 def test_isolated_node_and_ragged_rows(ctx):
     # two tets sharing a face + one node touched by no cell (empty row apart
     # from the diagonal the reference always inserts, BSRFormat.h:679)
