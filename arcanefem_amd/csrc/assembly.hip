@@ -2688,8 +2688,15 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       // stream, the other uniform slices through the uniform instance beside them
       const char* ke = getenv("AFEM_ASSEMBLY_STENCIL");  // read per call: the parity test toggles it
       const bool use_k = has_u && umode == 1 && s.n_k > 0 && !(ke && atoi(ke) == 0);
-      const bool fork = (has_u && (s.n_ms > 0 || s.n_mb > 0 || (use_k && s.n_ur > 0))) ||
-                        (!has_u && s.n_ms > 0 && s.n_mb > 0);
+      // with the stencil split every list runs on the context stream, the small
+      // ones first: beside the stencil kernel's persistent grid a side-stream
+      // launch only gets CUs as its waves retire (its kernel time stretches to
+      // the whole assembly), one after the other the kernel times add up to the
+      // assembly time (AFEM_ASSEMBLY_SIDE=1: side stream, diagnostic)
+      const char* se = getenv("AFEM_ASSEMBLY_SIDE");
+      const bool serial_k = use_k && !(se && atoi(se) == 1);
+      const bool fork = !serial_k && ((has_u && (s.n_ms > 0 || s.n_mb > 0 || (use_k && s.n_ur > 0))) ||
+                                      (!has_u && s.n_ms > 0 && s.n_mb > 0));
       hipStream_t side = ctx.stream;
       if (fork) {
         side = ctx.side();
@@ -2701,8 +2708,8 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       const size_t shm_mb = (size_t)strip_tile_bytes(dimc, s.mb_nodes, s.mb_w);
       const bool mb_ok = s.mb_w <= 32 && s.n_mb >= 0 && shm_mb <= kTileLdsMax;
       AFEM_REQUIRE(s.n_mb == 0 || (mb_ok && s.max_strip_c <= 4), AFEM_ERR_STATE, "strip lists exceed the kernels");
-      hipStream_t s_ms = has_u ? side : ctx.stream;
-      hipStream_t s_mb = has_u ? side : (s.n_ms > 0 ? side : ctx.stream);
+      hipStream_t s_ms = has_u && !serial_k ? side : ctx.stream;
+      hipStream_t s_mb = has_u && !serial_k ? side : (s.n_ms > 0 && !serial_k ? side : ctx.stream);
       if (s.n_ms > 0)
         launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 0>), k_assemble_strip<4, 2, 16, 0>, s.n_ms,
                  s.rec_ms.p, s.tickets.p + 128, shm_ms, s_ms, s.ms_nodes, ms_w);

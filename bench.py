@@ -121,7 +121,9 @@ def roofline(bsr, mesh, kernel_ms):
     st = bsr.stats()
     # the instances the assembly launches: uniform slices, compact general
     # slices, big general slices (> 16 slots / > 352 nodes, assembly.hip)
-    names = ["k_assemble_strip<4,2,16,uniform>"] if st["uniform_slices"] > 0 else []
+    names = ["k_assemble_stencil<kSigKuhn3D>"] if st["stencil_slices"] > 0 else []
+    if st["uniform_slices"] > st["stencil_slices"]:
+        names.append("k_assemble_strip<4,2,16,uniform>")
     names.append("k_assemble_strip<4,2,16,general>")
     if st["max_slice_width"] > 16 or st["max_slice_nodes"] > 352:
         names.append("k_assemble_strip<4,4,32,general>")
@@ -133,7 +135,8 @@ def roofline(bsr, mesh, kernel_ms):
             "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(ab),
             "kernel_ms": round(kernel_ms, 4),
             "inc_padding": round(st["inc_table_entries"] / max(int(st["n_incidences"]), 1) - 1.0, 4),
-            "uniform_slice_frac": round(st["uniform_slices"] / max(st["n_slices"], 1), 4)}
+            "uniform_slice_frac": round(st["uniform_slices"] / max(st["n_slices"], 1), 4),
+            "stencil_slice_frac": round(st["stencil_slices"] / max(st["n_slices"], 1), 4)}
 
 
 def pmc_traffic(path, n):

@@ -19,13 +19,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def counters(d, kernel="k_assemble_strip"):
+def counters(d, kernel=("k_assemble_strip", "k_assemble_stencil")):
     """Per assembly: the mean per dispatch of each matching kernel, summed over
     the kernels (the assembly launches a uniform-strip and a general instance)."""
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True):
         for x in csv.DictReader(open(f)):
-            if kernel in x["Kernel_Name"]:
+            if any(k in x["Kernel_Name"] for k in kernel):
                 acc[x["Counter_Name"]][x["Kernel_Name"]].append(float(x["Counter_Value"]))
     return {c: sum(sum(v) / len(v) for v in per.values()) for c, per in acc.items()}
 
@@ -41,7 +41,7 @@ def main():
     c = {}
     for sub in ("pmc_sq", "pmc_fetch", "pmc_write", "pmc_lds"):
         c.update(counters(os.path.join(prof, sub)))
-    lines = [f"# {tag}: per assembly = sum over the k_assemble_strip instances of their mean per dispatch "
+    lines = [f"# {tag}: per assembly = sum over the k_assemble_stencil / k_assemble_strip instances of their mean per dispatch "
              "(rocprofv3 --pmc, separate passes)"]
     for k in sorted(c):
         lines.append(f"{k:32s} {c[k]:.6g}")

@@ -7,7 +7,7 @@
 set -e
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/prof}
-K=${2:-k_assemble_strip}
+K=${2:-k_assemble_st}
 B=${B:-"bench.py --steps 10 --warmup 2 --cg-iters 20 --no-cpu-baseline --no-extras"}
 mkdir -p $OUT
 timeout -k 5 200 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1
