@@ -67,7 +67,7 @@ class SolverOpts(ctypes.Structure):
 
 class SolveStats(ctypes.Structure):
     _fields_ = [("iterations", ctypes.c_int32), ("converged", ctypes.c_int32), ("rel_residual", ctypes.c_double),
-                ("residual_norm", ctypes.c_double), ("solve_ms", ctypes.c_double)]
+                ("residual_norm", ctypes.c_double), ("solve_ms", ctypes.c_double), ("spmv_kernel", ctypes.c_int32)]
 
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64)

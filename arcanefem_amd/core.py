@@ -471,7 +471,7 @@ class DoFLinearSystem:
         st = C.SolveStats()
         call("afem_ls_solve", self.impl, ctypes.byref(st))
         return dict(iterations=st.iterations, converged=bool(st.converged), rel_residual=st.rel_residual,
-                    residual_norm=st.residual_norm, solve_ms=st.solve_ms)
+                    residual_norm=st.residual_norm, solve_ms=st.solve_ms, spmv_kernel=st.spmv_kernel)
 
     def spmv(self, x_dptr: int, y_dptr: int):
         call("afem_ls_spmv", self.impl, ctypes.c_void_p(x_dptr), ctypes.c_void_p(y_dptr))

@@ -142,7 +142,7 @@ struct alignas(16) SliceRec {
   uint32_t strip_off;  // strip_ptr[sl] / 1024
   uint32_t snode_off;  // snode_ptr[sl]
   uint32_t meta;       // slice nodes | width (max row length) << 16 | strip steps << 24
-  uint32_t pad;        // (dword fields only: the kernel reads records with scalar loads)
+  uint32_t sig;        // stencil list: index of the slice's compiled-in strip signature (else 0)
   uint64_t pat;        // uniform slices: shift/swap bits
 };
 static_assert(sizeof(SliceRec) == 32, "SliceRec is one s_load_dwordx8");
@@ -216,10 +216,10 @@ struct Structure {
   int64_t n_ms = 0, n_mb = 0;
   int ms_nodes = 0, mb_nodes = 0, mb_w = 0;
   int u_nodes = 0, u_w = 0;  // maxima over the uniform list (its LDS tile)
-  // stencil split of the uniform list (scalar assembly): the slices of the
-  // dominant compiled-in signature (rec_k, signature sig_k) and the other
-  // uniform slices (rec_ur + their slot streams urslot); rec_u stays whole
-  // (block-3 uses it)
+  // stencil split of the uniform list (scalar assembly): the slices of any
+  // compiled-in signature (rec_k, SliceRec::sig; sig_k = the most frequent
+  // one, -1 if none) and the other uniform slices (rec_ur + their slot
+  // streams urslot); rec_u stays whole (block-3 uses it)
   DevBuf<SliceRec> rec_k, rec_ur;
   DevBuf<uint8_t> urslot;
   int64_t n_k = 0, n_ur = 0;
@@ -320,6 +320,7 @@ struct LinearSystem {
   std::map<int32_t, std::pair<uint8_t, double>> host_elim;
   // solver work
   DevBuf<double> r, z, p, q, dinv, partial, scal;
+  mutable DevBuf<uint8_t> pat_flag;  // rows whose columns follow the dominant offset pattern (pattern SpMV)
   DevBuf<double> x0;      // the caller's initial guess (opts.initial_guess = 1)
   DevBuf<double> binv;    // block-Jacobi 3: inverse node blocks [n/3][9]
   DevBuf<int32_t> blist;  // multi-rank CG: SpMV row blocks, interior ones first

@@ -1126,7 +1126,133 @@ __host__ __device__ constexpr int64_t stencil_tile_bytes(int64_t u_cap, int64_t 
   return ((24 * u_cap > 512 * w ? 24 * u_cap : 512 * w) + 15) / 16 * 16 + 512;
 }
 
-template <const StencilSig& S>
+// one slice of signature S (the steps, the RHS and the write-back of k_assemble_stencil)
+template <const StencilSig& S, int MAXC>
+__device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nsteps, int lane, const double* cxyz,
+                                              double* flat, int64_t* rbs, double s_coef, double f_meas,
+                                              double* __restrict__ vals, double* __restrict__ rhs, int rhs_add)
+{
+  constexpr int W = S.w, D = S.dslot, NS = S.nsteps;
+  static_assert(NS <= 16 * MAXC && W <= 16, "stencil signature beyond the kernel's strip chunks");
+    const int32_t row = cur.row;
+    const bool active = row >= 0;
+    auto coord = [&](int u) {
+      const double* q = cxyz + 3 * u;
+      return V3{ q[0], q[1], q[2] };
+    };
+    auto uloc_at = [&](int j) -> int {
+      const u32x4 w = cur.cu[j >> 4];
+      const int q = (j >> 2) & 3;
+      const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
+      return (int)((wq >> (8 * (j & 3))) & 0xFFu);
+    };
+    const V3 xi = coord((int)(cur.dl >> 16));
+    double acc[W];
+#pragma unroll
+    for (int t = 0; t < W; ++t) acc[t] = 0.0;
+    double macc = 0.0;
+    V3 eP{ 0.0, 0.0, 0.0 }, eQ = sub(coord(uloc_at(0)), xi), eR = sub(coord(uloc_at(1)), xi);
+    V3 cP = cross(eQ, eR), cN{ 0.0, 0.0, 0.0 };
+    V3 xc = coord(uloc_at(2));
+    // the uniform instance's loop shape: a scalar guard every 2 steps (the
+    // slice's step count, NS for every slice of the list) keeps the steps in
+    // their own blocks, so the coordinate reads stay one step ahead instead of
+    // being hoisted all at once; after full unrolling the window slots and the
+    // shift/swap arms are constants
+#pragma unroll
+    for (int j = 2; j < NS; ++j) {
+      if ((j & 1) == 0 && j >= nsteps) break;
+      const V3 xn = j + 1 < NS ? coord(uloc_at(j + 1 < NS ? j + 1 : j)) : xc;
+      const V3 eD = sub(xc, xi);
+      V3 cRn;
+      if ((S.pat >> j) & 1u) {
+        cRn = cN;
+      }
+      else {
+        cRn = cP;
+        eP = eQ;
+      }
+      eQ = eR;
+      eR = eD;
+      cP = cross(eQ, eR);
+      cN = cross(eP, eR);
+      const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
+      const double meas = fabs(dot(eP, cP));
+      const double s = -s_coef * recip1(fmax(meas, 1e-300));
+      const double kP = dot(m, cP) * s;
+      const double kQ = -dot(m, cN) * s;
+      const double kR = dot(m, cRn) * s;
+      macc += meas;
+      const int iP = kStencilWin<S>.p[j], iQ = kStencilWin<S>.q[j], iR = kStencilWin<S>.r[j];
+      acc[iP] = add_nc(acc[iP], kP);
+      acc[iQ] = add_nc(acc[iQ], kQ);
+      acc[iR] = add_nc(acc[iR], kR);
+      // keep the adds in their step: an accumulator read only at the end would
+      // otherwise be summed there (machine sinking), with all 3 x 24 products live
+      asm volatile("" : "+v"(acc[iP]), "+v"(acc[iQ]), "+v"(acc[iR]));
+      xc = xn;
+    }
+
+    // ---- RHS (as k_assemble_strip)
+    {
+      const unsigned long long am = __ballot(active);
+      const int src = active ? lane : (int)__ffsll((long long)am) - 1;
+      const double rv = __shfl(f_meas * macc, src);
+      const int32_t rr = __shfl(row, src);
+      if (rhs) rhs[rr] = rhs_add ? rhs[rr] + rv : rv;
+    }
+    // ---- diagonal (-sum of the row's other entries, in slot order) + write-back image
+    double sum = 0.0;
+#pragma unroll
+    for (int t = 0; t < W; ++t)
+      if (t != D) sum += acc[t];
+    wave_sync_lds();  // every lane's coordinate reads before the image overwrites them
+#pragma unroll
+    for (int t = 0; t < W; ++t) flat[lane * W + t] = t == D ? -sum : acc[t];
+    rbs[lane] = active ? cur.rb : -1;
+    wave_sync_lds();
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const int P = 64 * k + lane;
+      const int L = P / W;
+      const int64_t r = rbs[L];
+      if (r >= 0) vals[r + (P - L * W)] = flat[P];
+    }
+    wave_sync_lds();
+}
+
+// signature index -> stencil_slice<S_index> (a scalar branch per slice)
+template <int I, const StencilSig& S0, const StencilSig&... SR>
+struct StencilDispatch {
+  template <int MAXC>
+  __device__ __forceinline__ static void run(int sig, const StripPre<MAXC>& cur, int nsteps, int lane,
+                                             const double* cxyz, double* flat, int64_t* rbs, double s_coef,
+                                             double f_meas, double* vals, double* rhs, int rhs_add)
+  {
+    if (sig == I || sizeof...(SR) == 0)
+      stencil_slice<S0, MAXC>(cur, nsteps, lane, cxyz, flat, rbs, s_coef, f_meas, vals, rhs, rhs_add);
+    else if constexpr (sizeof...(SR) > 0)
+      StencilDispatch<I + 1, SR...>::template run<MAXC>(sig, cur, nsteps, lane, cxyz, flat, rbs, s_coef, f_meas,
+                                                        vals, rhs, rhs_add);
+  }
+};
+
+template <const StencilSig&... SS>
+constexpr int stencil_maxc()
+{
+  int m = 1;
+  for (int c : { ((SS.nsteps + 15) / 16)... }) m = c > m ? c : m;
+  return m;
+}
+template <const StencilSig&... SS>
+constexpr int stencil_maxw()
+{
+  int m = 1;
+  for (int w : { SS.w... }) m = w > m ? w : m;
+  return m;
+}
+
+template <const StencilSig&... SS>
 __global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, const SliceRec* __restrict__ recs,
                                                             unsigned long long* __restrict__ tickets, int u_cap,
                                                             const int32_t* __restrict__ perm,
@@ -1138,12 +1264,11 @@ __global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, co
                                                             double f_meas, double* __restrict__ vals,
                                                             double* __restrict__ rhs, int rhs_add)
 {
-  constexpr int W = S.w, D = S.dslot, NS = S.nsteps;
-  constexpr int MAXC = (NS + 15) / 16;
+  constexpr int MAXC = stencil_maxc<SS...>();
   extern __shared__ __align__(16) unsigned char smem[];
   double* const cxyz = reinterpret_cast<double*>(smem);
   double* const flat = cxyz;  // the write-back image overlays the coordinates
-  int64_t* const rbs = reinterpret_cast<int64_t*>(smem + stencil_tile_bytes(u_cap, W) - 512);
+  int64_t* const rbs = reinterpret_cast<int64_t*>(smem + stencil_tile_bytes(u_cap, stencil_maxw<SS...>()) - 512);
   const int lane = threadIdx.x;
   // claiming and the four-stage pipeline of k_assemble_strip
   const int xcd = (int)(blockIdx.x & 7);
@@ -1214,92 +1339,8 @@ __global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, co
     gather(nid1, nxt);
     load_nid(R2, nid2);
 
-    const int32_t row = cur.row;
-    const bool active = row >= 0;
-    auto coord = [&](int u) {
-      const double* q = cxyz + 3 * u;
-      return V3{ q[0], q[1], q[2] };
-    };
-    auto uloc_at = [&](int j) -> int {
-      const u32x4 w = cur.cu[j >> 4];
-      const int q = (j >> 2) & 3;
-      const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
-      return (int)((wq >> (8 * (j & 3))) & 0xFFu);
-    };
-    const V3 xi = coord((int)(cur.dl >> 16));
-    double acc[W];
-#pragma unroll
-    for (int t = 0; t < W; ++t) acc[t] = 0.0;
-    double macc = 0.0;
-    V3 eP{ 0.0, 0.0, 0.0 }, eQ = sub(coord(uloc_at(0)), xi), eR = sub(coord(uloc_at(1)), xi);
-    V3 cP = cross(eQ, eR), cN{ 0.0, 0.0, 0.0 };
-    V3 xc = coord(uloc_at(2));
-    // the uniform instance's loop shape: a scalar guard every 2 steps (the
-    // slice's step count, NS for every slice of the list) keeps the steps in
-    // their own blocks, so the coordinate reads stay one step ahead instead of
-    // being hoisted all at once; after full unrolling the window slots and the
-    // shift/swap arms are constants
-    const int nsteps = (int)(R0.meta >> 24);
-#pragma unroll
-    for (int j = 2; j < NS; ++j) {
-      if ((j & 1) == 0 && j >= nsteps) break;
-      const V3 xn = j + 1 < NS ? coord(uloc_at(j + 1 < NS ? j + 1 : j)) : xc;
-      const V3 eD = sub(xc, xi);
-      V3 cRn;
-      if ((S.pat >> j) & 1u) {
-        cRn = cN;
-      }
-      else {
-        cRn = cP;
-        eP = eQ;
-      }
-      eQ = eR;
-      eR = eD;
-      cP = cross(eQ, eR);
-      cN = cross(eP, eR);
-      const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
-      const double meas = fabs(dot(eP, cP));
-      const double s = -s_coef * recip1(fmax(meas, 1e-300));
-      const double kP = dot(m, cP) * s;
-      const double kQ = -dot(m, cN) * s;
-      const double kR = dot(m, cRn) * s;
-      macc += meas;
-      const int iP = kStencilWin<S>.p[j], iQ = kStencilWin<S>.q[j], iR = kStencilWin<S>.r[j];
-      acc[iP] = add_nc(acc[iP], kP);
-      acc[iQ] = add_nc(acc[iQ], kQ);
-      acc[iR] = add_nc(acc[iR], kR);
-      // keep the adds in their step: an accumulator read only at the end would
-      // otherwise be summed there (machine sinking), with all 3 x 24 products live
-      asm volatile("" : "+v"(acc[iP]), "+v"(acc[iQ]), "+v"(acc[iR]));
-      xc = xn;
-    }
-
-    // ---- RHS (as k_assemble_strip)
-    {
-      const unsigned long long am = __ballot(active);
-      const int src = active ? lane : (int)__ffsll((long long)am) - 1;
-      const double rv = __shfl(f_meas * macc, src);
-      const int32_t rr = __shfl(row, src);
-      if (rhs) rhs[rr] = rhs_add ? rhs[rr] + rv : rv;
-    }
-    // ---- diagonal (-sum of the row's other entries, in slot order) + write-back image
-    double sum = 0.0;
-#pragma unroll
-    for (int t = 0; t < W; ++t)
-      if (t != D) sum += acc[t];
-    wave_sync_lds();  // every lane's coordinate reads before the image overwrites them
-#pragma unroll
-    for (int t = 0; t < W; ++t) flat[lane * W + t] = t == D ? -sum : acc[t];
-    rbs[lane] = active ? cur.rb : -1;
-    wave_sync_lds();
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int P = 64 * k + lane;
-      const int L = P / W;
-      const int64_t r = rbs[L];
-      if (r >= 0) vals[r + (P - L * W)] = flat[P];
-    }
-    wave_sync_lds();
+    StencilDispatch<0, SS...>::template run<MAXC>((int)R0.sig, cur, (int)(R0.meta >> 24), lane, cxyz, flat, rbs,
+                                                  s_coef, f_meas, vals, rhs, rhs_add);
     if (p1 >= r1) break;
     p0 = p1;
     p1 = p2;
@@ -2569,36 +2610,26 @@ int occ_override()
 }
 }  // namespace
 
-// the stencil instance of signature `sig` (stencil_sigs.inc) over s.rec_k
-void launch_stencil(int sig, const Structure& s, int n_cu, const double* coords, double s_coef, double f_meas,
-                    double* vals, double* rhs, int rhs_add, unsigned long long* tk, hipStream_t stream)
+// the stencil kernel (every compiled-in signature, stencil_sigs.inc) over s.rec_k
+void launch_stencil(const Structure& s, int n_cu, const double* coords, double s_coef, double f_meas, double* vals,
+                    double* rhs, int rhs_add, unsigned long long* tk, hipStream_t stream)
 {
-  static std::map<std::pair<const void*, size_t>, int> occ_k;
-  auto go = [&](const void* fn, auto kern, int w) {
-    const size_t shm = (size_t)stencil_tile_bytes(s.k_nodes, w);
-    auto it = occ_k.find({ fn, shm });
-    if (it == occ_k.end()) {
-      int q = 0;
-      AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, fn, 64, shm));
-      it = occ_k.emplace(std::make_pair(fn, shm), q < 1 ? 1 : q).first;
-    }
-    const int per_cu = occ_override() > 0 ? occ_override() : it->second;
-    int64_t nblk = (int64_t)n_cu * per_cu;
-    if (nblk > s.n_k) nblk = s.n_k < 8 ? 8 : s.n_k;
-    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm, stream, s.n_k, s.rec_k.p, tk, s.k_nodes, s.perm.p,
-                       s.pos_rb.p, s.pos_dl.p, s.strip_u.p, s.snode.p, coords, s_coef, f_meas, vals, rhs, rhs_add);
-    AFEM_LAUNCHED();
-  };
-  switch (sig) {
-#define AFEM_STENCIL_CASE(ID_, SIG_)                                                              \
-  case ID_:                                                                                      \
-    go(reinterpret_cast<const void*>(&k_assemble_stencil<SIG_>), k_assemble_stencil<SIG_>, SIG_.w); \
-    break;
-    AFEM_STENCIL_SIGS(AFEM_STENCIL_CASE)
-#undef AFEM_STENCIL_CASE
-    default:
-      throw Error(AFEM_ERR_STATE, "unknown stencil signature");
+  static int occ_k = 0;
+  static size_t occ_shm = 0;
+  auto kern = k_assemble_stencil<AFEM_STENCIL_PACK>;
+  const size_t shm = (size_t)stencil_tile_bytes(s.k_nodes, stencil_maxw<AFEM_STENCIL_PACK>());
+  if (occ_shm != shm) {
+    int q = 0;
+    AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, reinterpret_cast<const void*>(kern), 64, shm));
+    occ_k = q < 1 ? 1 : q;
+    occ_shm = shm;
   }
+  const int per_cu = occ_override() > 0 ? occ_override() : occ_k;
+  int64_t nblk = (int64_t)n_cu * per_cu;
+  if (nblk > s.n_k) nblk = s.n_k < 8 ? 8 : s.n_k;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm, stream, s.n_k, s.rec_k.p, tk, s.k_nodes, s.perm.p,
+                     s.pos_rb.p, s.pos_dl.p, s.strip_u.p, s.snode.p, coords, s_coef, f_meas, vals, rhs, rhs_add);
+  AFEM_LAUNCHED();
 }
 
 int stencil_match(uint64_t pat, int nsteps, int w, const uint8_t* slot32)
@@ -2722,7 +2753,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
           launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 1>), k_assemble_strip<4, 2, 16, 1>,
                    s.n_ur, s.rec_ur.p, s.tickets.p, shm_ur, side, s.ur_nodes, s.ur_w, s.urslot.p);
         }
-        launch_stencil(s.sig_k, s, ctx.n_cu, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add,
+        launch_stencil(s, ctx.n_cu, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add,
                        s.tickets.p + 384, ctx.stream);
       }
       else if (has_u) {

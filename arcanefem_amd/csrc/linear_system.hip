@@ -6,6 +6,7 @@
 // (Aleph semantics, femutils/AlephDoFLinearSystem.cc:192-223,501-583).
 #include "afem_internal.hpp"
 
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 
@@ -411,6 +412,156 @@ __global__ __launch_bounds__(256) void k_spmv_v16(int64_t n_rows, const int64_t*
       y[r] = si;
       if (DOT) d = x[r] * si;
     }
+  }
+  if (DOT) {
+    double bs = block_sum(d);
+    if (threadIdx.x == 0) partial[blockIdx.x] = bs;
+  }
+}
+
+// Pattern-compressed column indices for the CG's SpMV.  A structured mesh
+// numbers its nodes lexicographically, so the interior rows of a Kuhn box have
+// the same column offsets c - r (15 of them).  PatOff holds the offsets of
+// one interior row; flag[r] = 1 marks every row whose columns are r + off[k],
+// k < len (k_pat_flags, once per solve): the SpMV forms those columns instead
+// of reading them (4 of the ~13 B per non-zero), the other rows read theirs.
+// Values, their order and the summation order are the CSR's: y is bitwise
+// the k_spmv_v16 result.
+struct PatOff {
+  int32_t len;
+  int32_t off[16];
+};
+
+__global__ __launch_bounds__(256) void k_pat_flags(int64_t n_rows, const int64_t* __restrict__ rows,
+                                                   const int32_t* __restrict__ cols, PatOff po,
+                                                   uint8_t* __restrict__ flag, unsigned long long* __restrict__ count)
+{
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool ok = false;
+  if (r < n_rows) {
+    const int64_t a = rows[r];
+    ok = rows[r + 1] - a == po.len;
+    for (int k = 0; k < po.len && ok; ++k) ok = (int64_t)cols[a + k] == r + po.off[k];
+    flag[r] = ok ? 1 : 0;
+  }
+  const unsigned long long m = __ballot(ok);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (unsigned long long)__popcll(m));
+}
+
+// k_spmv_stream4u with the block's column indices formed in LDS first: the
+// thread of a pattern row writes r + off[k] for its row's positions, the
+// thread of any other row copies its columns from memory; the stream then
+// reads 4 columns per lane from LDS (ds_read_b128) instead of HBM.  Products,
+// their order and the row sums are k_spmv_stream4u's (bitwise equal y).
+// sample t of 256 rows spread over the range: its length and (<= 16) column offsets
+__global__ void k_pat_sample(int64_t n_rows, const int64_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                             int32_t* __restrict__ out)
+{
+  const int t = threadIdx.x;
+  const int64_t r = (int64_t)(t + 1) * n_rows / (blockDim.x + 2);
+  const int64_t a = rows[r], len = rows[r + 1] - a;
+  out[17 * t] = (int32_t)(len <= 16 ? len : 0);
+  for (int k = 0; k < 16; ++k) out[17 * t + 1 + k] = k < len ? (int32_t)(cols[a + k] - r) : 0;
+}
+
+template <bool DOT>
+__global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t nnz, const int64_t* __restrict__ rows,
+                                                       const int32_t* __restrict__ cols,
+                                                       const double* __restrict__ vals,
+                                                       const uint8_t* __restrict__ flag, PatOff po,
+                                                       const double* __restrict__ x, double* __restrict__ y,
+                                                       double* __restrict__ partial, int64_t max_seg)
+{
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* prod = reinterpret_cast<double*>(smem);
+  // the column image [q - (a & ~3)] overlays the products (every column is in
+  // registers before the first product is stored: segments <= kSpmvU groups)
+  int32_t* cl = reinterpret_cast<int32_t*>(smem);
+  const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t r0 = blk * kThreads;
+  const int64_t r1 = (r0 + kThreads < n_rows) ? r0 + kThreads : n_rows;
+  const int64_t a = rows[r0], b = rows[r1];
+  const int64_t a4 = a & ~int64_t(3);
+  const int64_t r = r0 + threadIdx.x;
+  int64_t ra = 0, re = 0;
+  if (r < r1) {
+    ra = rows[r];
+    re = rows[r + 1];
+    if (flag[r]) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < po.len) cl[ra - a4 + k] = (int32_t)r + po.off[k];
+    }
+    else {
+      for (int64_t k = ra; k < re; ++k) cl[k - a4] = cols[k];
+    }
+  }
+  __syncthreads();
+  const int64_t q0 = a4 + 4 * (int64_t)threadIdx.x;
+  auto load4 = [&](int64_t q, int (&c)[4], double (&v)[4]) {
+    const int4 c4 = *reinterpret_cast<const int4*>(cl + (q - a4));
+    c[0] = q >= a ? c4.x : 0;
+    c[1] = q + 1 >= a && q + 1 < b ? c4.y : 0;
+    c[2] = q + 2 >= a && q + 2 < b ? c4.z : 0;
+    c[3] = q + 3 >= a && q + 3 < b ? c4.w : 0;
+    if (q + 4 <= nnz) {
+      const double2 v01 = *reinterpret_cast<const double2*>(vals + q);
+      const double2 v23 = *reinterpret_cast<const double2*>(vals + q + 2);
+      v[0] = v01.x;
+      v[1] = v01.y;
+      v[2] = v23.x;
+      v[3] = v23.y;
+    }
+    else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = q + j < nnz ? vals[q + j] : 0.0;
+    }
+  };
+  const int rot = (int)(threadIdx.x >> 3) & 3;
+  auto put4 = [&](int64_t q, const double (&v)[4], const double (&xv)[4]) {
+    double pr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pr[j] = v[j] * xv[j];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = (t + rot) & 3;
+      const double w = j == 0 ? pr[0] : (j == 1 ? pr[1] : (j == 2 ? pr[2] : pr[3]));
+      if (q + j >= a && q + j < b) prod[q + j - a] = w;
+    }
+  };
+  {
+    int c[kSpmvU][4];
+    double v[kSpmvU][4];
+#pragma unroll
+    for (int u = 0; u < kSpmvU; ++u) {
+      const int64_t q = q0 + (int64_t)u * 4 * kThreads;
+      if (q < b) {
+        load4(q, c[u], v[u]);
+      }
+      else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          c[u][j] = 0;
+          v[u][j] = 0.0;
+        }
+      }
+    }
+    double xv[kSpmvU][4];
+#pragma unroll
+    for (int u = 0; u < kSpmvU; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xv[u][j] = x[c[u][j]];
+    __syncthreads();  // every column read before the products overwrite the column image
+#pragma unroll
+    for (int u = 0; u < kSpmvU; ++u) put4(q0 + (int64_t)u * 4 * kThreads, v[u], xv[u]);
+  }
+  __syncthreads();
+  double d = 0.0;
+  if (r < r1) {
+    double s = 0.0;
+    for (int64_t k = ra - a, e = re - a; k < e; ++k) s += prod[k];
+    y[r] = s;
+    if (DOT) d = x[r] * s;
   }
   if (DOT) {
     double bs = block_sum(d);
@@ -994,6 +1145,9 @@ struct SpmvPlan {
   int64_t blk_n = 0;
   const int64_t* blk_rows = nullptr;
   const int32_t* blk_cols = nullptr;
+  // rpb = -3: k_spmv_pat (pattern rows form their columns)
+  const uint8_t* pat_flag = nullptr;
+  PatOff po{};
 };
 
 __global__ void k_block_seg(int64_t n_rows, int rpb, const int64_t* __restrict__ row_ptr, unsigned long long* out)
@@ -1085,6 +1239,60 @@ SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
 {
   SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, ls.n_rows, ls.csr_cols, ls.csr_vals);
   const char* e = getenv("AFEM_SPMV");
+  // the pattern SpMV: the default for single-rank scalar systems (AFEM_SPMV=nopat
+  // or any other diagnostic mode: the CSR kernels as they are)
+  if ((!e || std::string(e) == "pat") && !ls.halo && ls.blk_k <= 1 && ls.n_rows > 64 && ls.csr_cols && ls.csr_vals &&
+      pl.rpb == kThreads && pl.wide && pl.max_seg + 3 <= 4 * kThreads * kSpmvU) {
+    // the most frequent column-offset pattern among 256 rows spread over the
+    // range (a structured box's interior stencil); rows that share it (k_pat_flags)
+    constexpr int kSamples = 256;
+    DevBuf<int32_t> smp;
+    smp.alloc(kSamples * 17);
+    hipLaunchKernelGGL(k_pat_sample, dim3(1), dim3(kSamples), 0, ctx.stream, ls.n_rows, ls.csr_rows, ls.csr_cols,
+                       smp.p);
+    AFEM_LAUNCHED();
+    std::vector<int32_t> hs(kSamples * 17);
+    AFEM_HIP(hipMemcpyAsync(hs.data(), smp.p, hs.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    std::map<std::vector<int64_t>, int> freq;
+    for (int i = 0; i < kSamples; ++i) {
+      const int len = hs[17 * i];
+      if (len < 1 || len > 16) continue;
+      ++freq[std::vector<int64_t>(hs.begin() + 17 * i + 1, hs.begin() + 17 * i + 1 + len)];
+    }
+    const std::vector<int64_t>* best = nullptr;
+    int bc = 0;
+    for (const auto& kv : freq)
+      if (kv.second > bc) {
+        bc = kv.second;
+        best = &kv.first;
+      }
+    const int64_t len = best ? (int64_t)best->size() : 0;
+    if (len >= 1 && len <= 16) {
+      int32_t c[16] = {};
+      for (int64_t k = 0; k < len; ++k) c[k] = (int32_t)(*best)[k];
+      const int64_t rc = 0;
+      PatOff po{};
+      po.len = (int32_t)len;
+      for (int k = 0; k < 16; ++k) po.off[k] = k < len ? (int32_t)(c[k] - rc) : 0;
+      if (ls.pat_flag.n < (size_t)ls.n_rows) ls.pat_flag.alloc(ls.n_rows);
+      DevBuf<unsigned long long> cnt;
+      cnt.alloc(1);
+      AFEM_HIP(hipMemsetAsync(cnt.p, 0, cnt.bytes(), ctx.stream));
+      hipLaunchKernelGGL(k_pat_flags, dim3(grid_for(ls.n_rows, 256)), dim3(256), 0, ctx.stream, ls.n_rows, ls.csr_rows,
+                         ls.csr_cols, po, ls.pat_flag.p, cnt.p);
+      AFEM_LAUNCHED();
+      unsigned long long hc = 0;
+      AFEM_HIP(hipMemcpyAsync(&hc, cnt.p, sizeof(hc), hipMemcpyDeviceToHost, ctx.stream));
+      ctx.sync();
+      if (hc * 2 >= (unsigned long long)ls.n_rows) {
+        pl.rpb = -3;
+        pl.po = po;
+        pl.pat_flag = ls.pat_flag.p;
+        return pl;
+      }
+    }
+  }
   if ((ls.blk_k == 2 || ls.blk_k == 3) && ls.blk_rows && ls.blk_n * ls.blk_k == ls.n_rows && ls.blk_n > 0 && !e) {
     pl.rpb = -2;
     pl.blk_k = ls.blk_k;
@@ -1115,6 +1323,15 @@ void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* ro
       AFEM_BLK(2)
     }
 #undef AFEM_BLK
+  }
+  else if (pl.rpb == -3) {
+    const size_t shm = (size_t)(8 * pl.max_seg + 32);
+    if (partial)
+      hipLaunchKernelGGL(k_spmv_pat<true>, dim3(nb), dim3(kThreads), shm, ctx.stream, n_rows, nnz, rows, cols, vals,
+                         pl.pat_flag, pl.po, x, y, partial, pl.max_seg);
+    else
+      hipLaunchKernelGGL(k_spmv_pat<false>, dim3(nb), dim3(kThreads), shm, ctx.stream, n_rows, nnz, rows, cols, vals,
+                         pl.pat_flag, pl.po, x, y, partial, pl.max_seg);
   }
   else if (pl.rpb < 0) {
     if (partial)
@@ -1324,6 +1541,7 @@ void ls_solve_direct(LinearSystem& ls, afem_solve_stats* st)
     st->rel_residual = bb > 0 ? std::sqrt(rr / bb) : 0.0;
     st->residual_norm = std::sqrt(rr);
     st->solve_ms = ms;
+    st->spmv_kernel = AFEM_SPMV_OTHER;
   }
 }
 }  // namespace
@@ -1588,6 +1806,11 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     st->rel_residual = rel;
     st->residual_norm = std::sqrt(std::fabs(ls.pinned[4]));
     st->solve_ms = ms;
+    st->spmv_kernel = pl.rpb == -3 ? AFEM_SPMV_PATTERN
+                      : pl.rpb == -2 ? AFEM_SPMV_BLOCK
+                      : pl.rpb == -1 ? AFEM_SPMV_VECTOR
+                      : (pl.rpb > 0 && pl.wide && pl.unroll) ? AFEM_SPMV_STREAM
+                                                             : AFEM_SPMV_OTHER;
   }
 }
 

@@ -1335,9 +1335,10 @@ void build_structure(Mesh& m, Structure& s)
       s.uslot.alloc(su.empty() ? 32 : su.size());
       if (!su.empty()) AFEM_HIP(hipMemcpyAsync(s.uslot.p, su.data(), su.size(), hipMemcpyHostToDevice, ctx.stream));
       {
-        // stencil split of the uniform list (scalar assembly): the slices of the
-        // most frequent compiled-in signature run k_assemble_stencil, the other
-        // uniform slices the uniform instance (rec_ur with their slot streams)
+        // stencil split of the uniform list (scalar assembly): the slices of a
+        // compiled-in signature run k_assemble_stencil (one kernel for all
+        // signatures, SliceRec::sig), the other uniform slices the uniform
+        // instance (rec_ur with their slot streams)
         std::vector<int> sid(ru.size());
         std::map<int, int64_t> cnt;
         for (size_t i = 0; i < ru.size(); ++i) {
@@ -1353,8 +1354,9 @@ void build_structure(Mesh& m, Structure& s)
         s.k_nodes = s.ur_nodes = s.ur_w = 0;
         for (size_t i = 0; i < ru.size(); ++i) {
           const SliceRec& r = ru[i];
-          if (best >= 0 && sid[i] == best) {
+          if (sid[i] >= 0) {
             rk.push_back(r);
+            rk.back().sig = (uint32_t)sid[i];
             s.k_nodes = std::max(s.k_nodes, (int)(r.meta & 0xFFFFu));
           }
           else {

@@ -42,6 +42,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MDoF/s assembly + CG iter/s, Poisson-3D P1 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# the CG's SpMV by afem_solve_stats.spmv_kernel (include/arcanefem_amd.h AFEM_SPMV_*)
+SPMV_KERNELS = {0: "k_spmv_stream4u", 1: "k_spmv_pat", 2: "k_spmv_v16", 3: "k_spmv_blk", 4: "other"}
 # block-3 assembly kernels by afem_bsr_stats.last_kernel (include/arcanefem_amd.h AFEM_KERNEL_*)
 ELAST3_KERNELS = {4: "k_assemble_elast_strip", 5: "k_assemble_elast_tet", 6: "k_assemble_elast_tet_global",
                   8: "k_assemble_elast_wg", 9: "k_assemble_elast_strip<..,BIG>"}
@@ -183,7 +185,8 @@ def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50):
            "roofline": roofline(bsr, mesh, kms),
            "cg_iter_per_s": round(ips, 2), "cg_roofline_frac": round(cg_bytes(nnz, mesh.n_own_nodes) * ips / 1e9
                                                                        / HBM_PEAK_GBS, 4),
-           "cg_device_ms": round(st["solve_ms"], 2), "sparsity_ms": round(sp_ms, 1)}
+           "cg_device_ms": round(st["solve_ms"], 2), "cg_spmv": SPMV_KERNELS.get(st["spmv_kernel"]),
+           "sparsity_ms": round(sp_ms, 1)}
     out["roofline"]["traffic"], out["roofline"]["traffic_profile"] = pmc_traffic(
         os.path.join(ROOT, "profiles", f"pmc_assembly_n{n}.json"), n)
     ctx.free(dbottom)
@@ -576,7 +579,7 @@ def main():
             "cg_iter_per_s": round(cg_iter_per_s, 2),
             "cg_ms_per_iter": round(cg_s * 1e3 / args.cg_iters, 4),
             "cg_roofline_frac": round(cg_bytes(nnz, n_own) * cg_iter_per_s / 1e9 / HBM_PEAK_GBS, 4),
-            "cg_device_ms": round(st["solve_ms"], 3),
+            "cg_device_ms": round(st["solve_ms"], 3), "cg_spmv": SPMV_KERNELS.get(st["spmv_kernel"]),
             "sparsity_ms": round(sparsity_ms, 1),
             "setup_s": round(setup_s, 2),
             **extras,

@@ -279,7 +279,13 @@ typedef struct afem_solve_stats {
   double rel_residual;  /* sqrt(r.z / r0.z0) */
   double residual_norm; /* ||b - A x||_2 over all ranks (recurrence residual) */
   double solve_ms;      /* device time of the solve */
+  int32_t spmv_kernel;  /* AFEM_SPMV_*: the SpMV the iteration ran */
 } afem_solve_stats;
+#define AFEM_SPMV_STREAM 0   /* CSR-stream (columns read from the CSR) */
+#define AFEM_SPMV_PATTERN 1  /* CSR-stream, interior-stencil rows form their columns */
+#define AFEM_SPMV_VECTOR 2   /* 16 lanes per row */
+#define AFEM_SPMV_BLOCK 3    /* node-block rows (NB_DOF 2 / 3) */
+#define AFEM_SPMV_OTHER 4    /* row-per-thread / no-unroll variants, direct solver */
 
 /* IDoFLinearSystemFactory::createInstance: a linear system over n_rows owned
  * DoFs; n_cols_local >= n_rows counts owned + ghost DoFs (column space of a
