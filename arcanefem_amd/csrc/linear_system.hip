@@ -470,14 +470,16 @@ __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t n
                                                        const double* __restrict__ vals,
                                                        const uint8_t* __restrict__ flag, PatOff po,
                                                        const double* __restrict__ x, double* __restrict__ y,
-                                                       double* __restrict__ partial, int64_t max_seg)
+                                                       double* __restrict__ partial, int64_t max_seg,
+                                                       const int32_t* __restrict__ blist = nullptr)
 {
   extern __shared__ __align__(16) unsigned char smem[];
   double* prod = reinterpret_cast<double*>(smem);
   // the column image [q - (a & ~3)] overlays the products (every column is in
   // registers before the first product is stored: segments <= kSpmvU groups)
   int32_t* cl = reinterpret_cast<int32_t*>(smem);
-  const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+  // blist: the row blocks of this launch (the CG's interior / halo-boundary split)
+  const int64_t blk = blist ? (int64_t)blist[blockIdx.x] : xcd_swizzle(blockIdx.x, gridDim.x);
   const int64_t r0 = blk * kThreads;
   const int64_t r1 = (r0 + kThreads < n_rows) ? r0 + kThreads : n_rows;
   const int64_t a = rows[r0], b = rows[r1];
@@ -1239,9 +1241,9 @@ SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
 {
   SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, ls.n_rows, ls.csr_cols, ls.csr_vals);
   const char* e = getenv("AFEM_SPMV");
-  // the pattern SpMV: the default for single-rank scalar systems (AFEM_SPMV=nopat
-  // or any other diagnostic mode: the CSR kernels as they are)
-  if ((!e || std::string(e) == "pat") && !ls.halo && ls.blk_k <= 1 && ls.n_rows > 64 && ls.csr_cols && ls.csr_vals &&
+  // the pattern SpMV: the default for scalar systems (AFEM_SPMV=nopat or any other
+  // diagnostic mode: the CSR kernels as they are)
+  if ((!e || std::string(e) == "pat") && ls.blk_k <= 1 && ls.n_rows > 64 && ls.csr_cols && ls.csr_vals &&
       pl.rpb == kThreads && pl.wide && pl.max_seg + 3 <= 4 * kThreads * kSpmvU) {
     // the most frequent column-offset pattern among 256 rows spread over the
     // range (a structured box's interior stencil); rows that share it (k_pat_flags)
@@ -1681,7 +1683,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   // of p is in flight (RCCL on the halo's stream), the rest after it lands
   // (host transport: the exchange completes in halo_begin; same split, so the
   // multi-rank GPU tests cover it)
-  const bool overlap = multi && ((pl.rpb > 0 && pl.wide && pl.unroll) || pl.rpb == -2);
+  const bool overlap = multi && ((pl.rpb > 0 && pl.wide && pl.unroll) || pl.rpb == -2 || pl.rpb == -3);
   int64_t n_int = 0;
   if (overlap) {
     // scalar rows per launch block: kThreads (CSR-stream) or K * 32 (node blocks)
@@ -1725,7 +1727,11 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
       const int64_t n_bd = pl.nblocks - n_int;
       auto part = [&](int64_t nbk, int64_t off) {
         if (nbk <= 0) return;
-        if (pl.rpb != -2)
+        if (pl.rpb == -3)
+          hipLaunchKernelGGL(k_spmv_pat<true>, dim3((unsigned)nbk), dim3(kThreads), (size_t)(8 * pl.max_seg + 32),
+                             ctx.stream, n, ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, pl.pat_flag, pl.po,
+                             ls.p.p, ls.q.p, ls.partial.p + off, pl.max_seg, ls.blist.p + off);
+        else if (pl.rpb != -2)
           hipLaunchKernelGGL(k_spmv_stream4u<true>, dim3((unsigned)nbk), dim3(kThreads), (size_t)pl.max_seg * 8,
                              ctx.stream, n, ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p,
                              ls.partial.p + off, ls.blist.p + off);

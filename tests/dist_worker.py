@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 # case parameters shared with the test
 POISSON = dict(n=5, nz=8)
+POISSON_PAT = dict(n=12, nz=16)  # slabs whose rows are mostly interior stencil rows: the pattern SpMV
 DYN = dict(n=3, nz=5, E=21e5, nu=0.28, rho=1.0, dt=1e-3, f=(0.0, -9.81, 1.0), steps=4)
 
 
@@ -34,8 +35,8 @@ def main():
     ctx = af.Context(0)
     comm = HostCommunicator(ctx)
     res = {}
-    if case == "poisson":
-        n, nz = POISSON["n"], POISSON["nz"]
+    if case in ("poisson", "poisson_pat"):
+        n, nz = (POISSON if case == "poisson" else POISSON_PAT)["n"], (POISSON if case == "poisson" else POISSON_PAT)["nz"]
         mesh = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=20250220, nranks=world, rank=rank)
         bsr = af.BSRFormat(mesh, 1).initialize(True)
         bsr.computeSparsity()
@@ -48,7 +49,7 @@ def main():
         st = ls.solve()
         _, _, l2g = mesh.download()
         res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
-                   converged=int(st["converged"]), rel=st["rel_residual"])
+                   converged=int(st["converged"]), rel=st["rel_residual"], spmv=st["spmv_kernel"])
         # CG iter/s with the halo attached (fixed iterations)
         ls.setSolverOptions(fixed_iterations=20)
         ls.solve()

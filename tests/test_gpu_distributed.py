@@ -53,10 +53,13 @@ def _run(case, world, tmp_path):
     return [dict(np.load(o)) for o in outs]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_distributed_poisson_solve(world, tmp_path):
-    res = _run("poisson", world, tmp_path)
-    n, nz = W.POISSON["n"], W.POISSON["nz"]
+@pytest.mark.parametrize("case,world", [("poisson", 2), ("poisson", 3), ("poisson_pat", 2)])
+def test_distributed_poisson_solve(case, world, tmp_path):
+    res = _run(case, world, tmp_path)
+    prm = W.POISSON if case == "poisson" else W.POISSON_PAT
+    n, nz = prm["n"], prm["nz"]
+    if case == "poisson_pat":  # the pattern SpMV in the interior / halo-boundary split
+        assert all(int(r["spmv"]) == 1 for r in res), [int(r["spmv"]) for r in res]
     g = O.structured_mesh(3, n, nz=nz)
     grp, gcols = O.sparsity(g["n_local"], g["n_own"], g["cells"])
     gvals, grhs = O.assemble_poisson(g["n_own"], g["cells"], g["coords"], grp, gcols, 5.5)
