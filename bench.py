@@ -82,10 +82,10 @@ def algorithmic_bytes(n_inc, n_local, n_own, nnz):
 
 
 def cg_bytes(nnz, n_own):
-    """Per Jacobi-PCG iteration of this implementation's kernel sequence
-    (DESIGN.md §3.3): SpMV 12 nnz + 8 (N+1) + 8 N gathers + 8 N store; update
-    64 N; direction 24 N."""
-    return 12 * nnz + 8 * (n_own + 1) + 104 * n_own
+    """Per Jacobi-PCG iteration: SpMV on the CSR 12 nnz + 8 (N+1)
+    + 8 N gathers + 8 N store; the two vector passes between the reductions
+    (r, z and r.z: 40 N; x and the new direction: 40 N)."""
+    return 12 * nnz + 8 * (n_own + 1) + 96 * n_own
 
 
 def poisson_setup(ctx, af, n, nz, world, rank):
