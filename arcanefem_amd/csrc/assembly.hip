@@ -1801,8 +1801,14 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
                                                            const double* __restrict__ coords, double lambda, double mu,
                                                            double c0, double fx, double fy, double fz,
                                                            double* __restrict__ vals, double* __restrict__ rhs,
-                                                           int rhs_add)
+                                                           int rhs_add, const uint8_t* __restrict__ strip_u,
+                                                           const SlotRec* __restrict__ uslots)
 {
+  // UMODE = 1 (uniform slices, as the scalar uniform instance): the slot bytes
+  // come from the slice's common 32-B slot stream (scalar loads), each step's
+  // coordinates from the lane's local-index stream (strip_u): no column-index
+  // table in LDS, no dependent LDS read per step
+  constexpr bool ULOC = UMODE == 1;
   extern __shared__ __align__(16) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1840,6 +1846,12 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
   SliceRec R0 = recs[p0];
   SliceRec R1 = recs[p1 < r1 ? p1 : p0];
   SliceRec R2 = recs[p2 < r1 ? p2 : p0];
+  SlotRec S0{}, S1{}, S2{};
+  if constexpr (ULOC) {
+    S0 = uslots[p0];
+    S1 = uslots[p1 < r1 ? p1 : p0];
+    S2 = uslots[p2 < r1 ? p2 : p0];
+  }
 
   // staging share of a thread: nodes u = tid and tid + 192 (u_cap <= 256)
   auto load_nid = [&](const SliceRec& R, int32_t(&nid)[2]) {
@@ -1853,6 +1865,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     int64_t rb;
     u32x4 l0, l1;
     u32x4 ch[MAXC];
+    u32x4 cu[MAXC];
     double x[2], y[2], z[2];
   };
   auto load_rows = [&](const SliceRec& R, Pre& p) {
@@ -1860,16 +1873,23 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     p.row = perm[q];
     p.dl = pos_dl[q];
     p.rb = pos_rb[q];
-    if (ci == 0) {  // the column-index table (staged by wave 0)
-      const int nq = 8 * (int)((R.meta >> 16) & 0xFFu);
-      const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R.lidx_off);
-      p.l0 = ls[max(min(lane, nq - 1), 0)];
-      p.l1 = ls[max(min(lane + 64, nq - 1), 0)];
-    }
     const int nc = (int)((R.meta >> 24) + 15) >> 4;
-    const u32x4* sp = reinterpret_cast<const u32x4*>(strip + (int64_t)R.strip_off * 1024) + lane;
+    if constexpr (ULOC) {
+      const u32x4* su = reinterpret_cast<const u32x4*>(strip_u + (int64_t)R.strip_off * 1024) + lane;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
+      for (int c = 0; c < MAXC; ++c) p.cu[c] = su[(int64_t)max(min(c, nc - 1), 0) * 64];
+    }
+    else {
+      if (ci == 0) {  // the column-index table (staged by wave 0)
+        const int nq = 8 * (int)((R.meta >> 16) & 0xFFu);
+        const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R.lidx_off);
+        p.l0 = ls[max(min(lane, nq - 1), 0)];
+        p.l1 = ls[max(min(lane + 64, nq - 1), 0)];
+      }
+      const u32x4* sp = reinterpret_cast<const u32x4*>(strip + (int64_t)R.strip_off * 1024) + lane;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
+    }
   };
   auto gather = [&](const int32_t(&nid)[2], Pre& p) {
 #pragma unroll
@@ -1896,6 +1916,8 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
   for (;;) {
     const unsigned long long t4 = issue();  // read at the end of this iteration
     const SliceRec R3 = recs[p3 < r1 ? p3 : p0];
+    SlotRec S3{};
+    if constexpr (ULOC) S3 = uslots[p3 < r1 ? p3 : p0];
     const int nsteps = (int)(R0.meta >> 24);
     const int W = (int)((R0.meta >> 16) & 0xFFu);
     const int nu = (int)(R0.meta & 0xFFFFu);
@@ -1909,7 +1931,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         cs[2 * u_cap + u] = cur.z[k];
       }
     }
-    if (ci == 0) {
+    if (!ULOC && ci == 0) {
       const int nq = 8 * W;
       u32x4* dst = reinterpret_cast<u32x4*>(li);
       dst[max(min(lane, nq - 1), 0)] = cur.l0;
@@ -1931,7 +1953,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     const uint32_t dslot = cur.dl & 0xFFu;
     const uint16_t* lrow = li + lane;
     auto coord = [&](int u) { return V3{ ca[u], cb[u], cc[u] }; };
-    const V3 xi = coord((int)lrow[dslot * 64]);
+    const V3 xi = coord(ULOC ? (int)(cur.dl >> 16) : (int)lrow[dslot * 64]);
     double macc = 0.0;
     V3 eP{ 0.0, 0.0, 0.0 }, eQ{ 0.0, 0.0, 0.0 }, eR{ 0.0, 0.0, 0.0 };
     V3 cP{ 0.0, 0.0, 0.0 }, cN{ 0.0, 0.0, 0.0 };
@@ -1950,10 +1972,21 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     auto sel = [](bool c, V3 a, V3 b) { return V3{ c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z }; };
     auto keep = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
     auto byte_at = [&](int j) -> uint32_t {
-      const u32x4 w = cur.ch[j >> 4];
+      if constexpr (ULOC) {  // scalar: the slice's common slot stream
+        return (S0.w[(j >> 2) & 7] >> (8 * (j & 3))) & 0xFFu;
+      }
+      else {
+        const u32x4 w = cur.ch[j >> 4];
+        const int q = (j >> 2) & 3;
+        const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
+        return (wq >> (8 * (j & 3))) & 0xFFu;
+      }
+    };
+    auto uloc_at = [&](int j) -> int {  // local node index of step j (ULOC)
+      const u32x4 w = cur.cu[j >> 4];
       const int q = (j >> 2) & 3;
       const uint32_t wq = q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w));
-      return (wq >> (8 * (j & 3))) & 0xFFu;
+      return (int)((wq >> (8 * (j & 3))) & 0xFFu);
     };
     constexpr int NSTEP = 16 * MAXC;
     if constexpr (UMODE == 1) {
@@ -1993,24 +2026,20 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
       };
       {
         const uint32_t b0 = byte_at(0), b1 = byte_at(1);
-        eQ = sub(coord(lidx_of(b0)), xi);
-        eR = sub(coord(lidx_of(b1)), xi);
+        eQ = sub(coord(uloc_at(0)), xi);
+        eR = sub(coord(uloc_at(1)), xi);
         aQ = acc_lane + 192 * (b0 & 63u);
         aR = acc_lane + 192 * (b1 & 63u);
         cP = cross(eQ, eR);
       }
-      int u1 = lidx_of(byte_at(2));
-      V3 xc = coord(u1);
-      u1 = lidx_of(byte_at(3));
+      V3 xc = coord(uloc_at(2));
 #pragma unroll
       for (int j = 2; j < NSTEP; ++j) {
         if ((j & 1) == 0 && j >= nsteps) break;
-        const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
-        const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
+        const V3 xn = j + 1 < NSTEP ? coord(uloc_at(j + 1 < NSTEP ? j + 1 : j)) : xc;
         if (__builtin_expect((pat >> j) & 1u, 0)) ustep(std::true_type{}, byte_at(j), xc);
         else ustep(std::false_type{}, byte_at(j), xc);
         xc = xn;
-        u1 = u2;
       }
     }
     else {
@@ -2127,6 +2156,11 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     R0 = R1;
     R1 = R2;
     R2 = R3;
+    if constexpr (ULOC) {
+      S0 = S1;
+      S1 = S2;
+      S2 = S3;
+    }
     cur = nxt;
 #pragma unroll
     for (int k = 0; k < 2; ++k) nid1[k] = nid2[k];
@@ -2986,7 +3020,7 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(192), shm, ctx.stream, n_items, list, tk, (int)ucap2,
                          s.max_slice_w, b.order_per_block, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p,
                          s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr,
-                         rhs_add);
+                         rhs_add, s.strip_u.p, reinterpret_cast<const SlotRec*>(s.uslot.p));
       AFEM_LAUNCHED();
     };
     if (use_uni)
