@@ -321,6 +321,8 @@ struct LinearSystem {
   // solver work
   DevBuf<double> r, z, p, q, dinv, partial, scal;
   mutable DevBuf<uint8_t> pat_flag;  // rows whose columns follow the dominant offset pattern (pattern SpMV)
+  mutable DevBuf<int32_t> pat_smp;   // the pattern detection's row samples
+  mutable DevBuf<unsigned long long> pat_cnt;
   DevBuf<double> x0;      // the caller's initial guess (opts.initial_guess = 1)
   DevBuf<double> binv;    // block-Jacobi 3: inverse node blocks [n/3][9]
   DevBuf<int32_t> blist;  // multi-rank CG: SpMV row blocks, interior ones first

@@ -1263,13 +1263,12 @@ SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
     // the most frequent column-offset pattern among 256 rows spread over the
     // range (a structured box's interior stencil); rows that share it (k_pat_flags)
     constexpr int kSamples = 256;
-    DevBuf<int32_t> smp;
-    smp.alloc(kSamples * 17);
+    if (ls.pat_smp.n < (size_t)(kSamples * 17)) ls.pat_smp.alloc(kSamples * 17);
     hipLaunchKernelGGL(k_pat_sample, dim3(1), dim3(kSamples), 0, ctx.stream, ls.n_rows, ls.csr_rows, ls.csr_cols,
-                       smp.p);
+                       ls.pat_smp.p);
     AFEM_LAUNCHED();
     std::vector<int32_t> hs(kSamples * 17);
-    AFEM_HIP(hipMemcpyAsync(hs.data(), smp.p, hs.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx.stream));
+    AFEM_HIP(hipMemcpyAsync(hs.data(), ls.pat_smp.p, hs.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx.stream));
     ctx.sync();
     std::map<std::vector<int64_t>, int> freq;
     for (int i = 0; i < kSamples; ++i) {
@@ -1293,14 +1292,13 @@ SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
       po.len = (int32_t)len;
       for (int k = 0; k < 16; ++k) po.off[k] = k < len ? (int32_t)(c[k] - rc) : 0;
       if (ls.pat_flag.n < (size_t)ls.n_rows) ls.pat_flag.alloc(ls.n_rows);
-      DevBuf<unsigned long long> cnt;
-      cnt.alloc(1);
-      AFEM_HIP(hipMemsetAsync(cnt.p, 0, cnt.bytes(), ctx.stream));
+      if (!ls.pat_cnt.p) ls.pat_cnt.alloc(1);
+      AFEM_HIP(hipMemsetAsync(ls.pat_cnt.p, 0, ls.pat_cnt.bytes(), ctx.stream));
       hipLaunchKernelGGL(k_pat_flags, dim3(grid_for(ls.n_rows, 256)), dim3(256), 0, ctx.stream, ls.n_rows, ls.csr_rows,
-                         ls.csr_cols, po, ls.pat_flag.p, cnt.p);
+                         ls.csr_cols, po, ls.pat_flag.p, ls.pat_cnt.p);
       AFEM_LAUNCHED();
       unsigned long long hc = 0;
-      AFEM_HIP(hipMemcpyAsync(&hc, cnt.p, sizeof(hc), hipMemcpyDeviceToHost, ctx.stream));
+      AFEM_HIP(hipMemcpyAsync(&hc, ls.pat_cnt.p, sizeof(hc), hipMemcpyDeviceToHost, ctx.stream));
       ctx.sync();
       if (hc * 2 >= (unsigned long long)ls.n_rows) {
         pl.rpb = -3;
