@@ -222,6 +222,11 @@ struct Structure {
   // streams urslot); rec_u stays whole (block-3 uses it)
   DevBuf<SliceRec> rec_k, rec_ur;
   DevBuf<uint8_t> urslot;
+  // block-3 split of the uniform list: signature-0 slices (rec_k0) and the rest
+  // (rec_u1 + their slot streams u1slot)
+  DevBuf<SliceRec> rec_k0, rec_u1;
+  DevBuf<uint8_t> u1slot;
+  int64_t n_k0 = 0, n_u1 = 0;
   int64_t n_k = 0, n_ur = 0;
   int sig_k = -1, k_nodes = 0, ur_nodes = 0, ur_w = 0;
   bool rec_ok = false;                     // offsets fit the 32-bit record fields

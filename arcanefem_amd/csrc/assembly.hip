@@ -1094,6 +1094,9 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
 // order, rounded like ds_add_f64: the adds are not contracted): the three
 // instances give the same bits.
 #include "stencil_sigs.inc"  // constexpr StencilSig kSig<name> (StencilSig: afem_internal.hpp)
+#define AFEM_STENCIL_PTR(ID_, SIG_) &SIG_,
+inline constexpr const StencilSig* kStencilSigPtrs[] = { AFEM_STENCIL_SIGS(AFEM_STENCIL_PTR) };
+#undef AFEM_STENCIL_PTR
 
 template <const StencilSig& S>
 struct StencilWin {  // slots of the window nodes P, Q, R after step j's rotation
@@ -1808,7 +1811,10 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
   // come from the slice's common 32-B slot stream (scalar loads), each step's
   // coordinates from the lane's local-index stream (strip_u): no column-index
   // table in LDS, no dependent LDS read per step
-  constexpr bool ULOC = UMODE == 1;
+  // UMODE = 3 (stencil): the same with the step bytes and shift/swap bits of
+  // compiled-in signature 0 (the interior brick; rec_k0): accumulator offsets
+  // are immediates, the shift/swap arms fixed at compile time
+  constexpr bool ULOC = UMODE == 1 || UMODE == 3;
   extern __shared__ __align__(16) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1847,7 +1853,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
   SliceRec R1 = recs[p1 < r1 ? p1 : p0];
   SliceRec R2 = recs[p2 < r1 ? p2 : p0];
   SlotRec S0{}, S1{}, S2{};
-  if constexpr (ULOC) {
+  if constexpr (UMODE == 1) {
     S0 = uslots[p0];
     S1 = uslots[p1 < r1 ? p1 : p0];
     S2 = uslots[p2 < r1 ? p2 : p0];
@@ -1917,7 +1923,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     const unsigned long long t4 = issue();  // read at the end of this iteration
     const SliceRec R3 = recs[p3 < r1 ? p3 : p0];
     SlotRec S3{};
-    if constexpr (ULOC) S3 = uslots[p3 < r1 ? p3 : p0];
+    if constexpr (UMODE == 1) S3 = uslots[p3 < r1 ? p3 : p0];
     const int nsteps = (int)(R0.meta >> 24);
     const int W = (int)((R0.meta >> 16) & 0xFFu);
     const int nu = (int)(R0.meta & 0xFFFFu);
@@ -1989,8 +1995,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
       return (int)((wq >> (8 * (j & 3))) & 0xFFu);
     };
     constexpr int NSTEP = 16 * MAXC;
-    if constexpr (UMODE == 1) {
-      const uint64_t pat = R0.pat;
+    if constexpr (ULOC) {
       auto ustep = [&](auto swap_c, uint32_t byte, V3 xd) {
         constexpr bool SWAP = decltype(swap_c)::value;
         double* const aD = acc_lane + 192 * (byte & 63u);
@@ -2024,22 +2029,36 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         gQ = elast_acc(gQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
         gR = elast_acc(V3{ 0.0, 0.0, 0.0 }, e, cRn, s, mass);
       };
-      {
-        const uint32_t b0 = byte_at(0), b1 = byte_at(1);
-        eQ = sub(coord(uloc_at(0)), xi);
-        eR = sub(coord(uloc_at(1)), xi);
-        aQ = acc_lane + 192 * (b0 & 63u);
-        aR = acc_lane + 192 * (b1 & 63u);
-        cP = cross(eQ, eR);
-      }
-      V3 xc = coord(uloc_at(2));
+      // bytes(j): step j's byte, swp(j): step j is a swap (scalar, or constants)
+      auto run = [&](auto bytes, auto swp) {
+        {
+          const uint32_t b0 = bytes(0), b1 = bytes(1);
+          eQ = sub(coord(uloc_at(0)), xi);
+          eR = sub(coord(uloc_at(1)), xi);
+          aQ = acc_lane + 192 * (b0 & 63u);
+          aR = acc_lane + 192 * (b1 & 63u);
+          cP = cross(eQ, eR);
+        }
+        V3 xc = coord(uloc_at(2));
 #pragma unroll
-      for (int j = 2; j < NSTEP; ++j) {
-        if ((j & 1) == 0 && j >= nsteps) break;
-        const V3 xn = j + 1 < NSTEP ? coord(uloc_at(j + 1 < NSTEP ? j + 1 : j)) : xc;
-        if (__builtin_expect((pat >> j) & 1u, 0)) ustep(std::true_type{}, byte_at(j), xc);
-        else ustep(std::false_type{}, byte_at(j), xc);
-        xc = xn;
+        for (int j = 2; j < NSTEP; ++j) {
+          if ((j & 1) == 0 && j >= nsteps) break;
+          const V3 xn = j + 1 < NSTEP ? coord(uloc_at(j + 1 < NSTEP ? j + 1 : j)) : xc;
+          if (__builtin_expect(swp(j), 0)) ustep(std::true_type{}, bytes(j), xc);
+          else ustep(std::false_type{}, bytes(j), xc);
+          xc = xn;
+        }
+      };
+      if constexpr (UMODE == 1) {
+        const uint64_t pat = R0.pat;
+        run(byte_at, [&](int j) { return ((pat >> j) & 1u) != 0; });
+      }
+      else {
+        // the list holds the slices of signature 0 (the interior brick) only (one
+        // unrolled body: a second one in the same kernel spilled to scratch)
+        constexpr const StencilSig& S = *kStencilSigPtrs[0];
+        run([](int j) -> uint32_t { return j < S.nsteps ? S.slot[j] : (uint32_t)(0xC0 | S.dslot); },
+            [](int j) { return ((S.pat >> j) & 1u) != 0; });
       }
     }
     else {
@@ -2156,7 +2175,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     R0 = R1;
     R1 = R2;
     R2 = R3;
-    if constexpr (ULOC) {
+    if constexpr (UMODE == 1) {
       S0 = S1;
       S1 = S2;
       S2 = S3;
@@ -3006,9 +3025,13 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
     static std::map<std::pair<const void*, size_t>, int> occ_wg;
     const char* ue = getenv("AFEM_ASSEMBLY_UNIFORM");
     const bool use_uni = !(ue && atoi(ue) == 0) && s.n_uni > 0;
-    if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);
+    // stencil split (AFEM_ASSEMBLY_STENCIL=0: the whole uniform list through the uniform instance)
+    const char* ke = getenv("AFEM_ASSEMBLY_STENCIL");
+    const bool use_k = use_uni && s.n_k0 > 0 && !(ke && atoi(ke) == 0);
+    if (s.tickets.n < 4 * 8 * 16) s.tickets.alloc(4 * 8 * 16);
     AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
-    auto launch = [&](const void* fn, auto kern, int64_t n_items, const SliceRec* list, unsigned long long* tk) {
+    auto launch = [&](const void* fn, auto kern, int64_t n_items, const SliceRec* list, unsigned long long* tk,
+                      const uint8_t* slots = nullptr) {
       auto it = occ_wg.find({ fn, shm });
       if (it == occ_wg.end()) {
         int q = 0;
@@ -3020,10 +3043,17 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(192), shm, ctx.stream, n_items, list, tk, (int)ucap2,
                          s.max_slice_w, b.order_per_block, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p,
                          s.snode.p, b.mesh->coords.p, lambda, 0.5 * mu2, c0, fx, fy, fz, b.values.p, f ? rhs : nullptr,
-                         rhs_add, s.strip_u.p, reinterpret_cast<const SlotRec*>(s.uslot.p));
+                         rhs_add, s.strip_u.p, reinterpret_cast<const SlotRec*>(slots ? slots : s.uslot.p));
       AFEM_LAUNCHED();
     };
-    if (use_uni)
+    if (use_k) {
+      launch(reinterpret_cast<const void*>(&k_assemble_elast_wg<2, 16, 3>), k_assemble_elast_wg<2, 16, 3>, s.n_k0,
+             s.rec_k0.p, s.tickets.p + 384);
+      if (s.n_u1 > 0)
+        launch(reinterpret_cast<const void*>(&k_assemble_elast_wg<2, 16, 1>), k_assemble_elast_wg<2, 16, 1>, s.n_u1,
+               s.rec_u1.p, s.tickets.p, s.u1slot.p);
+    }
+    else if (use_uni)
       launch(reinterpret_cast<const void*>(&k_assemble_elast_wg<2, 16, 1>), k_assemble_elast_wg<2, 16, 1>, s.n_uni,
              s.rec_u.p, s.tickets.p);
     const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;

@@ -1349,8 +1349,8 @@ void build_structure(Mesh& m, Structure& s)
         int best = -1;
         for (const auto& kv : cnt)
           if (best < 0 || kv.second > cnt[best]) best = kv.first;
-        std::vector<SliceRec> rk, rur;
-        std::vector<uint8_t> sur;
+        std::vector<SliceRec> rk, rur, rk0, ru1;
+        std::vector<uint8_t> sur, su1;
         s.k_nodes = s.ur_nodes = s.ur_w = 0;
         for (size_t i = 0; i < ru.size(); ++i) {
           const SliceRec& r = ru[i];
@@ -1371,6 +1371,22 @@ void build_structure(Mesh& m, Structure& s)
         s.n_ur = (int64_t)rur.size();
         upload(s.rec_k, rk);
         upload(s.rec_ur, rur);
+        for (size_t i = 0; i < ru.size(); ++i) {
+          if (sid[i] == 0) {
+            rk0.push_back(ru[i]);
+          }
+          else {
+            ru1.push_back(ru[i]);
+            su1.insert(su1.end(), su.begin() + 32 * i, su.begin() + 32 * (i + 1));
+          }
+        }
+        s.n_k0 = (int64_t)rk0.size();
+        s.n_u1 = (int64_t)ru1.size();
+        upload(s.rec_k0, rk0);
+        upload(s.rec_u1, ru1);
+        s.u1slot.alloc(su1.empty() ? 32 : su1.size());
+        if (!su1.empty())
+          AFEM_HIP(hipMemcpyAsync(s.u1slot.p, su1.data(), su1.size(), hipMemcpyHostToDevice, ctx.stream));
         s.urslot.alloc(sur.empty() ? 32 : sur.size());
         if (!sur.empty())
           AFEM_HIP(hipMemcpyAsync(s.urslot.p, sur.data(), sur.size(), hipMemcpyHostToDevice, ctx.stream));

@@ -83,6 +83,40 @@ def test_elasticity3d_uniform_variant_bitwise(ctx, monkeypatch, use_csr):
     assert np.array_equal(r_uni, r_gen)
 
 
+@pytest.mark.parametrize("n", [13, 22])
+@pytest.mark.parametrize("use_csr", [False, True])
+def test_elasticity3d_stencil_instance_bitwise(ctx, monkeypatch, n, use_csr):
+    """Interior bricks (compiled-in signature 0) run the workgroup kernel's
+    stencil instance (step bytes and shift/swap arms as constants): the same
+    bits as the uniform instance (AFEM_ASSEMBLY_STENCIL=0) and the oracle's
+    values."""
+    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=4)
+    bsr = af.BSRFormat(mesh, 3).initialize(use_csr)
+    bsr.computeSparsity()
+    st = bsr.stats()
+    assert st["stencil_sig"] == 0 and st["stencil_slices"] > 0
+    n3 = 3 * mesh.n_own_nodes
+    drhs = ctx.malloc(8 * n3)
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
+    assert bsr.stats()["last_kernel"] == 8
+    v_k, r_k = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
+    monkeypatch.setenv("AFEM_ASSEMBLY_STENCIL", "0")
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
+    rows, cols, v_u = bsr.download()
+    r_u = ctx.to_host(drhs, n3, np.float64)
+    ctx.free(drhs)
+    assert np.array_equal(v_k, v_u), f"{np.count_nonzero(v_k != v_u)} values differ"
+    assert np.array_equal(r_k, r_u)
+    cells, coords, _ = mesh.download()
+    orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+    ovals, orhs = O.assemble_elasticity_tet(mesh.n_own_nodes, cells, coords, orp, ocols, LAM, MU2, 3.7e6,
+                                            (0.5, -1.0, 2.0))
+    if use_csr:
+        ovals = O.blocks_to_row_order_k(orp, ovals, 3)
+    assert np.abs(v_k - ovals).max() <= VAL_TOL * np.abs(ovals).max()
+    assert np.abs(r_k - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+
+
 @pytest.mark.parametrize("which", ["bigbox", "box"])
 @pytest.mark.parametrize("use_csr", [False, True])
 def test_elasticity3d_workgroup_kernel_bitwise(ctx, monkeypatch, which, use_csr):
