@@ -2136,10 +2136,17 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
       if (t < W)
 #pragma unroll
         for (int k = 0; k < 3; ++k) sum[k] += rv[3 * t + k];
+    // stencil instance, full slice (64 rows of the signature's length WS): row L's
+    // values are flat positions [9 WS L, 9 WS (L + 1)) -- a division by a
+    // constant instead of the owner / prefix tables
+    constexpr int WS = UMODE == 3 ? kStencilSigPtrs[0]->w : 0;
+    const bool full = UMODE == 3 && total == 64 * WS;
     if (ci == 0) {
-      fps[lane] = fp;
       rbs[lane] = active ? rb : 0;
-      for (int t = 0; t < len; ++t) bown[fp + t] = (uint8_t)lane;
+      if (!full) {
+        fps[lane] = fp;
+        for (int t = 0; t < len; ++t) bown[fp + t] = (uint8_t)lane;
+      }
     }
     __syncthreads();  // every wave's accumulator reads before the flat image overwrites them
     double* const flat = acc_all;
@@ -2162,9 +2169,18 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     __syncthreads();
     const int64_t pn = uni(claim[0]);
     // store: flat position P is value P - 9 fps[L] of row lane L = bown[P / 9]
-    for (int P = tid; P < 9 * total; P += 192) {
-      const int L = bown[P / 9];
-      vals[9 * rbs[L] + (P - 9 * fps[L])] = flat[P];
+    if (UMODE == 3 && full) {
+      constexpr int B = 9 * (WS > 0 ? WS : 1);
+      for (int P = tid; P < 64 * B; P += 192) {
+        const int L = P / B;
+        vals[9 * rbs[L] + (P - L * B)] = flat[P];
+      }
+    }
+    else {
+      for (int P = tid; P < 9 * total; P += 192) {
+        const int L = bown[P / 9];
+        vals[9 * rbs[L] + (P - 9 * fps[L])] = flat[P];
+      }
     }
     __syncthreads();
     if (p1 >= r1) break;
