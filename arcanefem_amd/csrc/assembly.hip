@@ -1692,7 +1692,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
           for (int k = 0; k < 3; ++k) {
             const int j = k + ci < 3 ? k + ci : k + ci - 3;
             const double v =
-                t == (int)dslot ? -sum[k] + (k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0) : acc_lane[192 * t + 64 * k];
+                t == (int)dslot ? add_nc(-sum[k], k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0) : acc_lane[192 * t + 64 * k];
             vals[per_block ? 9 * (rb + t) + 3 * ci + j : 9 * rb + 3 * (int64_t)ci * len + 3 * t + j] = v;
           }
         }
@@ -1745,7 +1745,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const int j = k + ci < 3 ? k + ci : k + ci - 3;
-        acc[fp + 3 * (int)dslot + j] = -sum[k] + (k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0);
+        acc[fp + 3 * (int)dslot + j] = add_nc(-sum[k], k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0);
       }
     }
     rbs[lane] = 9 * rb + 3 * ci * (per_block ? 1 : (int64_t)len);
@@ -2153,14 +2153,27 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     // value (t, k) of the rotated frame = block column j = (ci + k) % 3; the
     // block (row, t) holds 9 values: per block [i][j] at 9 t + 3 i + j, per
     // row (CSR order) at 3 len i + 3 t + j
-    if (active) {
+    if (UMODE == 3 && full) {
+      // every row: the signature's length and diagonal slot, prefix 9 WS lane
+      constexpr int DS = UMODE == 3 ? kStencilSigPtrs[0]->dslot : 0;
+      double* const fr = flat + 9 * WS * lane + (per_block ? 3 * ci : 3 * WS * ci);
+#pragma unroll
+      for (int t = 0; t < WS; ++t)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int j = k + ci < 3 ? k + ci : k + ci - 3;
+          const double v = t == DS ? add_nc(-sum[k], k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0) : rv[3 * t + k];
+          fr[(per_block ? 9 * t : 3 * t) + j] = v;
+        }
+    }
+    else if (active) {
 #pragma unroll
       for (int t = 0; t < MAXW; ++t)
         if (t < len) {
 #pragma unroll
           for (int k = 0; k < 3; ++k) {
             const int j = k + ci < 3 ? k + ci : k + ci - 3;
-            const double v = t == (int)dslot ? -sum[k] + (k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0) : rv[3 * t + k];
+            const double v = t == (int)dslot ? add_nc(-sum[k], k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0) : rv[3 * t + k];
             flat[9 * fp + (per_block ? 9 * t + 3 * ci + j : 3 * len * ci + 3 * t + j)] = v;
           }
         }
@@ -2334,7 +2347,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_tet(int u_cap, int w_cap,
       if (t != (int)dslot)
         for (int jj = 0; jj < 3; ++jj) sum[jj] += acc_lane[192 * t + 64 * jj];
     for (int jj = 0; jj < 3; ++jj)
-      acc_lane[192 * dslot + 64 * jj] = -sum[jj] + (jj == ci ? c0 * macc * (1.0 / 24.0) : 0.0);
+      acc_lane[192 * dslot + 64 * jj] = add_nc(-sum[jj], jj == ci ? c0 * macc * (1.0 / 24.0) : 0.0);
     for (int t = 0; t < len; ++t)
       for (int jj = 0; jj < 3; ++jj)
         vals[per_block ? (rb + t) * 9 + 3 * ci + jj : rb * 9 + (int64_t)ci * 3 * len + 3 * t + jj] =
