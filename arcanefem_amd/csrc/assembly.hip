@@ -1101,10 +1101,18 @@ inline constexpr const StencilSig* kStencilSigPtrs[] = { AFEM_STENCIL_SIGS(AFEM_
 template <const StencilSig& S>
 struct StencilWin {  // slots of the window nodes P, Q, R after step j's rotation
   int p[32] = {}, q[32] = {}, r[32] = {};
+  // first[j]: the node step j drops leaves the window for the first time (its
+  // accumulator's first contribution: a store, not an add); fin[k]: the same for
+  // the final P, Q, R
+  bool first[32] = {}, fin[3] = {};
   constexpr StencilWin()
   {
+    bool seen[64] = {};
     int P = S.dslot, Q = S.slot[0] & 63, R = S.slot[1] & 63;
     for (int j = 2; j < S.nsteps; ++j) {
+      const int d = ((S.pat >> j) & 1u) ? Q : P;
+      first[j] = !seen[d];
+      seen[d] = true;
       if (!((S.pat >> j) & 1u)) P = Q;
       Q = R;
       R = S.slot[j] & 63;
@@ -1112,6 +1120,11 @@ struct StencilWin {  // slots of the window nodes P, Q, R after step j's rotatio
       q[j] = Q;
       r[j] = R;
     }
+    fin[0] = !seen[P];
+    seen[P] = true;
+    fin[1] = !seen[Q];
+    seen[Q] = true;
+    fin[2] = !seen[R];
   }
 };
 template <const StencilSig& S>
@@ -1400,6 +1413,14 @@ __device__ __forceinline__ void flush3(double* a, V3 g)
   atomicAdd(a, g.x);
   atomicAdd(a + 64, g.y);
   atomicAdd(a + 128, g.z);
+}
+// the node's first flush (stencil instance: known at compile time): a store,
+// so the accumulators need no zero fill (0 + g = g)
+__device__ __forceinline__ void store3(double* a, V3 g)
+{
+  a[0] = g.x;
+  a[64] = g.y;
+  a[128] = g.z;
 }
 
 // ---------------------------------------------------------------- block-3 elasticity, persistent strips
@@ -1943,7 +1964,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
       dst[max(min(lane, nq - 1), 0)] = cur.l0;
       dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
     }
-    {
+    if constexpr (UMODE != 3) {  // the stencil instance stores every slot's first contribution
       double2* a2 = reinterpret_cast<double2*>(acc);
       for (int q = lane; q < 96 * W; q += 64) a2[q] = make_double2(0.0, 0.0);
     }
@@ -1996,19 +2017,22 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     };
     constexpr int NSTEP = 16 * MAXC;
     if constexpr (ULOC) {
-      auto ustep = [&](auto swap_c, uint32_t byte, V3 xd) {
+      auto ustep = [&](auto swap_c, auto first_c, uint32_t byte, V3 xd) {
         constexpr bool SWAP = decltype(swap_c)::value;
+        constexpr bool FIRST = decltype(first_c)::value;
         double* const aD = acc_lane + 192 * (byte & 63u);
         const V3 eD = sub(xd, xi);
         V3 cRn;
         if constexpr (SWAP) {
           cRn = cN;
-          flush3(aQ, gQ);
+          if constexpr (FIRST) store3(aQ, gQ);
+          else flush3(aQ, gQ);
         }
         else {
           cRn = cP;
           eP = eQ;
-          flush3(aP, gP);
+          if constexpr (FIRST) store3(aP, gP);
+          else flush3(aP, gP);
           aP = aQ;
           gP = gQ;
         }
@@ -2030,7 +2054,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         gR = elast_acc(V3{ 0.0, 0.0, 0.0 }, e, cRn, s, mass);
       };
       // bytes(j): step j's byte, swp(j): step j is a swap (scalar, or constants)
-      auto run = [&](auto bytes, auto swp) {
+      auto run = [&](auto bytes, auto swp, auto fst) {
         {
           const uint32_t b0 = bytes(0), b1 = bytes(1);
           eQ = sub(coord(uloc_at(0)), xi);
@@ -2044,21 +2068,28 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         for (int j = 2; j < NSTEP; ++j) {
           if ((j & 1) == 0 && j >= nsteps) break;
           const V3 xn = j + 1 < NSTEP ? coord(uloc_at(j + 1 < NSTEP ? j + 1 : j)) : xc;
-          if (__builtin_expect(swp(j), 0)) ustep(std::true_type{}, bytes(j), xc);
-          else ustep(std::false_type{}, bytes(j), xc);
+          if (fst(j)) {
+            if (swp(j)) ustep(std::true_type{}, std::true_type{}, bytes(j), xc);
+            else ustep(std::false_type{}, std::true_type{}, bytes(j), xc);
+          }
+          else {
+            if (__builtin_expect(swp(j), 0)) ustep(std::true_type{}, std::false_type{}, bytes(j), xc);
+            else ustep(std::false_type{}, std::false_type{}, bytes(j), xc);
+          }
           xc = xn;
         }
       };
       if constexpr (UMODE == 1) {
         const uint64_t pat = R0.pat;
-        run(byte_at, [&](int j) { return ((pat >> j) & 1u) != 0; });
+        run(byte_at, [&](int j) { return ((pat >> j) & 1u) != 0; }, [](int) { return false; });
       }
       else {
         // the list holds the slices of signature 0 (the interior brick) only (one
         // unrolled body: a second one in the same kernel spilled to scratch)
         constexpr const StencilSig& S = *kStencilSigPtrs[0];
         run([](int j) -> uint32_t { return j < S.nsteps ? S.slot[j] : (uint32_t)(0xC0 | S.dslot); },
-            [](int j) { return ((S.pat >> j) & 1u) != 0; });
+            [](int j) { return ((S.pat >> j) & 1u) != 0; },
+            [](int j) { return j < S.nsteps && kStencilWin<S>.first[j]; });
       }
     }
     else {
@@ -2102,9 +2133,20 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         u1 = u2;
       }
     }
-    flush3(aP, gP);
-    flush3(aQ, gQ);
-    flush3(aR, gR);
+    if constexpr (UMODE == 3) {
+      constexpr const StencilSig& S = *kStencilSigPtrs[0];
+      if (kStencilWin<S>.fin[0]) store3(aP, gP);
+      else flush3(aP, gP);
+      if (kStencilWin<S>.fin[1]) store3(aQ, gQ);
+      else flush3(aQ, gQ);
+      if (kStencilWin<S>.fin[2]) store3(aR, gR);
+      else flush3(aR, gR);
+    }
+    else {
+      flush3(aP, gP);
+      flush3(aQ, gQ);
+      flush3(aR, gR);
+    }
     if (rhs && active) {
       const double rv = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
       rhs[3 * (int64_t)row + ci] = rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv;
