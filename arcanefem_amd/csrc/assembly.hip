@@ -2162,22 +2162,39 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     }
     const int total = __shfl(fp, 63);  // blocks of the slice
     fp -= len;
-    if (active) {
-      acc_lane[192 * dslot] = 0.0;
-      acc_lane[192 * dslot + 64] = 0.0;
-      acc_lane[192 * dslot + 128] = 0.0;
-    }
     double rv[3 * MAXW];
-#pragma unroll
-    for (int t = 0; t < MAXW; ++t)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) rv[3 * t + k] = acc_lane[192 * min(t, W - 1) + 64 * k];
     double sum[3] = { 0.0, 0.0, 0.0 };
+    if constexpr (UMODE == 3) {
+      // the signature's slots at constant offsets; the diagonal slot is skipped
+      // (the other instances add its zeroed accumulator: +0, the same sums)
+      constexpr int WS0 = kStencilSigPtrs[0]->w, DS0 = kStencilSigPtrs[0]->dslot;
 #pragma unroll
-    for (int t = 0; t < MAXW; ++t)
-      if (t < W)
+      for (int t = 0; t < WS0; ++t)
+        if (t != DS0)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) sum[k] += rv[3 * t + k];
+          for (int k = 0; k < 3; ++k) rv[3 * t + k] = acc_lane[192 * t + 64 * k];
+#pragma unroll
+      for (int t = 0; t < WS0; ++t)
+        if (t != DS0)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) sum[k] += rv[3 * t + k];
+    }
+    else {
+      if (active) {
+        acc_lane[192 * dslot] = 0.0;
+        acc_lane[192 * dslot + 64] = 0.0;
+        acc_lane[192 * dslot + 128] = 0.0;
+      }
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rv[3 * t + k] = acc_lane[192 * min(t, W - 1) + 64 * k];
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t)
+        if (t < W)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) sum[k] += rv[3 * t + k];
+    }
     // stencil instance, full slice (64 rows of the signature's length WS): row L's
     // values are flat positions [9 WS L, 9 WS (L + 1)) -- a division by a
     // constant instead of the owner / prefix tables
