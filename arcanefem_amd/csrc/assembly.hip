@@ -1194,7 +1194,7 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
       cN = cross(eP, eR);
       const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
       const double meas = fabs(dot(eP, cP));
-      const double s = -s_coef * recip1(fmax(meas, 1e-300));
+      const double s = -s_coef * recip1(meas);  // no padding steps run here: meas > 0
       const double kP = dot(m, cP) * s;
       const double kQ = -dot(m, cN) * s;
       const double kR = dot(m, cRn) * s;
@@ -2045,7 +2045,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         cN = cross(eP, eR);
         const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
         const double meas = fabs(dot(eP, cP));
-        const double s = -recip1(6.0 * fmax(meas, 1e-300));
+        const double s = -recip1(6.0 * (UMODE == 3 ? meas : fmax(meas, 1e-300)));
         const double mass = c0 * meas * (1.0 / 120.0);
         macc += meas;
         const ElastPre e = elast_pre(m, lambda, mu);
