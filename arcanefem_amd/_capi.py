@@ -165,6 +165,8 @@ SIGNATURES = {
     "afem_elastodynamics_create": [P, P, ctypes.POINTER(NewmarkParams), P, I64, INT, PP],
     "afem_elastodynamics_set_solver_options": [P, ctypes.POINTER(SolverOpts)],
     "afem_elastodynamics_step": [P, ctypes.POINTER(SolveStats)],
+    "afem_elastodynamics_set_dirichlet": [P, P, P, I64, INT],
+    "afem_elastodynamics_set_time_step": [P, D],
     "afem_elastodynamics_state": [P, PP, PP, PP],
     "afem_elastodynamics_destroy": [P],
     "afem_comm_destroy": [P],

@@ -372,7 +372,11 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st);
 void ls_spmv(LinearSystem& ls, const double* x, double* y);
 void ls_build_from_host_coo(LinearSystem& ls);
 void ls_point_update(LinearSystem& ls, int32_t row, int32_t col, double v, bool set);
-void ls_set_list(LinearSystem& ls, const int32_t* ids, int64_t n, int mem, int kind, double value, double penalty);
+// kind 0 penalty, 1 row elimination, 2 row+column elimination of the listed DoFs
+// (owned ones); dvalues (device, one per id; ids in device memory) or the
+// common value
+void ls_set_list(LinearSystem& ls, const int32_t* ids, int64_t n, int mem, int kind, double value, double penalty,
+                 const double* dvalues = nullptr);
 
 void mesh_structured(Ctx& ctx, Mesh& m, int dim, int n, int nz, double jitter, uint64_t seed, int nranks, int rank);
 void mesh_structured_bottom(Mesh& m, std::vector<int32_t>& ids);
@@ -405,18 +409,24 @@ struct Elastodynamics {
   LinearSystem ls, lsm;   // the solve, and the mass operator's SpMV
   DevBuf<double> U, V, A, W, MW;
   DevBuf<int32_t> fixed;  // clamped DoFs
+  DevBuf<int32_t> imp_ids;  // imposed displacements (afem_elastodynamics_set_dirichlet): owned DoFs
+  DevBuf<double> imp_vals;  //   and their values
   int64_t n = 0, n_cols = 0;
   afem_solve_stats last{};
 };
 Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* prm, const int32_t* fixed_nodes,
                            int64_t n_fixed, int mem);
 void dyn_step(Elastodynamics* d, afem_solve_stats* st);
+void dyn_set_dirichlet(Elastodynamics* d, const int32_t* dofs, const double* values, int64_t n, int mem);
+void dyn_set_time_step(Elastodynamics* d, double dt);
 void dyn_destroy(Elastodynamics* d);
 
 void vec_lincomb(Ctx& ctx, int64_t n, double a, const double* x, double b, const double* y, double c, const double* z,
                  double* out);
 void newmark_update(Ctx& ctx, int64_t n, double dt, double beta, double gamma, const double* un, double* u, double* v,
                     double* a);
+// x[ids[i]] = vals[i] (device arrays)
+void vec_scatter(Ctx& ctx, int64_t n, const int32_t* ids, const double* vals, double* x);
 
 void comm_unique_id(uint8_t* out);
 Comm* comm_create(Ctx& ctx, const uint8_t* id, int nranks, int rank);

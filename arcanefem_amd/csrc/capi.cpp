@@ -1115,6 +1115,23 @@ int afem_elastodynamics_step(afem_elastodynamics* h, afem_solve_stats* st)
   API_END
 }
 
+int afem_elastodynamics_set_dirichlet(afem_elastodynamics* h, const int32_t* dofs, const double* values, int64_t n,
+                                      int mem)
+{
+  API_BEGIN
+  NOT_NULL(h);
+  dyn_set_dirichlet(h->d, dofs, values, n, mem);
+  API_END
+}
+
+int afem_elastodynamics_set_time_step(afem_elastodynamics* h, double dt)
+{
+  API_BEGIN
+  NOT_NULL(h);
+  dyn_set_time_step(h->d, dt);
+  API_END
+}
+
 int afem_elastodynamics_state(afem_elastodynamics* h, double** u, double** v, double** a)
 {
   API_BEGIN

@@ -41,7 +41,21 @@ __global__ void k_newmark(int64_t n, double dt, double beta, double gamma, const
   }
 }
 
+__global__ void k_scatter_vals(int64_t n, const int32_t* __restrict__ ids, const double* __restrict__ vals,
+                               double* __restrict__ x)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[ids[i]] = vals[i];
+}
+
 }  // namespace
+
+void vec_scatter(Ctx& ctx, int64_t n, const int32_t* ids, const double* vals, double* x)
+{
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_scatter_vals, dim3(grid_for(n, 256)), dim3(256), 0, ctx.stream, n, ids, vals, x);
+  AFEM_LAUNCHED();
+}
 
 void vec_lincomb(Ctx& ctx, int64_t n, double a, const double* x, double b, const double* y, double c, const double* z,
                  double* out)

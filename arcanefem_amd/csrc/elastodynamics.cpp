@@ -14,6 +14,7 @@
 // device.  Rayleigh damping (etam, etak) and the
 // generalized-alpha variant are not implemented.
 #include <cmath>
+#include <map>
 #include <vector>
 
 #include "afem_internal.hpp"
@@ -189,15 +190,69 @@ void dyn_step(Elastodynamics* d, afem_solve_stats* st)
     vec_lincomb(ctx, d->n, 1.0, d->ls.rhs.p, 1.0, d->MW.p, 0.0, nullptr, d->ls.rhs.p);
     // clamped DoFs by penalty (the reference's default Dirichlet treatment)
     if (d->fixed.n) ls_set_list(d->ls, d->fixed.p, (int64_t)d->fixed.n, AFEM_MEM_DEVICE, 0, 0.0, d->p.penalty);
+    // imposed displacements: diagonal = penalty, rhs = u penalty
+    // (modules/passmo/ElastodynamicModule.cc:1923-1939)
+    if (d->imp_ids.n)
+      ls_set_list(d->ls, d->imp_ids.p, (int64_t)d->imp_ids.n, AFEM_MEM_DEVICE, 0, 0.0, d->p.penalty, d->imp_vals.p);
     // warm start from the Newmark predictor U + dt V + dt^2 (1/2 - beta) A
     // (the PCG's stopping target is unchanged: the zero guess's residual)
     vec_lincomb(ctx, d->n, 1.0, d->U.p, d->p.dt, d->V.p, d->p.dt * d->p.dt * (0.5 - d->beta), d->A.p, d->ls.sol.p);
     d->ls.opts.initial_guess = 1;
     ls_solve(d->ls, &d->last);
+    // the imposed values re-applied to the solution (_doSolve, :2369-2371)
+    if (d->imp_ids.n) vec_scatter(ctx, (int64_t)d->imp_ids.n, d->imp_ids.p, d->imp_vals.p, d->ls.sol.p);
     newmark_update(ctx, d->n, d->p.dt, d->beta, d->gamma, d->ls.sol.p, d->U.p, d->V.p, d->A.p);
     ctx.sync();
     if (st) *st = d->last;
   }
+}
+
+void dyn_set_dirichlet(Elastodynamics* d, const int32_t* dofs, const double* values, int64_t n, int mem)
+{
+  AFEM_REQUIRE(n == 0 || (dofs && values), AFEM_ERR_ARG, "afem_elastodynamics_set_dirichlet: dofs / values is NULL");
+  AFEM_REQUIRE(n >= 0, AFEM_ERR_ARG, "afem_elastodynamics_set_dirichlet: negative count");
+  Ctx& ctx = *d->ctx;
+  ctx.set_device();
+  std::vector<int32_t> hd(n);
+  std::vector<double> hv(n);
+  if (n) {
+    const hipMemcpyKind k = mem == AFEM_MEM_HOST ? hipMemcpyHostToHost : hipMemcpyDeviceToHost;
+    AFEM_HIP(hipMemcpyAsync(hd.data(), dofs, n * sizeof(int32_t), k, ctx.stream));
+    AFEM_HIP(hipMemcpyAsync(hv.data(), values, n * sizeof(double), k, ctx.stream));
+    ctx.sync();
+  }
+  // owned DoFs only (the reference loops over ownNodes(), :1923); the last
+  // value of a DoF listed twice wins, as the module's successive conditions
+  std::map<int32_t, double> m;
+  for (int64_t i = 0; i < n; ++i) {
+    AFEM_REQUIRE(hd[i] >= 0 && hd[i] < d->n_cols, AFEM_ERR_ARG, "imposed DoF id out of range");
+    if (hd[i] < d->n) m[hd[i]] = hv[i];
+  }
+  std::vector<int32_t> ids;
+  std::vector<double> vals;
+  for (const auto& kv : m) {
+    ids.push_back(kv.first);
+    vals.push_back(kv.second);
+  }
+  d->imp_ids.alloc(ids.size());
+  d->imp_vals.alloc(vals.size());
+  if (!ids.empty()) {
+    AFEM_HIP(hipMemcpyAsync(d->imp_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+    AFEM_HIP(hipMemcpyAsync(d->imp_vals.p, vals.data(), vals.size() * 8, hipMemcpyHostToDevice, ctx.stream));
+  }
+  ctx.sync();
+}
+
+void dyn_set_time_step(Elastodynamics* d, double dt)
+{
+  AFEM_REQUIRE(dt > 0, AFEM_ERR_ARG, "afem_elastodynamics_set_time_step: dt must be > 0");
+  if (dt == d->p.dt) return;
+  d->p.dt = dt;
+  d->c0 = d->p.rho / (d->beta * dt * dt);
+  d->c3 = d->p.rho / d->beta / dt;
+  // c4 does not depend on dt; the operator c0 M + K does: a reused multigrid
+  // hierarchy is rebuilt at the next solve
+  d->ls.mg.reset();
 }
 
 void dyn_destroy(Elastodynamics* d)

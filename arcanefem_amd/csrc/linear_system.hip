@@ -23,14 +23,17 @@ constexpr uint8_t kElimRow = 1, kElimRowCol = 2;
 // ---------------------------------------------------------------- BC kernels
 // kind 0: penalty  (femutils/ArcaneFemFunctionsGpu.h:434-456)
 // kind 1: row elimination, kind 2: row+column elimination (:461-482)
-__global__ void k_set_list(int64_t n, const int32_t* __restrict__ ids, int kind, double value, double penalty,
-                           int64_t n_rows, uint8_t* __restrict__ forced_info, double* __restrict__ forced_value,
+// values (may be null): one value per listed DoF instead of the common `value`
+__global__ void k_set_list(int64_t n, const int32_t* __restrict__ ids, int kind, double value,
+                           const double* __restrict__ values, double penalty, int64_t n_rows,
+                           uint8_t* __restrict__ forced_info, double* __restrict__ forced_value,
                            uint8_t* __restrict__ elim_info, double* __restrict__ elim_value, double* __restrict__ rhs)
 {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   int32_t d = ids[t];
   if (d < 0 || d >= n_rows) return;  // isOwn() filter
+  if (values) value = values[t];
   if (kind == 0) {
     forced_info[d] = 1;
     forced_value[d] = penalty;
@@ -1403,7 +1406,8 @@ void require_csr(LinearSystem& ls)
 
 }  // namespace
 
-void ls_set_list(LinearSystem& ls, const int32_t* ids, int64_t n, int mem, int kind, double value, double penalty)
+void ls_set_list(LinearSystem& ls, const int32_t* ids, int64_t n, int mem, int kind, double value, double penalty,
+                 const double* dvalues)
 {
   Ctx& ctx = *ls.ctx;
   if (n <= 0) return;
@@ -1414,8 +1418,9 @@ void ls_set_list(LinearSystem& ls, const int32_t* ids, int64_t n, int mem, int k
     AFEM_HIP(hipMemcpyAsync(tmp.p, ids, tmp.bytes(), hipMemcpyHostToDevice, ctx.stream));
     dids = tmp.p;
   }
+  AFEM_REQUIRE(!dvalues || mem == AFEM_MEM_DEVICE, AFEM_ERR_ARG, "ls_set_list: per-DoF values need device ids");
   hipLaunchKernelGGL(k_set_list, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, ctx.stream, n, dids, kind, value,
-                     penalty, ls.n_rows, ls.forced_info.p, ls.forced_value.p, ls.elim_info.p, ls.elim_value.p,
+                     dvalues, penalty, ls.n_rows, ls.forced_info.p, ls.forced_value.p, ls.elim_info.p, ls.elim_value.p,
                      ls.rhs.p);
   AFEM_LAUNCHED();
   if (tmp.p) ctx.sync();

@@ -45,6 +45,15 @@ def newmark_coefficients(rho: float, dt: float):
     return gamma, beta, c0, c3, c4
 
 
+def young_from_lame(lam: float, mu: float):
+    """(E, nu) of Lame parameters the way passmo converts its "lame" input
+    (modules/passmo/ElastodynamicModule.cc:270-277): x = lambda/mu,
+    nu = x/2/(1+x), E = 2 mu (1+nu)."""
+    x = lam / mu
+    nu = x / 2.0 / (1.0 + x)
+    return 2.0 * mu * (1.0 + nu), nu
+
+
 class Elastodynamics3D:
     def __init__(self, ctx: Context, mesh: Mesh, E: float, nu: float, rho: float, dt: float,
                  body_force=(0.0, 0.0, 0.0), fixed_nodes=None, penalty: float = 1.0e30, rtol: float = 1e-12,
@@ -76,6 +85,21 @@ class Elastodynamics3D:
         self.last_stats = dict(iterations=st.iterations, converged=bool(st.converged), rel_residual=st.rel_residual,
                                residual_norm=st.residual_norm, solve_ms=st.solve_ms)
         return self.last_stats
+
+    def setDirichlet(self, dofs, values):
+        """Imposed displacements by penalty (passmo's dirichlet-surface /
+        point conditions, modules/passmo/ElastodynamicModule.cc:1923-1939 and
+        the re-application after the solve :2369-2371): local DoF ids
+        (3 node + component) and their values; replaces the previous list."""
+        d = np.ascontiguousarray(dofs, dtype=np.int32).ravel()
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(values, dtype=np.float64), d.shape))
+        call("afem_elastodynamics_set_dirichlet", self.h, ctypes.c_void_p(d.ctypes.data) if d.size else None,
+             ctypes.c_void_p(v.ctypes.data) if v.size else None, d.size, C.AFEM_MEM_HOST)
+
+    def setTimeStep(self, dt: float):
+        """dt from the next step on (passmo's shortened final step, :525-530)."""
+        call("afem_elastodynamics_set_time_step", self.h, float(dt))
+        self.dt = float(dt)
 
     def state_dptrs(self):
         u, v, a = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()

@@ -49,16 +49,21 @@ ELAST3_KERNELS = {4: "k_assemble_elast_strip", 5: "k_assemble_elast_tet", 6: "k_
                   8: "k_assemble_elast_wg", 9: "k_assemble_elast_strip<..,BIG>"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU).  Under torch.distributed.run WORLD_SIZE decides; without a launcher "
+                         "bench.py spawns the N rank processes itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=215, help="cells per unit length (C2: 215 -> 10.08M DoF per GPU)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: an n x n x n box per GPU stacked in z (C2 per GPU; n = 231 is BASELINE.md's C4 weak "
+                         "size); strong: ONE n x n x n box cut into N z-slabs (C4, n = 463)")
+    ap.add_argument("--n", type=int, default=None,
+                    help="cells per unit length (default: weak 215 -> 10.08M DoF per GPU, strong 463 -> 99.9M DoF)")
     ap.add_argument("--cg-iters", type=int, default=100)
-    ap.add_argument("--cpu-baseline-n", type=int, default=60)
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true",
+                    help="skip the CPU baselines (the oracle timed at the C2 size on the host cores, N = 1 only)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_assembly_C2.json"))
     ap.add_argument("--no-extras", action="store_true", help="skip the C3 / C4 / C5 side measurements")
     ap.add_argument("--c3-n", type=int, default=170, help="C3 block-3 elasticity box (170 -> 5.0M nodes)")
@@ -70,7 +75,54 @@ def parse():
                     help="N > 1: the CG's transport (host: gloo callbacks, for rehearsing several ranks on one GPU)")
     ap.add_argument("--unstructured-levels", type=int, default=6,
                     help="refinements of L-shape-3D.msh for the unstructured leg (6 -> 12 M DoF); 0: skip")
-    return ap.parse_args()
+    args = ap.parse_args(argv)
+    if args.n is None:
+        args.n = 215 if args.scaling == "weak" else 463
+    return args
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(nranks):
+    """`--gpus N` without a launcher: start the N rank processes the way
+    torch.distributed.run would (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*;
+    the same command line), wait for them, exit with the first failure.  This
+    process touches no GPU API (the ranks do).  A rank that fails ends the
+    others (they would wait in the rendezvous or a barrier forever)."""
+    import subprocess
+
+    port = str(_free_port())
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks), LOCAL_WORLD_SIZE=str(nranks),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    code, t_fail = 0, None
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and code == 0:
+                code = rc if rc > 0 else 1
+                t_fail = time.time()
+                for q in live:  # the PIDs this launcher started, nothing else
+                    q.terminate()
+        if t_fail is not None and time.time() - t_fail > 20:
+            for q in live:
+                q.kill()
+        time.sleep(0.05)
+    return code
 
 
 def algorithmic_bytes(n_inc, n_local, n_own, nnz):
@@ -331,10 +383,12 @@ def elastodynamics_c5(ctx, af, n, steps, preconditioners=("multigrid", "jacobi")
         dyn.step()
         ctx.synchronize()
         first_ms = (time.perf_counter() - t0) * 1e3
-        iters = []
+        iters, conv = [], []
         t0 = time.perf_counter()
         for _ in range(steps):
-            iters.append(int(dyn.step()["iterations"]))
+            st = dyn.step()
+            iters.append(int(st["iterations"]))
+            conv.append(bool(st["converged"]))
         ctx.synchronize()
         dt = (time.perf_counter() - t0) / steps
         key = "" if pc == preconditioners[0] else f"{pc}_"
@@ -342,58 +396,89 @@ def elastodynamics_c5(ctx, af, n, steps, preconditioners=("multigrid", "jacobi")
         out[f"{key}steps_per_s"] = round(1.0 / dt, 2)
         out[f"{key}ms_per_step"] = round(dt * 1e3, 2)
         out[f"{key}cg_iterations_per_step"] = float(np.mean(iters))
+        out[f"{key}iterations"] = iters
+        out[f"{key}converged"] = conv
         out[f"{key}first_step_ms"] = round(first_ms, 1)
         dyn.close()
     mesh.close()
     return out
 
 
-def _threads():
-    return min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1))
+def host_cores():
+    """(threads the CPU baseline uses, cores this process may run on, nproc):
+    every core of the affinity mask, capped by OMP_NUM_THREADS when the lease
+    sets it (16 per GPU on the MI355X boxes)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    lim = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(aff, lim) if lim > 0 else aff), aff, nproc
 
 
-def cpu_baseline(n, seconds):
-    """The oracle (C restatement of the reference's cell-loop assembly with
-    linear column search, femutils/BSRFormat.h:807-836, + RHS + penalty) on
-    this host over a bounded sample: single-threaded, and on all the host
-    threads this job may use (OpenMP, atomic adds: the reference's multi-core
-    cell loop).  `value` is the multi-core rate."""
+def download_c2(ctx, mesh, bsr, ls, bottom):
+    """The headline's input and output, copied to the host for the CPU
+    baseline: cells, coordinates, structure (bit-equal to the oracle's own
+    sparsity, tests/test_gpu_parity.py) and the GPU's assembled values / RHS
+    (compared with the oracle's below, a parity check at the C2 size)."""
+    cells, coords, _ = mesh.download()
+    rp, cols, vals = bsr.download()
+    return dict(cells=cells, coords=coords, n_own=mesh.n_own_nodes, rp=rp, cols=cols, gpu_vals=vals,
+                gpu_rhs=ls.rhs_host(), dirichlet=bottom)
+
+
+def cpu_baseline(c2, runs=5):
+    """the oracle (C restatement of the reference's cell
+    loop with linear column search, femutils/BSRFormat.h:807-836, + RHS +
+    penalty) at the headline's C2 size on this host: one single-threaded
+    assembly, then the median of `runs` on every core this job may use
+    (OpenMP, atomic adds: the reference's multi-core loop) after one warm-up.
+    `value` is the multi-core rate.  The oracle's values are also compared with
+    the GPU's (max relative difference in `sample`)."""
     from oracle import oracle as O
 
-    m = O.structured_mesh(3, n)
-    cells, coords, n_own = m["cells"], m["coords"], m["n_own"]
-    rp, cols = O.sparsity(m["n_local"], n_own, cells)
+    cells, coords, n_own, rp, cols = c2["cells"], c2["coords"], c2["n_own"], c2["rp"], c2["cols"]
 
-    def run(fn, budget):
-        reps, t = 0, 0.0
-        while t < budget and reps < 1000:
-            t0 = time.perf_counter()
-            vals, rhs = fn(n_own, cells, coords, rp, cols, 5.5)
-            O.dirichlet_penalty(m["dirichlet"], 0.5, 1e30, rp, cols, vals, rhs)
-            t += time.perf_counter() - t0
-            reps += 1
-        return reps, t
+    def one(fn):
+        t0 = time.perf_counter()
+        vals, rhs = fn(n_own, cells, coords, rp, cols, 5.5)
+        O.dirichlet_penalty(c2["dirichlet"], 0.5, 1e30, rp, cols, vals, rhs)
+        return time.perf_counter() - t0, vals, rhs
 
-    r1, t1 = run(O.assemble_poisson, 0.4 * seconds)
-    threads = O.omp_threads(_threads())
-    O.assemble_poisson_omp(n_own, cells, coords, rp, cols, 5.5)  # thread pool warm-up
-    rm, tm = run(O.assemble_poisson_omp, 0.6 * seconds)
-    return {"value": n_own * rm / tm / 1e6, "unit": "MDoF/s", "cores": threads, "kind": "port",
-            "sample": f"Poisson-3D P1 Kuhn box n={n} ({n_own} DoF, {cells.shape[0]} tets): {rm} assemblies in "
-                      f"{tm:.1f} s on {threads} OpenMP threads (oracle/oracle.c cell loop, atomic adds, gcc -O2); "
-                      f"single thread {n_own * r1 / t1 / 1e6:.2f} MDoF/s ({r1} assemblies in {t1:.1f} s)"}
+    t1, _, _ = one(O.assemble_poisson)
+    cores, aff, nproc = host_cores()
+    threads = O.omp_threads(cores)
+    one(O.assemble_poisson_omp)  # thread-pool warm-up
+    ts = []
+    for _ in range(runs):
+        t, vals, rhs = one(O.assemble_poisson_omp)
+        ts.append(t)
+    tm = float(np.median(ts))
+    scale = np.abs(vals).max()
+    dv = float(np.abs(vals - c2["gpu_vals"]).max() / scale)
+    free = np.abs(vals) < 1e20  # the penalty diagonal is set, not summed
+    dvf = float(np.abs(vals[free] - c2["gpu_vals"][free]).max() / np.abs(vals[free]).max())
+    drhs = float(np.abs(rhs - c2["gpu_rhs"]).max() / np.abs(rhs).max())
+    c2["orc_vals"], c2["orc_rhs"] = vals, rhs
+    return {"value": round(n_own / tm / 1e6, 2), "unit": "MDoF/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "affinity_cores": aff,
+            "sample": f"C2 itself: Poisson-3D P1 Kuhn box ({n_own} DoF, {cells.shape[0]} tets, {cols.size} nnz), "
+                      f"structure from the GPU run: median of {runs} assemblies {tm * 1e3:.0f} ms on {threads} "
+                      f"OpenMP threads (oracle/oracle.c cell loop, atomic adds; nproc {nproc}, {aff} cores in the "
+                      f"affinity mask, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}); single thread "
+                      f"{t1 * 1e3:.0f} ms = {n_own / t1 / 1e6:.2f} MDoF/s; oracle vs GPU values max rel diff "
+                      f"{dvf:.1e} (free rows; {dv:.1e} overall), RHS {drhs:.1e}"}
 
 
-def cpu_baseline_cg(n, iters=50, runs=5):
-    """the oracle's Jacobi-PCG with OpenMP on the same CSR
-    kind, exactly `iters` iterations, median of `runs` after one warm-up."""
+def cpu_baseline_cg(c2, iters=50, runs=3):
+    """the oracle's Jacobi-PCG with OpenMP on the C2 CSR
+    the CPU baseline assembled, exactly `iters` iterations, median of `runs`
+    after one warm-up."""
     from oracle import oracle as O
 
-    m = O.structured_mesh(3, n)
-    rp, cols = O.sparsity(m["n_local"], m["n_own"], m["cells"])
-    vals, rhs = O.assemble_poisson(m["n_own"], m["cells"], m["coords"], rp, cols, 5.5)
-    O.dirichlet_penalty(m["dirichlet"], 0.5, 1e30, rp, cols, vals, rhs)
-    threads = O.omp_threads(_threads())
+    rp, cols, vals, rhs = c2["rp"], c2["cols"], c2["orc_vals"], c2["orc_rhs"]
+    threads = O.omp_threads(host_cores()[0])
     O.pcg_jacobi_omp(rp, cols, vals, rhs, max_iter=-iters)
     ts = []
     for _ in range(runs):
@@ -402,9 +487,9 @@ def cpu_baseline_cg(n, iters=50, runs=5):
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
     return {"value": round(iters / t, 2), "unit": "iter/s", "cores": threads, "kind": "port",
-            "sample": f"Jacobi-PCG (oracle/oracle.c orc_pcg_jacobi_omp) on the Poisson-3D Kuhn box n={n} "
-                      f"({m['n_own']} DoF, {int(rp[-1])} nnz): {iters} fixed iterations, median of {runs} runs "
-                      f"{t * 1e3:.1f} ms on {threads} OpenMP threads"}
+            "sample": f"Jacobi-PCG (oracle/oracle.c orc_pcg_jacobi_omp) on the C2 system ({rp.size - 1} DoF, "
+                      f"{int(rp[-1])} nnz): {iters} fixed iterations, median of {runs} runs {t * 1e3:.1f} ms on "
+                      f"{threads} OpenMP threads"}
 
 
 def cpu_baseline_c1(runs=3):
@@ -440,23 +525,31 @@ def cpu_baseline_c1(runs=3):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("gloo")
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
 
     import arcanefem_amd as af
 
     ndev = af.device_count()
     if ndev < 1:
         raise SystemExit("bench.py needs a GPU (libafem.so has no CPU path)")
+    if world > 1 and args.comm == "rccl" and ndev < world:
+        # RCCL runs one rank per device; --comm host rehearses several ranks on one GPU
+        raise SystemExit(f"bench.py: {world} ranks over RCCL need {world} GPUs, this host shows {ndev} "
+                         f"(use --comm host to run them on one GPU over the host transport)")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
     ctx = af.Context(local_rank % ndev)
     n = args.n
-    nz = n * world
+    nz = n * world if args.scaling == "weak" else n
     t_setup = time.perf_counter()
     mesh, bsr, ls, bottom, dbottom, sparsity_ms = poisson_setup(ctx, af, n, nz, world, rank)
     nnz = bsr.view().nnz_blocks
@@ -533,7 +626,10 @@ def main():
             if tag:
                 rf["traffic_profile"] = tag
         extras = {}
+        c2 = None
         if world == 1:
+            if not args.no_cpu_baseline:
+                c2 = download_c2(ctx, mesh, bsr, ls, bottom)
             # free the headline's buffers before the large side legs
             ctx.free(dbottom)
             ls.reset()
@@ -541,17 +637,26 @@ def main():
             mesh.close()
             dbottom = None
         if not args.no_extras and world == 1:
-            if args.c4_n > 0:
+            if args.c4_n > 0 and not (args.scaling == "strong" and n == args.c4_n):
                 extras["c4"] = poisson_c4(ctx, af, args.c4_n)
             extras["c3"] = elasticity_c3(ctx, af, args.c3_n)
             if args.unstructured_levels > 0:
                 extras["unstructured"] = unstructured_leg(ctx, af, "L-shape-3D.msh", args.unstructured_levels)
             extras["c5"] = elastodynamics_c5(ctx, af, args.c5_n, args.c5_steps)
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args.cpu_baseline_n, args.cpu_baseline_seconds)
-            extras["cpu_baseline_cg"] = cpu_baseline_cg(args.cpu_baseline_n)
+        if c2 is not None:
+            cpu = cpu_baseline(c2)
+            extras["cpu_baseline_cg"] = cpu_baseline_cg(c2)
             extras["cpu_baseline_c1"] = cpu_baseline_c1()
+            del c2
+        if args.scaling == "weak":
+            workload = (f"C2 Poisson-3D P1, jittered Kuhn-tet box n={n} per GPU stacked in z "
+                        f"({n_own} DoF, {n_cells} tets on rank 0), CSR assembly (matrix+RHS+penalty Dirichlet z=0) "
+                        f"on fixed sparsity; CG = Jacobi-PCG on it")
+        else:
+            workload = (f"C4 Poisson-3D P1, ONE jittered Kuhn-tet box n={n} ({int(total_dof)} DoF) cut into "
+                        f"{world} z-slab(s) ({n_own} DoF, {n_cells} tets on rank 0), CSR assembly "
+                        f"(matrix+RHS+penalty Dirichlet z=0) on fixed sparsity; CG = Jacobi-PCG on it")
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -561,17 +666,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": (f"C2 Poisson-3D P1, jittered Kuhn-tet box n={n} per GPU "
-                             f"({n_own} DoF, {n_cells} tets per GPU), CSR assembly "
-                             f"(matrix+RHS+penalty Dirichlet z=0) on fixed sparsity; CG = Jacobi-PCG on it"),
+                "workload": workload,
                 "n": n,
-                "dof_per_gpu": int(n_own),
-                "nnz_per_gpu": int(nnz),
+                "scaling": args.scaling,
+                "dof_total": int(total_dof),
+                "dof_rank0": int(n_own),
+                "nnz_rank0": int(nnz),
                 "parallelism": f"z-slab x{world}, {'RCCL' if args.comm == 'rccl' else 'host-transport'} halo + all-reduce in CG",
             },
             "roofline": rf,

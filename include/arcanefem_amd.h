@@ -399,6 +399,20 @@ int afem_elastodynamics_create(afem_mesh* mesh, afem_comm* comm, const afem_newm
                                const int32_t* fixed_nodes, int64_t n_fixed, int mem, afem_elastodynamics** out);
 int afem_elastodynamics_set_solver_options(afem_elastodynamics* dyn, const afem_solver_opts* opts);
 int afem_elastodynamics_step(afem_elastodynamics* dyn, afem_solve_stats* stats);
+/* Imposed displacements by penalty (passmo's dirichlet-surface-condition /
+ * dirichlet-point-condition with enforce-Dirichlet-method Penalty,
+ * modules/passmo/ElastodynamicModule.cc:1923-1939): each listed DoF (local id
+ * 3*node + component; non-owned ones ignored) gets diagonal = penalty and
+ * rhs = value * penalty at every step, and its value is re-applied to the
+ * solution before the Newmark update (_doSolve, :2369-2371).  Replaces the
+ * previous list (n = 0 clears it); the fixed nodes of afem_elastodynamics_create
+ * stay clamped. */
+int afem_elastodynamics_set_dirichlet(afem_elastodynamics* dyn, const int32_t* dofs, const double* values, int64_t n,
+                                      int mem);
+/* Changes dt from the next step on (passmo shortens the step that would
+ * overshoot the final time, modules/passmo/ElastodynamicModule.cc:525-530);
+ * the Newmark coefficients follow and a reused multigrid hierarchy is rebuilt. */
+int afem_elastodynamics_set_time_step(afem_elastodynamics* dyn, double dt);
 /* device arrays of 3*n_own_nodes doubles (DoF lid = 3 node + i) */
 int afem_elastodynamics_state(afem_elastodynamics* dyn, double** u, double** v, double** a);
 int afem_elastodynamics_destroy(afem_elastodynamics* dyn);

@@ -486,6 +486,124 @@ def newmark_elastodynamics(n_nodes, cells, coords, E, nu, rho, dt, n_steps, body
 
 
 # --------------------------------------------------------------------------
+# passmo: the reference's 3D elastodynamics (modules/passmo), P1 tetrahedra
+# --------------------------------------------------------------------------
+# 4-point Gauss rule of order 2 on the reference tetrahedron
+# (femutils/GaussQuadrature.h:202, 209-241; ArcaneFemFunctions.h:2359-2396,
+# 2503-2508, 2583-2587): points (a2,a2,a2), (a2,a2,b2), (a2,b2,a2), (b2,a2,a2)
+# in (x,y,z) = xtet/ytet/ztet[1][rank], weight 1/24 each.
+_PM_A2 = (5.0 - np.sqrt(5.0)) / 20.0
+_PM_B2 = (5.0 + 3.0 * np.sqrt(5.0)) / 20.0
+_PM_GAUSS = [(_PM_A2, _PM_A2, _PM_A2), (_PM_A2, _PM_A2, _PM_B2), (_PM_A2, _PM_B2, _PM_A2), (_PM_B2, _PM_A2, _PM_A2)]
+_PM_WEIGHT = 1.0 / 24.0
+# Tetra4 reference shape functions (ArcaneFemFunctions.h:1973-2004)
+_PM_DPHI = np.array([[-1.0, -1.0, -1.0], [1.0, 0.0, 0.0], [0.0, 1.0, 0.0], [0.0, 0.0, 1.0]])
+
+
+def _pm_phi(r):
+    x, y, z = r
+    return np.array([1.0 - x - y - z, x, y, z])
+
+
+def passmo_element_tet4(xyz, lam, mu, rho):
+    """Per-Gauss-point element stiffness and mass of a P1 tetrahedron exactly
+    as modules/passmo/ElastodynamicModule.cc computes them: Jacobian matrix
+    jac[i][j] = sum_n dPhi_n[i] x_n[j] and its determinant (_initGaussStep,
+    :414-465), B = jac^-1 dPhi (_computeK :1450-1478), Voigt B_ii / B_jj rows
+    and kij = wt (B_ii^T D B_jj), D = [[a,l,l],[l,a,l],[l,l,a]] + mu on the
+    shear terms, wt = w_g det (:1483-1573); Me(ii,jj) = wt rho Phi_i Phi_j on
+    equal components (_computeElemMass :1390-1420).  Returns the two lists of
+    the 4 Gauss points' 12x12 matrices (DoF 3 node + component)."""
+    X = np.asarray(xyz, dtype=np.float64).reshape(4, 3)
+    jac = _PM_DPHI.T @ X  # jac[i][j] = sum_n dPhi_n[i] * x_n[j]
+    det = np.linalg.det(jac)
+    ijac = np.linalg.inv(jac)
+    a = lam + 2.0 * mu
+    Ks, Ms = [], []
+    for g in _PM_GAUSS:
+        wt = _PM_WEIGHT * det
+        B = ijac @ _PM_DPHI.T  # [3, 4]: B(i, inod) = sum_j ijac[i][j] dPhi_inod[j]
+        V = np.zeros((12, 6))  # Voigt row of DoF 3 inod + l: (xx, yy, zz, xy, xz, yz)
+        for n in range(4):
+            bx, by, bz = B[:, n]
+            V[3 * n + 0] = (bx, 0.0, 0.0, by, bz, 0.0)
+            V[3 * n + 1] = (0.0, by, 0.0, bx, 0.0, bz)
+            V[3 * n + 2] = (0.0, 0.0, bz, 0.0, bx, by)
+        D = np.array([[a, lam, lam, 0, 0, 0], [lam, a, lam, 0, 0, 0], [lam, lam, a, 0, 0, 0],
+                      [0, 0, 0, mu, 0, 0], [0, 0, 0, 0, mu, 0], [0, 0, 0, 0, 0, mu]], dtype=np.float64)
+        Ks.append(wt * (V @ D @ V.T))
+        phi = _pm_phi(g)
+        M = np.zeros((12, 12))
+        for i in range(4):
+            for j in range(4):
+                for comp in range(3):
+                    M[3 * i + comp, 3 * j + comp] = wt * rho * phi[i] * phi[j]
+        Ms.append(M)
+    return Ks, Ms
+
+
+def passmo_time_steps(start, final, dt):
+    """The time steps modules/passmo/ElastodynamicModule.cc::compute (:469-536)
+    takes: Arcane advances globalTime by deltat before each compute; a step
+    whose t + dt overshoots the final time shortens the NEXT step to
+    final - t (:525-530); the step that reaches t >= final checks the result
+    file and stops the loop.  Returns the list of dt of the executed steps."""
+    t, dts = start, []
+    while True:
+        t = t + dt
+        dts.append(dt)
+        if t < final:
+            if t + dt > final:
+                dt = final - t
+        else:
+            return dts
+
+
+def passmo_newmark(cells, coords, lam, mu, rho, dts, imposed, penalty=1.0e64, beta=0.25, gamma=0.5):
+    """CPU restatement of the passmo 3D Newmark loop (P1 tetrahedra, Penalty
+    Dirichlet, no gravity / traction / paraxial terms, alfam = alfaf = 0):
+    per step the LHS sum over the cell's Gauss points of cm Me + Ke with
+    cm = 1/beta/dt^2 (_assembleLinearLHS :1709-1793, matrixAddValue of every
+    (node1 own, node2) pair); the RHS of non-imposed DoFs sum_g Me(ii,jj)
+    cm u_pred_j with u_pred = d + dt v + dt^2 (1/2 - beta) a (:1799-1915);
+    imposed DoFs matrixSetValue(diag, penalty) (Aleph: the set overrides the
+    adds) and rhs = u penalty (:1923-1939); a direct solve (the reference's
+    solver converges to ~1e-9 on the golden); the imposed displacements
+    re-applied after the solve (_doSolve :2343-2371); the Newmark update
+    a = (d1 - u_pred)/beta/dt^2, v = v + dt (1-gamma) a_n + dt gamma a
+    (_updateNewmark :555-591).  `imposed`: dict DoF -> value (DoF = 3 node +
+    component).  Returns U, V, A after the steps."""
+    cells = np.asarray(cells)
+    coords = np.asarray(coords, dtype=np.float64).reshape(-1, 3)
+    n = 3 * coords.shape[0]
+    elems = [passmo_element_tet4(coords[c], lam, mu, rho) for c in cells]
+    dofs = [(3 * np.asarray(c)[:, None] + np.arange(3)[None, :]).ravel() for c in cells]
+    imp = np.array(sorted(imposed), dtype=np.int64)
+    val = np.array([imposed[d] for d in imp], dtype=np.float64)
+    U, V, A = np.zeros(n), np.zeros(n), np.zeros(n)
+    free = np.ones(n, dtype=bool)
+    free[imp] = False
+    for dt in dts:
+        dt2 = dt * dt
+        cm = 1.0 / beta / dt2
+        L = np.zeros((n, n))
+        b = np.zeros(n)
+        upred = U + dt * V + dt2 * (0.5 - beta) * A
+        for d, (Ks, Ms) in zip(dofs, elems):
+            for Ke, Me in zip(Ks, Ms):
+                L[np.ix_(d, d)] += cm * Me + Ke
+                b[d] += np.where(free[d], Me @ (cm * upred[d]), 0.0)
+        L[imp, imp] = penalty
+        b[imp] = val * penalty
+        d1 = np.linalg.solve(L, b)
+        d1[imp] = val
+        an = (d1 - upred) / beta / dt2
+        V = V + dt * (1.0 - gamma) * A + dt * gamma * an
+        A, U = an, d1
+    return U, V, A
+
+
+# --------------------------------------------------------------------------
 # extended-precision reference of the P1 Laplacian values (test infrastructure)
 # --------------------------------------------------------------------------
 def assemble_poisson_extended(n_rows, cells, coords, row_ptr, cols):

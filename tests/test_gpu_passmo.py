@@ -1,0 +1,70 @@
+"""GPU: the reference's passmo 3D elastodynamics golden through the product
+path (afem_elastodynamics_* over the C ABI: block-3 re-assembly of c0 M + K
+every step by the strip kernels on an array-fed Gmsh mesh, imposed
+displacements by penalty 1e64, PCG, Newmark update on the device).
+
+Case modules/passmo/inputs/bar3d_tetra.arc (tests/test_oracle_passmo.py has
+the parameters and the CPU replay): 25 steps of dt 0.08 (the last shortened to
+land on t = 2, afem_elastodynamics_set_time_step), surfaceleft clamped,
+surfaceright Ux = 1.  Gates: the golden modules/passmo/tests/bar3d-tetra.txt at
+the module's epsilon 1e-4 (measured restatement error 1-2e-9), and the CPU
+oracle's replay (passmo's own Gauss-point element, direct solves) to 1e-9.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+import test_oracle_passmo as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def bar():
+    from arcanefem_amd.gmsh import read_gmsh
+
+    return read_gmsh(os.path.join(T.GOLDEN, T.BAR3D["mesh"]))
+
+
+def _replay_gpu(ctx, bar, preconditioner):
+    import arcanefem_amd as af
+    from arcanefem_amd.elastodynamics import Elastodynamics3D, young_from_lame
+
+    p = T.BAR3D
+    mesh = af.Mesh.from_arrays(ctx, 3, bar.cells, bar.coords)
+    E, nu = young_from_lame(p["lam"], p["mu"])
+    dts = O.passmo_time_steps(p["start"], p["final"], p["dt"])
+    dyn = Elastodynamics3D(ctx, mesh, E, nu, p["rho"], dts[0], penalty=p["penalty"], rtol=1e-14,
+                           preconditioner=preconditioner)
+    imp = T.bar3d_imposed(bar)
+    dyn.setDirichlet(np.array(sorted(imp), dtype=np.int32), np.array([imp[d] for d in sorted(imp)]))
+    iters = []
+    for dt in dts:
+        if dt != dyn.dt:
+            dyn.setTimeStep(dt)
+        st = dyn.step()
+        assert st["converged"], st
+        iters.append(st["iterations"])
+    U, V, A = dyn.state_host()
+    dyn.close()
+    mesh.close()
+    return U, V, A, iters
+
+
+@pytest.mark.parametrize("preconditioner", ["jacobi", "block3"])
+def test_bar3d_golden_gpu(ctx, bar, preconditioner):
+    U, V, A, iters = _replay_gpu(ctx, bar, preconditioner)
+    nerr, mx = T.check_golden(bar, U)
+    assert nerr == 0
+    assert mx < 5e-9, mx
+    dts = O.passmo_time_steps(T.BAR3D["start"], T.BAR3D["final"], T.BAR3D["dt"])
+    Uo, Vo, Ao = O.passmo_newmark(bar.cells, bar.coords, T.BAR3D["lam"], T.BAR3D["mu"], T.BAR3D["rho"], dts,
+                                  T.bar3d_imposed(bar), T.BAR3D["penalty"])
+    for gpu, orc in ((U, Uo), (V, Vo), (A, Ao)):
+        assert np.abs(gpu - orc).max() <= 1e-9 * np.abs(orc).max(), np.abs(gpu - orc).max() / np.abs(orc).max()
+    imp = T.bar3d_imposed(bar)
+    ids = np.array(sorted(imp))
+    assert np.array_equal(U[ids], np.array([imp[d] for d in ids]))  # re-applied exactly
