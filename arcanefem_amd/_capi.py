@@ -50,6 +50,15 @@ class CsrView(ctypes.Structure):
                 ("columns", ctypes.c_void_p), ("values", ctypes.c_void_p)]
 
 
+class AssemblyView(ctypes.Structure):
+    """afem_assembly_view (device pointers of a structure for generic element-functor assembly)."""
+    _fields_ = [("n_rows", ctypes.c_int64), ("n_nodes", ctypes.c_int64), ("n_cells", ctypes.c_int64),
+                ("nb_node_per_cell", ctypes.c_int32), ("block_size", ctypes.c_int32),
+                ("ordered_per_block", ctypes.c_int32), ("dim", ctypes.c_int32), ("cell_node", ctypes.c_void_p),
+                ("coords", ctypes.c_void_p), ("rows", ctypes.c_void_p), ("columns", ctypes.c_void_p),
+                ("values", ctypes.c_void_p), ("error_flag", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
+
+
 class BsrStats(ctypes.Structure):
     _fields_ = [("n_incidences", ctypes.c_int64), ("inc_table_entries", ctypes.c_int64),
                 ("max_row_len", ctypes.c_int32), ("rows_per_block", ctypes.c_int32), ("max_seg", ctypes.c_int64),
@@ -131,6 +140,7 @@ SIGNATURES = {
     "afem_bsr_get_value": [P, I32, I32, ctypes.POINTER(D)],
     "afem_bsr_view": [P, ctypes.POINTER(CsrView)],
     "afem_bsr_get_stats": [P, ctypes.POINTER(BsrStats)],
+    "afem_bsr_assembly_view": [P, ctypes.POINTER(AssemblyView)],
     "afem_bsr_get_sizes": [P, ctypes.POINTER(I64), ctypes.POINTER(I64)],
     "afem_bsr_export_csr32": [P, P, P, P, P],
     "afem_bsr_download": [P, P, P, P],
@@ -169,6 +179,7 @@ SIGNATURES = {
     "afem_elastodynamics_set_time_step": [P, D],
     "afem_elastodynamics_state": [P, PP, PP, PP],
     "afem_elastodynamics_destroy": [P],
+    "afem_comm_host_async": [P, INT],
     "afem_comm_destroy": [P],
     "afem_comm_allreduce_sum": [P, P, I64],
     "afem_ls_set_halo": [P, P, INT, P, P, P, P, P],

@@ -369,6 +369,10 @@ class DoFLinearSystem:
         rnc = None if rows_nb_column is None else np.ascontiguousarray(rows_nb_column, dtype=np.int32)
         call("afem_ls_set_csr_values", self.impl, _ptr(rows), None if rnc is None else _ptr(rnc), _ptr(columns),
              _ptr(values), rows.shape[0], columns.shape[0], C.AFEM_MEM_HOST)
+        # the view stays the matrix until solve (libafem re-reads the values
+        # then): keep the arrays alive; a float64 contiguous `values` is the
+        # caller's own array, so its later edits are seen
+        self._host_view = (rows, rnc, columns, values)
 
     def hasSetCSRValues(self) -> bool:
         self._check_init()
@@ -479,6 +483,24 @@ class DoFLinearSystem:
     def clearValues(self):
         self._check_init()
         call("afem_ls_clear_values", self.impl)
+        self._host_view = None
+
+    def set_halo(self, comm, neighbors, send_ids, recv_ids):
+        """afem_ls_set_halo from the caller's own synchronisation lists (what
+        an Arcane shim builds from the DoF family's IVariableSynchronizer,
+        femutils/FemDoFsOnNodes.cc:125-126): for each neighbour rank (in order)
+        the owned DoFs to send and the ghost DoFs (ids >= n_rows) to receive."""
+        nbr = np.ascontiguousarray(neighbors, dtype=np.int32)
+        sl = [np.ascontiguousarray(a, dtype=np.int32) for a in send_ids]
+        rl = [np.ascontiguousarray(a, dtype=np.int32) for a in recv_ids]
+        if len(sl) != nbr.size or len(rl) != nbr.size:
+            raise ValueError("one send and one receive list per neighbour")
+        sc = np.array([a.size for a in sl], dtype=np.int64)
+        rc = np.array([a.size for a in rl], dtype=np.int64)
+        si = np.concatenate(sl + [np.zeros(1, np.int32)])  # never empty: a valid pointer
+        ri = np.concatenate(rl + [np.zeros(1, np.int32)])
+        call("afem_ls_set_halo", self.impl, comm.h, nbr.size, _ptr(nbr) if nbr.size else None,
+             _ptr(sc) if nbr.size else None, _ptr(si), _ptr(rc) if nbr.size else None, _ptr(ri))
 
     def set_halo_structured(self, comm, mesh: Mesh):
         call("afem_ls_set_halo_structured", self.impl, comm.h, mesh.h)

@@ -10,6 +10,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -169,6 +170,7 @@ struct Structure {
   // meshes use the node order.  The matrix itself stays in node order.
   DevBuf<int32_t> perm;  // [n_slices*64]
   bool brick_order = false;
+  bool lattice = false;  // brick order of a lattice recovered from the coordinates (array-fed mesh)
   // Lanes [j*run, (j+1)*run) of a slice hold consecutive rows (an x-run of a
   // brick, or the whole slice in node order), idle lanes only at the end of
   // a run: their value segments are one contiguous range.
@@ -254,6 +256,7 @@ struct Bsr {
   DevBuf<int64_t> csr_rows;
   DevBuf<int32_t> csr_cols;
   DevBuf<double> csr_vals;  // per-block layout permuted to CSR order
+  DevBuf<int32_t> gen_flag;  // error flag of the generic element-functor assembly (afem_bsr_assembly_view)
 };
 
 // ------------------------------------------------------------------ communicator / halo
@@ -269,11 +272,20 @@ struct Halo {
   // own stream while the context stream computes (created lazily)
   hipStream_t cs = nullptr;
   hipEvent_t ev_packed = nullptr, ev_done = nullptr;
+  // asynchronous host transport (afem_comm_host_async): the caller's exchange
+  // callback runs on `worker` between halo_begin and halo_end, on the pinned
+  // staging buffer hpin (send part, then receive part)
+  double* hpin = nullptr;
+  size_t hpin_n = 0;
+  std::thread worker;
+  int worker_rc = 0;
   Halo() = default;
   Halo(const Halo&) = delete;
   Halo& operator=(const Halo&) = delete;
   ~Halo()
   {
+    if (worker.joinable()) worker.join();
+    if (hpin) (void)hipHostFree(hpin);
     if (ev_packed) (void)hipEventDestroy(ev_packed);
     if (ev_done) (void)hipEventDestroy(ev_done);
     if (cs) (void)hipStreamDestroy(cs);
@@ -287,7 +299,8 @@ void halo_exchange(Halo& h, Ctx& ctx, double* x);
 void halo_begin(Halo& h, Ctx& ctx, double* x);
 void halo_end(Halo& h, Ctx& ctx, double* x);
 void comm_allreduce(Comm* c, Ctx& ctx, double* d, int64_t n);
-bool comm_is_host(Comm* c);  // host-transport communicator (synchronous exchanges)
+bool comm_is_host(Comm* c);  // host-transport communicator
+void comm_set_host_async(Comm* c, bool on);  // host transport: exchange on a worker thread (halo_begin/end)
 
 // ------------------------------------------------------------------ linear system
 struct Multigrid;
@@ -316,6 +329,12 @@ struct LinearSystem {
   DevBuf<int64_t> own_rows;   // when the view came in the reference int32 layout
   DevBuf<int32_t> own_cols;
   DevBuf<double> own_vals;    // host-uploaded or COO-built matrix
+  // setCSRValues on HOST memory: the caller's arrays stay the matrix until the
+  // solve (femutils/DoFLinearSystem.h:251-258) -- point updates edit them and
+  // afem_ls_solve re-reads the values (own_vals is the device copy)
+  const int32_t* hv_rows = nullptr;
+  const int32_t* hv_cols = nullptr;
+  double* hv_vals = nullptr;
   // the CSR was rebuilt from the host COO maps (matrixAddValue without a
   // view): later adds/sets go to the maps again; any other CSR view (device,
   // host-uploaded, BSR) is updated in place

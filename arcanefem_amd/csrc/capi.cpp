@@ -561,6 +561,31 @@ int afem_bsr_view(afem_bsr* b, afem_csr_view* v)
   API_END
 }
 
+int afem_bsr_assembly_view(afem_bsr* b, afem_assembly_view* v)
+{
+  API_BEGIN
+  NOT_NULL(b);
+  NOT_NULL(v);
+  AFEM_REQUIRE(b->has_sparsity, AFEM_ERR_STATE, "no sparsity (computeSparsity first)");
+  if (!b->gen_flag.p) b->gen_flag.alloc(1);
+  const Mesh& m = *b->mesh;
+  v->n_rows = b->s.n_rows;
+  v->n_nodes = m.n_nodes;
+  v->n_cells = m.n_cells;
+  v->nb_node_per_cell = m.nv;
+  v->block_size = b->nb_dof;
+  v->ordered_per_block = b->order_per_block ? 1 : 0;
+  v->dim = m.dim;
+  v->cell_node = m.cell_node.p;
+  v->coords = m.coords.p;
+  v->rows = b->s.row_ptr.p;
+  v->columns = b->s.cols.p;
+  v->values = b->values.p;
+  v->error_flag = b->gen_flag.p;
+  v->stream = (void*)m.ctx->stream;
+  API_END
+}
+
 int afem_bsr_get_stats(afem_bsr* b, afem_bsr_stats* st)
 {
   API_BEGIN
@@ -575,7 +600,7 @@ int afem_bsr_get_stats(afem_bsr* b, afem_bsr_stats* st)
   st->max_slice_nodes = b->s.max_slice_nodes;
   st->max_slice_width = b->s.max_slice_w;
   st->n_slices = b->s.n_slices;
-  st->brick_order = b->s.brick_order ? 1 : 0;
+  st->brick_order = b->s.lattice ? 2 : b->s.brick_order ? 1 : 0;
   st->uniform_slices = (int32_t)b->s.n_uni;
   st->stencil_slices = (int32_t)b->s.n_k;
   st->stencil_sig = b->s.sig_k;
@@ -683,6 +708,9 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
   ls->mg.reset();
   ls->has_csr = true;
   ls->csr_from_coo = false;
+  ls->hv_rows = nullptr;
+  ls->hv_cols = nullptr;
+  ls->hv_vals = nullptr;
   ls->csr_n = b->s.n_rows * k;
   ls->csr_nnz = b->s.nnz * k * k;
   API_END
@@ -779,6 +807,18 @@ int afem_ls_get_solver_options(afem_ls* ls, afem_solver_opts* o)
 // maps is a derived copy, so further adds go to the maps.
 static bool ls_uses_device_view(afem_ls* ls) { return ls->has_csr && !ls->csr_from_coo; }
 
+// a point update of a host view also edits the caller's arrays (the solve
+// re-reads them); the device copy is updated too (SpMV / getCSRValues before solve)
+static void host_view_update(afem_ls* ls, int32_t row, int32_t col, double v, bool set)
+{
+  const int64_t b = ls->hv_rows[row], e = row + 1 < ls->csr_n ? ls->hv_rows[row + 1] : ls->csr_nnz;
+  for (int64_t k = b; k < e; ++k)
+    if (ls->hv_cols[k] == col) {
+      ls->hv_vals[k] = set ? v : ls->hv_vals[k] + v;
+      return;
+    }
+}
+
 int afem_ls_matrix_add_value(afem_ls* ls, int32_t row, int32_t col, double v)
 {
   API_BEGIN
@@ -788,6 +828,7 @@ int afem_ls_matrix_add_value(afem_ls* ls, int32_t row, int32_t col, double v)
   ls->ctx->set_device();
   if (ls_uses_device_view(ls)) {
     ls_point_update(*ls, row, col, v, false);
+    if (ls->hv_vals) host_view_update(ls, row, col, v, false);
   }
   else {
     if (v == 0.0) return AFEM_OK;  // femutils/AlephDoFLinearSystem.cc:198-199
@@ -807,6 +848,7 @@ int afem_ls_matrix_set_value(afem_ls* ls, int32_t row, int32_t col, double v)
   ls->ctx->set_device();
   if (ls_uses_device_view(ls)) {
     ls_point_update(*ls, row, col, v, true);
+    if (ls->hv_vals) host_view_update(ls, row, col, v, true);
   }
   else {
     ls->has_csr = false;
@@ -902,8 +944,15 @@ int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows
   ls->csr_nnz = nb_nz;
   ls->has_csr = true;
   ls->csr_from_coo = false;
+  ls->hv_rows = nullptr;
+  ls->hv_cols = nullptr;
+  ls->hv_vals = nullptr;
   if (mem == AFEM_MEM_HOST) {
-    // host view: values now live on the device copy; keep the COO maps empty
+    // host view: the caller's arrays stay the matrix until solve (point
+    // updates edit them, the solve re-reads the values); keep the COO maps empty
+    ls->hv_rows = rows;
+    ls->hv_cols = columns;
+    ls->hv_vals = values;
     ls->add_map.clear();
     ls->set_map.clear();
   }
@@ -1017,6 +1066,9 @@ int afem_ls_clear_values(afem_ls* ls)
   ls->mg.reset();
   ls->csr_cols = nullptr;
   ls->csr_vals = nullptr;
+  ls->hv_rows = nullptr;
+  ls->hv_cols = nullptr;
+  ls->hv_vals = nullptr;
   ls->add_map.clear();
   ls->set_map.clear();
   ls->host_elim.clear();
@@ -1031,6 +1083,14 @@ int afem_ls_solve(afem_ls* ls, afem_solve_stats* st)
 {
   API_BEGIN
   NOT_NULL(ls);
+  if (ls->hv_vals && ls->has_csr && !ls->csr_from_coo && ls->csr_nnz > 0) {
+    // host view: the values as they are now (the module may have edited its
+    // view since setCSRValues; Hypre reads the live view at solve,
+    // femutils/HypreDoFLinearSystem.cc:148-156, 587-599)
+    ls->ctx->set_device();
+    AFEM_HIP(hipMemcpyAsync(ls->own_vals.p, ls->hv_vals, (size_t)ls->csr_nnz * 8, hipMemcpyHostToDevice,
+                            ls->ctx->stream));
+  }
   ls_solve(*ls, st);
   API_END
 }
@@ -1231,6 +1291,14 @@ int afem_comm_allreduce_sum(afem_comm* c, double* d, int64_t n)
   AFEM_REQUIRE(n >= 0, AFEM_ERR_ARG, "negative count");
   c->ctx->set_device();
   comm_allreduce(c->c, *c->ctx, d, n);
+  API_END
+}
+
+int afem_comm_host_async(afem_comm* comm, int enable)
+{
+  API_BEGIN
+  NOT_NULL(comm);
+  comm_set_host_async(comm->c, enable != 0);
   API_END
 }
 

@@ -20,6 +20,7 @@ struct Comm {
   // host transport (afem_comm_create_host): the caller's IParallelMng-like
   // callbacks move the halo and the dot-product sums through host memory
   bool host = false;
+  bool host_async = false;  // halo_begin hands the exchange to a worker thread, halo_end joins it
   afem_host_transport ht{};
   double* pin = nullptr;  // pinned staging buffer (allreduce / halo)
   size_t pin_n = 0;
@@ -121,6 +122,11 @@ void comm_allreduce(Comm* c, Ctx& ctx, double* d, int64_t n)
 
 int comm_nranks(Comm* c) { return c ? c->nranks : 1; }
 bool comm_is_host(Comm* c) { return c && c->host; }
+void comm_set_host_async(Comm* c, bool on)
+{
+  AFEM_REQUIRE(c && c->host, AFEM_ERR_ARG, "afem_comm_host_async: not a host-transport communicator");
+  c->host_async = on;
+}
 int comm_rank(Comm* c) { return c ? c->rank : 0; }
 
 void halo_setup(Halo& h, Ctx& ctx, Comm* comm, int n_nbr, const int32_t* nbr, const int64_t* send_cnt,
@@ -176,11 +182,66 @@ void post_sendrecv(Halo& h, hipStream_t st)
 }
 }  // namespace
 
+namespace {
+// host transport, asynchronous: pack on the context stream, copy the send part
+// to the halo's pinned buffer, and let a worker thread wait for that copy and
+// run the caller's exchange callback while the context stream computes
+void host_begin_async(Halo& h, Ctx& ctx, double* x)
+{
+  Comm* c = h.comm;
+  const size_t need = (size_t)(h.n_send + h.n_recv);
+  if (need > h.hpin_n) {
+    if (h.hpin) (void)hipHostFree(h.hpin);
+    h.hpin = nullptr;
+    AFEM_HIP(hipHostMalloc(reinterpret_cast<void**>(&h.hpin), need * sizeof(double), hipHostMallocDefault));
+    h.hpin_n = need;
+  }
+  if (!h.ev_packed) AFEM_HIP(hipEventCreateWithFlags(&h.ev_packed, hipEventDisableTiming));
+  if (h.n_send) {
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(h.n_send, 256)), dim3(256), 0, ctx.stream, h.n_send, h.send_ids.p, x,
+                       h.send_buf.p);
+    AFEM_LAUNCHED();
+    AFEM_HIP(hipMemcpyAsync(h.hpin, h.send_buf.p, h.n_send * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+  }
+  AFEM_HIP(hipEventRecord(h.ev_packed, ctx.stream));
+  AFEM_REQUIRE(!h.worker.joinable(), AFEM_ERR_STATE, "halo_begin: an exchange is already in flight");
+  const int dev = ctx.device;
+  h.worker_rc = 0;
+  h.worker = std::thread([&h, c, dev]() {
+    if (hipSetDevice(dev) != hipSuccess || hipEventSynchronize(h.ev_packed) != hipSuccess) {
+      h.worker_rc = -1;
+      return;
+    }
+    std::vector<int32_t> nb(h.nbr.begin(), h.nbr.end());
+    h.worker_rc = c->ht.exchange(c->ht.user, (int)nb.size(), nb.data(), h.hpin, h.send_cnt.data(), h.hpin + h.n_send,
+                                 h.recv_cnt.data());
+  });
+}
+
+void host_end_async(Halo& h, Ctx& ctx, double* x)
+{
+  if (!h.worker.joinable()) return;
+  h.worker.join();
+  AFEM_REQUIRE(h.worker_rc == 0, AFEM_ERR_COMM,
+               h.worker_rc < 0 ? "host transport: waiting for the packed halo failed" : "host transport: exchange failed");
+  if (h.n_recv) {
+    AFEM_HIP(hipMemcpyAsync(h.recv_buf.p, h.hpin + h.n_send, h.n_recv * sizeof(double), hipMemcpyHostToDevice,
+                            ctx.stream));
+    hipLaunchKernelGGL(k_scatter, dim3(grid_for(h.n_recv, 256)), dim3(256), 0, ctx.stream, h.n_recv, h.recv_ids.p,
+                       h.recv_buf.p, x);
+    AFEM_LAUNCHED();
+  }
+}
+}  // namespace
+
 void halo_begin(Halo& h, Ctx& ctx, double* x)
 {
   if (!h.comm || h.comm->nranks == 1 || h.nbr.empty()) return;
-  if (h.comm->host) {  // host transport: synchronous anyway
-    halo_exchange(h, ctx, x);
+  if (h.comm->host) {
+    if (h.comm->host_async)
+      host_begin_async(h, ctx, x);
+    else
+      halo_exchange(h, ctx, x);  // synchronous transport: the whole exchange here
     return;
   }
   if (!h.cs) {
@@ -201,7 +262,11 @@ void halo_begin(Halo& h, Ctx& ctx, double* x)
 
 void halo_end(Halo& h, Ctx& ctx, double* x)
 {
-  if (!h.comm || h.comm->nranks == 1 || h.nbr.empty() || h.comm->host) return;
+  if (!h.comm || h.comm->nranks == 1 || h.nbr.empty()) return;
+  if (h.comm->host) {
+    host_end_async(h, ctx, x);  // no-op unless halo_begin started a worker
+    return;
+  }
   AFEM_HIP(hipStreamWaitEvent(ctx.stream, h.ev_done, 0));
   if (h.n_recv) {
     hipLaunchKernelGGL(k_scatter, dim3(grid_for(h.n_recv, 256)), dim3(256), 0, ctx.stream, h.n_recv, h.recv_ids.p,

@@ -1699,8 +1699,8 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   bool converged = fixed ? false : (ls.pinned[0] == 0.0 || rel <= o.rtol);
   // multi-rank: the row blocks that read no ghost column run while the halo
   // of p is in flight (RCCL on the halo's stream), the rest after it lands
-  // (host transport: the exchange completes in halo_begin; same split, so the
-  // multi-rank GPU tests cover it)
+  // (host transport: on a worker thread between halo_begin and halo_end with
+  // afem_comm_host_async, else inside halo_begin; same split either way)
   const bool overlap = multi && ((pl.rpb > 0 && pl.wide && pl.unroll) || pl.rpb == -2 || pl.rpb == -3);
   int64_t n_int = 0;
   if (overlap) {

@@ -22,6 +22,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <string>
 
@@ -325,6 +326,61 @@ __global__ void k_perm_identity(int64_t n_pos, int64_t n_rows, int32_t* __restri
 {
   int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p < n_pos) perm[p] = p < n_rows ? (int32_t)p : -1;
+}
+
+// ---- lattice recovery (meshes that arrive as arrays): when the owned nodes
+// of a tetrahedral mesh sit on a (jittered) lattice -- a structured box in any
+// numbering, e.g. the caller's own or a random one -- the processing order is
+// the brick order of that lattice, so the uniform / stencil instances apply as
+// they do to the generator's boxes.  Per axis the owned nodes' coordinates are
+// sorted and cut into layers at the gaps wider than half the widest gap (within
+// a layer the jitter spread is < 0.2 h, between layers > 0.8 h); the layer
+// counts must multiply to the owned node count and every lattice point must
+// hold exactly one node.  Only the ORDER depends on this: strips, signatures
+// and bank placement are computed from the real connectivity afterwards, so a
+// wrong guess costs speed, never values.
+__global__ void k_axis_keys(int64_t n, const double* __restrict__ coords, int a, uint64_t* __restrict__ keys,
+                            int32_t* __restrict__ ids)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = (uint64_t)ordered_bits(coords[3 * i + a]);
+  ids[i] = (int32_t)i;
+}
+__global__ void k_max_gap(int64_t n, const uint64_t* __restrict__ sorted, unsigned long long* __restrict__ out)
+{
+  double g = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += (int64_t)gridDim.x * blockDim.x)
+    g = fmax(g, from_ordered_bits(sorted[i + 1]) - from_ordered_bits(sorted[i]));
+  atomicMax(out, (unsigned long long)__double_as_longlong(g));  // g >= 0: the bits order like the values
+}
+__global__ void k_gap_flags(int64_t n, const uint64_t* __restrict__ sorted, double thr,
+                            int32_t* __restrict__ flag)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  flag[i] = (i + 1 < n && from_ordered_bits(sorted[i + 1]) - from_ordered_bits(sorted[i]) > thr) ? 1 : 0;
+}
+// layer of sorted position i = number of layer boundaries before it
+__global__ void k_layer_scatter(int64_t n, const int32_t* __restrict__ ids, const int64_t* __restrict__ scan,
+                                int32_t* __restrict__ layer)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) layer[ids[i]] = (int32_t)scan[i];
+}
+__global__ void k_lattice_fill(int64_t n, const int32_t* __restrict__ lx, const int32_t* __restrict__ ly,
+                               const int32_t* __restrict__ lz, int64_t Lx, int64_t Ly, int32_t* __restrict__ lat,
+                               int32_t* __restrict__ bad)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t c = lx[i] + Lx * (ly[i] + Ly * (int64_t)lz[i]);
+  if (atomicCAS(lat + c, -1, (int32_t)i) != -1) *bad = 1;
+}
+__global__ void k_perm_map(int64_t n_pos, const int32_t* __restrict__ lat, int32_t* __restrict__ perm)
+{
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_pos && perm[p] >= 0) perm[p] = lat[perm[p]];
 }
 
 // Per slice: the max incidence count (ELL width, rounded up to a multiple of
@@ -948,6 +1004,84 @@ __global__ void k_strip_width(int64_t n_slices, const int32_t* __restrict__ stri
 
 }  // namespace
 
+namespace {
+// the owned nodes' lattice (see k_axis_keys): on success the brick order of
+// that lattice in s.perm (s.n_slices, s.run, s.brick_order set) and true
+bool lattice_order(Ctx& ctx, const Mesh& m, int64_t n_rows, Structure& s)
+{
+  DevBuf<uint64_t> keys, keys_s;
+  DevBuf<int32_t> ids, ids_s, flag;
+  DevBuf<int64_t> scan;
+  DevBuf<int32_t> layer[3];
+  keys.alloc(n_rows);
+  keys_s.alloc(n_rows);
+  ids.alloc(n_rows);
+  ids_s.alloc(n_rows);
+  flag.alloc(n_rows);
+  scan.alloc(n_rows + 1);
+  size_t tmp_bytes = 0;
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys.p, keys_s.p, ids.p, ids_s.p, (int)n_rows, 0, 64,
+                                              ctx.stream));
+  DevBuf<unsigned char> tmp;
+  tmp.alloc(tmp_bytes > 0 ? tmp_bytes : 1);
+  DevBuf<unsigned long long> gap;
+  gap.alloc(1);
+  int64_t L[3];
+  for (int a = 0; a < 3; ++a) {
+    hipLaunchKernelGGL(k_axis_keys, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, m.coords.p, a,
+                       keys.p, ids.p);
+    AFEM_LAUNCHED();
+    AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tmp_bytes, keys.p, keys_s.p, ids.p, ids_s.p, (int)n_rows, 0,
+                                                64, ctx.stream));
+    AFEM_HIP(hipMemsetAsync(gap.p, 0, gap.bytes(), ctx.stream));
+    hipLaunchKernelGGL(k_max_gap, dim3(1024), dim3(256), 0, ctx.stream, n_rows, keys_s.p, gap.p);
+    AFEM_LAUNCHED();
+    unsigned long long hg = 0;
+    AFEM_HIP(hipMemcpyAsync(&hg, gap.p, sizeof(hg), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    double g;
+    memcpy(&g, &hg, sizeof(g));
+    if (!(g > 0.0)) return false;
+    hipLaunchKernelGGL(k_gap_flags, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, keys_s.p, 0.5 * g,
+                       flag.p);
+    AFEM_LAUNCHED();
+    exclusive_scan_i32_to_i64(ctx, flag.p, scan.p, n_rows);
+    L[a] = read_i64(ctx, scan.p + n_rows) + 1;
+    layer[a].alloc(n_rows);
+    hipLaunchKernelGGL(k_layer_scatter, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, ids_s.p,
+                       scan.p, layer[a].p);
+    AFEM_LAUNCHED();
+  }
+  if (L[0] < 2 || L[1] < 2 || L[2] < 2 || L[0] * L[1] * L[2] != n_rows) return false;
+  DevBuf<int32_t> lat, bad;
+  lat.alloc(n_rows);
+  bad.alloc(1);
+  AFEM_HIP(hipMemsetAsync(lat.p, 0xFF, lat.bytes(), ctx.stream));
+  AFEM_HIP(hipMemsetAsync(bad.p, 0, bad.bytes(), ctx.stream));
+  hipLaunchKernelGGL(k_lattice_fill, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, layer[0].p,
+                     layer[1].p, layer[2].p, L[0], L[1], lat.p, bad.p);
+  AFEM_LAUNCHED();
+  int32_t hb = 0;
+  AFEM_HIP(hipMemcpyAsync(&hb, bad.p, sizeof(hb), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  if (hb) return false;
+  const FaceTiles F = face_tiles(L[0], L[1], L[2]);
+  s.n_slices = F.start[6];
+  s.perm.alloc(s.n_slices * 64);
+  hipLaunchKernelGGL(k_perm_bricks_bd, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream, s.n_slices,
+                     L[0], L[1], L[2], F, s.perm.p);
+  AFEM_LAUNCHED();
+  hipLaunchKernelGGL(k_perm_map, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream, s.n_slices * 64,
+                     lat.p, s.perm.p);
+  AFEM_LAUNCHED();
+  ctx.sync();
+  s.run = 1;
+  s.brick_order = true;
+  s.lattice = true;
+  return true;
+}
+}  // namespace
+
 void build_structure(Mesh& m, Structure& s)
 {
   Ctx& ctx = *m.ctx;
@@ -1052,10 +1186,11 @@ void build_structure(Mesh& m, Structure& s)
     }
     s.brick_order = true;
   }
-  else {
+  else if (!(nv == 4 && m.dim == 3 && n_rows >= 8 && !getenv("AFEM_ORDER") && lattice_order(ctx, m, n_rows, s))) {
     s.n_slices = (n_rows + 63) / 64;
     s.perm.alloc(s.n_slices * 64);
-    // AFEM_ORDER=node: the caller's node order; =morton: Morton curve (diagnostics)
+    // AFEM_ORDER=node: the caller's node order; =morton: Morton curve; =hilbert:
+    // the Hilbert curve even for a lattice (diagnostics)
     const char* oe = getenv("AFEM_ORDER");
     const bool node_order = (oe && std::string(oe) == "node") || n_rows < 2;
     if (node_order) {

@@ -27,7 +27,7 @@ class HostCommunicator:
     reference's IParallelMng::reduce / sendRecv over the ranks of the default
     process group."""
 
-    def __init__(self, ctx, group=None):
+    def __init__(self, ctx, group=None, async_exchange: bool = False):
         import torch
         import torch.distributed as dist
 
@@ -73,6 +73,10 @@ class HostCommunicator:
         h = ctypes.c_void_p()
         call("afem_comm_create_host", ctx.h, self.nranks, self.rank, ctypes.byref(self._t), ctypes.byref(h))
         self.h = h
+        if async_exchange:
+            # the halo callback then runs on libafem's worker thread while the CG's
+            # interior SpMV is on the GPU (afem_comm_host_async)
+            call("afem_comm_host_async", self.h, 1)
 
     def close(self):
         if self.h:

@@ -65,7 +65,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true",
                     help="skip the CPU baselines (the oracle timed at the C2 size on the host cores, N = 1 only)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_assembly_C2.json"))
-    ap.add_argument("--no-extras", action="store_true", help="skip the C3 / C4 / C5 side measurements")
+    ap.add_argument("--no-extras", action="store_true", help="skip the side measurements (N = 1 only anyway)")
+    ap.add_argument("--legs", default="c4,c3,c2_arrays,unstructured,c5",
+                    help="the side measurements to run (comma list of c4, c3, c2_arrays, unstructured, c5)")
     ap.add_argument("--c3-n", type=int, default=170, help="C3 block-3 elasticity box (170 -> 5.0M nodes)")
     ap.add_argument("--c4-n", type=int, default=463, help="C4 Poisson box on one GPU (463 -> 99.9M DoF); 0: skip")
     ap.add_argument("--c5-n", type=int, default=128,
@@ -362,6 +364,53 @@ def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2):
     return out
 
 
+def c2_arrays_leg(ctx, af, n, reps=10, warmup=2):
+    """C2 handed over the way a caller's mesh arrives: the generator's box
+    downloaded, its nodes and cells renumbered by a seeded random permutation
+    (seed 1234, SURVEY §8d's robustness variant) and uploaded with
+    afem_mesh_create.  The structure build recovers the lattice from the
+    coordinates (brick_order 2) and the assembly runs the same instances as on
+    the generator's box.  Poisson assembly + source, median kernel time,
+    roofline as C2's."""
+    m0 = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+    cells, coords, _ = m0.download()
+    m0.close()
+    rng = np.random.default_rng(1234)
+    p = rng.permutation(coords.shape[0]).astype(np.int32)
+    cells = p[cells][rng.permutation(cells.shape[0])]
+    pc = np.empty_like(coords)
+    pc[p] = coords
+    del coords
+    mesh = af.Mesh.from_arrays(ctx, 3, cells, pc)
+    del cells, pc
+    bsr = af.BSRFormat(mesh, 1).initialize(True)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    bsr.computeSparsity()
+    ctx.synchronize()
+    sp_ms = (time.perf_counter() - t0) * 1e3
+    rhs = ctx.malloc(8 * mesh.n_own_nodes)
+    for _ in range(warmup):
+        bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set")
+    ctx.synchronize()
+    for i in range(reps):
+        ctx.event_record(200 + 2 * i)
+        bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set")
+        ctx.event_record(201 + 2 * i)
+    ctx.synchronize()
+    kms = float(np.median([ctx.event_elapsed(200 + 2 * i, 201 + 2 * i) for i in range(reps)]))
+    st = bsr.stats()
+    out = {"config": f"C2 box n={n} via afem_mesh_create, nodes and cells in a random order (seed 1234): "
+                     f"{mesh.n_own_nodes} DoF, {mesh.n_cells} tets, Poisson assembly + source",
+           "dof": int(mesh.n_own_nodes), "value": round(mesh.n_own_nodes / (kms * 1e-3) / 1e6, 1),
+           "unit": "MDoF/s (assembly kernels)", "kernel_ms": round(kms, 4), "roofline": roofline(bsr, mesh, kms),
+           "brick_order": int(st["brick_order"]), "sparsity_ms": round(sp_ms, 1)}
+    ctx.free(rhs)
+    bsr.close()
+    mesh.close()
+    return out
+
+
 def elastodynamics_c5(ctx, af, n, steps, preconditioners=("multigrid", "jacobi")):
     """BASELINE config C5 on one GPU: 3D Newmark elastodynamics, every step
     re-assembles c0 M + K and the body-force RHS on the fixed block-3
@@ -465,7 +514,7 @@ def cpu_baseline(c2, runs=5):
             "nproc": nproc, "affinity_cores": aff,
             "sample": f"C2 itself: Poisson-3D P1 Kuhn box ({n_own} DoF, {cells.shape[0]} tets, {cols.size} nnz), "
                       f"structure from the GPU run: median of {runs} assemblies {tm * 1e3:.0f} ms on {threads} "
-                      f"OpenMP threads (oracle/oracle.c cell loop, atomic adds; nproc {nproc}, {aff} cores in the "
+                      f"OpenMP threads (oracle/oracle.c cell loop, atomic adds, gcc -O3 -march=x86-64-v4; nproc {nproc}, {aff} cores in the "
                       f"affinity mask, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}); single thread "
                       f"{t1 * 1e3:.0f} ms = {n_own / t1 / 1e6:.2f} MDoF/s; oracle vs GPU values max rel diff "
                       f"{dvf:.1e} (free rows; {dv:.1e} overall), RHS {drhs:.1e}"}
@@ -636,12 +685,16 @@ def main():
             bsr.close()
             mesh.close()
             dbottom = None
-        if not args.no_extras and world == 1:
-            if args.c4_n > 0 and not (args.scaling == "strong" and n == args.c4_n):
-                extras["c4"] = poisson_c4(ctx, af, args.c4_n)
+        legs = set() if args.no_extras or world > 1 else set(args.legs.split(","))
+        if "c4" in legs and args.c4_n > 0 and not (args.scaling == "strong" and n == args.c4_n):
+            extras["c4"] = poisson_c4(ctx, af, args.c4_n)
+        if "c3" in legs:
             extras["c3"] = elasticity_c3(ctx, af, args.c3_n)
-            if args.unstructured_levels > 0:
-                extras["unstructured"] = unstructured_leg(ctx, af, "L-shape-3D.msh", args.unstructured_levels)
+        if "c2_arrays" in legs:
+            extras["c2_arrays"] = c2_arrays_leg(ctx, af, 215)
+        if "unstructured" in legs and args.unstructured_levels > 0:
+            extras["unstructured"] = unstructured_leg(ctx, af, "L-shape-3D.msh", args.unstructured_levels)
+        if "c5" in legs:
             extras["c5"] = elastodynamics_c5(ctx, af, args.c5_n, args.c5_steps)
         cpu = None
         if c2 is not None:

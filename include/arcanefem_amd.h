@@ -216,9 +216,10 @@ typedef struct afem_bsr_stats {
   int32_t max_slice_width;  /* max row length within one slice */
   int64_t n_slices;         /* assembly slices (wavefronts per launch) */
   int32_t brick_order;      /* 1: slices are node bricks of a structured box: 4x4x4 interior bricks
-                               (8x8 in 2D) and 8x8 tiles of the boundary faces; 0: slices follow a
-                               Hilbert-curve order of the node coordinates (plain node order under
-                               AFEM_ORDER=node) */
+                               (8x8 in 2D) and 8x8 tiles of the boundary faces; 2: the same bricks of
+                               a lattice recovered from the coordinates of a mesh given as arrays
+                               (any numbering); 0: slices follow a Hilbert-curve order of the node
+                               coordinates (plain node order under AFEM_ORDER=node) */
   int32_t uniform_slices;   /* slices whose 64 rows share one strip topology (uniform-control assembly variant) */
   int32_t last_kernel;      /* AFEM_KERNEL_* that ran the last assembly of this matrix */
   int32_t stencil_slices;   /* uniform slices of a compiled-in strip signature (scalar stencil instance) */
@@ -241,6 +242,29 @@ int afem_bsr_get_stats(afem_bsr* bsr, afem_bsr_stats* stats);
  * Any pointer may be NULL; sizes via afem_bsr_get_sizes. */
 int afem_bsr_get_sizes(afem_bsr* bsr, int64_t* n_scalar_rows, int64_t* nnz_scalar);
 int afem_bsr_export_csr32(afem_bsr* bsr, int32_t* rows, int32_t* rows_nb_column, int32_t* columns, double* values);
+/* Device pointers of a structure for a generic element-functor assembly
+ * (include/arcanefem_amd_generic.hpp: BSRFormat::assembleBilinear(lambda),
+ * femutils/BSRFormat.h:786-837): the mesh's cells and coordinates, the BSR
+ * rows / sorted columns / values in the matrix's layout, a device error flag
+ * and the context stream (hipStream_t) the kernel is enqueued on.  Valid until
+ * the structure is recomputed or destroyed. */
+typedef struct afem_assembly_view {
+  int64_t n_rows;            /* owned nodes = block rows */
+  int64_t n_nodes;           /* local nodes (columns) */
+  int64_t n_cells;
+  int32_t nb_node_per_cell;
+  int32_t block_size;        /* NB_DOF */
+  int32_t ordered_per_block; /* value layout, as afem_csr_view */
+  int32_t dim;
+  const int32_t* cell_node;  /* device [n_cells*nb_node_per_cell] */
+  const double* coords;      /* device [n_nodes*3] */
+  const int64_t* rows;       /* device [n_rows+1] */
+  const int32_t* columns;    /* device [nnz_blocks], sorted per row */
+  double* values;            /* device [nnz_blocks*NB_DOF^2] */
+  int32_t* error_flag;       /* device, one int: set when an element couples nodes outside the sparsity */
+  void* stream;              /* hipStream_t of the structure's context */
+} afem_assembly_view;
+int afem_bsr_assembly_view(afem_bsr* bsr, afem_assembly_view* view);
 /* Copies the internal (block) arrays to host. */
 int afem_bsr_download(afem_bsr* bsr, int64_t* rows, int32_t* columns, double* values);
 /* BSRFormat::toLinearSystem (femutils/BSRFormat.h:414-430): hands the matrix to
@@ -308,8 +332,12 @@ int afem_ls_eliminate_row_column(afem_ls* ls, int32_t row, double v);
 /* setCSRValues with the reference's CSRFormatView layout: rows[nb_row] (no
  * sentinel; the last row ends at nb_nz), rows_nb_column[nb_row] (may be NULL),
  * columns[nb_nz], values[nb_nz].  The view is non-owning and must stay valid
- * until solve (femutils/DoFLinearSystem.h:251-258); values are updated in
- * place by the BC kernels at solve. */
+ * until solve (femutils/DoFLinearSystem.h:251-258).  Device memory: the
+ * view is used in place (the BC kernels update its values at solve).  Host
+ * memory: structure and values are copied to the device now, matrixAdd/
+ * SetValue edit the caller's arrays (and the copy), and afem_ls_solve
+ * re-reads the values from the caller's array first, so edits made to the
+ * view after this call are seen by the solve; the BCs go into the device copy. */
 int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows_nb_column, const int32_t* columns,
                            double* values, int32_t nb_row, int32_t nb_nz, int mem);
 int afem_ls_has_set_csr_values(afem_ls* ls, int* has);
@@ -440,6 +468,12 @@ typedef struct afem_host_transport {
 } afem_host_transport;
 int afem_comm_create_host(afem_ctx* ctx, int nranks, int rank, const afem_host_transport* transport,
                           afem_comm** out);
+/* Host transport only: enable != 0 runs the exchange callback on a worker
+ * thread, so the CG's interior SpMV proceeds while the halo is in flight
+ * (halo posted after the pack, joined before the boundary rows; the callbacks
+ * are then called from that thread, never concurrently with another call on
+ * the same communicator).  Default: synchronous. */
+int afem_comm_host_async(afem_comm* comm, int enable);
 int afem_comm_destroy(afem_comm* comm);
 /* In-place sum over ranks of n doubles (device pointer) on the context stream. */
 int afem_comm_allreduce_sum(afem_comm* comm, double* dbuf, int64_t n);

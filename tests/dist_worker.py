@@ -33,8 +33,13 @@ def main():
     from arcanefem_amd.parallel import HostCommunicator
 
     ctx = af.Context(0)
-    comm = HostCommunicator(ctx)
+    # "*_async" / "lists:*": the exchange callback on libafem's worker thread
+    # (afem_comm_host_async): the CG's interior SpMV runs with the halo in flight
+    asy = case.endswith("_async") or case.startswith("lists:")
+    comm = HostCommunicator(ctx, async_exchange=asy)
     res = {}
+    if case.endswith("_async"):
+        case = case[:-len("_async")]
     if case in ("poisson", "poisson_pat"):
         n, nz = (POISSON if case == "poisson" else POISSON_PAT)["n"], (POISSON if case == "poisson" else POISSON_PAT)["nz"]
         mesh = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=20250220, nranks=world, rank=rank)
@@ -53,6 +58,46 @@ def main():
         # CG iter/s with the halo attached (fixed iterations)
         ls.setSolverOptions(fixed_iterations=20)
         ls.solve()
+    elif case.startswith("lists:"):
+        # the halo from the caller's own synchronisation lists (afem_ls_set_halo:
+        # what the Arcane shim builds from IVariableSynchronizer), then
+        # afem_ls_synchronize of a ghosted vector (m_u.synchronize())
+        from golden_cases import CASES
+        from arcanefem_amd.gmsh import read_gmsh
+
+        mfile, f, bcs, _, P = CASES[case[6:]]
+        gm = read_gmsh(os.path.join(ROOT, "tests", "golden", mfile))
+        part = af.partition_rcb(gm.dim, gm.coords, world)
+        plan = af.subdomain_plan(gm.cells, part, world, rank)
+        l2g = plan["local_to_global"]
+        g2l = np.full(gm.n_nodes, -1, dtype=np.int64)
+        g2l[l2g] = np.arange(l2g.size)
+        lcells = g2l[gm.cells[plan["cells"]]].astype(np.int32)
+        assert (lcells >= 0).all()
+        mesh = af.Mesh.from_arrays(ctx, gm.dim, lcells, gm.coords[l2g], n_own=plan["n_own"])
+        bsr = af.BSRFormat(mesh, 1).initialize(True)
+        bsr.computeSparsity()
+        ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes, mesh.n_nodes)
+        bsr.assemblePoissonP1(1.0, f, ls.rhsVariable(), rhs_mode="set")
+        bsr.toLinearSystem(ls)
+        for g, v in bcs:
+            loc = g2l[gm.group_nodes(g)]
+            own = loc[(loc >= 0) & (loc < mesh.n_own_nodes)].astype(np.int32)
+            if own.size:
+                ls.applyDirichletViaPenalty(own, v, P)
+        nbr = plan["neighbors"]
+        ls.set_halo(comm, nbr, [plan["send"][int(r)] for r in nbr], [plan["recv"][int(r)] for r in nbr])
+        # synchronize(): owners' values land in the ghosts
+        xs = np.where(np.arange(l2g.size) < mesh.n_own_nodes, l2g + 0.25, -1.0)
+        dx = ctx.malloc(8 * xs.size)
+        ctx.to_device(dx, xs)
+        ls.synchronize(dx)
+        synced = ctx.to_host(dx, xs.size, np.float64)
+        ctx.free(dx)
+        ls.setSolverOptions(rtol=1e-14, max_iter=20000)
+        st = ls.solve()
+        res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
+                   converged=int(st["converged"]), rel=st["rel_residual"], synced=synced, spmv=st["spmv_kernel"])
     elif case.startswith("gmsh:"):
         # a reference Gmsh mesh partitioned by libafem's RCB into `world`
         # ghosted subdomains (afem_mesh_create_subdomain), Poisson + penalty

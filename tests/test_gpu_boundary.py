@@ -365,6 +365,32 @@ def test_host_csr_view_accepts_point_updates(ctx):
     assert st["converged"] and np.abs(x - xo).max() / np.abs(xo).max() <= SOL_TOL
 
 
+def test_host_csr_view_is_read_at_solve(ctx):
+    """The view contract of femutils/DoFLinearSystem.h:251-258: a host CSR view
+    stays the matrix until solve.  The module edits its own value array after
+    setCSRValues (no matrixAddValue call); the solve must see the edit, as
+    Hypre's solve reads the live view (HypreDoFLinearSystem.cc:587-599)."""
+    gm = read_gmsh(path("circle_cut.msh"))
+    n = gm.n_nodes
+    orp, ocols = O.sparsity(n, n, gm.cells)
+    ovals, orhs = O.assemble_poisson(n, gm.cells, gm.coords, orp, ocols, 5.5)
+    O.dirichlet_penalty(gm.group_nodes("horizontal"), 0.5, 1e30, orp, ocols, ovals, orhs)
+    vals = ovals.copy()
+    ls = af.DoFLinearSystem().initialize(ctx, n)
+    ls.setCSRValues(orp[:-1].astype(np.int32), np.diff(orp).astype(np.int32), ocols, vals)
+    ls.set_rhs_host(orhs)
+    # the module's own edit after the hand-over: a mass-like shift of every diagonal
+    diag = np.array([orp[r] + np.searchsorted(ocols[orp[r]:orp[r + 1]], r) for r in range(n)])
+    free = vals[diag] < 1e20
+    vals[diag[free]] += 3.0
+    ovals[diag[free]] += 3.0
+    ls.setSolverOptions(method="direct")
+    st = ls.solve()
+    x = ls.solution_host()
+    xo = np.linalg.solve(O.csr_to_dense(orp, ocols, ovals), orhs)
+    assert st["converged"] and np.abs(x - xo).max() / np.abs(xo).max() <= SOL_TOL
+
+
 def test_boundary_argument_checks(ctx):
     # ADVICE r1 (capi.cpp:544): a subdomain CSR has ghost columns, the linear
     # system must span them

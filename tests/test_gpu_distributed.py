@@ -53,9 +53,14 @@ def _run(case, world, tmp_path):
     return [dict(np.load(o)) for o in outs]
 
 
-@pytest.mark.parametrize("case,world", [("poisson", 2), ("poisson", 3), ("poisson_pat", 2)])
+@pytest.mark.parametrize("case,world", [("poisson", 2), ("poisson", 3), ("poisson_pat", 2), ("poisson_async", 3),
+                                        ("poisson_pat_async", 2)])
 def test_distributed_poisson_solve(case, world, tmp_path):
+    """*_async: the host transport's exchange runs on libafem's worker thread
+    between halo_begin and halo_end, so the interior row blocks of every CG
+    SpMV run with the halo actually in flight."""
     res = _run(case, world, tmp_path)
+    case = case.replace("_async", "")
     prm = W.POISSON if case == "poisson" else W.POISSON_PAT
     n, nz = prm["n"], prm["nz"]
     if case == "poisson_pat":  # the pattern SpMV in the interior / halo-boundary split
@@ -140,3 +145,32 @@ def test_distributed_gmsh_subdomains(case, world, tmp_path):
     nerr, mx = O.check_node_result({int(t): x[i] for i, t in enumerate(gm.node_tags)}, gold, 1e-4)
     assert nerr == 0
     assert mx <= GOLDEN_TOL[case] * 1.5
+
+
+@pytest.mark.parametrize("case,world", [("sphere_3D", 3), ("L-shape_2D", 2)])
+def test_distributed_halo_from_caller_lists(case, world, tmp_path):
+    """The halo plan handed over as the caller's own lists (afem_ls_set_halo,
+    the shim's path from Arcane's IVariableSynchronizer) on meshes uploaded
+    as plain arrays, the exchange asynchronous: afem_ls_synchronize fills
+    every ghost with its owner's value and the distributed solve equals the
+    single-domain direct solve."""
+    from golden_cases import CASES
+    from arcanefem_amd.gmsh import read_gmsh
+
+    res = _run("lists:" + case, world, tmp_path)
+    mfile, f, bcs, gfile, P = CASES[case]
+    gm = read_gmsh(os.path.join(HERE, "golden", mfile))
+    rp, cols = O.sparsity(gm.n_nodes, gm.n_nodes, gm.cells)
+    vals, rhs = O.assemble_poisson(gm.n_nodes, gm.cells, gm.coords, rp, cols, f)
+    for g, v in bcs:
+        O.dirichlet_penalty(gm.group_nodes(g), v, P, rp, cols, vals, rhs)
+    xo = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
+    x = np.full(gm.n_nodes, np.nan)
+    for r in res:
+        k = int(r["n_own"])
+        assert np.array_equal(r["synced"], r["l2g"] + 0.25)  # owned kept, ghosts = owners' values
+        x[r["l2g"][:k]] = r["x"][:k]
+        assert r["converged"]
+    assert len({int(r["iters"]) for r in res}) == 1
+    assert not np.isnan(x).any()
+    assert np.abs(x - xo).max() / np.abs(xo).max() <= 1e-10

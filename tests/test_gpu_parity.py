@@ -391,14 +391,18 @@ def test_spmv_matches_oracle(ctx):
 
 
 @pytest.mark.parametrize("dim,n", [(3, 12), (2, 40)])
-@pytest.mark.parametrize("order", ["hilbert", "morton", "node"])
+@pytest.mark.parametrize("order", ["default", "hilbert", "morton", "node"])
 def test_random_node_permutation(ctx, monkeypatch, dim, n, order):
     # SURVEY §8d robustness variant: the structured mesh with a seeded random
-    # node and cell numbering; slices follow a Hilbert curve of the node
-    # coordinates (default), a Morton curve (AFEM_ORDER=morton) or the
-    # caller's node order (AFEM_ORDER=node, read at every computeSparsity);
-    # the assembled matrix must be the permuted
-    # matrix of the unpermuted box either way
+    # node and cell numbering, handed over as arrays.  Default: a 3D mesh whose
+    # owned nodes sit on a lattice gets the brick order of that lattice
+    # (recovered from the coordinates, brick_order 2; in the generator's
+    # numbering its bricks reach the uniform / stencil instances,
+    # test_lattice_order_matches_generator_box); other meshes (2D here) follow a
+    # Hilbert curve of the node coordinates.  AFEM_ORDER=hilbert / morton /
+    # node force the Hilbert curve, a Morton curve or the caller's node order
+    # (read at every computeSparsity).  The assembled matrix must be the
+    # permuted matrix of the unpermuted box in every case.
     ref = O.structured_mesh(dim, n, jitter=0.2, seed=20250220)
     rng = np.random.default_rng(1234)
     nn = ref["n_local"]
@@ -407,16 +411,23 @@ def test_random_node_permutation(ctx, monkeypatch, dim, n, order):
     coords = np.empty_like(ref["coords"])
     coords[p] = ref["coords"]
     mesh = af.Mesh.from_arrays(ctx, dim, cells, coords)
-    if order != "hilbert":
+    if order != "default":
         monkeypatch.setenv("AFEM_ORDER", order)
     bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
     st = bsr.stats()
-    assert st["brick_order"] == 0
-    if order != "hilbert":
+    if order == "default" and dim == 3:
+        # bricks of the recovered lattice; a random numbering scatters each
+        # row's sorted columns, so the bricks' slot streams differ row to row
+        # (no uniform slices: the general instance runs them)
+        assert st["brick_order"] == 2
+    else:
+        assert st["brick_order"] == 0
+    if order != "default":
         monkeypatch.delenv("AFEM_ORDER")
     if order != "node":
-        # the curve sort ran: a slice's rows are spatial neighbours, so it
-        # couples to far fewer distinct nodes than 64 random rows would
+        # the curve sort / brick order ran: a slice's rows are spatial
+        # neighbours, so it couples to far fewer distinct nodes than 64 random
+        # rows would
         m2 = af.Mesh.from_arrays(ctx, dim, cells, coords)
         monkeypatch.setenv("AFEM_ORDER", "node")
         b2, _ = _assemble_gpu(ctx, m2, 5.5)
@@ -440,6 +451,51 @@ def test_random_node_permutation(ctx, monkeypatch, dim, n, order):
     for i in range(nn):
         for k in range(rows[i], rows[i + 1]):
             assert abs(vals[k] - A0[(i, cols[k])]) <= VAL_TOL * scale
+
+
+@pytest.mark.parametrize("n,nz,jitter", [(9, 9, 0.2), (14, 5, 0.0), (5, 23, 0.19)])
+def test_lattice_order_matches_generator_box(ctx, n, nz, jitter):
+    """A generator box handed over as plain arrays in its own numbering: the
+    recovered lattice gives the generator's brick order, the same stencil /
+    uniform slice lists and bitwise the same matrix and RHS as the box made by
+    afem_mesh_create_structured (unjittered and non-cubic boxes included)."""
+    m0 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=jitter, seed=5)
+    b0, l0 = _assemble_gpu(ctx, m0, 5.5)
+    cells, coords, _ = m0.download()
+    m1 = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    b1, l1 = _assemble_gpu(ctx, m1, 5.5)
+    s0, s1 = b0.stats(), b1.stats()
+    assert s0["brick_order"] == 1 and s1["brick_order"] == 2
+    for k in ("n_slices", "uniform_slices", "stencil_slices", "stencil_sig", "max_slice_nodes"):
+        assert s0[k] == s1[k], (k, s0[k], s1[k])
+    r0, c0, v0 = b0.download()
+    r1, c1, v1 = b1.download()
+    assert np.array_equal(r0, r1) and np.array_equal(c0, c1)
+    assert np.array_equal(v0, v1)
+    assert np.array_equal(l0.rhs_host(), l1.rhs_host())
+
+
+def test_lattice_order_rejects_non_lattices(ctx):
+    """Coordinates that are not a lattice (a Kuhn box whose node layers are
+    warped beyond the gap rule, and one missing node) fall back to the
+    Hilbert order; the values stay the oracle's."""
+    ref = O.structured_mesh(3, 8, jitter=0.2, seed=9)
+    coords = ref["coords"].copy()
+    coords[:, 0] += 0.9 * (coords[:, 1] ** 2)  # shear the x layers into each other
+    mesh = af.Mesh.from_arrays(ctx, 3, ref["cells"], coords)
+    bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+    assert bsr.stats()["brick_order"] == 0
+    rows, cols, vals = bsr.download()
+    orp, ocols = O.sparsity(ref["n_local"], ref["n_local"], ref["cells"])
+    ovals, _ = O.assemble_poisson(ref["n_local"], ref["cells"], coords, orp, ocols, 5.5)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    _check_values(vals, ovals)
+    # drop the cells of node 0's corner: node 0 is isolated but still a lattice point;
+    # drop node count instead: the last node removed -> layer product != n_rows
+    keep = ~(ref["cells"] == ref["n_local"] - 1).any(axis=1)
+    m2 = af.Mesh.from_arrays(ctx, 3, ref["cells"][keep], ref["coords"][:-1])
+    b2, _ = _assemble_gpu(ctx, m2, 5.5)
+    assert b2.stats()["brick_order"] == 0
 
 
 @pytest.mark.parametrize("dim", [2, 3])

@@ -59,7 +59,7 @@ def test_bar3d_golden_gpu(ctx, bar, preconditioner):
     U, V, A, iters = _replay_gpu(ctx, bar, preconditioner)
     nerr, mx = T.check_golden(bar, U)
     assert nerr == 0
-    assert mx < 5e-9, mx
+    assert mx < 1e-8, mx  # the CPU replay: 1-2e-9 (the golden came from an iterative solve)
     dts = O.passmo_time_steps(T.BAR3D["start"], T.BAR3D["final"], T.BAR3D["dt"])
     Uo, Vo, Ao = O.passmo_newmark(bar.cells, bar.coords, T.BAR3D["lam"], T.BAR3D["mu"], T.BAR3D["rho"], dts,
                                   T.bar3d_imposed(bar), T.BAR3D["penalty"])
