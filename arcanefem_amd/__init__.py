@@ -6,6 +6,7 @@ gfx950 behind the C ABI of include/arcanefem_amd.h (libafem.so, in-tree).
 """
 from ._capi import AfemError, LIB_PATH, load  # noqa: F401
 from .core import (BSRFormat, Communicator, Context, DoFLinearSystem, HipDoFLinearSystemFactory,  # noqa: F401
-                   Mesh, applyNeumannToRhs, device_count, partition_rcb, structured_halo_plan, subdomain_plan)
+                   Mesh, applyNeumannToRhs, device_count, partition_rcb, set_variant, structured_halo_plan,
+                   subdomain_plan)
 
 __version__ = "0.1.0"

@@ -106,6 +106,7 @@ INT = ctypes.c_int
 # name -> argtypes (all return int status, except afem_last_error / afem_version)
 SIGNATURES = {
     "afem_device_count": [ctypes.POINTER(INT)],
+    "afem_set_variant": [ctypes.c_char_p, ctypes.c_char_p],
     "afem_ctx_create": [INT, P, PP],
     "afem_ctx_destroy": [P],
     "afem_ctx_synchronize": [P],

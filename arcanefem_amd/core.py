@@ -23,7 +23,7 @@ from . import _capi as C
 from ._capi import AfemError, call
 
 __all__ = ["AfemError", "Context", "Mesh", "BSRFormat", "DoFLinearSystem", "HipDoFLinearSystemFactory",
-           "applyNeumannToRhs", "device_count", "structured_halo_plan"]
+           "applyNeumannToRhs", "device_count", "set_variant", "structured_halo_plan"]
 
 
 def _ptr(a: np.ndarray):
@@ -54,6 +54,12 @@ def applyNeumannToRhs(mesh: "Mesh", rhs_dptr: int, faces, value, mode: str = "no
     fc = None if face_cells is None else np.ascontiguousarray(face_cells, dtype=np.int32)
     call("afem_apply_neumann", mesh.h, nb_dof, NEUMANN_MODES[mode], _ptr(v), faces.shape[0], _ptr(faces),
          None if fc is None else _ptr(fc), C.AFEM_MEM_HOST, ctypes.c_void_p(rhs_dptr))
+
+
+def set_variant(name: str, value=None):
+    """afem_set_variant: select a kernel variant (diagnostics / A-B runs;
+    include/arcanefem_amd.h lists the knobs); None returns to the default."""
+    call("afem_set_variant", name.encode(), None if value is None else str(value).encode())
 
 
 def device_count() -> int:

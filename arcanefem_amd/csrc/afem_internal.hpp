@@ -25,6 +25,11 @@ struct Error : std::runtime_error {
 
 [[noreturn]] void throw_hip(hipError_t e, const char* expr, const char* file, int line);
 
+// kernel-variant knob `name` (AFEM_*): afem_set_variant's value, else the
+// environment's at first lookup, else nullptr (the default variant)
+const char* variant(const char* name);
+void set_variant(const char* name, const char* value);
+
 #define AFEM_HIP(x)                                              \
   do {                                                           \
     hipError_t e_ = (x);                                         \

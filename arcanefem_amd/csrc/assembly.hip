@@ -2744,7 +2744,7 @@ constexpr int64_t kTileLdsMax = 64 * 1024;
 int occ_override()
 {
   static const int v = [] {
-    const char* e = getenv("AFEM_ASSEMBLY_WAVES_PER_CU");
+    const char* e = variant("AFEM_ASSEMBLY_WAVES_PER_CU");
     return e ? atoi(e) : 0;
   }();
   return v;
@@ -2805,7 +2805,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   // row strips: the default path (AFEM_ASSEMBLY_STRIPS=0 selects the
   // per-cell incidence kernel, a diagnostic)
   static const bool strips_env = [] {
-    const char* e = getenv("AFEM_ASSEMBLY_STRIPS");
+    const char* e = variant("AFEM_ASSEMBLY_STRIPS");
     return !(e && atoi(e) == 0);
   }();
   if (strips_env && s.strip_ok && s.rec_ok && s.nnz < (int64_t(1) << 32) && s.max_strip_c <= 4 &&
@@ -2816,7 +2816,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
     const size_t shm_u = (size_t)(8 * 64 * (int64_t)s.max_slice_w + strip_coord_bytes(dimc, s.max_slice_nodes, s.max_slice_w));
     static std::map<std::pair<const void*, size_t>, int> occ_s;
     // AFEM_ASSEMBLY_UNIFORM=0: every slice through the general variant (diagnostic)
-    const char* ue = getenv("AFEM_ASSEMBLY_UNIFORM");  // read per call: the parity test toggles it
+    const char* ue = variant("AFEM_ASSEMBLY_UNIFORM");  // read per call: the parity test toggles it
     const int umode = ue ? atoi(ue) : 1;               // 0 off, 1 branches, 2 selects
     const bool uni_env = umode != 0;
     const bool use_uni = uni_env && s.n_uni > 0;
@@ -2858,14 +2858,14 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       // stencil split (AFEM_ASSEMBLY_STENCIL=0: the whole uniform list through the
       // uniform instance, diagnostic): the signature's slices on the context
       // stream, the other uniform slices through the uniform instance beside them
-      const char* ke = getenv("AFEM_ASSEMBLY_STENCIL");  // read per call: the parity test toggles it
+      const char* ke = variant("AFEM_ASSEMBLY_STENCIL");  // read per call: the parity test toggles it
       const bool use_k = has_u && umode == 1 && s.n_k > 0 && !(ke && atoi(ke) == 0);
       // with the stencil split every list runs on the context stream, the small
       // ones first: beside the stencil kernel's persistent grid a side-stream
       // launch only gets CUs as its waves retire (its kernel time stretches to
       // the whole assembly), one after the other the kernel times add up to the
       // assembly time (AFEM_ASSEMBLY_SIDE=1: side stream, diagnostic)
-      const char* se = getenv("AFEM_ASSEMBLY_SIDE");
+      const char* se = variant("AFEM_ASSEMBLY_SIDE");
       const bool serial_k = use_k && !(se && atoi(se) == 1);
       const bool fork = !serial_k && ((has_u && (s.n_ms > 0 || s.n_mb > 0 || (use_k && s.n_ur > 0))) ||
                                       (!has_u && s.n_ms > 0 && s.n_mb > 0));
@@ -3035,7 +3035,7 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
   const bool big_ok = s.strip_ok && s.rec_ok && s.max_strip_c <= 4 && s.max_slice_w <= 32 &&
                       shm_big <= 160 * 1024 && s.nnz * 9 < (int64_t(1) << 40);
   const bool fits_small = s.strip_ok && s.max_slice_w <= 16 && shm_old <= 160 * 1024;
-  const char* be = getenv("AFEM_ELAST_BIG");  // 0: the global kernel instead (diagnostic)
+  const char* be = variant("AFEM_ELAST_BIG");  // 0: the global kernel instead (diagnostic)
   if (!fits_small && big_ok && !(be && atoi(be) == 0)) {
     // three lists (sparsity.hip): uniform and compact slices (<= 16 slots, <= 32
     // steps, <= 352 nodes) through the <2, 16> instance with a tile sized by
@@ -3104,17 +3104,17 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
     return;
   }
   // one workgroup (three waves) per slice (AFEM_ELAST_WG=0: one wave per (slice, component), diagnostic)
-  const char* we = getenv("AFEM_ELAST_WG");
+  const char* we = variant("AFEM_ELAST_WG");
   const bool use_wg = !(we && atoi(we) == 0);
   const int64_t ucap2 = (s.max_slice_nodes + 1) & ~int64_t(1);  // 16-B aligned column-index table
   if (use_wg && s.rec_ok && s.max_strip_c <= 2 && s.max_slice_w <= 16 && s.max_slice_nodes <= 256 &&
       s.nnz * 9 < (int64_t(1) << 40) && elast_wg_bytes(ucap2, s.max_slice_w) <= 160 * 1024) {
     const size_t shm = (size_t)elast_wg_bytes(ucap2, s.max_slice_w);
     static std::map<std::pair<const void*, size_t>, int> occ_wg;
-    const char* ue = getenv("AFEM_ASSEMBLY_UNIFORM");
+    const char* ue = variant("AFEM_ASSEMBLY_UNIFORM");
     const bool use_uni = !(ue && atoi(ue) == 0) && s.n_uni > 0;
     // stencil split (AFEM_ASSEMBLY_STENCIL=0: the whole uniform list through the uniform instance)
-    const char* ke = getenv("AFEM_ASSEMBLY_STENCIL");
+    const char* ke = variant("AFEM_ASSEMBLY_STENCIL");
     const bool use_k = use_uni && s.n_k0 > 0 && !(ke && atoi(ke) == 0);
     if (s.tickets.n < 4 * 8 * 16) s.tickets.alloc(4 * 8 * 16);
     AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
@@ -3153,14 +3153,14 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
   }
   // persistent pipelined kernel, one wave per (slice, component) (AFEM_ELAST_STRIP=0: the
   // one-wave-per-item kernel, diagnostic)
-  const char* ee = getenv("AFEM_ELAST_STRIP");
+  const char* ee = variant("AFEM_ELAST_STRIP");
   const bool use_new = !(ee && atoi(ee) == 0);
   if (use_new && s.rec_ok && s.max_strip_c <= 2 && s.max_slice_w <= 16 && s.max_slice_nodes <= 256 &&
       s.nnz * 9 < (int64_t(1) << 40)) {
     const size_t shm2 = (size_t)elast_tile_bytes(s.max_slice_nodes, s.max_slice_w);
     static std::map<std::pair<const void*, size_t>, int> occ;
     // AFEM_ASSEMBLY_UNIFORM=0: every slice through the general instance (diagnostic)
-    const char* ue = getenv("AFEM_ASSEMBLY_UNIFORM");
+    const char* ue = variant("AFEM_ASSEMBLY_UNIFORM");
     const bool use_uni = !(ue && atoi(ue) == 0) && s.n_uni > 0;
     if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);
     AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));

@@ -8,6 +8,8 @@
 #include <string>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "afem_internal.hpp"
 
 using namespace afem;
@@ -30,6 +32,16 @@ int fail(int code, const char* msg)
   catch (const std::exception& e) { return fail(AFEM_ERR_ARG, e.what()); } \
   catch (...) { return fail(AFEM_ERR_ARG, "unknown exception"); } \
   return AFEM_OK;
+
+// roctx range over an entry point (the reference's Accelerator::ProfileRegion /
+// [ArcaneFem-Timer] phases): visible in rocprofv3 --marker-trace
+struct RoctxRange {
+  explicit RoctxRange(const char* m) { roctxRangePushA(m); }
+  ~RoctxRange() { roctxRangePop(); }
+  RoctxRange(const RoctxRange&) = delete;
+  RoctxRange& operator=(const RoctxRange&) = delete;
+};
+#define AFEM_RANGE(name) RoctxRange afem_range_(name)
 
 #define NOT_NULL(p) AFEM_REQUIRE((p) != nullptr, AFEM_ERR_ARG, #p " must not be NULL")
 
@@ -98,6 +110,15 @@ extern "C" {
 
 const char* afem_last_error(void) { return g_last_error.c_str(); }
 int afem_version(void) { return 100; }
+
+int afem_set_variant(const char* name, const char* value)
+{
+  API_BEGIN
+  NOT_NULL(name);
+  AFEM_REQUIRE(strncmp(name, "AFEM_", 5) == 0, AFEM_ERR_ARG, "afem_set_variant: knob names start with AFEM_");
+  afem::set_variant(name, value);
+  API_END
+}
 
 int afem_device_count(int* count)
 {
@@ -457,6 +478,7 @@ int afem_bsr_create(afem_mesh* mesh, int nb_dof, int use_csr, afem_bsr** out)
 int afem_bsr_compute_sparsity(afem_bsr* b)
 {
   API_BEGIN
+  AFEM_RANGE("afem: BSRFormat::computeSparsity");
   NOT_NULL(b);
   b->mesh->ctx->set_device();
   b->has_sparsity = false;
@@ -481,6 +503,7 @@ int afem_bsr_assemble_poisson_p1(afem_bsr* b, double coef, double f, double* rhs
 int afem_bsr_assemble_poisson_p1_ex(afem_bsr* b, double coef, double f, double* rhs, int rhs_mode)
 {
   API_BEGIN
+  AFEM_RANGE("afem: BSRFormat::assembleBilinear (Poisson P1)");
   NOT_NULL(b);
   AFEM_REQUIRE(b->has_sparsity, AFEM_ERR_STATE, "assembleBilinear called before computeSparsity");
   AFEM_REQUIRE(rhs_mode == AFEM_RHS_ADD || rhs_mode == AFEM_RHS_SET, AFEM_ERR_ARG, "unknown rhs_mode");
@@ -506,6 +529,7 @@ int afem_bsr_assemble_elasticity_p1_ex(afem_bsr* b, double lambda, double mu2, d
                                        double* rhs, int rhs_mode)
 {
   API_BEGIN
+  AFEM_RANGE("afem: BSRFormat::assembleBilinear (elasticity P1)");
   NOT_NULL(b);
   AFEM_REQUIRE(b->has_sparsity, AFEM_ERR_STATE, "assembleBilinear called before computeSparsity");
   AFEM_REQUIRE(b->mesh->nv == 4 && b->nb_dof == 3, AFEM_ERR_NOT_IMPL,
@@ -1045,6 +1069,7 @@ int afem_apply_neumann(afem_mesh* mesh, int nb_dof, int mode, const double value
 int afem_ls_apply_boundary_conditions(afem_ls* ls)
 {
   API_BEGIN
+  AFEM_RANGE("afem: applyBoundaryConditions");
   NOT_NULL(ls);
   ls->ctx->set_device();
   if (!ls->has_csr && (!ls->add_map.empty() || !ls->set_map.empty())) ls_build_from_host_coo(*ls);
@@ -1082,6 +1107,7 @@ int afem_ls_clear_values(afem_ls* ls)
 int afem_ls_solve(afem_ls* ls, afem_solve_stats* st)
 {
   API_BEGIN
+  AFEM_RANGE("afem: DoFLinearSystem::solve");
   NOT_NULL(ls);
   if (ls->hv_vals && ls->has_csr && !ls->csr_from_coo && ls->csr_nnz > 0) {
     // host view: the values as they are now (the module may have edited its
@@ -1170,6 +1196,7 @@ int afem_elastodynamics_set_solver_options(afem_elastodynamics* h, const afem_so
 int afem_elastodynamics_step(afem_elastodynamics* h, afem_solve_stats* st)
 {
   API_BEGIN
+  AFEM_RANGE("afem: elastodynamics step");
   NOT_NULL(h);
   dyn_step(h->d, st);
   API_END

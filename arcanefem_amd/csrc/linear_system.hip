@@ -1195,7 +1195,7 @@ SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows, const int32_t*
   pl.nblocks = nb;
   // AFEM_SPMV=stream (scalar-load stream) / v16 (16 lanes per row) / s4 (no unrolling): diagnostics
   const int mode = [] {  // read per plan (tools/cg_probe.py toggles it in one process)
-    const char* e = getenv("AFEM_SPMV");
+    const char* e = variant("AFEM_SPMV");
     if (e && std::string(e) == "stream") return 1;
     if (e && std::string(e) == "v16") return 2;
     if (e && std::string(e) == "s4") return 3;
@@ -1258,7 +1258,7 @@ namespace {
 SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
 {
   SpmvPlan pl = plan_spmv(ctx, ls.csr_rows, ls.n_rows, ls.csr_cols, ls.csr_vals);
-  const char* e = getenv("AFEM_SPMV");
+  const char* e = variant("AFEM_SPMV");
   // the pattern SpMV: the default for scalar systems (AFEM_SPMV=nopat or any other
   // diagnostic mode: the CSR kernels as they are)
   if ((!e || std::string(e) == "pat") && ls.blk_k <= 1 && ls.n_rows > 64 && ls.csr_cols && ls.csr_vals &&
@@ -1739,6 +1739,52 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     }
     n_int = ls.blist_nint;
   }
+  // the part of an iteration after the SpMV (with_spmv: the whole iteration,
+  // for the captured graph of the single-rank, non-split path)
+  auto rest_of_iteration = [&](int par, bool with_spmv) {
+    if (with_spmv)
+      launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p, ls.csr_nnz);
+    reduce_to(ctx, ls.partial.p, pl.nblocks, scal + 2);
+    if (comm) comm_allreduce(comm, ctx, scal + 2, 1);
+    if (use_mg) {
+      hipLaunchKernelGGL(k_cg_xr, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p, ls.r.p,
+                         ls.q.p);
+      AFEM_LAUNCHED();
+      mg_apply(ls, ls.r.p, ls.z.p);
+      hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.r.p, ls.z.p, ls.partial.p);
+      AFEM_LAUNCHED();
+    }
+    else if (blk3)
+      hipLaunchKernelGGL(k_cg_update_b3, dim3(vb3), dim3(kThreads), 0, ctx.stream, nb3, scal, par, ls.sol.p, ls.p.p,
+                         ls.r.p, ls.q.p, ls.z.p, ls.binv.p, ls.partial.p);
+    else
+      hipLaunchKernelGGL(k_cg_update_rz, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.r.p, ls.q.p,
+                         ls.z.p, ls.dinv.p, ls.partial.p);
+    AFEM_LAUNCHED();
+    reduce_to(ctx, ls.partial.p, blk3 ? vb3 : vb, scal + (par ^ 1));
+    if (comm) comm_allreduce(comm, ctx, scal + (par ^ 1), 1);
+    if (use_mg || blk3)
+      hipLaunchKernelGGL(k_cg_dir, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.z.p, ls.p.p);
+    else
+      hipLaunchKernelGGL(k_cg_dir_x, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.z.p, ls.p.p);
+    AFEM_LAUNCHED();
+  };
+  // graph replay of whole iterations (single rank, no split SpMV, no
+  // multigrid: every launch of an iteration is a plain kernel), in batches of
+  // the convergence-check period (even: the ping-pong parity of the scalars
+  // repeats); AFEM_CG_GRAPH=0 launches every kernel (diagnostics)
+  const char* cgg = variant("AFEM_CG_GRAPH");
+  const int gbatch = fixed ? 16 : check;
+  const bool graph = !multi && !use_mg && !comm && !overlap && (gbatch % 2) == 0 && gbatch >= 2 &&
+                     !(cgg && atoi(cgg) == 0);
+  hipGraphExec_t gexec = nullptr;
+  struct GraphGuard {
+    hipGraphExec_t& g;
+    ~GraphGuard()
+    {
+      if (g) (void)hipGraphExecDestroy(g);
+    }
+  } graph_guard{ gexec };
   while (!converged && it < max_it) {
     const int par = it & 1;
     if (overlap) {
@@ -1768,36 +1814,29 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
       halo_end(*ls.halo, ctx, ls.p.p);
       part(n_bd, n_int);
     }
+    else if (graph && (it & 1) == 0 && it + gbatch <= max_it) {
+      // single rank: `gbatch` whole iterations replayed as one captured graph
+      if (!gexec) {
+        hipGraph_t g = nullptr;
+        AFEM_HIP(hipStreamBeginCapture(ctx.stream, hipStreamCaptureModeThreadLocal));
+        for (int b = 0; b < gbatch; ++b) rest_of_iteration(b & 1, true);
+        AFEM_HIP(hipStreamEndCapture(ctx.stream, &g));
+        const hipError_t e = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        AFEM_HIP(e);
+      }
+      AFEM_HIP(hipGraphLaunch(gexec, ctx.stream));
+      it += gbatch - 1;  // the last one is counted below
+      ++it;
+      goto checked;
+    }
     else {
       if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
       launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p, ls.csr_nnz);
     }
-
-    reduce_to(ctx, ls.partial.p, pl.nblocks, scal + 2);
-    if (comm) comm_allreduce(comm, ctx, scal + 2, 1);
-    if (use_mg) {
-      hipLaunchKernelGGL(k_cg_xr, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p, ls.r.p,
-                         ls.q.p);
-      AFEM_LAUNCHED();
-      mg_apply(ls, ls.r.p, ls.z.p);
-      hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.r.p, ls.z.p, ls.partial.p);
-      AFEM_LAUNCHED();
-    }
-    else if (blk3)
-      hipLaunchKernelGGL(k_cg_update_b3, dim3(vb3), dim3(kThreads), 0, ctx.stream, nb3, scal, par, ls.sol.p, ls.p.p,
-                         ls.r.p, ls.q.p, ls.z.p, ls.binv.p, ls.partial.p);
-    else
-      hipLaunchKernelGGL(k_cg_update_rz, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.r.p, ls.q.p,
-                         ls.z.p, ls.dinv.p, ls.partial.p);
-    AFEM_LAUNCHED();
-    reduce_to(ctx, ls.partial.p, blk3 ? vb3 : vb, scal + (par ^ 1));
-    if (comm) comm_allreduce(comm, ctx, scal + (par ^ 1), 1);
-    if (use_mg || blk3)
-      hipLaunchKernelGGL(k_cg_dir, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.z.p, ls.p.p);
-    else
-      hipLaunchKernelGGL(k_cg_dir_x, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.z.p, ls.p.p);
-    AFEM_LAUNCHED();
+    rest_of_iteration(par, false);
     ++it;
+  checked:
     if (!fixed && (it % check == 0 || it == max_it)) {
       AFEM_HIP(hipMemcpyAsync(ls.pinned, scal, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
       ctx.sync();

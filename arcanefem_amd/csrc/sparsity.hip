@@ -1155,7 +1155,7 @@ void build_structure(Mesh& m, Structure& s)
     AFEM_REQUIRE(ax * ay * az == n_rows, AFEM_ERR_STATE, "structured mesh: owned node box does not match n_own");
     const int bx = st.dim == 3 ? 4 : 8, bz = st.dim == 3 ? 4 : 1;
     // AFEM_BRICKS=plain: the plain 4x4x4 brick grid over the whole box (diagnostic)
-    const char* be = getenv("AFEM_BRICKS");
+    const char* be = variant("AFEM_BRICKS");
     const bool boundary_aware = st.dim == 3 && !(be && std::string(be) == "plain");
     if (boundary_aware) {
       const FaceTiles F = face_tiles(ax, ay, az);
@@ -1186,12 +1186,12 @@ void build_structure(Mesh& m, Structure& s)
     }
     s.brick_order = true;
   }
-  else if (!(nv == 4 && m.dim == 3 && n_rows >= 8 && !getenv("AFEM_ORDER") && lattice_order(ctx, m, n_rows, s))) {
+  else if (!(nv == 4 && m.dim == 3 && n_rows >= 8 && !variant("AFEM_ORDER") && lattice_order(ctx, m, n_rows, s))) {
     s.n_slices = (n_rows + 63) / 64;
     s.perm.alloc(s.n_slices * 64);
     // AFEM_ORDER=node: the caller's node order; =morton: Morton curve; =hilbert:
     // the Hilbert curve even for a lattice (diagnostics)
-    const char* oe = getenv("AFEM_ORDER");
+    const char* oe = variant("AFEM_ORDER");
     const bool node_order = (oe && std::string(oe) == "node") || n_rows < 2;
     if (node_order) {
       hipLaunchKernelGGL(k_perm_identity, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream,
@@ -1347,7 +1347,7 @@ void build_structure(Mesh& m, Structure& s)
                          s.spat.p, sslot.p);
       AFEM_LAUNCHED();
       // LDS-bank-aware node placement of the uniform slices (AFEM_BANK_PLACE=0: sorted order, diagnostic)
-      const char* bpe = getenv("AFEM_BANK_PLACE");
+      const char* bpe = variant("AFEM_BANK_PLACE");
       if (!(bpe && atoi(bpe) == 0) && nv == 4) {
         DevBuf<uint8_t> q_of_u;
         q_of_u.alloc(s.n_slices * 256);
@@ -1355,7 +1355,7 @@ void build_structure(Mesh& m, Structure& s)
         nu_new.alloc(s.n_slices);
         // positions < maxq: 232 keeps the uniform instance's LDS image at 13.3 KB per wave
         // (12 waves per CU with 15 slots); classes c < 8 get 8 positions, the others 7
-        const char* bpm = getenv("AFEM_BANK_PLACE_MAX");
+        const char* bpm = variant("AFEM_BANK_PLACE_MAX");
         const int maxq = bpm ? std::max(64, std::min(256, atoi(bpm))) : 232;
         hipLaunchKernelGGL(k_bank_place, dim3((unsigned)s.n_slices), dim3(64), 0, ctx.stream, s.n_slices, uflag.p,
                            s.perm.p, s.snode_ptr.p, s.strip_u.p, s.strip_ptr.p, s.strip_n.p, s.pos_dl.p, q_of_u.p,
@@ -1528,7 +1528,7 @@ void build_structure(Mesh& m, Structure& s)
       }
       upload(s.rec_m, rm);
       upload(s.rec_all, ra);
-      if (getenv("AFEM_DEBUG_SLICES")) {  // diagnostic: slice node counts and widths
+      if (variant("AFEM_DEBUG_SLICES")) {  // diagnostic: slice node counts and widths
         std::vector<int64_t> nus(ns);
         for (size_t i = 0; i < ns; ++i) nus[i] = hsn[i + 1] - hsn[i];
         std::sort(nus.begin(), nus.end());
@@ -1538,7 +1538,7 @@ void build_structure(Mesh& m, Structure& s)
         fprintf(stderr, "afem slices %zu nodes p50 %lld p90 %lld p99 %lld max %lld | width p50 %lld p90 %lld max %lld\n",
                 ns, q(nus, 0.5), q(nus, 0.9), q(nus, 0.99), q(nus, 1.0), q(ws, 0.5), q(ws, 0.9), q(ws, 1.0));
       }
-      if (getenv("AFEM_DEBUG_PATTERNS")) {  // diagnostic: strip patterns of the uniform slices
+      if (variant("AFEM_DEBUG_PATTERNS")) {  // diagnostic: strip patterns of the uniform slices
         std::map<std::pair<uint64_t, int>, int64_t> h;
         std::map<std::string, int64_t> hs2;  // pattern + steps + slot stream
         for (size_t i = 0; i < ru.size(); ++i) {

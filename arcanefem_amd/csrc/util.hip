@@ -6,8 +6,52 @@
 #include <algorithm>
 #include <climits>
 #include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <string>
 
 namespace afem {
+
+// Kernel-variant knobs (diagnostics and A/B measurements): an
+// explicit override (afem_set_variant) wins, else the process environment as
+// it was the first time the knob was looked up; unset = the default variant.
+namespace {
+struct Variants {
+  std::mutex mu;
+  std::map<std::string, std::string> set;          // afem_set_variant
+  std::map<std::string, std::pair<bool, std::string>> env;  // first lookup of the environment
+};
+Variants& variants()
+{
+  static Variants v;
+  return v;
+}
+}  // namespace
+
+const char* variant(const char* name)
+{
+  Variants& v = variants();
+  std::lock_guard<std::mutex> g(v.mu);
+  auto it = v.set.find(name);
+  if (it != v.set.end()) return it->second.c_str();
+  auto e = v.env.find(name);
+  if (e == v.env.end()) {
+    const char* x = getenv(name);
+    e = v.env.emplace(name, std::make_pair(x != nullptr, std::string(x ? x : ""))).first;
+  }
+  return e->second.first ? e->second.second.c_str() : nullptr;
+}
+
+void set_variant(const char* name, const char* value)
+{
+  Variants& v = variants();
+  std::lock_guard<std::mutex> g(v.mu);
+  if (value)
+    v.set[name] = value;
+  else
+    v.set.erase(name);
+}
 
 void throw_hip(hipError_t e, const char* expr, const char* file, int line)
 {

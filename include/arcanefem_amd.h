@@ -64,6 +64,18 @@ typedef struct afem_comm afem_comm; /* RCCL communicator (IParallelMng subset) *
 const char* afem_last_error(void);
 int afem_version(void); /* major*10000 + minor*100 + patch */
 int afem_device_count(int* count);
+/* Kernel-variant knobs, for diagnostics and A/B measurements:
+ * name "AFEM_*", value a string, NULL to return to the default.  Knobs:
+ * AFEM_ASSEMBLY_STENCIL / _UNIFORM / _STRIPS / _SIDE / _WAVES_PER_CU,
+ * AFEM_ELAST_WG / _STRIP / _BIG (assembly instances), AFEM_SPMV (CG SpMV),
+ * AFEM_CG_GRAPH (0: no graph replay of the single-rank CG iterations),
+ * AFEM_ORDER / AFEM_BRICKS / AFEM_BANK_PLACE / _MAX (structure build),
+ * AFEM_DEBUG_SLICES / _PATTERNS (stderr dumps).  Without an explicit value a
+ * knob takes the process environment's value at its first use; unset means
+ * the default variant, which is what every result in DESIGN.md used.  The
+ * variant that ran is reported (afem_bsr_stats.last_kernel,
+ * afem_solve_stats.spmv_kernel); every variant gives the oracle's values. */
+int afem_set_variant(const char* name, const char* value);
 
 /* ---------------------------------------------------------------- context */
 /* hip_stream may be NULL: the context then creates and owns a non-blocking

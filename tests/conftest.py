@@ -23,3 +23,21 @@ def ctx():
     c = af.Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture
+def variant():
+    """Select kernel variants (afem_set_variant) for one test; every knob set
+    through it returns to the default at teardown.  variant(name, None)
+    returns one knob to the default at once."""
+    import arcanefem_amd as af
+
+    used = set()
+
+    def set_(name, value):
+        used.add(name)
+        af.set_variant(name, value)
+
+    yield set_
+    for n in used:
+        af.set_variant(n, None)

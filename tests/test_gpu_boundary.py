@@ -458,10 +458,10 @@ def test_fan_mesh_scalar_fallbacks(ctx, dim, m, kern):
 @pytest.mark.parametrize("m,kern,env", [(40, K_E3_GLOBAL, None), (31, K_E3_GLOBAL, None), (12, K_E3_WG, None),
                                         (12, K_E3_STRIP, "AFEM_ELAST_WG"), (12, K_E3_ITEM, "AFEM_ELAST_STRIP")])
 @pytest.mark.parametrize("use_csr", [False, True])
-def test_fan_mesh_block3_fallback(ctx, monkeypatch, m, kern, env, use_csr):
+def test_fan_mesh_block3_fallback(ctx, variant, m, kern, env, use_csr):
     if env:  # the alternative kernels, forced
-        monkeypatch.setenv("AFEM_ELAST_WG", "0")
-        monkeypatch.setenv(env, "0")
+        variant("AFEM_ELAST_WG", "0")
+        variant(env, "0")
     cells, coords = fan_mesh_3d(m, seed=2)
     n = coords.shape[0]
     mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)

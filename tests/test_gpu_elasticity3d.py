@@ -2,10 +2,12 @@
 LHS form c0*M + K (config C5): the HIP kernel through the C ABI against the
 oracle's restatement (oracle/oracle.c orc_assemble_elasticity_tet).
 
-No reference module assembles 3D elasticity, so parity is
-against the oracle restatement of the reference's 2D element
-(modules/elasticity/FemModule.h:112-140) lifted to 3D; the restatement itself
-is pinned by known answers in tests/test_oracle_elasticity3d.py.
+Parity is against the oracle restatement (the reference's 2D element,
+modules/elasticity/FemModule.h:112-140, in 3D), which is pinned by the
+reference's own 3D case: passmo's Gauss-point element equals it to 1e-13 and
+its Newmark replay meets the bar3d-tetra golden (tests/test_oracle_passmo.py;
+the same replay through libafem: tests/test_gpu_passmo.py), plus the known
+answers of tests/test_oracle_elasticity3d.py.
 Tolerance: |gpu - oracle| <= 1e-12 * max|oracle| per entry.
 """
 import numpy as np
@@ -66,7 +68,7 @@ def test_elasticity3d_assembly_parity(ctx, which, use_csr, c0, force):
 
 
 @pytest.mark.parametrize("use_csr", [False, True])
-def test_elasticity3d_uniform_variant_bitwise(ctx, monkeypatch, use_csr):
+def test_elasticity3d_uniform_variant_bitwise(ctx, variant, use_csr):
     mesh = _mesh(ctx, "bigbox")
     bsr = af.BSRFormat(mesh, 3).initialize(use_csr)
     bsr.computeSparsity()
@@ -75,7 +77,7 @@ def test_elasticity3d_uniform_variant_bitwise(ctx, monkeypatch, use_csr):
     drhs = ctx.malloc(8 * n3)
     bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
     v_uni, r_uni = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
-    monkeypatch.setenv("AFEM_ASSEMBLY_UNIFORM", "0")
+    variant("AFEM_ASSEMBLY_UNIFORM", "0")
     bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
     v_gen, r_gen = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
     ctx.free(drhs)
@@ -85,7 +87,7 @@ def test_elasticity3d_uniform_variant_bitwise(ctx, monkeypatch, use_csr):
 
 @pytest.mark.parametrize("n", [13, 22])
 @pytest.mark.parametrize("use_csr", [False, True])
-def test_elasticity3d_stencil_instance_bitwise(ctx, monkeypatch, n, use_csr):
+def test_elasticity3d_stencil_instance_bitwise(ctx, variant, n, use_csr):
     """Interior bricks (compiled-in signature 0) run the workgroup kernel's
     stencil instance (step bytes and shift/swap arms as constants): the same
     bits as the uniform instance (AFEM_ASSEMBLY_STENCIL=0) and the oracle's
@@ -100,7 +102,7 @@ def test_elasticity3d_stencil_instance_bitwise(ctx, monkeypatch, n, use_csr):
     bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
     assert bsr.stats()["last_kernel"] == 8
     v_k, r_k = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
-    monkeypatch.setenv("AFEM_ASSEMBLY_STENCIL", "0")
+    variant("AFEM_ASSEMBLY_STENCIL", "0")
     bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
     rows, cols, v_u = bsr.download()
     r_u = ctx.to_host(drhs, n3, np.float64)
@@ -119,7 +121,7 @@ def test_elasticity3d_stencil_instance_bitwise(ctx, monkeypatch, n, use_csr):
 
 @pytest.mark.parametrize("which", ["bigbox", "box"])
 @pytest.mark.parametrize("use_csr", [False, True])
-def test_elasticity3d_workgroup_kernel_bitwise(ctx, monkeypatch, which, use_csr):
+def test_elasticity3d_workgroup_kernel_bitwise(ctx, variant, which, use_csr):
     """The three-wave-per-slice kernel (k_assemble_elast_wg) against the
     one-wave-per-(slice, component) kernel: the same arithmetic per entry (up
     to the compiler's FMA contraction: last-bit differences)."""
@@ -131,7 +133,7 @@ def test_elasticity3d_workgroup_kernel_bitwise(ctx, monkeypatch, which, use_csr)
     bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
     assert bsr.stats()["last_kernel"] == 8
     v_wg, r_wg = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
-    monkeypatch.setenv("AFEM_ELAST_WG", "0")
+    variant("AFEM_ELAST_WG", "0")
     bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
     assert bsr.stats()["last_kernel"] == 4
     v_st, r_st = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
@@ -145,7 +147,7 @@ def test_elasticity3d_workgroup_kernel_bitwise(ctx, monkeypatch, which, use_csr)
 
 @pytest.mark.parametrize("levels", [2, 3])
 @pytest.mark.parametrize("use_csr", [False, True])
-def test_elasticity3d_unstructured_refined(ctx, monkeypatch, levels, use_csr):
+def test_elasticity3d_unstructured_refined(ctx, variant, levels, use_csr):
     """An unstructured mesh (the reference's L-shape-3D refined `levels` times:
     irregular valences, rows longer than 16, Hilbert slices beyond 256 nodes at
     3 levels) through the block-3 kernel for such meshes (AFEM_KERNEL_ELAST3_BIG)
@@ -173,9 +175,9 @@ def test_elasticity3d_unstructured_refined(ctx, monkeypatch, levels, use_csr):
     assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
     assert np.abs(vals - ovals).max() <= VAL_TOL * np.abs(ovals).max()
     assert np.abs(rhs - orhs).max() <= VAL_TOL * np.abs(orhs).max()
-    monkeypatch.setenv("AFEM_ELAST_BIG", "0")
-    monkeypatch.setenv("AFEM_ELAST_WG", "0")
-    monkeypatch.setenv("AFEM_ELAST_STRIP", "0")
+    variant("AFEM_ELAST_BIG", "0")
+    variant("AFEM_ELAST_WG", "0")
+    variant("AFEM_ELAST_STRIP", "0")
     bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
     _, _, gvals = bsr.download()
     ctx.free(drhs)
@@ -319,11 +321,11 @@ def _blocks(rows, vals, k, use_csr):
 @pytest.mark.parametrize("which", ["box", "slab", "lshape", "tri"])
 @pytest.mark.parametrize("use_csr", [False, True])
 @pytest.mark.parametrize("spmv", ["blk", "csr"])
-def test_block_spmv_matches_block_product(ctx, monkeypatch, which, use_csr, spmv):
+def test_block_spmv_matches_block_product(ctx, variant, which, use_csr, spmv):
     # the node-block SpMV (k_spmv_blk: node columns instead of scalar ones)
     # and the scalar CSR kernels (AFEM_SPMV=v16) against the block product
     if spmv == "csr":
-        monkeypatch.setenv("AFEM_SPMV", "v16")
+        variant("AFEM_SPMV", "v16")
     k = 2 if which == "tri" else 3
     mesh = af.Mesh.structured(ctx, 2, 21, seed=3) if which == "tri" else _mesh(ctx, which)
     bsr = af.BSRFormat(mesh, k).initialize(use_csr)

@@ -98,7 +98,7 @@ def test_assembly_bitwise_reproducible(ctx):
         assert np.array_equal(r1, ls.rhs_host())
 
 
-def test_uniform_strip_variant(ctx, monkeypatch):
+def test_uniform_strip_variant(ctx, variant):
     # interior 4x4x4 bricks of a structured box share one strip topology and
     # run the uniform-control kernel; it must give the general kernel's bits
     # and match the oracle
@@ -108,7 +108,7 @@ def test_uniform_strip_variant(ctx, monkeypatch):
     assert st["brick_order"] == 1 and 0 < st["uniform_slices"] < st["n_slices"]
     _, _, v_uni = bsr.download()
     r_uni = ls.rhs_host()
-    monkeypatch.setenv("AFEM_ASSEMBLY_UNIFORM", "0")
+    variant("AFEM_ASSEMBLY_UNIFORM", "0")
     bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
     rows, cols, v_gen = bsr.download()
     assert np.array_equal(v_uni, v_gen), "uniform and general strip kernels differ"
@@ -122,7 +122,7 @@ def test_uniform_strip_variant(ctx, monkeypatch):
 
 
 @pytest.mark.parametrize("n", [23, 40])
-def test_stencil_instance_bitwise(ctx, monkeypatch, n):
+def test_stencil_instance_bitwise(ctx, variant, n):
     """Interior bricks of a Kuhn box match the compiled-in strip signature
     (stencil_sigs.inc) and run k_assemble_stencil (register accumulators): the
     same bits as the uniform instance (AFEM_ASSEMBLY_STENCIL=0) and the general
@@ -134,12 +134,12 @@ def test_stencil_instance_bitwise(ctx, monkeypatch, n):
     assert st["stencil_sig"] == 0 and 0 < st["stencil_slices"] <= st["uniform_slices"]
     _, _, v_k = bsr.download()
     r_k = ls.rhs_host()
-    monkeypatch.setenv("AFEM_ASSEMBLY_STENCIL", "0")
+    variant("AFEM_ASSEMBLY_STENCIL", "0")
     bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
     _, _, v_uni = bsr.download()
     assert np.array_equal(v_k, v_uni), f"stencil and uniform instances differ in {np.count_nonzero(v_k != v_uni)} values"
     assert np.array_equal(r_k, ls.rhs_host())
-    monkeypatch.setenv("AFEM_ASSEMBLY_UNIFORM", "0")
+    variant("AFEM_ASSEMBLY_UNIFORM", "0")
     bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
     rows, cols, v_gen = bsr.download()
     assert np.array_equal(v_k, v_gen)
@@ -392,7 +392,7 @@ def test_spmv_matches_oracle(ctx):
 
 @pytest.mark.parametrize("dim,n", [(3, 12), (2, 40)])
 @pytest.mark.parametrize("order", ["default", "hilbert", "morton", "node"])
-def test_random_node_permutation(ctx, monkeypatch, dim, n, order):
+def test_random_node_permutation(ctx, variant, dim, n, order):
     # SURVEY §8d robustness variant: the structured mesh with a seeded random
     # node and cell numbering, handed over as arrays.  Default: a 3D mesh whose
     # owned nodes sit on a lattice gets the brick order of that lattice
@@ -412,7 +412,7 @@ def test_random_node_permutation(ctx, monkeypatch, dim, n, order):
     coords[p] = ref["coords"]
     mesh = af.Mesh.from_arrays(ctx, dim, cells, coords)
     if order != "default":
-        monkeypatch.setenv("AFEM_ORDER", order)
+        variant("AFEM_ORDER", order)
     bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
     st = bsr.stats()
     if order == "default" and dim == 3:
@@ -423,15 +423,15 @@ def test_random_node_permutation(ctx, monkeypatch, dim, n, order):
     else:
         assert st["brick_order"] == 0
     if order != "default":
-        monkeypatch.delenv("AFEM_ORDER")
+        variant("AFEM_ORDER", None)
     if order != "node":
         # the curve sort / brick order ran: a slice's rows are spatial
         # neighbours, so it couples to far fewer distinct nodes than 64 random
         # rows would
         m2 = af.Mesh.from_arrays(ctx, dim, cells, coords)
-        monkeypatch.setenv("AFEM_ORDER", "node")
+        variant("AFEM_ORDER", "node")
         b2, _ = _assemble_gpu(ctx, m2, 5.5)
-        monkeypatch.delenv("AFEM_ORDER")
+        variant("AFEM_ORDER", None)
         assert st["max_slice_nodes"] < 0.6 * b2.stats()["max_slice_nodes"]
     rows, cols, vals = bsr.download()
     orp, ocols = O.sparsity(nn, nn, cells)
@@ -607,7 +607,7 @@ def test_initial_guess_current_solution(ctx):
 
 
 @pytest.mark.parametrize("n", [9, 30])
-def test_pattern_spmv(ctx, monkeypatch, n):
+def test_pattern_spmv(ctx, variant, n):
     """The pattern-compressed SpMV (interior rows of a Kuhn box form their
     columns as row + the offsets of the interior stencil, the others read
     theirs, into the block's LDS column image): the same products in the same
@@ -623,7 +623,7 @@ def test_pattern_spmv(ctx, monkeypatch, n):
     ctx.to_device(dx, x)
     ys = {}
     for mode in ("nopat", "pat"):
-        monkeypatch.setenv("AFEM_SPMV", mode)
+        variant("AFEM_SPMV", mode)
         ls.spmv(dx, dy)
         ys[mode] = ctx.to_host(dy, nn, np.float64)
     ctx.free(dx)
@@ -632,9 +632,9 @@ def test_pattern_spmv(ctx, monkeypatch, n):
     sols, kern = {}, {}
     for mode in ("nopat", "pat", None):
         if mode is None:
-            monkeypatch.delenv("AFEM_SPMV")  # the default: the pattern kernel
+            variant("AFEM_SPMV", None)  # the default: the pattern kernel
         else:
-            monkeypatch.setenv("AFEM_SPMV", mode)
+            variant("AFEM_SPMV", mode)
         kern[mode] = ls.solve()["spmv_kernel"]
         sols[mode] = ls.solution_host()
     assert kern == {"nopat": 0, "pat": 1, None: 1}, kern
@@ -657,3 +657,22 @@ def test_stencil_on_slab_subdomains(ctx, rank):
     assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
     _check_values(vals, ovals)
     assert np.abs(ls.rhs_host() - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+
+
+@pytest.mark.parametrize("mode", [dict(rtol=1e-13), dict(fixed_iterations=37)])
+def test_cg_graph_replay_bitwise(ctx, variant, mode):
+    """The single-rank CG replays whole iterations as a captured HIP graph
+    (batches of the convergence-check period / 16 fixed iterations); it must
+    run exactly the launches of the per-kernel loop (AFEM_CG_GRAPH=0): the
+    same iteration count and the same solution bits."""
+    mesh = af.Mesh.structured(ctx, 3, 17, jitter=0.2, seed=3)
+    bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+    ls.applyDirichletViaPenalty(mesh.bottom_nodes(), 0.5, 1e30)
+    out = []
+    for g in (None, "0"):
+        variant("AFEM_CG_GRAPH", g)
+        ls.setSolverOptions(**mode)
+        st = ls.solve()
+        out.append((st["iterations"], ls.solution_host()))
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1])

@@ -68,6 +68,10 @@ def per_entry_gates(vals, ovals, ext, mag, label):
                max_kappa=float(kappa[np.isfinite(kappa)].max()) if np.isfinite(kappa).any() else 0.0)
     print(f"{label}: " + ", ".join(f"{k}={v:.3e}" if isinstance(v, float) else f"{k}={v}" for k, v in out.items()))
     assert out["gpu_vs_oracle_rel_wellcond"] <= REL_TOL
+    # BASELINE.md §5's plain per-entry gate (1e-10 relative) holds for all but
+    # the near-cancelling entries; those are a small minority, bounded below
+    assert out["gpu_vs_oracle_frac_within_1e10"] >= 0.999, out["gpu_vs_oracle_frac_within_1e10"]
+    assert int((rel_orc > REL_TOL).sum()) <= out["ill_conditioned"]
     assert out["gpu_vs_oracle_over_mag"] <= 1e-12
     assert out["gpu_vs_ext_rel_kappa_le_1e5"] <= REL_TOL
     assert out["gpu_vs_ext_over_mag"] <= 1e-14

@@ -1,6 +1,8 @@
 """Known answers pinning the oracle's block-3 tetrahedral elasticity
-restatement (no reference module or golden file covers 3D elasticity:
-SURVEY.md §8c "not pinned by any reference test"): symmetry, exactly six
+restatement, beside the reference pin of tests/test_oracle_passmo.py (the
+passmo module assembles 3D P1 elasticity + mass on the CPU,
+modules/passmo/ElastodynamicModule.cc:1389-1793, and its bar3d-tetra golden
+fixes the element and the Newmark loop; SURVEY.md §8c had missed it): symmetry, exactly six
 rigid-body zero modes, the patch test (exact strain energy of a uniform
 strain), consistent mass summing to the volume, and reduction to the
 reference's 2D TRIA3 element for plane-strain prisms is not attempted (the
