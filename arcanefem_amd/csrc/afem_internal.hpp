@@ -363,7 +363,12 @@ struct LinearSystem {
   std::unique_ptr<Halo> halo;
   // structured Kuhn box on one rank (BSR from Mesh.structured): the geometric
   // multigrid preconditioner's fine grid (multigrid.hip); mg_k = NB_DOF, 0: none
-  int mg_k = 0, mg_nx = 0, mg_nz = 0;
+  int mg_k = 0, mg_nx = 0, mg_nz = 0;  // the OWNED box: (nx+1)^2 (nz+1) nodes in lexicographic local ids
+  // a ghosted subdomain (slab of a multi-rank system): the preconditioner is a
+  // local V-cycle on the owned block (ghost columns dropped: block Jacobi over
+  // the ranks, no communication), on a box padded by one decoupled layer when
+  // the owned cell count in z is odd
+  bool mg_multi = false;
   std::unique_ptr<Multigrid, MgDeleter> mg;
 };
 

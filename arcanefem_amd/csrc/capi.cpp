@@ -725,10 +725,12 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
   }
   // structured box on one rank: the multigrid preconditioner's fine grid
   const StructuredInfo& st = b->mesh->st;
-  const bool box = st.valid && st.dim == 3 && st.nranks == 1 && b->mesh->nv == 4 && !b->mesh->part.valid;
+  // (a z-slab of several ranks: its owned box, for the block-Jacobi V-cycle)
+  const bool box = st.valid && st.dim == 3 && b->mesh->nv == 4 && !b->mesh->part.valid;
   ls->mg_k = box ? k : 0;
   ls->mg_nx = box ? st.n : 0;
-  ls->mg_nz = box ? st.nz : 0;
+  ls->mg_nz = box ? (st.k1 - st.k0) - 1 : 0;
+  ls->mg_multi = box && st.nranks > 1;
   ls->mg.reset();
   ls->has_csr = true;
   ls->csr_from_coo = false;

@@ -133,12 +133,13 @@ Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* pr
         l->blk_rows = d->K.s.row_ptr.p;
         l->blk_cols = d->K.s.cols.p;
       }
-      {  // structured box on one rank: the solve may use the multigrid preconditioner
+      {  // structured box (or z-slab: block-Jacobi V-cycles over the ranks): the multigrid preconditioner
         const StructuredInfo& st = mesh->st;
-        if (st.valid && st.dim == 3 && st.nranks == 1 && !mesh->part.valid) {
+        if (st.valid && st.dim == 3 && !mesh->part.valid) {
           d->ls.mg_k = 3;
           d->ls.mg_nx = st.n;
-          d->ls.mg_nz = st.nz;
+          d->ls.mg_nz = (st.k1 - st.k0) - 1;
+          d->ls.mg_multi = st.nranks > 1;
         }
       }
       d->ls.csr_vals = d->K.values.p;

@@ -1625,7 +1625,8 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     AFEM_LAUNCHED();
   }
   // geometric multigrid (structured box, one rank); other systems: point Jacobi
-  const bool use_mg = ls.opts.multigrid != 0 && !blk3 && !multi && mg_available(ls);
+  // (several ranks: block-Jacobi V-cycles on the slabs' owned blocks, mg_available)
+  const bool use_mg = ls.opts.multigrid != 0 && !blk3 && mg_available(ls);
   if (use_mg) mg_setup(ls);
   // r = b - A x0, z = M^-1 r, p = z and the r.z partials (all rows, free rows)
   auto cg_init = [&]() {

@@ -255,6 +255,61 @@ __global__ __launch_bounds__(64) void k_mg_gemv(int n, const double* __restrict_
   if (threadIdx.x == 0) x[i] = s;
 }
 
+// fine level of a ghosted slab (block-Jacobi V-cycle): row lengths of the
+// owned block (the owned columns are the prefix of each sorted row: ghosts are
+// numbered after the owned nodes) and one for every node of the pad layer
+__global__ void k_mg_own_len(int64_t nn_own, int64_t nn, const int64_t* __restrict__ bp,
+                             const int32_t* __restrict__ bc, int64_t* __restrict__ len)
+{
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nn) return;
+  if (r >= nn_own) {
+    len[r] = 1;
+    return;
+  }
+  int64_t l = 0;
+  for (int64_t q = bp[r]; q < bp[r + 1] && bc[q] < nn_own; ++q) ++l;
+  len[r] = l;
+}
+// copy of the owned block (values in the node-block CSR order, K u len + K s + w);
+// a pad node gets a decoupled diagonal block: the diagonal of the owned node
+// below it (same scale as its neighbours for the smoother and the Galerkin sums)
+template <int K>
+__global__ void k_mg_own_copy(int64_t nn_own, int64_t nn, int64_t layer, const int64_t* __restrict__ bp,
+                              const int32_t* __restrict__ bc, const double* __restrict__ v,
+                              const int64_t* __restrict__ nbp, int32_t* __restrict__ nbc, double* __restrict__ nv)
+{
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nn) return;
+  const int64_t o = nbp[r];
+  if (r >= nn_own) {
+    const int64_t below = r - layer;
+    const int64_t b0 = bp[below];
+    const int len = (int)(bp[below + 1] - b0);
+    int s = 0;
+    for (int q = 0; q < len; ++q)
+      if (bc[b0 + q] == (int32_t)below) s = q;
+    nbc[o] = (int32_t)r;
+    for (int u = 0; u < K; ++u)
+      for (int w = 0; w < K; ++w) nv[K * K * o + K * u + w] = u == w ? v[K * K * b0 + K * u * len + K * s + u] : 0.0;
+    return;
+  }
+  const int64_t b0 = bp[r];
+  const int len = (int)(bp[r + 1] - b0);
+  const int nl = (int)(nbp[r + 1] - o);
+  for (int s = 0; s < nl; ++s) nbc[o + s] = bc[b0 + s];
+  for (int u = 0; u < K; ++u)
+    for (int s = 0; s < nl; ++s)
+      for (int w = 0; w < K; ++w) nv[K * K * o + K * u * nl + K * s + w] = v[K * K * b0 + K * u * len + K * s + w];
+}
+// b = F r on the owned rows, 0 on the pad layer
+__global__ void k_mg_mask_pad(int64_t n, int64_t n_all, const uint8_t* __restrict__ cons,
+                              const double* __restrict__ r, double* __restrict__ b)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_all; i += (int64_t)gridDim.x * blockDim.x)
+    b[i] = i < n && !cons[i] ? r[i] : 0.0;
+}
+
 constexpr int kVec = 1024;  // grid of the vector kernels
 
 }  // namespace
@@ -290,9 +345,11 @@ void MgDeleter::operator()(Multigrid* m) const { delete m; }
 
 bool mg_available(const LinearSystem& ls)
 {
-  if (ls.mg_k < 1 || ls.mg_k > 3 || ls.mg_nx < 2 || ls.mg_nz < 2) return false;
-  if (ls.mg_nx % 2 || ls.mg_nz % 2) return false;  // no coarse level
-  if (ls.halo) return false;                        // one rank
+  if (ls.mg_k < 1 || ls.mg_k > 3 || ls.mg_nx < 2 || ls.mg_nz < 1) return false;
+  if (ls.mg_nx % 2) return false;                      // no coarse level
+  if (!ls.mg_multi && ls.mg_nz % 2) return false;      // one rank: an odd box has no coarse level
+  if (ls.mg_nz + ls.mg_nz % 2 < 2) return false;
+  if (ls.halo && !ls.mg_multi) return false;           // a halo over a mesh whose owned part is no box
   const Dims d{ ls.mg_nx, ls.mg_nx, ls.mg_nz };
   if (d.nodes() * ls.mg_k != ls.n_rows) return false;
   if (ls.mg_k == 1 ? !ls.csr_rows : (ls.blk_k != ls.mg_k || !ls.blk_rows)) return false;
@@ -438,7 +495,7 @@ bool dense_inverse(Ctx& ctx, Multigrid& mg, MgLevel& L)
 void mg_setup(LinearSystem& ls)
 {
   Ctx& ctx = *ls.ctx;
-  AFEM_REQUIRE(mg_available(ls), AFEM_ERR_STATE, "multigrid: not a structured single-rank system");
+  AFEM_REQUIRE(mg_available(ls), AFEM_ERR_STATE, "multigrid: not a structured box / z-slab system");
   const bool reuse = ls.opts.multigrid == 2;
   const void* krows = ls.mg_k == 1 ? (const void*)ls.csr_rows : (const void*)ls.blk_rows;
   if (reuse && ls.mg && ls.mg->key_rows == krows && ls.mg->key_vals == ls.csr_vals && ls.mg->key_n == ls.n_rows)
@@ -449,13 +506,52 @@ void mg_setup(LinearSystem& ls)
   mg->partial.alloc(kVec);
   {
     MgLevel L;
-    L.d = Dims{ ls.mg_nx, ls.mg_nx, ls.mg_nz };
-    L.nn = L.d.nodes();
-    L.n = k * L.nn;
-    L.bp = k == 1 ? ls.csr_rows : ls.blk_rows;
-    L.bc = k == 1 ? ls.csr_cols : ls.blk_cols;
-    L.v = ls.csr_vals;
-    L.dinv = ls.dinv.p;  // computed by ls_solve (k_inv_diag) before the setup
+    const int64_t* bp = k == 1 ? ls.csr_rows : ls.blk_rows;
+    const int32_t* bc = k == 1 ? ls.csr_cols : ls.blk_cols;
+    if (!ls.mg_multi) {
+      L.d = Dims{ ls.mg_nx, ls.mg_nx, ls.mg_nz };
+      L.nn = L.d.nodes();
+      L.n = k * L.nn;
+      L.bp = bp;
+      L.bc = bc;
+      L.v = ls.csr_vals;
+      L.dinv = ls.dinv.p;  // computed by ls_solve (k_inv_diag) before the setup
+    }
+    else {
+      // a slab of several ranks: the owned block (ghost columns dropped), padded
+      // in z by one decoupled layer when its cell count is odd
+      const int pad = ls.mg_nz % 2;
+      const Dims own{ ls.mg_nx, ls.mg_nx, ls.mg_nz };
+      L.d = Dims{ ls.mg_nx, ls.mg_nx, ls.mg_nz + pad };
+      L.nn = L.d.nodes();
+      L.n = k * L.nn;
+      const int64_t nn_own = own.nodes(), layer = (int64_t)(ls.mg_nx + 1) * (ls.mg_nx + 1);
+      DevBuf<int64_t> len;
+      len.alloc(L.nn);
+      const unsigned g = grid_for(L.nn, 256);
+      hipLaunchKernelGGL(k_mg_own_len, dim3(g), dim3(256), 0, ctx.stream, nn_own, L.nn, bp, bc, len.p);
+      AFEM_LAUNCHED();
+      L.own_bp.alloc(L.nn + 1);
+      exclusive_scan_i64(ctx, len.p, L.own_bp.p, L.nn);
+      const int64_t nb = read_i64(ctx, L.own_bp.p + L.nn);
+      L.own_bc.alloc(nb);
+      L.own_v.alloc((size_t)nb * k * k);
+      L.own_dinv.alloc(L.n);
+      dispatch_k(k, [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        hipLaunchKernelGGL(k_mg_own_copy<K>, dim3(g), dim3(256), 0, ctx.stream, nn_own, L.nn, layer, bp, bc,
+                           ls.csr_vals, L.own_bp.p, L.own_bc.p, L.own_v.p);
+        AFEM_LAUNCHED();
+        hipLaunchKernelGGL(k_mg_dinv<K>, dim3(g), dim3(256), 0, ctx.stream, L.nn, L.own_bp.p, L.own_bc.p, L.own_v.p,
+                           L.own_dinv.p);
+        AFEM_LAUNCHED();
+      });
+      ctx.sync();
+      L.bp = L.own_bp.p;
+      L.bc = L.own_bc.p;
+      L.v = L.own_v.p;
+      L.dinv = L.own_dinv.p;
+    }
     mg->lv.push_back(std::move(L));
   }
   DevBuf<int> err;
@@ -574,11 +670,15 @@ void mg_apply(LinearSystem& ls, const double* r, double* z)
   Multigrid& mg = *ls.mg;
   MgLevel& L0 = mg.lv[0];
   const unsigned g = (unsigned)std::min<int64_t>(kVec, (L0.n + 255) / 256);
-  hipLaunchKernelGGL(k_mg_mask, dim3(g), dim3(256), 0, ctx.stream, L0.n, ls.cons.p, r, L0.b.p);
+  const int64_t n = ls.n_rows;  // < L0.n when the slab's box is padded
+  if (n == L0.n)
+    hipLaunchKernelGGL(k_mg_mask, dim3(g), dim3(256), 0, ctx.stream, L0.n, ls.cons.p, r, L0.b.p);
+  else
+    hipLaunchKernelGGL(k_mg_mask_pad, dim3(g), dim3(256), 0, ctx.stream, n, L0.n, ls.cons.p, r, L0.b.p);
   AFEM_LAUNCHED();
   vcycle(ctx, mg, 0, L0.b.p);
-  AFEM_HIP(hipMemcpyAsync(z, L0.x.p, L0.n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
-  hipLaunchKernelGGL(k_mg_fix, dim3(g), dim3(256), 0, ctx.stream, L0.n, ls.cons.p, r, ls.dinv.p, z);
+  AFEM_HIP(hipMemcpyAsync(z, L0.x.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
+  hipLaunchKernelGGL(k_mg_fix, dim3(g), dim3(256), 0, ctx.stream, n, ls.cons.p, r, ls.dinv.p, z);
   AFEM_LAUNCHED();
 }
 

@@ -20,6 +20,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 POISSON = dict(n=5, nz=8)
 POISSON_PAT = dict(n=12, nz=16)  # slabs whose rows are mostly interior stencil rows: the pattern SpMV
 DYN = dict(n=3, nz=5, E=21e5, nu=0.28, rho=1.0, dt=1e-3, f=(0.0, -9.81, 1.0), steps=4)
+# slabs whose owned boxes coarsen (even n; 2 ranks: 8 and 9 owned layers -> 7 (padded) and 8 cells in z)
+POISSON_MG = dict(n=8, nz=16)
+DYN_MG = dict(n=8, nz=12, E=21e5, nu=0.28, rho=1.0, dt=1e-3, f=(0.0, -9.81, 1.0), steps=3)
 
 
 def main():
@@ -40,8 +43,9 @@ def main():
     res = {}
     if case.endswith("_async"):
         case = case[:-len("_async")]
-    if case in ("poisson", "poisson_pat"):
-        n, nz = (POISSON if case == "poisson" else POISSON_PAT)["n"], (POISSON if case == "poisson" else POISSON_PAT)["nz"]
+    if case in ("poisson", "poisson_pat", "poisson_mg"):
+        prm = {"poisson": POISSON, "poisson_pat": POISSON_PAT, "poisson_mg": POISSON_MG}[case]
+        n, nz = prm["n"], prm["nz"]
         mesh = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=20250220, nranks=world, rank=rank)
         bsr = af.BSRFormat(mesh, 1).initialize(True)
         bsr.computeSparsity()
@@ -50,11 +54,17 @@ def main():
         bsr.toLinearSystem(ls)
         ls.applyDirichletViaPenalty(mesh.bottom_nodes(), 0.5, 1e30)
         ls.set_halo_structured(comm, mesh)
+        if case == "poisson_mg":  # block-Jacobi V-cycles on the slabs' owned boxes, against point Jacobi
+            ls.setSolverOptions(rtol=1e-14, max_iter=20000, preconditioner="jacobi")
+            it_j = ls.solve()["iterations"]
+            ls.setSolverOptions(preconditioner="multigrid")
         ls.setSolverOptions(rtol=1e-14, max_iter=20000)
         st = ls.solve()
         _, _, l2g = mesh.download()
         res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
                    converged=int(st["converged"]), rel=st["rel_residual"], spmv=st["spmv_kernel"])
+        if case == "poisson_mg":
+            res["iters_jacobi"] = it_j
         # CG iter/s with the halo attached (fixed iterations)
         ls.setSolverOptions(fixed_iterations=20)
         ls.solve()
@@ -127,15 +137,16 @@ def main():
         st = ls.solve()
         res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
                    converged=int(st["converged"]), rel=st["rel_residual"], part=part)
-    elif case == "elastodynamics":
+    elif case in ("elastodynamics", "elastodynamics_mg"):
         from arcanefem_amd.elastodynamics import Elastodynamics3D
 
-        p = DYN
+        p = DYN if case == "elastodynamics" else DYN_MG
+        pc = "jacobi" if case == "elastodynamics" else "multigrid"
         mesh = af.Mesh.structured(ctx, 3, p["n"], nz=p["nz"], jitter=0.2, seed=20250220, nranks=world, rank=rank)
         _, coords, l2g = mesh.download()
         fixed = np.nonzero(coords[:, 0] < 0.5 / p["n"])[0].astype(np.int32)  # the x = 0 layer, ghosts included
         sim = Elastodynamics3D(ctx, mesh, p["E"], p["nu"], p["rho"], p["dt"], body_force=p["f"], fixed_nodes=fixed,
-                               rtol=1e-14, comm=comm)
+                               rtol=1e-14, comm=comm, preconditioner=pc)
         its = []
         for _ in range(p["steps"]):
             st = sim.step()

@@ -54,14 +54,14 @@ def _run(case, world, tmp_path):
 
 
 @pytest.mark.parametrize("case,world", [("poisson", 2), ("poisson", 3), ("poisson_pat", 2), ("poisson_async", 3),
-                                        ("poisson_pat_async", 2)])
+                                        ("poisson_pat_async", 2), ("poisson_mg", 2), ("poisson_mg_async", 3)])
 def test_distributed_poisson_solve(case, world, tmp_path):
     """*_async: the host transport's exchange runs on libafem's worker thread
     between halo_begin and halo_end, so the interior row blocks of every CG
     SpMV run with the halo actually in flight."""
     res = _run(case, world, tmp_path)
     case = case.replace("_async", "")
-    prm = W.POISSON if case == "poisson" else W.POISSON_PAT
+    prm = {"poisson": W.POISSON, "poisson_pat": W.POISSON_PAT, "poisson_mg": W.POISSON_MG}[case]
     n, nz = prm["n"], prm["nz"]
     if case == "poisson_pat":  # the pattern SpMV in the interior / halo-boundary split
         assert all(int(r["spmv"]) == 1 for r in res), [int(r["spmv"]) for r in res]
@@ -80,6 +80,10 @@ def test_distributed_poisson_solve(case, world, tmp_path):
         iters.add(int(r["iters"]))
         assert r["converged"]
     assert len(iters) == 1  # one iteration sequence (the reductions are global)
+    if case == "poisson_mg":  # block-Jacobi V-cycles over the slabs: far fewer iterations than point Jacobi
+        it_mg, it_j = int(res[0]["iters"]), int(res[0]["iters_jacobi"])
+        print(f"multigrid {it_mg} vs jacobi {it_j} iterations")
+        assert 3 * it_mg <= it_j, (it_mg, it_j)
     assert not np.isnan(x).any()
     assert np.abs(x - xg).max() / np.abs(xg).max() <= 1e-10
     for r in res:  # synchronised ghosts equal the owners' values
@@ -88,10 +92,14 @@ def test_distributed_poisson_solve(case, world, tmp_path):
         assert np.abs(r["x"][k:] - x[gid]).max() <= 1e-15 * np.abs(xg).max()
 
 
-def test_distributed_elastodynamics(tmp_path):
-    p = W.DYN
+@pytest.mark.parametrize("case", ["elastodynamics", "elastodynamics_mg"])
+def test_distributed_elastodynamics(tmp_path, case):
+    """C5's loop over 2 slabs: point-Jacobi PCG, and the block-Jacobi V-cycle
+    preconditioner (each rank's owned box coarsened, no communication in the
+    preconditioner) -- both must match the single-domain oracle Newmark loop."""
+    p = W.DYN if case == "elastodynamics" else W.DYN_MG
     world = 2
-    res = _run("elastodynamics", world, tmp_path)
+    res = _run(case, world, tmp_path)
     g = O.structured_mesh(3, p["n"], nz=p["nz"])
     fixed = np.nonzero(g["coords"][:, 0] < 0.5 / p["n"])[0]
     Uo, Vo, Ao = O.newmark_elastodynamics(g["n_own"], g["cells"], g["coords"], p["E"], p["nu"], p["rho"], p["dt"],
