@@ -1773,11 +1773,13 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   // graph replay of whole iterations (single rank, no split SpMV, no
   // multigrid: every launch of an iteration is a plain kernel), in batches of
   // the convergence-check period (even: the ping-pong parity of the scalars
-  // repeats); AFEM_CG_GRAPH=0 launches every kernel (diagnostics)
+  // repeats).  Opt-in (AFEM_CG_GRAPH=1): measured on MI355X at C2 the replayed
+  // batches cost MORE device time than the launched kernels (0.68 vs 0.60 ms
+  // per iteration, profiles/r03_v3_bench.json vs r03_v3_cg_nograph_bench.json)
   const char* cgg = variant("AFEM_CG_GRAPH");
   const int gbatch = fixed ? 16 : check;
   const bool graph = !multi && !use_mg && !comm && !overlap && (gbatch % 2) == 0 && gbatch >= 2 &&
-                     !(cgg && atoi(cgg) == 0);
+                     (cgg && atoi(cgg) == 1);
   hipGraphExec_t gexec = nullptr;
   struct GraphGuard {
     hipGraphExec_t& g;
