@@ -1143,16 +1143,10 @@ __host__ __device__ constexpr int64_t stencil_tile_bytes(int64_t u_cap, int64_t 
 }
 
 // one slice of signature S (the steps, the RHS and the write-back of k_assemble_stencil)
-struct NoMid {
-  __device__ __forceinline__ void operator()() const {}
-};
-// mid(): called between the steps and the write-back (the DMA kernel's next
-// node-id loads: in flight across the stores, not across the step loop)
-template <const StencilSig& S, int MAXC, class Mid = NoMid>
+template <const StencilSig& S, int MAXC>
 __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nsteps, int lane, const double* cxyz,
                                               double* flat, int64_t* rbs, double s_coef, double f_meas,
-                                              double* __restrict__ vals, double* __restrict__ rhs, int rhs_add,
-                                              const Mid& mid = Mid())
+                                              double* __restrict__ vals, double* __restrict__ rhs, int rhs_add)
 {
   constexpr int W = S.w, D = S.dslot, NS = S.nsteps;
   static_assert(NS <= 16 * MAXC && W <= 16, "stencil signature beyond the kernel's strip chunks");
@@ -1214,7 +1208,6 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
       asm volatile("" : "+v"(acc[iP]), "+v"(acc[iQ]), "+v"(acc[iR]));
       xc = xn;
     }
-    mid();
 
     // ---- RHS (as k_assemble_strip)
     {
@@ -1247,17 +1240,16 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
 // signature index -> stencil_slice<S_index> (a scalar branch per slice)
 template <int I, const StencilSig& S0, const StencilSig&... SR>
 struct StencilDispatch {
-  template <int MAXC, class Mid = NoMid>
+  template <int MAXC>
   __device__ __forceinline__ static void run(int sig, const StripPre<MAXC>& cur, int nsteps, int lane,
                                              const double* cxyz, double* flat, int64_t* rbs, double s_coef,
-                                             double f_meas, double* vals, double* rhs, int rhs_add,
-                                             const Mid& mid = Mid())
+                                             double f_meas, double* vals, double* rhs, int rhs_add)
   {
     if (sig == I || sizeof...(SR) == 0)
-      stencil_slice<S0, MAXC, Mid>(cur, nsteps, lane, cxyz, flat, rbs, s_coef, f_meas, vals, rhs, rhs_add, mid);
+      stencil_slice<S0, MAXC>(cur, nsteps, lane, cxyz, flat, rbs, s_coef, f_meas, vals, rhs, rhs_add);
     else if constexpr (sizeof...(SR) > 0)
-      StencilDispatch<I + 1, SR...>::template run<MAXC, Mid>(sig, cur, nsteps, lane, cxyz, flat, rbs, s_coef,
-                                                             f_meas, vals, rhs, rhs_add, mid);
+      StencilDispatch<I + 1, SR...>::template run<MAXC>(sig, cur, nsteps, lane, cxyz, flat, rbs, s_coef, f_meas,
+                                                        vals, rhs, rhs_add);
   }
 };
 
@@ -1376,148 +1368,6 @@ __global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, co
     cur = nxt;
 #pragma unroll
     for (int k = 0; k < 4; ++k) nid1[k] = nid2[k];
-  }
-}
-
-// ---- the stencil kernel with its coordinates staged by LDS-DMA
-// Each slice's coordinates go global -> LDS with global_load_lds_dwordx3 (no
-// VGPR destination): lane l of a wave-instruction c moves half (12 B) of the
-// node at position 32c + l/2, which lands at byte 24 (32c + l/2) + 12 (l & 1) --
-// the 24-B AoS image the steps read, placement included.  Two coordinate
-// buffers per wave: the DMA of slice i+1 is in flight while slice i runs (its
-// coordinates were waited for at the end of slice i-1), so the 24 VGPRs that
-// carried the next slice's coordinates through the step loop are free.
-//   LDS per wave: S = max(img, cz) + cz, buffers at 0 and S - cz; slice i's
-//   write-back image overlays its own buffer (at 0, or ending at S) and never
-//   reaches the other one; + 512 B of row offsets.
-__host__ __device__ constexpr int64_t stencil_dma_cz(int64_t u_cap)
-{
-  return 768 * ((u_cap + 31) / 32);
-}
-__host__ __device__ constexpr int64_t stencil_dma_span(int64_t u_cap, int64_t w)
-{
-  return (512 * w > stencil_dma_cz(u_cap) ? 512 * w : stencil_dma_cz(u_cap)) + stencil_dma_cz(u_cap);
-}
-__host__ __device__ constexpr int64_t stencil_dma_bytes(int64_t u_cap, int64_t w)
-{
-  return stencil_dma_span(u_cap, w) + 512;
-}
-
-// one 12-B LDS-DMA piece per lane: m0 = the wave-uniform LDS byte address of
-// the instruction's 768-B run (m0 is compiler-reserved: set and restored here).
-// The compiler does not count it: the consumer's s_waitcnt vmcnt is explicit.
-__device__ __forceinline__ void glds12(const void* gsrc, uint32_t lds_dst)
-{
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx3 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
-
-template <const StencilSig&... SS>
-__global__ __launch_bounds__(64, 3) void k_assemble_stencil_dma(
-  int64_t n_slices, const SliceRec* __restrict__ recs, unsigned long long* __restrict__ tickets, int u_cap,
-  const int32_t* __restrict__ perm, const int64_t* __restrict__ pos_rb, const uint32_t* __restrict__ pos_dl,
-  const uint8_t* __restrict__ strip_u, const int32_t* __restrict__ snode, const double* __restrict__ coords,
-  double s_coef, double f_meas, double* __restrict__ vals, double* __restrict__ rhs, int rhs_add)
-{
-  constexpr int MAXC = stencil_maxc<SS...>();
-  constexpr int WMAX = stencil_maxw<SS...>();
-  extern __shared__ __align__(16) unsigned char smem[];
-  const uint32_t cz = (uint32_t)stencil_dma_cz(u_cap), span = (uint32_t)stencil_dma_span(u_cap, WMAX);
-  int64_t* const rbs = reinterpret_cast<int64_t*>(smem + span);
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
-  const int lane = threadIdx.x;
-  const int xcd = (int)(blockIdx.x & 7);
-  const int64_t r0 = n_slices * xcd / 8, r1 = n_slices * (xcd + 1) / 8;
-  auto claim_issue = [&]() -> unsigned long long {
-    unsigned long long t = 0;
-    if (lane == 0) t = atomicAdd(tickets + 16 * xcd, 1ull);
-    return t;
-  };
-  auto claim_get = [&](unsigned long long t) -> int64_t {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)t);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(t >> 32));
-    return r0 + (int64_t)(((uint64_t)hi << 32) | lo);
-  };
-  int64_t p0 = claim_get(claim_issue());
-  if (p0 >= r1) return;
-  int64_t p1 = claim_get(claim_issue());
-  int64_t p2 = claim_get(claim_issue());
-  int64_t p3 = claim_get(claim_issue());
-  SliceRec R0 = recs[p0];
-  SliceRec R1 = recs[p1 < r1 ? p1 : p0];
-  SliceRec R2 = recs[p2 < r1 ? p2 : p0];
-  // node ids of the positions this lane moves (position 32c + lane/2, clamped
-  // to the slice's last node: the extra pieces rewrite real coordinates)
-  auto load_nid = [&](const SliceRec& R, int32_t(&nid)[8]) {
-    const int nu = (int)(R.meta & 0xFFFFu);
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-      nid[c] = snode[(int64_t)R.snode_off + max(min((lane >> 1) + 32 * c, nu - 1), 0)];
-  };
-  auto issue_dma = [&](const SliceRec& R, const int32_t(&nid)[8], uint32_t buf) {
-    const int nu = (int)(R.meta & 0xFFFFu);
-    const unsigned char* base = reinterpret_cast<const unsigned char*>(coords) + 12 * (lane & 1);
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-      if (32 * c < nu) glds12(base + 24 * (int64_t)nid[c], lds0 + buf + 768u * c);
-  };
-  auto load_rows = [&](const SliceRec& R, StripPre<MAXC>& p) {
-    const int64_t q = (int64_t)R.sl * 64 + lane;
-    p.row = perm[q];
-    p.dl = pos_dl[q];
-    p.rb = pos_rb[q];
-    const u32x4* su = reinterpret_cast<const u32x4*>(strip_u + (int64_t)R.strip_off * 1024) + lane;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) p.cu[c] = su[(int64_t)c * 64];
-  };
-  StripPre<MAXC> cur, nxt;
-  int32_t nidn[8];
-  uint32_t buf = 0, obuf = span - cz;  // this slice's coordinate buffer, the other one
-  {
-    int32_t nid[8];
-    load_nid(R0, nid);
-    __builtin_amdgcn_s_waitcnt(0);
-    issue_dma(R0, nid, buf);
-    load_nid(R1, nid);
-    __builtin_amdgcn_s_waitcnt(0);
-    issue_dma(R1, nid, obuf);
-    load_rows(R0, cur);
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  for (;;) {
-    const unsigned long long t4 = claim_issue();
-    const SliceRec R3 = recs[p3 < r1 ? p3 : p0];
-    const uint32_t img = buf == 0 ? 0u : span - 512u * (uint32_t)WMAX;
-    StencilDispatch<0, SS...>::template run<MAXC>((int)R0.sig, cur, (int)(R0.meta >> 24), lane,
-                                                  reinterpret_cast<const double*>(smem + buf),
-                                                  reinterpret_cast<double*>(smem + img), rbs, s_coef, f_meas, vals,
-                                                  rhs, rhs_add, [&]() {
-                                                    load_rows(R1, nxt);
-                                                    load_nid(R2, nidn);
-                                                  });
-    if (p1 >= r1) break;
-    // the next slice's coordinates (DMA issued at the end of the previous
-    // slice): at least the 13 vector-memory instructions of this iteration
-    // (claim, rows, node ids) were issued after it, so vmcnt(13) covers it and
-    // leaves most of this slice's value stores in flight
-    asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
-    // slice p2's coordinates into the buffer this slice just released (the
-    // write-back's image reads retired: stencil_slice's last wave_sync_lds)
-    issue_dma(R2, nidn, buf);
-    p0 = p1;
-    p1 = p2;
-    p2 = p3;
-    p3 = claim_get(t4);
-    R0 = R1;
-    R1 = R2;
-    R2 = R3;
-    cur = nxt;
-    const uint32_t t = buf;
-    buf = obuf;
-    obuf = t;
   }
 }
 
@@ -2908,12 +2758,8 @@ void launch_stencil(const Structure& s, int n_cu, const double* coords, double s
   static int occ_k = 0;
   static size_t occ_shm = 0;
   static const void* occ_kern = nullptr;
-  // AFEM_STENCIL_DMA=0: the register-staged coordinates (A/B diagnostics)
-  const char* dv = variant("AFEM_STENCIL_DMA");
-  const bool dma = !(dv && atoi(dv) == 0) && s.k_nodes <= 256;
-  auto kern = dma ? k_assemble_stencil_dma<AFEM_STENCIL_PACK> : k_assemble_stencil<AFEM_STENCIL_PACK>;
-  const size_t shm = dma ? (size_t)stencil_dma_bytes(s.k_nodes, stencil_maxw<AFEM_STENCIL_PACK>())
-                         : (size_t)stencil_tile_bytes(s.k_nodes, stencil_maxw<AFEM_STENCIL_PACK>());
+  auto kern = k_assemble_stencil<AFEM_STENCIL_PACK>;
+  const size_t shm = (size_t)stencil_tile_bytes(s.k_nodes, stencil_maxw<AFEM_STENCIL_PACK>());
   if (occ_shm != shm || occ_kern != reinterpret_cast<const void*>(kern)) {
     occ_kern = reinterpret_cast<const void*>(kern);
     int q = 0;

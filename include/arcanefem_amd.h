@@ -69,7 +69,7 @@ int afem_device_count(int* count);
  * AFEM_ASSEMBLY_STENCIL / _UNIFORM / _STRIPS / _SIDE / _WAVES_PER_CU,
  * AFEM_ELAST_WG / _STRIP / _BIG (assembly instances), AFEM_SPMV (CG SpMV),
  * AFEM_CG_GRAPH (1: replay the single-rank CG iterations as a HIP graph; off by
- * default, slower on MI355X), AFEM_STENCIL_DMA (0: register-staged coordinates),
+ * default, slower on MI355X),
  * AFEM_ORDER / AFEM_BRICKS / AFEM_BANK_PLACE / _MAX (structure build),
  * AFEM_DEBUG_SLICES / _PATTERNS (stderr dumps).  Without an explicit value a
  * knob takes the process environment's value at its first use; unset means
