@@ -369,6 +369,14 @@ struct LinearSystem {
   // the ranks, no communication), on a box padded by one decoupled layer when
   // the owned cell count in z is odd
   bool mg_multi = false;
+  // the slab's place in the global box (z-slabs of Mesh.structured): global
+  // cells in z, first owned node layer, whether a ghost layer below exists
+  // (local numbering: owned layers, then the ghost layer below, then above).
+  // With an even global box the preconditioner is ONE global V-cycle: the fine
+  // level distributed (halo exchanges), the coarse levels replicated on every
+  // rank (multigrid.hip); AFEM_MG_MULTI=block keeps the block-Jacobi V-cycles
+  int mg_nzg = 0, mg_k0 = 0;
+  bool mg_glo = false;
   std::unique_ptr<Multigrid, MgDeleter> mg;
 };
 

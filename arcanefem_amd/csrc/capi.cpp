@@ -731,6 +731,9 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
   ls->mg_nx = box ? st.n : 0;
   ls->mg_nz = box ? (st.k1 - st.k0) - 1 : 0;
   ls->mg_multi = box && st.nranks > 1;
+  ls->mg_nzg = box ? st.nz : 0;
+  ls->mg_k0 = box ? st.k0 : 0;
+  ls->mg_glo = box && st.ghost_lo >= 0;
   ls->mg.reset();
   ls->has_csr = true;
   ls->csr_from_coo = false;

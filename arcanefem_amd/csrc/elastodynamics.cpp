@@ -140,6 +140,9 @@ Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* pr
           d->ls.mg_nx = st.n;
           d->ls.mg_nz = (st.k1 - st.k0) - 1;
           d->ls.mg_multi = st.nranks > 1;
+          d->ls.mg_nzg = st.nz;
+          d->ls.mg_k0 = st.k0;
+          d->ls.mg_glo = st.ghost_lo >= 0;
         }
       }
       d->ls.csr_vals = d->K.values.p;

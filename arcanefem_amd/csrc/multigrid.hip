@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <string>
 #include <vector>
 
 namespace afem {
@@ -310,6 +311,124 @@ __global__ void k_mg_mask_pad(int64_t n, int64_t n_all, const uint8_t* __restric
     b[i] = i < n && !cons[i] ? r[i] : 0.0;
 }
 
+// ---- the global V-cycle over z-slabs: fine level distributed, coarse levels replicated
+// A slab's local node numbering (Mesh.structured with nranks > 1): the owned
+// layers k0 .. k0+nown-1, then the ghost layer below (if any), then the one above.
+struct SlabMap {
+  int np1;    // nodes per row (nx + 1)
+  int64_t L;  // nodes per layer
+  int k0, nown, glo;
+  __host__ __device__ int gz(int li) const { return li < nown ? k0 + li : (li == nown && glo ? k0 - 1 : k0 + nown); }
+  __host__ __device__ bool owned_z(int z) const { return z >= k0 && z < k0 + nown; }
+  __host__ __device__ int64_t local_owned(int x, int y, int z) const { return (int64_t)(z - k0) * L + x + (int64_t)np1 * y; }
+};
+
+// the part of A_c = P^T A P over the slab's OWNED fine rows (global coarse
+// numbering; summed over the ranks afterwards); loop order of k_mg_galerkin
+template <int K>
+__global__ void k_mg_galerkin_part(Dims fd, Dims cd, SlabMap sm, const int64_t* __restrict__ fbp,
+                                   const int32_t* __restrict__ fbc, const double* __restrict__ fv,
+                                   const int64_t* __restrict__ cbp, const int32_t* __restrict__ cbc,
+                                   double* __restrict__ cv, int* __restrict__ err)
+{
+  const int64_t I = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (I >= cd.nodes()) return;
+  int cx, cy, cz;
+  decompose(cd, I, cx, cy, cz);
+  if (2 * cz + 1 < sm.k0 || 2 * cz - 1 >= sm.k0 + sm.nown) return;
+  const int64_t c0 = cbp[I];
+  const int clen = (int)(cbp[I + 1] - c0);
+  for (int o = 0; o < 15; ++o) {
+    const int fx = 2 * cx + c_st[o][0], fy = 2 * cy + c_st[o][1], fz = 2 * cz + c_st[o][2];
+    if (!fd.in(fx, fy, fz) || !sm.owned_z(fz)) continue;
+    const double wi = o == 0 ? 1.0 : 0.5;
+    const int64_t fi = sm.local_owned(fx, fy, fz);
+    const int64_t f0 = fbp[fi];
+    const int flen = (int)(fbp[fi + 1] - f0);
+    for (int s = 0; s < flen; ++s) {
+      const int64_t col = fbc[f0 + s];
+      const int li = (int)(col / sm.L);
+      const int64_t pos = col - (int64_t)li * sm.L;
+      const int jx = (int)(pos % sm.np1), jy = (int)(pos / sm.np1), jz = sm.gz(li);
+      const int a = jx & 1, b = jy & 1, c = jz & 1;
+      const int px = jx >> 1, py = jy >> 1, pz = jz >> 1;
+      const int np = (a | b | c) ? 2 : 1;
+      const double w = wi * (np == 2 ? 0.5 : 1.0);
+      for (int p = 0; p < np; ++p) {
+        const int32_t J = (int32_t)cd.id(px + p * a, py + p * b, pz + p * c);
+        int t = -1;
+        for (int q = 0; q < clen; ++q)
+          if (cbc[c0 + q] == J) {
+            t = q;
+            break;
+          }
+        if (t < 0) {
+          *err = 1;
+          continue;
+        }
+        for (int u = 0; u < K; ++u)
+          for (int v = 0; v < K; ++v)
+            cv[K * K * c0 + K * u * clen + K * t + v] += w * fv[K * K * f0 + K * u * flen + K * s + v];
+      }
+    }
+  }
+}
+
+// the part of r_c = P^T r_f over the slab's owned fine nodes (every coarse node
+// written: 0 away from the slab; summed over the ranks afterwards)
+template <int K>
+__global__ void k_mg_restrict_part(Dims fd, Dims cd, SlabMap sm, const double* __restrict__ rf,
+                                   double* __restrict__ rc)
+{
+  const int64_t I = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (I >= cd.nodes()) return;
+  int cx, cy, cz;
+  decompose(cd, I, cx, cy, cz);
+  double acc[K];
+  for (int u = 0; u < K; ++u) acc[u] = 0.0;
+  if (!(2 * cz + 1 < sm.k0 || 2 * cz - 1 >= sm.k0 + sm.nown)) {
+    for (int o = 0; o < 15; ++o) {
+      const int fx = 2 * cx + c_st[o][0], fy = 2 * cy + c_st[o][1], fz = 2 * cz + c_st[o][2];
+      if (!fd.in(fx, fy, fz) || !sm.owned_z(fz)) continue;
+      const double w = o == 0 ? 1.0 : 0.5;
+      const int64_t fi = sm.local_owned(fx, fy, fz);
+      for (int u = 0; u < K; ++u) acc[u] += w * rf[K * fi + u];
+    }
+  }
+  for (int u = 0; u < K; ++u) rc[K * I + u] = acc[u];
+}
+
+// x_f += P x_c on the slab's owned fine nodes (x_c global)
+template <int K>
+__global__ void k_mg_prolong_own(Dims cd, SlabMap sm, int64_t nn_own, const double* __restrict__ xc,
+                                 double* __restrict__ xf)
+{
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nn_own) return;
+  const int li = (int)(f / sm.L);
+  const int64_t pos = f - (int64_t)li * sm.L;
+  const int x = (int)(pos % sm.np1), y = (int)(pos / sm.np1), z = sm.k0 + li;
+  const int a = x & 1, b = y & 1, c = z & 1;
+  const int64_t P0 = cd.id(x >> 1, y >> 1, z >> 1);
+  if (a | b | c) {
+    const int64_t P1 = cd.id((x >> 1) + a, (y >> 1) + b, (z >> 1) + c);
+    for (int u = 0; u < K; ++u) xf[K * f + u] += 0.5 * (xc[K * P0 + u] + xc[K * P1 + u]);
+  }
+  else {
+    for (int u = 0; u < K; ++u) xf[K * f + u] += xc[K * P0 + u];
+  }
+}
+
+// the power iteration's start vector by GLOBAL index (the one-rank sequence of k_mg_fill)
+__global__ void k_mg_fill_off(int64_t n, int64_t off, double* __restrict__ v)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t h = (uint64_t)(i + off) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    v[i] = 0.5 + (double)(h & 0xFFFF) / 65536.0;
+  }
+}
+
 constexpr int kVec = 1024;  // grid of the vector kernels
 
 }  // namespace
@@ -331,6 +450,11 @@ struct MgLevel {
 struct Multigrid {
   int k = 1;
   int sweeps = kSweeps;
+  // global V-cycle over z-slabs: level 0 is the slab's owned rows (vectors with
+  // the ghost entries of the system's halo), levels >= 1 the global box's
+  bool global = false;
+  SlabMap sm{};
+  Dims gfine{};
   std::vector<MgLevel> lv;
   DevBuf<double> ainv;  // dense inverse of the coarsest level (n_dense x n_dense) or empty
   int n_dense = 0;
@@ -343,8 +467,24 @@ struct Multigrid {
 
 void MgDeleter::operator()(Multigrid* m) const { delete m; }
 
+namespace {
+// one global V-cycle over the slabs (else: block-Jacobi V-cycles on the owned blocks)
+bool mg_global_mode(const LinearSystem& ls)
+{
+  if (!ls.mg_multi || !ls.halo || !ls.halo->comm) return false;
+  const char* e = variant("AFEM_MG_MULTI");
+  if (e && std::string(e) == "block") return false;
+  return ls.mg_nx >= 2 && ls.mg_nx % 2 == 0 && ls.mg_nzg >= 2 && ls.mg_nzg % 2 == 0 && ls.mg_nz >= 0;
+}
+}  // namespace
+
 bool mg_available(const LinearSystem& ls)
 {
+  if (ls.mg_k >= 1 && ls.mg_k <= 3 && mg_global_mode(ls)) {
+    const Dims d{ ls.mg_nx, ls.mg_nx, ls.mg_nz };
+    if (d.nodes() * ls.mg_k != ls.n_rows) return false;
+    return ls.mg_k == 1 ? ls.csr_rows != nullptr : (ls.blk_k == ls.mg_k && ls.blk_rows);
+  }
   if (ls.mg_k < 1 || ls.mg_k > 3 || ls.mg_nx < 2 || ls.mg_nz < 1) return false;
   if (ls.mg_nx % 2) return false;                      // no coarse level
   if (!ls.mg_multi && ls.mg_nz % 2) return false;      // one rank: an odd box has no coarse level
@@ -490,6 +630,49 @@ bool dense_inverse(Ctx& ctx, Multigrid& mg, MgLevel& L)
   return true;
 }
 
+double allreduce_scalar(LinearSystem& ls, double v)
+{
+  Ctx& ctx = *ls.ctx;
+  DevBuf<double> d;
+  d.alloc(1);
+  AFEM_HIP(hipMemcpyAsync(d.p, &v, sizeof(double), hipMemcpyHostToDevice, ctx.stream));
+  comm_allreduce(ls.halo->comm, ctx, d.p, 1);
+  double out = 0.0;
+  AFEM_HIP(hipMemcpyAsync(&out, d.p, sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  return out;
+}
+
+// lambda_max(D^-1 A) of the distributed fine level: the one-rank power
+// iteration with the halo exchanged before every product and the norms summed
+// over the ranks (start vector by global index)
+double power_lambda_global(LinearSystem& ls, Multigrid& mg, MgLevel& L)
+{
+  Ctx& ctx = *ls.ctx;
+  const int k = mg.k;
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
+  hipLaunchKernelGGL(k_mg_fill_off, dim3(g), dim3(256), 0, ctx.stream, L.n, (int64_t)k * mg.sm.k0 * mg.sm.L, L.x.p);
+  AFEM_LAUNCHED();
+  hipLaunchKernelGGL(k_mg_norm2, dim3(g), dim3(256), 0, ctx.stream, L.n, L.x.p, mg.partial.p);
+  AFEM_LAUNCHED();
+  double nv = std::sqrt(allreduce_scalar(ls, host_sum(ctx, mg.partial, (int)g)));
+  double lam = 0.0;
+  for (int it = 0; it < kPowerIts; ++it) {
+    halo_exchange(*ls.halo, ctx, L.x.p);
+    spmv_blk_epi(ctx, k, 0, L.nn, L.bp, L.bc, L.v, L.x.p, L.t.p, nullptr, nullptr, 0.0);
+    hipLaunchKernelGGL(k_mg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, L.dinv, L.t.p, mg.partial.p);
+    AFEM_LAUNCHED();
+    const double nw = std::sqrt(allreduce_scalar(ls, host_sum(ctx, mg.partial, (int)g)));
+    lam = nv > 0 ? nw / nv : 0.0;
+    if (!(nw > 0)) break;
+    hipLaunchKernelGGL(k_mg_mul, dim3(g), dim3(256), 0, ctx.stream, L.n, 1.0 / nw, L.t.p);
+    AFEM_LAUNCHED();
+    std::swap(L.x, L.t);
+    nv = 1.0;
+  }
+  return lam;
+}
+
 }  // namespace
 
 void mg_setup(LinearSystem& ls)
@@ -504,11 +687,64 @@ void mg_setup(LinearSystem& ls)
   const int k = ls.mg_k;
   mg->k = k;
   mg->partial.alloc(kVec);
+  mg->global = mg_global_mode(ls);
+  DevBuf<int> err;
+  err.alloc(1);
+  AFEM_HIP(hipMemsetAsync(err.p, 0, sizeof(int), ctx.stream));
   {
     MgLevel L;
     const int64_t* bp = k == 1 ? ls.csr_rows : ls.blk_rows;
     const int32_t* bc = k == 1 ? ls.csr_cols : ls.blk_cols;
-    if (!ls.mg_multi) {
+    if (mg->global) {
+      // level 0: the slab's owned rows as they are (local columns, ghosts included)
+      L.d = Dims{ ls.mg_nx, ls.mg_nx, ls.mg_nz };
+      L.nn = L.d.nodes();
+      L.n = k * L.nn;
+      L.bp = bp;
+      L.bc = bc;
+      L.v = ls.csr_vals;
+      L.dinv = ls.dinv.p;
+      mg->sm = SlabMap{ ls.mg_nx + 1, (int64_t)(ls.mg_nx + 1) * (ls.mg_nx + 1), ls.mg_k0, ls.mg_nz + 1, ls.mg_glo ? 1 : 0 };
+      mg->gfine = Dims{ ls.mg_nx, ls.mg_nx, ls.mg_nzg };
+      mg->lv.push_back(std::move(L));
+      // level 1: the global coarse box, A_1 = sum over the ranks of their owned rows' P^T A P parts
+      MgLevel C;
+      C.d = Dims{ ls.mg_nx / 2, ls.mg_nx / 2, ls.mg_nzg / 2 };
+      C.nn = C.d.nodes();
+      C.n = k * C.nn;
+      std::vector<int64_t> hbp;
+      std::vector<int32_t> hbc;
+      coarse_structure(C.d, hbp, hbc);
+      C.own_bp.alloc(hbp.size());
+      C.own_bc.alloc(hbc.size());
+      AFEM_HIP(hipMemcpyAsync(C.own_bp.p, hbp.data(), hbp.size() * 8, hipMemcpyHostToDevice, ctx.stream));
+      AFEM_HIP(hipMemcpyAsync(C.own_bc.p, hbc.data(), hbc.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+      C.own_v.alloc(hbc.size() * k * k);
+      AFEM_HIP(hipMemsetAsync(C.own_v.p, 0, C.own_v.bytes(), ctx.stream));
+      C.own_dinv.alloc(C.n);
+      const MgLevel& F = mg->lv.back();
+      const unsigned g = (unsigned)grid_for(C.nn, 128);
+      dispatch_k(k, [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        hipLaunchKernelGGL(k_mg_galerkin_part<K>, dim3(g), dim3(128), 0, ctx.stream, mg->gfine, C.d, mg->sm, F.bp, F.bc,
+                           F.v, C.own_bp.p, C.own_bc.p, C.own_v.p, err.p);
+        AFEM_LAUNCHED();
+      });
+      comm_allreduce(ls.halo->comm, ctx, C.own_v.p, (int64_t)C.own_v.n);
+      dispatch_k(k, [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        hipLaunchKernelGGL(k_mg_dinv<K>, dim3(g), dim3(128), 0, ctx.stream, C.nn, C.own_bp.p, C.own_bc.p, C.own_v.p,
+                           C.own_dinv.p);
+        AFEM_LAUNCHED();
+      });
+      C.bp = C.own_bp.p;
+      C.bc = C.own_bc.p;
+      C.v = C.own_v.p;
+      C.dinv = C.own_dinv.p;
+      ctx.sync();
+      mg->lv.push_back(std::move(C));
+    }
+    else if (!ls.mg_multi) {
       L.d = Dims{ ls.mg_nx, ls.mg_nx, ls.mg_nz };
       L.nn = L.d.nodes();
       L.n = k * L.nn;
@@ -552,11 +788,8 @@ void mg_setup(LinearSystem& ls)
       L.v = L.own_v.p;
       L.dinv = L.own_dinv.p;
     }
-    mg->lv.push_back(std::move(L));
+    if (!mg->global) mg->lv.push_back(std::move(L));
   }
-  DevBuf<int> err;
-  err.alloc(1);
-  AFEM_HIP(hipMemsetAsync(err.p, 0, sizeof(int), ctx.stream));
   while (true) {
     const MgLevel& F = mg->lv.back();
     if (F.n <= kDenseMax || F.d.nx % 2 || F.d.ny % 2 || F.d.nz % 2 || F.d.nx < 2 || F.d.nz < 2) break;
@@ -595,12 +828,18 @@ void mg_setup(LinearSystem& ls)
   AFEM_HIP(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, ctx.stream));
   ctx.sync();
   AFEM_REQUIRE(!herr, AFEM_ERR_STATE, "multigrid: Galerkin product outside the coarse Kuhn stencil");
-  for (MgLevel& L : mg->lv) {
-    L.x.alloc(L.n);
-    L.t.alloc(L.n);
+  for (size_t l = 0; l < mg->lv.size(); ++l) {
+    MgLevel& L = mg->lv[l];
+    const bool dist = mg->global && l == 0;  // vectors with the halo's ghost entries
+    L.x.alloc(dist ? ls.n_cols : L.n);
+    L.t.alloc(dist ? ls.n_cols : L.n);
+    if (dist) {
+      AFEM_HIP(hipMemsetAsync(L.x.p, 0, L.x.bytes(), ctx.stream));
+      AFEM_HIP(hipMemsetAsync(L.t.p, 0, L.t.bytes(), ctx.stream));
+    }
     L.b.alloc(L.n);
     L.r.alloc(L.n);
-    const double lam = power_lambda(ctx, *mg, L);
+    const double lam = dist ? power_lambda_global(ls, *mg, L) : power_lambda(ctx, *mg, L);
     L.omega = lam > 0 ? 4.0 / (3.0 * 1.05 * lam) : 0.6;
   }
   MgLevel& Lc = mg->lv.back();
@@ -662,6 +901,41 @@ void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
   smooth(ctx, mg, L, b, mg.sweeps, false);
 }
 
+// level 0 of the global V-cycle (the steps of vcycle on the slab's owned
+// rows): the halo before every product, the restriction summed over the ranks,
+// levels >= 1 replicated (the same arithmetic on every rank)
+void vcycle_global(LinearSystem& ls, Multigrid& mg, const double* b)
+{
+  Ctx& ctx = *ls.ctx;
+  MgLevel& L = mg.lv[0];
+  MgLevel& C = mg.lv[1];
+  smooth(ctx, mg, L, b, 1, true);
+  for (int s = 1; s < mg.sweeps; ++s) {
+    halo_exchange(*ls.halo, ctx, L.x.p);
+    smooth(ctx, mg, L, b, 1, false);
+  }
+  halo_exchange(*ls.halo, ctx, L.x.p);
+  spmv_blk_epi(ctx, mg.k, 2, L.nn, L.bp, L.bc, L.v, L.x.p, L.r.p, b, nullptr, 0.0);
+  dispatch_k(mg.k, [&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    hipLaunchKernelGGL(k_mg_restrict_part<K>, dim3((unsigned)grid_for(C.nn, 256)), dim3(256), 0, ctx.stream,
+                       mg.gfine, C.d, mg.sm, L.r.p, C.b.p);
+    AFEM_LAUNCHED();
+  });
+  comm_allreduce(ls.halo->comm, ctx, C.b.p, C.n);
+  vcycle(ctx, mg, 1, C.b.p);
+  dispatch_k(mg.k, [&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    hipLaunchKernelGGL(k_mg_prolong_own<K>, dim3((unsigned)grid_for(L.nn, 256)), dim3(256), 0, ctx.stream, C.d,
+                       mg.sm, L.nn, C.x.p, L.x.p);
+    AFEM_LAUNCHED();
+  });
+  for (int s = 0; s < mg.sweeps; ++s) {
+    halo_exchange(*ls.halo, ctx, L.x.p);
+    smooth(ctx, mg, L, b, 1, false);
+  }
+}
+
 }  // namespace
 
 void mg_apply(LinearSystem& ls, const double* r, double* z)
@@ -676,7 +950,10 @@ void mg_apply(LinearSystem& ls, const double* r, double* z)
   else
     hipLaunchKernelGGL(k_mg_mask_pad, dim3(g), dim3(256), 0, ctx.stream, n, L0.n, ls.cons.p, r, L0.b.p);
   AFEM_LAUNCHED();
-  vcycle(ctx, mg, 0, L0.b.p);
+  if (mg.global)
+    vcycle_global(ls, mg, L0.b.p);
+  else
+    vcycle(ctx, mg, 0, L0.b.p);
   AFEM_HIP(hipMemcpyAsync(z, L0.x.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
   hipLaunchKernelGGL(k_mg_fix, dim3(g), dim3(256), 0, ctx.stream, n, ls.cons.p, r, ls.dinv.p, z);
   AFEM_LAUNCHED();

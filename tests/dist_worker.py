@@ -54,9 +54,15 @@ def main():
         bsr.toLinearSystem(ls)
         ls.applyDirichletViaPenalty(mesh.bottom_nodes(), 0.5, 1e30)
         ls.set_halo_structured(comm, mesh)
-        if case == "poisson_mg":  # block-Jacobi V-cycles on the slabs' owned boxes, against point Jacobi
+        if case == "poisson_mg":
+            # point Jacobi, then the block-Jacobi V-cycles on the slabs' owned boxes,
+            # then (below) the global V-cycle: fine level distributed, coarse levels replicated
             ls.setSolverOptions(rtol=1e-14, max_iter=20000, preconditioner="jacobi")
             it_j = ls.solve()["iterations"]
+            af.set_variant("AFEM_MG_MULTI", "block")
+            ls.setSolverOptions(preconditioner="multigrid")
+            it_b = ls.solve()["iterations"]
+            af.set_variant("AFEM_MG_MULTI", None)
             ls.setSolverOptions(preconditioner="multigrid")
         ls.setSolverOptions(rtol=1e-14, max_iter=20000)
         st = ls.solve()
@@ -65,6 +71,17 @@ def main():
                    converged=int(st["converged"]), rel=st["rel_residual"], spmv=st["spmv_kernel"])
         if case == "poisson_mg":
             res["iters_jacobi"] = it_j
+            res["iters_block"] = it_b
+            if rank == 0:  # the same global box on ONE rank: the multigrid solve the slabs must reproduce
+                m1 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=20250220)
+                b1 = af.BSRFormat(m1, 1).initialize(True)
+                b1.computeSparsity()
+                l1 = af.DoFLinearSystem().initialize(ctx, m1.n_own_nodes, m1.n_nodes)
+                b1.assemblePoissonP1(1.0, 5.5, l1.rhsVariable(), rhs_mode="set")
+                b1.toLinearSystem(l1)
+                l1.applyDirichletViaPenalty(m1.bottom_nodes(), 0.5, 1e30)
+                l1.setSolverOptions(rtol=1e-14, max_iter=20000, preconditioner="multigrid")
+                res["iters_single"] = l1.solve()["iterations"]
         # CG iter/s with the halo attached (fixed iterations)
         ls.setSolverOptions(fixed_iterations=20)
         ls.solve()
@@ -155,6 +172,14 @@ def main():
         U, V, A = sim.state_host()
         res = dict(l2g=l2g, n_own=mesh.n_own_nodes, U=U, V=V, A=A, iters=np.array(its))
         sim.close()
+        if case == "elastodynamics_mg" and rank == 0:  # the one-rank multigrid loop's iterations
+            m1 = af.Mesh.structured(ctx, 3, p["n"], nz=p["nz"], jitter=0.2, seed=20250220)
+            _, c1, _ = m1.download()
+            f1 = np.nonzero(c1[:, 0] < 0.5 / p["n"])[0].astype(np.int32)
+            s1 = Elastodynamics3D(ctx, m1, p["E"], p["nu"], p["rho"], p["dt"], body_force=p["f"], fixed_nodes=f1,
+                                  rtol=1e-14, preconditioner="multigrid")
+            res["iters_single"] = np.array([s1.step()["iterations"] for _ in range(p["steps"])])
+            s1.close()
     else:
         raise SystemExit(f"unknown case {case}")
     assert not comm.errors, comm.errors

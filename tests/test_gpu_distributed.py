@@ -80,11 +80,15 @@ def test_distributed_poisson_solve(case, world, tmp_path):
         iters.add(int(r["iters"]))
         assert r["converged"]
     assert len(iters) == 1  # one iteration sequence (the reductions are global)
-    if case == "poisson_mg":  # block-Jacobi V-cycles over the slabs: far fewer iterations than point Jacobi
-        it_mg, it_j = int(res[0]["iters"]), int(res[0]["iters_jacobi"])
-        print(f"multigrid {it_mg} vs jacobi {it_j} iterations")
-        # (measured: 3 slabs of 4-5 cells, 54 vs 128; thinner slabs, weaker blocks)
-        assert (3 if world == 2 else 2) * it_mg <= it_j, (it_mg, it_j)
+    if case == "poisson_mg":
+        # the global V-cycle over the slabs is the one-rank multigrid solve (up to the
+        # rounding of the distributed sums); the block-Jacobi V-cycles (AFEM_MG_MULTI=block)
+        # lose the coupling between slabs but still beat point Jacobi
+        it_mg, it_j, it_b = int(res[0]["iters"]), int(res[0]["iters_jacobi"]), int(res[0]["iters_block"])
+        it_1 = int(res[0]["iters_single"])
+        print(f"global multigrid {it_mg}, one rank {it_1}, block-Jacobi V-cycles {it_b}, point Jacobi {it_j}")
+        assert abs(it_mg - it_1) <= 1, (it_mg, it_1)
+        assert it_mg <= it_b and 2 * it_b <= it_j, (it_mg, it_b, it_j)
     assert not np.isnan(x).any()
     assert np.abs(x - xg).max() / np.abs(xg).max() <= 1e-10
     for r in res:  # synchronised ghosts equal the owners' values
@@ -95,9 +99,10 @@ def test_distributed_poisson_solve(case, world, tmp_path):
 
 @pytest.mark.parametrize("case", ["elastodynamics", "elastodynamics_mg"])
 def test_distributed_elastodynamics(tmp_path, case):
-    """C5's loop over 2 slabs: point-Jacobi PCG, and the block-Jacobi V-cycle
-    preconditioner (each rank's owned box coarsened, no communication in the
-    preconditioner) -- both must match the single-domain oracle Newmark loop."""
+    """C5's loop over 2 slabs: point-Jacobi PCG, and the multigrid PCG (one
+    global V-cycle: fine level distributed, coarse levels replicated) -- both
+    must match the single-domain oracle Newmark loop; the multigrid one also
+    the one-rank multigrid iteration counts."""
     p = W.DYN if case == "elastodynamics" else W.DYN_MG
     world = 2
     res = _run(case, world, tmp_path)
@@ -115,6 +120,9 @@ def test_distributed_elastodynamics(tmp_path, case):
         U[d], V[d], A[d] = r["U"], r["V"], r["A"]
         its.append(r["iters"])
     assert np.array_equal(its[0], its[1])
+    if case == "elastodynamics_mg":  # the global V-cycle: the one-rank multigrid iteration counts
+        print("iterations per step", its[0], "one rank", res[0]["iters_single"])
+        assert np.abs(its[0] - res[0]["iters_single"]).max() <= 1
     for gpu, orc in ((U, Uo), (V, Vo), (A, Ao)):
         assert not np.isnan(gpu).any()
         assert np.abs(gpu - orc).max() <= 1e-8 * np.abs(orc).max(), np.abs(gpu - orc).max() / np.abs(orc).max()
