@@ -452,7 +452,7 @@ class DoFLinearSystem:
         """initial_guess: "zero" (default) or "current" (start the PCG from the
         solution vector's values); preconditioner: "jacobi" (default),
         "block3" (3x3 node-block Jacobi, NB_DOF = 3 systems), "multigrid"
-        (geometric multigrid V-cycle on structured boxes, one rank; rebuilt
+        (geometric multigrid V-cycle on structured boxes, one rank or z-slabs; rebuilt
         every solve) or "multigrid-reuse" (built once, reused while the
         matrix structure is unchanged)."""
         o = C.SolverOpts()

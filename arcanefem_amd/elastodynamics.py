@@ -70,7 +70,7 @@ class Elastodynamics3D:
              ctypes.c_void_p(fixed.ctypes.data) if fixed.size else None, fixed.size, C.AFEM_MEM_HOST,
              ctypes.byref(h))
         self.h = h
-        # "multigrid": the geometric multigrid V-cycle on structured boxes (one rank), built at
+        # "multigrid": the geometric multigrid V-cycle on structured boxes (one rank or z-slabs), built at
         # the first step and reused (the Newmark operator c0 M + K is the same every step)
         blk, mgm = {"jacobi": (0, 0), "block3": (3, 0), "multigrid": (0, 2)}[preconditioner]
         o = C.SolverOpts(C.AFEM_SOLVER_PCG, max_iter, rtol, 0.0, 8, 0, 0, blk, mgm)

@@ -305,7 +305,9 @@ typedef struct afem_solver_opts {
                                systems; constraint rows decoupled from their block mates) */
   int32_t multigrid;        /* 0: off (default); 1: geometric multigrid V-cycle preconditioner (Galerkin coarse
                                operators of the Kuhn-box hierarchy, damped-Jacobi smoothing) on systems from a
-                               structured box on one rank, rebuilt at every solve; 2: built at the first solve
+                               structured box -- one rank, or its z-slabs over several ranks (one global
+                               V-cycle: fine level distributed over the halo, coarse levels replicated) --
+                               rebuilt at every solve; 2: built at the first solve
                                and reused while the matrix structure stays the same (time stepping with a
                                constant operator).  Other systems fall back to point Jacobi. */
 } afem_solver_opts;
