@@ -236,6 +236,7 @@ struct Structure {
   int64_t n_k0 = 0, n_u1 = 0;
   int64_t n_k = 0, n_ur = 0;
   int sig_k = -1, k_nodes = 0, ur_nodes = 0, ur_w = 0;
+  int64_t n_strip_shared = 0;  // stencil slices reading their signature's shared strip_u copy
   bool rec_ok = false;                     // offsets fit the 32-bit record fields
   DevBuf<int64_t> pos_rb;                  // [n_slices*64] row_ptr of each position's row (0: idle)
   DevBuf<uint32_t> pos_dl;                 // [n_slices*64] diagonal slot | row length << 8

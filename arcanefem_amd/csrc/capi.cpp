@@ -628,6 +628,7 @@ int afem_bsr_get_stats(afem_bsr* b, afem_bsr_stats* st)
   st->uniform_slices = (int32_t)b->s.n_uni;
   st->stencil_slices = (int32_t)b->s.n_k;
   st->stencil_sig = b->s.sig_k;
+  st->shared_strip_slices = b->s.n_strip_shared;
   st->last_kernel = b->last_kernel;
   API_END
 }

@@ -192,7 +192,8 @@ def roofline(bsr, mesh, kernel_ms):
             "kernel_ms": round(kernel_ms, 4),
             "inc_padding": round(st["inc_table_entries"] / max(int(st["n_incidences"]), 1) - 1.0, 4),
             "uniform_slice_frac": round(st["uniform_slices"] / max(st["n_slices"], 1), 4),
-            "stencil_slice_frac": round(st["stencil_slices"] / max(st["n_slices"], 1), 4)}
+            "stencil_slice_frac": round(st["stencil_slices"] / max(st["n_slices"], 1), 4),
+            "shared_strip_frac": round(st.get("shared_strip_slices", 0) / max(st["n_slices"], 1), 4)}
 
 
 def pmc_traffic(path, n):

@@ -237,6 +237,8 @@ typedef struct afem_bsr_stats {
   int32_t last_kernel;      /* AFEM_KERNEL_* that ran the last assembly of this matrix */
   int32_t stencil_slices;   /* uniform slices of a compiled-in strip signature (scalar stencil instance) */
   int32_t stencil_sig;      /* that signature's index (-1: none) */
+  int64_t shared_strip_slices; /* stencil slices reading their signature's one copy of the per-lane
+                                  local-index stream (byte-identical streams: interior bricks) */
 } afem_bsr_stats;
 #define AFEM_KERNEL_NONE 0
 #define AFEM_KERNEL_STRIP 1          /* scalar row-strip kernel (uniform + general instances) */
