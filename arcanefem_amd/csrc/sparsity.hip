@@ -937,24 +937,6 @@ __global__ void k_max_i32(int64_t n, const int32_t* __restrict__ v, unsigned lon
 // swap bits (bit j = step j is a swap) and the common step bytes (32: the
 // scalar slot stream of the uniform kernel; padding steps carry the diagonal
 // slot).  One wave per slice.
-// Hilbert key of each slice's first row node (the stencil list's processing order)
-__global__ void k_slice_curve_key(int64_t n_slices, const int32_t* __restrict__ perm, const double* __restrict__ coords,
-                                  const unsigned long long* __restrict__ box, uint64_t* __restrict__ keys)
-{
-  const int64_t sl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sl >= n_slices) return;
-  int32_t r = -1;
-  for (int l = 0; l < 64 && r < 0; ++l) r = perm[sl * 64 + l];
-  uint32_t q[3] = { 0, 0, 0 };
-  if (r >= 0)
-    for (int a = 0; a < 3; ++a) {
-      const double lo = from_ordered_bits(box[a]), hi = from_ordered_bits(box[3 + a]);
-      const double t = hi > lo ? (coords[3 * (int64_t)r + a] - lo) / (hi - lo) : 0.0;
-      q[a] = (uint32_t)fmin(fmax(t * 2097151.0, 0.0), 2097151.0);
-    }
-  keys[sl] = hilbert3(q[0], q[1], q[2]);
-}
-
 // same[i] = 1: slice i's local-index stream (strip_u, nch[i] chunks of 1 KB)
 // equals the one at rep[i] byte for byte (one 64-lane block per slice)
 __global__ __launch_bounds__(64) void k_strip_same(int64_t n, const uint32_t* __restrict__ off,
@@ -1538,28 +1520,6 @@ void build_structure(Mesh& m, Structure& s)
         s.sig_k = best;
         s.n_k = (int64_t)rk.size();
         s.n_ur = (int64_t)rur.size();
-        // Stencil list in the Hilbert order of the bricks: each XCD's eighth of the
-        // list (and each wave's run of claims) is a compact 3D region, so the
-        // coordinates a brick shares with its z- and y-neighbours are still in the
-        // XCD's L2 (brick order alone: x-neighbours only).  AFEM_SLICE_CURVE=0: off.
-        const char* sce = variant("AFEM_SLICE_CURVE");
-        if (rk.size() >= 64 && !(sce && atoi(sce) == 0) && m.dim == 3) {
-          DevBuf<unsigned long long> box;
-          box.alloc(6);
-          const unsigned long long init[6] = { ~0ull, ~0ull, ~0ull, 0ull, 0ull, 0ull };
-          AFEM_HIP(hipMemcpyAsync(box.p, init, sizeof(init), hipMemcpyHostToDevice, ctx.stream));
-          hipLaunchKernelGGL(k_bbox, dim3(1024), dim3(256), 0, ctx.stream, n_rows, m.coords.p, box.p);
-          AFEM_LAUNCHED();
-          DevBuf<uint64_t> dk;
-          dk.alloc(ns);
-          hipLaunchKernelGGL(k_slice_curve_key, dim3(grid_for((int64_t)ns, 256)), dim3(256), 0, ctx.stream,
-                             (int64_t)ns, s.perm.p, m.coords.p, box.p, dk.p);
-          AFEM_LAUNCHED();
-          std::vector<uint64_t> hk(ns);
-          AFEM_HIP(hipMemcpyAsync(hk.data(), dk.p, ns * 8, hipMemcpyDeviceToHost, ctx.stream));
-          ctx.sync();
-          std::stable_sort(rk.begin(), rk.end(), [&](const SliceRec& a, const SliceRec& b) { return hk[a.sl] < hk[b.sl]; });
-        }
         // Interior bricks of one signature have byte-identical local-index streams
         // (same strip, same node-list layout and bank placement): those slices read
         // the signature's first copy (2 KB, L2-resident) instead of their own --
