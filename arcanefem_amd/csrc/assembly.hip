@@ -1222,17 +1222,39 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
 #pragma unroll
     for (int t = 0; t < W; ++t)
       if (t != D) sum += acc[t];
+    // brick x-runs: when lanes 4q..4q+3 hold consecutive rows (all of the
+    // signature's length W), their 4W values are one contiguous range at rb(4q):
+    // the run's base is a wave-uniform scalar and lane l stores value l of the
+    // run -- no owner division, no dependent LDS read of the row offsets
+    const int64_t rb = active ? cur.rb : -1;
+    const int64_t rb_run = __shfl(rb, lane & ~3);
+    const bool runs = __all(active && rb == rb_run + (int64_t)W * (lane & 3));
     wave_sync_lds();  // every lane's coordinate reads before the image overwrites them
 #pragma unroll
     for (int t = 0; t < W; ++t) flat[lane * W + t] = t == D ? -sum : acc[t];
-    rbs[lane] = active ? cur.rb : -1;
+    if (!runs) rbs[lane] = rb;
     wave_sync_lds();
+    if (runs) {
+      static_assert(4 * W <= 64, "a run's values exceed the wave");
+      // lanes past the run's 4W values repeat its last value (same address, same
+      // value): no exec-mask branch, so the 16 image reads issue together
+      const int o = lane < 4 * W ? lane : 4 * W - 1;
 #pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int P = 64 * k + lane;
-      const int L = P / W;
-      const int64_t r = rbs[L];
-      if (r >= 0) vals[r + (P - L * W)] = flat[P];
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)rb, 4 * r);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)rb >> 32), 4 * r);
+        double* const dst = vals + (int64_t)(((uint64_t)hi << 32) | lo);
+        dst[o] = flat[4 * W * r + o];
+      }
+    }
+    else {
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        const int P = 64 * k + lane;
+        const int L = P / W;
+        const int64_t r = rbs[L];
+        if (r >= 0) vals[r + (P - L * W)] = flat[P];
+      }
     }
     wave_sync_lds();
 }
@@ -2243,9 +2265,34 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     // store: flat position P is value P - 9 fps[L] of row lane L = bown[P / 9]
     if (UMODE == 3 && full) {
       constexpr int B = 9 * (WS > 0 ? WS : 1);
-      for (int P = tid; P < 64 * B; P += 192) {
-        const int L = P / B;
-        vals[9 * rbs[L] + (P - L * B)] = flat[P];
+      // brick x-runs: lanes 4q..4q+3 hold consecutive rows of the same length,
+      // so their 4B values are one contiguous range at 9 rb(4q) (both layouts:
+      // a node row's 9 len values are contiguous in either) -- the run's base is
+      // a wave-uniform scalar, each thread's offsets are constants: no
+      // per-value owner division, no dependent LDS read, no 64-bit address math
+      const int64_t rb_run = __shfl(rb, lane & ~3);
+      if (__all(rb == rb_run + (int64_t)WS * (lane & 3))) {
+        constexpr int RUN = 4 * B;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)rb, 4 * r);
+          const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)rb >> 32), 4 * r);
+          double* const dst = vals + 9 * (int64_t)(((uint64_t)hi << 32) | lo);
+          const double* const src = flat + RUN * r;
+#pragma unroll
+          for (int i = 0; i < (RUN + 191) / 192; ++i) {
+            // threads past the run repeat its last value (same address and
+            // value): no exec-mask branch between the image reads
+            const int o = min(tid + 192 * i, RUN - 1);
+            dst[o] = src[o];
+          }
+        }
+      }
+      else {
+        for (int P = tid; P < 64 * B; P += 192) {
+          const int L = P / B;
+          vals[9 * rbs[L] + (P - L * B)] = flat[P];
+        }
       }
     }
     else {
