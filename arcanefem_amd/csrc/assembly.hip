@@ -1229,13 +1229,12 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
     const int64_t rb = active ? cur.rb : -1;
     const int64_t rb_run = __shfl(rb, lane & ~3);
     const bool runs = __all(active && rb == rb_run + (int64_t)W * (lane & 3));
-    wave_sync_lds();  // every lane's coordinate reads before the image overwrites them
-#pragma unroll
-    for (int t = 0; t < W; ++t) flat[lane * W + t] = t == D ? -sum : acc[t];
-    if (!runs) rbs[lane] = rb;
-    wave_sync_lds();
     if (runs) {
       static_assert(4 * W <= 64, "a run's values exceed the wave");
+      wave_sync_lds();  // every lane's coordinate reads before the image overwrites them
+#pragma unroll
+      for (int t = 0; t < W; ++t) flat[lane * W + t] = t == D ? -sum : acc[t];
+      wave_sync_lds();
       // lanes past the run's 4W values repeat its last value (same address, same
       // value): no exec-mask branch, so the 16 image reads issue together
       const int o = lane < 4 * W ? lane : 4 * W - 1;
@@ -1247,14 +1246,12 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
         dst[o] = flat[4 * W * r + o];
       }
     }
-    else {
+    else if (active) {
+      // partial bricks and face tiles whose lanes are not x-runs (a few % of the
+      // slices): each lane stores its row's W values straight from the registers
+      // (no image, no owner table: nothing of this path is kept live across slices)
 #pragma unroll
-      for (int k = 0; k < W; ++k) {
-        const int P = 64 * k + lane;
-        const int L = P / W;
-        const int64_t r = rbs[L];
-        if (r >= 0) vals[r + (P - L * W)] = flat[P];
-      }
+      for (int t = 0; t < W; ++t) vals[rb + t] = t == D ? -sum : acc[t];
     }
     wave_sync_lds();
 }
