@@ -240,7 +240,8 @@ struct Structure {
   bool rec_ok = false;                     // offsets fit the 32-bit record fields
   DevBuf<int64_t> pos_rb;                  // [n_slices*64] row_ptr of each position's row (0: idle)
   DevBuf<uint32_t> pos_dl;                 // [n_slices*64] diagonal slot | row length << 8
-  DevBuf<unsigned long long> tickets;  // dynamic slice claiming (assembly), 2 x 8 XCD counters
+  DevBuf<unsigned long long> tickets;  // dynamic slice claiming (assembly): a ring of per-assembly counter slots
+  int64_t ticket_gen = 0;              // assemblies since the ring was last zeroed (assembly.hip next_tickets)
   int64_t n_slices = 0;
   int64_t n_incidences = 0;  // real (non-padding) entries
   int max_row_len = 0;

@@ -2795,6 +2795,25 @@ int occ_override()
 }
 }  // namespace
 
+// Claim counters of the persistent assembly kernels: one 4-KB slot per
+// assembly (up to 4 launches x 8 XCD counters, 128 B apart) from a ring of
+// kTicketRing slots zeroed together -- one memset every kTicketRing
+// assemblies instead of a fill launch per assembly.  Every launch of an
+// assembly is joined to the context stream before the next one starts, so a
+// ring reset (stream-ordered) never races a running kernel.
+constexpr int64_t kTicketRing = 256, kTicketSlot = 4 * 8 * 16;
+unsigned long long* next_tickets(Structure& s, Ctx& ctx)
+{
+  if (s.tickets.n < kTicketRing * kTicketSlot) {
+    s.tickets.alloc(kTicketRing * kTicketSlot);
+    s.ticket_gen = 0;
+  }
+  if (s.ticket_gen % kTicketRing == 0) AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
+  unsigned long long* const t = s.tickets.p + (s.ticket_gen % kTicketRing) * kTicketSlot;
+  ++s.ticket_gen;
+  return t;
+}
+
 // the stencil kernel (every compiled-in signature, stencil_sigs.inc) over s.rec_k
 void launch_stencil(const Structure& s, int n_cu, const double* coords, double s_coef, double f_meas, double* vals,
                     double* rhs, int rhs_add, unsigned long long* tk, hipStream_t stream)
@@ -2867,8 +2886,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
     const bool uni_env = umode != 0;
     const bool use_uni = uni_env && s.n_uni > 0;
     const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;
-    if (s.tickets.n < 4 * 8 * 16) s.tickets.alloc(4 * 8 * 16);  // one counter per XCD, 128-B apart, per launch
-    AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
+    unsigned long long* const tk0 = next_tickets(s, ctx);  // this assembly's claim counters
     auto launch_s = [&](const void* fn, auto kern, int64_t n_list, const SliceRec* list, unsigned long long* tk,
                         size_t shm_s, hipStream_t stream, int ucap = -1, int wcap = -1,
                         const uint8_t* slots = nullptr) {
@@ -2912,9 +2930,15 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       // the whole assembly), one after the other the kernel times add up to the
       // assembly time (AFEM_ASSEMBLY_SIDE=1: side stream, diagnostic)
       const char* se = variant("AFEM_ASSEMBLY_SIDE");
-      const bool serial_k = use_k && !(se && atoi(se) == 1);
-      const bool fork = !serial_k && ((has_u && (s.n_ms > 0 || s.n_mb > 0 || (use_k && s.n_ur > 0))) ||
-                                      (!has_u && s.n_ms > 0 && s.n_mb > 0));
+      const int side_mode = se ? atoi(se) : 0;
+      const bool serial_k = use_k && side_mode != 1;
+      // AFEM_ASSEMBLY_SIDE=2: the small lists first on the context stream, the
+      // stencil kernel on the side stream right after (forked before them), so
+      // the small lists' waves are dispatched first and the stencil grid fills
+      // the rest of the chip beside them
+      const bool k_side = use_k && side_mode == 2 && (s.n_ms > 0 || s.n_mb > 0);
+      const bool fork = k_side || (!serial_k && ((has_u && (s.n_ms > 0 || s.n_mb > 0 || (use_k && s.n_ur > 0))) ||
+                                                 (!has_u && s.n_ms > 0 && s.n_mb > 0)));
       hipStream_t side = ctx.stream;
       if (fork) {
         side = ctx.side();
@@ -2930,27 +2954,27 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       hipStream_t s_mb = has_u && !serial_k ? side : (s.n_ms > 0 && !serial_k ? side : ctx.stream);
       if (s.n_ms > 0)
         launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 0>), k_assemble_strip<4, 2, 16, 0>, s.n_ms,
-                 s.rec_ms.p, s.tickets.p + 128, shm_ms, s_ms, s.ms_nodes, ms_w);
+                 s.rec_ms.p, tk0 + 128, shm_ms, s_ms, s.ms_nodes, ms_w);
       if (s.n_mb > 0)
         launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 4, 32, 0>), k_assemble_strip<4, 4, 32, 0>, s.n_mb,
-                 s.rec_mb.p, s.tickets.p + 256, shm_mb, s_mb, s.mb_nodes, s.mb_w);
+                 s.rec_mb.p, tk0 + 256, shm_mb, s_mb, s.mb_nodes, s.mb_w);
       if (use_k) {
         if (s.n_ur > 0) {
           const size_t shm_ur = (size_t)(8 * 64 * (int64_t)s.ur_w + strip_coord_bytes(dimc, s.ur_nodes, s.ur_w));
           launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 1>), k_assemble_strip<4, 2, 16, 1>,
-                   s.n_ur, s.rec_ur.p, s.tickets.p, shm_ur, side, s.ur_nodes, s.ur_w, s.urslot.p);
+                   s.n_ur, s.rec_ur.p, tk0, shm_ur, side, s.ur_nodes, s.ur_w, s.urslot.p);
         }
         launch_stencil(s, ctx.n_cu, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add,
-                       s.tickets.p + 384, ctx.stream);
+                       tk0 + 384, k_side ? side : ctx.stream);
       }
       else if (has_u) {
         const size_t shm_uu = (size_t)(8 * 64 * (int64_t)s.u_w + strip_coord_bytes(dimc, s.u_nodes, s.u_w));
         if (umode == 2)
           launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 2>), k_assemble_strip<4, 2, 16, 2>,
-                   s.n_uni, s.rec_u.p, s.tickets.p, shm_uu, ctx.stream, s.u_nodes, s.u_w);
+                   s.n_uni, s.rec_u.p, tk0, shm_uu, ctx.stream, s.u_nodes, s.u_w);
         else
           launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 1>), k_assemble_strip<4, 2, 16, 1>,
-                   s.n_uni, s.rec_u.p, s.tickets.p, shm_uu, ctx.stream, s.u_nodes, s.u_w);
+                   s.n_uni, s.rec_u.p, tk0, shm_uu, ctx.stream, s.u_nodes, s.u_w);
       }
       AFEM_LAUNCHED();
       if (fork) {
@@ -2968,13 +2992,13 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
         AFEM_HIP(hipStreamWaitEvent(ms, ctx.ev_fork, 0));
       }
       if (small) {
-        if (n_mix > 0) AFEM_STRIP_K(4, 2, 16, 0, n_mix, list_m, s.tickets.p + 128, shm_g, ms);
-        if (use_uni && umode == 2) AFEM_STRIP_K(4, 2, 16, 2, s.n_uni, s.rec_u.p, s.tickets.p, shm_u, ctx.stream);
-        else if (use_uni) AFEM_STRIP_K(4, 2, 16, 1, s.n_uni, s.rec_u.p, s.tickets.p, shm_u, ctx.stream);
+        if (n_mix > 0) AFEM_STRIP_K(4, 2, 16, 0, n_mix, list_m, tk0 + 128, shm_g, ms);
+        if (use_uni && umode == 2) AFEM_STRIP_K(4, 2, 16, 2, s.n_uni, s.rec_u.p, tk0, shm_u, ctx.stream);
+        else if (use_uni) AFEM_STRIP_K(4, 2, 16, 1, s.n_uni, s.rec_u.p, tk0, shm_u, ctx.stream);
       }
       else {
-        if (n_mix > 0) AFEM_STRIP_K(4, 4, 32, 0, n_mix, list_m, s.tickets.p + 128, shm_g, ms);
-        if (use_uni) AFEM_STRIP_K(4, 4, 32, 1, s.n_uni, s.rec_u.p, s.tickets.p, shm_u, ctx.stream);
+        if (n_mix > 0) AFEM_STRIP_K(4, 4, 32, 0, n_mix, list_m, tk0 + 128, shm_g, ms);
+        if (use_uni) AFEM_STRIP_K(4, 4, 32, 1, s.n_uni, s.rec_u.p, tk0, shm_u, ctx.stream);
       }
       AFEM_LAUNCHED();
       if (fork) {
@@ -2983,8 +3007,8 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       }
     }
     else {
-      if (small) AFEM_STRIP_K(3, 2, 16, 0, s.n_slices, s.rec_all.p, s.tickets.p + 128, shm_g, ctx.stream);
-      else AFEM_STRIP_K(3, 4, 32, 0, s.n_slices, s.rec_all.p, s.tickets.p + 128, shm_g, ctx.stream);
+      if (small) AFEM_STRIP_K(3, 2, 16, 0, s.n_slices, s.rec_all.p, tk0 + 128, shm_g, ctx.stream);
+      else AFEM_STRIP_K(3, 4, 32, 0, s.n_slices, s.rec_all.p, tk0 + 128, shm_g, ctx.stream);
     }
 #undef AFEM_STRIP_K
     AFEM_LAUNCHED();
@@ -3089,8 +3113,7 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
     // stream: the few large slices no longer set the LDS tile (and the
     // occupancy) of all
     static std::map<std::pair<const void*, size_t>, int> occ_big;
-    if (s.tickets.n < 3 * 8 * 16) s.tickets.alloc(3 * 8 * 16);
-    AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
+    unsigned long long* const tk0 = next_tickets(s, ctx);  // this assembly's claim counters
     auto launch = [&](const void* fn, auto kern, int64_t n_list, const SliceRec* list, unsigned long long* tk,
                       int ucap, int wcap, hipStream_t st) {
       const size_t shm = (size_t)elast_tile_bytes(ucap, wcap);
@@ -3113,7 +3136,7 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
                        elast_tile_bytes(s.mb_nodes, s.mb_w) <= 160 * 1024;
     if (!split) {
       launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<4, 32, 0, true>), k_assemble_elast_strip<4, 32, 0, true>,
-             s.n_slices, s.rec_all.p, s.tickets.p, s.max_slice_nodes, s.max_slice_w, ctx.stream);
+             s.n_slices, s.rec_all.p, tk0, s.max_slice_nodes, s.max_slice_w, ctx.stream);
     }
     else {
       const bool fork = s.n_mb > 0;
@@ -3125,13 +3148,13 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
       }
       if (s.n_mb > 0)
         launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<4, 32, 0, true>),
-               k_assemble_elast_strip<4, 32, 0, true>, s.n_mb, s.rec_mb.p, s.tickets.p + 256, s.mb_nodes, s.mb_w, side);
+               k_assemble_elast_strip<4, 32, 0, true>, s.n_mb, s.rec_mb.p, tk0 + 256, s.mb_nodes, s.mb_w, side);
       if (s.n_ms > 0)
         launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16, 0, true>),
-               k_assemble_elast_strip<2, 16, 0, true>, s.n_ms, s.rec_ms.p, s.tickets.p + 128, c_nodes, 16, ctx.stream);
+               k_assemble_elast_strip<2, 16, 0, true>, s.n_ms, s.rec_ms.p, tk0 + 128, c_nodes, 16, ctx.stream);
       if (s.n_uni > 0)
         launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16, 0, true>),
-               k_assemble_elast_strip<2, 16, 0, true>, s.n_uni, s.rec_u.p, s.tickets.p, c_nodes, 16, ctx.stream);
+               k_assemble_elast_strip<2, 16, 0, true>, s.n_uni, s.rec_u.p, tk0, c_nodes, 16, ctx.stream);
       if (fork) {
         AFEM_HIP(hipEventRecord(ctx.ev_join, side));
         AFEM_HIP(hipStreamWaitEvent(ctx.stream, ctx.ev_join, 0));
@@ -3162,8 +3185,7 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
     // stencil split (AFEM_ASSEMBLY_STENCIL=0: the whole uniform list through the uniform instance)
     const char* ke = variant("AFEM_ASSEMBLY_STENCIL");
     const bool use_k = use_uni && s.n_k0 > 0 && !(ke && atoi(ke) == 0);
-    if (s.tickets.n < 4 * 8 * 16) s.tickets.alloc(4 * 8 * 16);
-    AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
+    unsigned long long* const tk0 = next_tickets(s, ctx);  // this assembly's claim counters
     auto launch = [&](const void* fn, auto kern, int64_t n_items, const SliceRec* list, unsigned long long* tk,
                       const uint8_t* slots = nullptr) {
       auto it = occ_wg.find({ fn, shm });
@@ -3182,18 +3204,18 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
     };
     if (use_k) {
       launch(reinterpret_cast<const void*>(&k_assemble_elast_wg<2, 16, 3>), k_assemble_elast_wg<2, 16, 3>, s.n_k0,
-             s.rec_k0.p, s.tickets.p + 384);
+             s.rec_k0.p, tk0 + 384);
       if (s.n_u1 > 0)
         launch(reinterpret_cast<const void*>(&k_assemble_elast_wg<2, 16, 1>), k_assemble_elast_wg<2, 16, 1>, s.n_u1,
-               s.rec_u1.p, s.tickets.p, s.u1slot.p);
+               s.rec_u1.p, tk0, s.u1slot.p);
     }
     else if (use_uni)
       launch(reinterpret_cast<const void*>(&k_assemble_elast_wg<2, 16, 1>), k_assemble_elast_wg<2, 16, 1>, s.n_uni,
-             s.rec_u.p, s.tickets.p);
+             s.rec_u.p, tk0);
     const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;
     if (n_mix > 0)
       launch(reinterpret_cast<const void*>(&k_assemble_elast_wg<2, 16, 0>), k_assemble_elast_wg<2, 16, 0>, n_mix,
-             use_uni ? s.rec_m.p : s.rec_all.p, s.tickets.p + 128);
+             use_uni ? s.rec_m.p : s.rec_all.p, tk0 + 128);
     b.last_kernel = AFEM_KERNEL_ELAST3_WG;
     return;
   }
@@ -3208,8 +3230,7 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
     // AFEM_ASSEMBLY_UNIFORM=0: every slice through the general instance (diagnostic)
     const char* ue = variant("AFEM_ASSEMBLY_UNIFORM");
     const bool use_uni = !(ue && atoi(ue) == 0) && s.n_uni > 0;
-    if (!s.tickets.p) s.tickets.alloc(2 * 8 * 16);
-    AFEM_HIP(hipMemsetAsync(s.tickets.p, 0, s.tickets.bytes(), ctx.stream));
+    unsigned long long* const tk0 = next_tickets(s, ctx);  // this assembly's claim counters
     auto launch = [&](const void* fn, auto kern, int64_t n_items, const SliceRec* list, unsigned long long* tk) {
       auto it = occ.find({ fn, shm2 });
       if (it == occ.end()) {
@@ -3226,11 +3247,11 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
     };
     if (use_uni)
       launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16, 1>), k_assemble_elast_strip<2, 16, 1>,
-             3 * s.n_uni, s.rec_u.p, s.tickets.p);
+             3 * s.n_uni, s.rec_u.p, tk0);
     const int64_t n_mix = use_uni ? s.n_mix : s.n_slices;
     if (n_mix > 0)
       launch(reinterpret_cast<const void*>(&k_assemble_elast_strip<2, 16, 0>), k_assemble_elast_strip<2, 16, 0>,
-             3 * n_mix, use_uni ? s.rec_m.p : s.rec_all.p, s.tickets.p + 128);
+             3 * n_mix, use_uni ? s.rec_m.p : s.rec_all.p, tk0 + 128);
     b.last_kernel = AFEM_KERNEL_ELAST3_STRIP;
     return;
   }

@@ -85,22 +85,40 @@ __global__ void k_apply_bcs(int64_t n_rows, const int64_t* __restrict__ rows, co
                             const double* __restrict__ forced_value, const uint8_t* __restrict__ elim_info,
                             const double* __restrict__ elim_value, double* __restrict__ rhs)
 {
-  int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= n_rows) return;
-  const uint8_t ei = elim_info[d];
-  const uint8_t fi = forced_info[d];
-  if (!ei && !fi) return;
-  const int64_t b = rows[d], e = rows[d + 1];
-  if (ei) {
-    for (int64_t k = b; k < e; ++k) vals[k] = (cols[k] == (int32_t)d) ? 1.0 : 0.0;
-    rhs[d] = elim_value[d];
+  // 16 rows per thread: the two flag arrays are read with one 16-B load each
+  // (a thread per row was bound by wave launches, not by the 2 B per row)
+  const int64_t d0 = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (d0 >= n_rows) return;
+  union Flags {
+    uint4 v;
+    uint8_t b[16];
+  } fi, ei;
+  if (d0 + 16 <= n_rows) {
+    fi.v = *reinterpret_cast<const uint4*>(forced_info + d0);
+    ei.v = *reinterpret_cast<const uint4*>(elim_info + d0);
   }
-  if (fi) {
-    for (int64_t k = b; k < e; ++k)
-      if (cols[k] == (int32_t)d) {
-        vals[k] = forced_value[d];
-        break;
-      }
+  else {
+    for (int i = 0; i < 16; ++i) {
+      fi.b[i] = d0 + i < n_rows ? forced_info[d0 + i] : 0;
+      ei.b[i] = d0 + i < n_rows ? elim_info[d0 + i] : 0;
+    }
+  }
+  if (!(fi.v.x | fi.v.y | fi.v.z | fi.v.w | ei.v.x | ei.v.y | ei.v.z | ei.v.w)) return;
+  for (int i = 0; i < 16; ++i) {
+    const int64_t d = d0 + i;
+    if (!ei.b[i] && !fi.b[i]) continue;
+    const int64_t b = rows[d], e = rows[d + 1];
+    if (ei.b[i]) {
+      for (int64_t k = b; k < e; ++k) vals[k] = (cols[k] == (int32_t)d) ? 1.0 : 0.0;
+      rhs[d] = elim_value[d];
+    }
+    if (fi.b[i]) {
+      for (int64_t k = b; k < e; ++k)
+        if (cols[k] == (int32_t)d) {
+          vals[k] = forced_value[d];
+          break;
+        }
+    }
   }
 }
 
@@ -1506,7 +1524,7 @@ void ls_apply_bcs(LinearSystem& ls)
                        ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.elim_info.p, ls.elim_value.p, ls.rhs.p);
     AFEM_LAUNCHED();
   }
-  hipLaunchKernelGGL(k_apply_bcs, dim3(grid_for(ls.n_rows, kThreads)), dim3(kThreads), 0, ctx.stream, ls.n_rows,
+  hipLaunchKernelGGL(k_apply_bcs, dim3(grid_for((ls.n_rows + 15) / 16, kThreads)), dim3(kThreads), 0, ctx.stream, ls.n_rows,
                      ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.forced_info.p, ls.forced_value.p, ls.elim_info.p,
                      ls.elim_value.p, ls.rhs.p);
   AFEM_LAUNCHED();
