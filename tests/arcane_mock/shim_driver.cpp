@@ -1,0 +1,242 @@
+// TEST DRIVER of the Arcane-side shim (shim/AfemDoFLinearSystem.cc, shim/BSRFormat.h)
+// against the single-subdomain Arcane mock (tests/arcane_mock/arcane_mock.hpp): it does
+// what an ArcaneFEM module does with the linear-system service, through the shim's
+// classes only, and writes the solutions for tests/test_gpu_shim.py to compare with the
+// oracle.
+//
+//   csr   : modules/poisson/FemModule.cc with the GPU BSR branch -- the module builds the
+//           CSR, hands it over with setCSRValues (host memory), its BC code writes
+//           rhs / forced info / forced value (penalty, femutils/ArcaneFemFunctionsGpu.h:
+//           434-457), then solve() (HypreDoFLinearSystemImpl semantics);
+//   add   : the sequential path -- matrixAddValue per entry, eliminateRow for the
+//           Dirichlet DoFs (AlephDoFLinearSystemImpl semantics);
+//   bsr   : BSRFormat<1> of the shim: initialize / computeSparsity / assembleBilinear(the
+//           module's element lambda) / toLinearSystem (device CSR view), then the
+//           penalty and solve() -- modules/poisson/FemModule.cc:261-272 unchanged.
+//
+// usage: shim_driver <case.bin> <out.bin>
+//   case.bin: int32 dim, nv; int64 n_nodes, n_cells; f64 coords[3 n]; i32 cells[nv nc];
+//             int64 n_dir; i32 dir[n_dir]; f64 dir_value; int64 nnz; i32 rows[n+1];
+//             i32 cols[nnz]; f64 vals[nnz]; f64 rhs[n]; f64 coef
+//   out.bin : f64 x_csr[n], x_add[n], x_bsr[n]
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <vector>
+
+#include "BSRFormat.h"
+#include "DoFLinearSystem.h"
+#include "IDoFLinearSystemFactory.h"
+
+using namespace Arcane::FemUtils;
+
+namespace
+{
+template <class T>
+bool rd(FILE* f, T* p, size_t n)
+{
+  return fread(p, sizeof(T), n, f) == n;
+}
+
+struct Case
+{
+  int32_t dim = 3, nv = 4;
+  int64_t n = 0, nc = 0, nnz = 0;
+  std::vector<double> coords, vals, rhs;
+  std::vector<int32_t> cells, dir, rows, cols;
+  double dir_value = 0, coef = 1;
+};
+
+bool load(const char* path, Case& c)
+{
+  FILE* f = fopen(path, "rb");
+  if (!f)
+    return false;
+  int64_t nd = 0;
+  bool ok = rd(f, &c.dim, 1) && rd(f, &c.nv, 1) && rd(f, &c.n, 1) && rd(f, &c.nc, 1);
+  if (ok) {
+    c.coords.resize(3 * c.n);
+    c.cells.resize(c.nv * c.nc);
+    ok = rd(f, c.coords.data(), c.coords.size()) && rd(f, c.cells.data(), c.cells.size()) && rd(f, &nd, 1);
+  }
+  if (ok) {
+    c.dir.resize(nd);
+    ok = rd(f, c.dir.data(), nd) && rd(f, &c.dir_value, 1) && rd(f, &c.nnz, 1);
+  }
+  if (ok) {
+    c.rows.resize(c.n + 1);
+    c.cols.resize(c.nnz);
+    c.vals.resize(c.nnz);
+    c.rhs.resize(c.n);
+    ok = rd(f, c.rows.data(), c.n + 1) && rd(f, c.cols.data(), c.nnz) && rd(f, c.vals.data(), c.nnz) &&
+         rd(f, c.rhs.data(), c.n) && rd(f, &c.coef, 1);
+  }
+  fclose(f);
+  return ok;
+}
+
+// the service a case file names (AfemLinearSystem), made by its registered factory
+DoFLinearSystemImpl* make_linear_system(IItemFamily* dofs)
+{
+  auto& reg = mockServiceRegistry<IDoFLinearSystemFactory>();
+  auto it = reg.find("AfemLinearSystem");
+  if (it == reg.end())
+    throw FatalErrorException("service AfemLinearSystem is not registered");
+  ServiceBuildInfo sbi;
+  std::unique_ptr<IDoFLinearSystemFactory> factory(it->second(sbi));
+  ISubDomain sd;
+  return factory->createInstance(&sd, dofs, "Afem");
+}
+
+// the module's penalty BC kernel (ArcaneFemFunctionsGpu.h:434-457) on the variables
+void penalty(DoFLinearSystem& ls, const Case& c, double p = 1.0e30)
+{
+  for (int32_t d : c.dir) {
+    ls.getForcedInfo()[DoFLocalId(d)] = true;
+    ls.getForcedValue()[DoFLocalId(d)] = p;
+    ls.rhsVariable()[DoFLocalId(d)] = p * c.dir_value;
+  }
+}
+
+std::vector<double> solution(DoFLinearSystem& ls, int64_t n)
+{
+  std::vector<double> x(n);
+  for (int64_t i = 0; i < n; ++i)
+    x[i] = ls.solutionVariable()[DoFLocalId((Int32)i)];
+  return x;
+}
+
+std::vector<double> run_csr(IItemFamily* dofs, const Case& c)
+{
+  DoFLinearSystem ls(make_linear_system(dofs));
+  std::vector<int32_t> rnc(c.n);
+  for (int64_t i = 0; i < c.n; ++i)
+    rnc[i] = c.rows[i + 1] - c.rows[i];
+  std::vector<double> vals = c.vals;  // the module's CSR values (the view is not owning)
+  CSRFormatView v(Span<const Int32>(c.rows.data(), c.n), Span<const Int32>(rnc.data(), c.n),
+                  Span<const Int32>(c.cols.data(), c.nnz), Span<Real>(vals.data(), c.nnz));
+  ls.setCSRValues(v);
+  for (int64_t i = 0; i < c.n; ++i)
+    ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs[i];
+  penalty(ls, c);
+  ls.solve();
+  return solution(ls, c.n);
+}
+
+std::vector<double> run_add(IItemFamily* dofs, const Case& c)
+{
+  DoFLinearSystem ls(make_linear_system(dofs));
+  for (int64_t i = 0; i < c.n; ++i)
+    for (int32_t k = c.rows[i]; k < c.rows[i + 1]; ++k)
+      ls.matrixAddValue(DoFLocalId((Int32)i), DoFLocalId(c.cols[k]), c.vals[k]);
+  for (int64_t i = 0; i < c.n; ++i)
+    ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs[i];
+  for (int32_t d : c.dir)
+    ls.eliminateRow(DoFLocalId(d), c.dir_value);
+  ls.solve();
+  return solution(ls, c.n);
+}
+
+std::vector<double> run_bsr(IMesh* mesh, IItemFamily* dofs, const Case& c)
+{
+  // the module's element lambda (modules/poisson/FemModule.cc:261-272 +
+  // FemModule.h:177-186): vol * coef * grad_i . grad_j from the captured geometry
+  double* d_coords = nullptr;
+  int32_t* d_cells = nullptr;
+  if (hipMalloc(&d_coords, sizeof(double) * c.coords.size()) != hipSuccess ||
+      hipMalloc(&d_cells, sizeof(int32_t) * c.cells.size()) != hipSuccess)
+    throw FatalErrorException("hipMalloc");
+  (void)hipMemcpy(d_coords, c.coords.data(), sizeof(double) * c.coords.size(), hipMemcpyHostToDevice);
+  (void)hipMemcpy(d_cells, c.cells.data(), sizeof(int32_t) * c.cells.size(), hipMemcpyHostToDevice);
+  const double coef = c.coef;
+  auto element = [=] __device__(CellLocalId cell) {
+    double x[4][3];
+    for (int a = 0; a < 4; ++a)
+      for (int d = 0; d < 3; ++d)
+        x[a][d] = d_coords[3 * (int64_t)d_cells[4 * (int64_t)cell.localId() + a] + d];
+    double e[3][3];
+    for (int a = 0; a < 3; ++a)
+      for (int d = 0; d < 3; ++d)
+        e[a][d] = x[a + 1][d] - x[0][d];
+    double g[4][3];
+    // cofactors of the edge matrix: det * grad(lambda_a), a = 1..3; grad(lambda_0) = -sum
+    for (int d = 0; d < 3; ++d) {
+      const int p = (d + 1) % 3, q = (d + 2) % 3;
+      g[1][d] = e[1][p] * e[2][q] - e[1][q] * e[2][p];
+      g[2][d] = e[2][p] * e[0][q] - e[2][q] * e[0][p];
+      g[3][d] = e[0][p] * e[1][q] - e[0][q] * e[1][p];
+      g[0][d] = -(g[1][d] + g[2][d] + g[3][d]);
+    }
+    const double det = e[0][0] * g[1][0] + e[0][1] * g[1][1] + e[0][2] * g[1][2];
+    const double s = coef / (6.0 * fabs(det));
+    afem::generic::FixedMatrix<4, 4> K;
+    for (int a = 0; a < 4; ++a)
+      for (int b = 0; b < 4; ++b)
+        K(a, b) = s * (g[a][0] * g[b][0] + g[a][1] * g[b][1] + g[a][2] * g[b][2]);
+    return K;
+  };
+  ITraceMng tm;
+  RunQueue queue(eMemoryRessource::Device);
+  FemDoFsOnNodes dofs_on_nodes(1);
+  Runner runner(eExecutionPolicy::HIP);
+  std::vector<double> x;
+  {
+    BSRFormat<1> bsr(&tm, queue, dofs_on_nodes);
+    bsr.initialize(mesh, true);
+    bsr.computeSparsity();
+    bsr.assembleBilinear(element);
+    DoFLinearSystem ls(make_linear_system(dofs));
+    ls.setRunner(&runner);  // the CSR arrays of toLinearSystem live in device memory
+    bsr.toLinearSystem(ls);
+    for (int64_t i = 0; i < c.n; ++i)
+      ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs[i];
+    penalty(ls, c);
+    ls.solve();
+    x = solution(ls, c.n);
+  }
+  (void)hipFree(d_coords);
+  (void)hipFree(d_cells);
+  return x;
+}
+} // namespace
+
+int main(int argc, char** argv)
+{
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s <case.bin> <out.bin>\n", argv[0]);
+    return 2;
+  }
+  Case c;
+  if (!load(argv[1], c) || c.dim != 3 || c.nv != 4) {
+    fprintf(stderr, "bad case file %s\n", argv[1]);
+    return 2;
+  }
+  try {
+    ITraceMng tm;
+    IParallelMng pm;
+    IItemFamily nodes((Int32)c.n, (Int32)c.n, &pm, &tm);
+    IItemFamily cells((Int32)c.nc, (Int32)c.nc, &pm, &tm);
+    cells.nv = c.nv;
+    cells.cell_node = c.cells;
+    IItemFamily dofs((Int32)c.n, (Int32)c.n, &pm, &tm);  // one DoF per node, lid = node lid
+    IMesh mesh(3, &nodes, &cells, &pm);
+    for (int64_t i = 0; i < c.n; ++i)
+      mesh.nodesCoordinates()[NodeLocalId((Int32)i)] = Real3{ c.coords[3 * i], c.coords[3 * i + 1], c.coords[3 * i + 2] };
+    const std::vector<double> a = run_csr(&dofs, c);
+    const std::vector<double> b = run_add(&dofs, c);
+    const std::vector<double> d = run_bsr(&mesh, &dofs, c);
+    FILE* f = fopen(argv[2], "wb");
+    if (!f)
+      return 1;
+    fwrite(a.data(), 8, a.size(), f);
+    fwrite(b.data(), 8, b.size(), f);
+    fwrite(d.data(), 8, d.size(), f);
+    fclose(f);
+  }
+  catch (const std::exception& e) {
+    fprintf(stderr, "shim_driver: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}
