@@ -1392,39 +1392,42 @@ __global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, co
 
 // Shared factors of a step's three window blocks (rotated frame: component
 // row x; c_row = -m, the sign folded into s < 0):
-//   K_rb^{0j} = s [lambda m_x c_j + mu (m_j c_x + delta_0j m.c)] + delta_0j mass
-// lm = lambda m_x, mm = mu m once per step; per block 3 + 3 + 3 FP64 ops and
-// the scale s applied last (a uniform padding step's huge s meets only
-// finite products: no inf * 0).
+//   K_rb^{00} = s [(lambda + 2 mu) m_x c_x + mu m_y c_y + mu m_z c_z] + mass
+//   K_rb^{01} = s [lambda m_x c_y + mu m_y c_x],  K_rb^{02} = s [lambda m_x c_z + mu m_z c_x]
+// with the scale folded into four per-step factors A = s (lambda + 2 mu) m_x,
+// B = s mu m_y, C = s mu m_z, D = s lambda m_x (7 FP64 operations per step):
+// per block then 3 + 2 + 2 fused multiply-adds and one add (the mass), the
+// accumulation included -- 8 operations instead of 12.  (A uniform padding
+// step's huge s meets finite m: the factors stay finite, and they only feed
+// the diagonal slot's sink.)
 struct ElastPre {
-  double lm, l0;
-  V3 mm;
+  double A, B, C, D;
 };
-__device__ __forceinline__ ElastPre elast_pre(V3 m, double lambda, double mu)
+__device__ __forceinline__ ElastPre elast_pre(V3 m, double s, double lambda, double mu)
 {
-  ElastPre e;
-  e.lm = lambda * m.x;
-  e.mm = V3{ mu * m.x, mu * m.y, mu * m.z };
-  e.l0 = e.lm + e.mm.x;
-  return e;
+  const double sx = s * m.x, sy = s * m.y, sz = s * m.z;
+  return ElastPre{ (lambda + 2.0 * mu) * sx, mu * sy, mu * sz, lambda * sx };
 }
-__device__ __forceinline__ void elast_block(double* a, const ElastPre& e, V3 c, double s, double mass)
+// explicit fma throughout: one rounding sequence whatever the instance (the
+// uniform and general instances, the one-wave and workgroup kernels agree bit
+// for bit)
+__device__ __forceinline__ void elast_block(double* a, const ElastPre& e, V3 c, double mass)
 {
-  // explicit fma: one rounding sequence whatever the instance (the uniform and
-  // general instances, and the one-wave and workgroup kernels, agree bit for bit)
-  const double t = fma(e.mm.z, c.z, fma(e.mm.y, c.y, e.mm.x * c.x));
-  atomicAdd(a, fma(fma(e.l0, c.x, t), s, mass));
-  atomicAdd(a + 64, fma(e.lm, c.y, e.mm.y * c.x) * s);
-  atomicAdd(a + 128, fma(e.lm, c.z, e.mm.z * c.x) * s);
+  atomicAdd(a, fma(e.A, c.x, fma(e.B, c.y, fma(e.C, c.z, mass))));
+  atomicAdd(a + 64, fma(e.D, c.y, e.B * c.x));
+  atomicAdd(a + 128, fma(e.D, c.z, e.C * c.x));
 }
 // the same three entries added to register partial sums g (register-window
-// accumulation); explicit fma throughout, so no instance is left to the
-// compiler's contraction choices (instances agree bit for bit)
-__device__ __forceinline__ V3 elast_acc(V3 g, const ElastPre& e, V3 c, double s, double mass)
+// accumulation)
+__device__ __forceinline__ V3 elast_acc(V3 g, const ElastPre& e, V3 c, double mass)
 {
-  const double t = fma(e.mm.z, c.z, fma(e.mm.y, c.y, e.mm.x * c.x));
-  return V3{ fma(fma(e.l0, c.x, t), s, mass) + g.x, fma(fma(e.lm, c.y, e.mm.y * c.x), s, g.y),
-             fma(fma(e.lm, c.z, e.mm.z * c.x), s, g.z) };
+  return V3{ fma(e.A, c.x, fma(e.B, c.y, fma(e.C, c.z, add_nc(g.x, mass)))), fma(e.D, c.y, fma(e.B, c.x, g.y)),
+             fma(e.D, c.z, fma(e.C, c.x, g.z)) };
+}
+// a node's first step in the window (its partial sums start here)
+__device__ __forceinline__ V3 elast_first(const ElastPre& e, V3 c, double mass)
+{
+  return V3{ fma(e.A, c.x, fma(e.B, c.y, fma(e.C, c.z, mass))), fma(e.D, c.y, e.B * c.x), fma(e.D, c.z, e.C * c.x) };
 }
 // flush a window node's register partial sums into its LDS accumulators [k][lane] (stride 64)
 __device__ __forceinline__ void flush3(double* a, V3 g)
@@ -1607,7 +1610,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
     auto sel = [](bool c, V3 a, V3 b) { return V3{ c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z }; };
     auto keep = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
     // entries (0, k) of K_rb in the rotated frame, c_r = -m (sign folded into s < 0)
-    auto block = [&](double* a, const ElastPre& e, V3 cb, double s, double mass) { elast_block(a, e, cb, s, mass); };
+    auto block = [&](double* a, const ElastPre& e, V3 cb, double mass) { elast_block(a, e, cb, mass); };
     auto step = [&](uint32_t byte, V3 xd) {
       const bool swap = (byte & 0xC0u) == 0x40u;
       const uint64_t em = (uint64_t)0 - (uint64_t)(byte < 0x80u);
@@ -1627,10 +1630,10 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
       const double s = keep(em, -recip1(6.0 * meas));
       const double mass = keep(em, c0 * meas * (1.0 / 120.0));
       macc += keep(em, meas);
-      const ElastPre e = elast_pre(m, lambda, mu);
-      block(aP, e, cP, s, mass);
-      block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
-      block(aR, e, cRn, s, mass);
+      const ElastPre e = elast_pre(m, s, lambda, mu);
+      block(aP, e, cP, mass);
+      block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, mass);
+      block(aR, e, cRn, mass);
     };
     auto byte_at = [&](int j) -> uint32_t {
       const u32x4 w = cur.ch[j >> 4];
@@ -1668,10 +1671,10 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
         const double s = -recip1(6.0 * fmax(meas, 1e-300));
         const double mass = c0 * meas * (1.0 / 120.0);
         macc += meas;
-        const ElastPre e = elast_pre(m, lambda, mu);
-        block(aP, e, cP, s, mass);
-        block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
-        block(aR, e, cRn, s, mass);
+        const ElastPre e = elast_pre(m, s, lambda, mu);
+        block(aP, e, cP, mass);
+        block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, mass);
+        block(aR, e, cRn, mass);
       };
       {
         const uint32_t b0 = byte_at(0), b1 = byte_at(1);
@@ -2067,10 +2070,10 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         const double s = -recip1(6.0 * (UMODE == 3 ? meas : fmax(meas, 1e-300)));
         const double mass = c0 * meas * (1.0 / 120.0);
         macc += meas;
-        const ElastPre e = elast_pre(m, lambda, mu);
-        gP = elast_acc(gP, e, cP, s, mass);
-        gQ = elast_acc(gQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
-        gR = elast_acc(V3{ 0.0, 0.0, 0.0 }, e, cRn, s, mass);
+        const ElastPre e = elast_pre(m, s, lambda, mu);
+        gP = elast_acc(gP, e, cP, mass);
+        gQ = elast_acc(gQ, e, V3{ -cN.x, -cN.y, -cN.z }, mass);
+        gR = elast_first(e, cRn, mass);
       };
       // bytes(j): step j's byte, swp(j): step j is a swap (scalar, or constants)
       auto run = [&](auto bytes, auto swp, auto fst) {
@@ -2134,10 +2137,10 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         const double s = keep(em, -recip1(6.0 * meas));
         const double mass = keep(em, c0 * meas * (1.0 / 120.0));
         macc += keep(em, meas);
-        const ElastPre e = elast_pre(m, lambda, mu);
-        gP = elast_acc(gP, e, cP, s, mass);
-        gQ = elast_acc(gQ, e, V3{ -cN.x, -cN.y, -cN.z }, s, mass);
-        gR = elast_acc(V3{ 0.0, 0.0, 0.0 }, e, cRn, s, mass);
+        const ElastPre e = elast_pre(m, s, lambda, mu);
+        gP = elast_acc(gP, e, cP, mass);
+        gQ = elast_acc(gQ, e, V3{ -cN.x, -cN.y, -cN.z }, mass);
+        gR = elast_first(e, cRn, mass);
       };
       int u1 = lidx_of(byte_at(0));
       V3 xc = coord(u1);
