@@ -1403,10 +1403,19 @@ __global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, co
 struct ElastPre {
   double A, B, C, D;
 };
-__device__ __forceinline__ ElastPre elast_pre(V3 m, double s, double lambda, double mu)
+// kernel constants: the 1/6 of the element scale 1/(6|det|) and the mass
+// factor c0/120 folded in once (s = -1/|det| per step)
+struct ElastK {
+  double a, b, d, m120;
+};
+__device__ __forceinline__ ElastK elast_consts(double lambda, double mu, double c0)
+{
+  return ElastK{ (lambda + 2.0 * mu) * (1.0 / 6.0), mu * (1.0 / 6.0), lambda * (1.0 / 6.0), c0 * (1.0 / 120.0) };
+}
+__device__ __forceinline__ ElastPre elast_pre(V3 m, double s, const ElastK& k)
 {
   const double sx = s * m.x, sy = s * m.y, sz = s * m.z;
-  return ElastPre{ (lambda + 2.0 * mu) * sx, mu * sy, mu * sz, lambda * sx };
+  return ElastPre{ k.a * sx, k.b * sy, k.b * sz, k.d * sx };
 }
 // explicit fma throughout: one rounding sequence whatever the instance (the
 // uniform and general instances, the one-wave and workgroup kernels agree bit
@@ -1478,6 +1487,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
                                                              double mu, double c0, double fx, double fy, double fz,
                                                              double* __restrict__ vals, double* __restrict__ rhs, int rhs_add)
 {
+  const ElastK ek = elast_consts(lambda, mu, c0);
   extern __shared__ __align__(16) unsigned char smem[];
   double* acc = reinterpret_cast<double*>(smem);  // [slot][k][lane]
   double* cxyz = reinterpret_cast<double*>(smem + 3 * 8 * 64 * (int64_t)w_cap);
@@ -1627,10 +1637,10 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
       cN = cross(eP, eR);
       const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
       const double meas = fabs(dot(eP, cP));
-      const double s = keep(em, -recip1(6.0 * meas));
-      const double mass = keep(em, c0 * meas * (1.0 / 120.0));
+      const double s = keep(em, -recip1(meas));
+      const double mass = keep(em, meas * ek.m120);
       macc += keep(em, meas);
-      const ElastPre e = elast_pre(m, s, lambda, mu);
+      const ElastPre e = elast_pre(m, s, ek);
       block(aP, e, cP, mass);
       block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, mass);
       block(aR, e, cRn, mass);
@@ -1668,10 +1678,10 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
         cN = cross(eP, eR);
         const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
         const double meas = fabs(dot(eP, cP));
-        const double s = -recip1(6.0 * fmax(meas, 1e-300));
-        const double mass = c0 * meas * (1.0 / 120.0);
+        const double s = -recip1(fmax(meas, 1e-300));
+        const double mass = meas * ek.m120;
         macc += meas;
-        const ElastPre e = elast_pre(m, s, lambda, mu);
+        const ElastPre e = elast_pre(m, s, ek);
         block(aP, e, cP, mass);
         block(aQ, e, V3{ -cN.x, -cN.y, -cN.z }, mass);
         block(aR, e, cRn, mass);
@@ -1850,6 +1860,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
                                                            int rhs_add, const uint8_t* __restrict__ strip_u,
                                                            const SlotRec* __restrict__ uslots)
 {
+  const ElastK ek = elast_consts(lambda, mu, c0);
   // UMODE = 1 (uniform slices, as the scalar uniform instance): the slot bytes
   // come from the slice's common 32-B slot stream (scalar loads), each step's
   // coordinates from the lane's local-index stream (strip_u): no column-index
@@ -2067,10 +2078,10 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         cN = cross(eP, eR);
         const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
         const double meas = fabs(dot(eP, cP));
-        const double s = -recip1(6.0 * (UMODE == 3 ? meas : fmax(meas, 1e-300)));
-        const double mass = c0 * meas * (1.0 / 120.0);
+        const double s = -recip1(UMODE == 3 ? meas : fmax(meas, 1e-300));
+        const double mass = meas * ek.m120;
         macc += meas;
-        const ElastPre e = elast_pre(m, s, lambda, mu);
+        const ElastPre e = elast_pre(m, s, ek);
         gP = elast_acc(gP, e, cP, mass);
         gQ = elast_acc(gQ, e, V3{ -cN.x, -cN.y, -cN.z }, mass);
         gR = elast_first(e, cRn, mass);
@@ -2134,10 +2145,10 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
         cN = cross(eP, eR);
         const V3 m = V3{ cP.x - cN.x + cRn.x, cP.y - cN.y + cRn.y, cP.z - cN.z + cRn.z };
         const double meas = fabs(dot(eP, cP));
-        const double s = keep(em, -recip1(6.0 * meas));
-        const double mass = keep(em, c0 * meas * (1.0 / 120.0));
+        const double s = keep(em, -recip1(meas));
+        const double mass = keep(em, meas * ek.m120);
         macc += keep(em, meas);
-        const ElastPre e = elast_pre(m, s, lambda, mu);
+        const ElastPre e = elast_pre(m, s, ek);
         gP = elast_acc(gP, e, cP, mass);
         gQ = elast_acc(gQ, e, V3{ -cN.x, -cN.y, -cN.z }, mass);
         gR = elast_first(e, cRn, mass);

@@ -31,11 +31,12 @@
  * layout once per structure).  Otherwise toLinearSystem goes through
  * matrixAddValue per entry, as BSRMatrix::toLinearSystem does (:261-280).
  *
- * Status: written against the reference's interfaces; it needs Arcane to
- * compile and has not been compiled here (Arcane is not installed).  What it
- * drives is tested: the generic entry by tests/test_gpu_generic.py
- * (examples/generic_assembly.hip, a hipcc-compiled device lambda), the
- * structure / CSR export by tests/test_gpu_boundary.py.
+ * Status: written against the reference's interfaces; Arcane is not
+ * installed here, so it is compiled against the single-subdomain Arcane mock
+ * of tests/arcane_mock/ (test infrastructure) and run on the GPU by
+ * tests/test_gpu_shim.py: initialize / computeSparsity / assembleBilinear(a
+ * device element lambda) / toLinearSystem / solve on the reference's
+ * sphere_3D case, equal to the oracle and the golden.
  */
 #ifndef AFEM_SHIM_BSRFORMAT_H
 #define AFEM_SHIM_BSRFORMAT_H
