@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cstdint>
 #include <cstring>
 #include <deque>
@@ -27,6 +29,7 @@
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace Arcane
@@ -279,18 +282,128 @@ namespace Parallel
   {};
 } // namespace Parallel
 
+//! the ranks of a mock job: threads of one process sharing this world
+//! (buffered point-to-point mailboxes, barrier-based collectives)
+class MockWorld
+{
+ public:
+
+  explicit MockWorld(Int32 n)
+  : m_n(n)
+  , m_red(n)
+  {}
+  Int32 size() const { return m_n; }
+  void barrier()
+  {
+    std::unique_lock<std::mutex> l(m_mu);
+    const long g = m_gen;
+    if (++m_arrived == m_n) {
+      m_arrived = 0;
+      ++m_gen;
+      m_cv.notify_all();
+    }
+    else
+      m_cv.wait(l, [&] { return m_gen != g; });
+  }
+  void post(Int32 src, Int32 dst, std::vector<Real> data)
+  {
+    std::lock_guard<std::mutex> l(m_mu);
+    m_box[{ src, dst }].push_back(std::move(data));
+    m_cv.notify_all();
+  }
+  std::vector<Real> take(Int32 src, Int32 dst)
+  {
+    std::unique_lock<std::mutex> l(m_mu);
+    auto& q = m_box[{ src, dst }];
+    m_cv.wait(l, [&] { return !q.empty(); });
+    std::vector<Real> v = std::move(q.front());
+    q.pop_front();
+    return v;
+  }
+  //! sum over the ranks in rank order (the same bits on every rank)
+  void reduceSum(Int32 rank, ArrayView<Real> v)
+  {
+    m_red[rank].assign(v.begin(), v.end());
+    barrier();
+    for (Int32 i = 0; i < v.size(); ++i) {
+      Real s = 0;
+      for (Int32 r = 0; r < m_n; ++r)
+        s += m_red[r][i];
+      v[i] = s;
+    }
+    barrier();
+  }
+  std::vector<Byte> bcast;
+
+ private:
+
+  Int32 m_n;
+  std::mutex m_mu;
+  std::condition_variable m_cv;
+  Int32 m_arrived = 0;
+  long m_gen = 0;
+  std::map<std::pair<Int32, Int32>, std::deque<std::vector<Real>>> m_box;
+  std::vector<std::vector<Real>> m_red;
+};
+
 class IParallelMng
 {
  public:
 
-  Int32 commRank() const { return 0; }
-  Int32 commSize() const { return 1; }
-  bool isParallel() const { return false; }
-  void reduce(Parallel::eReduceType, ArrayView<Real>) {}
-  Parallel::Request send(ConstArrayView<Real>, Int32, bool) { throw FatalErrorException("mock: one rank"); }
-  Parallel::Request recv(ArrayView<Real>, Int32, bool) { throw FatalErrorException("mock: one rank"); }
-  void waitAllRequests(ArrayView<Parallel::Request>) {}
-  void broadcast(ArrayView<Byte>, Int32) {}
+  IParallelMng() = default;  // one rank
+  IParallelMng(MockWorld* w, Int32 rank)
+  : m_w(w)
+  , m_rank(rank)
+  {}
+  Int32 commRank() const { return m_rank; }
+  Int32 commSize() const { return m_w ? m_w->size() : 1; }
+  bool isParallel() const { return commSize() > 1; }
+  void reduce(Parallel::eReduceType t, ArrayView<Real> v)
+  {
+    if (t != Parallel::ReduceSum)
+      throw FatalErrorException("mock: ReduceSum only");
+    if (m_w)
+      m_w->reduceSum(m_rank, v);
+  }
+  //! buffered: the data are copied out at once, the request is complete
+  Parallel::Request send(ConstArrayView<Real> v, Int32 dst, bool)
+  {
+    m_w->post(m_rank, dst, std::vector<Real>(v.begin(), v.end()));
+    return {};
+  }
+  //! completed by waitAllRequests
+  Parallel::Request recv(ArrayView<Real> v, Int32 src, bool)
+  {
+    m_pending.emplace_back(v, src);
+    return {};
+  }
+  void waitAllRequests(ArrayView<Parallel::Request>)
+  {
+    for (auto& [v, src] : m_pending) {
+      const std::vector<Real> d = m_w->take(src, m_rank);
+      if ((Int32)d.size() != v.size())
+        throw FatalErrorException("mock: message size mismatch");
+      std::copy(d.begin(), d.end(), v.begin());
+    }
+    m_pending.clear();
+  }
+  void broadcast(ArrayView<Byte> v, Int32 root)
+  {
+    if (!m_w)
+      return;
+    if (m_rank == root)
+      m_w->bcast.assign(v.begin(), v.end());
+    m_w->barrier();
+    if (m_rank != root)
+      std::copy(m_w->bcast.begin(), m_w->bcast.end(), v.begin());
+    m_w->barrier();
+  }
+
+ private:
+
+  MockWorld* m_w = nullptr;
+  Int32 m_rank = 0;
+  std::vector<std::pair<ArrayView<Real>, Int32>> m_pending;
 };
 
 // ------------------------------------------------------------------ items
@@ -392,13 +505,17 @@ using CellGroup = ItemGroup;
 #define ENUMERATE_NODE(name, group) AFEM_MOCK_ENUMERATE(name, group)
 #define ENUMERATE_CELL(name, group) AFEM_MOCK_ENUMERATE(name, group)
 
+//! per communicating rank: the owned items it receives from us (shared) and
+//! our ghosts it owns (FemDoFsOnNodes::computeSynchronizeInfos' lists)
 class IVariableSynchronizer
 {
  public:
 
-  Int32ConstArrayView communicatingRanks() const { return {}; }
-  Int32ConstArrayView sharedItems(Int32) const { return {}; }
-  Int32ConstArrayView ghostItems(Int32) const { return {}; }
+  Int32ConstArrayView communicatingRanks() const { return Int32ConstArrayView((Int32)ranks.size(), ranks.data()); }
+  Int32ConstArrayView sharedItems(Int32 i) const { return Int32ConstArrayView((Int32)shared[i].size(), shared[i].data()); }
+  Int32ConstArrayView ghostItems(Int32 i) const { return Int32ConstArrayView((Int32)ghosts[i].size(), ghosts[i].data()); }
+  std::vector<Int32> ranks;
+  std::vector<std::vector<Int32>> shared, ghosts;
 };
 
 //! a family of items with dense local ids 0..n-1; cells carry their nodes
@@ -476,7 +593,8 @@ class ItemVariableScalarRefT
  public:
 
   explicit ItemVariableScalarRefT(const VariableBuildInfo& vbi)
-  : m_v(vbi.family->maxLocalId())
+  : m_family(vbi.family)
+  , m_v(vbi.family->maxLocalId())
   {}
   ItemVariableScalarRefT(Int32 n)
   : m_v(n)
@@ -484,11 +602,37 @@ class ItemVariableScalarRefT
   void fill(const T& x) { std::fill(m_v.begin(), m_v.end(), x); }
   T& operator[](LID i) { return m_v[i.localId()]; }
   const T& operator[](LID i) const { return m_v[i.localId()]; }
-  void synchronize() {}  // one subdomain: no ghosts to refresh
+  //! the owners' values into the ghosts (Real variables, over the family's synchronizer)
+  void synchronize()
+  {
+    if constexpr (std::is_same_v<T, Real>) {
+      if (!m_family || !m_family->parallelMng()->isParallel())
+        return;
+      IParallelMng* pm = m_family->parallelMng();
+      IVariableSynchronizer* sync = m_family->allItemsSynchronizer();
+      const Int32ConstArrayView ranks = sync->communicatingRanks();
+      std::vector<std::vector<Real>> in(ranks.size());
+      for (Int32 i = 0; i < ranks.size(); ++i) {
+        std::vector<Real> out;
+        for (Int32 lid : sync->sharedItems(i))
+          out.push_back(m_v[lid]);
+        pm->send(ConstArrayView<Real>((Int32)out.size(), out.data()), ranks[i], false);
+        in[i].resize(sync->ghostItems(i).size());
+        pm->recv(ArrayView<Real>((Int32)in[i].size(), in[i].data()), ranks[i], false);
+      }
+      pm->waitAllRequests({});
+      for (Int32 i = 0; i < ranks.size(); ++i) {
+        Int32 k = 0;
+        for (Int32 lid : sync->ghostItems(i))
+          m_v[lid] = in[i][k++];
+      }
+    }
+  }
   Int32 size() const { return (Int32)m_v.size(); }
 
  private:
 
+  IItemFamily* m_family = nullptr;
   std::deque<T> m_v;  // deque<bool> holds real bools (operator[] returns bool&)
 };
 using VariableDoFReal = ItemVariableScalarRefT<DoFLocalId, Real>;

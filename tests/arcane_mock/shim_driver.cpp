@@ -15,6 +15,16 @@
 //           penalty and solve() -- modules/poisson/FemModule.cc:261-272 unchanged.
 //
 // usage: shim_driver <case.bin> <out.bin>
+//        shim_driver par <nranks> <case_prefix> <out_prefix>
+//   par: the csr flow on nranks subdomains at once (threads sharing a MockWorld: the
+//   transport is the shim's IParallelMng one, transport = "host"), with Arcane-style
+//   local ids (owned and ghost DoFs interleaved), the halo from the DoF family's
+//   IVariableSynchronizer (_buildHalo) and the solution synchronised by the shim.
+//   <case_prefix><r>.bin: int64 n, n_cells; f64 coords[3 n]; i32 cells[4 nc];
+//     u8 own[n]; int32 n_nbr; per neighbour: int32 rank, int64 ns, i32 shared[ns],
+//     int64 ng, i32 ghosts[ng]; int64 n_dir; i32 dir[n_dir]; f64 dir_value;
+//     int64 nnz; i32 rows[n+1]; i32 cols[nnz]; f64 vals[nnz]; f64 rhs[n]
+//   <out_prefix><r>.bin: f64 x[n] (every local DoF, ghosts synchronised)
 //   case.bin: int32 dim, nv; int64 n_nodes, n_cells; f64 coords[3 n]; i32 cells[nv nc];
 //             int64 n_dir; i32 dir[n_dir]; f64 dir_value; int64 nnz; i32 rows[n+1];
 //             i32 cols[nnz]; f64 vals[nnz]; f64 rhs[n]; f64 coef
@@ -23,6 +33,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "BSRFormat.h"
@@ -199,10 +211,130 @@ std::vector<double> run_bsr(IMesh* mesh, IItemFamily* dofs, const Case& c)
   (void)hipFree(d_cells);
   return x;
 }
+struct RankCase
+{
+  int64_t n = 0, nc = 0, nnz = 0;
+  std::vector<double> coords, vals, rhs;
+  std::vector<int32_t> cells, dir, rows, cols;
+  std::vector<char> own;
+  std::vector<Int32> nbr;
+  std::vector<std::vector<Int32>> shared, ghosts;
+  double dir_value = 0;
+};
+
+bool load_rank(const std::string& path, RankCase& c)
+{
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f)
+    return false;
+  bool ok = rd(f, &c.n, 1) && rd(f, &c.nc, 1);
+  int32_t nn = 0;
+  int64_t nd = 0;
+  if (ok) {
+    c.coords.resize(3 * c.n);
+    c.cells.resize(4 * c.nc);
+    c.own.resize(c.n);
+    ok = rd(f, c.coords.data(), c.coords.size()) && rd(f, c.cells.data(), c.cells.size()) && rd(f, c.own.data(), c.n) &&
+         rd(f, &nn, 1);
+  }
+  for (int32_t i = 0; ok && i < nn; ++i) {
+    int32_t r = 0;
+    int64_t ns = 0, ng = 0;
+    ok = rd(f, &r, 1) && rd(f, &ns, 1);
+    c.nbr.push_back(r);
+    c.shared.emplace_back(ns);
+    ok = ok && rd(f, c.shared.back().data(), ns) && rd(f, &ng, 1);
+    c.ghosts.emplace_back(ng);
+    ok = ok && rd(f, c.ghosts.back().data(), ng);
+  }
+  if (ok) {
+    ok = rd(f, &nd, 1);
+    c.dir.resize(nd);
+    ok = ok && rd(f, c.dir.data(), nd) && rd(f, &c.dir_value, 1) && rd(f, &c.nnz, 1);
+  }
+  if (ok) {
+    c.rows.resize(c.n + 1);
+    c.cols.resize(c.nnz);
+    c.vals.resize(c.nnz);
+    c.rhs.resize(c.n);
+    ok = rd(f, c.rows.data(), c.n + 1) && rd(f, c.cols.data(), c.nnz) && rd(f, c.vals.data(), c.nnz) &&
+         rd(f, c.rhs.data(), c.n);
+  }
+  fclose(f);
+  return ok;
+}
+
+// one rank of the par mode: the module's Hypre-path calls on its subdomain
+void run_rank(MockWorld* world, Int32 rank, const RankCase& c, std::vector<double>& x, std::string& err)
+{
+  try {
+    ITraceMng tm;
+    IParallelMng pm(world, rank);
+    IItemFamily dofs((Int32)c.n, 0, &pm, &tm);
+    dofs.setOwnMask(c.own);
+    IVariableSynchronizer* sync = dofs.allItemsSynchronizer();
+    sync->ranks = c.nbr;
+    sync->shared = c.shared;
+    sync->ghosts = c.ghosts;
+    DoFLinearSystem ls(make_linear_system(&dofs));
+    std::vector<int32_t> rnc(c.n);
+    for (int64_t i = 0; i < c.n; ++i)
+      rnc[i] = c.rows[i + 1] - c.rows[i];
+    std::vector<double> vals = c.vals;
+    // rows: the reference's layout without the sentinel (HypreDoFLinearSystem.cc:140-141)
+    CSRFormatView v(Span<const Int32>(c.rows.data(), c.n), Span<const Int32>(rnc.data(), c.n),
+                    Span<const Int32>(c.cols.data(), c.nnz), Span<Real>(vals.data(), c.nnz));
+    ls.setCSRValues(v);
+    for (int64_t i = 0; i < c.n; ++i)
+      ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs[i];
+    for (int32_t d : c.dir) {
+      ls.getForcedInfo()[DoFLocalId(d)] = true;
+      ls.getForcedValue()[DoFLocalId(d)] = 1.0e30;
+      ls.rhsVariable()[DoFLocalId(d)] = 1.0e30 * c.dir_value;
+    }
+    ls.solve();
+    x = solution(ls, c.n);
+  }
+  catch (const std::exception& e) {
+    err = e.what();
+  }
+}
+
+int run_par(int nranks, const std::string& in, const std::string& out)
+{
+  std::vector<RankCase> cases(nranks);
+  for (int r = 0; r < nranks; ++r)
+    if (!load_rank(in + std::to_string(r) + ".bin", cases[r])) {
+      fprintf(stderr, "bad case file %s%d.bin\n", in.c_str(), r);
+      return 2;
+    }
+  MockWorld world(nranks);
+  std::vector<std::vector<double>> xs(nranks);
+  std::vector<std::string> errs(nranks);
+  std::vector<std::thread> th;
+  for (int r = 0; r < nranks; ++r)
+    th.emplace_back(run_rank, &world, r, std::cref(cases[r]), std::ref(xs[r]), std::ref(errs[r]));
+  for (auto& t : th)
+    t.join();
+  for (int r = 0; r < nranks; ++r) {
+    if (!errs[r].empty()) {
+      fprintf(stderr, "shim_driver rank %d: %s\n", r, errs[r].c_str());
+      return 1;
+    }
+    FILE* f = fopen((out + std::to_string(r) + ".bin").c_str(), "wb");
+    if (!f)
+      return 1;
+    fwrite(xs[r].data(), 8, xs[r].size(), f);
+    fclose(f);
+  }
+  return 0;
+}
 } // namespace
 
 int main(int argc, char** argv)
 {
+  if (argc >= 5 && std::string(argv[1]) == "par")
+    return run_par(atoi(argv[2]), argv[3], argv[4]);
   if (argc < 3) {
     fprintf(stderr, "usage: %s <case.bin> <out.bin>\n", argv[0]);
     return 2;

@@ -81,3 +81,102 @@ def test_shim_flows_match_oracle_and_golden(tmp_path):
     for x_ in (x_csr, x_add, x_bsr):
         nerr, _ = O.check_node_result({int(t): x_[i] for i, t in enumerate(gm.node_tags)}, gold, 1e-4)
         assert nerr == 0
+
+
+def _write_rank_case(fname, n, cells, coords, own, nbr, shared, ghosts, dirichlet, value, rows, cols, vals, rhs):
+    with open(fname, "wb") as fh:
+        fh.write(np.array([n, cells.shape[0]], np.int64).tobytes())
+        fh.write(np.ascontiguousarray(coords, np.float64).tobytes())
+        fh.write(np.ascontiguousarray(cells, np.int32).tobytes())
+        fh.write(np.ascontiguousarray(own, np.uint8).tobytes())
+        fh.write(np.array([len(nbr)], np.int32).tobytes())
+        for r in nbr:
+            fh.write(np.array([r], np.int32).tobytes())
+            fh.write(np.array([shared[r].size], np.int64).tobytes())
+            fh.write(np.ascontiguousarray(shared[r], np.int32).tobytes())
+            fh.write(np.array([ghosts[r].size], np.int64).tobytes())
+            fh.write(np.ascontiguousarray(ghosts[r], np.int32).tobytes())
+        fh.write(np.array([dirichlet.size], np.int64).tobytes())
+        fh.write(np.ascontiguousarray(dirichlet, np.int32).tobytes())
+        fh.write(np.array([value], np.float64).tobytes())
+        fh.write(np.array([cols.size], np.int64).tobytes())
+        fh.write(np.ascontiguousarray(rows, np.int32).tobytes())
+        fh.write(np.ascontiguousarray(cols, np.int32).tobytes())
+        fh.write(np.ascontiguousarray(vals, np.float64).tobytes())
+        fh.write(np.ascontiguousarray(rhs, np.float64).tobytes())
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shim_subdomains_over_the_parallel_mng(tmp_path, world):
+    """The shim on `world` subdomains (threads sharing the mock's MockWorld,
+    transport = "host": libafem's halo and reductions go through the shim's
+    IParallelMng transport).  Each subdomain has Arcane-style local ids --
+    owned and ghost DoFs interleaved by a random permutation -- so the shim's
+    numbering (_computeNumbering), its permuted setCSRValues copy, the halo
+    built from the DoF family's IVariableSynchronizer lists (_buildHalo,
+    FemDoFsOnNodes.cc:125-126) and the solution's synchronize() all run.  The
+    partition is libafem's RCB with its subdomain plan (the lists Arcane's
+    ghost layer would give).  Owned values equal the single-domain oracle
+    solve to 1e-10, every ghost its owner's value bit for bit."""
+    import arcanefem_amd as af
+
+    assert os.path.exists(EXE), "tests/arcane_mock/shim_driver not built (__graft_entry__.build())"
+    mfile, f, bcs, gfile, P = CASES["sphere_3D"]
+    gm = read_gmsh(path(mfile))
+    (group, value), = bcs
+    is_dir = np.zeros(gm.n_nodes, bool)
+    is_dir[gm.group_nodes(group)] = True
+    part = af.partition_rcb(3, gm.coords, world)
+    rng = np.random.default_rng(7 + world)
+    l2g_arc = []
+    for r in range(world):
+        plan = af.subdomain_plan(gm.cells, part, world, r)
+        l2g, n_own = plan["local_to_global"], plan["n_own"]
+        n = l2g.size
+        g2l = np.full(gm.n_nodes, -1, np.int64)
+        g2l[l2g] = np.arange(n)
+        lcells = g2l[gm.cells[plan["cells"]]].astype(np.int32)
+        rp, cols = O.sparsity(n, n_own, lcells)  # libafem-local numbering: owned rows first
+        vals, rhs = O.assemble_poisson(n_own, lcells, gm.coords[l2g], rp, cols, f)
+        pi = rng.permutation(n)  # libafem-local index -> Arcane local id
+        inv = np.argsort(pi)
+        rows_a, cols_a, vals_a = [0], [], []
+        for L in range(n):
+            a = inv[L]
+            if a < n_own:
+                c = pi[cols[rp[a]:rp[a + 1]]]
+                o = np.argsort(c)
+                cols_a.extend(c[o])
+                vals_a.extend(vals[rp[a]:rp[a + 1]][o])
+            rows_a.append(len(cols_a))
+        own = inv < n_own
+        rhs_a = np.where(own, rhs[np.minimum(inv, n_own - 1)], 0.0)
+        dirichlet = np.flatnonzero(own & is_dir[l2g[inv]]).astype(np.int32)
+        nbr = [int(x) for x in plan["neighbors"]]
+        _write_rank_case(str(tmp_path / f"case{r}.bin"), n, pi[lcells].astype(np.int32), gm.coords[l2g[inv]], own,
+                         nbr, {q: pi[plan["send"][q]] for q in nbr}, {q: pi[plan["recv"][q]] for q in nbr},
+                         dirichlet, value, np.array(rows_a), np.array(cols_a), np.array(vals_a), rhs_a)
+        l2g_arc.append((l2g[inv], own))
+    r = subprocess.run([EXE, "par", str(world), str(tmp_path / "case"), str(tmp_path / "out")], capture_output=True,
+                       text=True, timeout=180,
+                       env=dict(os.environ, AFEM_OPT_RTOL="1e-14", AFEM_OPT_SOLVER="pcg", AFEM_OPT_MAX_ITER="20000",
+                                AFEM_OPT_TRANSPORT="host"))
+    assert r.returncode == 0, r.stderr
+    # the single-domain system, solved directly
+    n = gm.n_nodes
+    rp, cols = O.sparsity(n, n, gm.cells)
+    vals, rhs = O.assemble_poisson(n, gm.cells, gm.coords, rp, cols, f)
+    O.dirichlet_penalty(np.flatnonzero(is_dir).astype(np.int32), value, P, rp, cols, vals, rhs)
+    xg = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
+    owner_val = np.full(n, np.nan)
+    xs = []
+    for q in range(world):
+        x = np.fromfile(str(tmp_path / f"out{q}.bin"), np.float64)
+        g, own = l2g_arc[q]
+        assert x.size == g.size
+        owner_val[g[own]] = x[own]
+        xs.append((x, g, own))
+    assert not np.isnan(owner_val).any()
+    assert np.abs(owner_val - xg).max() <= 1e-10 * np.abs(xg).max()
+    for x, g, own in xs:
+        assert np.array_equal(x[~own], owner_val[g[~own]])  # synchronize(): ghosts hold their owners' values
