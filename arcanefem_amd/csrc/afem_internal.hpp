@@ -354,7 +354,6 @@ struct LinearSystem {
   mutable DevBuf<uint8_t> pat_flag;  // rows whose columns follow the dominant offset pattern (pattern SpMV)
   mutable DevBuf<int32_t> pat_smp;   // the pattern detection's row samples
   mutable DevBuf<unsigned long long> pat_cnt;
-  mutable DevBuf<double> pat_ell;    // the pattern rows' values in [k][row] order (ELL SpMV, one rank)
   DevBuf<double> x0;      // the caller's initial guess (opts.initial_guess = 1)
   DevBuf<double> binv;    // block-Jacobi 3: inverse node blocks [n/3][9]
   DevBuf<int32_t> blist;  // multi-rank CG: SpMV row blocks, interior ones first

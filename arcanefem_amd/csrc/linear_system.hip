@@ -592,64 +592,6 @@ __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t n
   }
 }
 
-// The pattern rows' values transposed once per solve into [k][row] order
-// (k_ell_pack), so the CG's SpMV streams them: k_spmv_ell reads, for a
-// thread's row, value k at ell[k n + r] and x[r + off[k]] -- both coalesced
-// across the wave, no column image, no LDS, no barrier but the dot product's.
-// Other rows (the box's boundary layers) walk their CSR row.  Products are
-// rounded on their own and summed in column order (the pattern offsets are
-// ascending), the block / partial layout is k_spmv_pat's: y and every CG
-// iterate are bitwise those of the CSR kernels.
-__global__ __launch_bounds__(256) void k_ell_pack(int64_t n_rows, const int64_t* __restrict__ rows,
-                                                  const double* __restrict__ vals, const uint8_t* __restrict__ flag,
-                                                  int len, double* __restrict__ ell)
-{
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n_rows) return;
-  const int64_t a = rows[r];
-  const bool f = flag[r] != 0;
-  for (int k = 0; k < len; ++k) ell[(int64_t)k * n_rows + r] = f ? vals[a + k] : 0.0;
-}
-
-template <bool DOT>
-__global__ __launch_bounds__(kThreads) void k_spmv_ell(int64_t n_rows, const int64_t* __restrict__ rows,
-                                                       const int32_t* __restrict__ cols,
-                                                       const double* __restrict__ vals,
-                                                       const uint8_t* __restrict__ flag, PatOff po,
-                                                       const double* __restrict__ ell,
-                                                       const double* __restrict__ x, double* __restrict__ y,
-                                                       double* __restrict__ partial)
-{
-#pragma clang fp contract(off)
-  const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int64_t r = blk * kThreads + threadIdx.x;
-  double d = 0.0;
-  if (r < n_rows) {
-    double s = 0.0;
-    if (flag[r]) {
-      double v[16], xv[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (k < po.len) {
-          v[k] = ell[(int64_t)k * n_rows + r];
-          xv[k] = x[r + po.off[k]];
-        }
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (k < po.len) s += v[k] * xv[k];
-    }
-    else {
-      for (int64_t q = rows[r], e = rows[r + 1]; q < e; ++q) s += vals[q] * x[cols[q]];
-    }
-    y[r] = s;
-    if (DOT) d = x[r] * s;
-  }
-  if (DOT) {
-    const double bs = block_sum(d);
-    if (threadIdx.x == 0) partial[blockIdx.x] = bs;
-  }
-}
-
 // Node-block SpMV of an NB_DOF = K system held in BSRFormat's CSR order
 // (femutils/BSRFormat.h:194-256: scalar row K r + i holds the node row's
 // K * len values as [block s][j]).  The node-row structure (block offsets bp,
@@ -1241,11 +1183,9 @@ struct SpmvPlan {
   int64_t blk_n = 0;
   const int64_t* blk_rows = nullptr;
   const int32_t* blk_cols = nullptr;
-  // rpb = -3: k_spmv_pat (pattern rows form their columns); rpb = -4:
-  // k_spmv_ell (the pattern rows' values in [k][row] order, one rank)
+  // rpb = -3: k_spmv_pat (pattern rows form their columns)
   const uint8_t* pat_flag = nullptr;
   PatOff po{};
-  const double* ell = nullptr;
 };
 
 __global__ void k_block_seg(int64_t n_rows, int rpb, const int64_t* __restrict__ row_ptr, unsigned long long* out)
@@ -1385,17 +1325,6 @@ SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
         pl.rpb = -3;
         pl.po = po;
         pl.pat_flag = ls.pat_flag.p;
-        // one rank (no interior / halo-boundary block split): the values
-        // transposed for k_spmv_ell (AFEM_SPMV=pat keeps k_spmv_pat)
-        if (!ls.halo && !e) {
-          const size_t ne = (size_t)len * (size_t)ls.n_rows;
-          if (ls.pat_ell.n < ne) ls.pat_ell.alloc(ne);
-          hipLaunchKernelGGL(k_ell_pack, dim3(grid_for(ls.n_rows, 256)), dim3(256), 0, ctx.stream, ls.n_rows,
-                             ls.csr_rows, ls.csr_vals, ls.pat_flag.p, (int)len, ls.pat_ell.p);
-          AFEM_LAUNCHED();
-          pl.rpb = -4;
-          pl.ell = ls.pat_ell.p;
-        }
         return pl;
       }
     }
@@ -1430,14 +1359,6 @@ void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* ro
       AFEM_BLK(2)
     }
 #undef AFEM_BLK
-  }
-  else if (pl.rpb == -4) {
-    if (partial)
-      hipLaunchKernelGGL(k_spmv_ell<true>, dim3(nb), dim3(kThreads), 0, ctx.stream, n_rows, rows, cols, vals,
-                         pl.pat_flag, pl.po, pl.ell, x, y, partial);
-    else
-      hipLaunchKernelGGL(k_spmv_ell<false>, dim3(nb), dim3(kThreads), 0, ctx.stream, n_rows, rows, cols, vals,
-                         pl.pat_flag, pl.po, pl.ell, x, y, partial);
   }
   else if (pl.rpb == -3) {
     const size_t shm = (size_t)(8 * pl.max_seg + 32);
@@ -1972,8 +1893,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     st->rel_residual = rel;
     st->residual_norm = std::sqrt(std::fabs(ls.pinned[4]));
     st->solve_ms = ms;
-    st->spmv_kernel = pl.rpb == -4 ? AFEM_SPMV_PATTERN_ELL
-                      : pl.rpb == -3 ? AFEM_SPMV_PATTERN
+    st->spmv_kernel = pl.rpb == -3 ? AFEM_SPMV_PATTERN
                       : pl.rpb == -2 ? AFEM_SPMV_BLOCK
                       : pl.rpb == -1 ? AFEM_SPMV_VECTOR
                       : (pl.rpb > 0 && pl.wide && pl.unroll) ? AFEM_SPMV_STREAM

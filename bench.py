@@ -43,7 +43,7 @@ sys.path.insert(0, ROOT)
 METRIC = "MDoF/s assembly + CG iter/s, Poisson-3D P1 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # the CG's SpMV by afem_solve_stats.spmv_kernel (include/arcanefem_amd.h AFEM_SPMV_*)
-SPMV_KERNELS = {0: "k_spmv_stream4u", 1: "k_spmv_pat", 2: "k_spmv_v16", 3: "k_spmv_blk", 4: "other", 5: "k_spmv_ell"}
+SPMV_KERNELS = {0: "k_spmv_stream4u", 1: "k_spmv_pat", 2: "k_spmv_v16", 3: "k_spmv_blk", 4: "other"}
 # block-3 assembly kernels by afem_bsr_stats.last_kernel (include/arcanefem_amd.h AFEM_KERNEL_*)
 ELAST3_KERNELS = {4: "k_assemble_elast_strip", 5: "k_assemble_elast_tet", 6: "k_assemble_elast_tet_global",
                   8: "k_assemble_elast_wg", 9: "k_assemble_elast_strip<..,BIG>"}

@@ -327,7 +327,6 @@ typedef struct afem_solve_stats {
 #define AFEM_SPMV_VECTOR 2   /* 16 lanes per row */
 #define AFEM_SPMV_BLOCK 3    /* node-block rows (NB_DOF 2 / 3) */
 #define AFEM_SPMV_OTHER 4    /* row-per-thread / no-unroll variants, direct solver */
-#define AFEM_SPMV_PATTERN_ELL 5 /* one rank: interior-stencil rows' values transposed to [k][row] per solve, streamed */
 
 /* IDoFLinearSystemFactory::createInstance: a linear system over n_rows owned
  * DoFs; n_cols_local >= n_rows counts owned + ghost DoFs (column space of a

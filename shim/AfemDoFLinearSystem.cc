@@ -211,28 +211,30 @@ class AfemDoFLinearSystemImpl
                 "setCSRValues");
       return;
     }
-    // owned rows in afem order, columns renumbered; a host copy (once per view)
+    // owned rows in afem order, columns renumbered; a host copy (once per view),
+    // kept in members: libafem reads a host view at solve()
     const Int32 nb_row = v.nbRow(), nnz = v.nbValue();
     std::vector<Int32> rows(nb_row), cols(nnz);
     std::vector<Real> vals(nnz);
     afemCheck(afem_memcpy(m_ctx, rows.data(), v.rows().data(), sizeof(Int32) * nb_row, AFEM_MEM_HOST, mem), "copy");
     afemCheck(afem_memcpy(m_ctx, cols.data(), v.columns().data(), sizeof(Int32) * nnz, AFEM_MEM_HOST, mem), "copy");
     afemCheck(afem_memcpy(m_ctx, vals.data(), v.values().data(), sizeof(Real) * nnz, AFEM_MEM_HOST, mem), "copy");
-    std::vector<Int32> prow(m_nb_own), pcol;
-    std::vector<Real> pval;
-    pcol.reserve(nnz);
-    pval.reserve(nnz);
+    m_prow.assign(m_nb_own, 0);
+    m_pcol.clear();
+    m_pval.clear();
+    m_pcol.reserve(nnz);
+    m_pval.reserve(nnz);
     for (Int32 a = 0; a < m_nb_own; ++a) {
       const Int32 lid = m_lid_of[a];
       const Int32 b = rows[lid], e = lid == nb_row - 1 ? nnz : rows[lid + 1]; // end as HypreDoFLinearSystem.cc:140-141
-      prow[a] = static_cast<Int32>(pcol.size());
+      m_prow[a] = static_cast<Int32>(m_pcol.size());
       for (Int32 k = b; k < e; ++k) {
-        pcol.push_back(m_index[cols[k]]);
-        pval.push_back(vals[k]);
+        m_pcol.push_back(m_index[cols[k]]);
+        m_pval.push_back(vals[k]);
       }
     }
-    afemCheck(afem_ls_set_csr_values(m_ls, prow.data(), nullptr, pcol.data(), pval.data(), m_nb_own,
-                                     static_cast<Int32>(pcol.size()), AFEM_MEM_HOST),
+    afemCheck(afem_ls_set_csr_values(m_ls, m_prow.data(), nullptr, m_pcol.data(), m_pval.data(), m_nb_own,
+                                     static_cast<Int32>(m_pcol.size()), AFEM_MEM_HOST),
               "setCSRValues");
   }
 
@@ -329,6 +331,9 @@ class AfemDoFLinearSystemImpl
   bool m_identity = true;
   UniqueArray<Int32> m_index;  //!< DoF local id -> afem index (owned first)
   UniqueArray<Int32> m_lid_of; //!< afem index -> DoF local id
+  //! the permuted copy of a view (several subdomains): libafem reads it at solve()
+  std::vector<Int32> m_prow, m_pcol;
+  std::vector<Real> m_pval;
 
  private:
 

@@ -610,10 +610,8 @@ def test_initial_guess_current_solution(ctx):
 def test_pattern_spmv(ctx, variant, n):
     """The pattern-compressed SpMV (interior rows of a Kuhn box form their
     columns as row + the offsets of the interior stencil, the others read
-    theirs, into the block's LDS column image) and, the default on one rank,
-    the same rows' values transposed to [k][row] and streamed (k_spmv_ell):
-    the same products in the same order as the CSR-stream kernel (bitwise
-    equal y), and the same CG solve."""
+    theirs, into the block's LDS column image): the same products in the same
+    order as the CSR-stream kernel (bitwise equal y), and the same CG solve."""
     mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=5)
     bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
     bottom = mesh.bottom_nodes()
@@ -624,22 +622,22 @@ def test_pattern_spmv(ctx, variant, n):
     dx, dy = ctx.malloc(8 * nn), ctx.malloc(8 * nn)
     ctx.to_device(dx, x)
     ys = {}
-    for mode in ("nopat", "pat", None):  # None: the default, k_spmv_ell on one rank
+    for mode in ("nopat", "pat"):
         variant("AFEM_SPMV", mode)
         ls.spmv(dx, dy)
         ys[mode] = ctx.to_host(dy, nn, np.float64)
     ctx.free(dx)
     ctx.free(dy)
-    assert np.array_equal(ys["nopat"], ys["pat"]) and np.array_equal(ys["pat"], ys[None])
+    assert np.array_equal(ys["nopat"], ys["pat"])
     sols, kern = {}, {}
     for mode in ("nopat", "pat", None):
         if mode is None:
-            variant("AFEM_SPMV", None)  # the default: the pattern rows' values transposed (k_spmv_ell)
+            variant("AFEM_SPMV", None)  # the default: the pattern kernel
         else:
             variant("AFEM_SPMV", mode)
         kern[mode] = ls.solve()["spmv_kernel"]
         sols[mode] = ls.solution_host()
-    assert kern == {"nopat": 0, "pat": 1, None: 5}, kern
+    assert kern == {"nopat": 0, "pat": 1, None: 1}, kern
     assert np.array_equal(sols["nopat"], sols["pat"]) and np.array_equal(sols["pat"], sols[None])
 
 

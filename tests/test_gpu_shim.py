@@ -106,7 +106,7 @@ def _write_rank_case(fname, n, cells, coords, own, nbr, shared, ghosts, dirichle
         fh.write(np.ascontiguousarray(rhs, np.float64).tobytes())
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_shim_subdomains_over_the_parallel_mng(tmp_path, world):
     """The shim on `world` subdomains (threads sharing the mock's MockWorld,
     transport = "host": libafem's halo and reductions go through the shim's
@@ -160,7 +160,8 @@ def test_shim_subdomains_over_the_parallel_mng(tmp_path, world):
     r = subprocess.run([EXE, "par", str(world), str(tmp_path / "case"), str(tmp_path / "out")], capture_output=True,
                        text=True, timeout=180,
                        env=dict(os.environ, AFEM_OPT_RTOL="1e-14", AFEM_OPT_SOLVER="pcg", AFEM_OPT_MAX_ITER="20000",
-                                AFEM_OPT_TRANSPORT="host"))
+                                AFEM_OPT_TRANSPORT="host", AFEM_MOCK_TRACE="1"))
+    print(r.stderr[-3000:])  # the shim's info() trace (shown when the test fails)
     assert r.returncode == 0, r.stderr
     # the single-domain system, solved directly
     n = gm.n_nodes
