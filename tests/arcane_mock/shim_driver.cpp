@@ -16,7 +16,7 @@
 //
 // usage: shim_driver <case.bin> <out.bin>
 //        shim_driver par <nranks> <case_prefix> <out_prefix>
-//   par: the csr flow on nranks subdomains at once (threads sharing a MockWorld: the
+//   par: the csr and bsr flows on nranks subdomains at once (threads sharing a MockWorld: the
 //   transport is the shim's IParallelMng one, transport = "host"), with Arcane-style
 //   local ids (owned and ghost DoFs interleaved), the halo from the DoF family's
 //   IVariableSynchronizer (_buildHalo) and the solution synchronised by the shim.
@@ -24,7 +24,7 @@
 //     u8 own[n]; int32 n_nbr; per neighbour: int32 rank, int64 ns, i32 shared[ns],
 //     int64 ng, i32 ghosts[ng]; int64 n_dir; i32 dir[n_dir]; f64 dir_value;
 //     int64 nnz; i32 rows[n+1]; i32 cols[nnz]; f64 vals[nnz]; f64 rhs[n]
-//   <out_prefix><r>.bin: f64 x[n] (every local DoF, ghosts synchronised)
+//   <out_prefix><r>.bin: f64 x_csr[n], x_bsr[n] (every local DoF, ghosts synchronised)
 //   case.bin: int32 dim, nv; int64 n_nodes, n_cells; f64 coords[3 n]; i32 cells[nv nc];
 //             int64 n_dir; i32 dir[n_dir]; f64 dir_value; int64 nnz; i32 rows[n+1];
 //             i32 cols[nnz]; f64 vals[nnz]; f64 rhs[n]; f64 coef
@@ -32,6 +32,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <memory>
 #include <string>
 #include <thread>
@@ -150,7 +151,8 @@ std::vector<double> run_add(IItemFamily* dofs, const Case& c)
   return solution(ls, c.n);
 }
 
-std::vector<double> run_bsr(IMesh* mesh, IItemFamily* dofs, const Case& c)
+std::vector<double> run_bsr(IMesh* mesh, IItemFamily* dofs, const Case& c,
+                            const std::function<void(DoFLinearSystem&)>& rhs_and_bc = {})
 {
   // the module's element lambda (modules/poisson/FemModule.cc:261-272 +
   // FemModule.h:177-186): vol * coef * grad_i . grad_j from the captured geometry
@@ -201,9 +203,13 @@ std::vector<double> run_bsr(IMesh* mesh, IItemFamily* dofs, const Case& c)
     DoFLinearSystem ls(make_linear_system(dofs));
     ls.setRunner(&runner);  // the CSR arrays of toLinearSystem live in device memory
     bsr.toLinearSystem(ls);
-    for (int64_t i = 0; i < c.n; ++i)
-      ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs[i];
-    penalty(ls, c);
+    if (rhs_and_bc)
+      rhs_and_bc(ls);
+    else {
+      for (int64_t i = 0; i < c.n; ++i)
+        ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs[i];
+      penalty(ls, c);
+    }
     ls.solve();
     x = solution(ls, c.n);
   }
@@ -264,7 +270,10 @@ bool load_rank(const std::string& path, RankCase& c)
   return ok;
 }
 
-// one rank of the par mode: the module's Hypre-path calls on its subdomain
+// one rank of the par mode: the module's Hypre-path calls on its subdomain,
+// then the shim's BSRFormat<1> on the same subdomain (element lambda over the
+// rank's cells, toLinearSystem through matrixAddValue: the ids are not the
+// identity), both solved over the shim's IParallelMng transport
 void run_rank(MockWorld* world, Int32 rank, const RankCase& c, std::vector<double>& x, std::string& err)
 {
   try {
@@ -276,24 +285,46 @@ void run_rank(MockWorld* world, Int32 rank, const RankCase& c, std::vector<doubl
     sync->ranks = c.nbr;
     sync->shared = c.shared;
     sync->ghosts = c.ghosts;
-    DoFLinearSystem ls(make_linear_system(&dofs));
-    std::vector<int32_t> rnc(c.n);
-    for (int64_t i = 0; i < c.n; ++i)
-      rnc[i] = c.rows[i + 1] - c.rows[i];
-    std::vector<double> vals = c.vals;
-    // rows: the reference's layout without the sentinel (HypreDoFLinearSystem.cc:140-141)
-    CSRFormatView v(Span<const Int32>(c.rows.data(), c.n), Span<const Int32>(rnc.data(), c.n),
-                    Span<const Int32>(c.cols.data(), c.nnz), Span<Real>(vals.data(), c.nnz));
-    ls.setCSRValues(v);
-    for (int64_t i = 0; i < c.n; ++i)
-      ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs[i];
-    for (int32_t d : c.dir) {
-      ls.getForcedInfo()[DoFLocalId(d)] = true;
-      ls.getForcedValue()[DoFLocalId(d)] = 1.0e30;
-      ls.rhsVariable()[DoFLocalId(d)] = 1.0e30 * c.dir_value;
+    auto bc = [&](DoFLinearSystem& ls) {
+      for (int64_t i = 0; i < c.n; ++i)
+        ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs[i];
+      for (int32_t d : c.dir) {
+        ls.getForcedInfo()[DoFLocalId(d)] = true;
+        ls.getForcedValue()[DoFLocalId(d)] = 1.0e30;
+        ls.rhsVariable()[DoFLocalId(d)] = 1.0e30 * c.dir_value;
+      }
+    };
+    {
+      DoFLinearSystem ls(make_linear_system(&dofs));
+      std::vector<int32_t> rnc(c.n);
+      for (int64_t i = 0; i < c.n; ++i)
+        rnc[i] = c.rows[i + 1] - c.rows[i];
+      std::vector<double> vals = c.vals;
+      // rows: the reference's layout without the sentinel (HypreDoFLinearSystem.cc:140-141)
+      CSRFormatView v(Span<const Int32>(c.rows.data(), c.n), Span<const Int32>(rnc.data(), c.n),
+                      Span<const Int32>(c.cols.data(), c.nnz), Span<Real>(vals.data(), c.nnz));
+      ls.setCSRValues(v);
+      bc(ls);
+      ls.solve();
+      x = solution(ls, c.n);
     }
-    ls.solve();
-    x = solution(ls, c.n);
+    {
+      IItemFamily nodes((Int32)c.n, 0, &pm, &tm);
+      nodes.setOwnMask(c.own);
+      IItemFamily cells((Int32)c.nc, (Int32)c.nc, &pm, &tm);
+      cells.nv = 4;
+      cells.cell_node = c.cells;
+      IMesh mesh(3, &nodes, &cells, &pm);
+      for (int64_t i = 0; i < c.n; ++i)
+        mesh.nodesCoordinates()[NodeLocalId((Int32)i)] = Real3{ c.coords[3 * i], c.coords[3 * i + 1], c.coords[3 * i + 2] };
+      Case one;
+      one.n = c.n;
+      one.nc = c.nc;
+      one.coords = c.coords;
+      one.cells = c.cells;
+      std::vector<double> xb = run_bsr(&mesh, &dofs, one, [&](DoFLinearSystem& ls) { bc(ls); });
+      x.insert(x.end(), xb.begin(), xb.end());
+    }
   }
   catch (const std::exception& e) {
     err = e.what();

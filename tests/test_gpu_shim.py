@@ -116,8 +116,10 @@ def test_shim_subdomains_over_the_parallel_mng(tmp_path, world):
     built from the DoF family's IVariableSynchronizer lists (_buildHalo,
     FemDoFsOnNodes.cc:125-126) and the solution's synchronize() all run.  The
     partition is libafem's RCB with its subdomain plan (the lists Arcane's
-    ghost layer would give).  Owned values equal the single-domain oracle
-    solve to 1e-10, every ghost its owner's value bit for bit."""
+    ghost layer would give).  The same again through the shim's BSRFormat<1>
+    (initialize / computeSparsity / assembleBilinear(element lambda) /
+    toLinearSystem) on each subdomain.  Owned values equal the single-domain
+    oracle solve to 1e-10, every ghost its owner's value bit for bit."""
     import arcanefem_amd as af
 
     assert os.path.exists(EXE), "tests/arcane_mock/shim_driver not built (__graft_entry__.build())"
@@ -169,15 +171,17 @@ def test_shim_subdomains_over_the_parallel_mng(tmp_path, world):
     vals, rhs = O.assemble_poisson(n, gm.cells, gm.coords, rp, cols, f)
     O.dirichlet_penalty(np.flatnonzero(is_dir).astype(np.int32), value, P, rp, cols, vals, rhs)
     xg = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
-    owner_val = np.full(n, np.nan)
-    xs = []
-    for q in range(world):
-        x = np.fromfile(str(tmp_path / f"out{q}.bin"), np.float64)
-        g, own = l2g_arc[q]
-        assert x.size == g.size
-        owner_val[g[own]] = x[own]
-        xs.append((x, g, own))
-    assert not np.isnan(owner_val).any()
-    assert np.abs(owner_val - xg).max() <= 1e-10 * np.abs(xg).max()
-    for x, g, own in xs:
-        assert np.array_equal(x[~own], owner_val[g[~own]])  # synchronize(): ghosts hold their owners' values
+    for flow in (0, 1):  # the setCSRValues flow, then the shim's BSRFormat<1> on the same subdomains
+        owner_val = np.full(n, np.nan)
+        xs = []
+        for q in range(world):
+            x2 = np.fromfile(str(tmp_path / f"out{q}.bin"), np.float64)
+            g, own = l2g_arc[q]
+            assert x2.size == 2 * g.size
+            x = x2[flow * g.size:(flow + 1) * g.size]
+            owner_val[g[own]] = x[own]
+            xs.append((x, g, own))
+        assert not np.isnan(owner_val).any()
+        assert np.abs(owner_val - xg).max() <= 1e-10 * np.abs(xg).max(), flow
+        for x, g, own in xs:
+            assert np.array_equal(x[~own], owner_val[g[~own]])  # synchronize(): ghosts hold their owners' values
