@@ -496,3 +496,57 @@ def test_fan_mesh_block2(ctx):
         if use_csr:
             ovals = O.blocks_to_row_order(orp, ovals)
         _close(vals, ovals)
+
+
+def test_apply_bcs_unsorted_view_and_row_tail(ctx):
+    """k_apply_bcs (4 rows per thread, the diagonal of a forced row found by a
+    binary search with a linear fallback): a host view whose rows are stored in
+    a scrambled column order, a row count that is not a multiple of 4, forced
+    and eliminated rows among the last ones -- the forced values land on the
+    diagonals and the eliminated rows become identity rows, as the oracle's
+    _applyForcedValuesToLhs / _applyRowElimination (HypreDoFLinearSystem.cc:319-382)."""
+    gm = read_gmsh(path("circle_cut.msh"))
+    n = gm.n_nodes
+    orp, ocols = O.sparsity(n, n, gm.cells)
+    ovals, orhs = O.assemble_poisson(n, gm.cells, gm.coords, orp, ocols, 5.5)
+    rng = np.random.default_rng(11)
+    cols, vals = ocols.copy(), ovals.copy()
+    for r in range(n):  # every row's entries in a random order
+        p = orp[r] + rng.permutation(orp[r + 1] - orp[r])
+        cols[orp[r]:orp[r + 1]], vals[orp[r]:orp[r + 1]] = ocols[p], ovals[p]
+    # the last rows (the partial group of 4 when n % 4 != 0) forced and eliminated; no row is
+    # both (the reference eliminates first, then forces the diagonal: the oracle's order differs)
+    forced = np.array([1, 2, n - 2, n - 1], dtype=np.int32)
+    elim = np.array([3, n - 3], dtype=np.int32)
+    ls = af.DoFLinearSystem().initialize(ctx, n)
+    ls.setCSRValues(orp[:-1].astype(np.int32), np.diff(orp).astype(np.int32), cols, vals)
+    ls.set_rhs_host(orhs)
+    ls.applyDirichletViaPenalty(forced, 0.5, 1e30)
+    ls.applyDirichletViaRowElimination(elim, 0.25)
+    ls.applyBoundaryConditions()
+    ov, orh = ovals.copy(), orhs.copy()
+    O.dirichlet_penalty(forced, 0.5, 1e30, orp, ocols, ov, orh)
+    O.row_elimination(elim, 0.25, orp, ocols, ov, orh)
+    ls.setSolverOptions(method="direct")
+    st = ls.solve()
+    x = ls.solution_host()
+    xo = np.linalg.solve(O.csr_to_dense(orp, ocols, ov), orh)
+    assert st["converged"] and np.abs(x - xo).max() / np.abs(xo).max() <= SOL_TOL
+    assert np.allclose(x[elim], 0.25) and np.allclose(x[forced], 0.5)
+
+
+def test_assembly_ticket_ring_wraps(ctx):
+    """The persistent assembly kernels' claim counters come from a ring of 256
+    per-assembly slots zeroed together (assembly.hip next_tickets): 300
+    assemblies in a row (past a wrap) all give the same bits."""
+    mesh = af.Mesh.structured(ctx, 3, 10, jitter=0.2, seed=3)
+    bsr = af.BSRFormat(mesh, 1).initialize(True)
+    bsr.computeSparsity()
+    ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes)
+    bsr.assemblePoissonP1(1.0, 2.0, ls.rhsVariable(), rhs_mode="set")
+    _, _, ref = bsr.download()
+    for i in range(300):
+        bsr.assemblePoissonP1(1.0, 2.0, ls.rhsVariable(), rhs_mode="set")
+        if i % 50 == 49 or i in (254, 255, 256, 257):
+            _, _, v = bsr.download()
+            assert np.array_equal(v, ref), i
