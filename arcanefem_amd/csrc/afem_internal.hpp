@@ -325,6 +325,7 @@ struct LinearSystem {
   bool has_csr = false;
   int64_t csr_n = 0, csr_nnz = 0;
   const int64_t* csr_rows = nullptr;
+  const int64_t* csr_diag = nullptr;  // diagonal positions when the view is a BSRFormat's own CSR (NB_DOF 1)
   const int32_t* csr_cols = nullptr;
   double* csr_vals = nullptr;
   // node-row structure of a view that came from a BSRFormat with NB_DOF = blk_k

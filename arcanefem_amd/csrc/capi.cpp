@@ -710,6 +710,7 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
   ls->blk_k = 0;
   if (k == 1) {
     ls->csr_rows = b->s.row_ptr.p;
+    ls->csr_diag = b->s.diag_pos.n >= (size_t)b->s.n_rows ? b->s.diag_pos.p : nullptr;
     ls->csr_cols = b->s.cols.p;
     ls->csr_vals = b->values.p;
   }
@@ -717,6 +718,7 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
     if (b->order_per_block) b->csr_vals.alloc(b->s.nnz * k * k);
     bsr_expand_scalar(*b, b->csr_vals.p);
     ls->csr_rows = b->csr_rows.p;
+    ls->csr_diag = nullptr;
     ls->csr_cols = b->csr_cols.p;
     ls->csr_vals = b->order_per_block ? b->csr_vals.p : b->values.p;
     ls->blk_k = k;  // the SpMV reads the node-row structure instead of the scalar columns
@@ -967,6 +969,7 @@ int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows
   }
   ctx.sync();
   ls->csr_rows = ls->own_rows.p;
+  ls->csr_diag = nullptr;
   ls->blk_k = 0;
   ls->mg_k = 0;
   ls->mg.reset();
@@ -1092,6 +1095,7 @@ int afem_ls_clear_values(afem_ls* ls)
   ls->has_csr = false;
   ls->csr_from_coo = false;
   ls->csr_rows = nullptr;
+  ls->csr_diag = nullptr;
   ls->blk_k = 0;
   ls->mg_k = 0;
   ls->mg.reset();

@@ -127,6 +127,7 @@ Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* pr
         l->csr_n = d->n;
         l->csr_nnz = d->K.s.nnz * 9;
         l->csr_rows = d->K.csr_rows.p;
+        l->csr_diag = nullptr;
         l->csr_cols = d->K.csr_cols.p;
         l->blk_k = 3;
         l->blk_n = d->K.s.n_rows;

@@ -82,12 +82,15 @@ __global__ void k_elim_columns(int64_t n_rows, const int64_t* __restrict__ rows,
 // (femutils/HypreDoFLinearSystem.cc:319-382).
 // 4 rows per thread: the two flag arrays read as one 32-bit word each (a
 // thread per row was bound by wave launches; 16 rows per thread serialised the
-// flagged rows of a Dirichlet face: 51 us), the diagonal of a forced row found
-// by a binary search of the sorted row (a linear scan for unsorted views)
+// flagged rows of a Dirichlet face: 51 us; a persistent grid-stride sweep: no
+// better), the diagonal of a forced row from the BSRFormat's diagonal
+// positions when the view is its CSR, else found by a binary search of the
+// sorted row (a linear scan for unsorted views)
 __global__ void k_apply_bcs(int64_t n_rows, const int64_t* __restrict__ rows, const int32_t* __restrict__ cols,
                             double* __restrict__ vals, const uint8_t* __restrict__ forced_info,
                             const double* __restrict__ forced_value, const uint8_t* __restrict__ elim_info,
-                            const double* __restrict__ elim_value, double* __restrict__ rhs)
+                            const double* __restrict__ elim_value, double* __restrict__ rhs,
+                            const int64_t* __restrict__ diag)
 {
   const int64_t d0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
   if (d0 >= n_rows) return;
@@ -108,12 +111,19 @@ __global__ void k_apply_bcs(int64_t n_rows, const int64_t* __restrict__ rows, co
     const bool ei = (ew >> (8 * i)) & 0xFFu, fi = (fw >> (8 * i)) & 0xFFu;
     if (!ei && !fi) continue;
     const int64_t d = d0 + i;
+    if (fi && !ei && diag) {
+      vals[diag[d]] = forced_value[d];
+      continue;
+    }
     const int64_t b = rows[d], e = rows[d + 1];
     if (ei) {
       for (int64_t k = b; k < e; ++k) vals[k] = (cols[k] == (int32_t)d) ? 1.0 : 0.0;
       rhs[d] = elim_value[d];
     }
-    if (fi) {
+    if (fi && diag) {  // the view is a BSRFormat's own CSR: its diagonal positions
+      vals[diag[d]] = forced_value[d];
+    }
+    else if (fi) {
       int64_t lo = b, hi = e;  // lower bound of d (sorted rows)
       while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
@@ -1516,6 +1526,7 @@ void ls_build_from_host_coo(LinearSystem& ls)
   ls.csr_n = ls.n_rows;
   ls.csr_nnz = (int64_t)cols.size();
   ls.csr_rows = ls.own_rows.p;
+  ls.csr_diag = nullptr;
   ls.csr_cols = ls.own_cols.p;
   ls.csr_vals = ls.own_vals.p;
   ls.blk_k = 0;
@@ -1538,7 +1549,7 @@ void ls_apply_bcs(LinearSystem& ls)
   }
   hipLaunchKernelGGL(k_apply_bcs, dim3(grid_for((ls.n_rows + 3) / 4, kThreads)), dim3(kThreads), 0, ctx.stream, ls.n_rows,
                      ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.forced_info.p, ls.forced_value.p, ls.elim_info.p,
-                     ls.elim_value.p, ls.rhs.p);
+                     ls.elim_value.p, ls.rhs.p, ls.csr_diag);
   AFEM_LAUNCHED();
 }
 
