@@ -159,35 +159,72 @@ __global__ void k_perm_bricks(int64_t n_slices, int dim, int64_t ax, int64_t ay,
 }
 
 // 3D structured boxes, boundary-aware: the interior nodes [1, a-2]^3 in 4x4x4
-// bricks (partial bricks at the upper end: idle lanes), then the six
-// boundary faces (k planes, j planes without the k rows, i planes without
-// both) in 8x8 tiles.  Interior bricks then share one strip topology (the
-// uniform assembly instance), and the boundary rows no longer spoil it for
-// the interior rows of their brick.
+// bricks (partial bricks at the upper end: idle lanes), then the six boundary
+// faces without their box edges in 8x8 tiles, the twelve box edges without
+// their corners in runs of 64 and the eight corners one slice each.  Every
+// slice then holds rows of one local topology: interior bricks share the
+// uniform assembly instance, each face its own, and the box edges / corners
+// no longer spoil a face tile (so no face tile falls back to the general
+// list; only the few edge and corner slices do).
 struct FaceTiles {
+  static constexpr int kMaxSeg = 26;  // 6 faces + 12 edges + 8 corners
   int64_t n_core, nbx, nby;
-  int64_t start[7];  // first slice of face f (start[6] = n_slices)
-  int64_t U[6], V[6], tu[6];
+  int nseg;
+  int64_t start[kMaxSeg + 1];  // first slice of segment g (start[nseg] = n_slices)
+  int64_t U[kMaxSeg], V[kMaxSeg], tu[kMaxSeg], o[kMaxSeg][3];
+  int8_t au[kMaxSeg], av[kMaxSeg], tw[kMaxSeg];  // u / v axes; tile width along u (8 faces, 64 lines)
 };
 
 __host__ __device__ inline FaceTiles face_tiles(int64_t ax, int64_t ay, int64_t az)
 {
   FaceTiles F{};
-  const int64_t cx = ax > 2 ? ax - 2 : 0, cy = ay > 2 ? ay - 2 : 0, cz = az > 2 ? az - 2 : 0;
-  F.nbx = (cx + 3) / 4;
-  F.nby = (cy + 3) / 4;
-  F.n_core = F.nbx * F.nby * ((cz + 3) / 4);
-  const int64_t U[6] = { ax, az > 1 ? ax : 0, ax, ay > 1 ? ax : 0, cy, ax > 1 ? cy : 0 };
-  const int64_t V[6] = { ay, ay, cz, cz, cz, cz };
+  const int64_t a[3] = { ax, ay, az };
+  const int64_t c[3] = { ax > 2 ? ax - 2 : 0, ay > 2 ? ay - 2 : 0, az > 2 ? az - 2 : 0 };
+  F.nbx = (c[0] + 3) / 4;
+  F.nby = (c[1] + 3) / 4;
+  F.n_core = F.nbx * F.nby * ((c[2] + 3) / 4);
   int64_t acc = F.n_core;
-  for (int f = 0; f < 6; ++f) {
-    F.U[f] = U[f];
-    F.V[f] = V[f];
-    F.tu[f] = (U[f] + 7) / 8;
-    F.start[f] = acc;
-    acc += (U[f] > 0 && V[f] > 0) ? F.tu[f] * ((V[f] + 7) / 8) : 0;
+  auto add = [&](int64_t U, int64_t V, int tw, int64_t o0, int64_t o1, int64_t o2, int au, int av) {
+    if (U <= 0 || V <= 0) return;
+    const int g = F.nseg++;
+    F.U[g] = U;
+    F.V[g] = V;
+    F.tw[g] = (int8_t)tw;
+    F.tu[g] = (U + tw - 1) / tw;
+    F.o[g][0] = o0;
+    F.o[g][1] = o1;
+    F.o[g][2] = o2;
+    F.au[g] = (int8_t)au;
+    F.av[g] = (int8_t)av;
+    F.start[g] = acc;
+    acc += F.tu[g] * ((V + 64 / tw - 1) / (64 / tw));
+  };
+  // the ends of axis d: one plane when the box is one node thick along d
+  auto n_end = [&](int d) { return a[d] > 1 ? 2 : 1; };
+  auto end = [&](int d, int e) { return e ? a[d] - 1 : (int64_t)0; };
+  for (int d = 2; d >= 0; --d) {  // faces: k planes, j planes, i planes; u, v = the other axes, lower first
+    const int u = d == 0 ? 1 : 0, v = d == 2 ? 1 : 2;
+    for (int e = 0; e < n_end(d); ++e) {
+      int64_t o[3] = { 1, 1, 1 };
+      o[d] = end(d, e);
+      add(c[u], c[v], 8, o[0], o[1], o[2], u, v);
+    }
   }
-  F.start[6] = acc;
+  for (int d = 0; d < 3; ++d) {  // edges along d
+    const int p = d == 0 ? 1 : 0, q = d == 2 ? 1 : 2;
+    for (int eq = 0; eq < n_end(q); ++eq)
+      for (int ep = 0; ep < n_end(p); ++ep) {
+        int64_t o[3];
+        o[d] = 1;
+        o[p] = end(p, ep);
+        o[q] = end(q, eq);
+        add(c[d], 1, 64, o[0], o[1], o[2], d, d);
+      }
+  }
+  for (int ek = 0; ek < n_end(2); ++ek)  // corners
+    for (int ej = 0; ej < n_end(1); ++ej)
+      for (int ei = 0; ei < n_end(0); ++ei) add(1, 1, 64, end(0, ei), end(1, ej), end(2, ek), 0, 0);
+  F.start[F.nseg] = acc;
   return F;
 }
 
@@ -207,19 +244,18 @@ __global__ void k_perm_bricks_bd(int64_t n_slices, int64_t ax, int64_t ay, int64
     if (i > ax - 2 || j > ay - 2 || k > az - 2) i = -1;
   }
   else {
-    int f = 0;
-    while (f < 5 && s >= F.start[f + 1]) ++f;
-    const int64_t t = s - F.start[f];
-    const int64_t u = 8 * (t % F.tu[f]) + (lane & 7), v = 8 * (t / F.tu[f]) + (lane >> 3);
-    if (u < F.U[f] && v < F.V[f]) {
-      switch (f) {
-        case 0: i = u; j = v; k = 0; break;
-        case 1: i = u; j = v; k = az - 1; break;
-        case 2: i = u; j = 0; k = 1 + v; break;
-        case 3: i = u; j = ay - 1; k = 1 + v; break;
-        case 4: i = 0; j = 1 + u; k = 1 + v; break;
-        default: i = ax - 1; j = 1 + u; k = 1 + v; break;
-      }
+    int g = 0;
+    while (g + 1 < F.nseg && s >= F.start[g + 1]) ++g;
+    const int64_t t = s - F.start[g];
+    const int tw = F.tw[g];
+    const int64_t u = tw * (t % F.tu[g]) + lane % tw, v = (64 / tw) * (t / F.tu[g]) + lane / tw;
+    if (u < F.U[g] && v < F.V[g]) {
+      int64_t x[3] = { F.o[g][0], F.o[g][1], F.o[g][2] };
+      x[F.au[g]] += u;
+      x[F.av[g]] += v;  // lines and corners: v = 0
+      i = x[0];
+      j = x[1];
+      k = x[2];
     }
   }
   perm[p] = i >= 0 ? (int32_t)(i + ax * (j + ay * k)) : -1;
@@ -1082,7 +1118,7 @@ bool lattice_order(Ctx& ctx, const Mesh& m, int64_t n_rows, Structure& s)
   ctx.sync();
   if (hb) return false;
   const FaceTiles F = face_tiles(L[0], L[1], L[2]);
-  s.n_slices = F.start[6];
+  s.n_slices = F.start[F.nseg];
   s.perm.alloc(s.n_slices * 64);
   hipLaunchKernelGGL(k_perm_bricks_bd, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream, s.n_slices,
                      L[0], L[1], L[2], F, s.perm.p);
@@ -1175,7 +1211,7 @@ void build_structure(Mesh& m, Structure& s)
     const bool boundary_aware = st.dim == 3 && !(be && std::string(be) == "plain");
     if (boundary_aware) {
       const FaceTiles F = face_tiles(ax, ay, az);
-      s.n_slices = F.start[6];
+      s.n_slices = F.start[F.nseg];
       s.perm.alloc(s.n_slices * 64);
       hipLaunchKernelGGL(k_perm_bricks_bd, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream,
                          s.n_slices, ax, ay, az, F, s.perm.p);
@@ -1443,16 +1479,21 @@ void build_structure(Mesh& m, Structure& s)
       }
       s.n_uni = (int64_t)ru.size();
       s.n_mix = (int64_t)rm.size();
+      constexpr int kSmallSliceNodes = 352;
+      auto small_slice = [&](const SliceRec& r) {
+        return (int)((r.meta >> 16) & 0xFFu) <= 16 && (int)(r.meta >> 24) <= 32 &&
+               (int)(r.meta & 0xFFFFu) <= kSmallSliceNodes;
+      };
+      std::vector<SliceRec> ms_h;  // the compact general list, host copy (the stencil split may extend it)
       {
         // general-instance slices: the compact ones (<= 16 slots, <= 32 steps,
         // <= 352 nodes: 90 % of a Hilbert-ordered unstructured mesh) in their
         // own list, so the big ones do not size the LDS tile of all
-        constexpr int kSmallSliceNodes = 352;
         std::vector<SliceRec> ms, mb;
         s.ms_nodes = s.mb_nodes = s.mb_w = 0;
         for (const SliceRec& r : rm) {
-          const int nu = (int)(r.meta & 0xFFFFu), w = (int)((r.meta >> 16) & 0xFFu), st = (int)(r.meta >> 24);
-          if (w <= 16 && st <= 32 && nu <= kSmallSliceNodes) {
+          const int nu = (int)(r.meta & 0xFFFFu), w = (int)((r.meta >> 16) & 0xFFu);
+          if (small_slice(r)) {
             ms.push_back(r);
             s.ms_nodes = std::max(s.ms_nodes, nu);
           }
@@ -1476,6 +1517,7 @@ void build_structure(Mesh& m, Structure& s)
         };
         up(s.rec_ms, ms);
         up(s.rec_mb, mb);
+        ms_h = std::move(ms);
       }
       auto upload = [&](DevBuf<SliceRec>& d, const std::vector<SliceRec>& h) {
         d.alloc(h.empty() ? 1 : h.size());
@@ -1516,6 +1558,23 @@ void build_structure(Mesh& m, Structure& s)
             s.ur_nodes = std::max(s.ur_nodes, (int)(r.meta & 0xFFFFu));
             s.ur_w = std::max(s.ur_w, (int)((r.meta >> 16) & 0xFFu));
           }
+        }
+        // a few uniform slices without a compiled-in signature beside the stencil
+        // slices (a box's edge runs and corners, boundary_aware order) join the
+        // compact general list: one small launch before the stencil kernel
+        // instead of two (AFEM_ASSEMBLY_FOLD=0 keeps them on the uniform instance)
+        const char* fe = variant("AFEM_ASSEMBLY_FOLD");
+        if (!(fe && atoi(fe) == 0) && !rk.empty() && !rur.empty() && rur.size() * 256 <= rk.size() &&
+            std::all_of(rur.begin(), rur.end(), small_slice)) {
+          for (const SliceRec& r : rur) {
+            ms_h.push_back(r);
+            s.ms_nodes = std::max(s.ms_nodes, (int)(r.meta & 0xFFFFu));
+          }
+          s.n_ms = (int64_t)ms_h.size();
+          upload(s.rec_ms, ms_h);
+          rur.clear();
+          sur.clear();
+          s.ur_nodes = s.ur_w = 0;
         }
         s.sig_k = best;
         s.n_k = (int64_t)rk.size();
@@ -1617,7 +1676,7 @@ void build_structure(Mesh& m, Structure& s)
         for (auto& kv : hs2) top.push_back({ kv.second, kv.first });
         std::sort(top.rbegin(), top.rend());
         fprintf(stderr, "afem pattern+slots: %zu distinct\n", top.size());
-        for (size_t i = 0; i < top.size() && i < 8; ++i)
+        for (size_t i = 0; i < top.size() && i < 48; ++i)
           fprintf(stderr, "afem  %lld  %s\n", (long long)top[i].first, top[i].second.c_str());
       }
       ctx.sync();

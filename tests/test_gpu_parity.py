@@ -105,7 +105,9 @@ def test_uniform_strip_variant(ctx, variant):
     mesh = af.Mesh.structured(ctx, 3, 23, seed=11)
     bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
     st = bsr.stats()
-    assert st["brick_order"] == 1 and 0 < st["uniform_slices"] < st["n_slices"]
+    # (boundary-aware order: faces, box edges and corners in their own slices,
+    # so at this size every slice is uniform)
+    assert st["brick_order"] == 1 and 0 < st["uniform_slices"] <= st["n_slices"]
     _, _, v_uni = bsr.download()
     r_uni = ls.rhs_host()
     variant("AFEM_ASSEMBLY_UNIFORM", "0")
@@ -150,6 +152,28 @@ def test_stencil_instance_bitwise(ctx, variant, n):
     assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
     _check_values(v_k, ovals)
     assert np.abs(r_k - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+
+
+def test_edge_slices_folded_into_general_list(ctx, variant):
+    """Box edges and corners (boundary-aware order: runs of 64 along the 12
+    edges, one slice per corner) are uniform slices without a compiled-in
+    signature; beside enough stencil slices they join the compact general list
+    (one launch before the stencil kernel).  Same bits as keeping them on the
+    uniform instance (AFEM_ASSEMBLY_FOLD=0) and as the general instance."""
+    mesh = af.Mesh.structured(ctx, 3, 100, jitter=0.2, seed=5)
+    bsr, ls = _assemble_gpu(ctx, mesh, 3.0)
+    st = bsr.stats()
+    assert st["stencil_slices"] < st["uniform_slices"] <= st["n_slices"]
+    _, _, v_fold = bsr.download()
+    r_fold = ls.rhs_host()
+    variant("AFEM_ASSEMBLY_FOLD", "0")
+    bsr2, ls2 = _assemble_gpu(ctx, mesh, 3.0)
+    _, _, v_nf = bsr2.download()
+    assert np.array_equal(v_fold, v_nf) and np.array_equal(r_fold, ls2.rhs_host())
+    variant("AFEM_ASSEMBLY_UNIFORM", "0")
+    bsr2.assemblePoissonP1(1.0, 3.0, ls2.rhsVariable(), rhs_mode="set")
+    _, _, v_gen = bsr2.download()
+    assert np.array_equal(v_fold, v_gen) and np.array_equal(r_fold, ls2.rhs_host())
 
 
 def test_isolated_node_and_ragged_rows(ctx):
