@@ -161,7 +161,8 @@ __global__ void k_perm_bricks(int64_t n_slices, int dim, int64_t ax, int64_t ay,
 // 3D structured boxes, boundary-aware: the interior nodes [1, a-2]^3 in 4x4x4
 // bricks (partial bricks at the upper end: idle lanes), then the six boundary
 // faces without their box edges in 8x8 tiles, the twelve box edges without
-// their corners in runs of 64 and the eight corners one slice each.  Every
+// their corners in runs of 32 (a run's slice then couples ~136 nodes: within
+// the block-3 workgroup kernel's 256) and the eight corners one slice each.  Every
 // slice then holds rows of one local topology: interior bricks share the
 // uniform assembly instance, each face its own, and the box edges / corners
 // no longer spoil a face tile (so no face tile falls back to the general
@@ -172,7 +173,7 @@ struct FaceTiles {
   int nseg;
   int64_t start[kMaxSeg + 1];  // first slice of segment g (start[nseg] = n_slices)
   int64_t U[kMaxSeg], V[kMaxSeg], tu[kMaxSeg], o[kMaxSeg][3];
-  int8_t au[kMaxSeg], av[kMaxSeg], tw[kMaxSeg];  // u / v axes; tile width along u (8 faces, 64 lines)
+  int8_t au[kMaxSeg], av[kMaxSeg], tw[kMaxSeg];  // u / v axes; tile width along u (8 faces, 32 edges)
 };
 
 __host__ __device__ inline FaceTiles face_tiles(int64_t ax, int64_t ay, int64_t az)
@@ -218,7 +219,7 @@ __host__ __device__ inline FaceTiles face_tiles(int64_t ax, int64_t ay, int64_t 
         o[d] = 1;
         o[p] = end(p, ep);
         o[q] = end(q, eq);
-        add(c[d], 1, 64, o[0], o[1], o[2], d, d);
+        add(c[d], 1, 32, o[0], o[1], o[2], d, d);
       }
   }
   for (int ek = 0; ek < n_end(2); ++ek)  // corners

@@ -85,6 +85,27 @@ def test_elasticity3d_uniform_variant_bitwise(ctx, variant, use_csr):
     assert np.array_equal(r_uni, r_gen)
 
 
+def test_elasticity3d_box_edges_stay_on_the_workgroup_kernel(ctx, variant):
+    """A box whose edges hold full runs (boundary-aware order: 32 rows per edge
+    slice) still fits the block-3 workgroup kernel (slices <= 256 nodes), and
+    its uniform / general instances give the same bits."""
+    mesh = af.Mesh.structured(ctx, 3, 70, jitter=0.2, seed=9)
+    bsr = af.BSRFormat(mesh, 3).initialize(False)
+    bsr.computeSparsity()
+    st = bsr.stats()
+    assert st["max_slice_nodes"] <= 256, st
+    n3 = 3 * mesh.n_own_nodes
+    drhs = ctx.malloc(8 * n3)
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
+    assert bsr.stats()["last_kernel"] == 8
+    v_k, r_k = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
+    variant("AFEM_ASSEMBLY_UNIFORM", "0")
+    bsr.assembleElasticityP1Ex(LAM, MU2, 3.7e6, (0.5, -1.0, 2.0), drhs, rhs_mode="set")
+    v_g, r_g = bsr.download()[2], ctx.to_host(drhs, n3, np.float64)
+    ctx.free(drhs)
+    assert np.array_equal(v_k, v_g) and np.array_equal(r_k, r_g)
+
+
 @pytest.mark.parametrize("n", [13, 22])
 @pytest.mark.parametrize("use_csr", [False, True])
 def test_elasticity3d_stencil_instance_bitwise(ctx, variant, n, use_csr):
