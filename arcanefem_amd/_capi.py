@@ -65,7 +65,8 @@ class BsrStats(ctypes.Structure):
                 ("max_slice_nodes", ctypes.c_int32), ("max_slice_width", ctypes.c_int32),
                 ("n_slices", ctypes.c_int64), ("brick_order", ctypes.c_int32), ("uniform_slices", ctypes.c_int32),
                 ("last_kernel", ctypes.c_int32), ("stencil_slices", ctypes.c_int32),
-                ("stencil_sig", ctypes.c_int32), ("shared_strip_slices", ctypes.c_int64)]
+                ("stencil_sig", ctypes.c_int32), ("shared_strip_slices", ctypes.c_int64),
+                ("uniform_instance_slices", ctypes.c_int64), ("general_slices", ctypes.c_int64)]
 
 
 class SolverOpts(ctypes.Structure):

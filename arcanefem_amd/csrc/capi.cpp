@@ -629,6 +629,8 @@ int afem_bsr_get_stats(afem_bsr* b, afem_bsr_stats* st)
   st->stencil_slices = (int32_t)b->s.n_k;
   st->stencil_sig = b->s.sig_k;
   st->shared_strip_slices = b->s.n_strip_shared;
+  st->uniform_instance_slices = b->s.n_ur;
+  st->general_slices = b->s.n_ms + b->s.n_mb;
   st->last_kernel = b->last_kernel;
   API_END
 }

@@ -178,9 +178,10 @@ def roofline(bsr, mesh, kernel_ms):
     # the instances the assembly launches: uniform slices, compact general
     # slices, big general slices (> 16 slots / > 352 nodes, assembly.hip)
     names = ["k_assemble_stencil<kSigKuhn3D>"] if st["stencil_slices"] > 0 else []
-    if st["uniform_slices"] > st["stencil_slices"]:
+    if st["uniform_instance_slices"] > 0 or (st["stencil_slices"] == 0 and st["uniform_slices"] > 0):
         names.append("k_assemble_strip<4,2,16,uniform>")
-    names.append("k_assemble_strip<4,2,16,general>")
+    if st["general_slices"] > 0:
+        names.append("k_assemble_strip<4,2,16,general>")
     if st["max_slice_width"] > 16 or st["max_slice_nodes"] > 352:
         names.append("k_assemble_strip<4,4,32,general>")
     kname = " + ".join(names)

@@ -229,7 +229,8 @@ typedef struct afem_bsr_stats {
   int32_t max_slice_width;  /* max row length within one slice */
   int64_t n_slices;         /* assembly slices (wavefronts per launch) */
   int32_t brick_order;      /* 1: slices are node bricks of a structured box: 4x4x4 interior bricks
-                               (8x8 in 2D) and 8x8 tiles of the boundary faces; 2: the same bricks of
+                               (8x8 in 2D), 8x8 tiles of the boundary faces, runs of 32 along the box
+                               edges and one slice per corner; 2: the same bricks of
                                a lattice recovered from the coordinates of a mesh given as arrays
                                (any numbering); 0: slices follow a Hilbert-curve order of the node
                                coordinates (plain node order under AFEM_ORDER=node) */
@@ -239,6 +240,10 @@ typedef struct afem_bsr_stats {
   int32_t stencil_sig;      /* that signature's index (-1: none) */
   int64_t shared_strip_slices; /* stencil slices reading their signature's one copy of the per-lane
                                   local-index stream (byte-identical streams: interior bricks) */
+  int64_t uniform_instance_slices; /* scalar assembly: uniform slices run by the uniform instance (no
+                                      compiled-in signature, not folded into the general list) */
+  int64_t general_slices;   /* scalar assembly: slices of the general instance's lists (with the
+                               folded uniform ones: a box's edge runs and corners) */
 } afem_bsr_stats;
 #define AFEM_KERNEL_NONE 0
 #define AFEM_KERNEL_STRIP 1          /* scalar row-strip kernel (uniform + general instances) */

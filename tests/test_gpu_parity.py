@@ -164,10 +164,13 @@ def test_edge_slices_folded_into_general_list(ctx, variant):
     bsr, ls = _assemble_gpu(ctx, mesh, 3.0)
     st = bsr.stats()
     assert st["stencil_slices"] < st["uniform_slices"] <= st["n_slices"]
+    assert st["uniform_instance_slices"] == 0 and st["general_slices"] > 0, st
     _, _, v_fold = bsr.download()
     r_fold = ls.rhs_host()
     variant("AFEM_ASSEMBLY_FOLD", "0")
     bsr2, ls2 = _assemble_gpu(ctx, mesh, 3.0)
+    st2 = bsr2.stats()
+    assert st2["uniform_instance_slices"] == st["uniform_slices"] - st["stencil_slices"], st2
     _, _, v_nf = bsr2.download()
     assert np.array_equal(v_fold, v_nf) and np.array_equal(r_fold, ls2.rhs_host())
     variant("AFEM_ASSEMBLY_UNIFORM", "0")
