@@ -18,7 +18,7 @@ ctx = af.Context(0)
 mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
 variants = []
 for v in (va, vb):
-    os.environ[var] = v
+    af.set_variant(var, v)  # the library caches the environment at its first read
     bsr = af.BSRFormat(mesh, 1).initialize(True)
     bsr.computeSparsity()
     ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes)
