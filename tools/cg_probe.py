@@ -36,7 +36,7 @@ res = {v: [] for v in a.vals}
 sols = {}
 for r in range(a.reps + 1):
     for v in a.vals:
-        os.environ[a.var] = v
+        af.set_variant(a.var, v)  # the library caches the environment at its first read
         st = ls.solve()
         if r:
             res[v].append(st["solve_ms"] / a.iters)
