@@ -72,6 +72,25 @@ def test_structured_assembly_parity(ctx, dim, n):
     assert np.abs(rhs - orhs).max() <= VAL_TOL * np.abs(orhs).max()
 
 
+def test_boundary_aware_order_on_thin_boxes(ctx):
+    """The boundary-aware brick order (interior bricks, face tiles, edge runs,
+    corners) on boxes one to a few cells thick along an axis (empty interiors,
+    faces that coincide, edges without interior nodes): every owned node in
+    exactly one slice (checked by the structure build) and the oracle's
+    matrix."""
+    for n, nz in [(1, 1), (1, 4), (3, 1), (4, 2), (9, 3), (2, 7), (33, 2)]:
+        mesh = af.Mesh.structured(ctx, 3, n, nz)
+        bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+        assert bsr.stats()["brick_order"] == 1
+        rows, cols, vals = bsr.download()
+        cells, coords, _ = mesh.download()
+        orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+        ovals, orhs = O.assemble_poisson(mesh.n_own_nodes, cells, coords, orp, ocols, 5.5)
+        assert np.array_equal(rows, orp) and np.array_equal(cols, ocols), (n, nz)
+        _check_values(vals, ovals)
+        assert np.abs(ls.rhs_host() - orhs).max() <= VAL_TOL * np.abs(orhs).max(), (n, nz)
+
+
 @pytest.mark.parametrize("case", list(CASES))
 def test_golden_mesh_assembly_parity(ctx, case):
     mfile, f, bcs, gfile, P = CASES[case]
