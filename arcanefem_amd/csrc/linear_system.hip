@@ -1011,6 +1011,8 @@ __global__ __launch_bounds__(kThreads) void k_cg_update_b3(int64_t nb, const dou
 // r, z) and k_cg_dir_x (x += alpha p with the p of this iteration, then
 // p = z + beta p: reads x, z, p, writes x, p) -- 80 B per row instead of the
 // 88 of k_cg_update + k_cg_dir; the same operations on the same values.
+// V2: two rows per thread and access (16-B loads / stores per lane)
+template <bool V2>
 __global__ __launch_bounds__(kThreads) void k_cg_update_rz(int64_t n, const double* __restrict__ scal, int par,
                                                            double* __restrict__ r, const double* __restrict__ q,
                                                            double* __restrict__ z, const double* __restrict__ dinv,
@@ -1019,16 +1021,45 @@ __global__ __launch_bounds__(kThreads) void k_cg_update_rz(int64_t n, const doub
   const double rz = scal[par], pq = scal[2];
   const double alpha = (pq != 0.0) ? rz / pq : 0.0;
   double s = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    double ri = r[i] - alpha * q[i];
-    r[i] = ri;
-    double zi = ri * dinv[i];
-    z[i] = zi;
-    s += ri * zi;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+  if constexpr (V2) {
+    double2* r2 = reinterpret_cast<double2*>(r);
+    double2* z2 = reinterpret_cast<double2*>(z);
+    const double2* q2 = reinterpret_cast<const double2*>(q);
+    const double2* d2 = reinterpret_cast<const double2*>(dinv);
+    for (int64_t i = t0; i < (n >> 1); i += st) {
+      double2 rv = r2[i];
+      const double2 qv = q2[i], dv = d2[i];
+      rv.x = rv.x - alpha * qv.x;
+      rv.y = rv.y - alpha * qv.y;
+      r2[i] = rv;
+      const double2 zv = make_double2(rv.x * dv.x, rv.y * dv.y);
+      z2[i] = zv;
+      s += rv.x * zv.x;
+      s += rv.y * zv.y;
+    }
+    if ((n & 1) && t0 == 0) {
+      const int64_t i = n - 1;
+      double ri = r[i] - alpha * q[i];
+      r[i] = ri;
+      double zi = ri * dinv[i];
+      z[i] = zi;
+      s += ri * zi;
+    }
+  }
+  else {
+    for (int64_t i = t0; i < n; i += st) {
+      double ri = r[i] - alpha * q[i];
+      r[i] = ri;
+      double zi = ri * dinv[i];
+      z[i] = zi;
+      s += ri * zi;
+    }
   }
   double bs = block_sum(s);
   if (threadIdx.x == 0) partial[blockIdx.x] = bs;
 }
+template <bool V2>
 __global__ __launch_bounds__(kThreads) void k_cg_dir_x(int64_t n, const double* __restrict__ scal, int par,
                                                        double* __restrict__ x, const double* __restrict__ z,
                                                        double* __restrict__ p)
@@ -1036,10 +1067,32 @@ __global__ __launch_bounds__(kThreads) void k_cg_dir_x(int64_t n, const double* 
   const double rz_old = scal[par], rz_new = scal[par ^ 1], pq = scal[2];
   const double alpha = (pq != 0.0) ? rz_old / pq : 0.0;
   const double beta = (rz_old != 0.0) ? rz_new / rz_old : 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const double pi = p[i];
-    x[i] += alpha * pi;
-    p[i] = z[i] + beta * pi;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+  if constexpr (V2) {
+    double2* x2 = reinterpret_cast<double2*>(x);
+    double2* p2 = reinterpret_cast<double2*>(p);
+    const double2* z2 = reinterpret_cast<const double2*>(z);
+    for (int64_t i = t0; i < (n >> 1); i += st) {
+      const double2 pv = p2[i], zv = z2[i];
+      double2 xv = x2[i];
+      xv.x += alpha * pv.x;
+      xv.y += alpha * pv.y;
+      x2[i] = xv;
+      p2[i] = make_double2(zv.x + beta * pv.x, zv.y + beta * pv.y);
+    }
+    if ((n & 1) && t0 == 0) {
+      const int64_t i = n - 1;
+      const double pi = p[i];
+      x[i] += alpha * pi;
+      p[i] = z[i] + beta * pi;
+    }
+  }
+  else {
+    for (int64_t i = t0; i < n; i += st) {
+      const double pi = p[i];
+      x[i] += alpha * pi;
+      p[i] = z[i] + beta * pi;
+    }
   }
 }
 
@@ -1795,6 +1848,9 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   }
   // the part of an iteration after the SpMV (with_spmv: the whole iteration,
   // for the captured graph of the single-rank, non-split path)
+  // AFEM_CG_VEC2=0: one row per thread and access in the vector kernels (variant)
+  const char* v2e = variant("AFEM_CG_VEC2");
+  const bool vec2 = !(v2e && atoi(v2e) == 0);
   auto rest_of_iteration = [&](int par, bool with_spmv) {
     if (with_spmv)
       launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p, ls.csr_nnz);
@@ -1812,15 +1868,16 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
       hipLaunchKernelGGL(k_cg_update_b3, dim3(vb3), dim3(kThreads), 0, ctx.stream, nb3, scal, par, ls.sol.p, ls.p.p,
                          ls.r.p, ls.q.p, ls.z.p, ls.binv.p, ls.partial.p);
     else
-      hipLaunchKernelGGL(k_cg_update_rz, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.r.p, ls.q.p,
-                         ls.z.p, ls.dinv.p, ls.partial.p);
+      hipLaunchKernelGGL(vec2 ? k_cg_update_rz<true> : k_cg_update_rz<false>, dim3(vb), dim3(kThreads), 0, ctx.stream,
+                         n, scal, par, ls.r.p, ls.q.p, ls.z.p, ls.dinv.p, ls.partial.p);
     AFEM_LAUNCHED();
     reduce_to(ctx, ls.partial.p, blk3 ? vb3 : vb, scal + (par ^ 1));
     if (comm) comm_allreduce(comm, ctx, scal + (par ^ 1), 1);
     if (use_mg || blk3)
       hipLaunchKernelGGL(k_cg_dir, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.z.p, ls.p.p);
     else
-      hipLaunchKernelGGL(k_cg_dir_x, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.z.p, ls.p.p);
+      hipLaunchKernelGGL(vec2 ? k_cg_dir_x<true> : k_cg_dir_x<false>, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal,
+                         par, ls.sol.p, ls.z.p, ls.p.p);
     AFEM_LAUNCHED();
   };
   // graph replay of whole iterations (single rank, no split SpMV, no
