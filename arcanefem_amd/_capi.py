@@ -59,6 +59,24 @@ class AssemblyView(ctypes.Structure):
                 ("values", ctypes.c_void_p), ("error_flag", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
 
 
+class FunctorPlan(ctypes.Structure):
+    """afem_functor_plan (cell-unit plan of the generic element-functor kernel)."""
+    _fields_ = [("n_units", ctypes.c_int64), ("n_stages", ctypes.c_int64), ("n_entries", ctypes.c_int64),
+                ("rows_per_layer", ctypes.c_int32), ("width", ctypes.c_int32), ("nbuf", ctypes.c_int32),
+                ("wide", ctypes.c_int32), ("block_size", ctypes.c_int32), ("nb_node_per_cell", ctypes.c_int32),
+                ("ordered_per_block", ctypes.c_int32), ("lattice", ctypes.c_int32), ("units", ctypes.c_void_p),
+                ("stage_ptr", ctypes.c_void_p), ("layer_rows", ctypes.c_void_p), ("entries", ctypes.c_void_p),
+                ("entries2", ctypes.c_void_p), ("rows", ctypes.c_void_p), ("values", ctypes.c_void_p),
+                ("stream", ctypes.c_void_p)]
+
+
+class Csr32View(ctypes.Structure):
+    """afem_csr32_view (BSRFormat::toLinearSystem in the caller's DoF numbering)."""
+    _fields_ = [("n_rows", ctypes.c_int64), ("nnz", ctypes.c_int64), ("rows", ctypes.c_void_p),
+                ("rows_nb_column", ctypes.c_void_p), ("columns", ctypes.c_void_p), ("values", ctypes.c_void_p),
+                ("identity", ctypes.c_int32)]
+
+
 class BsrStats(ctypes.Structure):
     _fields_ = [("n_incidences", ctypes.c_int64), ("inc_table_entries", ctypes.c_int64),
                 ("max_row_len", ctypes.c_int32), ("rows_per_block", ctypes.c_int32), ("max_seg", ctypes.c_int64),
@@ -143,6 +161,8 @@ SIGNATURES = {
     "afem_bsr_view": [P, ctypes.POINTER(CsrView)],
     "afem_bsr_get_stats": [P, ctypes.POINTER(BsrStats)],
     "afem_bsr_assembly_view": [P, ctypes.POINTER(AssemblyView)],
+    "afem_bsr_functor_plan": [P, ctypes.POINTER(FunctorPlan)],
+    "afem_bsr_to_csr32_mapped": [P, P, I64, ctypes.POINTER(Csr32View)],
     "afem_bsr_get_sizes": [P, ctypes.POINTER(I64), ctypes.POINTER(I64)],
     "afem_bsr_export_csr32": [P, P, P, P, P],
     "afem_bsr_download": [P, P, P, P],
@@ -156,6 +176,7 @@ SIGNATURES = {
     "afem_ls_eliminate_row": [P, I32, D],
     "afem_ls_eliminate_row_column": [P, I32, D],
     "afem_ls_set_csr_values": [P, P, P, P, P, I32, I32, INT],
+    "afem_ls_set_csr_values_mapped": [P, P, P, P, P, I32, I32, P, I64],
     "afem_ls_has_set_csr_values": [P, ctypes.POINTER(INT)],
     "afem_ls_get_csr_values": [P, ctypes.POINTER(CsrView)],
     "afem_ls_rhs": [P, PP],

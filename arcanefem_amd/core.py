@@ -295,6 +295,14 @@ class BSRFormat:
         call("afem_bsr_get_stats", self.h, ctypes.byref(s))
         return {k: getattr(s, k) for k, _ in s._fields_}
 
+    def functor_plan(self) -> dict:
+        """The cell-unit plan of the generic element-functor kernel
+        (afem_bsr_functor_plan; built at the first call)."""
+        p = C.FunctorPlan()
+        call("afem_bsr_functor_plan", self.h, ctypes.byref(p))
+        return {k: getattr(p, k) for k, _ in p._fields_ if not k in
+                ("units", "stage_ptr", "layer_rows", "entries", "entries2", "rows", "values", "stream")}
+
     def download(self):
         """Block arrays: rows[n+1] int64, columns[nnz] int32, values[nnz*k*k]."""
         v = self.view()

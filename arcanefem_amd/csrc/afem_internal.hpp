@@ -251,6 +251,37 @@ struct Structure {
 
 struct LinearSystem;
 
+// Cell-unit plan of a structure for generic element functors
+// (functor_plan.hip; the kernel is the header template
+// include/arcanefem_amd_generic.hpp k_assemble_units): units of at most 64
+// rows per layer -- lattice columns of fx x fy nodes cut into z segments of
+// zs layers (every cell spans at most two consecutive layers), or rl-row
+// pieces of the processing-order slices (one layer) -- and, per (unit, layer)
+// "stage", the cells whose highest in-unit vertex lies in that layer, each
+// with the unit-local row position and the row slots of its vertices.
+struct FunctorPlan {
+  bool valid = false;
+  int nb_dof = 0;
+  int rl = 64, w = 0, nbuf = 1, wide = 0, lattice = 0;
+  int fx = 0, fy = 0, zs = 1;
+  int64_t n_units = 0, n_stages = 0, n_entries = 0, n_coalesced = 0;
+  DevBuf<afem_functor_unit> units;
+  DevBuf<int64_t> stage_ptr;   // [n_stages + 1]
+  DevBuf<int32_t> layer_rows;  // [n_stages * rl]
+  DevBuf<uint32_t> ent, ent2;  // compact: 4 u32 per entry; wide: 4 u32 slots + 2 u32 (cell, pos)
+};
+void functor_plan_build(struct Bsr& b);
+
+// BSRFormat::toLinearSystem in the caller's DoF numbering (handover.hip):
+// the scalar CSR (int32, CSRFormatView layout) and the value gather index
+struct HandOver {
+  bool valid = false, identity = false;
+  int64_t n_rows = 0, nnz = 0;
+  DevBuf<int32_t> rows, rnc, cols;
+  DevBuf<int64_t> src;  // value index in the BSR values (not kept when identity)
+  DevBuf<double> vals;
+};
+
 struct Bsr {
   Mesh* mesh = nullptr;
   int nb_dof = 1;
@@ -264,7 +295,11 @@ struct Bsr {
   DevBuf<int32_t> csr_cols;
   DevBuf<double> csr_vals;  // per-block layout permuted to CSR order
   DevBuf<int32_t> gen_flag;  // error flag of the generic element-functor assembly (afem_bsr_assembly_view)
+  FunctorPlan fplan;         // cell-unit plan of the generic assembly (built at its first use)
+  HandOver hand;             // toLinearSystem in the caller's numbering (afem_bsr_to_csr32_mapped)
 };
+void bsr_csr32_mapped_build(Bsr& b, const int32_t* dof_of_host, int64_t n_dof_rows);
+double* bsr_csr32_mapped_values(Bsr& b);  // the values in the mapped CSR order (gathered, or aliased)
 
 // ------------------------------------------------------------------ communicator / halo
 struct Comm;
@@ -337,6 +372,11 @@ struct LinearSystem {
   DevBuf<int64_t> own_rows;   // when the view came in the reference int32 layout
   DevBuf<int32_t> own_cols;
   DevBuf<double> own_vals;    // host-uploaded or COO-built matrix
+  // setCSRValues in the caller's numbering (afem_ls_set_csr_values_mapped):
+  // the caller's device values stay the matrix (gathered into own_vals at
+  // solve, point updates and the BC pass written back through mv_src)
+  double* mv_vals = nullptr;
+  DevBuf<int64_t> mv_src;
   // setCSRValues on HOST memory: the caller's arrays stay the matrix until the
   // solve (femutils/DoFLinearSystem.h:251-258) -- point updates edit them and
   // afem_ls_solve re-reads the values (own_vals is the device copy)
@@ -390,6 +430,10 @@ int64_t read_i64(Ctx& ctx, const int64_t* d);
 void device_minmax_i32(Ctx& ctx, const int32_t* a, int64_t n, int32_t* lo, int32_t* hi);
 
 void build_structure(Mesh& m, Structure& s);
+// node -> incident-cell lists of the owned nodes (sorted by cell id); returns the entry count
+int64_t node_cell_adjacency(Ctx& ctx, const Mesh& m, int64_t n_rows, DevBuf<int64_t>& nc_ptr, DevBuf<int32_t>& nc);
+// per-axis layer index of every owned node when they sit on a (jittered) lattice (sparsity.hip)
+bool lattice_coords(Ctx& ctx, const Mesh& m, int64_t n_rows, DevBuf<int32_t> layer[3], int64_t L[3]);
 // rhs_add: 1 accumulate into rhs (applyConstantSourceToRhs), 0 overwrite
 void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add);
 void assemble_elasticity_tri(Bsr& b, double lambda, double mu2);
@@ -408,6 +452,11 @@ int mg_levels(const LinearSystem& ls);
 void spmv_blk_epi(Ctx& ctx, int k, int epi, int64_t n_brows, const int64_t* bp, const int32_t* bc, const double* vals,
                   const double* x, double* y, const double* b, const double* dinv, double omega);
 void ls_apply_bcs(LinearSystem& ls);
+void ls_set_csr_mapped(LinearSystem& ls, const int32_t* rows, const int32_t* columns, double* values, int32_t nb_row,
+                       int32_t nnz, const int32_t* index_host, int64_t n_index);
+void ls_mapped_gather(LinearSystem& ls);
+void ls_mapped_scatter_back(LinearSystem& ls);
+void ls_mapped_point_update(LinearSystem& ls, int32_t row, int32_t col, double v, bool set);
 void ls_solve(LinearSystem& ls, afem_solve_stats* st);
 void ls_spmv(LinearSystem& ls, const double* x, double* y);
 void ls_build_from_host_coo(LinearSystem& ls);

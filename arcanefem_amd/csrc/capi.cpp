@@ -482,6 +482,8 @@ int afem_bsr_compute_sparsity(afem_bsr* b)
   NOT_NULL(b);
   b->mesh->ctx->set_device();
   b->has_sparsity = false;
+  b->fplan = FunctorPlan();
+  b->hand = HandOver();
   build_structure(*b->mesh, b->s);
   b->values.alloc((size_t)b->s.nnz * b->nb_dof * b->nb_dof);
   AFEM_HIP(hipMemsetAsync(b->values.p, 0, b->values.bytes(), b->mesh->ctx->stream));
@@ -607,6 +609,59 @@ int afem_bsr_assembly_view(afem_bsr* b, afem_assembly_view* v)
   v->values = b->values.p;
   v->error_flag = b->gen_flag.p;
   v->stream = (void*)m.ctx->stream;
+  API_END
+}
+
+int afem_bsr_to_csr32_mapped(afem_bsr* b, const int32_t* dof_of, int64_t n_dof_rows, afem_csr32_view* v)
+{
+  API_BEGIN
+  AFEM_RANGE("afem: BSRFormat::toLinearSystem (mapped CSR)");
+  NOT_NULL(b);
+  NOT_NULL(v);
+  AFEM_REQUIRE(b->has_sparsity, AFEM_ERR_STATE, "no sparsity (computeSparsity first)");
+  b->mesh->ctx->set_device();
+  if (dof_of) bsr_csr32_mapped_build(*b, dof_of, n_dof_rows);
+  double* vals = bsr_csr32_mapped_values(*b);
+  const HandOver& H = b->hand;
+  v->n_rows = H.n_rows;
+  v->nnz = H.nnz;
+  v->rows = H.rows.p;
+  v->rows_nb_column = H.rnc.p;
+  v->columns = H.cols.p;
+  v->values = vals;
+  v->identity = H.identity ? 1 : 0;
+  API_END
+}
+
+int afem_bsr_functor_plan(afem_bsr* b, afem_functor_plan* p)
+{
+  API_BEGIN
+  AFEM_RANGE("afem: BSRFormat functor plan");
+  NOT_NULL(b);
+  NOT_NULL(p);
+  AFEM_REQUIRE(b->has_sparsity, AFEM_ERR_STATE, "no sparsity (computeSparsity first)");
+  b->mesh->ctx->set_device();
+  if (!b->fplan.valid) functor_plan_build(*b);
+  const FunctorPlan& P = b->fplan;
+  p->n_units = P.n_units;
+  p->n_stages = P.n_stages;
+  p->n_entries = P.n_entries;
+  p->rows_per_layer = P.rl;
+  p->width = P.w;
+  p->nbuf = P.nbuf;
+  p->wide = P.wide;
+  p->block_size = b->nb_dof;
+  p->nb_node_per_cell = b->mesh->nv;
+  p->ordered_per_block = b->order_per_block ? 1 : 0;
+  p->lattice = P.lattice;
+  p->units = P.units.p;
+  p->stage_ptr = P.stage_ptr.p;
+  p->layer_rows = P.layer_rows.p;
+  p->entries = P.ent.p;
+  p->entries2 = P.wide ? P.ent2.p : nullptr;
+  p->rows = b->s.row_ptr.p;
+  p->values = b->values.p;
+  p->stream = (void*)b->mesh->ctx->stream;
   API_END
 }
 
@@ -745,6 +800,7 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
   ls->hv_rows = nullptr;
   ls->hv_cols = nullptr;
   ls->hv_vals = nullptr;
+  ls->mv_vals = nullptr;
   ls->csr_n = b->s.n_rows * k;
   ls->csr_nnz = b->s.nnz * k * k;
   API_END
@@ -861,7 +917,10 @@ int afem_ls_matrix_add_value(afem_ls* ls, int32_t row, int32_t col, double v)
                "matrixAddValue: row or column out of range");
   ls->ctx->set_device();
   if (ls_uses_device_view(ls)) {
-    ls_point_update(*ls, row, col, v, false);
+    if (ls->mv_vals)
+      ls_mapped_point_update(*ls, row, col, v, false);
+    else
+      ls_point_update(*ls, row, col, v, false);
     if (ls->hv_vals) host_view_update(ls, row, col, v, false);
   }
   else {
@@ -881,7 +940,10 @@ int afem_ls_matrix_set_value(afem_ls* ls, int32_t row, int32_t col, double v)
                "matrixSetValue: row or column out of range");
   ls->ctx->set_device();
   if (ls_uses_device_view(ls)) {
-    ls_point_update(*ls, row, col, v, true);
+    if (ls->mv_vals)
+      ls_mapped_point_update(*ls, row, col, v, true);
+    else
+      ls_point_update(*ls, row, col, v, true);
     if (ls->hv_vals) host_view_update(ls, row, col, v, true);
   }
   else {
@@ -972,6 +1034,7 @@ int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows
   ctx.sync();
   ls->csr_rows = ls->own_rows.p;
   ls->csr_diag = nullptr;
+  ls->mv_vals = nullptr;
   ls->blk_k = 0;
   ls->mg_k = 0;
   ls->mg.reset();
@@ -991,6 +1054,35 @@ int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows
     ls->add_map.clear();
     ls->set_map.clear();
   }
+  API_END
+}
+
+int afem_ls_set_csr_values_mapped(afem_ls* ls, const int32_t* rows, const int32_t* rows_nb_column,
+                                  const int32_t* columns, double* values, int32_t nb_row, int32_t nb_nz,
+                                  const int32_t* index, int64_t n_index)
+{
+  API_BEGIN
+  NOT_NULL(ls);
+  NOT_NULL(rows);
+  NOT_NULL(columns);
+  NOT_NULL(values);
+  NOT_NULL(index);
+  AFEM_REQUIRE(nb_row >= 0 && nb_nz >= 0 && n_index >= 0, AFEM_ERR_ARG, "setCSRValues: negative size");
+  (void)rows_nb_column;  // derived from rows, as femutils/HypreDoFLinearSystem.cc:140-141 does
+  ls->ctx->set_device();
+  ls->has_csr = false;
+  ls_set_csr_mapped(*ls, rows, columns, values, nb_row, nb_nz, index, n_index);
+  ls->csr_diag = nullptr;
+  ls->blk_k = 0;
+  ls->mg_k = 0;
+  ls->mg.reset();
+  ls->has_csr = true;
+  ls->csr_from_coo = false;
+  ls->hv_rows = nullptr;
+  ls->hv_cols = nullptr;
+  ls->hv_vals = nullptr;
+  ls->add_map.clear();
+  ls->set_map.clear();
   API_END
 }
 
@@ -1082,9 +1174,24 @@ int afem_ls_apply_boundary_conditions(afem_ls* ls)
   API_BEGIN
   AFEM_RANGE("afem: applyBoundaryConditions");
   NOT_NULL(ls);
-  ls->ctx->set_device();
+  Ctx& ctx = *ls->ctx;
+  ctx.set_device();
   if (!ls->has_csr && (!ls->add_map.empty() || !ls->set_map.empty())) ls_build_from_host_coo(*ls);
+  const bool host_view = ls->hv_vals && ls->has_csr && !ls->csr_from_coo && ls->csr_nnz > 0;
+  if (host_view)  // the live host view (as afem_ls_solve reads it)
+    AFEM_HIP(hipMemcpyAsync(ls->own_vals.p, ls->hv_vals, (size_t)ls->csr_nnz * 8, hipMemcpyHostToDevice, ctx.stream));
+  const bool mapped = ls->mv_vals && ls->has_csr && !ls->csr_from_coo;
+  if (mapped) ls_mapped_gather(*ls);
   ls_apply_bcs(*ls);
+  if (mapped) ls_mapped_scatter_back(*ls);  // into the caller's view, as for a host view below
+  if (host_view) {
+    // Hypre applies the forced values to the view's own values
+    // (femutils/HypreDoFLinearSystem.cc:319-382): write them back, so the
+    // re-read at solve() sees the eliminated rows / columns and the second
+    // pass there is a no-op (the right-hand side is not corrected twice)
+    AFEM_HIP(hipMemcpyAsync(ls->hv_vals, ls->own_vals.p, (size_t)ls->csr_nnz * 8, hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+  }
   API_END
 }
 
@@ -1106,6 +1213,7 @@ int afem_ls_clear_values(afem_ls* ls)
   ls->hv_rows = nullptr;
   ls->hv_cols = nullptr;
   ls->hv_vals = nullptr;
+  ls->mv_vals = nullptr;
   ls->add_map.clear();
   ls->set_map.clear();
   ls->host_elim.clear();
@@ -1128,6 +1236,11 @@ int afem_ls_solve(afem_ls* ls, afem_solve_stats* st)
     ls->ctx->set_device();
     AFEM_HIP(hipMemcpyAsync(ls->own_vals.p, ls->hv_vals, (size_t)ls->csr_nnz * 8, hipMemcpyHostToDevice,
                             ls->ctx->stream));
+  }
+  if (ls->mv_vals && ls->has_csr && !ls->csr_from_coo) {
+    // a mapped device view: its values as they are now (same contract)
+    ls->ctx->set_device();
+    ls_mapped_gather(*ls);
   }
   ls_solve(*ls, st);
   API_END

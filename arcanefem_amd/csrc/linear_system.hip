@@ -1588,6 +1588,7 @@ void ls_build_from_host_coo(LinearSystem& ls)
   ctx.sync();
   ls.has_csr = true;
   ls.csr_from_coo = true;
+  ls.mv_vals = nullptr;
   ls.csr_n = ls.n_rows;
   ls.csr_nnz = (int64_t)cols.size();
   ls.csr_rows = ls.own_rows.p;

@@ -1057,15 +1057,14 @@ __global__ void k_strip_width(int64_t n_slices, const int32_t* __restrict__ stri
 
 }  // namespace
 
-namespace {
-// the owned nodes' lattice (see k_axis_keys): on success the brick order of
-// that lattice in s.perm (s.n_slices, s.run, s.brick_order set) and true
-bool lattice_order(Ctx& ctx, const Mesh& m, int64_t n_rows, Structure& s)
+// the owned nodes' lattice (see k_axis_keys): on success every owned node's
+// layer index per axis in layer[0..2] (the sorted-coordinate order of each
+// axis), the layer counts in L and true
+bool lattice_coords(Ctx& ctx, const Mesh& m, int64_t n_rows, DevBuf<int32_t> layer[3], int64_t L[3])
 {
   DevBuf<uint64_t> keys, keys_s;
   DevBuf<int32_t> ids, ids_s, flag;
   DevBuf<int64_t> scan;
-  DevBuf<int32_t> layer[3];
   keys.alloc(n_rows);
   keys_s.alloc(n_rows);
   ids.alloc(n_rows);
@@ -1079,7 +1078,6 @@ bool lattice_order(Ctx& ctx, const Mesh& m, int64_t n_rows, Structure& s)
   tmp.alloc(tmp_bytes > 0 ? tmp_bytes : 1);
   DevBuf<unsigned long long> gap;
   gap.alloc(1);
-  int64_t L[3];
   for (int a = 0; a < 3; ++a) {
     hipLaunchKernelGGL(k_axis_keys, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, m.coords.p, a,
                        keys.p, ids.p);
@@ -1106,6 +1104,17 @@ bool lattice_order(Ctx& ctx, const Mesh& m, int64_t n_rows, Structure& s)
     AFEM_LAUNCHED();
   }
   if (L[0] < 2 || L[1] < 2 || L[2] < 2 || L[0] * L[1] * L[2] != n_rows) return false;
+  return true;
+}
+
+namespace {
+// the brick order of the owned nodes' lattice (lattice_coords) in s.perm
+// (s.n_slices, s.run, s.brick_order set) and true, or false (no lattice)
+bool lattice_order(Ctx& ctx, const Mesh& m, int64_t n_rows, Structure& s)
+{
+  DevBuf<int32_t> layer[3];
+  int64_t L[3];
+  if (!lattice_coords(ctx, m, n_rows, layer, L)) return false;
   DevBuf<int32_t> lat, bad;
   lat.alloc(n_rows);
   bad.alloc(1);
@@ -1135,6 +1144,33 @@ bool lattice_order(Ctx& ctx, const Mesh& m, int64_t n_rows, Structure& s)
 }
 }  // namespace
 
+int64_t node_cell_adjacency(Ctx& ctx, const Mesh& m, int64_t n_rows, DevBuf<int64_t>& nc_ptr, DevBuf<int32_t>& nc)
+{
+  const int nv = m.nv;
+  DevBuf<int32_t> cnt;
+  cnt.alloc(n_rows);
+  AFEM_HIP(hipMemsetAsync(cnt.p, 0, cnt.bytes(), ctx.stream));
+  const int64_t n_entries = m.n_cells * nv;
+  if (n_entries) {
+    hipLaunchKernelGGL(k_count_incidence, dim3(grid_for(n_entries, 256)), dim3(256), 0, ctx.stream, n_entries,
+                       m.cell_node.p, n_rows, cnt.p);
+    AFEM_LAUNCHED();
+  }
+  nc_ptr.alloc(n_rows + 1);
+  exclusive_scan_i32_to_i64(ctx, cnt.p, nc_ptr.p, n_rows);
+  const int64_t n_inc = read_i64(ctx, nc_ptr.p + n_rows);
+  nc.alloc(n_inc > 0 ? n_inc : 1);
+  AFEM_HIP(hipMemsetAsync(cnt.p, 0, cnt.bytes(), ctx.stream));
+  if (n_entries) {
+    hipLaunchKernelGGL(k_fill_incidence, dim3(grid_for(n_entries, 256)), dim3(256), 0, ctx.stream, m.n_cells, nv,
+                       m.cell_node.p, n_rows, nc_ptr.p, cnt.p, nc.p);
+    AFEM_LAUNCHED();
+  }
+  hipLaunchKernelGGL(k_sort_lists, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, nc_ptr.p, nc.p);
+  AFEM_LAUNCHED();
+  return n_inc;
+}
+
 void build_structure(Mesh& m, Structure& s)
 {
   Ctx& ctx = *m.ctx;
@@ -1146,30 +1182,9 @@ void build_structure(Mesh& m, Structure& s)
   AFEM_REQUIRE(n_rows > 0, AFEM_ERR_ARG, "computeSparsity: mesh has no owned node");
 
   // 1. node -> cell adjacency of owned nodes
-  DevBuf<int32_t> cnt;
-  cnt.alloc(n_rows);
-  AFEM_HIP(hipMemsetAsync(cnt.p, 0, cnt.bytes(), ctx.stream));
-  const int64_t n_entries = m.n_cells * nv;
-  if (n_entries) {
-    hipLaunchKernelGGL(k_count_incidence, dim3(grid_for(n_entries, 256)), dim3(256), 0, ctx.stream, n_entries,
-                       m.cell_node.p, n_rows, cnt.p);
-    AFEM_LAUNCHED();
-  }
   DevBuf<int64_t> nc_ptr;
-  nc_ptr.alloc(n_rows + 1);
-  exclusive_scan_i32_to_i64(ctx, cnt.p, nc_ptr.p, n_rows);
-  const int64_t n_inc = read_i64(ctx, nc_ptr.p + n_rows);
-  s.n_incidences = n_inc;
   DevBuf<int32_t> nc;
-  nc.alloc(n_inc > 0 ? n_inc : 1);
-  AFEM_HIP(hipMemsetAsync(cnt.p, 0, cnt.bytes(), ctx.stream));
-  if (n_entries) {
-    hipLaunchKernelGGL(k_fill_incidence, dim3(grid_for(n_entries, 256)), dim3(256), 0, ctx.stream, m.n_cells, nv,
-                       m.cell_node.p, n_rows, nc_ptr.p, cnt.p, nc.p);
-    AFEM_LAUNCHED();
-  }
-  hipLaunchKernelGGL(k_sort_lists, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, nc_ptr.p, nc.p);
-  AFEM_LAUNCHED();
+  s.n_incidences = node_cell_adjacency(ctx, m, n_rows, nc_ptr, nc);
 
   // 2. rows = sorted unique union of incident cells' nodes
   DevBuf<int32_t> row_len;

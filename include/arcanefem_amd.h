@@ -285,6 +285,73 @@ typedef struct afem_assembly_view {
   void* stream;              /* hipStream_t of the structure's context */
 } afem_assembly_view;
 int afem_bsr_assembly_view(afem_bsr* bsr, afem_assembly_view* view);
+/* Cell-unit plan of a structure for generic element functors: what the
+ * atomic-free cell kernel of include/arcanefem_amd_generic.hpp
+ * (afem::generic::assemble_bilinear) walks.  The reference's
+ * BSRFormat<NB_DOF>::assembleBilinear(f) (femutils/BSRFormat.h:786-837,
+ * 937-1100, 1105-1111) evaluates f once per cell and scatters with global
+ * atomics (or once per (row, cell) without them).  Here one wavefront owns a
+ * UNIT -- at most 64 owned rows per layer: a column of fx x fy lattice nodes
+ * over a segment of z layers (meshes on a lattice: the generator's boxes and
+ * array-fed lattice meshes), else 64/NB_DOF^2-row pieces of the structure's
+ * processing-order slices -- and keeps the k x k blocks of its rows in LDS
+ * (two layers live).  A unit's cells come in STAGES (stage L: the cells whose
+ * highest in-unit vertex lies in layer L; after stage L layer L-1 is
+ * complete and is written out): every lane evaluates f for one cell of the
+ * stage at a time and adds the rows it owns into LDS.  Entries (one per
+ * (unit, cell)): compact (width <= 16): 4 u32 {cell, slots of vertices 0|1,
+ * slots of 2|3 (4 bits per vertex b), row positions (8 bits per vertex a:
+ * 0x80 valid | layer parity << 6 | lane)}; wide: 4 u32 of 8-bit slots per
+ * vertex + 2 u32 {cell, positions}.  Built at the first call (one-time,
+ * device), rebuilt with the structure; owned by bsr. */
+typedef struct afem_functor_unit {
+  int64_t first_stage;       /* index of the unit's first stage (= layer) */
+  int32_t n_stages;          /* layers of the unit */
+  int32_t flags;             /* 1: rows come in runs of 8 consecutive rows per 8 lanes (coalesced write-back) */
+} afem_functor_unit;
+typedef struct afem_functor_plan {
+  int64_t n_units;
+  int64_t n_stages;          /* stages (= layers) over all units */
+  int64_t n_entries;         /* (unit, cell) pairs: cell evaluations per assembly */
+  int32_t rows_per_layer;    /* lanes that own a row (<= 64) */
+  int32_t width;             /* slot stride of the LDS accumulators (max row length) */
+  int32_t nbuf;              /* 2: two layers live (lattice columns), 1: single-layer units */
+  int32_t wide;              /* entry format: 0 compact, 1 wide */
+  int32_t block_size;        /* NB_DOF */
+  int32_t nb_node_per_cell;
+  int32_t ordered_per_block; /* value layout, as afem_csr_view */
+  int32_t lattice;           /* 1: lattice columns, 0: slice pieces */
+  const afem_functor_unit* units; /* device [n_units] */
+  const int64_t* stage_ptr;  /* device [n_stages+1]: entries of stage s are [stage_ptr[s], stage_ptr[s+1]) */
+  const int32_t* layer_rows; /* device [n_stages*rows_per_layer]: row of (stage, lane) or -1 */
+  const uint32_t* entries;   /* device, 16 B per entry (see above) */
+  const uint32_t* entries2;  /* device, wide format: 8 B per entry (cell, positions); else NULL */
+  const int64_t* rows;       /* device [n_rows+1] block-row offsets */
+  double* values;            /* device, the matrix's values */
+  void* stream;              /* hipStream_t of the structure's context */
+} afem_functor_plan;
+int afem_bsr_functor_plan(afem_bsr* bsr, afem_functor_plan* plan);
+/* BSRFormat::toLinearSystem with use_csr (femutils/BSRFormat.h:414-430 through
+ * BSRMatrix::toCsr, :194-256) in the CALLER's DoF numbering, on the device:
+ * dof_of[node*NB_DOF + i] (host, n_nodes*NB_DOF entries: owned and ghost
+ * nodes in libafem's numbering) is the caller's DoF local id, n_dof_rows the
+ * caller's DoF count.  The CSR has n_dof_rows rows in the CSRFormatView layout
+ * (rows without sentinel, rows_nb_column, columns = caller DoF ids in block
+ * order; rows of DoFs that are not owned are empty, the isOwn filter of
+ * :815, 870), device memory owned by bsr.  dof_of != NULL (re)builds the
+ * structure (one time); NULL reuses it.  Every call puts the current values in
+ * that order (one gather kernel on the context stream; no copy at all when the
+ * map is the identity: values then alias the matrix). */
+typedef struct afem_csr32_view {
+  int64_t n_rows;
+  int64_t nnz;
+  const int32_t* rows;           /* device [n_rows] */
+  const int32_t* rows_nb_column; /* device [n_rows] */
+  const int32_t* columns;        /* device [nnz] */
+  double* values;                /* device [nnz] */
+  int32_t identity;              /* 1: values alias the matrix's own array */
+} afem_csr32_view;
+int afem_bsr_to_csr32_mapped(afem_bsr* bsr, const int32_t* dof_of, int64_t n_dof_rows, afem_csr32_view* out);
 /* Copies the internal (block) arrays to host. */
 int afem_bsr_download(afem_bsr* bsr, int64_t* rows, int32_t* columns, double* values);
 /* BSRFormat::toLinearSystem (femutils/BSRFormat.h:414-430): hands the matrix to
@@ -362,6 +429,16 @@ int afem_ls_eliminate_row_column(afem_ls* ls, int32_t row, double v);
  * view after this call are seen by the solve; the BCs go into the device copy. */
 int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows_nb_column, const int32_t* columns,
                            double* values, int32_t nb_row, int32_t nb_nz, int mem);
+/* setCSRValues for a DEVICE view in the caller's numbering (several
+ * subdomains: Arcane interleaves owned and ghost DoFs): index[lid] is the
+ * linear system's index of caller DoF lid (owned: [0, n_rows), ghosts:
+ * [n_rows, n_cols), -1 none; host, n_index entries).  The owned rows are kept
+ * in the linear system's order (structure built here, on the device); the
+ * caller's values stay the matrix until solve (re-read there), point updates
+ * and afem_ls_apply_boundary_conditions write through to them. */
+int afem_ls_set_csr_values_mapped(afem_ls* ls, const int32_t* rows, const int32_t* rows_nb_column,
+                                  const int32_t* columns, double* values, int32_t nb_row, int32_t nb_nz,
+                                  const int32_t* index, int64_t n_index);
 int afem_ls_has_set_csr_values(afem_ls* ls, int* has);
 int afem_ls_get_csr_values(afem_ls* ls, afem_csr_view* view);
 /* rhsVariable / solutionVariable / getForced{Info,Value} / getElimination{Info,Value}:

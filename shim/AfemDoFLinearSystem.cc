@@ -32,9 +32,11 @@
  * own().index() order, then the ghosts): the global row numbering of the
  * Hypre backend (_computeMatrixNumerotation, :264-303) is the same
  * owned-first order.  When the permutation is the identity (one subdomain)
- * the CSR view is handed over without a copy; otherwise a permuted copy of
- * the owned rows is made once per setCSRValues (ghost rows are empty: the
- * assembly filters isOwn(row), femutils/BSRFormat.h:815,870).
+ * the CSR view is handed over without a copy; otherwise libafem keeps the
+ * owned rows of a device view in its order on the device
+ * (afem_ls_set_csr_values_mapped: the module's values stay the matrix, read
+ * at solve) and a host view is copied permuted once per setCSRValues (ghost
+ * rows are empty: the assembly filters isOwn(row), femutils/BSRFormat.h:815,870).
  *
  * Parallel: one process per GPU, one Arcane subdomain per rank.  The halo
  * lists are the DoF family's synchronisation lists built by
@@ -211,9 +213,17 @@ class AfemDoFLinearSystemImpl
                 "setCSRValues");
       return;
     }
-    // owned rows in afem order, columns renumbered; a host copy (once per view),
-    // kept in members: libafem reads a host view at solve()
     const Int32 nb_row = v.nbRow(), nnz = v.nbValue();
+    if (mem == AFEM_MEM_DEVICE) {
+      // device view (BSRFormat::toLinearSystem): libafem renumbers it on the
+      // device, the module's values stay the matrix until solve()
+      afemCheck(afem_ls_set_csr_values_mapped(m_ls, v.rows().data(), v.rowsNbColumn().data(), v.columns().data(),
+                                              v.values().data(), nb_row, nnz, m_index.data(), m_index.size()),
+                "setCSRValues");
+      return;
+    }
+    // host view: owned rows in afem order, columns renumbered; a host copy
+    // (once per view), kept in members: libafem reads a host view at solve()
     std::vector<Int32> rows(nb_row), cols(nnz);
     std::vector<Real> vals(nnz);
     afemCheck(afem_memcpy(m_ctx, rows.data(), v.rows().data(), sizeof(Int32) * nb_row, AFEM_MEM_HOST, mem), "copy");

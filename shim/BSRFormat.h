@@ -16,27 +16,35 @@
  * directory precedes femutils/ on the include path (shim/CMakeLists.txt,
  * AFEM_BSR_SHIM).  The module's element lambda
  *   [=] ARCCORE_HOST_DEVICE (CellLocalId c) { return _computeElementMatrixTetra4Gpu(c, cn_cv, in_node_coord); }
- * runs inside libafem's generic cell kernel (one lane per cell, binary search
- * of the sorted row, f64 atomics: the reference's assembleBilinearAtomic
- * semantics); it still reads the geometry through the Arcane views it
- * captured.  The module's own BC kernels then write the linear system's
- * variables, as with the reference.
+ * runs inside libafem's cell-unit kernel (afem::generic::assemble_bilinear:
+ * one wavefront per unit of rows, the element blocks added in LDS, every
+ * value written once -- no global atomics, no column search; it still reads
+ * the geometry through the Arcane views it captured).  Like the reference it
+ * accumulates into the values; right after computeSparsity /
+ * resetMatrixValues (values known to be zero) it writes them instead (same
+ * result, no read of the old values).  The module's own BC kernels then
+ * write the linear system's variables, as with the reference.
  *
- * Numbering.  libafem numbers the owned nodes first, then the ghosts; cells
- * keep Arcane's local ids (so CellLocalId(c) in the lambda is the cell the
- * kernel scatters) and their nodes are renumbered.  With one subdomain and an
- * identity numbering (own nodes are lids 0..n_own-1) the CSR handed to the
- * linear system aliases libafem's device values (NB_DOF = 1, per-row layout:
- * no copy per assembly; rows / columns converted to the reference's int32
- * layout once per structure).  Otherwise toLinearSystem goes through
- * matrixAddValue per entry, as BSRMatrix::toLinearSystem does (:261-280).
+ * Numbering.  libafem numbers the owned nodes first, then the ghosts, and
+ * gets the mesh's cells in enumeration order (local ids may have holes): the
+ * lambda is called with the Arcane CellLocalId of the cell the kernel
+ * scatters (a device map), never with a hole.  toLinearSystem with
+ * use_csr hands the linear system a DEVICE CSR view in the module's DoF
+ * numbering (BSRMatrix::toCsr, femutils/BSRFormat.h:194-256: rows = DoF local
+ * ids, columns = node DoF ids in block order) for every NB_DOF and any
+ * numbering: libafem builds that CSR once from the DoF ids of
+ * FemDoFsOnNodes and gathers the values into it at each hand-over (one
+ * kernel; with the identity numbering and NB_DOF = 1 the values are the
+ * matrix's own array, no copy).  Without use_csr, toLinearSystem goes
+ * through matrixAddValue per entry, as BSRMatrix::toLinearSystem does
+ * (:261-280).
  *
  * Status: written against the reference's interfaces; Arcane is not
- * installed here, so it is compiled against the single-subdomain Arcane mock
- * of tests/arcane_mock/ (test infrastructure) and run on the GPU by
- * tests/test_gpu_shim.py: initialize / computeSparsity / assembleBilinear(a
- * device element lambda) / toLinearSystem / solve on the reference's
- * sphere_3D case, equal to the oracle and the golden.
+ * installed here, so it is compiled against the Arcane mock of
+ * tests/arcane_mock/ (test infrastructure) and run on the GPU by
+ * tests/test_gpu_shim.py: BSRFormat<1> (Poisson) and BSRFormat<3>
+ * (elasticity) on 1-3 subdomains with Arcane-style interleaved local ids,
+ * against the oracle and the golden.
  */
 #ifndef AFEM_SHIM_BSRFORMAT_H
 #define AFEM_SHIM_BSRFORMAT_H
@@ -75,6 +83,8 @@ class BSRFormat : public TraceAccessor
 
   ~BSRFormat()
   {
+    if (m_d_cell_lid)
+      afem_free(m_ctx, m_d_cell_lid);
     if (m_bsr)
       afem_bsr_destroy(m_bsr);
     if (m_afem_mesh)
@@ -103,32 +113,53 @@ class BSRFormat : public TraceAccessor
   void computeSparsity()
   {
     _check(afem_bsr_compute_sparsity(m_bsr), "afem_bsr_compute_sparsity");
-    m_csr_ready = false;
+    m_map_ready = false;
+    m_values_zero = true;
   }
 
   template <class Function>
   void assembleBilinear(Function compute_element_matrix)
   {
     m_queue.barrier();  // the module's previous device work (views it captured) is done
-    auto f = [=] __device__(int32_t c) { return compute_element_matrix(CellLocalId(c)); };
-    const int rc = m_mesh->dimension() == 2 ? afem::generic::assemble_bilinear<3, NB_DOF>(m_bsr, f)
-                                            : afem::generic::assemble_bilinear<4, NB_DOF>(m_bsr, f);
+    const int32_t* cell_lid = m_d_cell_lid;
+    auto f = [=] __device__(int32_t c) { return compute_element_matrix(CellLocalId(cell_lid[c])); };
+    const auto mode = m_values_zero ? afem::generic::Mode::Overwrite : afem::generic::Mode::Accumulate;
+    const int rc = m_mesh->dimension() == 2 ? afem::generic::assemble_bilinear<3, NB_DOF>(m_bsr, f, mode)
+                                            : afem::generic::assemble_bilinear<4, NB_DOF>(m_bsr, f, mode);
     _check(rc, "BSRFormat::assembleBilinear");
+    m_values_zero = false;
   }
 
-  void resetMatrixValues() { _check(afem_bsr_reset_values(m_bsr), "afem_bsr_reset_values"); }
+  void resetMatrixValues()
+  {
+    _check(afem_bsr_reset_values(m_bsr), "afem_bsr_reset_values");
+    m_values_zero = true;
+  }
 
   void toLinearSystem(DoFLinearSystem& linear_system)
   {
-    if (m_use_csr && m_identity && NB_DOF == 1) {
+    if (m_use_csr) {
       if (!linear_system.hasSetCSRValues())
         ARCANE_THROW(ArgumentException, "BSRFormat(toLinearSystem): Linear system was set to use CSR but is incompatible");
-      _exportStructure();
-      afem_csr_view v;
-      _check(afem_bsr_view(m_bsr, &v), "afem_bsr_view");
-      // values alias libafem's device array (per-row layout = CSR order for NB_DOF = 1)
-      Span<Real> values(v.values, static_cast<Int64>(v.nnz_blocks));
-      CSRFormatView view(m_rows.to1DSpan(), m_rows_nb_column.to1DSpan(), m_columns.to1DSpan(), values);
+      // BSRMatrix::toCsr in the module's DoF numbering, on the device
+      afem_csr32_view v;
+      if (!m_map_ready) {
+        auto node_dof(m_dofs_on_nodes.nodeDoFConnectivityView());
+        std::vector<int32_t> dof_of(m_node_of.size() * NB_DOF);
+        Int32 n_dof_rows = 0;
+        for (size_t a = 0; a < m_node_of.size(); ++a)
+          for (Int32 i = 0; i < NB_DOF; ++i) {
+            const Int32 d = node_dof.dofId(NodeLocalId(m_node_of[a]), i).localId();
+            dof_of[a * NB_DOF + i] = d;
+            n_dof_rows = d + 1 > n_dof_rows ? d + 1 : n_dof_rows;
+          }
+        _check(afem_bsr_to_csr32_mapped(m_bsr, dof_of.data(), n_dof_rows, &v), "BSRFormat::toLinearSystem");
+        m_map_ready = true;
+      }
+      else
+        _check(afem_bsr_to_csr32_mapped(m_bsr, nullptr, 0, &v), "BSRFormat::toLinearSystem");
+      CSRFormatView view(Span<const Int32>(v.rows, v.n_rows), Span<const Int32>(v.rows_nb_column, v.n_rows),
+                         Span<const Int32>(v.columns, v.nnz), Span<Real>(v.values, v.nnz));
       linear_system.setCSRValues(view);
       return;
     }
@@ -157,13 +188,13 @@ class BSRFormat : public TraceAccessor
   const FemDoFsOnNodes& m_dofs_on_nodes;
   IMesh* m_mesh = nullptr;
   bool m_use_csr = false;
-  bool m_identity = true;
-  bool m_csr_ready = false;
+  bool m_map_ready = false;   //!< libafem holds the DoF map of toLinearSystem
+  bool m_values_zero = true;  //!< values known to be zero (computeSparsity / resetMatrixValues)
   afem_ctx* m_ctx = nullptr;
   afem_mesh* m_afem_mesh = nullptr;
   afem_bsr* m_bsr = nullptr;
   std::vector<Int32> m_node_of; //!< libafem node -> Arcane node local id
-  NumArray<Int32, MDDim1> m_rows, m_rows_nb_column, m_columns;
+  int32_t* m_d_cell_lid = nullptr; //!< device: libafem cell -> Arcane cell local id
 
   static void _check(int rc, const char* what)
   {
@@ -171,7 +202,7 @@ class BSRFormat : public TraceAccessor
       ARCANE_FATAL("libafem: {0} failed (code {1}): {2}", what, rc, afem_last_error());
   }
 
-  //! owned nodes first (own() order), then the ghosts; cells in local-id order
+  //! owned nodes first (own() order), then the ghosts; the cells in enumeration order
   void _buildMesh()
   {
     const Int32 max_lid = m_mesh->nodeFamily()->maxLocalId();
@@ -188,19 +219,28 @@ class BSRFormat : public TraceAccessor
         m_node_of.push_back(inode.itemLocalId());
       }
     }
-    m_identity = true;
-    for (size_t a = 0; a < m_node_of.size() && m_identity; ++a)
-      m_identity = m_node_of[a] == static_cast<Int32>(a);
+    // the mesh's cells only (local ids may have holes): libafem cell c is
+    // Arcane cell m_cell_lid[c], which the element lambda is called with
     const int nv = m_mesh->dimension() + 1;
-    const Int32 max_cell = m_mesh->cellFamily()->maxLocalId();
-    std::vector<int32_t> cell_node(static_cast<size_t>(max_cell) * nv, 0);
+    std::vector<int32_t> cell_node, cell_lid;
     ENUMERATE_CELL (icell, m_mesh->allCells()) {
       Cell cell = *icell;
       if (cell.nbNode() != nv)
         ARCANE_THROW(NotImplementedException, "BSRFormat: P1 simplices only (TRIA3 / TETRA4)");
+      cell_lid.push_back(icell.itemLocalId());
       for (int i = 0; i < nv; ++i)
-        cell_node[static_cast<size_t>(icell.itemLocalId()) * nv + i] = afem_of[cell.node(i).localId()];
+        cell_node.push_back(afem_of[cell.node(i).localId()]);
     }
+    const Int64 n_cells = static_cast<Int64>(cell_lid.size());
+    if (m_d_cell_lid)
+      _check(afem_free(m_ctx, m_d_cell_lid), "afem_free");
+    m_d_cell_lid = nullptr;
+    void* p = nullptr;
+    _check(afem_malloc(m_ctx, sizeof(int32_t) * (n_cells > 0 ? n_cells : 1), &p), "afem_malloc");
+    m_d_cell_lid = static_cast<int32_t*>(p);
+    if (n_cells > 0)
+      _check(afem_memcpy(m_ctx, m_d_cell_lid, cell_lid.data(), sizeof(int32_t) * n_cells, AFEM_MEM_DEVICE, AFEM_MEM_HOST),
+             "afem_memcpy");
     VariableNodeReal3& node_coord = m_mesh->nodesCoordinates();
     std::vector<double> coords(3 * m_node_of.size());
     for (size_t a = 0; a < m_node_of.size(); ++a) {
@@ -209,31 +249,9 @@ class BSRFormat : public TraceAccessor
       coords[3 * a + 1] = x.y;
       coords[3 * a + 2] = x.z;
     }
-    _check(afem_mesh_create(m_ctx, m_mesh->dimension(), nv, static_cast<int64_t>(m_node_of.size()), n_own, max_cell,
+    _check(afem_mesh_create(m_ctx, m_mesh->dimension(), nv, static_cast<int64_t>(m_node_of.size()), n_own, n_cells,
                             cell_node.data(), coords.data(), AFEM_MEM_HOST, &m_afem_mesh),
            "afem_mesh_create");
-  }
-
-  //! rows / rows_nb_column / columns in the reference's int32 layout (once per structure)
-  void _exportStructure()
-  {
-    if (m_csr_ready)
-      return;
-    int64_t n_rows = 0, nnz = 0;
-    _check(afem_bsr_get_sizes(m_bsr, &n_rows, &nnz), "afem_bsr_get_sizes");
-    std::vector<int32_t> rows(n_rows), rnc(n_rows), cols(nnz);
-    _check(afem_bsr_export_csr32(m_bsr, rows.data(), rnc.data(), cols.data(), nullptr), "afem_bsr_export_csr32");
-    m_rows.resize(n_rows);
-    m_rows_nb_column.resize(n_rows);
-    m_columns.resize(nnz);
-    auto mem = m_queue.memoryRessource();
-    m_rows = NumArray<Int32, MDDim1>(n_rows, mem);
-    m_rows_nb_column = NumArray<Int32, MDDim1>(n_rows, mem);
-    m_columns = NumArray<Int32, MDDim1>(nnz, mem);
-    m_rows.copy(ConstArrayView<Int32>(static_cast<Int32>(n_rows), rows.data()));
-    m_rows_nb_column.copy(ConstArrayView<Int32>(static_cast<Int32>(n_rows), rnc.data()));
-    m_columns.copy(ConstArrayView<Int32>(static_cast<Int32>(nnz), cols.data()));
-    m_csr_ready = true;
   }
 };
 

@@ -23,8 +23,9 @@
 //   <case_prefix><r>.bin: int64 n, n_cells; f64 coords[3 n]; i32 cells[4 nc];
 //     u8 own[n]; int32 n_nbr; per neighbour: int32 rank, int64 ns, i32 shared[ns],
 //     int64 ng, i32 ghosts[ng]; int64 n_dir; i32 dir[n_dir]; f64 dir_value;
-//     int64 nnz; i32 rows[n+1]; i32 cols[nnz]; f64 vals[nnz]; f64 rhs[n]
-//   <out_prefix><r>.bin: f64 x_csr[n], x_bsr[n] (every local DoF, ghosts synchronised)
+//     int64 nnz; i32 rows[n+1]; i32 cols[nnz]; f64 vals[nnz]; f64 rhs[n];
+//     f64 rhs3[3 n], lambda, mu (BSRFormat<3>: clamped nodes = dir, body-force right-hand side)
+//   <out_prefix><r>.bin: f64 x_csr[n], x_bsr[n], x_bsr3[3 n] (every local DoF, ghosts synchronised)
 //   case.bin: int32 dim, nv; int64 n_nodes, n_cells; f64 coords[3 n]; i32 cells[nv nc];
 //             int64 n_dir; i32 dir[n_dir]; f64 dir_value; int64 nnz; i32 rows[n+1];
 //             i32 cols[nnz]; f64 vals[nnz]; f64 rhs[n]; f64 coef
@@ -151,78 +152,141 @@ std::vector<double> run_add(IItemFamily* dofs, const Case& c)
   return solution(ls, c.n);
 }
 
+// the element's geometry, read through the views the module's lambda captures:
+// cofactors of the edge matrix det * grad(lambda_a) (grad(lambda_0) = -sum) and det
+struct TetGeom
+{
+  double g[4][3], det;
+};
+
+__device__ TetGeom tet_geom(const double* d_coords, const int32_t* d_cells, Int32 cell)
+{
+  double x[4][3];
+  for (int a = 0; a < 4; ++a)
+    for (int d = 0; d < 3; ++d)
+      x[a][d] = d_coords[3 * (int64_t)d_cells[4 * (int64_t)cell + a] + d];
+  double e[3][3];
+  for (int a = 0; a < 3; ++a)
+    for (int d = 0; d < 3; ++d)
+      e[a][d] = x[a + 1][d] - x[0][d];
+  TetGeom t;
+  for (int d = 0; d < 3; ++d) {
+    const int p = (d + 1) % 3, q = (d + 2) % 3;
+    t.g[1][d] = e[1][p] * e[2][q] - e[1][q] * e[2][p];
+    t.g[2][d] = e[2][p] * e[0][q] - e[2][q] * e[0][p];
+    t.g[3][d] = e[0][p] * e[1][q] - e[0][q] * e[1][p];
+    t.g[0][d] = -(t.g[1][d] + t.g[2][d] + t.g[3][d]);
+  }
+  t.det = e[0][0] * t.g[1][0] + e[0][1] * t.g[1][1] + e[0][2] * t.g[1][2];
+  return t;
+}
+
+// BSRFormat<NB_DOF> of the shim as the modules drive it: initialize /
+// computeSparsity / assembleBilinear(element lambda) / toLinearSystem (device
+// CSR view in the DoF numbering of FemDoFsOnNodes) / the module's BCs / solve
+template <int NB_DOF, class Element>
+std::vector<double> run_bsr_k(IMesh* mesh, IItemFamily* dofs, Element element, Int64 n_dofs,
+                              const std::function<void(DoFLinearSystem&)>& rhs_and_bc)
+{
+  ITraceMng tm;
+  RunQueue queue(eMemoryRessource::Device);
+  FemDoFsOnNodes dofs_on_nodes(NB_DOF);
+  Runner runner(eExecutionPolicy::HIP);
+  std::vector<double> x;
+  BSRFormat<NB_DOF> bsr(&tm, queue, dofs_on_nodes);
+  bsr.initialize(mesh, true);
+  bsr.computeSparsity();
+  bsr.assembleBilinear(element);
+  DoFLinearSystem ls(make_linear_system(dofs));
+  ls.setRunner(&runner);  // the CSR arrays of toLinearSystem live in device memory
+  bsr.toLinearSystem(ls);
+  rhs_and_bc(ls);
+  ls.solve();
+  return solution(ls, n_dofs);
+}
+
+struct DeviceGeometry
+{
+  double* coords = nullptr;
+  int32_t* cells = nullptr;
+  DeviceGeometry(const std::vector<double>& c, const std::vector<int32_t>& cl)
+  {
+    if (hipMalloc(&coords, sizeof(double) * c.size()) != hipSuccess ||
+        hipMalloc(&cells, sizeof(int32_t) * cl.size()) != hipSuccess)
+      throw FatalErrorException("hipMalloc");
+    (void)hipMemcpy(coords, c.data(), sizeof(double) * c.size(), hipMemcpyHostToDevice);
+    (void)hipMemcpy(cells, cl.data(), sizeof(int32_t) * cl.size(), hipMemcpyHostToDevice);
+  }
+  ~DeviceGeometry()
+  {
+    (void)hipFree(coords);
+    (void)hipFree(cells);
+  }
+};
+
 std::vector<double> run_bsr(IMesh* mesh, IItemFamily* dofs, const Case& c,
                             const std::function<void(DoFLinearSystem&)>& rhs_and_bc = {})
 {
   // the module's element lambda (modules/poisson/FemModule.cc:261-272 +
   // FemModule.h:177-186): vol * coef * grad_i . grad_j from the captured geometry
-  double* d_coords = nullptr;
-  int32_t* d_cells = nullptr;
-  if (hipMalloc(&d_coords, sizeof(double) * c.coords.size()) != hipSuccess ||
-      hipMalloc(&d_cells, sizeof(int32_t) * c.cells.size()) != hipSuccess)
-    throw FatalErrorException("hipMalloc");
-  (void)hipMemcpy(d_coords, c.coords.data(), sizeof(double) * c.coords.size(), hipMemcpyHostToDevice);
-  (void)hipMemcpy(d_cells, c.cells.data(), sizeof(int32_t) * c.cells.size(), hipMemcpyHostToDevice);
+  DeviceGeometry geo(c.coords, c.cells);
+  const double* d_coords = geo.coords;
+  const int32_t* d_cells = geo.cells;
   const double coef = c.coef;
   auto element = [=] __device__(CellLocalId cell) {
-    double x[4][3];
-    for (int a = 0; a < 4; ++a)
-      for (int d = 0; d < 3; ++d)
-        x[a][d] = d_coords[3 * (int64_t)d_cells[4 * (int64_t)cell.localId() + a] + d];
-    double e[3][3];
-    for (int a = 0; a < 3; ++a)
-      for (int d = 0; d < 3; ++d)
-        e[a][d] = x[a + 1][d] - x[0][d];
-    double g[4][3];
-    // cofactors of the edge matrix: det * grad(lambda_a), a = 1..3; grad(lambda_0) = -sum
-    for (int d = 0; d < 3; ++d) {
-      const int p = (d + 1) % 3, q = (d + 2) % 3;
-      g[1][d] = e[1][p] * e[2][q] - e[1][q] * e[2][p];
-      g[2][d] = e[2][p] * e[0][q] - e[2][q] * e[0][p];
-      g[3][d] = e[0][p] * e[1][q] - e[0][q] * e[1][p];
-      g[0][d] = -(g[1][d] + g[2][d] + g[3][d]);
-    }
-    const double det = e[0][0] * g[1][0] + e[0][1] * g[1][1] + e[0][2] * g[1][2];
-    const double s = coef / (6.0 * fabs(det));
+    const TetGeom t = tet_geom(d_coords, d_cells, cell.localId());
+    const double s = coef / (6.0 * fabs(t.det));
     afem::generic::FixedMatrix<4, 4> K;
     for (int a = 0; a < 4; ++a)
       for (int b = 0; b < 4; ++b)
-        K(a, b) = s * (g[a][0] * g[b][0] + g[a][1] * g[b][1] + g[a][2] * g[b][2]);
+        K(a, b) = s * (t.g[a][0] * t.g[b][0] + t.g[a][1] * t.g[b][1] + t.g[a][2] * t.g[b][2]);
     return K;
   };
-  ITraceMng tm;
-  RunQueue queue(eMemoryRessource::Device);
-  FemDoFsOnNodes dofs_on_nodes(1);
-  Runner runner(eExecutionPolicy::HIP);
-  std::vector<double> x;
-  {
-    BSRFormat<1> bsr(&tm, queue, dofs_on_nodes);
-    bsr.initialize(mesh, true);
-    bsr.computeSparsity();
-    bsr.assembleBilinear(element);
-    DoFLinearSystem ls(make_linear_system(dofs));
-    ls.setRunner(&runner);  // the CSR arrays of toLinearSystem live in device memory
-    bsr.toLinearSystem(ls);
-    if (rhs_and_bc)
+  auto bc = [&](DoFLinearSystem& ls) {
+    if (rhs_and_bc) {
       rhs_and_bc(ls);
-    else {
-      for (int64_t i = 0; i < c.n; ++i)
-        ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs[i];
-      penalty(ls, c);
+      return;
     }
-    ls.solve();
-    x = solution(ls, c.n);
-  }
-  (void)hipFree(d_coords);
-  (void)hipFree(d_cells);
-  return x;
+    for (int64_t i = 0; i < c.n; ++i)
+      ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs[i];
+    penalty(ls, c);
+  };
+  return run_bsr_k<1>(mesh, dofs, element, c.n, bc);
+}
+
+// BSRFormat<3>: the block-3 P1 elasticity element (the 3D form of
+// computeElementMatrixTRIA3Base, modules/elasticity/FemModule.h:112-140):
+// vol [lambda g_a,i g_b,j + mu (g_a,j g_b,i + delta_ij g_a.g_b)]
+std::vector<double> run_bsr3(IMesh* mesh, IItemFamily* dofs, const std::vector<double>& coords,
+                             const std::vector<int32_t>& cells, double lambda, double mu, Int64 n_nodes,
+                             const std::function<void(DoFLinearSystem&)>& rhs_and_bc)
+{
+  DeviceGeometry geo(coords, cells);
+  const double* d_coords = geo.coords;
+  const int32_t* d_cells = geo.cells;
+  auto element = [=] __device__(CellLocalId cell) {
+    const TetGeom t = tet_geom(d_coords, d_cells, cell.localId());
+    const double s = 1.0 / (6.0 * fabs(t.det));  // vol * (1/det)^2
+    afem::generic::FixedMatrix<12, 12> K;
+    for (int a = 0; a < 4; ++a)
+      for (int b = 0; b < 4; ++b) {
+        const double gg = t.g[a][0] * t.g[b][0] + t.g[a][1] * t.g[b][1] + t.g[a][2] * t.g[b][2];
+        for (int i = 0; i < 3; ++i)
+          for (int j = 0; j < 3; ++j)
+            K(3 * a + i, 3 * b + j) =
+            s * (lambda * t.g[a][i] * t.g[b][j] + mu * (t.g[a][j] * t.g[b][i] + (i == j ? gg : 0.0)));
+      }
+    return K;
+  };
+  return run_bsr_k<3>(mesh, dofs, element, 3 * n_nodes, rhs_and_bc);
 }
 struct RankCase
 {
   int64_t n = 0, nc = 0, nnz = 0;
-  std::vector<double> coords, vals, rhs;
+  std::vector<double> coords, vals, rhs, rhs3;
   std::vector<int32_t> cells, dir, rows, cols;
   std::vector<char> own;
+  double lambda = 0, mu = 0;
   std::vector<Int32> nbr;
   std::vector<std::vector<Int32>> shared, ghosts;
   double dir_value = 0;
@@ -265,6 +329,10 @@ bool load_rank(const std::string& path, RankCase& c)
     c.rhs.resize(c.n);
     ok = rd(f, c.rows.data(), c.n + 1) && rd(f, c.cols.data(), c.nnz) && rd(f, c.vals.data(), c.nnz) &&
          rd(f, c.rhs.data(), c.n);
+  }
+  if (ok) {
+    c.rhs3.resize(3 * c.n);
+    ok = rd(f, c.rhs3.data(), 3 * c.n) && rd(f, &c.lambda, 1) && rd(f, &c.mu, 1);
   }
   fclose(f);
   return ok;
@@ -324,6 +392,38 @@ void run_rank(MockWorld* world, Int32 rank, const RankCase& c, std::vector<doubl
       one.cells = c.cells;
       std::vector<double> xb = run_bsr(&mesh, &dofs, one, [&](DoFLinearSystem& ls) { bc(ls); });
       x.insert(x.end(), xb.begin(), xb.end());
+      // BSRFormat<3>: DoF lid = node lid * 3 + i (FemDoFsOnNodes), owners and
+      // synchronisation lists of the nodes' DoFs
+      IItemFamily dofs3((Int32)(3 * c.n), 0, &pm, &tm);
+      std::vector<char> own3(3 * c.n);
+      for (int64_t i = 0; i < 3 * c.n; ++i)
+        own3[i] = c.own[i / 3];
+      dofs3.setOwnMask(own3);
+      IVariableSynchronizer* sync3 = dofs3.allItemsSynchronizer();
+      sync3->ranks = c.nbr;
+      for (size_t q = 0; q < c.nbr.size(); ++q) {
+        std::vector<Int32> sh, gh;
+        for (Int32 lid : c.shared[q])
+          for (Int32 i = 0; i < 3; ++i)
+            sh.push_back(3 * lid + i);
+        for (Int32 lid : c.ghosts[q])
+          for (Int32 i = 0; i < 3; ++i)
+            gh.push_back(3 * lid + i);
+        sync3->shared.push_back(sh);
+        sync3->ghosts.push_back(gh);
+      }
+      auto bc3 = [&](DoFLinearSystem& ls) {
+        for (int64_t i = 0; i < 3 * c.n; ++i)
+          ls.rhsVariable()[DoFLocalId((Int32)i)] = c.rhs3[i];
+        for (int32_t d : c.dir)
+          for (Int32 i = 0; i < 3; ++i) {
+            ls.getForcedInfo()[DoFLocalId(3 * d + i)] = true;
+            ls.getForcedValue()[DoFLocalId(3 * d + i)] = 1.0e30;
+            ls.rhsVariable()[DoFLocalId(3 * d + i)] = 0.0;  // clamped: u = 0
+          }
+      };
+      std::vector<double> x3 = run_bsr3(&mesh, &dofs3, c.coords, c.cells, c.lambda, c.mu, c.n, bc3);
+      x.insert(x.end(), x3.begin(), x3.end());
     }
   }
   catch (const std::exception& e) {

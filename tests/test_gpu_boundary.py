@@ -391,6 +391,40 @@ def test_host_csr_view_is_read_at_solve(ctx):
     assert st["converged"] and np.abs(x - xo).max() / np.abs(xo).max() <= SOL_TOL
 
 
+@pytest.mark.parametrize("method", ["direct", "pcg"])
+def test_host_csr_view_apply_bcs_then_solve(ctx, method):
+    """ADVICE r3 (capi.cpp:1124): on a host CSR view, applyBoundaryConditions
+    and then solve() with row+column elimination.  The elimination is applied
+    once: it lands in the module's view (as Hypre edits the view's values,
+    HypreDoFLinearSystem.cc:319-382) and the solve's second pass is a no-op, so
+    b_j -= A_ji g is not subtracted twice."""
+    gm = read_gmsh(path("circle_cut.msh"))
+    n = gm.n_nodes
+    orp, ocols = O.sparsity(n, n, gm.cells)
+    ovals, orhs = O.assemble_poisson(n, gm.cells, gm.coords, orp, ocols, 5.5)
+    vals = ovals.copy()
+    ls = af.DoFLinearSystem().initialize(ctx, n)
+    ls.setCSRValues(orp[:-1].astype(np.int32), np.diff(orp).astype(np.int32), ocols, vals)
+    ls.set_rhs_host(orhs)
+    rc = gm.group_nodes("horizontal")
+    for d in rc:
+        ls.eliminateRowColumn(int(d), 0.5)
+    ls.applyBoundaryConditions()
+    info = np.zeros(n, np.uint8)
+    val = np.zeros(n)
+    info[rc], val[rc] = 2, 0.5
+    O.eliminate(info, val, orp, ocols, ovals, orhs)
+    _close(vals, ovals)  # the eliminated matrix is in the module's view
+    _close(ls.rhs_host(), orhs)
+    ls.setSolverOptions(method=method, rtol=1e-14, max_iter=20000)
+    st = ls.solve()
+    _close(ls.rhs_host(), orhs)  # not corrected a second time
+    x = ls.solution_host()
+    xo = np.linalg.solve(O.csr_to_dense(orp, ocols, ovals), orhs)
+    assert st["converged"] and np.abs(x - xo).max() / np.abs(xo).max() <= SOL_TOL
+    assert np.all(x[rc] == 0.5)
+
+
 def test_boundary_argument_checks(ctx):
     # ADVICE r1 (capi.cpp:544): a subdomain CSR has ghost columns, the linear
     # system must span them

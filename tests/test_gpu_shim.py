@@ -83,7 +83,13 @@ def test_shim_flows_match_oracle_and_golden(tmp_path):
         assert nerr == 0
 
 
-def _write_rank_case(fname, n, cells, coords, own, nbr, shared, ghosts, dirichlet, value, rows, cols, vals, rhs):
+E3, NU3 = 21.0e5, 0.28
+LAM3, MU3 = E3 * NU3 / ((1 + NU3) * (1 - 2 * NU3)), E3 / (2 * (1 + NU3))
+BODY3 = np.array([0.5, -0.25, -1.0])
+
+
+def _write_rank_case(fname, n, cells, coords, own, nbr, shared, ghosts, dirichlet, value, rows, cols, vals, rhs,
+                     rhs3):
     with open(fname, "wb") as fh:
         fh.write(np.array([n, cells.shape[0]], np.int64).tobytes())
         fh.write(np.ascontiguousarray(coords, np.float64).tobytes())
@@ -104,6 +110,18 @@ def _write_rank_case(fname, n, cells, coords, own, nbr, shared, ghosts, dirichle
         fh.write(np.ascontiguousarray(cols, np.int32).tobytes())
         fh.write(np.ascontiguousarray(vals, np.float64).tobytes())
         fh.write(np.ascontiguousarray(rhs, np.float64).tobytes())
+        fh.write(np.ascontiguousarray(rhs3, np.float64).tobytes())
+        fh.write(np.array([LAM3, MU3], np.float64).tobytes())
+
+
+def _dense_blocks(rp, cols, vals, k):
+    """Per-block k x k values -> the dense scalar matrix."""
+    n = rp.shape[0] - 1
+    A = np.zeros((k * n, k * n))
+    for r in range(n):
+        for t in range(rp[r], rp[r + 1]):
+            A[k * r:k * r + k, k * cols[t]:k * cols[t] + k] = vals[k * k * t:k * k * (t + 1)].reshape(k, k)
+    return A
 
 
 @pytest.mark.parametrize("world", [1, 2, 3])
@@ -117,9 +135,12 @@ def test_shim_subdomains_over_the_parallel_mng(tmp_path, world):
     FemDoFsOnNodes.cc:125-126) and the solution's synchronize() all run.  The
     partition is libafem's RCB with its subdomain plan (the lists Arcane's
     ghost layer would give).  The same again through the shim's BSRFormat<1>
-    (initialize / computeSparsity / assembleBilinear(element lambda) /
-    toLinearSystem) on each subdomain.  Owned values equal the single-domain
-    oracle solve to 1e-10, every ghost its owner's value bit for bit."""
+    and BSRFormat<3> (block-3 elasticity, body force, clamped nodes)
+    (initialize / computeSparsity / assembleBilinear(element lambda) on the
+    cell-unit kernel / toLinearSystem: a device CSR view in the subdomain's
+    DoF numbering, renumbered on the device by the linear system) on each
+    subdomain.  Owned values equal the single-domain oracle solve to 1e-10,
+    every ghost its owner's value bit for bit."""
     import arcanefem_amd as af
 
     assert os.path.exists(EXE), "tests/arcane_mock/shim_driver not built (__graft_entry__.build())"
@@ -153,11 +174,13 @@ def test_shim_subdomains_over_the_parallel_mng(tmp_path, world):
             rows_a.append(len(cols_a))
         own = inv < n_own
         rhs_a = np.where(own, rhs[np.minimum(inv, n_own - 1)], 0.0)
+        _, rhs3 = O.assemble_elasticity_tet(n_own, lcells, gm.coords[l2g], rp, cols, LAM3, 2 * MU3, 0.0, BODY3)
+        rhs3_a = np.where(own[:, None], rhs3.reshape(-1, 3)[np.minimum(inv, n_own - 1)], 0.0).ravel()
         dirichlet = np.flatnonzero(own & is_dir[l2g[inv]]).astype(np.int32)
         nbr = [int(x) for x in plan["neighbors"]]
         _write_rank_case(str(tmp_path / f"case{r}.bin"), n, pi[lcells].astype(np.int32), gm.coords[l2g[inv]], own,
                          nbr, {q: pi[plan["send"][q]] for q in nbr}, {q: pi[plan["recv"][q]] for q in nbr},
-                         dirichlet, value, np.array(rows_a), np.array(cols_a), np.array(vals_a), rhs_a)
+                         dirichlet, value, np.array(rows_a), np.array(cols_a), np.array(vals_a), rhs_a, rhs3_a)
         l2g_arc.append((l2g[inv], own))
     r = subprocess.run([EXE, "par", str(world), str(tmp_path / "case"), str(tmp_path / "out")], capture_output=True,
                        text=True, timeout=180,
@@ -171,17 +194,25 @@ def test_shim_subdomains_over_the_parallel_mng(tmp_path, world):
     vals, rhs = O.assemble_poisson(n, gm.cells, gm.coords, rp, cols, f)
     O.dirichlet_penalty(np.flatnonzero(is_dir).astype(np.int32), value, P, rp, cols, vals, rhs)
     xg = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
-    for flow in (0, 1):  # the setCSRValues flow, then the shim's BSRFormat<1> on the same subdomains
-        owner_val = np.full(n, np.nan)
+    # BSRFormat<3>: the block-3 elasticity system, clamped on the Dirichlet nodes by penalty
+    ev, erhs = O.assemble_elasticity_tet(n, gm.cells, gm.coords, rp, cols, LAM3, 2 * MU3, 0.0, BODY3)
+    A3 = _dense_blocks(rp, cols, ev, 3)
+    clamp = (3 * np.flatnonzero(is_dir)[:, None] + np.arange(3)).ravel()
+    A3[clamp, clamp] = 1.0e30
+    erhs[clamp] = 0.0
+    x3 = np.linalg.solve(A3, erhs).reshape(-1, 3)
+    # the setCSRValues flow, the shim's BSRFormat<1>, then its BSRFormat<3> on the same subdomains
+    for flow, k, xref in ((0, 1, xg[:, None]), (1, 1, xg[:, None]), (2, 3, x3)):
+        owner_val = np.full((n, k), np.nan)
         xs = []
         for q in range(world):
-            x2 = np.fromfile(str(tmp_path / f"out{q}.bin"), np.float64)
+            xq = np.fromfile(str(tmp_path / f"out{q}.bin"), np.float64)
             g, own = l2g_arc[q]
-            assert x2.size == 2 * g.size
-            x = x2[flow * g.size:(flow + 1) * g.size]
+            assert xq.size == 5 * g.size
+            x = xq[flow * g.size:flow * g.size + k * g.size].reshape(-1, k)
             owner_val[g[own]] = x[own]
             xs.append((x, g, own))
         assert not np.isnan(owner_val).any()
-        assert np.abs(owner_val - xg).max() <= 1e-10 * np.abs(xg).max(), flow
+        assert np.abs(owner_val - xref).max() <= 1e-10 * np.abs(xref).max(), flow
         for x, g, own in xs:
             assert np.array_equal(x[~own], owner_val[g[~own]])  # synchronize(): ghosts hold their owners' values
