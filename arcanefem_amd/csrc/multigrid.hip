@@ -318,9 +318,14 @@ struct SlabMap {
   int np1;    // nodes per row (nx + 1)
   int64_t L;  // nodes per layer
   int k0, nown, glo;
+  int ghi;    // a ghost layer above (distributed coarse levels; level 0 does not use it)
   __host__ __device__ int gz(int li) const { return li < nown ? k0 + li : (li == nown && glo ? k0 - 1 : k0 + nown); }
   __host__ __device__ bool owned_z(int z) const { return z >= k0 && z < k0 + nown; }
+  __host__ __device__ bool local_z(int z) const { return owned_z(z) || (glo && z == k0 - 1) || (ghi && z == k0 + nown); }
+  __host__ __device__ int local_layer(int z) const { return owned_z(z) ? z - k0 : (z == k0 - 1 ? nown : nown + glo); }
   __host__ __device__ int64_t local_owned(int x, int y, int z) const { return (int64_t)(z - k0) * L + x + (int64_t)np1 * y; }
+  __host__ __device__ int64_t local_of(int x, int y, int z) const { return (int64_t)local_layer(z) * L + x + (int64_t)np1 * y; }
+  __host__ __device__ int64_t n_local() const { return (int64_t)(nown + glo + ghi) * L; }
 };
 
 // the part of A_c = P^T A P over the slab's OWNED fine rows (global coarse
@@ -419,6 +424,174 @@ __global__ void k_mg_prolong_own(Dims cd, SlabMap sm, int64_t nn_own, const doub
   }
 }
 
+// ---- distributed coarse levels: every level above the gather level is cut into
+// z-slabs like the fine one (owned coarse layer Z = the owner of fine layer 2Z),
+// local numbering as level 0 (owned layers, ghost layer below, ghost layer above),
+// one halo per level.  The Galerkin product of an owned coarse row needs the fine
+// rows of the layers 2Z - 1 .. 2Z + 1, so the fine boundary layers' rows travel
+// to the neighbours once at setup, as "fat" rows: 15 entries of (global column
+// id, K^2 values), column -1 past the row's end.  Fat slots: the first and the
+// last owned layer (sent), the ghost layer below and the one above (received).
+constexpr int kFatRow = 15;
+
+__host__ __device__ inline int fat_slot(const SlabMap& sm, int li)
+{
+  if (li == 0) return 0;
+  if (li == sm.nown - 1) return 1;
+  return li == sm.nown && sm.glo ? 2 : 3;
+}
+
+template <int K>
+__global__ void k_mg_fat_rows(Dims gd, SlabMap sm, const int64_t* __restrict__ bp, const int32_t* __restrict__ bc,
+                              const double* __restrict__ v, double* __restrict__ fat, int* __restrict__ err)
+{
+  constexpr int E = 1 + K * K;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * sm.L) return;
+  const int li = t < sm.L ? 0 : sm.nown - 1;
+  if (t >= sm.L && sm.nown == 1) return;  // one owned layer: slot 0 only
+  const int64_t r = (int64_t)li * sm.L + t % sm.L;
+  const int64_t b0 = bp[r];
+  const int len = (int)(bp[r + 1] - b0);
+  if (len > kFatRow) *err = 1;
+  double* out = fat + ((int64_t)fat_slot(sm, li) * sm.L + t % sm.L) * kFatRow * E;
+  for (int s = 0; s < kFatRow; ++s) {
+    if (s < len) {
+      const int64_t col = bc[b0 + s];
+      const int lc = (int)(col / sm.L);
+      const int64_t pos = col - (int64_t)lc * sm.L;
+      out[s * E] = (double)gd.id((int)(pos % sm.np1), (int)(pos / sm.np1), sm.gz(lc));
+      for (int u = 0; u < K; ++u)
+        for (int w = 0; w < K; ++w) out[s * E + 1 + K * u + w] = v[K * K * b0 + K * u * len + K * s + w];
+    }
+    else {
+      out[s * E] = -1.0;
+    }
+  }
+}
+
+// A_c = P^T A P for the OWNED rows of a distributed coarse level (local
+// numbering, loop order of k_mg_galerkin); fine rows of ghost layers from `fat`
+template <int K>
+__global__ void k_mg_galerkin_dist(Dims fgd, Dims cgd, SlabMap fsm, SlabMap csm, const int64_t* __restrict__ fbp,
+                                   const int32_t* __restrict__ fbc, const double* __restrict__ fv,
+                                   const double* __restrict__ fat, const int64_t* __restrict__ cbp,
+                                   const int32_t* __restrict__ cbc, double* __restrict__ cv, int* __restrict__ err)
+{
+  constexpr int E = 1 + K * K;
+  const int64_t I = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (I >= (int64_t)csm.nown * csm.L) return;
+  const int li = (int)(I / csm.L);
+  const int64_t pos = I - (int64_t)li * csm.L;
+  const int cx = (int)(pos % csm.np1), cy = (int)(pos / csm.np1), cz = csm.k0 + li;
+  const int64_t c0 = cbp[I];
+  const int clen = (int)(cbp[I + 1] - c0);
+  for (int o = 0; o < 15; ++o) {
+    const int fx = 2 * cx + c_st[o][0], fy = 2 * cy + c_st[o][1], fz = 2 * cz + c_st[o][2];
+    if (!fgd.in(fx, fy, fz)) continue;
+    if (!fsm.local_z(fz)) {
+      *err = 1;
+      continue;
+    }
+    const double wi = o == 0 ? 1.0 : 0.5;
+    const bool own = fsm.owned_z(fz);
+    const int64_t fi = fsm.local_of(fx, fy, fz);
+    int64_t f0 = 0;
+    int flen = 0;
+    const double* fr = nullptr;
+    if (own) {
+      f0 = fbp[fi];
+      flen = (int)(fbp[fi + 1] - f0);
+    }
+    else {
+      fr = fat + ((int64_t)fat_slot(fsm, fsm.local_layer(fz)) * fsm.L + fx + (int64_t)fsm.np1 * fy) * kFatRow * E;
+      while (flen < kFatRow && fr[flen * E] >= 0.0) ++flen;
+    }
+    for (int s = 0; s < flen; ++s) {
+      int jx, jy, jz;
+      if (own) {
+        const int64_t col = fbc[f0 + s];
+        const int lc = (int)(col / fsm.L);
+        const int64_t p = col - (int64_t)lc * fsm.L;
+        jx = (int)(p % fsm.np1);
+        jy = (int)(p / fsm.np1);
+        jz = fsm.gz(lc);
+      }
+      else {
+        decompose(fgd, (int64_t)fr[s * E], jx, jy, jz);
+      }
+      const int a = jx & 1, b = jy & 1, c = jz & 1;
+      const int px = jx >> 1, py = jy >> 1, pz = jz >> 1;
+      const int np = (a | b | c) ? 2 : 1;
+      const double w = wi * (np == 2 ? 0.5 : 1.0);
+      for (int p = 0; p < np; ++p) {
+        const int qz = pz + p * c;
+        if (!csm.local_z(qz)) {
+          *err = 1;
+          continue;
+        }
+        const int32_t J = (int32_t)csm.local_of(px + p * a, py + p * b, qz);
+        int t = -1;
+        for (int q = 0; q < clen; ++q)
+          if (cbc[c0 + q] == J) {
+            t = q;
+            break;
+          }
+        if (t < 0) {
+          *err = 1;
+          continue;
+        }
+        for (int u = 0; u < K; ++u)
+          for (int v = 0; v < K; ++v)
+            cv[K * K * c0 + K * u * clen + K * t + v] +=
+            w * (own ? fv[K * K * f0 + K * u * flen + K * s + v] : fr[s * E + 1 + K * u + v]);
+      }
+    }
+  }
+}
+
+// r_c = P^T r_f on the owned coarse nodes (r_f with its ghost layers exchanged)
+template <int K>
+__global__ void k_mg_restrict_dist(Dims fgd, SlabMap fsm, SlabMap csm, const double* __restrict__ rf,
+                                   double* __restrict__ rc)
+{
+  const int64_t I = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (I >= (int64_t)csm.nown * csm.L) return;
+  const int li = (int)(I / csm.L);
+  const int64_t pos = I - (int64_t)li * csm.L;
+  const int cx = (int)(pos % csm.np1), cy = (int)(pos / csm.np1), cz = csm.k0 + li;
+  double acc[K];
+  for (int u = 0; u < K; ++u) acc[u] = 0.0;
+  for (int o = 0; o < 15; ++o) {
+    const int fx = 2 * cx + c_st[o][0], fy = 2 * cy + c_st[o][1], fz = 2 * cz + c_st[o][2];
+    if (!fgd.in(fx, fy, fz)) continue;
+    const double w = o == 0 ? 1.0 : 0.5;
+    const int64_t fi = fsm.local_of(fx, fy, fz);
+    for (int u = 0; u < K; ++u) acc[u] += w * rf[K * fi + u];
+  }
+  for (int u = 0; u < K; ++u) rc[K * I + u] = acc[u];
+}
+
+// x_f += P x_c on the owned fine nodes (x_c with its ghost layers exchanged)
+template <int K>
+__global__ void k_mg_prolong_dist(SlabMap fsm, SlabMap csm, const double* __restrict__ xc, double* __restrict__ xf)
+{
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= (int64_t)fsm.nown * fsm.L) return;
+  const int li = (int)(f / fsm.L);
+  const int64_t pos = f - (int64_t)li * fsm.L;
+  const int x = (int)(pos % fsm.np1), y = (int)(pos / fsm.np1), z = fsm.k0 + li;
+  const int a = x & 1, b = y & 1, c = z & 1;
+  const int64_t P0 = csm.local_of(x >> 1, y >> 1, z >> 1);
+  if (a | b | c) {
+    const int64_t P1 = csm.local_of((x >> 1) + a, (y >> 1) + b, (z >> 1) + c);
+    for (int u = 0; u < K; ++u) xf[K * f + u] += 0.5 * (xc[K * P0 + u] + xc[K * P1 + u]);
+  }
+  else {
+    for (int u = 0; u < K; ++u) xf[K * f + u] += xc[K * P0 + u];
+  }
+}
+
 // the power iteration's start vector by GLOBAL index (the one-rank sequence of k_mg_fill)
 __global__ void k_mg_fill_off(int64_t n, int64_t off, double* __restrict__ v)
 {
@@ -445,6 +618,15 @@ struct MgLevel {
   DevBuf<double> own_v, own_dinv;
   DevBuf<double> x, t, b, r;  // iterate (ping-pong x / t), right-hand side, residual
   double omega = 0.0;
+  // a distributed level (global V-cycle over z-slabs): the slab's owned rows in
+  // local numbering (sm), the global box gd, the halo of its vectors (level 0:
+  // the system's own), vectors x / t / r with the ghost entries (ncol)
+  bool dist = false;
+  SlabMap sm{};
+  Dims gd{};
+  std::unique_ptr<Halo> halo;
+  int64_t ncol = 0;
+  std::vector<int> lo, hi;  // every rank's owned layers [lo, hi) at this level
 };
 
 struct Multigrid {
@@ -455,6 +637,7 @@ struct Multigrid {
   bool global = false;
   SlabMap sm{};
   Dims gfine{};
+  int n_dist = 0;  // levels [0, n_dist) are distributed, the rest replicated
   std::vector<MgLevel> lv;
   DevBuf<double> ainv;  // dense inverse of the coarsest level (n_dense x n_dense) or empty
   int n_dense = 0;
@@ -646,19 +829,22 @@ double allreduce_scalar(LinearSystem& ls, double v)
 // lambda_max(D^-1 A) of the distributed fine level: the one-rank power
 // iteration with the halo exchanged before every product and the norms summed
 // over the ranks (start vector by global index)
+Halo& level_halo(LinearSystem& ls, MgLevel& L) { return L.halo ? *L.halo : *ls.halo; }
+
 double power_lambda_global(LinearSystem& ls, Multigrid& mg, MgLevel& L)
 {
   Ctx& ctx = *ls.ctx;
   const int k = mg.k;
+  Halo& H = level_halo(ls, L);
   const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
-  hipLaunchKernelGGL(k_mg_fill_off, dim3(g), dim3(256), 0, ctx.stream, L.n, (int64_t)k * mg.sm.k0 * mg.sm.L, L.x.p);
+  hipLaunchKernelGGL(k_mg_fill_off, dim3(g), dim3(256), 0, ctx.stream, L.n, (int64_t)k * L.sm.k0 * L.sm.L, L.x.p);
   AFEM_LAUNCHED();
   hipLaunchKernelGGL(k_mg_norm2, dim3(g), dim3(256), 0, ctx.stream, L.n, L.x.p, mg.partial.p);
   AFEM_LAUNCHED();
   double nv = std::sqrt(allreduce_scalar(ls, host_sum(ctx, mg.partial, (int)g)));
   double lam = 0.0;
   for (int it = 0; it < kPowerIts; ++it) {
-    halo_exchange(*ls.halo, ctx, L.x.p);
+    halo_exchange(H, ctx, L.x.p);
     spmv_blk_epi(ctx, k, 0, L.nn, L.bp, L.bc, L.v, L.x.p, L.t.p, nullptr, nullptr, 0.0);
     hipLaunchKernelGGL(k_mg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, L.dinv, L.t.p, mg.partial.p);
     AFEM_LAUNCHED();
@@ -671,6 +857,198 @@ double power_lambda_global(LinearSystem& ls, Multigrid& mg, MgLevel& L)
     nv = 1.0;
   }
   return lam;
+}
+
+// the halo of a distributed level's vectors: its owned boundary layers to the
+// z-neighbours, their layers into its ghost layers (node ids x `width`, slots
+// of `slot`: the vector's layer of a local layer; identity for plain vectors)
+template <class Slot>
+std::unique_ptr<Halo> slab_halo(LinearSystem& ls, const SlabMap& sm, int width, Slot slot)
+{
+  Ctx& ctx = *ls.ctx;
+  Comm* comm = ls.halo->comm;
+  const int rank = comm_rank(comm);
+  std::vector<int32_t> nbr, si, ri;
+  std::vector<int64_t> sc, rc;
+  auto layer = [&](int li, std::vector<int32_t>& out) {
+    for (int64_t i = 0; i < sm.L; ++i) out.push_back((int32_t)(slot(li) * sm.L + i));
+  };
+  if (sm.glo) {
+    nbr.push_back(rank - 1);
+    sc.push_back(sm.L);
+    rc.push_back(sm.L);
+    layer(0, si);
+    layer(sm.nown, ri);
+  }
+  if (sm.ghi) {
+    nbr.push_back(rank + 1);
+    sc.push_back(sm.L);
+    rc.push_back(sm.L);
+    layer(sm.nown - 1, si);
+    layer(sm.nown + sm.glo, ri);
+  }
+  expand_dof_lists(width, sc, rc, si, ri);
+  std::unique_ptr<Halo> h(new Halo());
+  halo_setup(*h, ctx, comm, (int)nbr.size(), nbr.data(), sc.data(), si.data(), rc.data(), ri.data());
+  return h;
+}
+
+// every rank's owned layers of a distributed level (summed over the ranks)
+void gather_ranges(LinearSystem& ls, MgLevel& L)
+{
+  Ctx& ctx = *ls.ctx;
+  Comm* comm = ls.halo->comm;
+  const int nr = comm_nranks(comm), rank = comm_rank(comm);
+  std::vector<double> h(2 * nr, 0.0);
+  h[2 * rank] = L.sm.k0;
+  h[2 * rank + 1] = L.sm.k0 + L.sm.nown;
+  DevBuf<double> d;
+  d.alloc(h.size());
+  AFEM_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, ctx.stream));
+  comm_allreduce(comm, ctx, d.p, (int64_t)h.size());
+  AFEM_HIP(hipMemcpyAsync(h.data(), d.p, h.size() * 8, hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  L.lo.resize(nr);
+  L.hi.resize(nr);
+  for (int r = 0; r < nr; ++r) {
+    L.lo[r] = (int)h[2 * r];
+    L.hi[r] = (int)h[2 * r + 1];
+  }
+}
+
+// the error flag of a setup step, the same on every rank (a rank
+// that failed alone would leave the others waiting in a collective)
+bool any_rank(LinearSystem& ls, const DevBuf<int>& err)
+{
+  int h = 0;
+  AFEM_HIP(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, ls.ctx->stream));
+  ls.ctx->sync();
+  return allreduce_scalar(ls, h ? 1.0 : 0.0) > 0.0;
+}
+
+// a distributed coarse level from the distributed level F: owned coarse layer Z
+// = the rank owning fine layer 2Z; Galerkin rows on the owned coarse nodes
+MgLevel dist_coarse(LinearSystem& ls, Multigrid& mg, MgLevel& F, const Dims& cgd, const std::vector<int>& clo,
+                    const std::vector<int>& chi)
+{
+  Ctx& ctx = *ls.ctx;
+  const int k = mg.k;
+  const int rank = comm_rank(ls.halo->comm);
+  MgLevel C;
+  C.dist = true;
+  C.gd = cgd;
+  C.lo = clo;
+  C.hi = chi;
+  C.sm = SlabMap{ cgd.nx + 1, (int64_t)(cgd.nx + 1) * (cgd.ny + 1), clo[rank], chi[rank] - clo[rank],
+                  clo[rank] > 0 ? 1 : 0, chi[rank] <= cgd.nz ? 1 : 0 };
+  C.d = Dims{ cgd.nx, cgd.ny, C.sm.nown - 1 };
+  C.nn = (int64_t)C.sm.nown * C.sm.L;
+  C.n = k * C.nn;
+  C.ncol = k * C.sm.n_local();
+  // owned rows: the coarse 15-block Kuhn stencil, local column ids, sorted
+  std::vector<int64_t> hbp(C.nn + 1, 0);
+  std::vector<int32_t> hbc;
+  hbc.reserve(C.nn * 15);
+  std::vector<int32_t> row;
+  for (int64_t I = 0; I < C.nn; ++I) {
+    const int li = (int)(I / C.sm.L);
+    const int64_t pos = I - (int64_t)li * C.sm.L;
+    const int x = (int)(pos % C.sm.np1), y = (int)(pos / C.sm.np1), z = C.sm.k0 + li;
+    row.clear();
+    for (int o = 0; o < 15; ++o) {
+      const int X = x + h_st[o][0], Y = y + h_st[o][1], Z = z + h_st[o][2];
+      if (cgd.in(X, Y, Z)) row.push_back((int32_t)C.sm.local_of(X, Y, Z));
+    }
+    std::sort(row.begin(), row.end());
+    hbc.insert(hbc.end(), row.begin(), row.end());
+    hbp[I + 1] = (int64_t)hbc.size();
+  }
+  C.own_bp.alloc(hbp.size());
+  C.own_bc.alloc(hbc.size());
+  AFEM_HIP(hipMemcpyAsync(C.own_bp.p, hbp.data(), hbp.size() * 8, hipMemcpyHostToDevice, ctx.stream));
+  AFEM_HIP(hipMemcpyAsync(C.own_bc.p, hbc.data(), hbc.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+  C.own_v.alloc(hbc.size() * k * k);
+  AFEM_HIP(hipMemsetAsync(C.own_v.p, 0, C.own_v.bytes(), ctx.stream));
+  C.own_dinv.alloc(C.n);
+  // the fine boundary layers' rows to the neighbours (fat rows)
+  const int W = kFatRow * (1 + k * k);
+  DevBuf<double> fat;
+  fat.alloc((size_t)4 * F.sm.L * W);
+  DevBuf<int> err;
+  err.alloc(1);
+  AFEM_HIP(hipMemsetAsync(err.p, 0, sizeof(int), ctx.stream));
+  dispatch_k(k, [&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    hipLaunchKernelGGL(k_mg_fat_rows<K>, dim3(grid_for(2 * F.sm.L, 128)), dim3(128), 0, ctx.stream, F.gd, F.sm, F.bp,
+                       F.bc, F.v, fat.p, err.p);
+    AFEM_LAUNCHED();
+  });
+  const SlabMap fsm = F.sm;
+  auto fat_halo = slab_halo(ls, fsm, W, [&](int li) { return fat_slot(fsm, li); });
+  halo_exchange(*fat_halo, ctx, fat.p);
+  dispatch_k(k, [&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    const unsigned g = (unsigned)grid_for(C.nn, 128);
+    hipLaunchKernelGGL(k_mg_galerkin_dist<K>, dim3(g), dim3(128), 0, ctx.stream, F.gd, cgd, F.sm, C.sm, F.bp, F.bc,
+                       F.v, fat.p, C.own_bp.p, C.own_bc.p, C.own_v.p, err.p);
+    AFEM_LAUNCHED();
+    hipLaunchKernelGGL(k_mg_dinv<K>, dim3(g), dim3(128), 0, ctx.stream, C.nn, C.own_bp.p, C.own_bc.p, C.own_v.p,
+                       C.own_dinv.p);
+    AFEM_LAUNCHED();
+  });
+  AFEM_REQUIRE(!any_rank(ls, err), AFEM_ERR_STATE, "multigrid: distributed Galerkin product outside the coarse stencil");
+  C.bp = C.own_bp.p;
+  C.bc = C.own_bc.p;
+  C.v = C.own_v.p;
+  C.dinv = C.own_dinv.p;
+  C.halo = slab_halo(ls, C.sm, k, [](int li) { return li; });
+  return C;
+}
+
+// the first replicated level (the global coarse box) from the distributed level
+// F: A_c = sum over the ranks of their owned rows' P^T A P parts
+MgLevel gathered_coarse(LinearSystem& ls, Multigrid& mg, MgLevel& F)
+{
+  Ctx& ctx = *ls.ctx;
+  const int k = mg.k;
+  MgLevel C;
+  C.d = Dims{ F.gd.nx / 2, F.gd.ny / 2, F.gd.nz / 2 };
+  C.nn = C.d.nodes();
+  C.n = k * C.nn;
+  std::vector<int64_t> hbp;
+  std::vector<int32_t> hbc;
+  coarse_structure(C.d, hbp, hbc);
+  C.own_bp.alloc(hbp.size());
+  C.own_bc.alloc(hbc.size());
+  AFEM_HIP(hipMemcpyAsync(C.own_bp.p, hbp.data(), hbp.size() * 8, hipMemcpyHostToDevice, ctx.stream));
+  AFEM_HIP(hipMemcpyAsync(C.own_bc.p, hbc.data(), hbc.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+  C.own_v.alloc(hbc.size() * k * k);
+  AFEM_HIP(hipMemsetAsync(C.own_v.p, 0, C.own_v.bytes(), ctx.stream));
+  C.own_dinv.alloc(C.n);
+  DevBuf<int> err;
+  err.alloc(1);
+  AFEM_HIP(hipMemsetAsync(err.p, 0, sizeof(int), ctx.stream));
+  const unsigned g = (unsigned)grid_for(C.nn, 128);
+  dispatch_k(k, [&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    hipLaunchKernelGGL(k_mg_galerkin_part<K>, dim3(g), dim3(128), 0, ctx.stream, F.gd, C.d, F.sm, F.bp, F.bc, F.v,
+                       C.own_bp.p, C.own_bc.p, C.own_v.p, err.p);
+    AFEM_LAUNCHED();
+  });
+  AFEM_REQUIRE(!any_rank(ls, err), AFEM_ERR_STATE, "multigrid: Galerkin product outside the coarse Kuhn stencil");
+  comm_allreduce(ls.halo->comm, ctx, C.own_v.p, (int64_t)C.own_v.n);
+  dispatch_k(k, [&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    hipLaunchKernelGGL(k_mg_dinv<K>, dim3(g), dim3(128), 0, ctx.stream, C.nn, C.own_bp.p, C.own_bc.p, C.own_v.p,
+                       C.own_dinv.p);
+    AFEM_LAUNCHED();
+  });
+  C.bp = C.own_bp.p;
+  C.bc = C.own_bc.p;
+  C.v = C.own_v.p;
+  C.dinv = C.own_dinv.p;
+  ctx.sync();
+  return C;
 }
 
 }  // namespace
@@ -704,45 +1082,47 @@ void mg_setup(LinearSystem& ls)
       L.bc = bc;
       L.v = ls.csr_vals;
       L.dinv = ls.dinv.p;
-      mg->sm = SlabMap{ ls.mg_nx + 1, (int64_t)(ls.mg_nx + 1) * (ls.mg_nx + 1), ls.mg_k0, ls.mg_nz + 1, ls.mg_glo ? 1 : 0 };
+      mg->sm = SlabMap{ ls.mg_nx + 1, (int64_t)(ls.mg_nx + 1) * (ls.mg_nx + 1), ls.mg_k0, ls.mg_nz + 1,
+                        ls.mg_glo ? 1 : 0, ls.mg_k0 + ls.mg_nz + 1 <= ls.mg_nzg ? 1 : 0 };
       mg->gfine = Dims{ ls.mg_nx, ls.mg_nx, ls.mg_nzg };
+      L.dist = true;
+      L.sm = mg->sm;
+      L.gd = mg->gfine;
+      L.ncol = ls.n_cols;
+      gather_ranges(ls, L);
       mg->lv.push_back(std::move(L));
-      // level 1: the global coarse box, A_1 = sum over the ranks of their owned rows' P^T A P parts
-      MgLevel C;
-      C.d = Dims{ ls.mg_nx / 2, ls.mg_nx / 2, ls.mg_nzg / 2 };
-      C.nn = C.d.nodes();
-      C.n = k * C.nn;
-      std::vector<int64_t> hbp;
-      std::vector<int32_t> hbc;
-      coarse_structure(C.d, hbp, hbc);
-      C.own_bp.alloc(hbp.size());
-      C.own_bc.alloc(hbc.size());
-      AFEM_HIP(hipMemcpyAsync(C.own_bp.p, hbp.data(), hbp.size() * 8, hipMemcpyHostToDevice, ctx.stream));
-      AFEM_HIP(hipMemcpyAsync(C.own_bc.p, hbc.data(), hbc.size() * 4, hipMemcpyHostToDevice, ctx.stream));
-      C.own_v.alloc(hbc.size() * k * k);
-      AFEM_HIP(hipMemsetAsync(C.own_v.p, 0, C.own_v.bytes(), ctx.stream));
-      C.own_dinv.alloc(C.n);
-      const MgLevel& F = mg->lv.back();
-      const unsigned g = (unsigned)grid_for(C.nn, 128);
-      dispatch_k(k, [&](auto kc) {
-        constexpr int K = decltype(kc)::value;
-        hipLaunchKernelGGL(k_mg_galerkin_part<K>, dim3(g), dim3(128), 0, ctx.stream, mg->gfine, C.d, mg->sm, F.bp, F.bc,
-                           F.v, C.own_bp.p, C.own_bc.p, C.own_v.p, err.p);
-        AFEM_LAUNCHED();
-      });
-      comm_allreduce(ls.halo->comm, ctx, C.own_v.p, (int64_t)C.own_v.n);
-      dispatch_k(k, [&](auto kc) {
-        constexpr int K = decltype(kc)::value;
-        hipLaunchKernelGGL(k_mg_dinv<K>, dim3(g), dim3(128), 0, ctx.stream, C.nn, C.own_bp.p, C.own_bc.p, C.own_v.p,
-                           C.own_dinv.p);
-        AFEM_LAUNCHED();
-      });
-      C.bp = C.own_bp.p;
-      C.bc = C.own_bc.p;
-      C.v = C.own_v.p;
-      C.dinv = C.own_dinv.p;
-      ctx.sync();
-      mg->lv.push_back(std::move(C));
+      mg->n_dist = 1;
+      // distributed coarse levels while every rank keeps a layer and the level is
+      // above 1/AFEM_MG_GATHER of the fine grid (default 512), then the global
+      // coarse box, replicated (the one-rank hierarchy's levels either way)
+      const char* ge = variant("AFEM_MG_GATHER");
+      const double ratio = ge && *ge ? std::atof(ge) : 512.0;
+      while (true) {
+        MgLevel& F = mg->lv.back();
+        const bool coarsen = (int64_t)k * F.gd.nodes() > kDenseMax && F.gd.nx % 2 == 0 && F.gd.ny % 2 == 0 &&
+                             F.gd.nz % 2 == 0 && F.gd.nx >= 2 && F.gd.nz >= 2;
+        if (!coarsen) break;  // F is the coarsest level: smoothing only
+        const Dims cgd{ F.gd.nx / 2, F.gd.ny / 2, F.gd.nz / 2 };
+        std::vector<int> clo(F.lo.size()), chi(F.lo.size());
+        bool every = true;
+        for (size_t r = 0; r < F.lo.size(); ++r) {
+          clo[r] = (F.lo[r] + 1) / 2;
+          chi[r] = (F.hi[r] + 1) / 2;
+          every = every && chi[r] > clo[r];
+        }
+        const bool dist = every && (int64_t)k * cgd.nodes() > kDenseMax &&
+                          (double)cgd.nodes() * ratio >= (double)mg->gfine.nodes();
+        if (dist) {
+          MgLevel C = dist_coarse(ls, *mg, F, cgd, clo, chi);
+          mg->lv.push_back(std::move(C));
+          ++mg->n_dist;
+        }
+        else {
+          MgLevel C = gathered_coarse(ls, *mg, F);
+          mg->lv.push_back(std::move(C));
+          break;
+        }
+      }
     }
     else if (!ls.mg_multi) {
       L.d = Dims{ ls.mg_nx, ls.mg_nx, ls.mg_nz };
@@ -790,7 +1170,7 @@ void mg_setup(LinearSystem& ls)
     }
     if (!mg->global) mg->lv.push_back(std::move(L));
   }
-  while (true) {
+  while (!mg->lv.back().dist) {
     const MgLevel& F = mg->lv.back();
     if (F.n <= kDenseMax || F.d.nx % 2 || F.d.ny % 2 || F.d.nz % 2 || F.d.nx < 2 || F.d.nz < 2) break;
     MgLevel C;
@@ -824,26 +1204,30 @@ void mg_setup(LinearSystem& ls)
     ctx.sync();  // the host structure vectors go out of scope
     mg->lv.push_back(std::move(C));
   }
-  int herr = 0;
-  AFEM_HIP(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, ctx.stream));
-  ctx.sync();
+  const bool herr = mg->global ? any_rank(ls, err) : [&] {
+    int h = 0;
+    AFEM_HIP(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    return h != 0;
+  }();
   AFEM_REQUIRE(!herr, AFEM_ERR_STATE, "multigrid: Galerkin product outside the coarse Kuhn stencil");
   for (size_t l = 0; l < mg->lv.size(); ++l) {
     MgLevel& L = mg->lv[l];
-    const bool dist = mg->global && l == 0;  // vectors with the halo's ghost entries
-    L.x.alloc(dist ? ls.n_cols : L.n);
-    L.t.alloc(dist ? ls.n_cols : L.n);
+    const bool dist = L.dist;  // vectors with the halo's ghost entries
+    L.x.alloc(dist ? L.ncol : L.n);
+    L.t.alloc(dist ? L.ncol : L.n);
+    L.r.alloc(dist ? L.ncol : L.n);
     if (dist) {
       AFEM_HIP(hipMemsetAsync(L.x.p, 0, L.x.bytes(), ctx.stream));
       AFEM_HIP(hipMemsetAsync(L.t.p, 0, L.t.bytes(), ctx.stream));
+      AFEM_HIP(hipMemsetAsync(L.r.p, 0, L.r.bytes(), ctx.stream));
     }
     L.b.alloc(L.n);
-    L.r.alloc(L.n);
     const double lam = dist ? power_lambda_global(ls, *mg, L) : power_lambda(ctx, *mg, L);
     L.omega = lam > 0 ? 4.0 / (3.0 * 1.05 * lam) : 0.6;
   }
   MgLevel& Lc = mg->lv.back();
-  if (mg->lv.size() > 1 && Lc.n <= kDenseMax) dense_inverse(ctx, *mg, Lc);
+  if (mg->lv.size() > 1 && !Lc.dist && Lc.n <= kDenseMax) dense_inverse(ctx, *mg, Lc);
   mg->key_rows = krows;
   mg->key_vals = ls.csr_vals;
   mg->key_n = ls.n_rows;
@@ -901,37 +1285,62 @@ void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
   smooth(ctx, mg, L, b, mg.sweeps, false);
 }
 
-// level 0 of the global V-cycle (the steps of vcycle on the slab's owned
-// rows): the halo before every product, the restriction summed over the ranks,
-// levels >= 1 replicated (the same arithmetic on every rank)
-void vcycle_global(LinearSystem& ls, Multigrid& mg, const double* b)
+// a distributed level of the global V-cycle (the steps of vcycle on the slab's
+// owned rows): the level's halo before every product; the restriction to a
+// distributed coarse level reads the fine residual's ghost layers, the one to
+// the gathered level is summed over the ranks; replicated levels run the same
+// arithmetic on every rank
+void vcycle_dist(LinearSystem& ls, Multigrid& mg, size_t l, const double* b)
 {
   Ctx& ctx = *ls.ctx;
-  MgLevel& L = mg.lv[0];
-  MgLevel& C = mg.lv[1];
+  MgLevel& L = mg.lv[l];
+  Halo& H = level_halo(ls, L);
+  const bool last = l + 1 == mg.lv.size();
+  const int pre = last ? (l == 0 ? 2 * mg.sweeps : kCoarseSweeps) : mg.sweeps;
   smooth(ctx, mg, L, b, 1, true);
-  for (int s = 1; s < mg.sweeps; ++s) {
-    halo_exchange(*ls.halo, ctx, L.x.p);
+  for (int s = 1; s < pre; ++s) {
+    halo_exchange(H, ctx, L.x.p);
     smooth(ctx, mg, L, b, 1, false);
   }
-  halo_exchange(*ls.halo, ctx, L.x.p);
+  if (last) return;  // coarsest level, distributed: smoothing only (the one-rank counts)
+  MgLevel& C = mg.lv[l + 1];
+  halo_exchange(H, ctx, L.x.p);
   spmv_blk_epi(ctx, mg.k, 2, L.nn, L.bp, L.bc, L.v, L.x.p, L.r.p, b, nullptr, 0.0);
-  dispatch_k(mg.k, [&](auto kc) {
-    constexpr int K = decltype(kc)::value;
-    hipLaunchKernelGGL(k_mg_restrict_part<K>, dim3((unsigned)grid_for(C.nn, 256)), dim3(256), 0, ctx.stream,
-                       mg.gfine, C.d, mg.sm, L.r.p, C.b.p);
-    AFEM_LAUNCHED();
-  });
-  comm_allreduce(ls.halo->comm, ctx, C.b.p, C.n);
-  vcycle(ctx, mg, 1, C.b.p);
-  dispatch_k(mg.k, [&](auto kc) {
-    constexpr int K = decltype(kc)::value;
-    hipLaunchKernelGGL(k_mg_prolong_own<K>, dim3((unsigned)grid_for(L.nn, 256)), dim3(256), 0, ctx.stream, C.d,
-                       mg.sm, L.nn, C.x.p, L.x.p);
-    AFEM_LAUNCHED();
-  });
+  if (C.dist) {
+    halo_exchange(H, ctx, L.r.p);
+    dispatch_k(mg.k, [&](auto kc) {
+      constexpr int K = decltype(kc)::value;
+      hipLaunchKernelGGL(k_mg_restrict_dist<K>, dim3((unsigned)grid_for(C.nn, 256)), dim3(256), 0, ctx.stream, L.gd,
+                         L.sm, C.sm, L.r.p, C.b.p);
+      AFEM_LAUNCHED();
+    });
+    vcycle_dist(ls, mg, l + 1, C.b.p);
+    halo_exchange(*C.halo, ctx, C.x.p);
+    dispatch_k(mg.k, [&](auto kc) {
+      constexpr int K = decltype(kc)::value;
+      hipLaunchKernelGGL(k_mg_prolong_dist<K>, dim3((unsigned)grid_for(L.nn, 256)), dim3(256), 0, ctx.stream, L.sm,
+                         C.sm, C.x.p, L.x.p);
+      AFEM_LAUNCHED();
+    });
+  }
+  else {
+    dispatch_k(mg.k, [&](auto kc) {
+      constexpr int K = decltype(kc)::value;
+      hipLaunchKernelGGL(k_mg_restrict_part<K>, dim3((unsigned)grid_for(C.nn, 256)), dim3(256), 0, ctx.stream, L.gd,
+                         C.d, L.sm, L.r.p, C.b.p);
+      AFEM_LAUNCHED();
+    });
+    comm_allreduce(ls.halo->comm, ctx, C.b.p, C.n);
+    vcycle(ctx, mg, l + 1, C.b.p);
+    dispatch_k(mg.k, [&](auto kc) {
+      constexpr int K = decltype(kc)::value;
+      hipLaunchKernelGGL(k_mg_prolong_own<K>, dim3((unsigned)grid_for(L.nn, 256)), dim3(256), 0, ctx.stream, C.d,
+                         L.sm, L.nn, C.x.p, L.x.p);
+      AFEM_LAUNCHED();
+    });
+  }
   for (int s = 0; s < mg.sweeps; ++s) {
-    halo_exchange(*ls.halo, ctx, L.x.p);
+    halo_exchange(H, ctx, L.x.p);
     smooth(ctx, mg, L, b, 1, false);
   }
 }
@@ -951,7 +1360,7 @@ void mg_apply(LinearSystem& ls, const double* r, double* z)
     hipLaunchKernelGGL(k_mg_mask_pad, dim3(g), dim3(256), 0, ctx.stream, n, L0.n, ls.cons.p, r, L0.b.p);
   AFEM_LAUNCHED();
   if (mg.global)
-    vcycle_global(ls, mg, L0.b.p);
+    vcycle_dist(ls, mg, 0, L0.b.p);
   else
     vcycle(ctx, mg, 0, L0.b.p);
   AFEM_HIP(hipMemcpyAsync(z, L0.x.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));

@@ -66,8 +66,8 @@ def parse(argv=None):
                     help="skip the CPU baselines (the oracle timed at the C2 size on the host cores, N = 1 only)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_assembly_C2.json"))
     ap.add_argument("--no-extras", action="store_true", help="skip the side measurements (N = 1 only anyway)")
-    ap.add_argument("--legs", default="c4,c3,c2_arrays,unstructured,c5",
-                    help="the side measurements to run (comma list of c4, c3, c2_arrays, unstructured, c5)")
+    ap.add_argument("--legs", default="c4,c3,c2_generic,c2_arrays,unstructured,c5",
+                    help="the side measurements to run (comma list of c4, c3, c2_generic, c2_arrays, unstructured, c5)")
     ap.add_argument("--c3-n", type=int, default=170, help="C3 block-3 elasticity box (170 -> 5.0M nodes)")
     ap.add_argument("--c4-n", type=int, default=463, help="C4 Poisson box on one GPU (463 -> 99.9M DoF); 0: skip")
     ap.add_argument("--c5-n", type=int, default=128,
@@ -413,6 +413,69 @@ def c2_arrays_leg(ctx, af, n, reps=10, warmup=2):
     return out
 
 
+def c2_generic_leg(ctx, af, n, reps=10, warmup=2, atomic_reps=2):
+    """C2 through the path an UNCHANGED module takes: BSRFormat::assembleBilinear
+    with the module's own element lambda (_computeElementMatrixTetra4Gpu,
+    modules/poisson/FemModule.h:177-186: examples/elements.hpp PoissonTet4,
+    compiled into examples/libafem_generic_example.so) on libafem's cell-unit
+    kernel (include/arcanefem_amd_generic.hpp k_assemble_units), values
+    written once (Mode::Overwrite = resetMatrixValues + assembleBilinear).
+    The roofline's algorithmic bytes are the headline's without the RHS (no
+    source term in assembleBilinear).  Also timed: the reference's algorithm
+    (one lane per cell, f64 atomics into HBM: assemble_bilinear_atomic) on the
+    same structure, and the values against the fixed-physics strip kernel."""
+    sys.path.insert(0, os.path.join(ROOT, "examples"))
+    import generic_example as gx
+
+    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+    bsr = af.BSRFormat(mesh, 1).initialize(True)
+    bsr.computeSparsity()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    plan = bsr.functor_plan()
+    ctx.synchronize()
+    plan_ms = (time.perf_counter() - t0) * 1e3
+
+    def timed(fn, base, r, w):
+        for _ in range(w):
+            fn()
+        ctx.synchronize()
+        for i in range(r):
+            ctx.event_record(base + 2 * i)
+            fn()
+            ctx.event_record(base + 2 * i + 1)
+        ctx.synchronize()
+        return [ctx.event_elapsed(base + 2 * i, base + 2 * i + 1) for i in range(r)]
+
+    ks = timed(lambda: gx.assemble(bsr, gx.POISSON, gx.UNITS, overwrite=True), 150, reps, warmup)
+    kms = float(np.median(ks))
+    vals_u = bsr.download()[2]
+    ka = timed(lambda: gx.assemble(bsr, gx.POISSON, gx.ATOMIC, overwrite=True), 190, atomic_reps, 1)
+    kam = float(np.median(ka))
+    bsr.assemblePoissonP1(1.0, 0.0, None)
+    vals_f = bsr.download()[2]
+    st = bsr.stats()
+    nnz = bsr.view().nnz_blocks
+    ab = 4 * int(st["n_incidences"]) + 24 * mesh.n_nodes + 8 * (mesh.n_own_nodes + 1) + 12 * nnz
+    ach = ab / (kms * 1e-3) / 1e9
+    out = {"config": f"C2 box n={n} ({mesh.n_own_nodes} DoF, {mesh.n_cells} tets): assembleBilinear(the Poisson "
+                     f"module's tet4 element lambda) through the generic element-functor entry, values overwritten",
+           "dof": int(mesh.n_own_nodes), "value": round(mesh.n_own_nodes / (kms * 1e-3) / 1e6, 1),
+           "unit": "MDoF/s (assembly kernel)", "kernel_ms": round(kms, 4), "kernel_ms_all": [round(x, 4) for x in ks],
+           "roofline": {"bound": "hbm", "kernel": "k_assemble_units<4,1,compact,PoissonTet4>",
+                        "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(ab)},
+           "evaluations_per_cell": round(plan["n_entries"] / mesh.n_cells, 4),
+           "plan": {k: int(plan[k]) for k in ("n_units", "n_stages", "n_entries", "rows_per_layer", "width", "nbuf",
+                                              "wide", "lattice")},
+           "plan_build_ms": round(plan_ms, 1),
+           "atomic_kernel_ms": round(kam, 4), "atomic_frac": round(ab / (kam * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "vs_fixed_physics_max_rel": float(np.abs(vals_u - vals_f).max() / np.abs(vals_f).max())}
+    bsr.close()
+    mesh.close()
+    return out
+
+
 def elastodynamics_c5(ctx, af, n, steps, preconditioners=("multigrid", "jacobi")):
     """BASELINE config C5 on one GPU: 3D Newmark elastodynamics, every step
     re-assembles c0 M + K and the body-force RHS on the fixed block-3
@@ -692,6 +755,8 @@ def main():
             extras["c4"] = poisson_c4(ctx, af, args.c4_n)
         if "c3" in legs:
             extras["c3"] = elasticity_c3(ctx, af, args.c3_n)
+        if "c2_generic" in legs:
+            extras["c2_generic"] = c2_generic_leg(ctx, af, 215)
         if "c2_arrays" in legs:
             extras["c2_arrays"] = c2_arrays_leg(ctx, af, 215)
         if "unstructured" in legs and args.unstructured_levels > 0:

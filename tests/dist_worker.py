@@ -19,9 +19,12 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 # case parameters shared with the test
 POISSON = dict(n=5, nz=8)
 POISSON_PAT = dict(n=12, nz=16)  # slabs whose rows are mostly interior stencil rows: the pattern SpMV
+POISSON_PAT8 = dict(n=12, nz=40)  # the same over 8 slabs (5-6 node layers each): the N = 8 z-slab split
 DYN = dict(n=3, nz=5, E=21e5, nu=0.28, rho=1.0, dt=1e-3, f=(0.0, -9.81, 1.0), steps=4)
 # slabs whose owned boxes coarsen (even n; 2 ranks: 8 and 9 owned layers -> 7 (padded) and 8 cells in z)
 POISSON_MG = dict(n=8, nz=16)
+# large enough for distributed coarse levels (level 1: 9 x 9 x 17 nodes over the slabs, then the gathered box)
+POISSON_MG2 = dict(n=16, nz=32)
 DYN_MG = dict(n=8, nz=12, E=21e5, nu=0.28, rho=1.0, dt=1e-3, f=(0.0, -9.81, 1.0), steps=3)
 
 
@@ -43,8 +46,9 @@ def main():
     res = {}
     if case.endswith("_async"):
         case = case[:-len("_async")]
-    if case in ("poisson", "poisson_pat", "poisson_mg"):
-        prm = {"poisson": POISSON, "poisson_pat": POISSON_PAT, "poisson_mg": POISSON_MG}[case]
+    if case in ("poisson", "poisson_pat", "poisson_pat8", "poisson_mg", "poisson_mg2"):
+        prm = {"poisson": POISSON, "poisson_pat": POISSON_PAT, "poisson_pat8": POISSON_PAT8, "poisson_mg": POISSON_MG,
+               "poisson_mg2": POISSON_MG2}[case]
         n, nz = prm["n"], prm["nz"]
         mesh = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=20250220, nranks=world, rank=rank)
         bsr = af.BSRFormat(mesh, 1).initialize(True)
@@ -54,7 +58,7 @@ def main():
         bsr.toLinearSystem(ls)
         ls.applyDirichletViaPenalty(mesh.bottom_nodes(), 0.5, 1e30)
         ls.set_halo_structured(comm, mesh)
-        if case == "poisson_mg":
+        if case in ("poisson_mg", "poisson_mg2"):
             # point Jacobi, then the block-Jacobi V-cycles on the slabs' owned boxes,
             # then (below) the global V-cycle: fine level distributed, coarse levels replicated
             ls.setSolverOptions(rtol=1e-14, max_iter=20000, preconditioner="jacobi")
@@ -69,7 +73,7 @@ def main():
         _, _, l2g = mesh.download()
         res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
                    converged=int(st["converged"]), rel=st["rel_residual"], spmv=st["spmv_kernel"])
-        if case == "poisson_mg":
+        if case in ("poisson_mg", "poisson_mg2"):
             res["iters_jacobi"] = it_j
             res["iters_block"] = it_b
             if rank == 0:  # the same global box on ONE rank: the multigrid solve the slabs must reproduce

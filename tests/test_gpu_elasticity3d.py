@@ -372,3 +372,110 @@ def test_block_spmv_matches_block_product(ctx, variant, which, use_csr, spmv):
     yo = np.zeros((rows.shape[0] - 1, k))
     np.add.at(yo, np.repeat(np.arange(rows.shape[0] - 1), np.diff(rows)), prod)
     assert np.abs(y - yo.ravel()).max() <= 1e-13 * np.abs(yo).max()
+
+
+# ---------------------------------------------------------------- C3 at its own size
+def _kuhn_neighbourhood(n, g, seed=20250220, jitter=0.2):
+    """The (up to 8) cubes around global node g of the generator's n^3 Kuhn
+    box with their exact coordinates: local cells, node ids, coordinates."""
+    np1 = n + 1
+    i, j, k = g % np1, (g // np1) % np1, g // (np1 * np1)
+    cubes = [(a, b, c) for a in (i - 1, i) for b in (j - 1, j) for c in (k - 1, k)
+             if 0 <= a < n and 0 <= b < n and 0 <= c < n]
+    e = np.eye(3, dtype=np.int64)
+    tets = []
+    for cube in cubes:
+        v0 = np.array(cube)
+        for perm in O.KUHN_PERMS:
+            v1 = v0 + e[perm[0]]
+            v2 = v1 + e[perm[1]]
+            tets.append([v0, v1, v2, v0 + 1])
+    T = np.array(tets)
+    gid = T[..., 0] + np1 * (T[..., 1] + np1 * T[..., 2])
+    nodes, local = np.unique(gid, return_inverse=True)
+    local = local.reshape(gid.shape).astype(np.int32)
+    h = 1.0 / n
+    ijk = np.stack([nodes % np1, (nodes // np1) % np1, nodes // (np1 * np1)], 1)
+    xyz = np.zeros((nodes.shape[0], 3))
+    for c in range(3):
+        u = O.hash_u01(seed, nodes * 3 + c)
+        xyz[:, c] = ijk[:, c].astype(np.float64) * h + (u - 0.5) * (jitter * h)
+    return nodes, local, xyz
+
+
+def test_c3_full_size_properties(ctx):
+    """BASELINE config C3 at its own size (n = 170: 5.0 M nodes, 15.0 M DoF,
+    74.3 M blocks, per-block layout as the bench's c3 leg): the structure size
+    nnz_b = 2E + N; the six rigid-body modes (3 translations, 3 rotations
+    x -> w x x, exact in P1) in the kernel of K through the product SpMV;
+    on ~400 sampled rows the block row against the oracle's
+    (orc_assemble_elasticity_tet on the row's cube neighbourhood with the
+    generator's exact coordinates) per entry at 1e-12 of the row's largest
+    entry, and block symmetry K_cr = K_rc^T; the body-force total f x volume."""
+    n = 170
+    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+    N = mesh.n_own_nodes
+    assert N == (n + 1) ** 3
+    bsr = af.BSRFormat(mesh, 3).initialize(False)
+    bsr.computeSparsity()
+    n3 = 3 * N
+    drhs = ctx.malloc(8 * n3)
+    bsr.assembleElasticityP1Ex(LAM, MU2, 0.0, (0.0, 0.0, -1.0), drhs, rhs_mode="set")
+    rhs = ctx.to_host(drhs, n3, np.float64)
+    ctx.free(drhs)
+    nnz_b = bsr.view().nnz_blocks
+    edges = 3 * n * (n + 1) ** 2 + 3 * n * n * (n + 1) + n ** 3
+    assert nnz_b == 2 * edges + N
+    rows, cols, vals = bsr.download()
+    vmax = np.abs(vals).max()
+    _, coords, _ = mesh.download()
+    # rigid-body modes through the product SpMV (k_spmv_blk on the node-row structure)
+    ls = af.DoFLinearSystem().initialize(ctx, n3)
+    bsr.toLinearSystem(ls)
+    x = ctx.malloc(8 * n3)
+    y = ctx.malloc(8 * n3)
+    X = coords[:N]
+    modes = []
+    for a in range(3):
+        v = np.zeros((N, 3))
+        v[:, a] = 1.0
+        modes.append(v)
+    for w in np.eye(3):
+        modes.append(np.cross(w, X))
+    worst = 0.0
+    for v in modes:
+        ctx.to_device(x, v.ravel())
+        ls.spmv(x, y)
+        r = ctx.to_host(y, n3, np.float64)
+        worst = max(worst, np.abs(r).max() / (vmax * np.abs(v).max()))
+    ctx.free(x)
+    ctx.free(y)
+    assert worst <= 1e-12, worst
+    # sampled rows: oracle parity per entry and block symmetry
+    rng = np.random.default_rng(170)
+    samples = np.concatenate([rng.integers(0, N, 400), [0, N - 1, (n + 1) ** 2 * 85 + (n + 1) * 5 + 3]])
+    worst_row = 0.0
+    for g in samples:
+        s, e = int(rows[g]), int(rows[g + 1])
+        nodes, local, xyz = _kuhn_neighbourhood(n, int(g))
+        orp, ocols = O.sparsity(nodes.shape[0], nodes.shape[0], local)
+        ov, _ = O.assemble_elasticity_tet(nodes.shape[0], local, xyz, orp, ocols, LAM, MU2)
+        rl = int(np.searchsorted(nodes, g))
+        assert np.array_equal(cols[s:e], nodes[ocols[orp[rl]:orp[rl + 1]]])
+        orow = ov[9 * orp[rl]:9 * orp[rl + 1]]
+        grow = vals[9 * s:9 * e]
+        worst_row = max(worst_row, np.abs(grow - orow).max() / np.abs(orow).max())
+        for t in range(s, e):
+            c = int(cols[t])
+            tt = int(rows[c]) + int(np.searchsorted(cols[rows[c]:rows[c + 1]], g))
+            assert cols[tt] == g
+            bt = vals[9 * tt:9 * tt + 9].reshape(3, 3)
+            assert np.abs(bt.T - vals[9 * t:9 * t + 9].reshape(3, 3)).max() <= 1e-14 * vmax
+    assert worst_row <= VAL_TOL, worst_row
+    # the body force's total: f_z x volume of the (jitter-deformed) unit box
+    assert abs(rhs[2::3].sum() + 1.0) < 1e-3 and abs(rhs[0::3].sum()) < 1e-12
+    print(f"C3 n={n}: {n3} DoF, {nnz_b} blocks; rigid modes max |K v| / (max|K| max|v|) {worst:.2e}; "
+          f"sampled rows max rel {worst_row:.2e}")
+    ls.reset()
+    bsr.close()
+    mesh.close()
