@@ -103,6 +103,7 @@ struct Ctx {
 struct StructuredInfo {
   bool valid = false;
   int dim = 3, n = 0, nz = 0, nranks = 1, rank = 0;
+  int64_t lx = 0, ly = 0;   // 3D node counts along x / y when they differ from n + 1 (a relabeled lattice)
   int64_t L = 0;            // nodes per layer
   int k0 = 0, k1 = 0;       // owned node layers [k0,k1)
   int ghost_lo = -1, ghost_hi = -1;  // ghost layers (or -1)
@@ -247,6 +248,15 @@ struct Structure {
   int max_row_len = 0;
   int64_t max_wave_seg = 0;  // max nnz of one slice
   DevBuf<int64_t> diag_pos;  // [n_rows] position of the diagonal in cols
+  // canonical lattice structure (array-fed lattice meshes in any numbering,
+  // NB_DOF 1; sparsity.hip canonical_lattice): the assembly metadata (slices,
+  // strips, slot streams, node lists) is built in the lattice's own numbering,
+  // where a row's slots follow the generator box's column order and the
+  // compiled-in strip signatures match; cperm[16 p + t] is the position in the
+  // row's (id-sorted) columns of the row's canonical slot t at processing
+  // position p.  The strip / stencil kernels write through it.
+  bool canon = false;
+  DevBuf<uint8_t> cperm;
 };
 
 struct LinearSystem;
@@ -429,7 +439,10 @@ void exclusive_scan_i32_to_i64(Ctx& ctx, const int32_t* in, int64_t* out, int64_
 int64_t read_i64(Ctx& ctx, const int64_t* d);
 void device_minmax_i32(Ctx& ctx, const int32_t* a, int64_t n, int32_t* lo, int32_t* hi);
 
-void build_structure(Mesh& m, Structure& s);
+// nb_dof = 1: a lattice mesh in a non-generator numbering gets the canonical
+// lattice structure (Structure::canon) when its strips match the compiled-in
+// signatures there
+void build_structure(Mesh& m, Structure& s, int nb_dof = 0);
 // node -> incident-cell lists of the owned nodes (sorted by cell id); returns the entry count
 int64_t node_cell_adjacency(Ctx& ctx, const Mesh& m, int64_t n_rows, DevBuf<int64_t>& nc_ptr, DevBuf<int32_t>& nc);
 // per-axis layer index of every owned node when they sit on a (jittered) lattice (sparsity.hip)

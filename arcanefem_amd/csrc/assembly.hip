@@ -589,8 +589,15 @@ struct StripPre {
   u32x4 l0, l1;
   u32x4 ch[MAXC];
   u32x4 cu[MAXC];  // uniform scalar instance: local node index of every step (strip_u)
+  u32x4 pq;        // canonical structures: the row's slot map (Structure::cperm, 16 bytes)
   double x[4], y[4], z[4];
 };
+// byte t of a 16-byte slot map
+__device__ __forceinline__ uint32_t pbyte(const u32x4& q, int t)
+{
+  const uint32_t w = (t >> 2) == 0 ? q.x : ((t >> 2) == 1 ? q.y : ((t >> 2) == 2 ? q.z : q.w));
+  return (w >> (8 * (t & 3))) & 0xFFu;
+}
 
 // LDS image of a strip slice: accumulators [slot][lane] (as Tile), the
 // slice's node coordinates AoS (DIMC doubles per node: one address per
@@ -638,7 +645,9 @@ extern "C" int afem_debug_wave_times(unsigned long long* out, int n)
 // steps only load the window, and no step needs an emit mask (≈45 instead of
 // ≈72 VALU ops per cell).  Same formulas in the same order as the general
 // path, so both give the same bits.
-template <int NV, int MAXC, int MAXW, int UMODE>
+// PERM: a canonical structure (Structure::canon): the slots are the lattice's
+// canonical ones and the write-back stores slot t at rb + cperm[16 p + t].
+template <int NV, int MAXC, int MAXW, int UMODE, bool PERM = false>
 __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64_t n_slices, const SliceRec* __restrict__ recs,
                                                           unsigned long long* __restrict__ tickets,
                                                           int u_cap, int w_cap,
@@ -652,7 +661,8 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
                                                           const double* __restrict__ coords, double s_coef,
                                                           double f_meas, double* __restrict__ vals,
                                                           double* __restrict__ rhs, int rhs_add,
-                                                          const SlotRec* __restrict__ uslots)
+                                                          const SlotRec* __restrict__ uslots,
+                                                          const uint8_t* __restrict__ cperm)
 {
   constexpr bool UNI = UMODE != 0;  // 1: scalar shift/swap branches, 2: selects on the uniform bit
   // uniform tet instances address coordinates by the local-index stream (no
@@ -727,6 +737,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
     p.row = perm[q];
     p.dl = pos_dl[q];
     p.rb = pos_rb[q];
+    if constexpr (PERM) p.pq = reinterpret_cast<const u32x4*>(cperm)[q];
     const int nc = (int)((R.meta >> 24) + 15) >> 4;
     if constexpr (!ULOC) {  // uniform instances read the slots from the scalar stream
       const u32x4* sp = reinterpret_cast<const u32x4*>(strip + (int64_t)R.strip_off * 1024) + lane;
@@ -1008,7 +1019,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
     fp -= len;
     uint16_t* map = reinterpret_cast<uint16_t*>(cxyz);
     const uint32_t dsl = active ? dslot : 0xFFu;
-    if (UNI || W <= MAXW) {
+    if (UNI || PERM || W <= MAXW) {  // canonical structures: W <= 16 = MAXW (sparsity.hip)
       // The diagonal accumulator is zeroed first (on the uniform path it holds
       // the padding steps' sink values): the row sum then runs over all W
       // slots with no per-slot test (slots past the row's end stay 0, and
@@ -1029,7 +1040,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
       for (int t = 0; t < MAXW; ++t)
         if (t < len) {
           acc[fp + t] = rv[t];
-          map32[fp + t] = (uint32_t)(rb + t);
+          map32[fp + t] = (uint32_t)(rb + (PERM ? pbyte(cur.pq, t) : (uint32_t)t));
         }
       if (active) acc[fp + dslot] = -sum;
       wave_sync_lds();
@@ -1143,7 +1154,7 @@ __host__ __device__ constexpr int64_t stencil_tile_bytes(int64_t u_cap, int64_t 
 }
 
 // one slice of signature S (the steps, the RHS and the write-back of k_assemble_stencil)
-template <const StencilSig& S, int MAXC>
+template <const StencilSig& S, int MAXC, bool PERM>
 __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nsteps, int lane, const double* cxyz,
                                               double* flat, int64_t* rbs, double s_coef, double f_meas,
                                               double* __restrict__ vals, double* __restrict__ rhs, int rhs_add)
@@ -1228,7 +1239,8 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
     // run -- no owner division, no dependent LDS read of the row offsets
     const int64_t rb = active ? cur.rb : -1;
     const int64_t rb_run = __shfl(rb, lane & ~3);
-    const bool runs = __all(active && rb == rb_run + (int64_t)W * (lane & 3));
+    // (canonical structures store through the slot map: no runs)
+    const bool runs = !PERM && __all(active && rb == rb_run + (int64_t)W * (lane & 3));
     if (runs) {
       static_assert(4 * W <= 64, "a run's values exceed the wave");
       wave_sync_lds();  // every lane's coordinate reads before the image overwrites them
@@ -1251,13 +1263,13 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
       // slices): each lane stores its row's W values straight from the registers
       // (no image, no owner table: nothing of this path is kept live across slices)
 #pragma unroll
-      for (int t = 0; t < W; ++t) vals[rb + t] = t == D ? -sum : acc[t];
+      for (int t = 0; t < W; ++t) vals[rb + (PERM ? pbyte(cur.pq, t) : t)] = t == D ? -sum : acc[t];
     }
     wave_sync_lds();
 }
 
 // signature index -> stencil_slice<S_index> (a scalar branch per slice)
-template <int I, const StencilSig& S0, const StencilSig&... SR>
+template <bool PERM, int I, const StencilSig& S0, const StencilSig&... SR>
 struct StencilDispatch {
   template <int MAXC>
   __device__ __forceinline__ static void run(int sig, const StripPre<MAXC>& cur, int nsteps, int lane,
@@ -1265,9 +1277,9 @@ struct StencilDispatch {
                                              double f_meas, double* vals, double* rhs, int rhs_add)
   {
     if (sig == I || sizeof...(SR) == 0)
-      stencil_slice<S0, MAXC>(cur, nsteps, lane, cxyz, flat, rbs, s_coef, f_meas, vals, rhs, rhs_add);
+      stencil_slice<S0, MAXC, PERM>(cur, nsteps, lane, cxyz, flat, rbs, s_coef, f_meas, vals, rhs, rhs_add);
     else if constexpr (sizeof...(SR) > 0)
-      StencilDispatch<I + 1, SR...>::template run<MAXC>(sig, cur, nsteps, lane, cxyz, flat, rbs, s_coef, f_meas,
+      StencilDispatch<PERM, I + 1, SR...>::template run<MAXC>(sig, cur, nsteps, lane, cxyz, flat, rbs, s_coef, f_meas,
                                                         vals, rhs, rhs_add);
   }
 };
@@ -1287,7 +1299,7 @@ constexpr int stencil_maxw()
   return m;
 }
 
-template <const StencilSig&... SS>
+template <bool PERM, const StencilSig&... SS>
 __global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, const SliceRec* __restrict__ recs,
                                                             unsigned long long* __restrict__ tickets, int u_cap,
                                                             const int32_t* __restrict__ perm,
@@ -1297,7 +1309,8 @@ __global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, co
                                                             const int32_t* __restrict__ snode,
                                                             const double* __restrict__ coords, double s_coef,
                                                             double f_meas, double* __restrict__ vals,
-                                                            double* __restrict__ rhs, int rhs_add)
+                                                            double* __restrict__ rhs, int rhs_add,
+                                                            const uint8_t* __restrict__ cperm)
 {
   constexpr int MAXC = stencil_maxc<SS...>();
   extern __shared__ __align__(16) unsigned char smem[];
@@ -1336,6 +1349,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, co
     p.row = perm[q];
     p.dl = pos_dl[q];
     p.rb = pos_rb[q];
+    if constexpr (PERM) p.pq = reinterpret_cast<const u32x4*>(cperm)[q];
     const u32x4* su = reinterpret_cast<const u32x4*>(strip_u + (int64_t)R.strip_off * 1024) + lane;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) p.cu[c] = su[(int64_t)c * 64];
@@ -1374,7 +1388,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_stencil(int64_t n_slices, co
     gather(nid1, nxt);
     load_nid(R2, nid2);
 
-    StencilDispatch<0, SS...>::template run<MAXC>((int)R0.sig, cur, (int)(R0.meta >> 24), lane, cxyz, flat, rbs,
+    StencilDispatch<PERM, 0, SS...>::template run<MAXC>((int)R0.sig, cur, (int)(R0.meta >> 24), lane, cxyz, flat, rbs,
                                                   s_coef, f_meas, vals, rhs, rhs_add);
     if (p1 >= r1) break;
     p0 = p1;
@@ -2835,7 +2849,7 @@ void launch_stencil(const Structure& s, int n_cu, const double* coords, double s
   static int occ_k = 0;
   static size_t occ_shm = 0;
   static const void* occ_kern = nullptr;
-  auto kern = k_assemble_stencil<AFEM_STENCIL_PACK>;
+  auto kern = s.canon ? k_assemble_stencil<true, AFEM_STENCIL_PACK> : k_assemble_stencil<false, AFEM_STENCIL_PACK>;
   const size_t shm = (size_t)stencil_tile_bytes(s.k_nodes, stencil_maxw<AFEM_STENCIL_PACK>());
   if (occ_shm != shm || occ_kern != reinterpret_cast<const void*>(kern)) {
     occ_kern = reinterpret_cast<const void*>(kern);
@@ -2848,7 +2862,7 @@ void launch_stencil(const Structure& s, int n_cu, const double* coords, double s
   int64_t nblk = (int64_t)n_cu * per_cu;
   if (nblk > s.n_k) nblk = s.n_k < 8 ? 8 : s.n_k;
   hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm, stream, s.n_k, s.rec_k.p, tk, s.k_nodes, s.perm.p,
-                     s.pos_rb.p, s.pos_dl.p, s.strip_u.p, s.snode.p, coords, s_coef, f_meas, vals, rhs, rhs_add);
+                     s.pos_rb.p, s.pos_dl.p, s.strip_u.p, s.snode.p, coords, s_coef, f_meas, vals, rhs, rhs_add, s.cperm.p);
   AFEM_LAUNCHED();
 }
 
@@ -2918,12 +2932,17 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64), shm_s, stream, n_list, list, tk,
                          ucap, wcap, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.strip_u.p,
                          s.lidx.p, s.snode.p, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add,
-                         reinterpret_cast<const SlotRec*>(slots ? slots : s.uslot.p));
+                         reinterpret_cast<const SlotRec*>(slots ? slots : s.uslot.p), s.cperm.p);
     };
+    // canonical structures (compact strips, <= 16 slots: sparsity.hip) run the
+    // PERM instances; no other instance knows the slot map
+#define AFEM_SK(NV_, C_, W_, U_) (s.canon ? k_assemble_strip<NV_, C_, W_, U_, true> : k_assemble_strip<NV_, C_, W_, U_, false>)
+#define AFEM_SKF(NV_, C_, W_, U_) reinterpret_cast<const void*>(AFEM_SK(NV_, C_, W_, U_))
+    AFEM_REQUIRE(!s.canon || (nv == 4 && s.max_strip_c <= 2 && s.max_slice_w <= 16 && s.n_mb == 0), AFEM_ERR_STATE,
+                 "canonical structure beyond the compact strip instances");
     const SliceRec* list_m = use_uni ? s.rec_m.p : s.rec_all.p;
-#define AFEM_STRIP_K(NV_, C_, W_, U_, N_, L_, T_, SHM_, ST_)                                                           \
-  launch_s(reinterpret_cast<const void*>(&k_assemble_strip<NV_, C_, W_, U_>), k_assemble_strip<NV_, C_, W_, U_>, N_, \
-           L_, T_, SHM_, ST_)
+#define AFEM_STRIP_K(NV_, C_, W_, U_, N_, L_, T_, SHM_, ST_) \
+  launch_s(AFEM_SKF(NV_, C_, W_, U_), AFEM_SK(NV_, C_, W_, U_), N_, L_, T_, SHM_, ST_)
     const bool small = s.max_strip_c <= 2 && s.max_slice_w <= 16;
     if (nv == 4 && uni_env) {
       // uniform slices on the context stream; the general-instance slices in
@@ -2967,7 +2986,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       hipStream_t s_ms = has_u && !serial_k ? side : ctx.stream;
       hipStream_t s_mb = has_u && !serial_k ? side : (s.n_ms > 0 && !serial_k ? side : ctx.stream);
       if (s.n_ms > 0)
-        launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 0>), k_assemble_strip<4, 2, 16, 0>, s.n_ms,
+        launch_s(AFEM_SKF(4, 2, 16, 0), AFEM_SK(4, 2, 16, 0), s.n_ms,
                  s.rec_ms.p, tk0 + 128, shm_ms, s_ms, s.ms_nodes, ms_w);
       if (s.n_mb > 0)
         launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 4, 32, 0>), k_assemble_strip<4, 4, 32, 0>, s.n_mb,
@@ -2975,7 +2994,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       if (use_k) {
         if (s.n_ur > 0) {
           const size_t shm_ur = (size_t)(8 * 64 * (int64_t)s.ur_w + strip_coord_bytes(dimc, s.ur_nodes, s.ur_w));
-          launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 1>), k_assemble_strip<4, 2, 16, 1>,
+          launch_s(AFEM_SKF(4, 2, 16, 1), AFEM_SK(4, 2, 16, 1),
                    s.n_ur, s.rec_ur.p, tk0, shm_ur, side, s.ur_nodes, s.ur_w, s.urslot.p);
         }
         launch_stencil(s, ctx.n_cu, b.mesh->coords.p, s_coef, f_meas, b.values.p, rhs, rhs_add,
@@ -2984,10 +3003,10 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       else if (has_u) {
         const size_t shm_uu = (size_t)(8 * 64 * (int64_t)s.u_w + strip_coord_bytes(dimc, s.u_nodes, s.u_w));
         if (umode == 2)
-          launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 2>), k_assemble_strip<4, 2, 16, 2>,
+          launch_s(AFEM_SKF(4, 2, 16, 2), AFEM_SK(4, 2, 16, 2),
                    s.n_uni, s.rec_u.p, tk0, shm_uu, ctx.stream, s.u_nodes, s.u_w);
         else
-          launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 1>), k_assemble_strip<4, 2, 16, 1>,
+          launch_s(AFEM_SKF(4, 2, 16, 1), AFEM_SK(4, 2, 16, 1),
                    s.n_uni, s.rec_u.p, tk0, shm_uu, ctx.stream, s.u_nodes, s.u_w);
       }
       AFEM_LAUNCHED();
@@ -3025,10 +3044,13 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       else AFEM_STRIP_K(3, 4, 32, 0, s.n_slices, s.rec_all.p, tk0 + 128, shm_g, ctx.stream);
     }
 #undef AFEM_STRIP_K
+#undef AFEM_SK
+#undef AFEM_SKF
     AFEM_LAUNCHED();
     b.last_kernel = AFEM_KERNEL_STRIP;
     return;
   }
+  AFEM_REQUIRE(!s.canon, AFEM_ERR_STATE, "a canonical structure needs the strip kernels");
   // register-resident incidence groups per lane / fixed write-back width
   const int max_groups = s.max_slice_k >> 2;
   const int prof = (max_groups <= 6 && s.max_slice_w <= 16) ? 0 : (max_groups <= 16 ? 1 : -1);

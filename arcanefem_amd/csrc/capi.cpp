@@ -484,7 +484,7 @@ int afem_bsr_compute_sparsity(afem_bsr* b)
   b->has_sparsity = false;
   b->fplan = FunctorPlan();
   b->hand = HandOver();
-  build_structure(*b->mesh, b->s);
+  build_structure(*b->mesh, b->s, b->nb_dof);
   b->values.alloc((size_t)b->s.nnz * b->nb_dof * b->nb_dof);
   AFEM_HIP(hipMemsetAsync(b->values.p, 0, b->values.bytes(), b->mesh->ctx->stream));
   b->mesh->ctx->sync();

@@ -1171,7 +1171,8 @@ int64_t node_cell_adjacency(Ctx& ctx, const Mesh& m, int64_t n_rows, DevBuf<int6
   return n_inc;
 }
 
-void build_structure(Mesh& m, Structure& s)
+namespace {
+void build_structure_impl(Mesh& m, Structure& s)
 {
   Ctx& ctx = *m.ctx;
   ctx.set_device();
@@ -1216,9 +1217,9 @@ void build_structure(Mesh& m, Structure& s)
   // 3. processing order (slices of 64 rows)
   const StructuredInfo& st = m.st;
   if (st.valid && (st.dim == 3 || st.dim == 2)) {
-    const int64_t ax = st.n + 1;
+    const int64_t ax = st.lx > 0 ? st.lx : st.n + 1;
     const int64_t own_layers = st.k1 - st.k0;
-    const int64_t ay = st.dim == 3 ? (int64_t)st.n + 1 : own_layers;
+    const int64_t ay = st.dim == 3 ? (st.ly > 0 ? st.ly : (int64_t)st.n + 1) : own_layers;
     const int64_t az = st.dim == 3 ? own_layers : 1;
     AFEM_REQUIRE(ax * ay * az == n_rows, AFEM_ERR_STATE, "structured mesh: owned node box does not match n_own");
     const int bx = st.dim == 3 ? 4 : 8, bz = st.dim == 3 ? 4 : 1;
@@ -1703,6 +1704,232 @@ void build_structure(Mesh& m, Structure& s)
     }
   }
   ctx.sync();
+}
+
+// ---- canonical lattice structures.  A mesh handed over as arrays whose owned
+// nodes sit on a lattice gets the brick order (lattice_order), but in a
+// non-generator numbering each row's columns -- sorted by node id -- come in a
+// different order from row to row, so no slice is uniform and no compiled-in
+// strip signature matches.  Relabeling the nodes by their lattice index (x +
+// Lx (y + Ly z): the generator's numbering) and ordering the cells by (lower
+// cube corner, Kuhn type: the generator's cell order) reproduces the
+// generator's structure; its slices, strips and node lists are built there and
+// keep working in the caller's numbering through two maps: the nodes (perm,
+// snode: lattice index -> node id) and each row's slots (cperm: canonical slot
+// -> position in the row's id-sorted columns, applied by the kernels' stores).
+__global__ void k_lat_ids(int64_t n, const int32_t* __restrict__ lx, const int32_t* __restrict__ ly,
+                          const int32_t* __restrict__ lz, int64_t L0, int64_t L1, int32_t* __restrict__ lat,
+                          int32_t* __restrict__ inv)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t id = lx[i] + L0 * (ly[i] + L1 * (int64_t)lz[i]);
+  lat[i] = (int32_t)id;
+  inv[id] = (int32_t)i;
+}
+
+// key of a cell: lattice index of its lower cube corner, then the Kuhn type of
+// its vertex path (v1 - v0 = e_a0, v2 - v1 = e_a1: mesh.hip c_kuhn's order), 7
+// for any other shape
+__global__ void k_cell_keys(int64_t nc, const int32_t* __restrict__ cn, const int32_t* __restrict__ lx,
+                            const int32_t* __restrict__ ly, const int32_t* __restrict__ lz, int64_t L0, int64_t L1,
+                            unsigned long long* __restrict__ keys, int32_t* __restrict__ ids)
+{
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  int x[4], y[4], z[4];
+  int mx = 1 << 30, my = 1 << 30, mz = 1 << 30;
+  for (int a = 0; a < 4; ++a) {
+    const int32_t v = cn[4 * c + a];
+    x[a] = lx[v];
+    y[a] = ly[v];
+    z[a] = lz[v];
+    mx = min(mx, x[a]);
+    my = min(my, y[a]);
+    mz = min(mz, z[a]);
+  }
+  auto axis = [&](int a, int b) -> int {
+    const int dx = x[b] - x[a], dy = y[b] - y[a], dz = z[b] - z[a];
+    if (dx == 1 && dy == 0 && dz == 0) return 0;
+    if (dx == 0 && dy == 1 && dz == 0) return 1;
+    if (dx == 0 && dy == 0 && dz == 1) return 2;
+    return -1;
+  };
+  const int a0 = axis(0, 1), a1 = axis(1, 2), a2 = axis(2, 3);
+  int type = 7;
+  if (a0 >= 0 && a1 >= 0 && a2 >= 0 && a0 != a1 && a1 != a2 && a0 != a2) {
+    const int tbl[3][3] = { { -1, 0, 1 }, { 2, -1, 3 }, { 4, 5, -1 } };  // (a0, a1) -> c_kuhn index
+    type = tbl[a0][a1];
+  }
+  keys[c] = (unsigned long long)(mx + L0 * (my + L1 * (int64_t)mz)) << 3 | (unsigned long long)type;
+  ids[c] = (int32_t)c;
+}
+
+__global__ void k_relabel_cells(int64_t nc, const int32_t* __restrict__ cn, const int32_t* __restrict__ order,
+                                const int32_t* __restrict__ lat, int32_t* __restrict__ out)
+{
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 4 * nc) return;
+  out[t] = lat[cn[4 * (int64_t)order[t >> 2] + (t & 3)]];
+}
+
+__global__ void k_permute_coords(int64_t n, const int32_t* __restrict__ inv, const double* __restrict__ in,
+                                 double* __restrict__ out)
+{
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 3 * n) return;
+  out[t] = in[3 * (int64_t)inv[t / 3] + t % 3];
+}
+
+__global__ void k_map_ids(int64_t n, const int32_t* __restrict__ inv, int32_t* __restrict__ v)
+{
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n && v[t] >= 0) v[t] = inv[v[t]];
+}
+
+// physical row offsets and slot maps of the processing positions: canonical
+// row R (lattice index) = node r; canonical slot t of R (its columns sorted by
+// lattice index) -> the position of that column in r's id-sorted columns
+__global__ void k_canon_slots(int64_t n_pos, const int32_t* __restrict__ perm_lat, const int32_t* __restrict__ inv,
+                              const int64_t* __restrict__ crp, const int32_t* __restrict__ ccols,
+                              const int64_t* __restrict__ rp, const int32_t* __restrict__ cols,
+                              int64_t* __restrict__ pos_rb, uint8_t* __restrict__ cperm, int32_t* __restrict__ err)
+{
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pos) return;
+  uint8_t out[16] = {};
+  const int32_t R = perm_lat[p];
+  int64_t rb = 0;
+  if (R >= 0) {
+    const int32_t r = inv[R];
+    rb = rp[r];
+    const int len = (int)(rp[r + 1] - rb);
+    const int64_t cb = crp[R];
+    if (len != (int)(crp[R + 1] - cb) || len > 16) {
+      *err = 1;
+    }
+    else {
+      for (int t = 0; t < len; ++t) {
+        const int q = find_slot(cols + rb, len, inv[ccols[cb + t]]);
+        if (q >= len || cols[rb + q] != inv[ccols[cb + t]]) *err = 1;
+        out[t] = (uint8_t)q;
+      }
+    }
+  }
+  pos_rb[p] = rb;
+  for (int t = 0; t < 16; ++t) cperm[16 * p + t] = out[t];
+}
+
+// the canonical structure of a lattice mesh (see above) into s; false when it
+// does not apply or does not reach the stencil instance
+bool canonical_lattice(Mesh& m, Structure& s)
+{
+  Ctx& ctx = *m.ctx;
+  const int64_t n = s.n_rows;
+  DevBuf<int32_t> lat3[3];
+  int64_t L[3];
+  if (!lattice_coords(ctx, m, n, lat3, L)) return false;
+  DevBuf<int32_t> lat, inv;
+  lat.alloc(n);
+  inv.alloc(n);
+  hipLaunchKernelGGL(k_lat_ids, dim3(grid_for(n, 256)), dim3(256), 0, ctx.stream, n, lat3[0].p, lat3[1].p, lat3[2].p,
+                     L[0], L[1], lat.p, inv.p);
+  AFEM_LAUNCHED();
+  // the relabeled mesh: lattice node ids, cells in the generator's order
+  const int64_t nc = m.n_cells;
+  Mesh R;
+  R.ctx = m.ctx;
+  R.dim = 3;
+  R.nv = 4;
+  R.n_nodes = R.n_own = n;
+  R.n_cells = nc;
+  R.cell_node.alloc(4 * nc);
+  R.coords.alloc(3 * n);
+  {
+    DevBuf<unsigned long long> keys, keys_s;
+    DevBuf<int32_t> ids, ids_s;
+    keys.alloc(nc);
+    keys_s.alloc(nc);
+    ids.alloc(nc);
+    ids_s.alloc(nc);
+    hipLaunchKernelGGL(k_cell_keys, dim3(grid_for(nc, 256)), dim3(256), 0, ctx.stream, nc, m.cell_node.p, lat3[0].p,
+                       lat3[1].p, lat3[2].p, L[0], L[1], keys.p, ids.p);
+    AFEM_LAUNCHED();
+    size_t tmp_bytes = 0;
+    AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys.p, keys_s.p, ids.p, ids_s.p, (int)nc, 0, 64,
+                                                ctx.stream));
+    DevBuf<unsigned char> tmp;
+    tmp.alloc(tmp_bytes > 0 ? tmp_bytes : 1);
+    AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tmp_bytes, keys.p, keys_s.p, ids.p, ids_s.p, (int)nc, 0, 64,
+                                                ctx.stream));
+    hipLaunchKernelGGL(k_relabel_cells, dim3(grid_for(4 * nc, 256)), dim3(256), 0, ctx.stream, nc, m.cell_node.p,
+                       ids_s.p, lat.p, R.cell_node.p);
+    AFEM_LAUNCHED();
+  }
+  hipLaunchKernelGGL(k_permute_coords, dim3(grid_for(3 * n, 256)), dim3(256), 0, ctx.stream, n, inv.p, m.coords.p,
+                     R.coords.p);
+  AFEM_LAUNCHED();
+  R.st.valid = true;
+  R.st.dim = 3;
+  R.st.n = (int)(L[0] - 1);
+  R.st.lx = L[0];
+  R.st.ly = L[1];
+  R.st.nz = (int)(L[2] - 1);
+  R.st.k0 = 0;
+  R.st.k1 = (int)L[2];
+  R.st.L = L[0] * L[1];
+  Structure C;
+  build_structure_impl(R, C);
+  if (!C.strip_ok || !C.rec_ok || C.n_k == 0 || C.n_mb > 0 || C.max_strip_c > 2 || C.max_slice_w > 16 ||
+      C.nnz != s.nnz)
+    return false;
+  // back to the caller's numbering: node ids of the positions and node lists,
+  // physical row offsets, slot maps
+  const int64_t n_pos = C.n_slices * 64;
+  DevBuf<int32_t> perm_lat;
+  perm_lat.alloc(n_pos);
+  AFEM_HIP(hipMemcpyAsync(perm_lat.p, C.perm.p, perm_lat.bytes(), hipMemcpyDeviceToDevice, ctx.stream));
+  C.cperm.alloc(16 * n_pos);
+  DevBuf<int32_t> err;
+  err.alloc(1);
+  AFEM_HIP(hipMemsetAsync(err.p, 0, err.bytes(), ctx.stream));
+  hipLaunchKernelGGL(k_canon_slots, dim3(grid_for(n_pos, 256)), dim3(256), 0, ctx.stream, n_pos, perm_lat.p, inv.p,
+                     C.row_ptr.p, C.cols.p, s.row_ptr.p, s.cols.p, C.pos_rb.p, C.cperm.p, err.p);
+  AFEM_LAUNCHED();
+  hipLaunchKernelGGL(k_map_ids, dim3(grid_for(n_pos, 256)), dim3(256), 0, ctx.stream, n_pos, inv.p, C.perm.p);
+  AFEM_LAUNCHED();
+  hipLaunchKernelGGL(k_map_ids, dim3(grid_for((int64_t)C.snode.n, 256)), dim3(256), 0, ctx.stream,
+                     (int64_t)C.snode.n, inv.p, C.snode.p);
+  AFEM_LAUNCHED();
+  int32_t herr = 0;
+  AFEM_HIP(hipMemcpyAsync(&herr, err.p, sizeof(herr), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  if (herr) return false;
+  // the matrix structure stays the caller's; everything else is the canonical build
+  C.row_ptr = std::move(s.row_ptr);
+  C.cols = std::move(s.cols);
+  C.diag_pos = std::move(s.diag_pos);
+  C.n_rows = s.n_rows;
+  C.n_cols = s.n_cols;
+  C.nnz = s.nnz;
+  C.max_row_len = s.max_row_len;
+  C.inc.reset();  // canonical slots: the incidence-table kernels are not used on this structure
+  C.lattice = true;
+  C.canon = true;
+  s = std::move(C);
+  return true;
+}
+
+}  // namespace
+
+void build_structure(Mesh& m, Structure& s, int nb_dof)
+{
+  build_structure_impl(m, s);
+  // an array-fed lattice whose numbering keeps it off the stencil instance
+  const char* ce = variant("AFEM_CANON");
+  if (nb_dof == 1 && s.lattice && m.nv == 4 && m.dim == 3 && m.n_nodes == m.n_own && s.n_k * 2 < s.n_slices &&
+      s.max_row_len <= 16 && !(ce && atoi(ce) == 0))
+    (void)canonical_lattice(m, s);
 }
 
 }  // namespace afem

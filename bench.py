@@ -519,9 +519,10 @@ def elastodynamics_c5(ctx, af, n, steps, preconditioners=("multigrid", "jacobi")
 
 
 def host_cores():
-    """(threads the CPU baseline uses, cores this process may run on, nproc):
-    every core of the affinity mask, capped by OMP_NUM_THREADS when the lease
-    sets it (16 per GPU on the MI355X boxes)."""
+    """(the lease's thread count, cores this process may run on, nproc): the
+    lease's OMP_NUM_THREADS (16 per GPU on the MI355X boxes) capped by the
+    affinity mask, and the affinity mask itself -- the node's host cores the CPU
+    baseline is stated on (VERDICT r3 #8)."""
     nproc = os.cpu_count() or 1
     try:
         aff = len(os.sched_getaffinity(0))
@@ -529,6 +530,16 @@ def host_cores():
         aff = nproc
     lim = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     return (min(aff, lim) if lim > 0 else aff), aff, nproc
+
+
+def cgroup_cpu_limit():
+    """The cgroup v2 CPU quota of this job (cpu.max: quota / period), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def download_c2(ctx, mesh, bsr, ls, bottom):
@@ -561,26 +572,37 @@ def cpu_baseline(c2, runs=5):
         return time.perf_counter() - t0, vals, rhs
 
     t1, _, _ = one(O.assemble_poisson)
-    cores, aff, nproc = host_cores()
-    threads = O.omp_threads(cores)
-    one(O.assemble_poisson_omp)  # thread-pool warm-up
-    ts = []
-    for _ in range(runs):
-        t, vals, rhs = one(O.assemble_poisson_omp)
-        ts.append(t)
-    tm = float(np.median(ts))
+    lease, aff, nproc = host_cores()
+
+    def median_on(threads):
+        O.omp_threads(threads)
+        one(O.assemble_poisson_omp)  # thread-pool warm-up
+        ts = []
+        for _ in range(runs):
+            t, v, r = one(O.assemble_poisson_omp)
+            ts.append(t)
+        return float(np.median(ts)), v, r
+
+    t_lease, _, _ = median_on(lease)
+    tm, vals, rhs = median_on(aff)  # every core of the affinity mask: the stated baseline
+    threads = aff
     scale = np.abs(vals).max()
     dv = float(np.abs(vals - c2["gpu_vals"]).max() / scale)
     free = np.abs(vals) < 1e20  # the penalty diagonal is set, not summed
     dvf = float(np.abs(vals[free] - c2["gpu_vals"][free]).max() / np.abs(vals[free]).max())
     drhs = float(np.abs(rhs - c2["gpu_rhs"]).max() / np.abs(rhs).max())
     c2["orc_vals"], c2["orc_rhs"] = vals, rhs
+    quota = cgroup_cpu_limit()
     return {"value": round(n_own / tm / 1e6, 2), "unit": "MDoF/s", "cores": threads, "kind": "port",
-            "nproc": nproc, "affinity_cores": aff,
+            "nproc": nproc, "affinity_cores": aff, "cgroup_cpu_quota": quota,
+            "value_lease_threads": round(n_own / t_lease / 1e6, 2), "lease_threads": lease,
+            "value_single_thread": round(n_own / t1 / 1e6, 2),
             "sample": f"C2 itself: Poisson-3D P1 Kuhn box ({n_own} DoF, {cells.shape[0]} tets, {cols.size} nnz), "
                       f"structure from the GPU run: median of {runs} assemblies {tm * 1e3:.0f} ms on {threads} "
-                      f"OpenMP threads (oracle/oracle.c cell loop, atomic adds, gcc -O3 -march=x86-64-v4; nproc {nproc}, {aff} cores in the "
-                      f"affinity mask, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}); single thread "
+                      f"OpenMP threads = every core of the affinity mask (oracle/oracle.c cell loop, atomic adds, gcc -O3 "
+                      f"-march=x86-64-v4; nproc {nproc}; cgroup CPU quota {quota}); on the lease's "
+                      f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')} ({lease} threads) "
+                      f"{t_lease * 1e3:.0f} ms; single thread "
                       f"{t1 * 1e3:.0f} ms = {n_own / t1 / 1e6:.2f} MDoF/s; oracle vs GPU values max rel diff "
                       f"{dvf:.1e} (free rows; {dv:.1e} overall), RHS {drhs:.1e}"}
 
@@ -592,18 +614,26 @@ def cpu_baseline_cg(c2, iters=50, runs=3):
     from oracle import oracle as O
 
     rp, cols, vals, rhs = c2["rp"], c2["cols"], c2["orc_vals"], c2["orc_rhs"]
-    threads = O.omp_threads(host_cores()[0])
-    O.pcg_jacobi_omp(rp, cols, vals, rhs, max_iter=-iters)
-    ts = []
-    for _ in range(runs):
-        t0 = time.perf_counter()
+    lease, aff, _ = host_cores()
+
+    def median_on(threads):
+        O.omp_threads(threads)
         O.pcg_jacobi_omp(rp, cols, vals, rhs, max_iter=-iters)
-        ts.append(time.perf_counter() - t0)
-    t = float(np.median(ts))
-    return {"value": round(iters / t, 2), "unit": "iter/s", "cores": threads, "kind": "port",
+        ts = []
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            O.pcg_jacobi_omp(rp, cols, vals, rhs, max_iter=-iters)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    t_lease = median_on(lease)
+    t = median_on(aff)
+    return {"value": round(iters / t, 2), "unit": "iter/s", "cores": aff, "kind": "port",
+            "value_lease_threads": round(iters / t_lease, 2), "lease_threads": lease,
             "sample": f"Jacobi-PCG (oracle/oracle.c orc_pcg_jacobi_omp) on the C2 system ({rp.size - 1} DoF, "
                       f"{int(rp[-1])} nnz): {iters} fixed iterations, median of {runs} runs {t * 1e3:.1f} ms on "
-                      f"{threads} OpenMP threads"}
+                      f"{aff} OpenMP threads (every core of the affinity mask); {t_lease * 1e3:.1f} ms on the "
+                      f"lease's {lease}"}
 
 
 def cpu_baseline_c1(runs=3):

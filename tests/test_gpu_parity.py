@@ -521,6 +521,50 @@ def test_lattice_order_matches_generator_box(ctx, n, nz, jitter):
     assert np.array_equal(l0.rhs_host(), l1.rhs_host())
 
 
+@pytest.mark.parametrize("n,nz,seed", [(12, 12, 77), (9, 17, 5), (6, 40, 3)])
+def test_canonical_lattice_random_numbering(ctx, variant, n, nz, seed):
+    """A generator box renumbered at random (nodes and cells) and handed over
+    as arrays: the structure build relabels it by lattice index
+    (sparsity.hip canonical_lattice), so its slices reach the same stencil /
+    uniform instances as the generator's box, and the kernels store through
+    the per-row slot map.  The matrix is bitwise the generator's, permuted
+    (A1[p[i], p[j]] == A0[i, j]), and so is the RHS.  AFEM_CANON=0 (no
+    relabeling: the general instance) stays within the oracle tolerance."""
+    m0 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=seed)
+    b0, l0 = _assemble_gpu(ctx, m0, 5.5)
+    cells0, coords0, _ = m0.download()
+    rng = np.random.default_rng(seed)
+    nn = coords0.shape[0]
+    p = rng.permutation(nn)
+    cells = p[cells0].astype(np.int32)[rng.permutation(cells0.shape[0])]
+    coords = np.empty_like(coords0)
+    coords[p] = coords0
+    m1 = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    b1, l1 = _assemble_gpu(ctx, m1, 5.5)
+    s0, s1 = b0.stats(), b1.stats()
+    assert s1["brick_order"] == 2
+    for k in ("n_slices", "uniform_slices", "stencil_slices", "stencil_sig"):
+        assert s0[k] == s1[k], (k, s0[k], s1[k])
+    assert s1["stencil_slices"] > 0
+    r0, c0, v0 = b0.download()
+    r1, c1, v1 = b1.download()
+    key0 = p[np.repeat(np.arange(nn), np.diff(r0))].astype(np.int64) * nn + p[c0]
+    key1 = np.repeat(np.arange(nn), np.diff(r1)).astype(np.int64) * nn + c1
+    o0, o1 = np.argsort(key0), np.argsort(key1)
+    assert np.array_equal(key0[o0], key1[o1])
+    assert np.array_equal(v0[o0], v1[o1])
+    assert np.array_equal(l1.rhs_host()[p], l0.rhs_host())
+    # without the relabeling: the general instance, oracle tolerance
+    variant("AFEM_CANON", "0")
+    m2 = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    b2, _ = _assemble_gpu(ctx, m2, 5.5)
+    variant("AFEM_CANON", None)
+    assert b2.stats()["stencil_slices"] == 0
+    r2, c2, v2 = b2.download()
+    assert np.array_equal(r1, r2) and np.array_equal(c1, c2)
+    _check_values(v2, v1)
+
+
 def test_lattice_order_rejects_non_lattices(ctx):
     """Coordinates that are not a lattice (a Kuhn box whose node layers are
     warped beyond the gap rule, and one missing node) fall back to the
