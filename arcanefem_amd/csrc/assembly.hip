@@ -665,6 +665,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
                                                           const uint8_t* __restrict__ cperm)
 {
   constexpr bool UNI = UMODE != 0;  // 1: scalar shift/swap branches, 2: selects on the uniform bit
+  static_assert(!(PERM && UMODE == 1), "the slot map needs the select instance's register budget");
   // uniform tet instances address coordinates by the local-index stream (no
   // column-index table in LDS, no dependent LDS read per step)
   constexpr bool ULOC = UNI && NV == 4;
@@ -1019,6 +1020,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
     fp -= len;
     uint16_t* map = reinterpret_cast<uint16_t*>(cxyz);
     const uint32_t dsl = active ? dslot : 0xFFu;
+    const u32x4 pq = cur.pq;
     if (UNI || PERM || W <= MAXW) {  // canonical structures: W <= 16 = MAXW (sparsity.hip)
       // The diagonal accumulator is zeroed first (on the uniform path it holds
       // the padding steps' sink values): the row sum then runs over all W
@@ -1040,7 +1042,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
       for (int t = 0; t < MAXW; ++t)
         if (t < len) {
           acc[fp + t] = rv[t];
-          map32[fp + t] = (uint32_t)(rb + (PERM ? pbyte(cur.pq, t) : (uint32_t)t));
+          map32[fp + t] = (uint32_t)(rb + (PERM ? pbyte(pq, t) : (uint32_t)t));
         }
       if (active) acc[fp + dslot] = -sum;
       wave_sync_lds();
@@ -2936,7 +2938,10 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
     };
     // canonical structures (compact strips, <= 16 slots: sparsity.hip) run the
     // PERM instances; no other instance knows the slot map
-#define AFEM_SK(NV_, C_, W_, U_) (s.canon ? k_assemble_strip<NV_, C_, W_, U_, true> : k_assemble_strip<NV_, C_, W_, U_, false>)
+    // (the uniform slices through the select instance, UMODE 2, same bits: the
+    // 3-waves-per-SIMD branch instance has no registers for the map)
+#define AFEM_SK(NV_, C_, W_, U_) \
+  (s.canon ? k_assemble_strip<NV_, C_, W_, (U_ == 1 ? 2 : U_), true> : k_assemble_strip<NV_, C_, W_, U_, false>)
 #define AFEM_SKF(NV_, C_, W_, U_) reinterpret_cast<const void*>(AFEM_SK(NV_, C_, W_, U_))
     AFEM_REQUIRE(!s.canon || (nv == 4 && s.max_strip_c <= 2 && s.max_slice_w <= 16 && s.n_mb == 0), AFEM_ERR_STATE,
                  "canonical structure beyond the compact strip instances");

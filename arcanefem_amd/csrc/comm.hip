@@ -185,7 +185,10 @@ void post_sendrecv(Halo& h, hipStream_t st)
 namespace {
 // host transport, asynchronous: pack on the context stream, copy the send part
 // to the halo's pinned buffer, and let a worker thread wait for that copy and
-// run the caller's exchange callback while the context stream computes
+// run the caller's exchange callback while the context stream computes.  The
+// callback thus runs on this worker thread, not the caller's: the transport
+// must allow that (afem_comm_host_async's contract in arcanefem_amd.h:
+// MPI_THREAD_SERIALIZED or better, a Python callback free to take the GIL)
 void host_begin_async(Halo& h, Ctx& ctx, double* x)
 {
   Comm* c = h.comm;

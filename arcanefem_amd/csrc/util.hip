@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 
 namespace afem {
@@ -21,6 +22,9 @@ struct Variants {
   std::mutex mu;
   std::map<std::string, std::string> set;          // afem_set_variant
   std::map<std::string, std::pair<bool, std::string>> env;  // first lookup of the environment
+  // every value ever returned, interned: a returned pointer stays valid after a
+  // later afem_set_variant replaces or clears the knob (set nodes never move)
+  std::set<std::string> pool;
 };
 Variants& variants()
 {
@@ -34,7 +38,7 @@ const char* variant(const char* name)
   Variants& v = variants();
   std::lock_guard<std::mutex> g(v.mu);
   auto it = v.set.find(name);
-  if (it != v.set.end()) return it->second.c_str();
+  if (it != v.set.end()) return v.pool.insert(it->second).first->c_str();
   auto e = v.env.find(name);
   if (e == v.env.end()) {
     const char* x = getenv(name);

@@ -571,7 +571,11 @@ int afem_comm_create_host(afem_ctx* ctx, int nranks, int rank, const afem_host_t
  * thread, so the CG's interior SpMV proceeds while the halo is in flight
  * (halo posted after the pack, joined before the boundary rows; the callbacks
  * are then called from that thread, never concurrently with another call on
- * the same communicator).  Default: synchronous. */
+ * the same communicator).  Default: synchronous.  Enable it only with an
+ * exchange callback that may run on a thread other than the caller's: an MPI
+ * transport needs at least MPI_THREAD_SERIALIZED, a Python (ctypes) callback
+ * takes the GIL on that thread, so the calling thread must not hold the GIL
+ * while it waits in the solve (ctypes releases it around foreign calls). */
 int afem_comm_host_async(afem_comm* comm, int enable);
 int afem_comm_destroy(afem_comm* comm);
 /* In-place sum over ranks of n doubles (device pointer) on the context stream. */

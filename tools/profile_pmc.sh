@@ -5,7 +5,8 @@
 # Summarise with: python tools/pmc_summary.py <out_dir> <kernel_regex>
 OUT=${1:-gpurun_out/pmc}
 K=${2:-k_assemble_p1}
-B="bench.py --steps 6 --warmup 1 --cg-iters 2 --no-cpu-baseline --no-extras"
+# PMC_CMD: the python program + arguments to profile (default: a short bench run)
+B=${PMC_CMD:-"bench.py --steps 6 --warmup 1 --cg-iters 2 --no-cpu-baseline --no-extras"}
 export TMPDIR=/tmp
 mkdir -p $OUT
 pass() {  # name, counters...
