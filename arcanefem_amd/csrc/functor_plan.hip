@@ -433,7 +433,9 @@ void functor_plan_build(Bsr& b)
       g.lattice = 0;
       g.rl = 64 / (k * k);
       g.zs = 1;
-      P.n_units = s.n_slices * 64 / g.rl;
+      // 64 / k^2 rows per piece: the last piece may be partial (k = 3: 7 rows,
+      // 64 positions per slice are 9 pieces and one row of the next)
+      P.n_units = (s.n_slices * 64 + g.rl - 1) / g.rl;
       P.n_stages = P.n_units;
       P.nbuf = 1;
     }

@@ -72,6 +72,40 @@ struct PoissonTet4 {
   }
 };
 
+// Poisson tet4 in the cofactor form (not a module's arithmetic: one
+// reciprocal per cell instead of the module's 12 gradient divisions + 1): with
+// e_k = x_k - x_0 and c_1 = e_2 x e_3, c_2 = e_3 x e_1, c_3 = e_1 x e_2,
+// c_0 = -(c_1 + c_2 + c_3), K_ab = c_a . c_b / (6 |e_1 . c_1|) -- what the
+// cell-unit kernel reaches with lean element physics
+struct PoissonTet4Lean {
+  CellAccess acc;
+  __device__ FixedMatrix<4, 4> operator()(int32_t c) const
+  {
+    const Tet t = load_tet(acc, c);
+    double e[3][3];
+    for (int k = 0; k < 3; ++k)
+      for (int d = 0; d < 3; ++d) e[k][d] = t.x[k + 1][d] - t.x[0][d];
+    double cf[4][3];
+    for (int k = 0; k < 3; ++k) {
+      const double* a = e[(k + 1) % 3];
+      const double* b = e[(k + 2) % 3];
+      cf[k + 1][0] = a[1] * b[2] - a[2] * b[1];
+      cf[k + 1][1] = a[2] * b[0] - a[0] * b[2];
+      cf[k + 1][2] = a[0] * b[1] - a[1] * b[0];
+    }
+    for (int d = 0; d < 3; ++d) cf[0][d] = -(cf[1][d] + cf[2][d] + cf[3][d]);
+    const double s = 1.0 / (6.0 * fabs(e[0][0] * cf[1][0] + e[0][1] * cf[1][1] + e[0][2] * cf[1][2]));
+    FixedMatrix<4, 4> K;
+    for (int a = 0; a < 4; ++a)
+      for (int b = a; b < 4; ++b) {
+        const double v = s * (cf[a][0] * cf[b][0] + cf[a][1] * cf[b][1] + cf[a][2] * cf[b][2]);
+        K(a, b) = v;
+        K(b, a) = v;
+      }
+    return K;
+  }
+};
+
 struct ElasticityTet4 {
   CellAccess acc;
   double lambda, mu;

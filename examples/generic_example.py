@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(_HERE, "libafem_generic_example.so")
-POISSON, ELASTICITY = 0, 1
+POISSON, ELASTICITY, POISSON_LEAN = 0, 1, 2
 UNITS, ATOMIC = 0, 1
 _lib = None
 

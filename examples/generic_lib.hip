@@ -4,7 +4,8 @@
 // benchmark's c2_generic leg and tests/test_gpu_generic.py drive it on any
 // structure libafem built.
 //   gx_assemble(bsr, kind, path, mode, lambda, mu):
-//     kind 0: Poisson (tet4 / tri3 by the mesh), 1: elasticity (tet4 NB_DOF 3 / tri3 NB_DOF 2);
+//     kind 0: Poisson (tet4 / tri3 by the mesh), 1: elasticity (tet4 NB_DOF 3 / tri3 NB_DOF 2),
+//          2: Poisson tet4 in the cofactor form (elements::PoissonTet4Lean);
 //     path 0: cell-unit kernel (assemble_bilinear), 1: f64-atomic kernel (assemble_bilinear_atomic);
 //     mode 0: accumulate into the values, 1: overwrite them.
 // Enqueued on the structure's context stream; no synchronisation (path 1 syncs for its error flag).
@@ -32,6 +33,8 @@ extern "C" int gx_assemble(afem_bsr* bsr, int kind, int path, int mode, double l
   const afem::generic::CellAccess acc{ v.cell_node, v.coords };
   if (kind == 0 && v.block_size == 1 && v.nb_node_per_cell == 4) return run<4, 1>(bsr, elements::PoissonTet4{ acc }, path, mode);
   if (kind == 0 && v.block_size == 1 && v.nb_node_per_cell == 3) return run<3, 1>(bsr, elements::PoissonTri3{ acc }, path, mode);
+  if (kind == 2 && v.block_size == 1 && v.nb_node_per_cell == 4)
+    return run<4, 1>(bsr, elements::PoissonTet4Lean{ acc }, path, mode);
   if (kind == 1 && v.block_size == 3 && v.nb_node_per_cell == 4)
     return run<4, 3>(bsr, elements::ElasticityTet4{ acc, lambda, mu }, path, mode);
   if (kind == 1 && v.block_size == 2 && v.nb_node_per_cell == 3)

@@ -19,7 +19,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 # case parameters shared with the test
 POISSON = dict(n=5, nz=8)
 POISSON_PAT = dict(n=12, nz=16)  # slabs whose rows are mostly interior stencil rows: the pattern SpMV
-POISSON_PAT8 = dict(n=12, nz=40)  # the same over 8 slabs (5-6 node layers each): the N = 8 z-slab split
+POISSON_PAT8 = dict(n=16, nz=71)  # the same over 8 slabs (9 node layers each; a middle slab's rows next to
+# either ghost layer miss the pattern: 7 of 9 layers x 15^2/17^2 interior in-layer rows = 61 % >= 1/2)
 DYN = dict(n=3, nz=5, E=21e5, nu=0.28, rho=1.0, dt=1e-3, f=(0.0, -9.81, 1.0), steps=4)
 # slabs whose owned boxes coarsen (even n; 2 ranks: 8 and 9 owned layers -> 7 (padded) and 8 cells in z)
 POISSON_MG = dict(n=8, nz=16)

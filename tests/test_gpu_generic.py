@@ -176,6 +176,25 @@ def test_unit_kernel_slice_plan_on_a_box(ctx, variant):
     mesh.close()
 
 
+@pytest.mark.parametrize("n", [3, 7])
+def test_unit_kernel_slice_plan_partial_last_piece(ctx, variant, n):
+    """k = 3 slice pieces hold 7 rows: 64 positions per slice do not divide
+    into them, and the last piece of the structure is partial.  A box of
+    (n + 1)^3 = 64 / 512 nodes fills its slices to the last lane, so the last
+    piece holds an active row (it was dropped when the piece count was
+    rounded down)."""
+    import arcanefem_amd as af
+
+    variant("AFEM_FUNCTOR_PLAN", "slices")
+    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=3)
+    assert mesh.n_own_nodes % 64 == 0
+    for per_row in (False, True):
+        plan = _unit_case(ctx, mesh, 3, per_row)
+        assert plan["lattice"] == 0 and plan["rows_per_layer"] == 7
+        assert plan["n_units"] * 7 >= mesh.n_own_nodes
+    mesh.close()
+
+
 def test_unit_kernel_evaluations_per_cell(ctx, variant):
     """The lattice columns evaluate each cell at most 1 + 1/8 + 1/8 + 1/zs
     times (the cells shared with the neighbour columns / segments; fewer at

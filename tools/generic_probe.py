@@ -99,3 +99,42 @@ print(f"n={n_big} dof={mesh.n_own_nodes} B_alg={ab / 1e9:.3f} GB units(overwrite
       f"frac {ab / (t_units * 1e-3) / 8e12:.3f} | units(accumulate) {t_units_acc:.3f} | atomic {t_atomic:.3f} ms "
       f"frac {ab / (t_atomic * 1e-3) / 8e12:.3f} | fixed {t_fixed:.3f} ms | max|units-fixed|/max "
       f"{np.abs(u - f).max() / np.abs(f).max():.2e}", flush=True)
+
+# ---- lean element physics (cofactor form, one reciprocal per cell) on the same box
+t_lean = timeit(lambda: gx.assemble(bsr, gx.POISSON_LEAN, gx.UNITS, overwrite=True), 100, reps)
+ln = vals(bsr)
+print(f"n={n_big} units(lean cofactor functor) {t_lean:.3f} ms frac {ab / (t_lean * 1e-3) / 8e12:.3f} "
+      f"max|lean-fixed|/max {np.abs(ln - f).max() / np.abs(f).max():.2e}", flush=True)
+bsr.close()
+mesh.close()
+
+# ---- unstructured: the bench's L-shape-3D refined `levels` times (argv[4], 0 = skip)
+levels = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+if levels > 0:
+    import bench
+    from arcanefem_amd.gmsh import read_gmsh
+
+    gm = read_gmsh(os.path.join(ROOT, "tests", "golden", "L-shape-3D.msh"))
+    cells, coords = bench.refine_tets(gm.cells, gm.coords, levels, "cpu")
+    mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    del cells, coords
+    bsr = af.BSRFormat(mesh, 1).initialize(True)
+    bsr.computeSparsity()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    plan = bsr.functor_plan()
+    ctx.synchronize()
+    print(f"unstructured levels={levels} dof={mesh.n_own_nodes} plan build {1e3 * (time.perf_counter() - t0):.1f} ms: "
+          f"{plan}", flush=True)
+    st = bsr.stats()
+    nnz = bsr.view().nnz_blocks
+    ab = 4 * st["n_incidences"] + 24 * mesh.n_nodes + 8 * (mesh.n_own_nodes + 1) + 12 * nnz
+    t_fixed = timeit(lambda: bsr.assemblePoissonP1(1.0, 0.0), 120, reps)
+    f = vals(bsr)
+    t_lean = timeit(lambda: gx.assemble(bsr, gx.POISSON_LEAN, gx.UNITS, overwrite=True), 160, reps)
+    ln = vals(bsr)
+    t_mod = timeit(lambda: gx.assemble(bsr, gx.POISSON, gx.UNITS, overwrite=True), 200, reps)
+    print(f"unstructured: fixed strip {t_fixed:.3f} ms frac {ab / (t_fixed * 1e-3) / 8e12:.3f} | units(lean) "
+          f"{t_lean:.3f} ms frac {ab / (t_lean * 1e-3) / 8e12:.3f} | units(module) {t_mod:.3f} ms frac "
+          f"{ab / (t_mod * 1e-3) / 8e12:.3f} | max|lean-fixed|/max {np.abs(ln - f).max() / np.abs(f).max():.2e}",
+          flush=True)
