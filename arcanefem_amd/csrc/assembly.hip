@@ -1243,7 +1243,27 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
     const int64_t rb_run = __shfl(rb, lane & ~3);
     // (canonical structures store through the slot map: no runs)
     const bool runs = !PERM && __all(active && rb == rb_run + (int64_t)W * (lane & 3));
-    if (runs) {
+    if constexpr (PERM) {
+      // canonical structure: the rows are scattered over the matrix (the
+      // caller's numbering), so a lane's own W stores would touch 64 rows per
+      // instruction.  Row L's values go to flat positions [W L, W (L + 1)) at
+      // their physical slots (the slot map), then consecutive lanes store
+      // consecutive positions: W / 64 rows per instruction, each row's values
+      // one contiguous range (the flat image of k_assemble_strip)
+      wave_sync_lds();  // every lane's coordinate reads before the image overwrites them
+#pragma unroll
+      for (int t = 0; t < W; ++t) flat[lane * W + (int)pbyte(cur.pq, t)] = t == D ? -sum : acc[t];
+      rbs[lane] = rb;
+      wave_sync_lds();
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        const int P = 64 * k + lane;
+        const int L = P / W;  // constant divisor
+        const int64_t base = rbs[L];
+        if (base >= 0) vals[base + (P - L * W)] = flat[P];
+      }
+    }
+    else if (runs) {
       static_assert(4 * W <= 64, "a run's values exceed the wave");
       wave_sync_lds();  // every lane's coordinate reads before the image overwrites them
 #pragma unroll
@@ -1265,7 +1285,7 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
       // slices): each lane stores its row's W values straight from the registers
       // (no image, no owner table: nothing of this path is kept live across slices)
 #pragma unroll
-      for (int t = 0; t < W; ++t) vals[rb + (PERM ? pbyte(cur.pq, t) : t)] = t == D ? -sum : acc[t];
+      for (int t = 0; t < W; ++t) vals[rb + t] = t == D ? -sum : acc[t];
     }
     wave_sync_lds();
 }

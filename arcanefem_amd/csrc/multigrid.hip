@@ -23,6 +23,17 @@
 //  * constraint rows (penalty / eliminated, the PCG's `cons` flags) are taken
 //    out of the cycle: z = F V(F r) + C D^-1 r (F free, C constraint masks), so
 //    the preconditioner stays SPD and eliminated rows keep a zero direction.
+// Several ranks (z-slabs of one box): ONE global V-cycle.  The fine level is
+// the slab's owned rows with the system's halo; the coarse levels stay cut
+// into z-slabs (owned coarse layer Z = the owner of fine layer 2Z; local
+// numbering: owned layers, ghost layer below, ghost layer above; a halo per
+// level; the Galerkin rows next to a slab boundary read the neighbour's fine
+// boundary rows, exchanged once at setup as 15-entry "fat" rows) down to the
+// gather level -- a rank would own no layer, the level fits kDenseMax, or it
+// is below 1/512 of the fine grid (AFEM_MG_GATHER) -- whose operator is the
+// sum over the ranks of their owned rows' P^T A P parts, replicated with
+// everything below it (the one-rank hierarchy, the same arithmetic on every
+// rank).  Setup errors are agreed over the ranks (any_rank).
 #include "afem_internal.hpp"
 
 #include <algorithm>
@@ -311,7 +322,7 @@ __global__ void k_mg_mask_pad(int64_t n, int64_t n_all, const uint8_t* __restric
     b[i] = i < n && !cons[i] ? r[i] : 0.0;
 }
 
-// ---- the global V-cycle over z-slabs: fine level distributed, coarse levels replicated
+// ---- the global V-cycle over z-slabs: the fine level (and the distributed coarse levels below)
 // A slab's local node numbering (Mesh.structured with nranks > 1): the owned
 // layers k0 .. k0+nown-1, then the ghost layer below (if any), then the one above.
 struct SlabMap {

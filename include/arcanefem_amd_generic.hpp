@@ -172,14 +172,41 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
   const int bufsz = p.width * KK * RL;
   for (int i = lane; i < p.nbuf * bufsz; i += 64) acc[i] = 0.0;
   __syncthreads();
+  // the lane's entry of the next iteration is loaded one iteration ahead (the
+  // next round of this stage, else the first round of the next stage), so its
+  // latency hides behind the functor; tagged with its index (a stage without
+  // entries breaks the chain: the next one loads in place)
+  uint4 nxt{};
+  uint2 nxt2{};
+  int64_t nxt_e = -1;
   for (int L = 0; L < U.n_stages; ++L) {
     const int64_t e0 = p.stage_ptr[U.first_stage + L], e1 = p.stage_ptr[U.first_stage + L + 1];
+    const int64_t e2 = L + 1 < U.n_stages ? p.stage_ptr[U.first_stage + L + 2] : e1;
     for (int64_t e = e0 + lane; e - lane < e1; e += 64) {
+      uint4 m{};
+      uint2 m2{};
+      if (e < e1) {
+        if (nxt_e == e) {
+          m = nxt;
+          m2 = nxt2;
+        }
+        else {
+          m = reinterpret_cast<const uint4*>(p.entries)[e];
+          if (WIDE) m2 = reinterpret_cast<const uint2*>(p.entries2)[e];
+        }
+      }
+      {
+        const bool more = e + 64 - lane < e1;
+        const int64_t en = more ? e + 64 : e1 + lane;
+        if (en < (more ? e1 : e2)) {
+          nxt = reinterpret_cast<const uint4*>(p.entries)[en];
+          if (WIDE) nxt2 = reinterpret_cast<const uint2*>(p.entries2)[en];
+          nxt_e = en;
+        }
+      }
       if (e < e1) {
         uint32_t cell, pos, sl[4];
         if (WIDE) {
-          const uint4 m = reinterpret_cast<const uint4*>(p.entries)[e];
-          const uint2 m2 = reinterpret_cast<const uint2*>(p.entries2)[e];
           sl[0] = m.x;
           sl[1] = m.y;
           sl[2] = m.z;
@@ -188,7 +215,6 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
           pos = m2.y;
         }
         else {
-          const uint4 m = reinterpret_cast<const uint4*>(p.entries)[e];
           cell = m.x;
           sl[0] = m.y & 0xffffu;
           sl[1] = m.y >> 16;

@@ -1,0 +1,52 @@
+"""A/B of the cell-unit kernel's plan knobs at the C2 size in one process:
+for each variant (comma list of KEY=VALUE, '-' = defaults) a fresh structure
+and plan, then the kernel time (median of `reps`, HIP events) with the Poisson
+module's element (elements::PoissonTet4) and the lean cofactor element.
+usage: python tools/generic_ab.py n reps variant [variant ...]"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "examples"))
+import arcanefem_amd as af  # noqa: E402
+import generic_example as gx  # noqa: E402
+
+n, reps = int(sys.argv[1]), int(sys.argv[2])
+ctx = af.Context(0)
+mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+ref = None
+for spec in sys.argv[3:]:
+    kv = [] if spec == "-" else [x.split("=") for x in spec.split(",")]
+    for k, v in kv:
+        af.set_variant(k, v)
+    bsr = af.BSRFormat(mesh, 1).initialize(True)
+    bsr.computeSparsity()
+    plan = bsr.functor_plan()
+    st = bsr.stats()
+    nnz = bsr.view().nnz_blocks
+    ab = 4 * st["n_incidences"] + 24 * mesh.n_nodes + 8 * (mesh.n_own_nodes + 1) + 12 * nnz
+    out = []
+    for kind in (gx.POISSON, gx.POISSON_LEAN):
+        gx.assemble(bsr, kind, gx.UNITS, overwrite=True)
+        ctx.synchronize()
+        for i in range(reps):
+            ctx.event_record(2 * i)
+            gx.assemble(bsr, kind, gx.UNITS, overwrite=True)
+            ctx.event_record(2 * i + 1)
+        ctx.synchronize()
+        t = float(np.median([ctx.event_elapsed(2 * i, 2 * i + 1) for i in range(reps)]))
+        out.append(f"{t:.3f} ms ({ab / (t * 1e-3) / 8e12:.3f})")
+    v = bsr.download()[2]
+    if ref is None:
+        bsr.assemblePoissonP1(1.0, 0.0)
+        ref = bsr.download()[2]
+    err = float(np.abs(v - ref).max() / np.abs(ref).max())
+    print(f"{spec:40s} units {plan['n_units']:6d} rl {plan['rows_per_layer']:2d} evals/cell "
+          f"{plan['n_entries'] / mesh.n_cells:.3f} coalesced {plan.get('n_coalesced', -1)} | module {out[0]} | "
+          f"lean {out[1]} | err {err:.1e}", flush=True)
+    for k, _ in kv:
+        af.set_variant(k, None)
+    bsr.close()
