@@ -17,8 +17,9 @@
 //    consecutive z layers, processed layer by layer (every cell spans at most
 //    two consecutive layers, checked), so only two layers of rows are live in
 //    LDS and the column's cells are shared with its neighbour columns only:
-//    1 + 1/fx + 1/fy + 1/zs evaluations per cell (8 x 8 x 20: 1.30, against
-//    1.75 for the 4x4x4 bricks of the strip kernels);
+//    1 + 1/fx + 1/fy + 1/zs evaluations per cell (C2's default 8 x 8 x 10:
+//    1.34, against 1.75 for the 4x4x4 bricks of the strip kernels; zs from a
+//    target of 16384 units: 3 % faster than 8192 units of zs 20, r04e);
 //  * other meshes: rl-row pieces of the structure's processing-order slices
 //    (Hilbert-ordered), one layer.
 //
@@ -421,7 +422,7 @@ void functor_plan_build(Bsr& b)
       g.tx = (L[0] + g.fx - 1) / g.fx;
       g.ty = (L[1] + g.fy - 1) / g.fy;
       const int64_t cols_n = g.tx * g.ty;
-      const int64_t target = env_int("AFEM_FUNCTOR_UNITS", 8192);
+      const int64_t target = env_int("AFEM_FUNCTOR_UNITS", 16384);
       const int64_t ns_want = std::max<int64_t>(1, (target + cols_n - 1) / cols_n);
       int64_t zs = env_int("AFEM_FUNCTOR_ZS", (g.Lz + ns_want - 1) / ns_want);
       zs = std::max<int64_t>(4, std::min<int64_t>(zs, 255));

@@ -29,7 +29,7 @@
  *     consecutive rows as contiguous stores through a flat LDS image,
  *     otherwise per row.
  *
- * f is evaluated once per (unit, cell): 1.30x per cell on an 8 x 8 x 20
+ * f is evaluated once per (unit, cell): 1.34x per cell on an 8 x 8 x 10
  * lattice column (the cells shared with the neighbour columns and segments),
  * against 1x for the atomic scatter and 4x for the reference's atomic-free
  * gather.  Mode::Accumulate adds to the current values like the reference

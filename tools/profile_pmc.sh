@@ -9,8 +9,10 @@ K=${2:-k_assemble_p1}
 B=${PMC_CMD:-"bench.py --steps 6 --warmup 1 --cg-iters 2 --no-cpu-baseline --no-extras"}
 export TMPDIR=/tmp
 mkdir -p $OUT
+# PMC_PASSES: the pass names to run (default: all)
 pass() {  # name, counters...
   local name=$1; shift
+  if [ -n "$PMC_PASSES" ] && [[ " $PMC_PASSES " != *" $name "* ]]; then return 0; fi
   echo "pass $name" >> $OUT/progress.log
   timeout -k 5 150 rocprofv3 --pmc "$@" --kernel-include-regex "$K" -f csv -d $OUT/$name -o run -- python3 $B > $OUT/$name.log 2>&1
   local rc=$?
