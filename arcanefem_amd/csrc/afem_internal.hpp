@@ -405,6 +405,12 @@ struct LinearSystem {
   mutable DevBuf<uint8_t> pat_flag;  // rows whose columns follow the dominant offset pattern (pattern SpMV)
   mutable DevBuf<int32_t> pat_smp;   // the pattern detection's row samples
   mutable DevBuf<unsigned long long> pat_cnt;
+  // the pattern SpMV's tiled block order at large layer sizes (linear_system.hip
+  // plan_spmv_ls): row blocks by (in-layer tile, layer), and each launch
+  // position's partial-sum slot (the default order's, so the dot products keep
+  // their summation order)
+  mutable DevBuf<int32_t> pat_order, pat_pslot;
+  mutable uint64_t pat_order_key = 0;
   DevBuf<double> x0;      // the caller's initial guess (opts.initial_guess = 1)
   DevBuf<double> binv;    // block-Jacobi 3: inverse node blocks [n/3][9]
   DevBuf<int32_t> blist;  // multi-rank CG: SpMV row blocks, interior ones first

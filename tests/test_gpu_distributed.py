@@ -110,8 +110,9 @@ def test_distributed_poisson_solve(case, world, tmp_path):
 
 @pytest.mark.parametrize("case,world", [("elastodynamics", 2), ("elastodynamics_mg", 2), ("elastodynamics_mg", 4)])
 def test_distributed_elastodynamics(tmp_path, case, world):
-    """C5's loop over 2 slabs: point-Jacobi PCG, and the multigrid PCG (one
-    global V-cycle: fine level distributed, coarse levels replicated) -- both
+    """C5's loop over 2 slabs: point-Jacobi PCG, and the multigrid PCG over 2
+    and 4 slabs (one global V-cycle: fine and coarse levels distributed down to
+    the gather level, replicated below it) -- both
     must match the single-domain oracle Newmark loop; the multigrid one also
     the one-rank multigrid iteration counts."""
     p = W.DYN if case == "elastodynamics" else W.DYN_MG

@@ -697,11 +697,17 @@ def test_initial_guess_current_solution(ctx):
 
 
 @pytest.mark.parametrize("n", [9, 30])
-def test_pattern_spmv(ctx, variant, n):
+@pytest.mark.parametrize("tile", [False, True])
+def test_pattern_spmv(ctx, variant, n, tile):
     """The pattern-compressed SpMV (interior rows of a Kuhn box form their
     columns as row + the offsets of the interior stencil, the others read
     theirs, into the block's LDS column image): the same products in the same
-    order as the CSR-stream kernel (bitwise equal y), and the same CG solve."""
+    order as the CSR-stream kernel (bitwise equal y), and the same CG solve.
+    tile: the row blocks in the tiled (in-layer tile, layer) order large
+    layers get (forced here by a 1-node layer threshold), partial dot products
+    in the default order's slots -- still bitwise equal."""
+    if tile:
+        variant("AFEM_SPMV_TILE_LAYER", "1")
     mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=5)
     bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
     bottom = mesh.bottom_nodes()
