@@ -21,7 +21,7 @@ for f in sorted(glob.glob(d + "/*/run_counter_collection.csv")):
         disp[key]["_grid"] = float(r.get("Grid_Size") or 0)
     for (k, _), c in disp.items():
         if c["_grid"] >= min_grid:
-            name = k.split("(")[0]
+            name = k.replace("(anonymous namespace)::", "").split("(")[0]
             for n, v in c.items():
                 if n != "_grid":
                     vals[(name, n)].append(v)
