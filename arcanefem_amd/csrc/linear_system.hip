@@ -477,20 +477,32 @@ struct PatOff {
   int32_t off[16];
 };
 
+// 16 lanes per row (coalesced column reads; one thread per row: 18.7 ms at C4):
+// lane k compares column k with r + off[k]
 __global__ __launch_bounds__(256) void k_pat_flags(int64_t n_rows, const int64_t* __restrict__ rows,
                                                    const int32_t* __restrict__ cols, PatOff po,
                                                    uint8_t* __restrict__ flag, unsigned long long* __restrict__ count)
 {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool ok = false;
-  if (r < n_rows) {
+  const int l16 = threadIdx.x & 15;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  int32_t my_off = 0;  // off[l16] (a select chain: no dynamic index into the argument)
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (k == l16) my_off = po.off[k];
+  bool bad = r >= n_rows;
+  if (!bad) {
     const int64_t a = rows[r];
-    ok = rows[r + 1] - a == po.len;
-    for (int k = 0; k < po.len && ok; ++k) ok = (int64_t)cols[a + k] == r + po.off[k];
-    flag[r] = ok ? 1 : 0;
+    if (rows[r + 1] - a != po.len)
+      bad = true;
+    else if (l16 < po.len)
+      bad = (int64_t)cols[a + l16] != r + my_off;
   }
-  const unsigned long long m = __ballot(ok);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (unsigned long long)__popcll(m));
+  const unsigned long long m = __ballot(bad);
+  const int g = (int)(threadIdx.x & 63) & ~15;  // this row's 16 lanes in the wave
+  const bool ok = ((m >> g) & 0xFFFFull) == 0;
+  if (l16 == 0 && r < n_rows) flag[r] = ok ? 1 : 0;
+  const unsigned long long rows_ok = __ballot(l16 == 0 && r < n_rows && ok);
+  if ((threadIdx.x & 63) == 0 && rows_ok) atomicAdd(count, (unsigned long long)__popcll(rows_ok));
 }
 
 // k_spmv_stream4u with the block's column indices formed in LDS first: the
@@ -772,20 +784,35 @@ __global__ __launch_bounds__(1024) void k_reduce(int64_t n, const double* __rest
 // the rest of the row by > 1e10 (penalty P = 1e30, eliminated identity rows)
 // is excluded from the reference value of the stopping test (same rule as
 // oracle/oracle.c::orc_pcg_jacobi).
-__global__ void k_inv_diag(int64_t n_rows, const int64_t* __restrict__ rows, const int32_t* __restrict__ cols,
-                           const double* __restrict__ vals, double* __restrict__ dinv, uint8_t* __restrict__ cons)
+// 16 lanes per row: the row's columns and values are read coalesced (one
+// thread per row walked 15 entries 120 B apart from its neighbours': 20 ms per
+// solve at C4, 0.3 of the iteration time of 50 CG iterations), the diagonal
+// and the |off-diagonal| sum are 16-lane reductions
+__global__ __launch_bounds__(256) void k_inv_diag(int64_t n_rows, const int64_t* __restrict__ rows,
+                                                  const int32_t* __restrict__ cols, const double* __restrict__ vals,
+                                                  double* __restrict__ dinv, uint8_t* __restrict__ cons)
 {
-  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n_rows) return;
+  const int l16 = threadIdx.x & 15;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int64_t rr = r < n_rows ? r : n_rows - 1;
+  const int64_t a = rows[rr], e = rows[rr + 1];
   double d = 0.0, off = 0.0;
-  for (int64_t k = rows[r]; k < rows[r + 1]; ++k) {
-    if (cols[k] == (int32_t)r)
-      d = vals[k];
+  for (int64_t k = a + l16; k < e; k += 16) {
+    const double v = vals[k];
+    if (cols[k] == (int32_t)rr)
+      d += v;
     else
-      off += fabs(vals[k]);
+      off += fabs(v);
   }
-  dinv[r] = (d != 0.0) ? 1.0 / d : 0.0;
-  cons[r] = fabs(d) > 1e10 * off ? 1 : 0;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {
+    d += __shfl_xor(d, o, 16);
+    off += __shfl_xor(off, o, 16);
+  }
+  if (l16 == 0 && r < n_rows) {
+    dinv[r] = (d != 0.0) ? 1.0 / d : 0.0;
+    cons[r] = fabs(d) > 1e10 * off ? 1 : 0;
+  }
 }
 
 // k_inv_diag for a system with a node-block structure (NB_DOF = K, BSRFormat's
@@ -1472,8 +1499,8 @@ SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
       if (ls.pat_flag.n < (size_t)ls.n_rows) ls.pat_flag.alloc(ls.n_rows);
       if (!ls.pat_cnt.p) ls.pat_cnt.alloc(1);
       AFEM_HIP(hipMemsetAsync(ls.pat_cnt.p, 0, ls.pat_cnt.bytes(), ctx.stream));
-      hipLaunchKernelGGL(k_pat_flags, dim3(grid_for(ls.n_rows, 256)), dim3(256), 0, ctx.stream, ls.n_rows, ls.csr_rows,
-                         ls.csr_cols, po, ls.pat_flag.p, ls.pat_cnt.p);
+      hipLaunchKernelGGL(k_pat_flags, dim3(grid_for(16 * ls.n_rows, 256)), dim3(256), 0, ctx.stream, ls.n_rows,
+                         ls.csr_rows, ls.csr_cols, po, ls.pat_flag.p, ls.pat_cnt.p);
       AFEM_LAUNCHED();
       unsigned long long hc = 0;
       AFEM_HIP(hipMemcpyAsync(&hc, ls.pat_cnt.p, sizeof(hc), hipMemcpyDeviceToHost, ctx.stream));
@@ -1789,7 +1816,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     hipLaunchKernelGGL(k_inv_diag_blk<2>, dim3(grid_for(16 * pl.blk_n, 256)), dim3(256), 0, ctx.stream, pl.blk_n,
                        pl.blk_rows, pl.blk_cols, ls.csr_vals, ls.dinv.p, ls.cons.p);
   else
-    hipLaunchKernelGGL(k_inv_diag, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, ctx.stream, n, ls.csr_rows,
+    hipLaunchKernelGGL(k_inv_diag, dim3(grid_for(16 * n, 256)), dim3(256), 0, ctx.stream, n, ls.csr_rows,
                        ls.csr_cols, ls.csr_vals, ls.dinv.p, ls.cons.p);
   AFEM_LAUNCHED();
   const bool blk3 = ls.opts.precond_block == 3;

@@ -815,6 +815,71 @@ __global__ void k_strip_local(int64_t n_pos, const uint8_t* __restrict__ strip, 
 // (identity).  Positions left free repeat the slice's first node.  Every
 // kernel addresses the cache through the remapped local indices, so the
 // values do not change.  One wavefront per slice.
+// General (non-uniform) slices: every lane reads a node of its own at a step,
+// so no shift makes the classes consistent.  A greedy colouring instead: step
+// by step, lane by lane, a node read for the first time takes the least-used
+// class (with room left below maxq) that no node read at the same step by
+// the lanes of its 32-lane half already holds (mod 32: the z read) or, within
+// its 16-lane quarter, holds mod 16 (the x, y read); nodes never read take any
+// class with room.  Placement as for the uniform slices: q = c + 32 m.
+__device__ void bank_place_general(int lane, int nu, int n, bool act, const uint8_t* st, int maxq, int* cls,
+                                   int* used, uint8_t* qo, int32_t* nu_out)
+{
+  for (int u = lane; u < 256; u += 64) cls[u] = -1;
+  if (lane < 32) used[lane] = 0;
+  __syncthreads();
+  auto cap = [&](int c) { return (maxq - c + 31) / 32; };  // positions c + 32 m < maxq
+  for (int j = 0; j < n; ++j) {
+    const int u = act ? (int)st[(j >> 4) * 1024 + (j & 15)] : -1;
+    for (int t = 0; t < 64; ++t) {
+      const int ut = __shfl(u, t);
+      if (ut < 0) continue;  // wave-uniform
+      const int myc = u >= 0 ? cls[u] : -1;
+      int bits = 0;
+      if (((lane ^ t) & 32) == 0 && lane != t && u >= 0 && u != ut && myc >= 0) {
+        bits = 1 << myc;
+        if (((lane ^ t) & 16) == 0) bits |= 1 << (myc ^ 16);
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) bits |= __shfl_xor(bits, o);
+      if (lane == t && cls[u] < 0) {
+        int best = -1, bu = 1 << 30;
+        for (int pass = 0; pass < 2 && best < 0; ++pass)
+          for (int c = 0; c < 32; ++c)
+            if (used[c] < cap(c) && (pass == 1 || !((bits >> c) & 1)) && used[c] < bu) {
+              best = c;
+              bu = used[c];
+            }
+        cls[u] = best;
+        ++used[best];
+      }
+      __syncthreads();
+    }
+  }
+  if (lane == 0) {
+    uint8_t cnt[32];
+    for (int c = 0; c < 32; ++c) cnt[c] = 0;
+    int top = -1;
+    for (int u = 0; u < nu; ++u) {
+      int c = cls[u];
+      if (c < 0) {  // never read by a step: any class with room
+        int bu = 1 << 30;
+        for (int k = 0; k < 32; ++k)
+          if (used[k] < cap(k) && used[k] < bu) {
+            c = k;
+            bu = used[k];
+          }
+        ++used[c];
+      }
+      const int q = c + 32 * cnt[c]++;
+      qo[u] = (uint8_t)q;
+      top = max(top, q);
+    }
+    for (int u = nu; u < 256; ++u) qo[u] = qo[0];
+    *nu_out = top + 1;
+  }
+}
+
 __global__ __launch_bounds__(64) void k_bank_place(int64_t n_slices, const uint8_t* __restrict__ uflag,
                                                    const int32_t* __restrict__ perm,
                                                    const int64_t* __restrict__ snode_ptr,
@@ -822,7 +887,7 @@ __global__ __launch_bounds__(64) void k_bank_place(int64_t n_slices, const uint8
                                                    const int64_t* __restrict__ strip_ptr,
                                                    const int32_t* __restrict__ strip_n,
                                                    const uint32_t* __restrict__ pos_dl, uint8_t* __restrict__ q_of_u,
-                                                   int32_t* __restrict__ nu_new, int maxq)
+                                                   int32_t* __restrict__ nu_new, int maxq, int general)
 {
   __shared__ int cls[256];
   __shared__ int shift[32];
@@ -837,6 +902,11 @@ __global__ __launch_bounds__(64) void k_bank_place(int64_t n_slices, const uint8
     if (lane == 0) nu_new[sl] = nu;
   };
   const int n = strip_n[sl];
+  if (!uflag[sl] && general && nu <= maxq && n <= 32) {
+    bank_place_general(lane, nu, n, perm[sl * 64 + lane] >= 0, strip_u + strip_ptr[sl] + lane * 16, maxq, cls,
+                       shift, qo, nu_new + sl);
+    return;
+  }
   if (!uflag[sl] || nu > maxq || n > 32) {
     identity();
     return;
@@ -1426,9 +1496,12 @@ void build_structure_impl(Mesh& m, Structure& s)
         // (12 waves per CU with 15 slots); classes c < 8 get 8 positions, the others 7
         const char* bpm = variant("AFEM_BANK_PLACE_MAX");
         const int maxq = bpm ? std::max(64, std::min(256, atoi(bpm))) : 232;
+        // general slices too (AFEM_BANK_PLACE_GENERAL=0: their sorted order, diagnostic)
+        const char* bge = variant("AFEM_BANK_PLACE_GENERAL");
+        const int general = (bge && atoi(bge) == 0) ? 0 : 1;
         hipLaunchKernelGGL(k_bank_place, dim3((unsigned)s.n_slices), dim3(64), 0, ctx.stream, s.n_slices, uflag.p,
                            s.perm.p, s.snode_ptr.p, s.strip_u.p, s.strip_ptr.p, s.strip_n.p, s.pos_dl.p, q_of_u.p,
-                           nu_new.p, maxq);
+                           nu_new.p, maxq, general);
         AFEM_LAUNCHED();
         DevBuf<int64_t> ptr_new;
         ptr_new.alloc(s.n_slices + 1);

@@ -565,6 +565,35 @@ def test_canonical_lattice_random_numbering(ctx, variant, n, nz, seed):
     _check_values(v2, v1)
 
 
+def test_bank_place_general_slices_bitwise(ctx, variant):
+    """LDS-bank-aware placement of the GENERAL slices' node lists (a greedy
+    colouring of the positions mod 32 over the lanes that read them at each
+    step, sparsity.hip bank_place_general) on an unstructured mesh: only the
+    coordinate cache's layout changes, so the matrix and the RHS are bitwise
+    those of the sorted order (AFEM_BANK_PLACE_GENERAL=0), and the oracle's."""
+    import bench
+
+    gm = read_gmsh(path("L-shape-3D.msh"))
+    cells, coords = bench.refine_tets(gm.cells, gm.coords, 3, "cpu")  # 25.6 k nodes, 133 k tets
+    out = {}
+    for mode in ("0", "1"):
+        variant("AFEM_BANK_PLACE_GENERAL", mode)
+        mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
+        bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+        st = bsr.stats()
+        assert st["general_slices"] > 0 and st["brick_order"] == 0
+        out[mode] = (bsr.download(), ls.rhs_host(), st["max_slice_nodes"])
+    (r0, c0, v0), h0, _ = out["0"]
+    (r1, c1, v1), h1, _ = out["1"]
+    assert np.array_equal(r0, r1) and np.array_equal(c0, c1)
+    assert np.array_equal(v0, v1) and np.array_equal(h0, h1)
+    n = coords.shape[0]
+    orp, ocols = O.sparsity(n, n, cells)
+    ovals, orhs = O.assemble_poisson(n, cells, coords, orp, ocols, 5.5)
+    assert np.array_equal(r1, orp) and np.array_equal(c1, ocols)
+    _check_values(v1, ovals)
+
+
 def test_lattice_order_rejects_non_lattices(ctx):
     """Coordinates that are not a lattice (a Kuhn box whose node layers are
     warped beyond the gap rule, and one missing node) fall back to the
