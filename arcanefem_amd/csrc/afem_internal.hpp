@@ -222,6 +222,10 @@ struct Structure {
   // tile, higher occupancy), big = the rest
   DevBuf<SliceRec> rec_ms, rec_mb;
   int64_t n_ms = 0, n_mb = 0;
+  // the compact list's first n_msl slices have <= 256 nodes: the instance that
+  // reads each step's node from the local-index stream (UMODE 3) runs them
+  int64_t n_msl = 0;
+  int msl_nodes = 0;
   int ms_nodes = 0, mb_nodes = 0, mb_w = 0;
   int u_nodes = 0, u_w = 0;  // maxima over the uniform list (its LDS tile)
   // stencil split of the uniform list (scalar assembly): the slices of any

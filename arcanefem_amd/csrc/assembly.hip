@@ -664,11 +664,15 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
                                                           const SlotRec* __restrict__ uslots,
                                                           const uint8_t* __restrict__ cperm)
 {
-  constexpr bool UNI = UMODE != 0;  // 1: scalar shift/swap branches, 2: selects on the uniform bit
+  // 1: scalar shift/swap branches, 2: selects on the uniform bit; 3: general
+  // (per-lane) steps, but each step's node from the lane's local-index stream
+  // (strip_u, slices of <= 256 nodes) instead of the column-index table
+  constexpr bool UNI = UMODE == 1 || UMODE == 2;
   static_assert(!(PERM && UMODE == 1), "the slot map needs the select instance's register budget");
   // uniform tet instances address coordinates by the local-index stream (no
   // column-index table in LDS, no dependent LDS read per step)
-  constexpr bool ULOC = UNI && NV == 4;
+  constexpr bool ULOC = (UNI && NV == 4) || UMODE == 3;
+  constexpr bool USLOT = UNI && NV == 4;  // the slot bytes from the slice's common scalar stream
   constexpr int DIMC = NV == 4 ? 3 : 2;
   extern __shared__ __align__(16) unsigned char smem[];
   double* acc = reinterpret_cast<double*>(smem);
@@ -722,7 +726,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
   // uniform tet instances: the slot stream is common to the slice's rows (32
   // bytes per list position, scalar loads riding with the records)
   SlotRec S0{}, S1{}, S2{};
-  if constexpr (ULOC) {
+  if constexpr (USLOT) {
     S0 = uslots[p0];
     S1 = uslots[p1 < r1 ? p1 : p0];
     S2 = uslots[p2 < r1 ? p2 : p0];
@@ -740,7 +744,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
     p.rb = pos_rb[q];
     if constexpr (PERM) p.pq = reinterpret_cast<const u32x4*>(cperm)[q];
     const int nc = (int)((R.meta >> 24) + 15) >> 4;
-    if constexpr (!ULOC) {  // uniform instances read the slots from the scalar stream
+    if constexpr (!USLOT) {  // uniform instances read the slots from the scalar stream
       const u32x4* sp = reinterpret_cast<const u32x4*>(strip + (int64_t)R.strip_off * 1024) + lane;
 #pragma unroll
       for (int c = 0; c < MAXC; ++c) p.ch[c] = sp[(int64_t)max(min(c, nc - 1), 0) * 64];
@@ -783,7 +787,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
     const unsigned long long t4 = claim_issue();    // read at the end of this iteration
     const SliceRec R3 = recs[p3 < r1 ? p3 : p0];    // scalar load, used two iterations later
     SlotRec S3{};
-    if constexpr (ULOC) S3 = uslots[p3 < r1 ? p3 : p0];
+    if constexpr (USLOT) S3 = uslots[p3 < r1 ? p3 : p0];
     const int nsteps = (int)(R0.meta >> 24);  // uniform over the wave
     const int W = (int)((R0.meta >> 16) & 0xFFu);
     const int64_t u0 = R0.snode_off;
@@ -797,7 +801,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
       cxyz[DIMC * idx + 1] = cur.y[k];
       if (DIMC == 3) cxyz[DIMC * idx + 2] = cur.z[k];
     }
-    if (!UNI && nu > 256) {  // uniform slices: <= 256 nodes, <= 16 slots (k_strip_classify)
+    if (!ULOC && nu > 256) {  // uniform / UMODE 3 slices: <= 256 nodes, <= 16 slots
       for (int u = lane + 256; u < nu; u += 64) {
         const int64_t n = snode[u0 + u];
         cxyz[DIMC * u] = coords[3 * n];
@@ -812,7 +816,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
         dst[max(min(lane, nq - 1), 0)] = cur.l0;
         dst[max(min(lane + 64, nq - 1), 0)] = cur.l1;
       }
-      if (!UNI && nq > 128) {
+      if (!ULOC && nq > 128) {
         const u32x4* ls = reinterpret_cast<const u32x4*>(lidx + R0.lidx_off);
         for (int q = lane + 128; q < nq; q += 64) dst[q] = ls[q];
       }
@@ -903,7 +907,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
     // j+1 are issued before step j's arithmetic and accumulator adds (no
     // alias hazard: coordinates and indices are not written in the loop).
     auto byte_at = [&](int j) -> uint32_t {
-      if constexpr (ULOC) {  // scalar: the slice's common slot stream
+      if constexpr (USLOT) {  // scalar: the slice's common slot stream
         return (S0.w[(j >> 2) & 7] >> (8 * (j & 3))) & 0xFFu;
       }
       else {
@@ -983,13 +987,20 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
       }
     }
     else {
-      int u1 = lidx_of(byte_at(0));
+      // the node of step j: UMODE 3 from the local-index stream (registers), else
+      // through the column-index table in LDS (a dependent read, 2-way bank
+      // conflicts between the lane pairs sharing a dword)
+      auto node_at = [&](int j) -> int {
+        if constexpr (UMODE == 3) return uloc_at(j);
+        else return lidx_of(byte_at(j));
+      };
+      int u1 = node_at(0);
       V3 xc = coord(u1);
-      u1 = lidx_of(byte_at(1));
+      u1 = node_at(1);
 #pragma unroll
       for (int j = 0; j < NSTEP; ++j) {
         if ((j & 3) == 0 && j >= nsteps) break;
-        const int u2 = j + 2 < NSTEP ? lidx_of(byte_at(j + 2)) : 0;
+        const int u2 = j + 2 < NSTEP ? node_at(j + 2) : 0;
         const V3 xn = j + 1 < NSTEP ? coord(u1) : xc;
         step(byte_at(j), xc);
         xc = xn;
@@ -1080,7 +1091,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
     R0 = R1;
     R1 = R2;
     R2 = R3;
-    if constexpr (ULOC) {
+    if constexpr (USLOT) {
       S0 = S1;
       S1 = S2;
       S2 = S3;
@@ -2851,7 +2862,7 @@ int occ_override()
 // assemblies instead of a fill launch per assembly.  Every launch of an
 // assembly is joined to the context stream before the next one starts, so a
 // ring reset (stream-ordered) never races a running kernel.
-constexpr int64_t kTicketRing = 256, kTicketSlot = 4 * 8 * 16;
+constexpr int64_t kTicketRing = 256, kTicketSlot = 5 * 8 * 16;
 unsigned long long* next_tickets(Structure& s, Ctx& ctx)
 {
   if (s.tickets.n < kTicketRing * kTicketSlot) {
@@ -3010,9 +3021,20 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       AFEM_REQUIRE(s.n_mb == 0 || (mb_ok && s.max_strip_c <= 4), AFEM_ERR_STATE, "strip lists exceed the kernels");
       hipStream_t s_ms = has_u && !serial_k ? side : ctx.stream;
       hipStream_t s_mb = has_u && !serial_k ? side : (s.n_ms > 0 && !serial_k ? side : ctx.stream);
-      if (s.n_ms > 0)
-        launch_s(AFEM_SKF(4, 2, 16, 0), AFEM_SK(4, 2, 16, 0), s.n_ms,
-                 s.rec_ms.p, tk0 + 128, shm_ms, s_ms, s.ms_nodes, ms_w);
+      // the compact list: its slices of <= 256 nodes through the local-index-stream
+      // instance (UMODE 3: no column-index table, no dependent LDS read per step;
+      // AFEM_ASSEMBLY_LOCAL=0: all through UMODE 0, diagnostic; canonical
+      // structures: UMODE 0 with the slot map), the rest through UMODE 0
+      const char* le = variant("AFEM_ASSEMBLY_LOCAL");
+      const int64_t n_loc = (!(le && atoi(le) == 0) && !s.canon) ? s.n_msl : 0;
+      if (n_loc > 0) {
+        const size_t shm_l = (size_t)strip_tile_bytes(dimc, s.msl_nodes, ms_w);
+        launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 3>), k_assemble_strip<4, 2, 16, 3>, n_loc,
+                 s.rec_ms.p, tk0 + 512, shm_l, s_ms, s.msl_nodes, ms_w);
+      }
+      if (s.n_ms > n_loc)
+        launch_s(AFEM_SKF(4, 2, 16, 0), AFEM_SK(4, 2, 16, 0), s.n_ms - n_loc,
+                 s.rec_ms.p + n_loc, tk0 + 128, shm_ms, s_ms, s.ms_nodes, ms_w);
       if (s.n_mb > 0)
         launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 4, 32, 0>), k_assemble_strip<4, 4, 32, 0>, s.n_mb,
                  s.rec_mb.p, tk0 + 256, shm_mb, s_mb, s.mb_nodes, s.mb_w);

@@ -478,31 +478,38 @@ struct PatOff {
 };
 
 // 16 lanes per row (coalesced column reads; one thread per row: 18.7 ms at C4):
-// lane k compares column k with r + off[k]
+// lane k compares column k with r + off[k].  A grid-stride loop: one counter
+// atomic per wave at the end (an atomic per wave of 4 rows, 25 M at C4, took
+// 300 ms on the one address)
 __global__ __launch_bounds__(256) void k_pat_flags(int64_t n_rows, const int64_t* __restrict__ rows,
                                                    const int32_t* __restrict__ cols, PatOff po,
                                                    uint8_t* __restrict__ flag, unsigned long long* __restrict__ count)
 {
   const int l16 = threadIdx.x & 15;
-  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
   int32_t my_off = 0;  // off[l16] (a select chain: no dynamic index into the argument)
 #pragma unroll
   for (int k = 0; k < 16; ++k)
     if (k == l16) my_off = po.off[k];
-  bool bad = r >= n_rows;
-  if (!bad) {
-    const int64_t a = rows[r];
-    if (rows[r + 1] - a != po.len)
-      bad = true;
-    else if (l16 < po.len)
-      bad = (int64_t)cols[a + l16] != r + my_off;
+  const int g = (int)(threadIdx.x & 63) & ~15;  // this row group's 16 lanes in the wave
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x / 16;
+  unsigned long long n_ok = 0;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;; r += stride) {
+    // wave-uniform exit (lane 0 holds the wave's first row): the ballots below see all 64 lanes
+    if (__shfl(r, 0) >= n_rows) break;
+    bool bad = r >= n_rows;
+    if (!bad) {
+      const int64_t a = rows[r];
+      if (rows[r + 1] - a != po.len)
+        bad = true;
+      else if (l16 < po.len)
+        bad = (int64_t)cols[a + l16] != r + my_off;
+    }
+    const unsigned long long m = __ballot(bad);
+    const bool ok = ((m >> g) & 0xFFFFull) == 0;
+    if (l16 == 0 && r < n_rows) flag[r] = ok ? 1 : 0;
+    n_ok += __popcll(__ballot(l16 == 0 && r < n_rows && ok));
   }
-  const unsigned long long m = __ballot(bad);
-  const int g = (int)(threadIdx.x & 63) & ~15;  // this row's 16 lanes in the wave
-  const bool ok = ((m >> g) & 0xFFFFull) == 0;
-  if (l16 == 0 && r < n_rows) flag[r] = ok ? 1 : 0;
-  const unsigned long long rows_ok = __ballot(l16 == 0 && r < n_rows && ok);
-  if ((threadIdx.x & 63) == 0 && rows_ok) atomicAdd(count, (unsigned long long)__popcll(rows_ok));
+  if ((threadIdx.x & 63) == 0 && n_ok) atomicAdd(count, n_ok);
 }
 
 // k_spmv_stream4u with the block's column indices formed in LDS first: the
@@ -1499,8 +1506,9 @@ SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
       if (ls.pat_flag.n < (size_t)ls.n_rows) ls.pat_flag.alloc(ls.n_rows);
       if (!ls.pat_cnt.p) ls.pat_cnt.alloc(1);
       AFEM_HIP(hipMemsetAsync(ls.pat_cnt.p, 0, ls.pat_cnt.bytes(), ctx.stream));
-      hipLaunchKernelGGL(k_pat_flags, dim3(grid_for(16 * ls.n_rows, 256)), dim3(256), 0, ctx.stream, ls.n_rows,
-                         ls.csr_rows, ls.csr_cols, po, ls.pat_flag.p, ls.pat_cnt.p);
+      const unsigned pf_blocks = (unsigned)std::min<int64_t>(8 * 256 * 4, grid_for(16 * ls.n_rows, 256));
+      hipLaunchKernelGGL(k_pat_flags, dim3(pf_blocks), dim3(256), 0, ctx.stream, ls.n_rows, ls.csr_rows, ls.csr_cols,
+                         po, ls.pat_flag.p, ls.pat_cnt.p);
       AFEM_LAUNCHED();
       unsigned long long hc = 0;
       AFEM_HIP(hipMemcpyAsync(&hc, ls.pat_cnt.p, sizeof(hc), hipMemcpyDeviceToHost, ctx.stream));

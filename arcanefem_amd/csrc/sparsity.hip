@@ -1496,9 +1496,11 @@ void build_structure_impl(Mesh& m, Structure& s)
         // (12 waves per CU with 15 slots); classes c < 8 get 8 positions, the others 7
         const char* bpm = variant("AFEM_BANK_PLACE_MAX");
         const int maxq = bpm ? std::max(64, std::min(256, atoi(bpm))) : 232;
-        // general slices too (AFEM_BANK_PLACE_GENERAL=0: their sorted order, diagnostic)
+        // general slices too with AFEM_BANK_PLACE_GENERAL=1 (a greedy colouring;
+        // measured on the refined L-shape: SQ_LDS_BANK_CONFLICT -4 %, kernel +2 %
+        // (1.407 vs 1.380 ms, r04g) -- their conflicts are not the coordinate reads)
         const char* bge = variant("AFEM_BANK_PLACE_GENERAL");
-        const int general = (bge && atoi(bge) == 0) ? 0 : 1;
+        const int general = (bge && atoi(bge) == 1) ? 1 : 0;
         hipLaunchKernelGGL(k_bank_place, dim3((unsigned)s.n_slices), dim3(64), 0, ctx.stream, s.n_slices, uflag.p,
                            s.perm.p, s.snode_ptr.p, s.strip_u.p, s.strip_ptr.p, s.strip_n.p, s.pos_dl.p, q_of_u.p,
                            nu_new.p, maxq, general);
@@ -1575,6 +1577,22 @@ void build_structure_impl(Mesh& m, Structure& s)
                (int)(r.meta & 0xFFFFu) <= kSmallSliceNodes;
       };
       std::vector<SliceRec> ms_h;  // the compact general list, host copy (the stencil split may extend it)
+      // upload of the compact list, its slices of <= 256 nodes first (stable: each
+      // part keeps the processing order), n_msl of them
+      auto upload_ms = [&](std::vector<SliceRec>& h) {
+        std::stable_partition(h.begin(), h.end(), [](const SliceRec& r) { return (r.meta & 0xFFFFu) <= 256; });
+        s.n_msl = 0;
+        s.msl_nodes = 0;
+        for (const SliceRec& r : h)
+          if ((r.meta & 0xFFFFu) <= 256) {
+            ++s.n_msl;
+            s.msl_nodes = std::max(s.msl_nodes, (int)(r.meta & 0xFFFFu));
+          }
+        s.rec_ms.alloc(h.empty() ? 1 : h.size());
+        if (!h.empty())
+          AFEM_HIP(hipMemcpyAsync(s.rec_ms.p, h.data(), h.size() * sizeof(SliceRec), hipMemcpyHostToDevice, ctx.stream));
+        ctx.sync();  // h may change before the copy ran
+      };
       {
         // general-instance slices: the compact ones (<= 16 slots, <= 32 steps,
         // <= 352 nodes: 90 % of a Hilbert-ordered unstructured mesh) in their
@@ -1605,9 +1623,9 @@ void build_structure_impl(Mesh& m, Structure& s)
           if (!h.empty())
             AFEM_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(SliceRec), hipMemcpyHostToDevice, ctx.stream));
         };
-        up(s.rec_ms, ms);
-        up(s.rec_mb, mb);
         ms_h = std::move(ms);
+        upload_ms(ms_h);
+        up(s.rec_mb, mb);
       }
       auto upload = [&](DevBuf<SliceRec>& d, const std::vector<SliceRec>& h) {
         d.alloc(h.empty() ? 1 : h.size());
@@ -1661,7 +1679,7 @@ void build_structure_impl(Mesh& m, Structure& s)
             s.ms_nodes = std::max(s.ms_nodes, (int)(r.meta & 0xFFFFu));
           }
           s.n_ms = (int64_t)ms_h.size();
-          upload(s.rec_ms, ms_h);
+          upload_ms(ms_h);
           rur.clear();
           sur.clear();
           s.ur_nodes = s.ur_w = 0;

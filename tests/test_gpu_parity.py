@@ -565,33 +565,37 @@ def test_canonical_lattice_random_numbering(ctx, variant, n, nz, seed):
     _check_values(v2, v1)
 
 
-def test_bank_place_general_slices_bitwise(ctx, variant):
-    """LDS-bank-aware placement of the GENERAL slices' node lists (a greedy
-    colouring of the positions mod 32 over the lanes that read them at each
-    step, sparsity.hip bank_place_general) on an unstructured mesh: only the
-    coordinate cache's layout changes, so the matrix and the RHS are bitwise
-    those of the sorted order (AFEM_BANK_PLACE_GENERAL=0), and the oracle's."""
+@pytest.mark.parametrize("knob,value", [("AFEM_BANK_PLACE_GENERAL", "1"), ("AFEM_ASSEMBLY_LOCAL", "0")])
+def test_general_slice_variants_bitwise(ctx, variant, knob, value):
+    """Two layouts of the general (unstructured) slices that must not change a
+    bit: LDS-bank-aware placement of their node lists (a greedy colouring of
+    the positions mod 32 over the lanes that read them at each step,
+    sparsity.hip bank_place_general; opt-in) and the column-index table
+    instead of the local-index stream (AFEM_ASSEMBLY_LOCAL=0: the slices of
+    <= 256 nodes otherwise run k_assemble_strip<4,2,16,3>).  On an
+    unstructured mesh: the matrix and the RHS bitwise equal to the default's,
+    and the oracle's."""
     import bench
 
     gm = read_gmsh(path("L-shape-3D.msh"))
     cells, coords = bench.refine_tets(gm.cells, gm.coords, 3, "cpu")  # 25.6 k nodes, 133 k tets
     out = {}
-    for mode in ("0", "1"):
-        variant("AFEM_BANK_PLACE_GENERAL", mode)
+    for mode in ("default", "variant"):
+        variant(knob, value if mode == "variant" else None)
         mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
         bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
         st = bsr.stats()
         assert st["general_slices"] > 0 and st["brick_order"] == 0
-        out[mode] = (bsr.download(), ls.rhs_host(), st["max_slice_nodes"])
-    (r0, c0, v0), h0, _ = out["0"]
-    (r1, c1, v1), h1, _ = out["1"]
+        out[mode] = (bsr.download(), ls.rhs_host())
+    (r0, c0, v0), h0 = out["default"]
+    (r1, c1, v1), h1 = out["variant"]
     assert np.array_equal(r0, r1) and np.array_equal(c0, c1)
     assert np.array_equal(v0, v1) and np.array_equal(h0, h1)
     n = coords.shape[0]
     orp, ocols = O.sparsity(n, n, cells)
     ovals, orhs = O.assemble_poisson(n, cells, coords, orp, ocols, 5.5)
-    assert np.array_equal(r1, orp) and np.array_equal(c1, ocols)
-    _check_values(v1, ovals)
+    assert np.array_equal(r0, orp) and np.array_equal(c0, ocols)
+    _check_values(v0, ovals)
 
 
 def test_lattice_order_rejects_non_lattices(ctx):
