@@ -3021,12 +3021,14 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       AFEM_REQUIRE(s.n_mb == 0 || (mb_ok && s.max_strip_c <= 4), AFEM_ERR_STATE, "strip lists exceed the kernels");
       hipStream_t s_ms = has_u && !serial_k ? side : ctx.stream;
       hipStream_t s_mb = has_u && !serial_k ? side : (s.n_ms > 0 && !serial_k ? side : ctx.stream);
-      // the compact list: its slices of <= 256 nodes through the local-index-stream
-      // instance (UMODE 3: no column-index table, no dependent LDS read per step;
-      // AFEM_ASSEMBLY_LOCAL=0: all through UMODE 0, diagnostic; canonical
-      // structures: UMODE 0 with the slot map), the rest through UMODE 0
+      // AFEM_ASSEMBLY_LOCAL=1: the compact list's slices of <= 256 nodes through the
+      // local-index-stream instance (UMODE 3: no column-index table, no dependent
+      // LDS read per step), the rest through UMODE 0.  Measured on the refined
+      // L-shape (r04h): 1.458 vs 1.413 ms -- 43 % of its compact slices have more
+      // than 256 nodes, the two launches run one after the other, and the bank
+      // conflicts stay (4.0e7 + 6.0e7 cycles: not the column-index reads)
       const char* le = variant("AFEM_ASSEMBLY_LOCAL");
-      const int64_t n_loc = (!(le && atoi(le) == 0) && !s.canon) ? s.n_msl : 0;
+      const int64_t n_loc = (le && atoi(le) == 1 && !s.canon) ? s.n_msl : 0;
       if (n_loc > 0) {
         const size_t shm_l = (size_t)strip_tile_bytes(dimc, s.msl_nodes, ms_w);
         launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 2, 16, 3>), k_assemble_strip<4, 2, 16, 3>, n_loc,

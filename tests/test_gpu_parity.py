@@ -565,14 +565,14 @@ def test_canonical_lattice_random_numbering(ctx, variant, n, nz, seed):
     _check_values(v2, v1)
 
 
-@pytest.mark.parametrize("knob,value", [("AFEM_BANK_PLACE_GENERAL", "1"), ("AFEM_ASSEMBLY_LOCAL", "0")])
+@pytest.mark.parametrize("knob,value", [("AFEM_BANK_PLACE_GENERAL", "1"), ("AFEM_ASSEMBLY_LOCAL", "1")])
 def test_general_slice_variants_bitwise(ctx, variant, knob, value):
     """Two layouts of the general (unstructured) slices that must not change a
     bit: LDS-bank-aware placement of their node lists (a greedy colouring of
     the positions mod 32 over the lanes that read them at each step,
-    sparsity.hip bank_place_general; opt-in) and the column-index table
-    instead of the local-index stream (AFEM_ASSEMBLY_LOCAL=0: the slices of
-    <= 256 nodes otherwise run k_assemble_strip<4,2,16,3>).  On an
+    sparsity.hip bank_place_general; opt-in) and the local-index stream
+    instead of the column-index table (AFEM_ASSEMBLY_LOCAL=1: the slices of
+    <= 256 nodes through k_assemble_strip<4,2,16,3>; opt-in).  On an
     unstructured mesh: the matrix and the RHS bitwise equal to the default's,
     and the oracle's."""
     import bench
