@@ -409,12 +409,6 @@ struct LinearSystem {
   mutable DevBuf<uint8_t> pat_flag;  // rows whose columns follow the dominant offset pattern (pattern SpMV)
   mutable DevBuf<int32_t> pat_smp;   // the pattern detection's row samples
   mutable DevBuf<unsigned long long> pat_cnt;
-  // the pattern SpMV's tiled block order at large layer sizes (linear_system.hip
-  // plan_spmv_ls): row blocks by (in-layer tile, layer), and each launch
-  // position's partial-sum slot (the default order's, so the dot products keep
-  // their summation order)
-  mutable DevBuf<int32_t> pat_order, pat_pslot;
-  mutable uint64_t pat_order_key = 0;
   DevBuf<double> x0;      // the caller's initial guess (opts.initial_guess = 1)
   DevBuf<double> binv;    // block-Jacobi 3: inverse node blocks [n/3][9]
   DevBuf<int32_t> blist;  // multi-rank CG: SpMV row blocks, interior ones first
@@ -459,6 +453,8 @@ int64_t node_cell_adjacency(Ctx& ctx, const Mesh& m, int64_t n_rows, DevBuf<int6
 bool lattice_coords(Ctx& ctx, const Mesh& m, int64_t n_rows, DevBuf<int32_t> layer[3], int64_t L[3]);
 // rhs_add: 1 accumulate into rhs (applyConstantSourceToRhs), 0 overwrite
 void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add);
+// the cell-first cube kernel on generator boxes / slabs (cubes.hip); false: not applicable
+bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add);
 void assemble_elasticity_tri(Bsr& b, double lambda, double mu2);
 void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const double* f, double* rhs, int rhs_add);
 void apply_neumann(Mesh& m, int k, int mode, const double* v, int64_t n_faces, const int32_t* face_nodes,

@@ -2919,6 +2919,8 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   Ctx& ctx = *b.mesh->ctx;
   const int nv = b.mesh->nv;
   AFEM_REQUIRE(b.nb_dof == 1, AFEM_ERR_ARG, "assembleBilinear(P1 Laplacian) needs NB_DOF = 1");
+  // generator boxes / slabs: the cell-first cube kernel (cubes.hip)
+  if (assemble_cubes(b, coef, f, rhs, rhs_add)) return;
   const int dimc = nv == 4 ? 3 : 2;
   int bucket = -1;
   for (int i = 0; i < 4 && bucket < 0; ++i)

@@ -1,0 +1,381 @@
+// Scalar P1 (Poisson) assembly on the generator's Kuhn boxes, cell first:
+// k_assemble_cubes.
+//
+// The strip / stencil kernels (assembly.hip) are row first: each of a tet's 4
+// rows walks its cells and recomputes the tet's geometry (two cross products,
+// |det|, the reciprocal: ~50 FP64 operations per row-step, 24 steps per row).
+// Here each cube of the lattice is evaluated ONCE per unit: its 6 Kuhn tets
+// (mesh.hip c_kuhn: for each axis permutation (a0,a1,a2) the tet
+// (v0, v0+e_a0, v0+e_a0+e_a1, v0+(1,1,1))) give the cofactors, |det| and the 6
+// off-diagonal entries K_ab = coef c_a.c_b / (6|det|) once; the contributions
+// of the 6 tets to each of the cube's 19 Kuhn edges are summed in registers
+// and added to the two rows of the edge with ds_add_f64 (LDS, wave-local, in
+// program order: deterministic), the |det| sums of each corner likewise (the
+// RHS source f |det| / 24, fused).  ~600 VALU operations per cube against
+// ~1500 per row for the strip kernels.
+//
+// Unit = one wavefront: a column of 7 x 7 rows (node lines) over zs owned node
+// layers.  Lane (i, j) owns the cube with lower corner (cx0 - 1 + i,
+// cy0 - 1 + j): the 8 x 8 cubes touching the column's 7 x 7 rows, one per lane
+// (the halo cubes are evaluated by both neighbouring columns: 64/49 = 1.31
+// evaluations per cube, plus 1/zs for the cube layer below a segment).  The
+// unit walks the cube layers upwards: node layer z's rows take the cube layers
+// z-1 and z, so two row-layer accumulator buffers (by parity) live in LDS,
+// [16][64] doubles each (15 column offsets in sorted order + the |det| sum),
+// and the node coordinates of the two layers of the current cube layer
+// (9 x 9 nodes each, staged from registers loaded one layer ahead).  When a
+// node layer is complete its 49 rows are written once: the values compacted
+// by each row's present neighbours into a flat LDS image, then each x-run of
+// 7 rows (contiguous in the matrix) with consecutive lanes.
+//
+// Applies to meshes from afem_mesh_create_structured (3D, NB_DOF 1, any
+// z-slab: the columns follow the local numbering -- owned layers, then the
+// ghost layer below, then above -- so the sorted column order of a row next to
+// the ghost layer below is recovered from the layers' local indices).  Values
+// equal the oracle's to rounding (1e-12 per entry); not bitwise the strip
+// kernels' (another summation order).  AFEM_ASSEMBLY_CUBES=0: the strip /
+// stencil path.
+#include "afem_internal.hpp"
+
+#include <algorithm>
+
+namespace afem {
+
+namespace {
+
+inline unsigned grid_for(int64_t n, int threads) { return (unsigned)((n + threads - 1) / threads); }
+
+struct P3 {
+  double x, y, z;
+};
+__device__ __forceinline__ P3 psub(P3 a, P3 b) { return P3{ a.x - b.x, a.y - b.y, a.z - b.z }; }
+__device__ __forceinline__ P3 pcross(P3 a, P3 b)
+{
+  return P3{ fma(a.y, b.z, -(a.z * b.y)), fma(a.z, b.x, -(a.x * b.z)), fma(a.x, b.y, -(a.y * b.x)) };
+}
+__device__ __forceinline__ double pdot(P3 a, P3 b) { return fma(a.z, b.z, fma(a.y, b.y, a.x * b.x)); }
+__device__ __forceinline__ double precip(double a)
+{
+  const double r = __builtin_amdgcn_rcp(a);
+  const double e = fma(-a, r, 1.0);
+  return fma(r, e, r);
+}
+
+struct CubeGeom {
+  int np1;           // nodes per x / y line
+  int nzc;           // cells of the global box in z (node layers 0..nzc)
+  int k0, k1;        // owned node layers [k0, k1)
+  int ghost_lo, ghost_hi;
+  int n_own_layers;
+  int64_t L;         // nodes per layer
+  int tx, ty, zs, ns;
+  double s_coef;     // coef / 6
+  double f_meas;     // f / 24
+};
+
+// is global node layer k one of the slab's local layers (owned or ghost)?
+__device__ __forceinline__ bool is_local(const CubeGeom& g, int k)
+{
+  return (k >= g.k0 && k < g.k1) || (k >= 0 && (k == g.ghost_lo || k == g.ghost_hi));
+}
+// local layer index of global node layer k (mesh.hip Layers::local_layer)
+__device__ __forceinline__ int local_layer(const CubeGeom& g, int k)
+{
+  if (k >= g.k0 && k < g.k1) return k - g.k0;
+  if (k == g.ghost_lo) return g.n_own_layers;
+  return g.n_own_layers + (g.ghost_lo >= 0 ? 1 : 0);
+}
+
+// the 15 column offsets of a Kuhn row sorted by node id (x + np1 (y + np1 z)):
+// by dz, then dy, then dx
+__host__ __device__ constexpr int o_of(int dx, int dy, int dz)
+{
+  return dz < 0 ? (dy < 0 ? (dx < 0 ? 0 : 1) : (dx < 0 ? 2 : 3))
+                : dz == 0 ? (dy < 0 ? (dx < 0 ? 4 : 5) : dy == 0 ? (dx < 0 ? 6 : (dx == 0 ? 7 : 8)) : (dx == 0 ? 9 : 10))
+                          : (dy == 0 ? (dx == 0 ? 11 : 12) : (dx == 0 ? 13 : 14));
+}
+constexpr int kOffX[15] = { -1, 0, -1, 0, -1, 0, -1, 0, 1, 0, 1, 0, 1, 0, 1 };
+constexpr int kOffY[15] = { -1, -1, 0, 0, -1, -1, 0, 0, 0, 1, 1, 0, 0, 1, 1 };
+constexpr int kOffZ[15] = { -1, -1, -1, -1, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1 };
+
+// corners c = ci + 2 cj + 4 ck; tet t = (0, 1 << a0, (1 << a0) | (1 << a1), 7)
+constexpr int kPerm[6][2] = { { 0, 1 }, { 0, 2 }, { 1, 0 }, { 1, 2 }, { 2, 0 }, { 2, 1 } };
+__host__ __device__ constexpr int tet_v(int t, int k)
+{
+  return k == 0 ? 0 : k == 1 ? (1 << kPerm[t][0]) : k == 2 ? ((1 << kPerm[t][0]) | (1 << kPerm[t][1])) : 7;
+}
+__host__ __device__ constexpr int cbit(int c, int a) { return (c >> a) & 1; }
+// the row offset index of corner b seen from corner a
+__host__ __device__ constexpr int edge_o(int a, int b)
+{
+  return o_of(cbit(b, 0) - cbit(a, 0), cbit(b, 1) - cbit(a, 1), cbit(b, 2) - cbit(a, 2));
+}
+// is (a, b), a < b, an edge of one of the 6 tets?
+__host__ __device__ constexpr bool is_edge(int a, int b)
+{
+  bool e = false;
+  for (int t = 0; t < 6; ++t)
+    for (int p = 0; p < 4; ++p)
+      for (int q = 0; q < 4; ++q)
+        if (tet_v(t, p) == a && tet_v(t, q) == b) e = true;
+  return e;
+}
+
+constexpr int kRun = 7;    // rows per x-run of a column
+constexpr int kRows = 49;  // rows per column layer
+constexpr int kCol = 9;    // staged nodes per x / y line (the column's rows + 1 halo line below)
+constexpr int kAcc = 16;   // accumulators per row: 15 offsets + |det| sum
+
+__global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
+                                                       const double* __restrict__ coords,
+                                                       double* __restrict__ vals, double* __restrict__ rhs,
+                                                       int rhs_add)
+{
+  __shared__ __align__(16) double acc[2][kAcc][64];
+  __shared__ double cz[2][3][kCol * kCol];  // SoA coordinates of two node layers
+  const int lane = threadIdx.x;
+  // XCD-aware: blocks go round-robin over the 8 XCDs; XCD x takes the x-th
+  // contiguous eighth of the units (x fastest, then y, then segments)
+  const int64_t n_units = (int64_t)g.tx * g.ty * g.ns;
+  const int64_t bid = blockIdx.x;
+  const int64_t qq = n_units >> 3, rem = n_units & 7, xc = bid & 7, jj = bid >> 3;
+  const int64_t u = xc * qq + (xc < rem ? xc : rem) + jj;
+  const int utx = (int)(u % g.tx);
+  const int uty = (int)((u / g.tx) % g.ty);
+  const int seg = (int)(u / ((int64_t)g.tx * g.ty));
+  const int cx0 = kRun * utx, cy0 = kRun * uty;
+  const int z0 = g.k0 + seg * g.zs;
+  const int z1 = min(z0 + g.zs, g.k1);
+  const int zc_first = max(z0 - 1, 0);
+  const int zc_last = min(z1 - 1, g.nzc - 1);  // cube layer zc: node layers zc, zc + 1
+
+  // this lane's cube (i, j) and its staging share (nodes q = lane, lane + 64 of 81)
+  const int ci = lane & 7, cj = lane >> 3;
+  const int gx = cx0 - 1 + ci, gy = cy0 - 1 + cj;  // lower corner
+  const bool cube_in = gx >= 0 && gy >= 0 && gx + 1 < g.np1 && gy + 1 < g.np1;
+  auto node_xy = [&](int q, int& nx, int& ny) {
+    nx = cx0 - 1 + q % kCol;
+    ny = cy0 - 1 + q / kCol;
+  };
+  double pre[2][3];
+  auto load_layer = [&](int k) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = lane + 64 * h;
+      int nx, ny;
+      node_xy(q, nx, ny);
+      pre[h][0] = pre[h][1] = pre[h][2] = 0.0;
+      if (q < kCol * kCol && nx >= 0 && ny >= 0 && nx < g.np1 && ny < g.np1 && is_local(g, k)) {
+        const int64_t id = (int64_t)local_layer(g, k) * g.L + nx + (int64_t)g.np1 * ny;
+        pre[h][0] = coords[3 * id];
+        pre[h][1] = coords[3 * id + 1];
+        pre[h][2] = coords[3 * id + 2];
+      }
+    }
+  };
+  auto store_layer = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = lane + 64 * h;
+      if (q < kCol * kCol) {
+        cz[buf][0][q] = pre[h][0];
+        cz[buf][1][q] = pre[h][1];
+        cz[buf][2][q] = pre[h][2];
+      }
+    }
+  };
+  for (int i = lane; i < 2 * kAcc * 64; i += 64) (&acc[0][0][0])[i] = 0.0;
+
+  // ---- node layer z complete: write its 49 rows (values compacted by the present neighbours) + RHS
+  auto flush = [&](int z) {
+    const int b = z & 1;
+    const int rx = lane % kRun, ry = lane / kRun;
+    const int nx = cx0 + rx, ny = cy0 + ry;
+    const bool valid = lane < kRows && nx < g.np1 && ny < g.np1;
+    // present neighbours and the order of their local ids: the dz groups by local layer index
+    uint32_t mask = 0;
+#pragma unroll
+    for (int o = 0; o < 15; ++o) {
+      const int xx = nx + kOffX[o], yy = ny + kOffY[o], zz = z + kOffZ[o];
+      if (xx >= 0 && yy >= 0 && xx < g.np1 && yy < g.np1 && zz >= 0 && zz <= g.nzc) mask |= 1u << o;
+    }
+    if (!valid) mask = 0;
+    const uint32_t gm0 = mask & 0x000Fu, gm1 = mask & 0x07F0u, gm2 = mask & 0x7800u;
+    const int lm = local_layer(g, z - 1), l0 = local_layer(g, z), lp = local_layer(g, z + 1);
+    const int n0 = __popc(gm0), n1 = __popc(gm1), n2 = __popc(gm2);
+    const int s0 = (l0 < lm ? n1 : 0) + (lp < lm ? n2 : 0);
+    const int s1 = (lm < l0 ? n0 : 0) + (lp < l0 ? n2 : 0);
+    const int s2 = (lm < lp ? n0 : 0) + (l0 < lp ? n1 : 0);
+    double v[15];
+    double sum = 0.0;
+#pragma unroll
+    for (int o = 0; o < 15; ++o) {
+      v[o] = acc[b][o][lane];
+      if (o != 7 && ((mask >> o) & 1u)) sum += v[o];
+    }
+    v[7] = -sum;
+    const double meas = acc[b][15][lane];
+    int64_t r = 0, rb = 0;
+    int len = 0;
+    if (valid) {
+      r = (int64_t)local_layer(g, z) * g.L + nx + (int64_t)g.np1 * ny;
+      rb = rows[r];
+      len = (int)(rows[r + 1] - rb);
+      if (rhs) rhs[r] = rhs_add ? rhs[r] + g.f_meas * meas : g.f_meas * meas;
+    }
+    // prefix of the row lengths within the x-run (7 lanes), the runs' offsets in the image
+    int p = 0;
+#pragma unroll
+    for (int d = 1; d < kRun; ++d) {
+      const int t = __shfl(len, lane - d);
+      if (rx - d >= 0) p += t;
+    }
+    int img0 = 0;  // image offset of this lane's run
+#pragma unroll
+    for (int q = 0; q < kRun; ++q) {
+      const int rl = __shfl(p + len, kRun * q + kRun - 1);
+      if (q < ry) img0 += rl;
+    }
+    __syncthreads();  // every lane's accumulator reads before the image overwrites them
+    double* img = &acc[b][0][0];
+    if (valid) {
+#pragma unroll
+      for (int o = 0; o < 15; ++o)
+        if ((mask >> o) & 1u) {
+          const int grp = o < 4 ? 0 : (o < 11 ? 1 : 2);
+          const uint32_t gmask = grp == 0 ? gm0 : (grp == 1 ? gm1 : gm2);
+          const int start = grp == 0 ? s0 : (grp == 1 ? s1 : s2);
+          img[img0 + p + start + __popc(gmask & ((1u << o) - 1u))] = v[o];
+        }
+    }
+    __syncthreads();
+    // x-run q: run_len(q) values from image offset img(q) to vals + rb(first row of run q)
+    int off = 0;
+#pragma unroll
+    for (int q = 0; q < kRun; ++q) {
+      const int rl = __shfl(p + len, kRun * q + kRun - 1);
+      const int64_t dst = __shfl(rb, kRun * q);
+      for (int t = lane; t < rl; t += 64) vals[dst + t] = img[off + t];
+      off += rl;
+    }
+    __syncthreads();
+    for (int i = lane; i < kAcc * 64; i += 64) img[i] = 0.0;
+    __syncthreads();
+  };
+
+  // ---- cube layer zc: the lane's cube, its 6 tets, 19 edge sums and 8 corner |det| sums
+  auto cubes = [&](int zc) {
+    if (!cube_in) return;
+    const int bb = zc & 1, bt = (zc + 1) & 1;
+    P3 X[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int buf = cbit(c, 2) ? bt : bb;
+      const int q = (ci + cbit(c, 0)) + kCol * (cj + cbit(c, 1));
+      X[c] = P3{ cz[buf][0][q], cz[buf][1][q], cz[buf][2][q] };
+    }
+    double ev[8][8];
+    double mv[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      mv[a] = 0.0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) ev[a][b] = 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      const int v1 = tet_v(t, 1), v2 = tet_v(t, 2);
+      const P3 e1 = psub(X[v1], X[0]), e2 = psub(X[v2], X[0]), e3 = psub(X[7], X[0]);
+      P3 k[4];
+      k[1] = pcross(e2, e3);
+      k[2] = pcross(e3, e1);
+      k[3] = pcross(e1, e2);
+      k[0] = P3{ -(k[1].x + k[2].x + k[3].x), -(k[1].y + k[2].y + k[3].y), -(k[1].z + k[2].z + k[3].z) };
+      const double meas = fabs(pdot(e1, k[1]));
+      const double s = g.s_coef * precip(meas);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        mv[tet_v(t, p)] += meas;
+#pragma unroll
+        for (int q = p + 1; q < 4; ++q) {
+          const int a = tet_v(t, p) < tet_v(t, q) ? tet_v(t, p) : tet_v(t, q);
+          const int b = tet_v(t, p) < tet_v(t, q) ? tet_v(t, q) : tet_v(t, p);
+          ev[a][b] += s * pdot(k[p], k[q]);
+        }
+      }
+    }
+    // corners that are rows of this unit, and their accumulator rows
+    bool in[8];
+    double* base[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int rx = ci - 1 + cbit(c, 0), ry = cj - 1 + cbit(c, 1), z = zc + cbit(c, 2);
+      in[c] = rx >= 0 && ry >= 0 && rx < kRun && ry < kRun && cx0 + rx < g.np1 && cy0 + ry < g.np1 && z >= z0 &&
+              z < z1;
+      base[c] = &acc[cbit(c, 2) ? bt : bb][0][0] + (in[c] ? rx + kRun * ry : 0);
+    }
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = a + 1; b < 8; ++b)
+        if (is_edge(a, b)) {
+          if (in[a]) atomicAdd(base[a] + 64 * edge_o(a, b), ev[a][b]);
+          if (in[b]) atomicAdd(base[b] + 64 * edge_o(b, a), ev[a][b]);
+        }
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (in[c]) atomicAdd(base[c] + 64 * 15, mv[c]);
+  };
+
+  // ---- walk the cube layers upwards (coordinates staged one layer ahead)
+  load_layer(zc_first);
+  store_layer(zc_first & 1);
+  load_layer(zc_first + 1);
+  for (int zc = zc_first; zc <= zc_last; ++zc) {
+    store_layer((zc + 1) & 1);
+    load_layer(zc + 2);  // in flight during this layer's cubes
+    __syncthreads();
+    cubes(zc);
+    __syncthreads();
+    if (zc >= z0 && zc < z1) flush(zc);
+  }
+  if (zc_last + 1 >= z0 && zc_last + 1 < z1) flush(zc_last + 1);  // the box's top layer (no cube above)
+}
+
+}  // namespace
+
+bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
+{
+  const Mesh& m = *b.mesh;
+  const StructuredInfo& st = m.st;
+  const char* ce = variant("AFEM_ASSEMBLY_CUBES");
+  if ((ce && atoi(ce) == 0) || !st.valid || st.dim != 3 || m.nv != 4 || b.nb_dof != 1 || b.s.canon ||
+      st.lx > 0 || st.ly > 0 || st.n < 1)
+    return false;
+  Ctx& ctx = *m.ctx;
+  CubeGeom g{};
+  g.np1 = st.n + 1;
+  g.nzc = st.nz;
+  g.k0 = st.k0;
+  g.k1 = st.k1;
+  g.ghost_lo = st.ghost_lo;
+  g.ghost_hi = st.ghost_hi;
+  g.n_own_layers = st.k1 - st.k0;
+  g.L = st.L;
+  if (g.n_own_layers <= 0 || g.L != (int64_t)g.np1 * g.np1 || g.nzc < 1) return false;
+  g.tx = g.ty = (g.np1 + kRun - 1) / kRun;
+  const char* ze = variant("AFEM_CUBES_ZS");
+  g.zs = std::max(1, ze ? atoi(ze) : 16);
+  g.ns = (g.n_own_layers + g.zs - 1) / g.zs;
+  g.s_coef = coef / 6.0;
+  g.f_meas = f / 24.0;
+  const int64_t n_units = (int64_t)g.tx * g.ty * g.ns;
+  AFEM_REQUIRE(n_units < (int64_t(1) << 31), AFEM_ERR_LIMIT, "cube kernel: too many units");
+  hipLaunchKernelGGL(k_assemble_cubes, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, b.s.row_ptr.p,
+                     m.coords.p, b.values.p, rhs, rhs_add);
+  AFEM_LAUNCHED();
+  b.last_kernel = AFEM_KERNEL_CUBES;
+  return true;
+}
+
+}  // namespace afem

@@ -535,8 +535,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t n
                                                        const uint8_t* __restrict__ flag, PatOff po,
                                                        const double* __restrict__ x, double* __restrict__ y,
                                                        double* __restrict__ partial, int64_t max_seg,
-                                                       const int32_t* __restrict__ blist = nullptr,
-                                                       const int32_t* __restrict__ pslot = nullptr)
+                                                       const int32_t* __restrict__ blist = nullptr)
 {
   extern __shared__ __align__(16) unsigned char smem[];
   double* prod = reinterpret_cast<double*>(smem);
@@ -632,7 +631,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t n
   }
   if (DOT) {
     double bs = block_sum(d);
-    if (threadIdx.x == 0) partial[pslot ? pslot[blockIdx.x] : blockIdx.x] = bs;
+    if (threadIdx.x == 0) partial[blockIdx.x] = bs;
   }
 }
 
@@ -793,32 +792,34 @@ __global__ __launch_bounds__(1024) void k_reduce(int64_t n, const double* __rest
 // oracle/oracle.c::orc_pcg_jacobi).
 // 16 lanes per row: the row's columns and values are read coalesced (one
 // thread per row walked 15 entries 120 B apart from its neighbours': 20 ms per
-// solve at C4, 0.3 of the iteration time of 50 CG iterations), the diagonal
-// and the |off-diagonal| sum are 16-lane reductions
+// solve at C4), the diagonal and the |off-diagonal| sum are 16-lane
+// reductions; a grid-stride loop over rows (one wave per 4 rows: 25 M waves
+// at C4, 7 ms, the launch of that many waves rather than the 18 GB read)
 __global__ __launch_bounds__(256) void k_inv_diag(int64_t n_rows, const int64_t* __restrict__ rows,
                                                   const int32_t* __restrict__ cols, const double* __restrict__ vals,
                                                   double* __restrict__ dinv, uint8_t* __restrict__ cons)
 {
   const int l16 = threadIdx.x & 15;
-  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-  const int64_t rr = r < n_rows ? r : n_rows - 1;
-  const int64_t a = rows[rr], e = rows[rr + 1];
-  double d = 0.0, off = 0.0;
-  for (int64_t k = a + l16; k < e; k += 16) {
-    const double v = vals[k];
-    if (cols[k] == (int32_t)rr)
-      d += v;
-    else
-      off += fabs(v);
-  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x / 16;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; r < n_rows; r += stride) {
+    const int64_t a = rows[r], e = rows[r + 1];
+    double d = 0.0, off = 0.0;
+    for (int64_t k = a + l16; k < e; k += 16) {
+      const double v = vals[k];
+      if (cols[k] == (int32_t)r)
+        d += v;
+      else
+        off += fabs(v);
+    }
 #pragma unroll
-  for (int o = 8; o > 0; o >>= 1) {
-    d += __shfl_xor(d, o, 16);
-    off += __shfl_xor(off, o, 16);
-  }
-  if (l16 == 0 && r < n_rows) {
-    dinv[r] = (d != 0.0) ? 1.0 / d : 0.0;
-    cons[r] = fabs(d) > 1e10 * off ? 1 : 0;
+    for (int o = 8; o > 0; o >>= 1) {
+      d += __shfl_xor(d, o, 16);
+      off += __shfl_xor(off, o, 16);
+    }
+    if (l16 == 0) {
+      dinv[r] = (d != 0.0) ? 1.0 / d : 0.0;
+      cons[r] = fabs(d) > 1e10 * off ? 1 : 0;
+    }
   }
 }
 
@@ -1310,9 +1311,6 @@ struct SpmvPlan {
   // rpb = -3: k_spmv_pat (pattern rows form their columns)
   const uint8_t* pat_flag = nullptr;
   PatOff po{};
-  // its tiled block order (large layers) and the partial-sum slot of each launch position
-  const int32_t* order = nullptr;
-  const int32_t* pslot = nullptr;
 };
 
 __global__ void k_block_seg(int64_t n_rows, int rpb, const int64_t* __restrict__ row_ptr, unsigned long long* out)
@@ -1398,70 +1396,6 @@ void spmv_blk_epi(Ctx& ctx, int k, int epi, int64_t n_brows, const int64_t* bp, 
 
 namespace {
 
-// Tiled block order of the pattern SpMV.  A Kuhn box numbered lexicographically
-// has the interior offsets +-{1, Lx, Lx+1, L, L+1, L+Lx, L+Lx+1} (L = nodes per
-// layer): a row block reads x over three layers.  In block order each XCD's
-// blocks in flight need x of [r - L, r + L]: at C4 (L = 215 k nodes) 3.4 MB
-// per XCD beside the streamed values, more than its 4 MB L2 keeps, and x is
-// fetched from HBM 2-3 times (PMC: 16.2 GB per SpMV at C4 for 14.3 GB
-// algorithmic, r04d).  Here the blocks go by (tile of 16 lines within a layer,
-// layer, block): an XCD walks one tile up through the layers, so its x window
-// is 3 layers of one tile.  Only for layers above 64 k nodes (C2's 46.6 k fit
-// the L2: block order there).  Each launch position writes its partial dot
-// product into the slot the default (XCD-swizzled) order gives the same block,
-// so the reduction adds the same numbers in the same order: y and every CG
-// iterate stay bitwise equal to the untiled kernels (AFEM_SPMV_TILE=0: off).
-void pat_tile_order(Ctx& ctx, const LinearSystem& ls, SpmvPlan& pl)
-{
-  const char* te = variant("AFEM_SPMV_TILE");
-  if (te && atoi(te) == 0) return;
-  int64_t pos[16];
-  int np = 0;
-  for (int k = 0; k < pl.po.len; ++k)
-    if (pl.po.off[k] > 0) pos[np++] = pl.po.off[k];
-  if (np != 7) return;
-  std::sort(pos, pos + np);
-  const int64_t Lx = pos[1], L = pos[3];
-  if (!(pos[0] == 1 && pos[2] == Lx + 1 && pos[4] == L + 1 && pos[5] == L + Lx && pos[6] == L + Lx + 1)) return;
-  const int64_t tile_min = [] {
-    const char* e = variant("AFEM_SPMV_TILE_LAYER");
-    return e ? (int64_t)atoll(e) : (int64_t)65536;
-  }();
-  if (L < tile_min) return;
-  const int64_t n = ls.n_rows, nb = (n + kThreads - 1) / kThreads;
-  const uint64_t key = (uint64_t)n * 1000003u ^ (uint64_t)L * 7919u ^ (uint64_t)Lx;
-  if (ls.pat_order_key != key || ls.pat_order.n < (size_t)nb) {
-    const int64_t T = 16 * Lx;  // rows per tile
-    std::vector<std::pair<uint64_t, int32_t>> kb((size_t)nb);
-    for (int64_t b = 0; b < nb; ++b) {
-      const int64_t r0 = b * kThreads, z = r0 / L, w = (r0 - z * L) / T;
-      kb[(size_t)b] = { ((uint64_t)w << 40) | ((uint64_t)z << 20), (int32_t)b };
-    }
-    std::stable_sort(kb.begin(), kb.end(), [](const auto& a, const auto& c) { return a.first < c.first; });
-    // launch position i runs on XCD i % 8: each XCD a contiguous eighth of the order
-    std::vector<int32_t> order((size_t)nb), pslot((size_t)nb);
-    const int64_t q = nb >> 3, rem = nb & 7;
-    auto start = [&](int64_t x) { return x * q + (x < rem ? x : rem); };
-    for (int64_t i = 0; i < nb; ++i) {
-      const int64_t x = i & 7, j = i >> 3;
-      const int32_t blk = kb[(size_t)(start(x) + j)].second;
-      order[(size_t)i] = blk;
-      // the launch position of blk in the default order (inverse of xcd_swizzle)
-      int64_t bx = 7;
-      while (bx > 0 && start(bx) > blk) --bx;
-      pslot[(size_t)i] = (int32_t)((blk - start(bx)) * 8 + bx);
-    }
-    ls.pat_order.alloc(nb);
-    ls.pat_pslot.alloc(nb);
-    AFEM_HIP(hipMemcpyAsync(ls.pat_order.p, order.data(), (size_t)nb * 4, hipMemcpyHostToDevice, ctx.stream));
-    AFEM_HIP(hipMemcpyAsync(ls.pat_pslot.p, pslot.data(), (size_t)nb * 4, hipMemcpyHostToDevice, ctx.stream));
-    ctx.sync();  // the host vectors go out of scope
-    ls.pat_order_key = key;
-  }
-  pl.order = ls.pat_order.p;
-  pl.pslot = ls.pat_pslot.p;
-}
-
 // the node-block SpMV when the system came from a BSRFormat with NB_DOF 2 or 3
 // (AFEM_SPMV=csr or any other diagnostic mode keeps the scalar CSR kernels)
 SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
@@ -1517,7 +1451,6 @@ SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
         pl.rpb = -3;
         pl.po = po;
         pl.pat_flag = ls.pat_flag.p;
-        pat_tile_order(ctx, ls, pl);
         return pl;
       }
     }
@@ -1557,10 +1490,10 @@ void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* ro
     const size_t shm = (size_t)(8 * pl.max_seg + 32);
     if (partial)
       hipLaunchKernelGGL(k_spmv_pat<true>, dim3(nb), dim3(kThreads), shm, ctx.stream, n_rows, nnz, rows, cols, vals,
-                         pl.pat_flag, pl.po, x, y, partial, pl.max_seg, pl.order, pl.pslot);
+                         pl.pat_flag, pl.po, x, y, partial, pl.max_seg);
     else
       hipLaunchKernelGGL(k_spmv_pat<false>, dim3(nb), dim3(kThreads), shm, ctx.stream, n_rows, nnz, rows, cols, vals,
-                         pl.pat_flag, pl.po, x, y, partial, pl.max_seg, pl.order, pl.pslot);
+                         pl.pat_flag, pl.po, x, y, partial, pl.max_seg);
   }
   else if (pl.rpb < 0) {
     if (partial)
@@ -1824,7 +1757,8 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     hipLaunchKernelGGL(k_inv_diag_blk<2>, dim3(grid_for(16 * pl.blk_n, 256)), dim3(256), 0, ctx.stream, pl.blk_n,
                        pl.blk_rows, pl.blk_cols, ls.csr_vals, ls.dinv.p, ls.cons.p);
   else
-    hipLaunchKernelGGL(k_inv_diag, dim3(grid_for(16 * n, 256)), dim3(256), 0, ctx.stream, n, ls.csr_rows,
+    hipLaunchKernelGGL(k_inv_diag, dim3((unsigned)std::min<int64_t>(8 * 256 * 8, grid_for(16 * n, 256))), dim3(256), 0,
+                       ctx.stream, n, ls.csr_rows,
                        ls.csr_cols, ls.csr_vals, ls.dinv.p, ls.cons.p);
   AFEM_LAUNCHED();
   const bool blk3 = ls.opts.precond_block == 3;

@@ -255,6 +255,7 @@ typedef struct afem_bsr_stats {
 #define AFEM_KERNEL_ELAST2 7         /* block-2 triangle kernel */
 #define AFEM_KERNEL_ELAST3_WG 8      /* block-3 persistent strip kernel, one 3-wave workgroup per slice */
 #define AFEM_KERNEL_ELAST3_BIG 9     /* block-3 persistent strip kernel for unstructured meshes (rows <= 32) */
+#define AFEM_KERNEL_CUBES 10         /* scalar cell-first cube kernel (generator Kuhn boxes and slabs) */
 int afem_bsr_get_stats(afem_bsr* bsr, afem_bsr_stats* stats);
 /* Copies the scalar CSR expansion to host in the reference's CSRFormatView
  * layout (BSRMatrix::toCsr, femutils/BSRFormat.h:194-256): rows[n] without

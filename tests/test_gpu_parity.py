@@ -117,7 +117,63 @@ def test_assembly_bitwise_reproducible(ctx):
         assert np.array_equal(r1, ls.rhs_host())
 
 
+@pytest.mark.parametrize("n,nz,zs", [(1, 1, None), (2, 5, None), (6, 6, None), (7, 3, 2), (8, 9, 1), (13, 20, 3),
+                                     (20, 7, None)])
+def test_cube_kernel_matches_oracle(ctx, variant, n, nz, zs):
+    """The cell-first cube kernel (cubes.hip, the default on generator boxes):
+    boxes whose line lengths are and are not multiples of the 7-row columns,
+    thin boxes, and z segments of 1-3 layers (AFEM_CUBES_ZS): values and RHS
+    against the oracle (1e-12 per entry) and against the row-strip kernels
+    (AFEM_ASSEMBLY_CUBES=0, the same to rounding); RHS added and set; and
+    bitwise run-to-run."""
+    if zs is not None:
+        variant("AFEM_CUBES_ZS", str(zs))
+    mesh = af.Mesh.structured(ctx, 3, n, nz, jitter=0.2, seed=31)
+    bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
+    assert bsr.stats()["last_kernel"] == 10  # AFEM_KERNEL_CUBES
+    rows, cols, vals = bsr.download()
+    rhs = ls.rhs_host()
+    cells, coords, _ = mesh.download()
+    orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+    ovals, orhs = O.assemble_poisson(mesh.n_own_nodes, cells, coords, orp, ocols, 5.5)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    _check_values(vals, ovals)
+    assert np.abs(rhs - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+    # RHS add mode on top, and the set mode again: reproducible bits
+    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="add")
+    assert np.array_equal(ls.rhs_host(), rhs + rhs)
+    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
+    assert np.array_equal(bsr.download()[2], vals) and np.array_equal(ls.rhs_host(), rhs)
+    variant("AFEM_ASSEMBLY_CUBES", "0")
+    bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable(), rhs_mode="set")
+    assert bsr.stats()["last_kernel"] != 10
+    v_strip = bsr.download()[2]
+    assert np.abs(vals - v_strip).max() <= VAL_TOL * np.abs(v_strip).max()
+    assert np.abs(ls.rhs_host() - rhs).max() <= VAL_TOL * np.abs(rhs).max()
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_cube_kernel_on_slabs(ctx, nranks):
+    """z-slab subdomains (owned layers, then the ghost layer below, then the one
+    above: a row next to the ghost layer below has its -z columns LAST in id
+    order): every slab's matrix and RHS against the oracle on the same
+    subdomain, through the cube kernel."""
+    for rank in range(nranks):
+        mesh = af.Mesh.structured(ctx, 3, 9, nz=11, jitter=0.2, seed=13, nranks=nranks, rank=rank)
+        bsr, ls = _assemble_gpu(ctx, mesh, 2.5)
+        assert bsr.stats()["last_kernel"] == 10
+        rows, cols, vals = bsr.download()
+        cells, coords, _ = mesh.download()
+        orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+        ovals, orhs = O.assemble_poisson(mesh.n_own_nodes, cells, coords, orp, ocols, 2.5)
+        assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+        _check_values(vals, ovals)
+        assert np.abs(ls.rhs_host() - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+        mesh.close()
+
+
 def test_uniform_strip_variant(ctx, variant):
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     # interior 4x4x4 bricks of a structured box share one strip topology and
     # run the uniform-control kernel; it must give the general kernel's bits
     # and match the oracle
@@ -148,6 +204,7 @@ def test_stencil_instance_bitwise(ctx, variant, n):
     (stencil_sigs.inc) and run k_assemble_stencil (register accumulators): the
     same bits as the uniform instance (AFEM_ASSEMBLY_STENCIL=0) and the general
     instance (AFEM_ASSEMBLY_UNIFORM=0), and the oracle's values."""
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=7)
     bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
     st = bsr.stats()
@@ -179,6 +236,7 @@ def test_edge_slices_folded_into_general_list(ctx, variant):
     signature; beside enough stencil slices they join the compact general list
     (one launch before the stencil kernel).  Same bits as keeping them on the
     uniform instance (AFEM_ASSEMBLY_FOLD=0) and as the general instance."""
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     mesh = af.Mesh.structured(ctx, 3, 100, jitter=0.2, seed=5)
     bsr, ls = _assemble_gpu(ctx, mesh, 3.0)
     st = bsr.stats()
@@ -500,11 +558,12 @@ def test_random_node_permutation(ctx, variant, dim, n, order):
 
 
 @pytest.mark.parametrize("n,nz,jitter", [(9, 9, 0.2), (14, 5, 0.0), (5, 23, 0.19)])
-def test_lattice_order_matches_generator_box(ctx, n, nz, jitter):
+def test_lattice_order_matches_generator_box(ctx, variant, n, nz, jitter):
     """A generator box handed over as plain arrays in its own numbering: the
     recovered lattice gives the generator's brick order, the same stencil /
     uniform slice lists and bitwise the same matrix and RHS as the box made by
     afem_mesh_create_structured (unjittered and non-cubic boxes included)."""
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     m0 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=jitter, seed=5)
     b0, l0 = _assemble_gpu(ctx, m0, 5.5)
     cells, coords, _ = m0.download()
@@ -530,6 +589,7 @@ def test_canonical_lattice_random_numbering(ctx, variant, n, nz, seed):
     the per-row slot map.  The matrix is bitwise the generator's, permuted
     (A1[p[i], p[j]] == A0[i, j]), and so is the RHS.  AFEM_CANON=0 (no
     relabeling: the general instance) stays within the oracle tolerance."""
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     m0 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=seed)
     b0, l0 = _assemble_gpu(ctx, m0, 5.5)
     cells0, coords0, _ = m0.download()
@@ -730,17 +790,11 @@ def test_initial_guess_current_solution(ctx):
 
 
 @pytest.mark.parametrize("n", [9, 30])
-@pytest.mark.parametrize("tile", [False, True])
-def test_pattern_spmv(ctx, variant, n, tile):
+def test_pattern_spmv(ctx, variant, n):
     """The pattern-compressed SpMV (interior rows of a Kuhn box form their
     columns as row + the offsets of the interior stencil, the others read
     theirs, into the block's LDS column image): the same products in the same
-    order as the CSR-stream kernel (bitwise equal y), and the same CG solve.
-    tile: the row blocks in the tiled (in-layer tile, layer) order large
-    layers get (forced here by a 1-node layer threshold), partial dot products
-    in the default order's slots -- still bitwise equal."""
-    if tile:
-        variant("AFEM_SPMV_TILE_LAYER", "1")
+    order as the CSR-stream kernel (bitwise equal y), and the same CG solve."""
     mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=5)
     bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
     bottom = mesh.bottom_nodes()
