@@ -157,47 +157,60 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
     nx = cx0 - 1 + q % kCol;
     ny = cy0 - 1 + q / kCol;
   };
+  // staging loads without branches (addresses clamped into the local mesh,
+  // out-of-range positions hold a duplicate that no cube reads): straight-line
+  // code, so the waits on them count past the later memory operations instead
+  // of draining everything (vmcnt(0)) at a branch join
   double pre[2][3];
   auto load_layer = [&](int k) {
+    const int kk = is_local(g, k) ? k : g.k0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int q = lane + 64 * h;
+      const int q = min(lane + 64 * h, kCol * kCol - 1);
       int nx, ny;
       node_xy(q, nx, ny);
-      pre[h][0] = pre[h][1] = pre[h][2] = 0.0;
-      if (q < kCol * kCol && nx >= 0 && ny >= 0 && nx < g.np1 && ny < g.np1 && is_local(g, k)) {
-        const int64_t id = (int64_t)local_layer(g, k) * g.L + nx + (int64_t)g.np1 * ny;
-        pre[h][0] = coords[3 * id];
-        pre[h][1] = coords[3 * id + 1];
-        pre[h][2] = coords[3 * id + 2];
-      }
+      nx = min(max(nx, 0), g.np1 - 1);
+      ny = min(max(ny, 0), g.np1 - 1);
+      const int64_t id = (int64_t)local_layer(g, kk) * g.L + nx + (int64_t)g.np1 * ny;
+      pre[h][0] = coords[3 * id];
+      pre[h][1] = coords[3 * id + 1];
+      pre[h][2] = coords[3 * id + 2];
     }
   };
   auto store_layer = [&](int buf) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int q = lane + 64 * h;
-      if (q < kCol * kCol) {
-        cz[buf][0][q] = pre[h][0];
-        cz[buf][1][q] = pre[h][1];
-        cz[buf][2][q] = pre[h][2];
-      }
+      const int q = min(lane + 64 * h, kCol * kCol - 1);  // lanes past the 81 nodes repeat node 80's store
+      cz[buf][0][q] = pre[h][0];
+      cz[buf][1][q] = pre[h][1];
+      cz[buf][2][q] = pre[h][2];
     }
   };
   for (int i = lane; i < 2 * kAcc * 64; i += 64) (&acc[0][0][0])[i] = 0.0;
 
-  // ---- node layer z complete: write its 49 rows (values compacted by the present neighbours) + RHS
+  // ---- node layer z complete: write its 49 rows (values compacted by the present neighbours) + RHS.
+  // The rows' offsets are loaded before the layer's cubes (prefetch_rows), so
+  // their latency hides behind the cube arithmetic instead of stalling here.
+  const int rx = lane % kRun, ry = lane / kRun;
+  const int nx = cx0 + rx, ny = cy0 + ry;
+  int64_t pf_rb = 0, pf_re = 0;
+  auto prefetch_rows = [&](int z) {  // clamped like load_layer: no branch
+    const int zz = (z >= z0 && z < z1) ? z : z0;
+    const int64_t r = (int64_t)local_layer(g, zz) * g.L + min(nx, g.np1 - 1) + (int64_t)g.np1 * min(ny, g.np1 - 1);
+    pf_rb = rows[r];
+    pf_re = rows[r + 1];
+  };
   auto flush = [&](int z) {
     const int b = z & 1;
-    const int rx = lane % kRun, ry = lane / kRun;
-    const int nx = cx0 + rx, ny = cy0 + ry;
     const bool valid = lane < kRows && nx < g.np1 && ny < g.np1;
     // present neighbours and the order of their local ids: the dz groups by local layer index
     uint32_t mask = 0;
 #pragma unroll
-    for (int o = 0; o < 15; ++o) {
+    for (int o = 0; o < 15; ++o) {  // branch-free (bitwise ands of the comparisons)
       const int xx = nx + kOffX[o], yy = ny + kOffY[o], zz = z + kOffZ[o];
-      if (xx >= 0 && yy >= 0 && xx < g.np1 && yy < g.np1 && zz >= 0 && zz <= g.nzc) mask |= 1u << o;
+      const uint32_t in = (uint32_t)(xx >= 0) & (uint32_t)(yy >= 0) & (uint32_t)(xx < g.np1) & (uint32_t)(yy < g.np1) &
+                          (uint32_t)(zz >= 0) & (uint32_t)(zz <= g.nzc);
+      mask |= in << o;
     }
     if (!valid) mask = 0;
     const uint32_t gm0 = mask & 0x000Fu, gm1 = mask & 0x07F0u, gm2 = mask & 0x7800u;
@@ -219,8 +232,8 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
     int len = 0;
     if (valid) {
       r = (int64_t)local_layer(g, z) * g.L + nx + (int64_t)g.np1 * ny;
-      rb = rows[r];
-      len = (int)(rows[r + 1] - rb);
+      rb = pf_rb;
+      len = (int)(pf_re - pf_rb);
       if (rhs) rhs[r] = rhs_add ? rhs[r] + g.f_meas * meas : g.f_meas * meas;
     }
     // prefix of the row lengths within the x-run (7 lanes), the runs' offsets in the image
@@ -255,7 +268,13 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
     for (int q = 0; q < kRun; ++q) {
       const int rl = __shfl(p + len, kRun * q + kRun - 1);
       const int64_t dst = __shfl(rb, kRun * q);
-      for (int t = lane; t < rl; t += 64) vals[dst + t] = img[off + t];
+      // a fixed count of (predicated) stores: the next layer's waits on its
+      // coordinate loads can count past them instead of draining every store
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // rl <= 7 rows x 15 = 105
+        const int t = lane + 64 * h;
+        if (t < rl) vals[dst + t] = img[off + t];
+      }
       off += rl;
     }
     __syncthreads();
@@ -334,12 +353,16 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
   for (int zc = zc_first; zc <= zc_last; ++zc) {
     store_layer((zc + 1) & 1);
     load_layer(zc + 2);  // in flight during this layer's cubes
+    prefetch_rows(zc);   // the offsets of the rows this iteration completes
     __syncthreads();
     cubes(zc);
     __syncthreads();
     if (zc >= z0 && zc < z1) flush(zc);
   }
-  if (zc_last + 1 >= z0 && zc_last + 1 < z1) flush(zc_last + 1);  // the box's top layer (no cube above)
+  if (zc_last + 1 >= z0 && zc_last + 1 < z1) {  // the box's top layer (no cube above)
+    prefetch_rows(zc_last + 1);
+    flush(zc_last + 1);
+  }
 }
 
 }  // namespace
