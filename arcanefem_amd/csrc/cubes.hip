@@ -323,27 +323,25 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
         }
       }
     }
-    // corners that are rows of this unit, and their accumulator rows
-    bool in[8];
-    double* base[8];
+    // the accumulator row of each corner: a row of this unit, else a sink row
+    // (rows 49..63 of the buffer, never flushed; spread over 15 of them so the
+    // sinks' same-address collisions stay few): every add runs unpredicated
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const int rx = ci - 1 + cbit(c, 0), ry = cj - 1 + cbit(c, 1), z = zc + cbit(c, 2);
-      in[c] = rx >= 0 && ry >= 0 && rx < kRun && ry < kRun && cx0 + rx < g.np1 && cy0 + ry < g.np1 && z >= z0 &&
-              z < z1;
-      base[c] = &acc[cbit(c, 2) ? bt : bb][0][0] + (in[c] ? rx + kRun * ry : 0);
+      const bool in = (uint32_t)(rx >= 0) & (uint32_t)(ry >= 0) & (uint32_t)(rx < kRun) & (uint32_t)(ry < kRun) &
+                      (uint32_t)(cx0 + rx < g.np1) & (uint32_t)(cy0 + ry < g.np1) & (uint32_t)(z >= z0) &
+                      (uint32_t)(z < z1);
+      const int row = in ? rx + kRun * ry : kRows + (lane % (64 - kRows));
+      double* const base = &acc[cbit(c, 2) ? bt : bb][0][0] + row;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (b == c) continue;
+        const int lo = c < b ? c : b, hi = c < b ? b : c;
+        if (is_edge(lo, hi)) atomicAdd(base + 64 * edge_o(c, b), ev[lo][hi]);
+      }
+      atomicAdd(base + 64 * 15, mv[c]);
     }
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = a + 1; b < 8; ++b)
-        if (is_edge(a, b)) {
-          if (in[a]) atomicAdd(base[a] + 64 * edge_o(a, b), ev[a][b]);
-          if (in[b]) atomicAdd(base[b] + 64 * edge_o(b, a), ev[a][b]);
-        }
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-      if (in[c]) atomicAdd(base[c] + 64 * 15, mv[c]);
   };
 
   // ---- walk the cube layers upwards (coordinates staged one layer ahead)
