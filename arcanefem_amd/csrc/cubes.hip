@@ -125,13 +125,15 @@ constexpr int kRun = 7;    // rows per x-run of a column
 constexpr int kRows = 49;  // rows per column layer
 constexpr int kCol = 9;    // staged nodes per x / y line (the column's rows + 1 halo line below)
 constexpr int kAcc = 16;   // accumulators per row: 15 offsets + |det| sum
+constexpr int kSink = 3;   // sink rows after the 49 (corners outside the unit)
+constexpr int kStride = kRows + kSink;  // accumulator rows per offset (52: 13.3 KB for both buffers)
 
 __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
                                                        const double* __restrict__ coords,
                                                        double* __restrict__ vals, double* __restrict__ rhs,
                                                        int rhs_add)
 {
-  __shared__ __align__(16) double acc[2][kAcc][64];
+  __shared__ __align__(16) double acc[2][kAcc][kStride];
   __shared__ double cz[2][3][kCol * kCol];  // SoA coordinates of two node layers
   const int lane = threadIdx.x;
   // XCD-aware: blocks go round-robin over the 8 XCDs; XCD x takes the x-th
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
       cz[buf][2][q] = pre[h][2];
     }
   };
-  for (int i = lane; i < 2 * kAcc * 64; i += 64) (&acc[0][0][0])[i] = 0.0;
+  for (int i = lane; i < 2 * kAcc * kStride; i += 64) (&acc[0][0][0])[i] = 0.0;
 
   // ---- node layer z complete: write its 49 rows (values compacted by the present neighbours) + RHS.
   // The rows' offsets are loaded before the layer's cubes (prefetch_rows), so
@@ -221,13 +223,14 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
     const int s2 = (lm < lp ? n0 : 0) + (l0 < lp ? n1 : 0);
     double v[15];
     double sum = 0.0;
+    const int lr = min(lane, kStride - 1);
 #pragma unroll
     for (int o = 0; o < 15; ++o) {
-      v[o] = acc[b][o][lane];
+      v[o] = acc[b][o][lr];
       if (o != 7 && ((mask >> o) & 1u)) sum += v[o];
     }
     v[7] = -sum;
-    const double meas = acc[b][15][lane];
+    const double meas = acc[b][15][lr];
     int64_t r = 0, rb = 0;
     int len = 0;
     if (valid) {
@@ -278,8 +281,9 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
       off += rl;
     }
     __syncthreads();
-    for (int i = lane; i < kAcc * 64; i += 64) img[i] = 0.0;
-    __syncthreads();
+    // zero the buffer for node layer z + 2 (the loop's next barrier orders this
+    // before any add into it)
+    for (int i = lane; i < kAcc * kStride; i += 64) img[i] = 0.0;
   };
 
   // ---- cube layer zc: the lane's cube, its 6 tets, 19 edge sums and 8 corner |det| sums
@@ -332,15 +336,15 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
       const bool in = (uint32_t)(rx >= 0) & (uint32_t)(ry >= 0) & (uint32_t)(rx < kRun) & (uint32_t)(ry < kRun) &
                       (uint32_t)(cx0 + rx < g.np1) & (uint32_t)(cy0 + ry < g.np1) & (uint32_t)(z >= z0) &
                       (uint32_t)(z < z1);
-      const int row = in ? rx + kRun * ry : kRows + (lane % (64 - kRows));
+      const int row = in ? rx + kRun * ry : kRows + (lane % kSink);
       double* const base = &acc[cbit(c, 2) ? bt : bb][0][0] + row;
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
         if (b == c) continue;
         const int lo = c < b ? c : b, hi = c < b ? b : c;
-        if (is_edge(lo, hi)) atomicAdd(base + 64 * edge_o(c, b), ev[lo][hi]);
+        if (is_edge(lo, hi)) atomicAdd(base + kStride * edge_o(c, b), ev[lo][hi]);
       }
-      atomicAdd(base + 64 * 15, mv[c]);
+      atomicAdd(base + kStride * 15, mv[c]);
     }
   };
 
