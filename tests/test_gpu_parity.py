@@ -126,6 +126,7 @@ def test_cube_kernel_matches_oracle(ctx, variant, n, nz, zs):
     against the oracle (1e-12 per entry) and against the row-strip kernels
     (AFEM_ASSEMBLY_CUBES=0, the same to rounding); RHS added and set; and
     bitwise run-to-run."""
+    variant("AFEM_ASSEMBLY_CUBES", "1")  # opt-in
     if zs is not None:
         variant("AFEM_CUBES_ZS", str(zs))
     mesh = af.Mesh.structured(ctx, 3, n, nz, jitter=0.2, seed=31)
@@ -153,11 +154,12 @@ def test_cube_kernel_matches_oracle(ctx, variant, n, nz, zs):
 
 
 @pytest.mark.parametrize("nranks", [2, 3])
-def test_cube_kernel_on_slabs(ctx, nranks):
+def test_cube_kernel_on_slabs(ctx, variant, nranks):
     """z-slab subdomains (owned layers, then the ghost layer below, then the one
     above: a row next to the ghost layer below has its -z columns LAST in id
     order): every slab's matrix and RHS against the oracle on the same
     subdomain, through the cube kernel."""
+    variant("AFEM_ASSEMBLY_CUBES", "1")  # opt-in
     for rank in range(nranks):
         mesh = af.Mesh.structured(ctx, 3, 9, nz=11, jitter=0.2, seed=13, nranks=nranks, rank=rank)
         bsr, ls = _assemble_gpu(ctx, mesh, 2.5)
