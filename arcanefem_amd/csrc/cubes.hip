@@ -21,7 +21,8 @@
 // evaluations per cube, plus 1/zs for the cube layer below a segment).  The
 // unit walks the cube layers upwards: node layer z's rows take the cube layers
 // z-1 and z, so two row-layer accumulator buffers (by parity) live in LDS,
-// [16][64] doubles each (15 column offsets in sorted order + the |det| sum),
+// [16][52] doubles each (15 column offsets in sorted order + the |det| sum;
+// 49 rows + 3 sink rows taking the adds of corners outside the unit),
 // and the node coordinates of the two layers of the current cube layer
 // (9 x 9 nodes each, staged from registers loaded one layer ahead).  When a
 // node layer is complete its 49 rows are written once: the values compacted
