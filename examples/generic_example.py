@@ -25,6 +25,8 @@ def load():
         L.gx_assemble.restype = ctypes.c_int
         L.gx_assemble.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                   ctypes.c_double]
+        L.gx_assemble_unrolled.restype = ctypes.c_int
+        L.gx_assemble_unrolled.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -37,3 +39,13 @@ def assemble(bsr, kind=POISSON, path=UNITS, overwrite=False, lam=0.0, mu=0.0):
     if rc != 0:
         L = _capi.load()
         raise _capi.AfemError(rc, "gx_assemble", L.afem_last_error().decode(errors="replace"))
+
+
+def assemble_unrolled(bsr, kind, un, overwrite=False):
+    """The cell-unit kernel with un (1-4) functor evaluations in flight per
+    lane (tet4 Poisson kinds only): the A/B of assemble_bilinear's default."""
+    from arcanefem_amd import _capi
+    rc = load().gx_assemble_unrolled(bsr.h, kind, un, 1 if overwrite else 0)
+    if rc != 0:
+        L = _capi.load()
+        raise _capi.AfemError(rc, "gx_assemble_unrolled", L.afem_last_error().decode(errors="replace"))

@@ -155,8 +155,16 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
 }
 
 /* One wavefront per unit (blockDim 64); dynamic LDS: nbuf * width * K^2 *
- * rows_per_layer doubles, layout [buffer][slot*K^2 + i*K + j][lane]. */
-template <int NV, int K, bool WIDE, class F>
+ * rows_per_layer doubles, layout [buffer][slot*K^2 + i*K + j][lane].
+ *
+ * UN functor evaluations per lane are in flight at once (entries e, e + 64,
+ * ..., e + 64 (UN-1) of the stage): the UN cells' connectivity and coordinate
+ * gathers issue together before any element is scattered, so a wave waits for
+ * one chain of dependent loads per UN cells (the kernel is load-latency bound:
+ * 16 KB of LDS per unit leave 2-3 waves per SIMD).  The scatter order stays
+ * the one-cell-at-a-time order (entry e's adds, then e + 64's, ...): the same
+ * bits for every UN. */
+template <int NV, int K, bool WIDE, int UN, class F>
 __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f, int overwrite)
 {
   extern __shared__ __align__(16) double acc[];
@@ -172,70 +180,91 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
   const int bufsz = p.width * KK * RL;
   for (int i = lane; i < p.nbuf * bufsz; i += 64) acc[i] = 0.0;
   __syncthreads();
-  // the lane's entry of the next iteration is loaded one iteration ahead (the
-  // next round of this stage, else the first round of the next stage), so its
-  // latency hides behind the functor; tagged with its index (a stage without
-  // entries breaks the chain: the next one loads in place)
-  uint4 nxt{};
-  uint2 nxt2{};
-  int64_t nxt_e = -1;
+  // the lane's entries of the next group are loaded one group ahead (the next
+  // group of this stage, else the first group of the next stage), so their
+  // latency hides behind the functors; tagged with the group's first entry (a
+  // stage without entries breaks the chain: the next one loads in place)
+  uint4 nxt[UN];
+  uint2 nxt2[UN];
+  int64_t nxt_base = -1;
   for (int L = 0; L < U.n_stages; ++L) {
     const int64_t e0 = p.stage_ptr[U.first_stage + L], e1 = p.stage_ptr[U.first_stage + L + 1];
     const int64_t e2 = L + 1 < U.n_stages ? p.stage_ptr[U.first_stage + L + 2] : e1;
-    for (int64_t e = e0 + lane; e - lane < e1; e += 64) {
-      uint4 m{};
-      uint2 m2{};
-      if (e < e1) {
-        if (nxt_e == e) {
-          m = nxt;
-          m2 = nxt2;
-        }
-        else {
-          m = reinterpret_cast<const uint4*>(p.entries)[e];
-          if (WIDE) m2 = reinterpret_cast<const uint2*>(p.entries2)[e];
+    for (int64_t eb = e0; eb < e1; eb += 64 * UN) {
+      uint4 m[UN];
+      uint2 m2[UN];
+      const bool have = nxt_base == eb;
+#pragma unroll
+      for (int v = 0; v < UN; ++v) {
+        const int64_t e = eb + 64 * v + lane;
+        m[v] = uint4{};
+        m2[v] = uint2{};
+        if (e < e1) {
+          if (have) {
+            m[v] = nxt[v];
+            m2[v] = nxt2[v];
+          }
+          else {
+            m[v] = reinterpret_cast<const uint4*>(p.entries)[e];
+            if (WIDE) m2[v] = reinterpret_cast<const uint2*>(p.entries2)[e];
+          }
         }
       }
       {
-        const bool more = e + 64 - lane < e1;
-        const int64_t en = more ? e + 64 : e1 + lane;
-        if (en < (more ? e1 : e2)) {
-          nxt = reinterpret_cast<const uint4*>(p.entries)[en];
-          if (WIDE) nxt2 = reinterpret_cast<const uint2*>(p.entries2)[en];
-          nxt_e = en;
+        const bool more = eb + 64 * UN < e1;
+        const int64_t nb = more ? eb + 64 * UN : e1, lim = more ? e1 : e2;
+        nxt_base = lim > nb ? nb : -1;
+#pragma unroll
+        for (int v = 0; v < UN; ++v) {
+          const int64_t en = nb + 64 * v + lane;
+          if (en < lim) {
+            nxt[v] = reinterpret_cast<const uint4*>(p.entries)[en];
+            if (WIDE) nxt2[v] = reinterpret_cast<const uint2*>(p.entries2)[en];
+          }
         }
       }
-      if (e < e1) {
-        uint32_t cell, pos, sl[4];
+      if (eb + lane >= e1) continue;  // no entry for this lane (then none of its later ones either)
+      uint32_t cell[UN], pos[UN], sl[UN][4];
+#pragma unroll
+      for (int v = 0; v < UN; ++v) {
         if (WIDE) {
-          sl[0] = m.x;
-          sl[1] = m.y;
-          sl[2] = m.z;
-          sl[3] = m.w;
-          cell = m2.x;
-          pos = m2.y;
+          sl[v][0] = m[v].x;
+          sl[v][1] = m[v].y;
+          sl[v][2] = m[v].z;
+          sl[v][3] = m[v].w;
+          cell[v] = m2[v].x;
+          pos[v] = m2[v].y;
         }
         else {
-          cell = m.x;
-          sl[0] = m.y & 0xffffu;
-          sl[1] = m.y >> 16;
-          sl[2] = m.z & 0xffffu;
-          sl[3] = m.z >> 16;
-          pos = m.w;
+          cell[v] = m[v].x;
+          sl[v][0] = m[v].y & 0xffffu;
+          sl[v][1] = m[v].y >> 16;
+          sl[v][2] = m[v].z & 0xffffu;
+          sl[v][3] = m[v].z >> 16;
+          pos[v] = m[v].w;
         }
-        const auto ke = f((int32_t)cell);
+      }
+      // a lane past the stage's end evaluates its first cell again (pure
+      // functor) and scatters nothing for it: no branch between the functors
+      decltype(f(0)) ke[UN];
+#pragma unroll
+      for (int v = 0; v < UN; ++v) ke[v] = f((int32_t)(eb + 64 * v + lane < e1 ? cell[v] : cell[0]));
+#pragma unroll
+      for (int v = 0; v < UN; ++v) {
+        if (eb + 64 * v + lane >= e1) break;
 #pragma unroll
         for (int a = 0; a < NV; ++a) {
-          const uint32_t pa = (pos >> (8 * a)) & 0xffu;
+          const uint32_t pa = (pos[v] >> (8 * a)) & 0xffu;
           if (!(pa & 0x80u)) continue;
           double* base = acc + ((pa >> 6) & 1u) * bufsz + (pa & 63u);
 #pragma unroll
           for (int b = 0; b < NV; ++b) {
-            const int s = WIDE ? (int)((sl[a] >> (8 * b)) & 0xffu) : (int)((sl[a] >> (4 * b)) & 0xfu);
+            const int s = WIDE ? (int)((sl[v][a] >> (8 * b)) & 0xffu) : (int)((sl[v][a] >> (4 * b)) & 0xfu);
 #pragma unroll
             for (int i = 0; i < K; ++i)
 #pragma unroll
               for (int jj = 0; jj < K; ++jj)
-                atomicAdd(base + (s * KK + i * K + jj) * RL, (double)ke(K * a + i, K * b + jj));
+                atomicAdd(base + (s * KK + i * K + jj) * RL, (double)ke[v](K * a + i, K * b + jj));
           }
         }
       }
@@ -245,6 +274,14 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
   }
   flush_layer<K, WIDE>(p, U, U.n_stages - 1, acc, bufsz, lane, overwrite);
 }
+
+/* Functor evaluations in flight per lane: 2 for element matrices up to 4 x 4
+ * (register room: the unit's LDS, not its VGPRs, bounds the occupancy), 1
+ * for the larger blocks (a 12 x 12 matrix is 288 VGPRs). */
+#ifndef AFEM_GENERIC_UNROLL
+#define AFEM_GENERIC_UNROLL 2
+#endif
+constexpr int default_unroll(int nk) { return nk * nk <= 16 ? AFEM_GENERIC_UNROLL : 1; }
 
 /* ------------------------------------------------------------ atomic kernel */
 
@@ -320,8 +357,8 @@ int assemble_bilinear_atomic(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate, b
  * call builds the structure's cell-unit plan (afem_bsr_functor_plan, one
  * time).  Couplings outside the sparsity cannot occur: the plan is built from
  * the same cells as the structure. */
-template <int NV, int K, class F>
-int assemble_bilinear(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate)
+template <int NV, int K, int UN, class F>
+int assemble_bilinear_unrolled(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate)
 {
   afem_functor_plan p;
   int rc = afem_bsr_functor_plan(bsr, &p);
@@ -333,10 +370,16 @@ int assemble_bilinear(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate)
   hipStream_t st = reinterpret_cast<hipStream_t>(p.stream);
   const int ow = mode == Mode::Overwrite ? 1 : 0;
   if (p.wide)
-    hipLaunchKernelGGL((k_assemble_units<NV, K, true, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, ow);
+    hipLaunchKernelGGL((k_assemble_units<NV, K, true, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, ow);
   else
-    hipLaunchKernelGGL((k_assemble_units<NV, K, false, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, ow);
+    hipLaunchKernelGGL((k_assemble_units<NV, K, false, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, ow);
   return hipGetLastError() == hipSuccess ? AFEM_OK : AFEM_ERR_HIP;
+}
+
+template <int NV, int K, class F>
+int assemble_bilinear(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate)
+{
+  return assemble_bilinear_unrolled<NV, K, default_unroll(NV * K)>(bsr, f, mode);
 }
 
 }  // namespace generic

@@ -2,6 +2,8 @@
 for each variant (comma list of KEY=VALUE, '-' = defaults) a fresh structure
 and plan, then the kernel time (median of `reps`, HIP events) with the Poisson
 module's element (elements::PoissonTet4) and the lean cofactor element.
+A variant key UN=k (k = 1..4) runs the kernel with k functor evaluations in
+flight per lane (gx_assemble_unrolled) instead of the default.
 usage: python tools/generic_ab.py n reps variant [variant ...]"""
 import os
 import sys
@@ -18,8 +20,17 @@ n, reps = int(sys.argv[1]), int(sys.argv[2])
 ctx = af.Context(0)
 mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
 ref = None
+first = None
 for spec in sys.argv[3:]:
     kv = [] if spec == "-" else [x.split("=") for x in spec.split(",")]
+    un = [int(v) for k, v in kv if k == "UN"]
+    kv = [(k, v) for k, v in kv if k != "UN"]
+
+    def run(kind):
+        if un:
+            gx.assemble_unrolled(bsr, kind, un[0], overwrite=True)
+        else:
+            gx.assemble(bsr, kind, gx.UNITS, overwrite=True)
     for k, v in kv:
         af.set_variant(k, v)
     bsr = af.BSRFormat(mesh, 1).initialize(True)
@@ -30,11 +41,11 @@ for spec in sys.argv[3:]:
     ab = 4 * st["n_incidences"] + 24 * mesh.n_nodes + 8 * (mesh.n_own_nodes + 1) + 12 * nnz
     out = []
     for kind in (gx.POISSON, gx.POISSON_LEAN):
-        gx.assemble(bsr, kind, gx.UNITS, overwrite=True)
+        run(kind)
         ctx.synchronize()
         for i in range(reps):
             ctx.event_record(2 * i)
-            gx.assemble(bsr, kind, gx.UNITS, overwrite=True)
+            run(kind)
             ctx.event_record(2 * i + 1)
         ctx.synchronize()
         t = float(np.median([ctx.event_elapsed(2 * i, 2 * i + 1) for i in range(reps)]))
@@ -44,9 +55,12 @@ for spec in sys.argv[3:]:
         bsr.assemblePoissonP1(1.0, 0.0)
         ref = bsr.download()[2]
     err = float(np.abs(v - ref).max() / np.abs(ref).max())
+    if first is None:
+        first = v
+    err = f"{err:.1e} bits-as-first {np.array_equal(v, first)}"
     print(f"{spec:40s} units {plan['n_units']:6d} rl {plan['rows_per_layer']:2d} evals/cell "
           f"{plan['n_entries'] / mesh.n_cells:.3f} coalesced {plan.get('n_coalesced', -1)} | module {out[0]} | "
-          f"lean {out[1]} | err {err:.1e}", flush=True)
+          f"lean {out[1]} | err {err}", flush=True)
     for k, _ in kv:
         af.set_variant(k, None)
     bsr.close()
