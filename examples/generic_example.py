@@ -26,7 +26,7 @@ def load():
         L.gx_assemble.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                   ctypes.c_double]
         L.gx_assemble_unrolled.restype = ctypes.c_int
-        L.gx_assemble_unrolled.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.gx_assemble_unrolled.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -41,11 +41,12 @@ def assemble(bsr, kind=POISSON, path=UNITS, overwrite=False, lam=0.0, mu=0.0):
         raise _capi.AfemError(rc, "gx_assemble", L.afem_last_error().decode(errors="replace"))
 
 
-def assemble_unrolled(bsr, kind, un, overwrite=False):
+def assemble_unrolled(bsr, kind, un, overwrite=False, pad=1):
     """The cell-unit kernel with un (1-4) functor evaluations in flight per
-    lane (tet4 Poisson kinds only): the A/B of assemble_bilinear's default."""
+    lane and LDS planes padded by pad rows (tet4 Poisson kinds only): the A/B
+    of assemble_bilinear's defaults."""
     from arcanefem_amd import _capi
-    rc = load().gx_assemble_unrolled(bsr.h, kind, un, 1 if overwrite else 0)
+    rc = load().gx_assemble_unrolled(bsr.h, kind, un, 1 if overwrite else 0, pad)
     if rc != 0:
         L = _capi.load()
         raise _capi.AfemError(rc, "gx_assemble_unrolled", L.afem_last_error().decode(errors="replace"))

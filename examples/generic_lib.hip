@@ -8,8 +8,9 @@
 //          2: Poisson tet4 in the cofactor form (elements::PoissonTet4Lean);
 //     path 0: cell-unit kernel (assemble_bilinear), 1: f64-atomic kernel (assemble_bilinear_atomic);
 //     mode 0: accumulate into the values, 1: overwrite them.
-//   gx_assemble_unrolled(bsr, kind, un, mode): kinds 0 / 2 on tet4 through the cell-unit kernel with
-//     un = 1..4 functor evaluations in flight per lane (the A/B of the default, tools/generic_ab.py).
+//   gx_assemble_unrolled(bsr, kind, un, mode, pad): kinds 0 / 2 on tet4 through the cell-unit kernel
+//     with un = 1..4 functor evaluations in flight per lane and LDS planes of rows + pad (the A/B of
+//     the defaults, tools/generic_ab.py).
 // Enqueued on the structure's context stream; no synchronisation (path 1 syncs for its error flag).
 #include "arcanefem_amd.h"
 #include "arcanefem_amd_generic.hpp"
@@ -46,15 +47,15 @@ extern "C" int gx_assemble(afem_bsr* bsr, int kind, int path, int mode, double l
 
 namespace {
 template <int UN>
-int run_un(afem_bsr* bsr, const afem::generic::CellAccess& acc, int kind, int mode)
+int run_un(afem_bsr* bsr, const afem::generic::CellAccess& acc, int kind, int mode, int pad)
 {
   const Mode m = mode ? Mode::Overwrite : Mode::Accumulate;
-  if (kind == 2) return afem::generic::assemble_bilinear_unrolled<4, 1, UN>(bsr, elements::PoissonTet4Lean{ acc }, m);
-  return afem::generic::assemble_bilinear_unrolled<4, 1, UN>(bsr, elements::PoissonTet4{ acc }, m);
+  if (kind == 2) return afem::generic::assemble_bilinear_unrolled<4, 1, UN>(bsr, elements::PoissonTet4Lean{ acc }, m, pad);
+  return afem::generic::assemble_bilinear_unrolled<4, 1, UN>(bsr, elements::PoissonTet4{ acc }, m, pad);
 }
 }  // namespace
 
-extern "C" int gx_assemble_unrolled(afem_bsr* bsr, int kind, int un, int mode)
+extern "C" int gx_assemble_unrolled(afem_bsr* bsr, int kind, int un, int mode, int pad)
 {
   afem_assembly_view v;
   int rc = afem_bsr_assembly_view(bsr, &v);
@@ -62,10 +63,10 @@ extern "C" int gx_assemble_unrolled(afem_bsr* bsr, int kind, int un, int mode)
   if (v.block_size != 1 || v.nb_node_per_cell != 4 || (kind != 0 && kind != 2)) return AFEM_ERR_ARG;
   const afem::generic::CellAccess acc{ v.cell_node, v.coords };
   switch (un) {
-    case 1: return run_un<1>(bsr, acc, kind, mode);
-    case 2: return run_un<2>(bsr, acc, kind, mode);
-    case 3: return run_un<3>(bsr, acc, kind, mode);
-    case 4: return run_un<4>(bsr, acc, kind, mode);
+    case 1: return run_un<1>(bsr, acc, kind, mode, pad);
+    case 2: return run_un<2>(bsr, acc, kind, mode, pad);
+    case 3: return run_un<3>(bsr, acc, kind, mode, pad);
+    case 4: return run_un<4>(bsr, acc, kind, mode, pad);
     default: return AFEM_ERR_ARG;
   }
 }

@@ -84,7 +84,7 @@ enum class Mode : int {
 /* Writes layer L of unit U (its LDS buffer) to the values and zeroes the buffer. */
 template <int K, bool WIDE>
 __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const afem_functor_unit& U, int L,
-                                            double* __restrict__ acc, int bufsz, int lane, int overwrite)
+                                            double* __restrict__ acc, int bufsz, int sr, int lane, int overwrite)
 {
   constexpr int KK = K * K;
   const int RL = p.rows_per_layer;
@@ -100,7 +100,7 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
     // runs of 8 consecutive rows per 8 lanes: one contiguous value range each
     double v[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) v[s] = s < len ? buf[s * RL + lane] : 0.0;
+    for (int s = 0; s < 16; ++s) v[s] = s < len ? buf[s * sr + lane] : 0.0;
     const long long rb0 = __shfl((long long)rb, lane & ~7);
     long long end = row >= 0 ? (long long)(rb + len) : rb0;
 #pragma unroll
@@ -143,7 +143,7 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
       for (int i = 0; i < K; ++i)
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-          const double val = buf[(s * KK + i * K + j) * RL + lane];
+          const double val = buf[(s * KK + i * K + j) * sr + lane];
           const int64_t idx = p.ordered_per_block ? (rb + s) * KK + i * K + j
                                                   : rb * KK + (int64_t)i * K * len + K * s + j;
           p.values[idx] = overwrite ? val : p.values[idx] + val;
@@ -154,8 +154,10 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
   __syncthreads();
 }
 
-/* One wavefront per unit (blockDim 64); dynamic LDS: nbuf * width * K^2 *
- * rows_per_layer doubles, layout [buffer][slot*K^2 + i*K + j][lane].
+/* One wavefront per unit (blockDim 64); dynamic LDS: nbuf * width * K^2 * sr
+ * doubles, layout [buffer][slot*K^2 + i*K + j][row], planes of sr =
+ * rows_per_layer + pad rows (pad 1: the slots of one row fall on different
+ * LDS banks -- the cells of one ds_add_f64 share rows, not slots).
  *
  * UN functor evaluations per lane are in flight at once (entries e, e + 64,
  * ..., e + 64 (UN-1) of the stage): the UN cells' connectivity and coordinate
@@ -165,7 +167,7 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
  * the one-cell-at-a-time order (entry e's adds, then e + 64's, ...): the same
  * bits for every UN. */
 template <int NV, int K, bool WIDE, int UN, class F>
-__global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f, int overwrite)
+__global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f, int sr, int overwrite)
 {
   extern __shared__ __align__(16) double acc[];
   constexpr int KK = K * K;
@@ -176,8 +178,7 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
   const int64_t q = n >> 3, rem = n & 7, x = bid & 7, j = bid >> 3;
   const int64_t u = x * q + (x < rem ? x : rem) + j;
   const afem_functor_unit U = p.units[u];
-  const int RL = p.rows_per_layer;
-  const int bufsz = p.width * KK * RL;
+  const int bufsz = p.width * KK * sr;
   for (int i = lane; i < p.nbuf * bufsz; i += 64) acc[i] = 0.0;
   __syncthreads();
   // the lane's entries of the next group are loaded one group ahead (the next
@@ -264,15 +265,15 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
             for (int i = 0; i < K; ++i)
 #pragma unroll
               for (int jj = 0; jj < K; ++jj)
-                atomicAdd(base + (s * KK + i * K + jj) * RL, (double)ke[v](K * a + i, K * b + jj));
+                atomicAdd(base + (s * KK + i * K + jj) * sr, (double)ke[v](K * a + i, K * b + jj));
           }
         }
       }
     }
     __syncthreads();
-    if (L > 0) flush_layer<K, WIDE>(p, U, L - 1, acc, bufsz, lane, overwrite);
+    if (L > 0) flush_layer<K, WIDE>(p, U, L - 1, acc, bufsz, sr, lane, overwrite);
   }
-  flush_layer<K, WIDE>(p, U, U.n_stages - 1, acc, bufsz, lane, overwrite);
+  flush_layer<K, WIDE>(p, U, U.n_stages - 1, acc, bufsz, sr, lane, overwrite);
 }
 
 /* Functor evaluations in flight per lane: 2 for element matrices up to 4 x 4
@@ -280,6 +281,9 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
  * for the larger blocks (a 12 x 12 matrix is 288 VGPRs). */
 #ifndef AFEM_GENERIC_UNROLL
 #define AFEM_GENERIC_UNROLL 2
+#endif
+#ifndef AFEM_GENERIC_PAD
+#define AFEM_GENERIC_PAD 1
 #endif
 constexpr int default_unroll(int nk) { return nk * nk <= 16 ? AFEM_GENERIC_UNROLL : 1; }
 
@@ -358,21 +362,26 @@ int assemble_bilinear_atomic(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate, b
  * time).  Couplings outside the sparsity cannot occur: the plan is built from
  * the same cells as the structure. */
 template <int NV, int K, int UN, class F>
-int assemble_bilinear_unrolled(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate)
+int assemble_bilinear_unrolled(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate, int pad = AFEM_GENERIC_PAD)
 {
   afem_functor_plan p;
   int rc = afem_bsr_functor_plan(bsr, &p);
   if (rc != AFEM_OK) return rc;
   if (p.nb_node_per_cell != NV || p.block_size != K) return AFEM_ERR_ARG;
-  const size_t lds = (size_t)p.nbuf * p.width * K * K * p.rows_per_layer * sizeof(double);
+  int sr = p.rows_per_layer + pad;
+  size_t lds = (size_t)p.nbuf * p.width * K * K * sr * sizeof(double);
+  if (lds > 64 * 1024 && pad) {  // no room for the padding: dense planes
+    sr = p.rows_per_layer;
+    lds = (size_t)p.nbuf * p.width * K * K * sr * sizeof(double);
+  }
   if (lds > 64 * 1024) return assemble_bilinear_atomic<NV, K>(bsr, f, mode, true);
   if (p.n_units == 0) return AFEM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(p.stream);
   const int ow = mode == Mode::Overwrite ? 1 : 0;
   if (p.wide)
-    hipLaunchKernelGGL((k_assemble_units<NV, K, true, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, ow);
+    hipLaunchKernelGGL((k_assemble_units<NV, K, true, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, sr, ow);
   else
-    hipLaunchKernelGGL((k_assemble_units<NV, K, false, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, ow);
+    hipLaunchKernelGGL((k_assemble_units<NV, K, false, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, sr, ow);
   return hipGetLastError() == hipSuccess ? AFEM_OK : AFEM_ERR_HIP;
 }
 

@@ -2,8 +2,9 @@
 for each variant (comma list of KEY=VALUE, '-' = defaults) a fresh structure
 and plan, then the kernel time (median of `reps`, HIP events) with the Poisson
 module's element (elements::PoissonTet4) and the lean cofactor element.
-A variant key UN=k (k = 1..4) runs the kernel with k functor evaluations in
-flight per lane (gx_assemble_unrolled) instead of the default.
+Variant keys UN=k (k = 1..4) and PAD=p run the kernel with k functor
+evaluations in flight per lane and LDS planes of rows + p (gx_assemble_unrolled;
+defaults 2 and 1).
 usage: python tools/generic_ab.py n reps variant [variant ...]"""
 import os
 import sys
@@ -24,11 +25,12 @@ first = None
 for spec in sys.argv[3:]:
     kv = [] if spec == "-" else [x.split("=") for x in spec.split(",")]
     un = [int(v) for k, v in kv if k == "UN"]
-    kv = [(k, v) for k, v in kv if k != "UN"]
+    pad = [int(v) for k, v in kv if k == "PAD"]
+    kv = [(k, v) for k, v in kv if k not in ("UN", "PAD")]
 
     def run(kind):
-        if un:
-            gx.assemble_unrolled(bsr, kind, un[0], overwrite=True)
+        if un or pad:
+            gx.assemble_unrolled(bsr, kind, un[0] if un else 2, overwrite=True, pad=pad[0] if pad else 1)
         else:
             gx.assemble(bsr, kind, gx.UNITS, overwrite=True)
     for k, v in kv:
