@@ -412,10 +412,11 @@ void functor_plan_build(Bsr& b)
       g.fx = 8;
       g.fy = k == 1 ? 8 : 4;
       if (k == 3) g.fx = 4;
-      // footprint overrides (measurements): fx * fy rows per layer, at most 64 / k^2
+      // footprint overrides (measurements): fx * fy block rows per layer (one
+      // lane each), at most 64
       g.fx = (int)std::max<int64_t>(1, env_int("AFEM_FUNCTOR_FX", g.fx));
       g.fy = (int)std::max<int64_t>(1, env_int("AFEM_FUNCTOR_FY", g.fy));
-      if (g.fx * g.fy * k * k > 64) throw Error(AFEM_ERR_ARG, "functor plan: AFEM_FUNCTOR_FX * FY exceeds 64 / k^2 rows");
+      if (g.fx * g.fy > 64) throw Error(AFEM_ERR_ARG, "functor plan: AFEM_FUNCTOR_FX * FY exceeds 64 rows");
       g.Lx = L[0];
       g.Ly = L[1];
       g.Lz = L[2];
