@@ -21,8 +21,7 @@
 // evaluations per cube, plus 1/zs for the cube layer below a segment).  The
 // unit walks the cube layers upwards: node layer z's rows take the cube layers
 // z-1 and z, so two row-layer accumulator buffers (by parity) live in LDS,
-// [16][52] doubles each (15 column offsets in sorted order + the |det| sum;
-// 49 rows + 3 sink rows taking the adds of corners outside the unit),
+// [16][64] doubles each (15 column offsets in sorted order + the |det| sum),
 // and the node coordinates of the two layers of the current cube layer
 // (9 x 9 nodes each, staged from registers loaded one layer ahead).  When a
 // node layer is complete its 49 rows are written once: the values compacted
@@ -126,15 +125,13 @@ constexpr int kRun = 7;    // rows per x-run of a column
 constexpr int kRows = 49;  // rows per column layer
 constexpr int kCol = 9;    // staged nodes per x / y line (the column's rows + 1 halo line below)
 constexpr int kAcc = 16;   // accumulators per row: 15 offsets + |det| sum
-constexpr int kSink = 3;   // sink rows after the 49 (corners outside the unit)
-constexpr int kStride = kRows + kSink;  // accumulator rows per offset (52: 13.3 KB for both buffers)
 
 __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
                                                        const double* __restrict__ coords,
                                                        double* __restrict__ vals, double* __restrict__ rhs,
                                                        int rhs_add)
 {
-  __shared__ __align__(16) double acc[2][kAcc][kStride];
+  __shared__ __align__(16) double acc[2][kAcc][64];
   __shared__ double cz[2][3][kCol * kCol];  // SoA coordinates of two node layers
   const int lane = threadIdx.x;
   // XCD-aware: blocks go round-robin over the 8 XCDs; XCD x takes the x-th
@@ -189,7 +186,7 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
       cz[buf][2][q] = pre[h][2];
     }
   };
-  for (int i = lane; i < 2 * kAcc * kStride; i += 64) (&acc[0][0][0])[i] = 0.0;
+  for (int i = lane; i < 2 * kAcc * 64; i += 64) (&acc[0][0][0])[i] = 0.0;
 
   // ---- node layer z complete: write its 49 rows (values compacted by the present neighbours) + RHS.
   // The rows' offsets are loaded before the layer's cubes (prefetch_rows), so
@@ -224,14 +221,13 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
     const int s2 = (lm < lp ? n0 : 0) + (l0 < lp ? n1 : 0);
     double v[15];
     double sum = 0.0;
-    const int lr = min(lane, kStride - 1);
 #pragma unroll
     for (int o = 0; o < 15; ++o) {
-      v[o] = acc[b][o][lr];
+      v[o] = acc[b][o][lane];
       if (o != 7 && ((mask >> o) & 1u)) sum += v[o];
     }
     v[7] = -sum;
-    const double meas = acc[b][15][lr];
+    const double meas = acc[b][15][lane];
     int64_t r = 0, rb = 0;
     int len = 0;
     if (valid) {
@@ -282,9 +278,8 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
       off += rl;
     }
     __syncthreads();
-    // zero the buffer for node layer z + 2 (the loop's next barrier orders this
-    // before any add into it)
-    for (int i = lane; i < kAcc * kStride; i += 64) img[i] = 0.0;
+    for (int i = lane; i < kAcc * 64; i += 64) img[i] = 0.0;
+    __syncthreads();
   };
 
   // ---- cube layer zc: the lane's cube, its 6 tets, 19 edge sums and 8 corner |det| sums
@@ -328,25 +323,27 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
         }
       }
     }
-    // the accumulator row of each corner: a row of this unit, else a sink row
-    // (rows 49..63 of the buffer, never flushed; spread over 15 of them so the
-    // sinks' same-address collisions stay few): every add runs unpredicated
+    // corners that are rows of this unit, and their accumulator rows
+    bool in[8];
+    double* base[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const int rx = ci - 1 + cbit(c, 0), ry = cj - 1 + cbit(c, 1), z = zc + cbit(c, 2);
-      const bool in = (uint32_t)(rx >= 0) & (uint32_t)(ry >= 0) & (uint32_t)(rx < kRun) & (uint32_t)(ry < kRun) &
-                      (uint32_t)(cx0 + rx < g.np1) & (uint32_t)(cy0 + ry < g.np1) & (uint32_t)(z >= z0) &
-                      (uint32_t)(z < z1);
-      const int row = in ? rx + kRun * ry : kRows + (lane % kSink);
-      double* const base = &acc[cbit(c, 2) ? bt : bb][0][0] + row;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        if (b == c) continue;
-        const int lo = c < b ? c : b, hi = c < b ? b : c;
-        if (is_edge(lo, hi)) atomicAdd(base + kStride * edge_o(c, b), ev[lo][hi]);
-      }
-      atomicAdd(base + kStride * 15, mv[c]);
+      in[c] = rx >= 0 && ry >= 0 && rx < kRun && ry < kRun && cx0 + rx < g.np1 && cy0 + ry < g.np1 && z >= z0 &&
+              z < z1;
+      base[c] = &acc[cbit(c, 2) ? bt : bb][0][0] + (in[c] ? rx + kRun * ry : 0);
     }
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = a + 1; b < 8; ++b)
+        if (is_edge(a, b)) {
+          if (in[a]) atomicAdd(base[a] + 64 * edge_o(a, b), ev[a][b]);
+          if (in[b]) atomicAdd(base[b] + 64 * edge_o(b, a), ev[a][b]);
+        }
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (in[c]) atomicAdd(base[c] + 64 * 15, mv[c]);
   };
 
   // ---- walk the cube layers upwards (coordinates staged one layer ahead)
