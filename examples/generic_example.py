@@ -41,7 +41,7 @@ def assemble(bsr, kind=POISSON, path=UNITS, overwrite=False, lam=0.0, mu=0.0):
         raise _capi.AfemError(rc, "gx_assemble", L.afem_last_error().decode(errors="replace"))
 
 
-def assemble_unrolled(bsr, kind, un, overwrite=False, pad=1):
+def assemble_unrolled(bsr, kind, un, overwrite=False, pad=0):
     """The cell-unit kernel with un (1-4) functor evaluations in flight per
     lane and LDS planes padded by pad rows (tet4 Poisson kinds only): the A/B
     of assemble_bilinear's defaults."""

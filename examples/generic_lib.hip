@@ -9,7 +9,7 @@
 //     path 0: cell-unit kernel (assemble_bilinear), 1: f64-atomic kernel (assemble_bilinear_atomic);
 //     mode 0: accumulate into the values, 1: overwrite them.
 //   gx_assemble_unrolled(bsr, kind, un, mode, pad): kinds 0 / 2 on tet4 through the cell-unit kernel
-//     with un = 1..4 functor evaluations in flight per lane and LDS planes of rows + pad (the A/B of
+//     with un = 1..4, 6, 8 functor evaluations in flight per lane and LDS planes of rows + pad (the A/B of
 //     the defaults, tools/generic_ab.py).
 // Enqueued on the structure's context stream; no synchronisation (path 1 syncs for its error flag).
 #include "arcanefem_amd.h"
@@ -67,6 +67,8 @@ extern "C" int gx_assemble_unrolled(afem_bsr* bsr, int kind, int un, int mode, i
     case 2: return run_un<2>(bsr, acc, kind, mode, pad);
     case 3: return run_un<3>(bsr, acc, kind, mode, pad);
     case 4: return run_un<4>(bsr, acc, kind, mode, pad);
+    case 6: return run_un<6>(bsr, acc, kind, mode, pad);
+    case 8: return run_un<8>(bsr, acc, kind, mode, pad);
     default: return AFEM_ERR_ARG;
   }
 }
