@@ -278,11 +278,14 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
   flush_layer<K, WIDE>(p, U, U.n_stages - 1, acc, bufsz, sr, lane, overwrite);
 }
 
-/* Functor evaluations in flight per lane: 2 for element matrices up to 4 x 4
- * (register room: the unit's LDS, not its VGPRs, bounds the occupancy), 1
- * for the larger blocks (a 12 x 12 matrix is 288 VGPRs). */
+/* Functor evaluations in flight per lane: 4 for element matrices up to 4 x 4
+ * (register room: the unit's LDS, not its VGPRs, bounds the occupancy; C2
+ * with the Poisson module's tet4 element, tools/generic_ab.py r04o: UN 1 /
+ * 2 / 3 / 4 / 6 / 8 = 2.16 / 1.87 / 1.88 / 1.79 / 1.98 / 2.85 ms -- 6 and 8
+ * cost waves: 224 and 256 VGPRs), 1 for the larger blocks (a 12 x 12 matrix
+ * is 288 VGPRs). */
 #ifndef AFEM_GENERIC_UNROLL
-#define AFEM_GENERIC_UNROLL 2
+#define AFEM_GENERIC_UNROLL 4
 #endif
 #ifndef AFEM_GENERIC_PAD
 #define AFEM_GENERIC_PAD 0

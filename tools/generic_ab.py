@@ -4,7 +4,7 @@ and plan, then the kernel time (median of `reps`, HIP events) with the Poisson
 module's element (elements::PoissonTet4) and the lean cofactor element.
 Variant keys UN=k (k = 1..4) and PAD=p run the kernel with k functor
 evaluations in flight per lane and LDS planes of rows + p (gx_assemble_unrolled;
-defaults: the header's).
+defaults: the header's, 4 and 0).
 usage: python tools/generic_ab.py n reps variant [variant ...]"""
 import os
 import sys
@@ -30,7 +30,7 @@ for spec in sys.argv[3:]:
 
     def run(kind):
         if un or pad:
-            gx.assemble_unrolled(bsr, kind, un[0] if un else 2, overwrite=True, pad=pad[0] if pad else 0)
+            gx.assemble_unrolled(bsr, kind, un[0] if un else 4, overwrite=True, pad=pad[0] if pad else 0)
         else:
             gx.assemble(bsr, kind, gx.UNITS, overwrite=True)
     for k, v in kv:
