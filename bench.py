@@ -413,7 +413,7 @@ def c2_arrays_leg(ctx, af, n, reps=10, warmup=2):
     return out
 
 
-def c2_generic_leg(ctx, af, n, reps=10, warmup=2, atomic_reps=2):
+def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2):
     """C2 through the path an UNCHANGED module takes: BSRFormat::assembleBilinear
     with the module's own element lambda (_computeElementMatrixTetra4Gpu,
     modules/poisson/FemModule.h:177-186: examples/elements.hpp PoissonTet4,
