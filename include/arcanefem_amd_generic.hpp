@@ -84,7 +84,7 @@ enum class Mode : int {
 /* Writes layer L of unit U (its LDS buffer) to the values and zeroes the buffer. */
 template <int K, bool WIDE>
 __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const afem_functor_unit& U, int L,
-                                            double* __restrict__ acc, int bufsz, int sr, int lane, int overwrite)
+                                            double* __restrict__ acc, int bufsz, int sr, int swz, int lane, int overwrite)
 {
   constexpr int KK = K * K;
   const int RL = p.rows_per_layer;
@@ -100,7 +100,7 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
     // runs of 8 consecutive rows per 8 lanes: one contiguous value range each
     double v[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) v[s] = s < len ? buf[s * sr + lane] : 0.0;
+    for (int s = 0; s < 16; ++s) v[s] = s < len ? buf[s * sr + (lane ^ (s & swz))] : 0.0;
     const long long rb0 = __shfl((long long)rb, lane & ~7);
     long long end = row >= 0 ? (long long)(rb + len) : rb0;
 #pragma unroll
@@ -143,7 +143,8 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
       for (int i = 0; i < K; ++i)
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-          const double val = buf[(s * KK + i * K + j) * sr + lane];
+          const int pl = s * KK + i * K + j;
+          const double val = buf[pl * sr + (lane ^ (pl & swz))];
           const int64_t idx = p.ordered_per_block ? (rb + s) * KK + i * K + j
                                                   : rb * KK + (int64_t)i * K * len + K * s + j;
           p.values[idx] = overwrite ? val : p.values[idx] + val;
@@ -159,7 +160,8 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
  * rows_per_layer + pad rows (pad 1 puts the slots of one row on different
  * LDS banks -- the cells of one ds_add_f64 share rows, not slots -- but its
  * 16.6 KB per unit leave 9 waves per CU instead of 10: 3 % slower at C2, so
- * the default is 0).
+ * the default is 0); pad < 0 keeps the dense planes and XOR-swizzles the rows
+ * of plane pl by pl mod 16 instead (row' = row ^ (pl & swz)).
  *
  * UN functor evaluations per lane are in flight at once (entries e, e + 64,
  * ..., e + 64 (UN-1) of the stage): the UN cells' connectivity and coordinate
@@ -169,7 +171,7 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
  * the one-cell-at-a-time order (entry e's adds, then e + 64's, ...): the same
  * bits for every UN. */
 template <int NV, int K, bool WIDE, int UN, class F>
-__global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f, int sr, int overwrite)
+__global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f, int sr, int swz, int overwrite)
 {
   extern __shared__ __align__(16) double acc[];
   constexpr int KK = K * K;
@@ -259,23 +261,26 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
         for (int a = 0; a < NV; ++a) {
           const uint32_t pa = (pos[v] >> (8 * a)) & 0xffu;
           if (!(pa & 0x80u)) continue;
-          double* base = acc + ((pa >> 6) & 1u) * bufsz + (pa & 63u);
+          double* const bufp = acc + ((pa >> 6) & 1u) * bufsz;
+          const int row = (int)(pa & 63u);
 #pragma unroll
           for (int b = 0; b < NV; ++b) {
             const int s = WIDE ? (int)((sl[v][a] >> (8 * b)) & 0xffu) : (int)((sl[v][a] >> (4 * b)) & 0xfu);
 #pragma unroll
             for (int i = 0; i < K; ++i)
 #pragma unroll
-              for (int jj = 0; jj < K; ++jj)
-                atomicAdd(base + (s * KK + i * K + jj) * sr, (double)ke[v](K * a + i, K * b + jj));
+              for (int jj = 0; jj < K; ++jj) {
+                const int pl = s * KK + i * K + jj;
+                atomicAdd(bufp + pl * sr + (row ^ (pl & swz)), (double)ke[v](K * a + i, K * b + jj));
+              }
           }
         }
       }
     }
     __syncthreads();
-    if (L > 0) flush_layer<K, WIDE>(p, U, L - 1, acc, bufsz, sr, lane, overwrite);
+    if (L > 0) flush_layer<K, WIDE>(p, U, L - 1, acc, bufsz, sr, swz, lane, overwrite);
   }
-  flush_layer<K, WIDE>(p, U, U.n_stages - 1, acc, bufsz, sr, lane, overwrite);
+  flush_layer<K, WIDE>(p, U, U.n_stages - 1, acc, bufsz, sr, swz, lane, overwrite);
 }
 
 /* Functor evaluations in flight per lane: 4 for element matrices up to 4 x 4
@@ -373,6 +378,11 @@ int assemble_bilinear_unrolled(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate,
   int rc = afem_bsr_functor_plan(bsr, &p);
   if (rc != AFEM_OK) return rc;
   if (p.nb_node_per_cell != NV || p.block_size != K) return AFEM_ERR_ARG;
+  // pad < 0: no padding, the rows of plane pl XOR-swizzled by pl mod 16 instead
+  // (power-of-two planes of at least 16 rows)
+  const int RL = p.rows_per_layer;
+  const int swz = pad < 0 && RL >= 16 && (RL & (RL - 1)) == 0 ? 15 : 0;
+  if (pad < 0) pad = 0;
   int sr = p.rows_per_layer + pad;
   size_t lds = (size_t)p.nbuf * p.width * K * K * sr * sizeof(double);
   if (lds > 64 * 1024 && pad) {  // no room for the padding: dense planes
@@ -384,9 +394,9 @@ int assemble_bilinear_unrolled(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate,
   hipStream_t st = reinterpret_cast<hipStream_t>(p.stream);
   const int ow = mode == Mode::Overwrite ? 1 : 0;
   if (p.wide)
-    hipLaunchKernelGGL((k_assemble_units<NV, K, true, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, sr, ow);
+    hipLaunchKernelGGL((k_assemble_units<NV, K, true, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, sr, swz, ow);
   else
-    hipLaunchKernelGGL((k_assemble_units<NV, K, false, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, sr, ow);
+    hipLaunchKernelGGL((k_assemble_units<NV, K, false, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, sr, swz, ow);
   return hipGetLastError() == hipSuccess ? AFEM_OK : AFEM_ERR_HIP;
 }
 

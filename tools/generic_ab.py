@@ -2,7 +2,7 @@
 for each variant (comma list of KEY=VALUE, '-' = defaults) a fresh structure
 and plan, then the kernel time (median of `reps`, HIP events) with the Poisson
 module's element (elements::PoissonTet4) and the lean cofactor element.
-Variant keys UN=k (k = 1..4) and PAD=p run the kernel with k functor
+Variant keys UN=k (k = 1..4, 6, 8) and PAD=p (-1: XOR-swizzled rows) run the kernel with k functor
 evaluations in flight per lane and LDS planes of rows + p (gx_assemble_unrolled;
 defaults: the header's, 4 and 0).
 usage: python tools/generic_ab.py n reps variant [variant ...]"""
