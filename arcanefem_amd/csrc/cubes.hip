@@ -126,10 +126,13 @@ constexpr int kRows = 49;  // rows per column layer
 constexpr int kCol = 9;    // staged nodes per x / y line (the column's rows + 1 halo line below)
 constexpr int kAcc = 16;   // accumulators per row: 15 offsets + |det| sum
 
+// HAS_RHS / RHS_ADD at compile time: the flush's global stores are then a
+// fixed, branch-free sequence, so the waits for the next layer's coordinates
+// count past them (vmcnt(N)) instead of draining them (vmcnt(0))
+template <bool HAS_RHS, bool RHS_ADD>
 __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
                                                        const double* __restrict__ coords,
-                                                       double* __restrict__ vals, double* __restrict__ rhs,
-                                                       int rhs_add)
+                                                       double* __restrict__ vals, double* __restrict__ rhs)
 {
   __shared__ __align__(16) double acc[2][kAcc][64];
   __shared__ double cz[2][3][kCol * kCol];  // SoA coordinates of two node layers
@@ -193,12 +196,14 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
   // their latency hides behind the cube arithmetic instead of stalling here.
   const int rx = lane % kRun, ry = lane / kRun;
   const int nx = cx0 + rx, ny = cy0 + ry;
-  int64_t pf_rb = 0, pf_re = 0;
+  int64_t pf_rb = 0, pf_re = 0, pf_r = 0;
+  double pf_rhs = 0.0;
   auto prefetch_rows = [&](int z) {  // clamped like load_layer: no branch
     const int zz = (z >= z0 && z < z1) ? z : z0;
-    const int64_t r = (int64_t)local_layer(g, zz) * g.L + min(nx, g.np1 - 1) + (int64_t)g.np1 * min(ny, g.np1 - 1);
-    pf_rb = rows[r];
-    pf_re = rows[r + 1];
+    pf_r = (int64_t)local_layer(g, zz) * g.L + min(nx, g.np1 - 1) + (int64_t)g.np1 * min(ny, g.np1 - 1);
+    pf_rb = rows[pf_r];
+    pf_re = rows[pf_r + 1];
+    if constexpr (RHS_ADD) pf_rhs = rhs[pf_r];
   };
   auto flush = [&](int z) {
     const int b = z & 1;
@@ -228,13 +233,17 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
     }
     v[7] = -sum;
     const double meas = acc[b][15][lane];
-    int64_t r = 0, rb = 0;
-    int len = 0;
-    if (valid) {
-      r = (int64_t)local_layer(g, z) * g.L + nx + (int64_t)g.np1 * ny;
-      rb = pf_rb;
-      len = (int)(pf_re - pf_rb);
-      if (rhs) rhs[r] = rhs_add ? rhs[r] + g.f_meas * meas : g.f_meas * meas;
+    // the prefetched offsets are consumed without a branch (selects), so the
+    // compiler keeps their load where prefetch_rows issued it
+    const int64_t rb = valid ? pf_rb : 0;
+    // (a 64-bit min: with only the low halves used the compiler reuses the
+    // loaded high half's register at once, a write-after-write wait on the load)
+    const int len = valid ? (int)min(pf_re - pf_rb, (int64_t)15) : 0;
+    if constexpr (HAS_RHS) {  // lanes without a row repeat lane 0's store (always a row)
+      const double rv = RHS_ADD ? pf_rhs + g.f_meas * meas : g.f_meas * meas;
+      const int64_t r0 = __shfl(pf_r, 0);
+      const double rv0 = __shfl(rv, 0);
+      rhs[valid ? pf_r : r0] = valid ? rv : rv0;
     }
     // prefix of the row lengths within the x-run (7 lanes), the runs' offsets in the image
     int p = 0;
@@ -262,29 +271,36 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
         }
     }
     __syncthreads();
-    // x-run q: run_len(q) values from image offset img(q) to vals + rb(first row of run q)
+    // x-run q: run_len(q) values from image offset img(q) to vals + rb(first row of run q).
+    // A fixed count of unpredicated stores: lanes past a run repeat the first
+    // value of run 0 (row 0 of the column is always a row: same address, same
+    // value), so the next layer's waits on its coordinate loads count past them
+    const int64_t dst0 = __shfl(rb, 0);
     int off = 0;
 #pragma unroll
     for (int q = 0; q < kRun; ++q) {
       const int rl = __shfl(p + len, kRun * q + kRun - 1);
       const int64_t dst = __shfl(rb, kRun * q);
-      // a fixed count of (predicated) stores: the next layer's waits on its
-      // coordinate loads can count past them instead of draining every store
 #pragma unroll
       for (int h = 0; h < 2; ++h) {  // rl <= 7 rows x 15 = 105
         const int t = lane + 64 * h;
-        if (t < rl) vals[dst + t] = img[off + t];
+        const bool ok = t < rl;
+        vals[ok ? dst + t : dst0] = img[ok ? off + t : 0];
       }
       off += rl;
     }
     __syncthreads();
-    for (int i = lane; i < kAcc * 64; i += 64) img[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < kAcc; ++i) img[64 * i + lane] = 0.0;
     __syncthreads();
   };
 
   // ---- cube layer zc: the lane's cube, its 6 tets, 19 edge sums and 8 corner |det| sums
   auto cubes = [&](int zc) {
-    if (!cube_in) return;
+    // no branch around the cube: a lane whose cube is outside the box works on
+    // its clamped (duplicated) coordinates and adds zeros -- a divergent region
+    // here made the compiler drain the next layer's loads (vmcnt(0)) before the
+    // arithmetic
     const int bb = zc & 1, bt = (zc + 1) & 1;
     P3 X[8];
 #pragma unroll
@@ -311,7 +327,7 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
       k[3] = pcross(e1, e2);
       k[0] = P3{ -(k[1].x + k[2].x + k[3].x), -(k[1].y + k[2].y + k[3].y), -(k[1].z + k[2].z + k[3].z) };
       const double meas = fabs(pdot(e1, k[1]));
-      const double s = g.s_coef * precip(meas);
+      const double s = g.s_coef * precip(fmax(meas, 1e-300));
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         mv[tet_v(t, p)] += meas;
@@ -323,41 +339,65 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
         }
       }
     }
-    // corners that are rows of this unit, and their accumulator rows
-    bool in[8];
+    // each corner's accumulator row: its own when it is a row of this unit,
+    // else the clamped row inside the column (then the lane adds zeros: x + 0
+    // = x, the sums are unchanged); every add runs unpredicated
+    uint64_t keep[8];
     double* base[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const int rx = ci - 1 + cbit(c, 0), ry = cj - 1 + cbit(c, 1), z = zc + cbit(c, 2);
-      in[c] = rx >= 0 && ry >= 0 && rx < kRun && ry < kRun && cx0 + rx < g.np1 && cy0 + ry < g.np1 && z >= z0 &&
-              z < z1;
-      base[c] = &acc[cbit(c, 2) ? bt : bb][0][0] + (in[c] ? rx + kRun * ry : 0);
+      const bool in = cube_in & (rx >= 0) & (ry >= 0) & (rx < kRun) & (ry < kRun) & (cx0 + rx < g.np1) &
+                      (cy0 + ry < g.np1) & (z >= z0) & (z < z1);
+      keep[c] = in ? ~0ull : 0ull;
+      base[c] = &acc[cbit(c, 2) ? bt : bb][0][0] + min(max(rx, 0), kRun - 1) + kRun * min(max(ry, 0), kRun - 1);
     }
+    auto kept = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
       for (int b = a + 1; b < 8; ++b)
         if (is_edge(a, b)) {
-          if (in[a]) atomicAdd(base[a] + 64 * edge_o(a, b), ev[a][b]);
-          if (in[b]) atomicAdd(base[b] + 64 * edge_o(b, a), ev[a][b]);
+          atomicAdd(base[a] + 64 * edge_o(a, b), kept(keep[a], ev[a][b]));
+          atomicAdd(base[b] + 64 * edge_o(b, a), kept(keep[b], ev[a][b]));
         }
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-      if (in[c]) atomicAdd(base[c] + 64 * 15, mv[c]);
+    for (int c = 0; c < 8; ++c) atomicAdd(base[c] + 64 * 15, kept(keep[c], mv[c]));
   };
 
   // ---- walk the cube layers upwards (coordinates staged one layer ahead)
+  // the node layers of cube layer zc sit in buffers zc & 1 and (zc + 1) & 1;
+  // layer zc + 2's coordinates are loaded at the top of iteration zc and
+  // staged at its end (into buffer zc & 1, read for the last time by the
+  // cubes): their wait then counts past the flush's stores (vmcnt(N)), and no
+  // wait sits at the loop head, where the entry and the back edge would merge
+  // into the stricter one
   load_layer(zc_first);
   store_layer(zc_first & 1);
   load_layer(zc_first + 1);
-  for (int zc = zc_first; zc <= zc_last; ++zc) {
-    store_layer((zc + 1) & 1);
-    load_layer(zc + 2);  // in flight during this layer's cubes
-    prefetch_rows(zc);   // the offsets of the rows this iteration completes
+  store_layer((zc_first + 1) & 1);
+  int zc = zc_first;
+  if (zc < z0) {  // the cube layer below the segment: its top corners only, no flush
+    load_layer(zc + 2);
     __syncthreads();
     cubes(zc);
     __syncthreads();
-    if (zc >= z0 && zc < z1) flush(zc);
+    store_layer(zc & 1);
+    ++zc;
+  }
+  // every layer of the loop completes a node layer of the segment (z0 <= zc
+  // <= zc_last < z1): the flush is unconditional, so the offsets' prefetch
+  // stays ahead of the cubes
+  for (; zc <= zc_last; ++zc) {
+    // the offsets of the rows this iteration completes, then the coordinates
+    // of layer zc + 2: the flush waits for the offsets only (counted vmcnt)
+    prefetch_rows(zc);
+    load_layer(zc + 2);
+    __syncthreads();
+    cubes(zc);
+    __syncthreads();
+    flush(zc);
+    store_layer(zc & 1);
   }
   if (zc_last + 1 >= z0 && zc_last + 1 < z1) {  // the box's top layer (no cube above)
     prefetch_rows(zc_last + 1);
@@ -394,8 +434,10 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   g.f_meas = f / 24.0;
   const int64_t n_units = (int64_t)g.tx * g.ty * g.ns;
   AFEM_REQUIRE(n_units < (int64_t(1) << 31), AFEM_ERR_LIMIT, "cube kernel: too many units");
-  hipLaunchKernelGGL(k_assemble_cubes, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, b.s.row_ptr.p,
-                     m.coords.p, b.values.p, rhs, rhs_add);
+  auto* kern = rhs ? (rhs_add ? &k_assemble_cubes<true, true> : &k_assemble_cubes<true, false>)
+                  : &k_assemble_cubes<false, false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, b.s.row_ptr.p, m.coords.p,
+                     b.values.p, rhs);
   AFEM_LAUNCHED();
   b.last_kernel = AFEM_KERNEL_CUBES;
   return true;
