@@ -129,12 +129,12 @@ constexpr int kAcc = 16;   // accumulators per row: 15 offsets + |det| sum
 // HAS_RHS / RHS_ADD at compile time: the flush's global stores are then a
 // fixed, branch-free sequence, so the waits for the next layer's coordinates
 // count past them (vmcnt(N)) instead of draining them (vmcnt(0))
-template <bool HAS_RHS, bool RHS_ADD>
+template <int STRIDE, bool HAS_RHS, bool RHS_ADD>
 __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
                                                        const double* __restrict__ coords,
                                                        double* __restrict__ vals, double* __restrict__ rhs)
 {
-  __shared__ __align__(16) double acc[2][kAcc][64];
+  __shared__ __align__(16) double acc[2][kAcc][STRIDE];  // STRIDE >= 49 rows per offset plane
   __shared__ double cz[2][3][kCol * kCol];  // SoA coordinates of two node layers
   const int lane = threadIdx.x;
   // XCD-aware: blocks go round-robin over the 8 XCDs; XCD x takes the x-th
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
       cz[buf][2][q] = pre[h][2];
     }
   };
-  for (int i = lane; i < 2 * kAcc * 64; i += 64) (&acc[0][0][0])[i] = 0.0;
+  for (int i = lane; i < 2 * kAcc * STRIDE; i += 64) (&acc[0][0][0])[i] = 0.0;
 
   // ---- node layer z complete: write its 49 rows (values compacted by the present neighbours) + RHS.
   // The rows' offsets are loaded before the layer's cubes (prefetch_rows), so
@@ -226,13 +226,14 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
     const int s2 = (lm < lp ? n0 : 0) + (l0 < lp ? n1 : 0);
     double v[15];
     double sum = 0.0;
+    const int lr = min(lane, STRIDE - 1);  // lanes past the 49 rows read a row they do not use
 #pragma unroll
     for (int o = 0; o < 15; ++o) {
-      v[o] = acc[b][o][lane];
+      v[o] = acc[b][o][lr];
       if (o != 7 && ((mask >> o) & 1u)) sum += v[o];
     }
     v[7] = -sum;
-    const double meas = acc[b][15][lane];
+    const double meas = acc[b][15][lr];
     // the prefetched offsets are consumed without a branch (selects), so the
     // compiler keeps their load where prefetch_rows issued it
     const int64_t rb = valid ? pf_rb : 0;
@@ -291,7 +292,7 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kAcc; ++i) img[64 * i + lane] = 0.0;
+    for (int i = 0; i < (kAcc * STRIDE + 63) / 64; ++i) img[min(64 * i + lane, kAcc * STRIDE - 1)] = 0.0;
     __syncthreads();
   };
 
@@ -342,27 +343,32 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
     // each corner's accumulator row: its own when it is a row of this unit,
     // else the clamped row inside the column (then the lane adds zeros: x + 0
     // = x, the sums are unchanged); every add runs unpredicated
-    uint64_t keep[8];
-    double* base[8];
+    // (the corners' rows from the cube's lower corner row: +1 in x, +kRun in y)
+    const int rx0 = ci - 1, ry0 = cj - 1;
+    const bool zlo = zc >= z0, zhi = zc + 1 < z1;
+    const bool xin0 = rx0 >= 0, xin1 = rx0 + 1 < kRun && cx0 + rx0 + 1 < g.np1;
+    const bool yin0 = ry0 >= 0, yin1 = ry0 + 1 < kRun && cy0 + ry0 + 1 < g.np1;
+    uint32_t inm = 0;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      const int rx = ci - 1 + cbit(c, 0), ry = cj - 1 + cbit(c, 1), z = zc + cbit(c, 2);
-      const bool in = cube_in & (rx >= 0) & (ry >= 0) & (rx < kRun) & (ry < kRun) & (cx0 + rx < g.np1) &
-                      (cy0 + ry < g.np1) & (z >= z0) & (z < z1);
-      keep[c] = in ? ~0ull : 0ull;
-      base[c] = &acc[cbit(c, 2) ? bt : bb][0][0] + min(max(rx, 0), kRun - 1) + kRun * min(max(ry, 0), kRun - 1);
+      const bool in = cube_in && (cbit(c, 0) ? xin1 : xin0) && (cbit(c, 1) ? yin1 : yin0) && (cbit(c, 2) ? zhi : zlo);
+      inm |= (uint32_t)in << c;
     }
-    auto kept = [](uint64_t m, double x) { return __longlong_as_double((long long)(m & (uint64_t)__double_as_longlong(x))); };
+    const int bx0 = max(rx0, 0), bx1 = min(rx0 + 1, kRun - 1), by0 = max(ry0, 0), by1 = min(ry0 + 1, kRun - 1);
+    auto base_of = [&](int c) {
+      return &acc[cbit(c, 2) ? bt : bb][0][0] + (cbit(c, 0) ? bx1 : bx0) + kRun * (cbit(c, 1) ? by1 : by0);
+    };
+    auto kept = [&](int c, double x) { return ((inm >> c) & 1u) ? x : 0.0; };
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
       for (int b = a + 1; b < 8; ++b)
         if (is_edge(a, b)) {
-          atomicAdd(base[a] + 64 * edge_o(a, b), kept(keep[a], ev[a][b]));
-          atomicAdd(base[b] + 64 * edge_o(b, a), kept(keep[b], ev[a][b]));
+          atomicAdd(base_of(a) + STRIDE * edge_o(a, b), kept(a, ev[a][b]));
+          atomicAdd(base_of(b) + STRIDE * edge_o(b, a), kept(b, ev[a][b]));
         }
 #pragma unroll
-    for (int c = 0; c < 8; ++c) atomicAdd(base[c] + 64 * 15, kept(keep[c], mv[c]));
+    for (int c = 0; c < 8; ++c) atomicAdd(base_of(c) + STRIDE * 15, kept(c, mv[c]));
   };
 
   // ---- walk the cube layers upwards (coordinates staged one layer ahead)
@@ -434,8 +440,13 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   g.f_meas = f / 24.0;
   const int64_t n_units = (int64_t)g.tx * g.ty * g.ns;
   AFEM_REQUIRE(n_units < (int64_t(1) << 31), AFEM_ERR_LIMIT, "cube kernel: too many units");
-  auto* kern = rhs ? (rhs_add ? &k_assemble_cubes<true, true> : &k_assemble_cubes<true, false>)
-                  : &k_assemble_cubes<false, false>;
+  // accumulator planes of 64 rows, or of 49 (12.3 instead of 16 KB of LDS: AFEM_CUBES_STRIDE=49)
+  const char* se = variant("AFEM_CUBES_STRIDE");
+  const bool s49 = se && atoi(se) == 49;
+  auto* kern = s49 ? (rhs ? (rhs_add ? &k_assemble_cubes<49, true, true> : &k_assemble_cubes<49, true, false>)
+                          : &k_assemble_cubes<49, false, false>)
+                   : (rhs ? (rhs_add ? &k_assemble_cubes<64, true, true> : &k_assemble_cubes<64, true, false>)
+                          : &k_assemble_cubes<64, false, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, b.s.row_ptr.p, m.coords.p,
                      b.values.p, rhs);
   AFEM_LAUNCHED();
