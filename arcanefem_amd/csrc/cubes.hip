@@ -354,9 +354,16 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
       const bool in = cube_in && (cbit(c, 0) ? xin1 : xin0) && (cbit(c, 1) ? yin1 : yin0) && (cbit(c, 2) ? zhi : zlo);
       inm |= (uint32_t)in << c;
     }
-    const int bx0 = max(rx0, 0), bx1 = min(rx0 + 1, kRun - 1), by0 = max(ry0, 0), by1 = min(ry0 + 1, kRun - 1);
+    // a corner outside the unit adds its zero into the OTHER node layer's
+    // buffer at row lane (mod STRIDE): no address shared with the lanes adding
+    // real values in the same instruction, none shared among the outside lanes
+    // (a clamped row inside the column serialised the same-address adds of
+    // neighbouring lanes: 0.73 -> 0.82 ms)
+    const int r00 = rx0 + kRun * ry0, rs = lane % STRIDE;
     auto base_of = [&](int c) {
-      return &acc[cbit(c, 2) ? bt : bb][0][0] + (cbit(c, 0) ? bx1 : bx0) + kRun * (cbit(c, 1) ? by1 : by0);
+      const bool in = (inm >> c) & 1u;
+      const int buf = (cbit(c, 2) ? bt : bb) ^ (in ? 0 : 1);
+      return &acc[buf][0][0] + (in ? r00 + cbit(c, 0) + kRun * cbit(c, 1) : rs);
     };
     auto kept = [&](int c, double x) { return ((inm >> c) & 1u) ? x : 0.0; };
 #pragma unroll
