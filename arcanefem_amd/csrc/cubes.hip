@@ -21,7 +21,8 @@
 // evaluations per cube, plus 1/zs for the cube layer below a segment).  The
 // unit walks the cube layers upwards: node layer z's rows take the cube layers
 // z-1 and z, so two row-layer accumulator buffers (by parity) live in LDS,
-// [16][64] doubles each (15 column offsets in sorted order + the |det| sum),
+// [15][STRIDE] doubles each (15 column offsets in sorted order; the diagonal's
+// plane, never added to, holds the |det| sum),
 // and the node coordinates of the two layers of the current cube layer
 // (9 x 9 nodes each, staged from registers loaded one layer ahead).  When a
 // node layer is complete its 49 rows are written once: the values compacted
@@ -124,13 +125,16 @@ __host__ __device__ constexpr bool is_edge(int a, int b)
 constexpr int kRun = 7;    // rows per x-run of a column
 constexpr int kRows = 49;  // rows per column layer
 constexpr int kCol = 9;    // staged nodes per x / y line (the column's rows + 1 halo line below)
-constexpr int kAcc = 16;   // accumulators per row: 15 offsets + |det| sum
+constexpr int kAcc = 15;   // accumulators per row: 15 offsets, the diagonal's (7, never added to:
+                           // v_7 = -sum of the others) holds the row's |det| sum
 
 // HAS_RHS / RHS_ADD at compile time: the flush's global stores are then a
 // fixed, branch-free sequence, so the waits for the next layer's coordinates
 // count past them (vmcnt(N)) instead of draining them (vmcnt(0))
+// amdgpu_waves_per_eu(3): 168 VGPRs, with the 49-row planes' 15.6 KB of LDS
+// 10 waves per CU (the 64-row planes' 19.3 KB keep 8 whatever the registers)
 template <int STRIDE, bool HAS_RHS, bool RHS_ADD>
-__global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
                                                        const double* __restrict__ coords,
                                                        double* __restrict__ vals, double* __restrict__ rhs)
 {
@@ -232,8 +236,8 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
       v[o] = acc[b][o][lr];
       if (o != 7 && ((mask >> o) & 1u)) sum += v[o];
     }
+    const double meas = v[7];
     v[7] = -sum;
-    const double meas = acc[b][15][lr];
     // the prefetched offsets are consumed without a branch (selects), so the
     // compiler keeps their load where prefetch_rows issued it
     const int64_t rb = valid ? pf_rb : 0;
@@ -375,7 +379,7 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
           atomicAdd(base_of(b) + STRIDE * edge_o(b, a), kept(b, ev[a][b]));
         }
 #pragma unroll
-    for (int c = 0; c < 8; ++c) atomicAdd(base_of(c) + STRIDE * 15, kept(c, mv[c]));
+    for (int c = 0; c < 8; ++c) atomicAdd(base_of(c) + STRIDE * 7, kept(c, mv[c]));  // the |det| sums
   };
 
   // ---- walk the cube layers upwards (coordinates staged one layer ahead)
@@ -405,9 +409,9 @@ __global__ __launch_bounds__(64) void k_assemble_cubes(CubeGeom g, const int64_t
     // the offsets of the rows this iteration completes, then the coordinates
     // of layer zc + 2: the flush waits for the offsets only (counted vmcnt)
     prefetch_rows(zc);
-    load_layer(zc + 2);
     __syncthreads();
     cubes(zc);
+    load_layer(zc + 2);  // after the cubes: its 12 registers are not live across them
     __syncthreads();
     flush(zc);
     store_layer(zc & 1);
