@@ -445,15 +445,18 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   if (g.n_own_layers <= 0 || g.L != (int64_t)g.np1 * g.np1 || g.nzc < 1) return false;
   g.tx = g.ty = (g.np1 + kRun - 1) / kRun;
   const char* ze = variant("AFEM_CUBES_ZS");
-  g.zs = std::max(1, ze ? atoi(ze) : 16);
+  // z segment: ~n/16 layers (C2 n = 215: 13, C4 n = 463: 29; r04x: zs 12 0.645 ms
+  // vs zs 8 0.649 at C2, zs 32 6.38 vs zs 24 6.81 ms at C4)
+  g.zs = std::max(1, ze ? atoi(ze) : std::min(48, std::max(8, g.np1 / 16)));
   g.ns = (g.n_own_layers + g.zs - 1) / g.zs;
   g.s_coef = coef / 6.0;
   g.f_meas = f / 24.0;
   const int64_t n_units = (int64_t)g.tx * g.ty * g.ns;
   AFEM_REQUIRE(n_units < (int64_t(1) << 31), AFEM_ERR_LIMIT, "cube kernel: too many units");
-  // accumulator planes of 64 rows, or of 49 (12.3 instead of 16 KB of LDS: AFEM_CUBES_STRIDE=49)
+  // accumulator planes of 49 rows (15.6 KB of LDS: 10 waves per CU), or of 64
+  // (AFEM_CUBES_STRIDE=64: 19.3 KB, 8 waves)
   const char* se = variant("AFEM_CUBES_STRIDE");
-  const bool s49 = se && atoi(se) == 49;
+  const bool s49 = !(se && atoi(se) == 64);
   auto* kern = s49 ? (rhs ? (rhs_add ? &k_assemble_cubes<49, true, true> : &k_assemble_cubes<49, true, false>)
                           : &k_assemble_cubes<49, false, false>)
                    : (rhs ? (rhs_add ? &k_assemble_cubes<64, true, true> : &k_assemble_cubes<64, true, false>)
