@@ -40,6 +40,10 @@
 
 #include <algorithm>
 
+// the 64-row instances cannot reach the 3-waves register target (their LDS
+// allows 2 per SIMD): the compiler says so for each; expected
+#pragma clang diagnostic ignored "-Wpass-failed"
+
 namespace afem {
 
 namespace {
