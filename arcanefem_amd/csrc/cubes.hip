@@ -137,7 +137,7 @@ constexpr int kAcc = 15;   // accumulators per row: 15 offsets, the diagonal's (
 // count past them (vmcnt(N)) instead of draining them (vmcnt(0))
 // amdgpu_waves_per_eu(3): 168 VGPRs, with the 49-row planes' 15.6 KB of LDS
 // 10 waves per CU (the 64-row planes' 19.3 KB keep 8 whatever the registers)
-template <int STRIDE, bool HAS_RHS, bool RHS_ADD>
+template <int STRIDE, bool CARRY, bool HAS_RHS, bool RHS_ADD>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
                                                        const double* __restrict__ coords,
                                                        double* __restrict__ vals, double* __restrict__ rhs)
@@ -305,6 +305,51 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   };
 
   // ---- cube layer zc: the lane's cube, its 6 tets, 19 edge sums and 8 corner |det| sums
+  // CARRY: the top face of the lane's cube (5 edges, 4 corner |det| sums) is
+  // the bottom face of its next cube layer, evaluated by the same lane: its
+  // sums stay in registers and go into LDS once, with the next cube's
+  double ce[5] = { 0.0, 0.0, 0.0, 0.0, 0.0 }, cm[4] = { 0.0, 0.0, 0.0, 0.0 };
+  // the corners' accumulator rows for cube layer zc
+  auto corner_frame = [&](int zc, uint32_t& inm, int& bb, int& bt) {
+    bb = zc & 1;
+    bt = (zc + 1) & 1;
+    const int rx0 = ci - 1, ry0 = cj - 1;
+    const bool zlo = zc >= z0, zhi = zc + 1 < z1;
+    const bool xin0 = rx0 >= 0, xin1 = rx0 + 1 < kRun && cx0 + rx0 + 1 < g.np1;
+    const bool yin0 = ry0 >= 0, yin1 = ry0 + 1 < kRun && cy0 + ry0 + 1 < g.np1;
+    inm = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const bool in = cube_in && (cbit(c, 0) ? xin1 : xin0) && (cbit(c, 1) ? yin1 : yin0) && (cbit(c, 2) ? zhi : zlo);
+      inm |= (uint32_t)in << c;
+    }
+  };
+  // a corner outside the unit adds its zero into the OTHER node layer's
+  // buffer at row lane (mod STRIDE): no address shared with the lanes adding
+  // real values in the same instruction, none shared among the outside lanes
+  // (a clamped row inside the column serialised the same-address adds of
+  // neighbouring lanes: 0.73 -> 0.82 ms)
+  const int r00 = (ci - 1) + kRun * (cj - 1), rs = lane % STRIDE;
+  auto base_at = [&](uint32_t inm, int bb, int bt, int c) {
+    const bool in = (inm >> c) & 1u;
+    const int buf = (cbit(c, 2) ? bt : bb) ^ (in ? 0 : 1);
+    return &acc[buf][0][0] + (in ? r00 + cbit(c, 0) + kRun * cbit(c, 1) : rs);
+  };
+  // the top face's carried sums into LDS (the box's top node layer: no cube above)
+  auto add_top = [&](int zc) {
+    uint32_t inm;
+    int bb, bt;
+    corner_frame(zc, inm, bb, bt);
+    auto kept = [&](int c, double x) { return ((inm >> c) & 1u) ? x : 0.0; };
+    constexpr int ta[5] = { 4, 4, 4, 5, 6 }, tb[5] = { 5, 6, 7, 7, 7 };
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      atomicAdd(base_at(inm, bb, bt, ta[i]) + STRIDE * edge_o(ta[i], tb[i]), kept(ta[i], ce[i]));
+      atomicAdd(base_at(inm, bb, bt, tb[i]) + STRIDE * edge_o(tb[i], ta[i]), kept(tb[i], ce[i]));
+    }
+#pragma unroll
+    for (int c = 4; c < 8; ++c) atomicAdd(base_at(inm, bb, bt, c) + STRIDE * 7, kept(c, cm[c - 4]));
+  };
   auto cubes = [&](int zc) {
     // no branch around the cube: a lane whose cube is outside the box works on
     // its clamped (duplicated) coordinates and adds zeros -- a divergent region
@@ -348,42 +393,40 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
         }
       }
     }
-    // each corner's accumulator row: its own when it is a row of this unit,
-    // else the clamped row inside the column (then the lane adds zeros: x + 0
-    // = x, the sums are unchanged); every add runs unpredicated
-    // (the corners' rows from the cube's lower corner row: +1 in x, +kRun in y)
-    const int rx0 = ci - 1, ry0 = cj - 1;
-    const bool zlo = zc >= z0, zhi = zc + 1 < z1;
-    const bool xin0 = rx0 >= 0, xin1 = rx0 + 1 < kRun && cx0 + rx0 + 1 < g.np1;
-    const bool yin0 = ry0 >= 0, yin1 = ry0 + 1 < kRun && cy0 + ry0 + 1 < g.np1;
-    uint32_t inm = 0;
+    if constexpr (CARRY) {
+      // bottom face = the previous cube layer's top face: its carried sums
+      ev[0][1] += ce[0];
+      ev[0][2] += ce[1];
+      ev[0][3] += ce[2];
+      ev[1][3] += ce[3];
+      ev[2][3] += ce[4];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const bool in = cube_in && (cbit(c, 0) ? xin1 : xin0) && (cbit(c, 1) ? yin1 : yin0) && (cbit(c, 2) ? zhi : zlo);
-      inm |= (uint32_t)in << c;
+      for (int c = 0; c < 4; ++c) mv[c] += cm[c];
+      ce[0] = ev[4][5];
+      ce[1] = ev[4][6];
+      ce[2] = ev[4][7];
+      ce[3] = ev[5][7];
+      ce[4] = ev[6][7];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) cm[c] = mv[c + 4];
     }
-    // a corner outside the unit adds its zero into the OTHER node layer's
-    // buffer at row lane (mod STRIDE): no address shared with the lanes adding
-    // real values in the same instruction, none shared among the outside lanes
-    // (a clamped row inside the column serialised the same-address adds of
-    // neighbouring lanes: 0.73 -> 0.82 ms)
-    const int r00 = rx0 + kRun * ry0, rs = lane % STRIDE;
-    auto base_of = [&](int c) {
-      const bool in = (inm >> c) & 1u;
-      const int buf = (cbit(c, 2) ? bt : bb) ^ (in ? 0 : 1);
-      return &acc[buf][0][0] + (in ? r00 + cbit(c, 0) + kRun * cbit(c, 1) : rs);
-    };
+    // each corner's accumulator row: its own when it is a row of this unit,
+    // else a zero into the other buffer (base_at); every add runs unpredicated
+    uint32_t inm;
+    int bb_, bt_;
+    corner_frame(zc, inm, bb_, bt_);
     auto kept = [&](int c, double x) { return ((inm >> c) & 1u) ? x : 0.0; };
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
       for (int b = a + 1; b < 8; ++b)
-        if (is_edge(a, b)) {
-          atomicAdd(base_of(a) + STRIDE * edge_o(a, b), kept(a, ev[a][b]));
-          atomicAdd(base_of(b) + STRIDE * edge_o(b, a), kept(b, ev[a][b]));
+        if (is_edge(a, b) && !(CARRY && cbit(a, 2) && cbit(b, 2))) {
+          atomicAdd(base_at(inm, bb_, bt_, a) + STRIDE * edge_o(a, b), kept(a, ev[a][b]));
+          atomicAdd(base_at(inm, bb_, bt_, b) + STRIDE * edge_o(b, a), kept(b, ev[a][b]));
         }
 #pragma unroll
-    for (int c = 0; c < 8; ++c) atomicAdd(base_of(c) + STRIDE * 7, kept(c, mv[c]));  // the |det| sums
+    for (int c = 0; c < 8; ++c)
+      if (!(CARRY && cbit(c, 2))) atomicAdd(base_at(inm, bb_, bt_, c) + STRIDE * 7, kept(c, mv[c]));  // |det| sums
   };
 
   // ---- walk the cube layers upwards (coordinates staged one layer ahead)
@@ -422,6 +465,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   }
   if (zc_last + 1 >= z0 && zc_last + 1 < z1) {  // the box's top layer (no cube above)
     prefetch_rows(zc_last + 1);
+    if constexpr (CARRY) {
+      add_top(zc_last);
+      __syncthreads();
+    }
     flush(zc_last + 1);
   }
 }
@@ -461,10 +508,14 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   // (AFEM_CUBES_STRIDE=64: 19.3 KB, 8 waves)
   const char* se = variant("AFEM_CUBES_STRIDE");
   const bool s49 = !(se && atoi(se) == 64);
-  auto* kern = s49 ? (rhs ? (rhs_add ? &k_assemble_cubes<49, true, true> : &k_assemble_cubes<49, true, false>)
-                          : &k_assemble_cubes<49, false, false>)
-                   : (rhs ? (rhs_add ? &k_assemble_cubes<64, true, true> : &k_assemble_cubes<64, true, false>)
-                          : &k_assemble_cubes<64, false, false>);
+  // the top face's sums carried in registers to the next cube layer (AFEM_CUBES_CARRY=1)
+  const char* ke = variant("AFEM_CUBES_CARRY");
+  const bool carry = ke && atoi(ke) == 1;
+#define AFEM_CUBES_K(S, C) (rhs ? (rhs_add ? &k_assemble_cubes<S, C, true, true> : &k_assemble_cubes<S, C, true, false>) \
+                            : &k_assemble_cubes<S, C, false, false>)
+  auto* kern = s49 ? (carry ? AFEM_CUBES_K(49, true) : AFEM_CUBES_K(49, false))
+                   : (carry ? AFEM_CUBES_K(64, true) : AFEM_CUBES_K(64, false));
+#undef AFEM_CUBES_K
   hipLaunchKernelGGL(kern, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, b.s.row_ptr.p, m.coords.p,
                      b.values.p, rhs);
   AFEM_LAUNCHED();
