@@ -504,13 +504,14 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   g.f_meas = f / 24.0;
   const int64_t n_units = (int64_t)g.tx * g.ty * g.ns;
   AFEM_REQUIRE(n_units < (int64_t(1) << 31), AFEM_ERR_LIMIT, "cube kernel: too many units");
-  // accumulator planes of 49 rows (15.6 KB of LDS: 10 waves per CU), or of 64
-  // (AFEM_CUBES_STRIDE=64: 19.3 KB, 8 waves)
+  // accumulator planes of 64 rows (19.3 KB of LDS, 8 waves per CU), or of 49
+  // (AFEM_CUBES_STRIDE=49: 15.6 KB, 10 waves -- with the carry it spills: r04y)
   const char* se = variant("AFEM_CUBES_STRIDE");
-  const bool s49 = !(se && atoi(se) == 64);
-  // the top face's sums carried in registers to the next cube layer (AFEM_CUBES_CARRY=1)
+  const bool s49 = se && atoi(se) == 49;
+  // the top face's sums carried in registers to the next cube layer (AFEM_CUBES_CARRY=0: not;
+  // r04y C2: 0.605 ms with the carry at 64-row planes, 0.660 without at 49)
   const char* ke = variant("AFEM_CUBES_CARRY");
-  const bool carry = ke && atoi(ke) == 1;
+  const bool carry = !(ke && atoi(ke) == 0);
 #define AFEM_CUBES_K(S, C) (rhs ? (rhs_add ? &k_assemble_cubes<S, C, true, true> : &k_assemble_cubes<S, C, true, false>) \
                             : &k_assemble_cubes<S, C, false, false>)
   auto* kern = s49 ? (carry ? AFEM_CUBES_K(49, true) : AFEM_CUBES_K(49, false))

@@ -153,14 +153,15 @@ def test_cube_kernel_matches_oracle(ctx, variant, n, nz, zs):
     assert np.abs(ls.rhs_host() - rhs).max() <= VAL_TOL * np.abs(rhs).max()
 
 
-@pytest.mark.parametrize("nranks,stride", [(2, "49"), (3, "49"), (3, "64")])
-def test_cube_kernel_on_slabs(ctx, variant, nranks, stride):
+@pytest.mark.parametrize("nranks,stride,carry", [(2, "64", "1"), (3, "64", "1"), (3, "49", "0"), (2, "64", "0")])
+def test_cube_kernel_on_slabs(ctx, variant, nranks, stride, carry):
     """z-slab subdomains (owned layers, then the ghost layer below, then the one
     above: a row next to the ghost layer below has its -z columns LAST in id
     order): every slab's matrix and RHS against the oracle on the same
     subdomain, through the cube kernel."""
     variant("AFEM_ASSEMBLY_CUBES", "1")  # opt-in
-    variant("AFEM_CUBES_STRIDE", stride)  # accumulator planes of 49 (default) or 64 rows
+    variant("AFEM_CUBES_STRIDE", stride)  # accumulator planes of 64 (default) or 49 rows
+    variant("AFEM_CUBES_CARRY", carry)  # top-face sums carried in registers (default) or not
     for rank in range(nranks):
         mesh = af.Mesh.structured(ctx, 3, 9, nz=11, jitter=0.2, seed=13, nranks=nranks, rank=rank)
         bsr, ls = _assemble_gpu(ctx, mesh, 2.5)
