@@ -137,7 +137,7 @@ constexpr int kAcc = 15;   // accumulators per row: 15 offsets, the diagonal's (
 // count past them (vmcnt(N)) instead of draining them (vmcnt(0))
 // amdgpu_waves_per_eu(3): 168 VGPRs, with the 49-row planes' 15.6 KB of LDS
 // 10 waves per CU (the 64-row planes' 19.3 KB keep 8 whatever the registers)
-template <int STRIDE, bool CARRY, bool HAS_RHS, bool RHS_ADD>
+template <int STRIDE, bool CARRY, bool XEX, bool HAS_RHS, bool RHS_ADD>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
                                                        const double* __restrict__ coords,
                                                        double* __restrict__ vals, double* __restrict__ rhs)
@@ -410,6 +410,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 #pragma unroll
       for (int c = 0; c < 4; ++c) cm[c] = mv[c + 4];
     }
+    if constexpr (XEX) {
+      // the x = 1 face of this lane's cube is the x = 0 face of lane + 1's
+      // (same 16-lane DPP row; a lane with ci = 7 gets a wrong neighbour but its
+      // x = 1 corners are outside the unit): that lane's face sums come over
+      // (row_shl:1, zero if its cube is outside the box) and this lane adds
+      // both -- 4 edges and 2 corners of the bottom layer (the top face's are
+      // carried, and exchanged as the next layer's bottom)
+      auto from_next = [&](double x) {
+        const long long v = __double_as_longlong(cube_in ? x : 0.0);
+        const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, 0x101, 0xf, 0xf, true);
+        const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((unsigned long long)v >> 32), 0x101, 0xf, 0xf, true);
+        return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
+      };
+      ev[1][3] += from_next(ev[0][2]);
+      ev[1][5] += from_next(ev[0][4]);
+      ev[1][7] += from_next(ev[0][6]);
+      ev[3][7] += from_next(ev[2][6]);
+      mv[1] += from_next(mv[0]);
+      mv[3] += from_next(mv[2]);
+    }
     // each corner's accumulator row: its own when it is a row of this unit,
     // else a zero into the other buffer (base_at); every add runs unpredicated
     uint32_t inm;
@@ -420,13 +440,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     for (int a = 0; a < 8; ++a)
 #pragma unroll
       for (int b = a + 1; b < 8; ++b)
-        if (is_edge(a, b) && !(CARRY && cbit(a, 2) && cbit(b, 2))) {
+        if (is_edge(a, b) && !(CARRY && cbit(a, 2) && cbit(b, 2)) &&
+            !(XEX && !cbit(a, 0) && !cbit(b, 0) && !(cbit(a, 2) && cbit(b, 2)))) {
           atomicAdd(base_at(inm, bb_, bt_, a) + STRIDE * edge_o(a, b), kept(a, ev[a][b]));
           atomicAdd(base_at(inm, bb_, bt_, b) + STRIDE * edge_o(b, a), kept(b, ev[a][b]));
         }
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      if (!(CARRY && cbit(c, 2))) atomicAdd(base_at(inm, bb_, bt_, c) + STRIDE * 7, kept(c, mv[c]));  // |det| sums
+      if (!(CARRY && cbit(c, 2)) && !(XEX && !cbit(c, 0) && !cbit(c, 2)))
+        atomicAdd(base_at(inm, bb_, bt_, c) + STRIDE * 7, kept(c, mv[c]));  // |det| sums
   };
 
   // ---- walk the cube layers upwards (coordinates staged one layer ahead)
@@ -509,13 +531,17 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   const char* se = variant("AFEM_CUBES_STRIDE");
   const bool s49 = se && atoi(se) == 49;
   // the top face's sums carried in registers to the next cube layer (AFEM_CUBES_CARRY=0: not;
-  // r04y C2: 0.605 ms with the carry at 64-row planes, 0.660 without at 49)
+  // r04y C2: 0.605 ms with the carry at 64-row planes, 0.660 without at 49); the x = 1 face's
+  // shared with lane + 1 over DPP (AFEM_CUBES_XEX=0: not; needs the carry)
   const char* ke = variant("AFEM_CUBES_CARRY");
   const bool carry = !(ke && atoi(ke) == 0);
-#define AFEM_CUBES_K(S, C) (rhs ? (rhs_add ? &k_assemble_cubes<S, C, true, true> : &k_assemble_cubes<S, C, true, false>) \
-                            : &k_assemble_cubes<S, C, false, false>)
-  auto* kern = s49 ? (carry ? AFEM_CUBES_K(49, true) : AFEM_CUBES_K(49, false))
-                   : (carry ? AFEM_CUBES_K(64, true) : AFEM_CUBES_K(64, false));
+  const char* xe = variant("AFEM_CUBES_XEX");
+  const bool xex = carry && !(xe && atoi(xe) == 0);
+#define AFEM_CUBES_K(S, C, X)                                                                                        \
+  (rhs ? (rhs_add ? &k_assemble_cubes<S, C, X, true, true> : &k_assemble_cubes<S, C, X, true, false>)                \
+       : &k_assemble_cubes<S, C, X, false, false>)
+  auto* kern = carry ? (xex ? AFEM_CUBES_K(64, true, true) : AFEM_CUBES_K(64, true, false))
+                     : (s49 ? AFEM_CUBES_K(49, false, false) : AFEM_CUBES_K(64, false, false));
 #undef AFEM_CUBES_K
   hipLaunchKernelGGL(kern, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, b.s.row_ptr.p, m.coords.p,
                      b.values.p, rhs);
