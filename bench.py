@@ -176,7 +176,8 @@ def make_step(ctx, bsr, ls, bottom, dbottom):
 def roofline(bsr, mesh, kernel_ms):
     st = bsr.stats()
     # the instances the assembly launches: uniform slices, compact general
-    # slices, big general slices (> 16 slots / > 352 nodes, assembly.hip)
+    # slices, big general slices (> 16 slots / > 352 nodes, assembly.hip);
+    # generator boxes under the cell-first kernel: k_assemble_cubes alone
     names = ["k_assemble_stencil<kSigKuhn3D>"] if st["stencil_slices"] > 0 else []
     if st["uniform_instance_slices"] > 0 or (st["stencil_slices"] == 0 and st["uniform_slices"] > 0):
         names.append("k_assemble_strip<4,2,16,uniform>")
@@ -184,6 +185,8 @@ def roofline(bsr, mesh, kernel_ms):
         names.append("k_assemble_strip<4,2,16,general>")
     if st["max_slice_width"] > 16 or st["max_slice_nodes"] > 352:
         names.append("k_assemble_strip<4,4,32,general>")
+    if st.get("last_kernel") == 10:  # AFEM_KERNEL_CUBES (cubes.hip)
+        names = ["k_assemble_cubes"]
     kname = " + ".join(names)
     nnz = bsr.view().nnz_blocks
     ab = algorithmic_bytes(int(st["n_incidences"]), mesh.n_nodes, mesh.n_own_nodes, nnz)
