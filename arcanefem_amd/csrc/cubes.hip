@@ -315,12 +315,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     bt = (zc + 1) & 1;
     const int rx0 = ci - 1, ry0 = cj - 1;
     const bool zlo = zc >= z0, zhi = zc + 1 < z1;
-    const bool xin0 = rx0 >= 0, xin1 = rx0 + 1 < kRun && cx0 + rx0 + 1 < g.np1;
-    const bool yin0 = ry0 >= 0, yin1 = ry0 + 1 < kRun && cy0 + ry0 + 1 < g.np1;
+    const bool xin0 = rx0 >= 0 && cx0 + rx0 < g.np1, xin1 = rx0 + 1 < kRun && cx0 + rx0 + 1 < g.np1;
+    const bool yin0 = ry0 >= 0 && cy0 + ry0 < g.np1, yin1 = ry0 + 1 < kRun && cy0 + ry0 + 1 < g.np1;
     inm = 0;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      const bool in = cube_in && (cbit(c, 0) ? xin1 : xin0) && (cbit(c, 1) ? yin1 : yin0) && (cbit(c, 2) ? zhi : zlo);
+      // (not the lane's cube_in: with the x exchange a corner row takes the
+      // neighbour's sums even when this lane's cube is outside the box)
+      const bool in = (cbit(c, 0) ? xin1 : xin0) && (cbit(c, 1) ? yin1 : yin0) && (cbit(c, 2) ? zhi : zlo);
       inm |= (uint32_t)in << c;
     }
   };
@@ -380,8 +382,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       k[2] = pcross(e3, e1);
       k[3] = pcross(e1, e2);
       k[0] = P3{ -(k[1].x + k[2].x + k[3].x), -(k[1].y + k[2].y + k[3].y), -(k[1].z + k[2].z + k[3].z) };
-      const double meas = fabs(pdot(e1, k[1]));
-      const double s = g.s_coef * precip(fmax(meas, 1e-300));
+      // a cube outside the box (clamped, duplicated coordinates) contributes
+      // exact zeros: its corners' rows may still take the x-neighbour's sums
+      const double meas = cube_in ? fabs(pdot(e1, k[1])) : 0.0;
+      const double s = cube_in ? g.s_coef * precip(fmax(meas, 1e-300)) : 0.0;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         mv[tet_v(t, p)] += meas;
@@ -414,11 +418,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       // the x = 1 face of this lane's cube is the x = 0 face of lane + 1's
       // (same 16-lane DPP row; a lane with ci = 7 gets a wrong neighbour but its
       // x = 1 corners are outside the unit): that lane's face sums come over
-      // (row_shl:1, zero if its cube is outside the box) and this lane adds
+      // (row_shl:1; zeros from a cube outside the box) and this lane adds
       // both -- 4 edges and 2 corners of the bottom layer (the top face's are
       // carried, and exchanged as the next layer's bottom)
       auto from_next = [&](double x) {
-        const long long v = __double_as_longlong(cube_in ? x : 0.0);
+        const long long v = __double_as_longlong(x);
         const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, 0x101, 0xf, 0xf, true);
         const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((unsigned long long)v >> 32), 0x101, 0xf, 0xf, true);
         return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
