@@ -34,8 +34,9 @@
 // ghost layer below, then above -- so the sorted column order of a row next to
 // the ghost layer below is recovered from the layers' local indices).  Values
 // equal the oracle's to rounding (1e-12 per entry); not bitwise the strip
-// kernels' (another summation order).  Opt-in: AFEM_ASSEMBLY_CUBES=1 (the
-// default is the strip / stencil path, faster on MI355X so far: DESIGN.md §3.1e).
+// kernels' (another summation order).  The default on generator boxes (C2:
+// 0.58-0.59 ms against the stencil kernel's 0.64);
+// AFEM_ASSEMBLY_CUBES=0 takes the strip / stencil path.
 #include "afem_internal.hpp"
 
 #include <algorithm>
@@ -505,8 +506,8 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
 {
   const Mesh& m = *b.mesh;
   const StructuredInfo& st = m.st;
-  const char* ce = variant("AFEM_ASSEMBLY_CUBES");  // opt-in (1): slower than the stencil kernel so far
-  if (!(ce && atoi(ce) == 1) || !st.valid || st.dim != 3 || m.nv != 4 || b.nb_dof != 1 || b.s.canon ||
+  const char* ce = variant("AFEM_ASSEMBLY_CUBES");  // 0: the strip / stencil kernels
+  if ((ce && atoi(ce) == 0) || !st.valid || st.dim != 3 || m.nv != 4 || b.nb_dof != 1 || b.s.canon ||
       st.lx > 0 || st.ly > 0 || st.n < 1)
     return false;
   Ctx& ctx = *m.ctx;

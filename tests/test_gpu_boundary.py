@@ -573,7 +573,7 @@ def test_assembly_ticket_ring_wraps(ctx, variant):
     """The persistent assembly kernels' claim counters come from a ring of 256
     per-assembly slots zeroed together (assembly.hip next_tickets): 300
     assemblies in a row (past a wrap) all give the same bits."""
-    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (cubes.hip is opt-in)
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     mesh = af.Mesh.structured(ctx, 3, 10, jitter=0.2, seed=3)
     bsr = af.BSRFormat(mesh, 1).initialize(True)
     bsr.computeSparsity()

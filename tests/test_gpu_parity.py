@@ -120,7 +120,7 @@ def test_assembly_bitwise_reproducible(ctx):
 @pytest.mark.parametrize("n,nz,zs", [(1, 1, None), (2, 5, None), (6, 6, None), (7, 3, 2), (8, 9, 1), (13, 20, 3),
                                      (20, 7, None)])
 def test_cube_kernel_matches_oracle(ctx, variant, n, nz, zs):
-    """The cell-first cube kernel (cubes.hip, opt-in on generator boxes):
+    """The cell-first cube kernel (cubes.hip, the default on generator boxes):
     boxes whose line lengths are and are not multiples of the 7-row columns,
     thin boxes, and z segments of 1-3 layers (AFEM_CUBES_ZS): values and RHS
     against the oracle (1e-12 per entry) and against the row-strip kernels
@@ -177,7 +177,7 @@ def test_cube_kernel_on_slabs(ctx, variant, nranks, stride, carry):
 
 
 def test_uniform_strip_variant(ctx, variant):
-    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (cubes.hip is opt-in)
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     # interior 4x4x4 bricks of a structured box share one strip topology and
     # run the uniform-control kernel; it must give the general kernel's bits
     # and match the oracle
@@ -208,7 +208,7 @@ def test_stencil_instance_bitwise(ctx, variant, n):
     (stencil_sigs.inc) and run k_assemble_stencil (register accumulators): the
     same bits as the uniform instance (AFEM_ASSEMBLY_STENCIL=0) and the general
     instance (AFEM_ASSEMBLY_UNIFORM=0), and the oracle's values."""
-    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (cubes.hip is opt-in)
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=7)
     bsr, ls = _assemble_gpu(ctx, mesh, 5.5)
     st = bsr.stats()
@@ -240,7 +240,7 @@ def test_edge_slices_folded_into_general_list(ctx, variant):
     signature; beside enough stencil slices they join the compact general list
     (one launch before the stencil kernel).  Same bits as keeping them on the
     uniform instance (AFEM_ASSEMBLY_FOLD=0) and as the general instance."""
-    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (cubes.hip is opt-in)
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     mesh = af.Mesh.structured(ctx, 3, 100, jitter=0.2, seed=5)
     bsr, ls = _assemble_gpu(ctx, mesh, 3.0)
     st = bsr.stats()
@@ -567,7 +567,7 @@ def test_lattice_order_matches_generator_box(ctx, variant, n, nz, jitter):
     recovered lattice gives the generator's brick order, the same stencil /
     uniform slice lists and bitwise the same matrix and RHS as the box made by
     afem_mesh_create_structured (unjittered and non-cubic boxes included)."""
-    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (cubes.hip is opt-in)
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     m0 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=jitter, seed=5)
     b0, l0 = _assemble_gpu(ctx, m0, 5.5)
     cells, coords, _ = m0.download()
@@ -593,7 +593,7 @@ def test_canonical_lattice_random_numbering(ctx, variant, n, nz, seed):
     the per-row slot map.  The matrix is bitwise the generator's, permuted
     (A1[p[i], p[j]] == A0[i, j]), and so is the RHS.  AFEM_CANON=0 (no
     relabeling: the general instance) stays within the oracle tolerance."""
-    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (cubes.hip is opt-in)
+    variant("AFEM_ASSEMBLY_CUBES", "0")  # the row-strip family (generator boxes default to cubes.hip)
     m0 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=seed)
     b0, l0 = _assemble_gpu(ctx, m0, 5.5)
     cells0, coords0, _ = m0.download()

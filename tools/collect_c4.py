@@ -10,7 +10,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_assemble_stencil", "k_assemble_strip")
+KERNELS = ("k_assemble_stencil", "k_assemble_strip", "k_assemble_cubes")
 
 
 def main():

@@ -19,7 +19,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def counters(d, kernel=("k_assemble_strip", "k_assemble_stencil")):
+def counters(d, kernel=("k_assemble_strip", "k_assemble_stencil", "k_assemble_cubes")):
     """Per assembly: the mean per dispatch of each matching kernel, summed over
     the kernels (the assembly launches a uniform-strip and a general instance)."""
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -41,7 +41,7 @@ def main():
     c = {}
     for sub in ("pmc_sq", "pmc_fetch", "pmc_write", "pmc_lds"):
         c.update(counters(os.path.join(prof, sub)))
-    lines = [f"# {tag}: per assembly = sum over the k_assemble_stencil / k_assemble_strip instances of their mean per dispatch "
+    lines = [f"# {tag}: per assembly = sum over the assembly kernels (k_assemble_cubes, or the k_assemble_stencil / k_assemble_strip instances) of their mean per dispatch "
              "(rocprofv3 --pmc, separate passes)"]
     for k in sorted(c):
         lines.append(f"{k:32s} {c[k]:.6g}")
