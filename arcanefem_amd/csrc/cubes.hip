@@ -138,7 +138,7 @@ constexpr int kAcc = 15;   // accumulators per row: 15 offsets, the diagonal's (
 // count past them (vmcnt(N)) instead of draining them (vmcnt(0))
 // amdgpu_waves_per_eu(3): 168 VGPRs, with the 49-row planes' 15.6 KB of LDS
 // 10 waves per CU (the 64-row planes' 19.3 KB keep 8 whatever the registers)
-template <int STRIDE, bool CARRY, bool XEX, bool HAS_RHS, bool RHS_ADD>
+template <int STRIDE, bool CARRY, bool XEX, bool YEX, bool HAS_RHS, bool RHS_ADD>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
                                                        const double* __restrict__ coords,
                                                        double* __restrict__ vals, double* __restrict__ rhs)
@@ -415,6 +415,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 #pragma unroll
       for (int c = 0; c < 4; ++c) cm[c] = mv[c + 4];
     }
+    if constexpr (YEX) {
+      // the y = 1 face is the y = 0 face of lane + 8's cube: its bottom-layer
+      // sums come over first (ds_bpermute; lanes with cj = 7 get their own,
+      // their y = 1 corners are outside the unit), so the x exchange below
+      // then passes on sums that already hold the diagonal neighbour's
+      ev[2][3] += __shfl_down(ev[0][1], 8);
+      ev[2][6] += __shfl_down(ev[0][4], 8);
+      ev[2][7] += __shfl_down(ev[0][5], 8);
+      ev[3][7] += __shfl_down(ev[1][5], 8);
+      mv[2] += __shfl_down(mv[0], 8);
+      mv[3] += __shfl_down(mv[1], 8);
+    }
     if constexpr (XEX) {
       // the x = 1 face of this lane's cube is the x = 0 face of lane + 1's
       // (same 16-lane DPP row; a lane with ci = 7 gets a wrong neighbour but its
@@ -446,13 +458,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 #pragma unroll
       for (int b = a + 1; b < 8; ++b)
         if (is_edge(a, b) && !(CARRY && cbit(a, 2) && cbit(b, 2)) &&
-            !(XEX && !cbit(a, 0) && !cbit(b, 0) && !(cbit(a, 2) && cbit(b, 2)))) {
+            !(XEX && !cbit(a, 0) && !cbit(b, 0) && !(cbit(a, 2) && cbit(b, 2))) &&
+            !(YEX && !cbit(a, 1) && !cbit(b, 1) && !(cbit(a, 2) && cbit(b, 2)))) {
           atomicAdd(base_at(inm, bb_, bt_, a) + STRIDE * edge_o(a, b), kept(a, ev[a][b]));
           atomicAdd(base_at(inm, bb_, bt_, b) + STRIDE * edge_o(b, a), kept(b, ev[a][b]));
         }
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      if (!(CARRY && cbit(c, 2)) && !(XEX && !cbit(c, 0) && !cbit(c, 2)))
+      if (!(CARRY && cbit(c, 2)) && !(XEX && !cbit(c, 0) && !cbit(c, 2)) && !(YEX && !cbit(c, 1) && !cbit(c, 2)))
         atomicAdd(base_at(inm, bb_, bt_, c) + STRIDE * 7, kept(c, mv[c]));  // |det| sums
   };
 
@@ -542,11 +555,15 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   const bool carry = !(ke && atoi(ke) == 0);
   const char* xe = variant("AFEM_CUBES_XEX");
   const bool xex = carry && !(xe && atoi(xe) == 0);
-#define AFEM_CUBES_K(S, C, X)                                                                                        \
-  (rhs ? (rhs_add ? &k_assemble_cubes<S, C, X, true, true> : &k_assemble_cubes<S, C, X, true, false>)                \
-       : &k_assemble_cubes<S, C, X, false, false>)
-  auto* kern = carry ? (xex ? AFEM_CUBES_K(64, true, true) : AFEM_CUBES_K(64, true, false))
-                     : (s49 ? AFEM_CUBES_K(49, false, false) : AFEM_CUBES_K(64, false, false));
+  // and the y = 1 face's with lane + 8 (AFEM_CUBES_YEX=0: not; needs the x exchange)
+  const char* ye = variant("AFEM_CUBES_YEX");
+  const bool yex = xex && !(ye && atoi(ye) == 0);
+#define AFEM_CUBES_K(S, C, X, Y)                                                                                     \
+  (rhs ? (rhs_add ? &k_assemble_cubes<S, C, X, Y, true, true> : &k_assemble_cubes<S, C, X, Y, true, false>)          \
+       : &k_assemble_cubes<S, C, X, Y, false, false>)
+  auto* kern = carry ? (xex ? (yex ? AFEM_CUBES_K(64, true, true, true) : AFEM_CUBES_K(64, true, true, false))
+                            : AFEM_CUBES_K(64, true, false, false))
+                     : (s49 ? AFEM_CUBES_K(49, false, false, false) : AFEM_CUBES_K(64, false, false, false));
 #undef AFEM_CUBES_K
   hipLaunchKernelGGL(kern, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, b.s.row_ptr.p, m.coords.p,
                      b.values.p, rhs);
