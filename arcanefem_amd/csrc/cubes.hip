@@ -300,8 +300,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       off += rl;
     }
     __syncthreads();
+    if constexpr ((kAcc * STRIDE) % 2 == 0) {  // 16-B stores (64-row planes: buffers 16-B aligned)
+      double2* const img2 = reinterpret_cast<double2*>(img);
 #pragma unroll
-    for (int i = 0; i < (kAcc * STRIDE + 63) / 64; ++i) img[min(64 * i + lane, kAcc * STRIDE - 1)] = 0.0;
+      for (int i = 0; i < (kAcc * STRIDE / 2 + 63) / 64; ++i)
+        img2[min(64 * i + lane, kAcc * STRIDE / 2 - 1)] = make_double2(0.0, 0.0);
+    }
+    else {
+#pragma unroll
+      for (int i = 0; i < (kAcc * STRIDE + 63) / 64; ++i) img[min(64 * i + lane, kAcc * STRIDE - 1)] = 0.0;
+    }
     __syncthreads();
   };
 
@@ -353,18 +361,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 #pragma unroll
     for (int c = 4; c < 8; ++c) atomicAdd(base_at(inm, bb, bt, c) + STRIDE * 7, kept(c, cm[c - 4]));
   };
+  P3 Xc[4];  // the lane's cube's top corners, the next cube layer's bottom ones
+  auto prime_corners = [&](int zc) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int q = (ci + cbit(c, 0)) + kCol * (cj + cbit(c, 1));
+      Xc[c] = P3{ cz[zc & 1][0][q], cz[zc & 1][1][q], cz[zc & 1][2][q] };
+    }
+  };
   auto cubes = [&](int zc) {
     // no branch around the cube: a lane whose cube is outside the box works on
     // its clamped (duplicated) coordinates and adds zeros -- a divergent region
     // here made the compiler drain the next layer's loads (vmcnt(0)) before the
     // arithmetic
     const int bb = zc & 1, bt = (zc + 1) & 1;
+    // with CARRY the bottom corners are the previous cube layer's top corners
+    // (registers: 12 LDS reads less per layer), the top ones from the staged layer
     P3 X[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int buf = cbit(c, 2) ? bt : bb;
+    for (int c = 0; c < 4; ++c) {
       const int q = (ci + cbit(c, 0)) + kCol * (cj + cbit(c, 1));
-      X[c] = P3{ cz[buf][0][q], cz[buf][1][q], cz[buf][2][q] };
+      X[c] = CARRY ? Xc[c] : P3{ cz[bb][0][q], cz[bb][1][q], cz[bb][2][q] };
+      X[c + 4] = P3{ cz[bt][0][q], cz[bt][1][q], cz[bt][2][q] };
+      if constexpr (CARRY) Xc[c] = X[c + 4];
     }
     double ev[8][8];
     double mv[8];
@@ -480,6 +499,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   store_layer(zc_first & 1);
   load_layer(zc_first + 1);
   store_layer((zc_first + 1) & 1);
+  __syncthreads();
+  if constexpr (CARRY) prime_corners(zc_first);
   int zc = zc_first;
   if (zc < z0) {  // the cube layer below the segment: its top corners only, no flush
     load_layer(zc + 2);
