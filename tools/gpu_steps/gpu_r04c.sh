@@ -7,4 +7,4 @@ timeout -k 10 300 python -u -m pytest -v --timeout 200 --timeout-method thread t
 rc=$?
 echo "tests rc=$rc" >> gpurun_out/r04c_tests.log
 case $rc in 124|137|134|139) exit $rc;; esac
-bash tools/gpu_r04b.sh
+bash tools/gpu_steps/gpu_r04b.sh
