@@ -261,6 +261,15 @@ struct Structure {
   // position p.  The strip / stencil kernels write through it.
   bool canon = false;
   DevBuf<uint8_t> cperm;
+  // canonical lattice of Kuhn cubes (every cell one of the 6 Kuhn tets of its
+  // cube): the cube kernel runs on it (cubes.hip).  Per lattice node i: the
+  // caller's node, its row's first value, and the position in that row of
+  // canonical slot t (4 bits each)
+  bool cube_ok = false;
+  int64_t cube_L[3] = { 0, 0, 0 };
+  DevBuf<int32_t> cube_phys;
+  DevBuf<int64_t> cube_rb;
+  DevBuf<uint64_t> cube_slot;
 };
 
 struct LinearSystem;

@@ -68,7 +68,7 @@ __device__ __forceinline__ double precip(double a)
 }
 
 struct CubeGeom {
-  int np1;           // nodes per x / y line
+  int npx, npy;      // nodes per x line, per y line
   int nzc;           // cells of the global box in z (node layers 0..nzc)
   int k0, k1;        // owned node layers [k0, k1)
   int ghost_lo, ghost_hi;
@@ -92,7 +92,7 @@ __device__ __forceinline__ int local_layer(const CubeGeom& g, int k)
   return g.n_own_layers + (g.ghost_lo >= 0 ? 1 : 0);
 }
 
-// the 15 column offsets of a Kuhn row sorted by node id (x + np1 (y + np1 z)):
+// the 15 column offsets of a Kuhn row sorted by node id (x + npx (y + npy z)):
 // by dz, then dy, then dx
 __host__ __device__ constexpr int o_of(int dx, int dy, int dz)
 {
@@ -138,10 +138,21 @@ constexpr int kAcc = 15;   // accumulators per row: 15 offsets, the diagonal's (
 // count past them (vmcnt(N)) instead of draining them (vmcnt(0))
 // amdgpu_waves_per_eu(3): 168 VGPRs, with the 49-row planes' 15.6 KB of LDS
 // 10 waves per CU (the 64-row planes' 19.3 KB keep 8 whatever the registers)
-template <int STRIDE, bool CARRY, bool XEX, bool YEX, bool HAS_RHS, bool RHS_ADD>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_assemble_cubes(CubeGeom g, const int64_t* __restrict__ rows,
-                                                       const double* __restrict__ coords,
-                                                       double* __restrict__ vals, double* __restrict__ rhs)
+// CANON: a lattice mesh in the caller's numbering (sparsity.hip canonical_lattice,
+// Structure::cube_*): the unit walks lattice indices; a node's coordinates
+// come through its caller id, a row's values go to the caller's row (first
+// value cc.rb, canonical slot t at position cc.slot >> 4t) through a per-row
+// image (row L at [15 L, 15 L + 15), stored row by row)
+struct CubeCanon {
+  const int32_t* phys;
+  const int64_t* rb;
+  const uint64_t* slot;
+};
+
+template <int STRIDE, bool CARRY, bool XEX, bool YEX, bool CANON, bool HAS_RHS, bool RHS_ADD>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_assemble_cubes(
+    CubeGeom g, const int64_t* __restrict__ rows, const double* __restrict__ coords, double* __restrict__ vals,
+    double* __restrict__ rhs, CubeCanon cc)
 {
   __shared__ __align__(16) double acc[2][kAcc][STRIDE];  // STRIDE >= 49 rows per offset plane
   __shared__ double cz[2][3][kCol * kCol];  // SoA coordinates of two node layers
@@ -164,7 +175,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   // this lane's cube (i, j) and its staging share (nodes q = lane, lane + 64 of 81)
   const int ci = lane & 7, cj = lane >> 3;
   const int gx = cx0 - 1 + ci, gy = cy0 - 1 + cj;  // lower corner
-  const bool cube_in = gx >= 0 && gy >= 0 && gx + 1 < g.np1 && gy + 1 < g.np1;
+  const bool cube_in = gx >= 0 && gy >= 0 && gx + 1 < g.npx && gy + 1 < g.npy;
   auto node_xy = [&](int q, int& nx, int& ny) {
     nx = cx0 - 1 + q % kCol;
     ny = cy0 - 1 + q / kCol;
@@ -174,19 +185,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   // code, so the waits on them count past the later memory operations instead
   // of draining everything (vmcnt(0)) at a branch join
   double pre[2][3];
-  auto load_layer = [&](int k) {
+  int32_t pid[2] = { 0, 0 };  // CANON: the caller's ids of the next staged layer's nodes
+  auto layer_ids = [&](int k, int64_t(&id)[2]) {
     const int kk = is_local(g, k) ? k : g.k0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int q = min(lane + 64 * h, kCol * kCol - 1);
       int nx, ny;
       node_xy(q, nx, ny);
-      nx = min(max(nx, 0), g.np1 - 1);
-      ny = min(max(ny, 0), g.np1 - 1);
-      const int64_t id = (int64_t)local_layer(g, kk) * g.L + nx + (int64_t)g.np1 * ny;
-      pre[h][0] = coords[3 * id];
-      pre[h][1] = coords[3 * id + 1];
-      pre[h][2] = coords[3 * id + 2];
+      nx = min(max(nx, 0), g.npx - 1);
+      ny = min(max(ny, 0), g.npy - 1);
+      id[h] = (int64_t)local_layer(g, kk) * g.L + nx + (int64_t)g.npx * ny;
+    }
+  };
+  // CANON: the ids first (prefetch_ids, one step ahead), the coordinates through them
+  auto prefetch_ids = [&](int k) {
+    if constexpr (CANON) {
+      int64_t id[2];
+      layer_ids(k, id);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) pid[h] = cc.phys[id[h]];
+    }
+  };
+  auto load_layer = [&](int k) {
+    int64_t id[2];
+    layer_ids(k, id);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t n = CANON ? (int64_t)pid[h] : id[h];
+      pre[h][0] = coords[3 * n];
+      pre[h][1] = coords[3 * n + 1];
+      pre[h][2] = coords[3 * n + 2];
     }
   };
   auto store_layer = [&](int buf) {
@@ -206,23 +235,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   const int rx = lane % kRun, ry = lane / kRun;
   const int nx = cx0 + rx, ny = cy0 + ry;
   int64_t pf_rb = 0, pf_re = 0, pf_r = 0;
+  uint64_t pf_slot = 0;
   double pf_rhs = 0.0;
   auto prefetch_rows = [&](int z) {  // clamped like load_layer: no branch
     const int zz = (z >= z0 && z < z1) ? z : z0;
-    pf_r = (int64_t)local_layer(g, zz) * g.L + min(nx, g.np1 - 1) + (int64_t)g.np1 * min(ny, g.np1 - 1);
-    pf_rb = rows[pf_r];
-    pf_re = rows[pf_r + 1];
-    if constexpr (RHS_ADD) pf_rhs = rhs[pf_r];
+    const int64_t li = (int64_t)local_layer(g, zz) * g.L + min(nx, g.npx - 1) + (int64_t)g.npx * min(ny, g.npy - 1);
+    if constexpr (CANON) {
+      pf_r = cc.phys[li];
+      pf_rb = cc.rb[li];
+      pf_slot = cc.slot[li];
+    }
+    else {
+      pf_r = li;
+      pf_rb = rows[pf_r];
+      pf_re = rows[pf_r + 1];
+      if constexpr (RHS_ADD) pf_rhs = rhs[pf_r];
+    }
   };
   auto flush = [&](int z) {
     const int b = z & 1;
-    const bool valid = lane < kRows && nx < g.np1 && ny < g.np1;
+    const bool valid = lane < kRows && nx < g.npx && ny < g.npy;
     // present neighbours and the order of their local ids: the dz groups by local layer index
     uint32_t mask = 0;
 #pragma unroll
     for (int o = 0; o < 15; ++o) {  // branch-free (bitwise ands of the comparisons)
       const int xx = nx + kOffX[o], yy = ny + kOffY[o], zz = z + kOffZ[o];
-      const uint32_t in = (uint32_t)(xx >= 0) & (uint32_t)(yy >= 0) & (uint32_t)(xx < g.np1) & (uint32_t)(yy < g.np1) &
+      const uint32_t in = (uint32_t)(xx >= 0) & (uint32_t)(yy >= 0) & (uint32_t)(xx < g.npx) & (uint32_t)(yy < g.npy) &
                           (uint32_t)(zz >= 0) & (uint32_t)(zz <= g.nzc);
       mask |= in << o;
     }
@@ -248,8 +286,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     const int64_t rb = valid ? pf_rb : 0;
     // (a 64-bit min: with only the low halves used the compiler reuses the
     // loaded high half's register at once, a write-after-write wait on the load)
-    const int len = valid ? (int)min(pf_re - pf_rb, (int64_t)15) : 0;
+    const int len = CANON ? (valid ? __popc(mask) : 0) : (valid ? (int)min(pf_re - pf_rb, (int64_t)15) : 0);
     if constexpr (HAS_RHS) {  // lanes without a row repeat lane 0's store (always a row)
+      if constexpr (CANON && RHS_ADD) pf_rhs = rhs[pf_r];
       const double rv = RHS_ADD ? pf_rhs + g.f_meas * meas : g.f_meas * meas;
       const int64_t r0 = __shfl(pf_r, 0);
       const double rv0 = __shfl(rv, 0);
@@ -270,6 +309,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     }
     __syncthreads();  // every lane's accumulator reads before the image overwrites them
     double* img = &acc[b][0][0];
+    if constexpr (CANON) {
+      // row L's values at [15 L, 15 L + 15) in the caller's column order; its
+      // first value and length in the free coordinate buffer of layer z & 1
+      int64_t* const rbs = reinterpret_cast<int64_t*>(&cz[z & 1][0][0]);
+      int* const lens = reinterpret_cast<int*>(rbs + 64);
+      rbs[lane] = rb;
+      lens[lane] = len;
+      if (valid) {
+#pragma unroll
+        for (int o = 0; o < 15; ++o)
+          if ((mask >> o) & 1u) {
+            const int t = __popc(mask & ((1u << o) - 1u));  // canonical slot (sorted lattice indices)
+            img[15 * lane + (int)((pf_slot >> (4 * t)) & 15u)] = v[o];
+          }
+      }
+      __syncthreads();
+      // row by row, consecutive lanes over a row's values; positions past a
+      // row's length repeat row 0's first value (always a row), so the store
+      // count is fixed
+      const int64_t rb0 = rbs[0];
+#pragma unroll
+      for (int i = 0; i < (15 * kRows + 63) / 64; ++i) {
+        const int P = min(64 * i + lane, 15 * kRows - 1);
+        const int L = P / 15, j = P - 15 * L;
+        const bool ok = j < lens[L];
+        vals[ok ? rbs[L] + j : rb0] = img[ok ? P : 0];
+      }
+    }
+    else {
     if (valid) {
 #pragma unroll
       for (int o = 0; o < 15; ++o)
@@ -299,6 +367,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       }
       off += rl;
     }
+    }
     __syncthreads();
     if constexpr ((kAcc * STRIDE) % 2 == 0) {  // 16-B stores (64-row planes: buffers 16-B aligned)
       double2* const img2 = reinterpret_cast<double2*>(img);
@@ -324,8 +393,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     bt = (zc + 1) & 1;
     const int rx0 = ci - 1, ry0 = cj - 1;
     const bool zlo = zc >= z0, zhi = zc + 1 < z1;
-    const bool xin0 = rx0 >= 0 && cx0 + rx0 < g.np1, xin1 = rx0 + 1 < kRun && cx0 + rx0 + 1 < g.np1;
-    const bool yin0 = ry0 >= 0 && cy0 + ry0 < g.np1, yin1 = ry0 + 1 < kRun && cy0 + ry0 + 1 < g.np1;
+    const bool xin0 = rx0 >= 0 && cx0 + rx0 < g.npx, xin1 = rx0 + 1 < kRun && cx0 + rx0 + 1 < g.npx;
+    const bool yin0 = ry0 >= 0 && cy0 + ry0 < g.npy, yin1 = ry0 + 1 < kRun && cy0 + ry0 + 1 < g.npy;
     inm = 0;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -495,14 +564,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   // cubes): their wait then counts past the flush's stores (vmcnt(N)), and no
   // wait sits at the loop head, where the entry and the back edge would merge
   // into the stricter one
+  prefetch_ids(zc_first);
   load_layer(zc_first);
   store_layer(zc_first & 1);
+  prefetch_ids(zc_first + 1);
   load_layer(zc_first + 1);
   store_layer((zc_first + 1) & 1);
   __syncthreads();
   if constexpr (CARRY) prime_corners(zc_first);
   int zc = zc_first;
   if (zc < z0) {  // the cube layer below the segment: its top corners only, no flush
+    prefetch_ids(zc + 2);
     load_layer(zc + 2);
     __syncthreads();
     cubes(zc);
@@ -516,6 +588,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   for (; zc <= zc_last; ++zc) {
     // the offsets of the rows this iteration completes, then the coordinates
     // of layer zc + 2: the flush waits for the offsets only (counted vmcnt)
+    prefetch_ids(zc + 2);  // CANON: the next staged layer's caller ids, in flight during the cubes
     prefetch_rows(zc);
     __syncthreads();
     cubes(zc);
@@ -540,26 +613,41 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
 {
   const Mesh& m = *b.mesh;
   const StructuredInfo& st = m.st;
+  const Structure& S = b.s;
   const char* ce = variant("AFEM_ASSEMBLY_CUBES");  // 0: the strip / stencil kernels
-  if ((ce && atoi(ce) == 0) || !st.valid || st.dim != 3 || m.nv != 4 || b.nb_dof != 1 || b.s.canon ||
-      st.lx > 0 || st.ly > 0 || st.n < 1)
-    return false;
+  if ((ce && atoi(ce) == 0) || m.nv != 4 || b.nb_dof != 1) return false;
+  // a generator box (or z-slab of one), or a lattice of Kuhn cubes in the caller's numbering
+  const bool canon = S.canon && S.cube_ok;
+  if (!canon && (!st.valid || st.dim != 3 || S.canon || st.lx > 0 || st.ly > 0 || st.n < 1)) return false;
   Ctx& ctx = *m.ctx;
   CubeGeom g{};
-  g.np1 = st.n + 1;
-  g.nzc = st.nz;
-  g.k0 = st.k0;
-  g.k1 = st.k1;
-  g.ghost_lo = st.ghost_lo;
-  g.ghost_hi = st.ghost_hi;
-  g.n_own_layers = st.k1 - st.k0;
-  g.L = st.L;
-  if (g.n_own_layers <= 0 || g.L != (int64_t)g.np1 * g.np1 || g.nzc < 1) return false;
-  g.tx = g.ty = (g.np1 + kRun - 1) / kRun;
+  if (canon) {
+    g.npx = (int)S.cube_L[0];
+    g.npy = (int)S.cube_L[1];
+    g.nzc = (int)S.cube_L[2] - 1;
+    g.k0 = 0;
+    g.k1 = (int)S.cube_L[2];
+    g.ghost_lo = g.ghost_hi = -1;
+    g.L = S.cube_L[0] * S.cube_L[1];
+  }
+  else {
+    g.npx = g.npy = st.n + 1;
+    g.nzc = st.nz;
+    g.k0 = st.k0;
+    g.k1 = st.k1;
+    g.ghost_lo = st.ghost_lo;
+    g.ghost_hi = st.ghost_hi;
+    g.L = st.L;
+    if (g.L != (int64_t)g.npx * g.npy) return false;
+  }
+  g.n_own_layers = g.k1 - g.k0;
+  if (g.n_own_layers <= 0 || g.nzc < 1 || g.npx < 2 || g.npy < 2) return false;
+  g.tx = (g.npx + kRun - 1) / kRun;
+  g.ty = (g.npy + kRun - 1) / kRun;
   const char* ze = variant("AFEM_CUBES_ZS");
   // z segment: ~n/16 layers (C2 n = 215: 13, C4 n = 463: 29; r04x: zs 12 0.645 ms
   // vs zs 8 0.649 at C2, zs 32 6.38 vs zs 24 6.81 ms at C4)
-  g.zs = std::max(1, ze ? atoi(ze) : std::min(48, std::max(8, g.np1 / 16)));
+  g.zs = std::max(1, ze ? atoi(ze) : std::min(48, std::max(8, std::max(g.npx, g.npy) / 16)));
   g.ns = (g.n_own_layers + g.zs - 1) / g.zs;
   g.s_coef = coef / 6.0;
   g.f_meas = f / 24.0;
@@ -573,21 +661,23 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   // r04y C2: 0.605 ms with the carry at 64-row planes, 0.660 without at 49); the x = 1 face's
   // shared with lane + 1 over DPP (AFEM_CUBES_XEX=0: not; needs the carry)
   const char* ke = variant("AFEM_CUBES_CARRY");
-  const bool carry = !(ke && atoi(ke) == 0);
+  const bool carry = canon || !(ke && atoi(ke) == 0);
   const char* xe = variant("AFEM_CUBES_XEX");
-  const bool xex = carry && !(xe && atoi(xe) == 0);
+  const bool xex = canon || (carry && !(xe && atoi(xe) == 0));
   // and the y = 1 face's with lane + 8 (AFEM_CUBES_YEX=0: not; needs the x exchange)
   const char* ye = variant("AFEM_CUBES_YEX");
-  const bool yex = xex && !(ye && atoi(ye) == 0);
-#define AFEM_CUBES_K(S, C, X, Y)                                                                                     \
-  (rhs ? (rhs_add ? &k_assemble_cubes<S, C, X, Y, true, true> : &k_assemble_cubes<S, C, X, Y, true, false>)          \
-       : &k_assemble_cubes<S, C, X, Y, false, false>)
-  auto* kern = carry ? (xex ? (yex ? AFEM_CUBES_K(64, true, true, true) : AFEM_CUBES_K(64, true, true, false))
-                            : AFEM_CUBES_K(64, true, false, false))
-                     : (s49 ? AFEM_CUBES_K(49, false, false, false) : AFEM_CUBES_K(64, false, false, false));
+  const bool yex = canon || (xex && !(ye && atoi(ye) == 0));
+#define AFEM_CUBES_K(S, C, X, Y, N)                                                                                  \
+  (rhs ? (rhs_add ? &k_assemble_cubes<S, C, X, Y, N, true, true> : &k_assemble_cubes<S, C, X, Y, N, true, false>)    \
+       : &k_assemble_cubes<S, C, X, Y, N, false, false>)
+  auto* kern = canon ? AFEM_CUBES_K(64, true, true, true, true)
+               : carry ? (xex ? (yex ? AFEM_CUBES_K(64, true, true, true, false) : AFEM_CUBES_K(64, true, true, false, false))
+                              : AFEM_CUBES_K(64, true, false, false, false))
+                       : (s49 ? AFEM_CUBES_K(49, false, false, false, false) : AFEM_CUBES_K(64, false, false, false, false));
 #undef AFEM_CUBES_K
-  hipLaunchKernelGGL(kern, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, b.s.row_ptr.p, m.coords.p,
-                     b.values.p, rhs);
+  const CubeCanon cc{ canon ? S.cube_phys.p : nullptr, canon ? S.cube_rb.p : nullptr, canon ? S.cube_slot.p : nullptr };
+  hipLaunchKernelGGL(kern, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, S.row_ptr.p, m.coords.p, b.values.p,
+                     rhs, cc);
   AFEM_LAUNCHED();
   b.last_kernel = AFEM_KERNEL_CUBES;
   return true;

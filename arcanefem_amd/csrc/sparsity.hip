@@ -1911,6 +1911,44 @@ __global__ void k_canon_slots(int64_t n_pos, const int32_t* __restrict__ perm_la
   for (int t = 0; t < 16; ++t) cperm[16 * p + t] = out[t];
 }
 
+// every cell a Kuhn tet (type < 6) and no two alike in one cube (sorted keys)
+__global__ void k_kuhn_check(int64_t nc, const unsigned long long* __restrict__ keys, int32_t* __restrict__ err)
+{
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  if ((keys[c] & 7ull) >= 6ull || (c > 0 && keys[c] == keys[c - 1])) *err = 1;
+}
+
+// the cube kernel's maps per lattice node i (canonical row i = the caller's
+// row inv[i]): that row's first value and, per canonical slot t (columns
+// sorted by lattice index), the position of the column in the caller's row
+__global__ void k_cube_maps(int64_t n, const int32_t* __restrict__ inv, const int64_t* __restrict__ crp,
+                            const int32_t* __restrict__ ccols, const int64_t* __restrict__ rp,
+                            const int32_t* __restrict__ cols, int64_t* __restrict__ rb_out,
+                            uint64_t* __restrict__ slot_out, int32_t* __restrict__ err)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t r = inv[i];
+  const int64_t rb = rp[r];
+  const int len = (int)(rp[r + 1] - rb);
+  const int64_t cb = crp[i];
+  uint64_t w = 0;
+  if (len != (int)(crp[i + 1] - cb) || len > 15) {
+    *err = 1;
+  }
+  else {
+    for (int t = 0; t < len; ++t) {
+      const int32_t c = inv[ccols[cb + t]];
+      const int q = find_slot(cols + rb, len, c);
+      if (q >= len || cols[rb + q] != c) *err = 1;
+      w |= (uint64_t)(q & 15) << (4 * t);
+    }
+  }
+  rb_out[i] = rb;
+  slot_out[i] = w;
+}
+
 // the canonical structure of a lattice mesh (see above) into s; false when it
 // does not apply or does not reach the stencil instance
 bool canonical_lattice(Mesh& m, Structure& s)
@@ -1928,6 +1966,7 @@ bool canonical_lattice(Mesh& m, Structure& s)
   AFEM_LAUNCHED();
   // the relabeled mesh: lattice node ids, cells in the generator's order
   const int64_t nc = m.n_cells;
+  bool kuhn = false;
   Mesh R;
   R.ctx = m.ctx;
   R.dim = 3;
@@ -1956,6 +1995,20 @@ bool canonical_lattice(Mesh& m, Structure& s)
     hipLaunchKernelGGL(k_relabel_cells, dim3(grid_for(4 * nc, 256)), dim3(256), 0, ctx.stream, nc, m.cell_node.p,
                        ids_s.p, lat.p, R.cell_node.p);
     AFEM_LAUNCHED();
+    // the cube kernel needs the generator's cells: 6 distinct Kuhn tets per lattice cube
+    const int64_t n_cubes = (L[0] - 1) * (L[1] - 1) * (L[2] - 1);
+    kuhn = nc == 6 * n_cubes && nc > 0;
+    if (kuhn) {
+      DevBuf<int32_t> kerr;
+      kerr.alloc(1);
+      AFEM_HIP(hipMemsetAsync(kerr.p, 0, kerr.bytes(), ctx.stream));
+      hipLaunchKernelGGL(k_kuhn_check, dim3(grid_for(nc, 256)), dim3(256), 0, ctx.stream, nc, keys_s.p, kerr.p);
+      AFEM_LAUNCHED();
+      int32_t h = 0;
+      AFEM_HIP(hipMemcpyAsync(&h, kerr.p, sizeof(h), hipMemcpyDeviceToHost, ctx.stream));
+      ctx.sync();
+      kuhn = h == 0;
+    }
   }
   hipLaunchKernelGGL(k_permute_coords, dim3(grid_for(3 * n, 256)), dim3(256), 0, ctx.stream, n, inv.p, m.coords.p,
                      R.coords.p);
@@ -1992,6 +2045,24 @@ bool canonical_lattice(Mesh& m, Structure& s)
   hipLaunchKernelGGL(k_map_ids, dim3(grid_for((int64_t)C.snode.n, 256)), dim3(256), 0, ctx.stream,
                      (int64_t)C.snode.n, inv.p, C.snode.p);
   AFEM_LAUNCHED();
+  // the cube kernel's maps (while C's row structure is still the canonical one)
+  if (kuhn) {
+    C.cube_phys.alloc(n);
+    C.cube_rb.alloc(n);
+    C.cube_slot.alloc(n);
+    AFEM_HIP(hipMemcpyAsync(C.cube_phys.p, inv.p, C.cube_phys.bytes(), hipMemcpyDeviceToDevice, ctx.stream));
+    DevBuf<int32_t> cerr;
+    cerr.alloc(1);
+    AFEM_HIP(hipMemsetAsync(cerr.p, 0, cerr.bytes(), ctx.stream));
+    hipLaunchKernelGGL(k_cube_maps, dim3(grid_for(n, 256)), dim3(256), 0, ctx.stream, n, inv.p, C.row_ptr.p, C.cols.p,
+                       s.row_ptr.p, s.cols.p, C.cube_rb.p, C.cube_slot.p, cerr.p);
+    AFEM_LAUNCHED();
+    int32_t h = 0;
+    AFEM_HIP(hipMemcpyAsync(&h, cerr.p, sizeof(h), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    C.cube_ok = h == 0;
+    for (int a = 0; a < 3; ++a) C.cube_L[a] = L[a];
+  }
   int32_t herr = 0;
   AFEM_HIP(hipMemcpyAsync(&herr, err.p, sizeof(herr), hipMemcpyDeviceToHost, ctx.stream));
   ctx.sync();

@@ -629,6 +629,55 @@ def test_canonical_lattice_random_numbering(ctx, variant, n, nz, seed):
     _check_values(v2, v1)
 
 
+@pytest.mark.parametrize("n,nz,seed", [(6, 6, 3), (9, 15, 4), (13, 5, 5), (1, 3, 6)])
+def test_cube_kernel_on_random_numbering(ctx, n, nz, seed):
+    """The cube kernel on a lattice of Kuhn cubes handed over as arrays in a
+    random node and cell numbering (Structure::cube_*: the unit walks lattice
+    indices, coordinates come through the caller's ids, each row's values go
+    through its slot map): bitwise the generator box's matrix and RHS (also
+    through the cube kernel), permuted; set and add RHS modes; the cells'
+    vertex order does not matter (the kernel derives the cubes from the
+    lattice).  Boxes too small for the canonical relabeling stay on the strip
+    kernels (oracle tolerance)."""
+    m0 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=seed)
+    b0, l0 = _assemble_gpu(ctx, m0, 5.5)
+    assert b0.stats()["last_kernel"] == 10
+    cells0, coords0, _ = m0.download()
+    rng = np.random.default_rng(seed)
+    nn = coords0.shape[0]
+    p = rng.permutation(nn)
+    cells = p[cells0].astype(np.int32)[rng.permutation(cells0.shape[0])]
+    coords = np.empty_like(coords0)
+    coords[p] = coords0
+    m1 = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    b1, l1 = _assemble_gpu(ctx, m1, 5.5)
+    if n >= 6:  # the canonical relabeling needs interior bricks (structure build)
+        assert b1.stats()["last_kernel"] == 10
+    r0, c0, v0 = b0.download()
+    r1, c1, v1 = b1.download()
+    key0 = p[np.repeat(np.arange(nn), np.diff(r0))].astype(np.int64) * nn + p[c0]
+    key1 = np.repeat(np.arange(nn), np.diff(r1)).astype(np.int64) * nn + c1
+    o0, o1 = np.argsort(key0), np.argsort(key1)
+    assert np.array_equal(key0[o0], key1[o1])
+    if b1.stats()["last_kernel"] == 10:
+        assert np.array_equal(v0[o0], v1[o1])
+        assert np.array_equal(l1.rhs_host()[p], l0.rhs_host())
+    else:
+        _check_values(v1[o1], v0[o0])
+    rhs1 = l1.rhs_host()
+    b1.assemblePoissonP1(1.0, 5.5, l1.rhsVariable(), rhs_mode="add")
+    assert np.array_equal(l1.rhs_host(), rhs1 + rhs1)
+    # another vertex order in every cell: the same cubes, the same bits
+    cells2 = np.ascontiguousarray(cells[:, [2, 0, 3, 1]])
+    m2 = af.Mesh.from_arrays(ctx, 3, cells2, coords)
+    b2, _ = _assemble_gpu(ctx, m2, 5.5)
+    assert b2.stats()["last_kernel"] == b1.stats()["last_kernel"]
+    if b1.stats()["last_kernel"] == 10:
+        assert np.array_equal(b2.download()[2], v1)
+    else:
+        _check_values(b2.download()[2], v1)
+
+
 @pytest.mark.parametrize("knob,value", [("AFEM_BANK_PLACE_GENERAL", "1"), ("AFEM_ASSEMBLY_LOCAL", "1")])
 def test_general_slice_variants_bitwise(ctx, variant, knob, value):
     """Two layouts of the general (unstructured) slices that must not change a
