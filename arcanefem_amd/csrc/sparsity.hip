@@ -1839,6 +1839,19 @@ __global__ void k_cell_keys(int64_t nc, const int32_t* __restrict__ cn, const in
     my = min(my, y[a]);
     mz = min(mz, z[a]);
   }
+  // vertices by lattice index (a Kuhn path climbs it at every step): the type
+  // does not depend on the cell's vertex order
+  auto lid = [&](int a) { return (int64_t)x[a] + L0 * ((int64_t)y[a] + L1 * (int64_t)z[a]); };
+  for (int i = 1; i < 4; ++i)
+    for (int j = i; j > 0 && lid(j) < lid(j - 1); --j) {
+      const int tx = x[j], ty = y[j], tz = z[j];
+      x[j] = x[j - 1];
+      y[j] = y[j - 1];
+      z[j] = z[j - 1];
+      x[j - 1] = tx;
+      y[j - 1] = ty;
+      z[j - 1] = tz;
+    }
   auto axis = [&](int a, int b) -> int {
     const int dx = x[b] - x[a], dy = y[b] - y[a], dz = z[b] - z[a];
     if (dx == 1 && dy == 0 && dz == 0) return 0;
