@@ -1869,12 +1869,22 @@ __global__ void k_cell_keys(int64_t nc, const int32_t* __restrict__ cn, const in
   ids[c] = (int32_t)c;
 }
 
+// the relabeled cells, each one's vertices in increasing lattice index (the
+// generator's Kuhn path order, whatever the caller's vertex order)
 __global__ void k_relabel_cells(int64_t nc, const int32_t* __restrict__ cn, const int32_t* __restrict__ order,
                                 const int32_t* __restrict__ lat, int32_t* __restrict__ out)
 {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 4 * nc) return;
-  out[t] = lat[cn[4 * (int64_t)order[t >> 2] + (t & 3)]];
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  int32_t v[4];
+  for (int a = 0; a < 4; ++a) v[a] = lat[cn[4 * (int64_t)order[c] + a]];
+  for (int i = 1; i < 4; ++i)
+    for (int j = i; j > 0 && v[j] < v[j - 1]; --j) {
+      const int32_t t = v[j];
+      v[j] = v[j - 1];
+      v[j - 1] = t;
+    }
+  for (int a = 0; a < 4; ++a) out[4 * c + a] = v[a];
 }
 
 __global__ void k_permute_coords(int64_t n, const int32_t* __restrict__ inv, const double* __restrict__ in,
@@ -2005,7 +2015,7 @@ bool canonical_lattice(Mesh& m, Structure& s)
     tmp.alloc(tmp_bytes > 0 ? tmp_bytes : 1);
     AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tmp_bytes, keys.p, keys_s.p, ids.p, ids_s.p, (int)nc, 0, 64,
                                                 ctx.stream));
-    hipLaunchKernelGGL(k_relabel_cells, dim3(grid_for(4 * nc, 256)), dim3(256), 0, ctx.stream, nc, m.cell_node.p,
+    hipLaunchKernelGGL(k_relabel_cells, dim3(grid_for(nc, 256)), dim3(256), 0, ctx.stream, nc, m.cell_node.p,
                        ids_s.p, lat.p, R.cell_node.p);
     AFEM_LAUNCHED();
     // the cube kernel needs the generator's cells: 6 distinct Kuhn tets per lattice cube
