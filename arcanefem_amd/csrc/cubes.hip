@@ -32,7 +32,9 @@
 // Applies to meshes from afem_mesh_create_structured (3D, NB_DOF 1, any
 // z-slab: the columns follow the local numbering -- owned layers, then the
 // ghost layer below, then above -- so the sorted column order of a row next to
-// the ghost layer below is recovered from the layers' local indices).  Values
+// the ghost layer below is recovered from the layers' local indices), and to
+// lattices of Kuhn cubes handed over as arrays in any numbering (CANON: the
+// structure's canonical maps, sparsity.hip canonical_lattice).  Values
 // equal the oracle's to rounding (1e-12 per entry); not bitwise the strip
 // kernels' (another summation order).  The default on generator boxes (C2:
 // 0.58-0.59 ms against the stencil kernel's 0.64);
