@@ -135,6 +135,23 @@ constexpr int kCol = 9;    // staged nodes per x / y line (the column's rows + 1
 constexpr int kAcc = 15;   // accumulators per row: 15 offsets, the diagonal's (7, never added to:
                            // v_7 = -sum of the others) holds the row's |det| sum
 
+// One wave per block: LDS operations of a wave execute in issue order, so
+// ordering its phases (staging -> cube adds -> flush reads -> image -> stores)
+// needs only the compiler to keep the order, not an lgkmcnt(0) drain as
+// __syncthreads emits (AFEM_CUBES_WAVESYNC=0 restores those)
+#ifndef AFEM_CUBES_WAVESYNC
+#define AFEM_CUBES_WAVESYNC 1
+#endif
+__device__ __forceinline__ void wave_lds_order()
+{
+#if AFEM_CUBES_WAVESYNC
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#else
+  __syncthreads();
+#endif
+}
+
 // HAS_RHS / RHS_ADD at compile time: the flush's global stores are then a
 // fixed, branch-free sequence, so the waits for the next layer's coordinates
 // count past them (vmcnt(N)) instead of draining them (vmcnt(0))
@@ -309,7 +326,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       const int rl = __shfl(p + len, kRun * q + kRun - 1);
       if (q < ry) img0 += rl;
     }
-    __syncthreads();  // every lane's accumulator reads before the image overwrites them
+    wave_lds_order();  // every lane's accumulator reads before the image overwrites them
     double* img = &acc[b][0][0];
     if constexpr (CANON) {
       // row L's values at [15 L, 15 L + 15) in the caller's column order; its
@@ -326,7 +343,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
             img[15 * lane + (int)((pf_slot >> (4 * t)) & 15u)] = v[o];
           }
       }
-      __syncthreads();
+      wave_lds_order();
       // row by row, consecutive lanes over a row's values; positions past a
       // row's length repeat row 0's first value (always a row), so the store
       // count is fixed
@@ -350,7 +367,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
           img[img0 + p + start + __popc(gmask & ((1u << o) - 1u))] = v[o];
         }
     }
-    __syncthreads();
+    wave_lds_order();
     // x-run q: run_len(q) values from image offset img(q) to vals + rb(first row of run q).
     // A fixed count of unpredicated stores: lanes past a run repeat the first
     // value of run 0 (row 0 of the column is always a row: same address, same
@@ -370,7 +387,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       off += rl;
     }
     }
-    __syncthreads();
+    wave_lds_order();
     if constexpr ((kAcc * STRIDE) % 2 == 0) {  // 16-B stores (64-row planes: buffers 16-B aligned)
       double2* const img2 = reinterpret_cast<double2*>(img);
 #pragma unroll
@@ -381,7 +398,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 #pragma unroll
       for (int i = 0; i < (kAcc * STRIDE + 63) / 64; ++i) img[min(64 * i + lane, kAcc * STRIDE - 1)] = 0.0;
     }
-    __syncthreads();
+    wave_lds_order();
   };
 
   // ---- cube layer zc: the lane's cube, its 6 tets, 19 edge sums and 8 corner |det| sums
@@ -572,15 +589,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   prefetch_ids(zc_first + 1);
   load_layer(zc_first + 1);
   store_layer((zc_first + 1) & 1);
-  __syncthreads();
+  wave_lds_order();
   if constexpr (CARRY) prime_corners(zc_first);
   int zc = zc_first;
   if (zc < z0) {  // the cube layer below the segment: its top corners only, no flush
     prefetch_ids(zc + 2);
     load_layer(zc + 2);
-    __syncthreads();
+    wave_lds_order();
     cubes(zc);
-    __syncthreads();
+    wave_lds_order();
     store_layer(zc & 1);
     ++zc;
   }
@@ -592,10 +609,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     // of layer zc + 2: the flush waits for the offsets only (counted vmcnt)
     prefetch_ids(zc + 2);  // CANON: the next staged layer's caller ids, in flight during the cubes
     prefetch_rows(zc);
-    __syncthreads();
+    wave_lds_order();
     cubes(zc);
     load_layer(zc + 2);  // after the cubes: its 12 registers are not live across them
-    __syncthreads();
+    wave_lds_order();
     flush(zc);
     store_layer(zc & 1);
   }
@@ -603,7 +620,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     prefetch_rows(zc_last + 1);
     if constexpr (CARRY) {
       add_top(zc_last);
-      __syncthreads();
+      wave_lds_order();
     }
     flush(zc_last + 1);
   }
