@@ -56,6 +56,8 @@ def parse(argv=None):
                          "bench.py spawns the N rank processes itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="untimed back-to-back steps before the warmup, until the GPU clocks settle (0: none)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="weak: an n x n x n box per GPU stacked in z (C2 per GPU; n = 231 is BASELINE.md's C4 weak "
                          "size); strong: ONE n x n x n box cut into N z-slabs (C4, n = 463)")
@@ -213,12 +215,33 @@ def pmc_traffic(path, n):
     return None, None
 
 
-def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50):
+def settle(ctx, step, ms):
+    """GPU clocks ramp over the first tens of milliseconds of load after an
+    idle spell (tools/warm_probe.py, DESIGN.md section 5: the cube kernel's
+    first C2 launches 0.71 ms, 0.55 ms after ~50 launches, 0.69 again after a
+    2 s pause; the stencil kernel likewise): the step runs back to back for
+    `ms` of wall time before the warmup steps, so the timed steps see the
+    clocks a sustained loop runs at.  Untimed; reported as settle_ms /
+    settle_steps.  Returns the step count."""
+    k = 0
+    if ms <= 0:
+        return k
+    t = time.perf_counter()
+    while (time.perf_counter() - t) * 1e3 < ms:
+        for _ in range(8):
+            step()
+        ctx.synchronize()
+        k += 8
+    return k
+
+
+def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50, settle_ms=150.0):
     """BASELINE config C4's problem (Poisson-3D at ~10^8 DoF) on ONE GPU: the
     north-star size.  Assembly kernel time = median of `reps` launches after
     `warmup` (HIP events), CG = `cg_iters` fixed Jacobi-PCG iterations."""
     mesh, bsr, ls, bottom, dbottom, sp_ms = poisson_setup(ctx, af, n, None, 1, 0)
     step = make_step(ctx, bsr, ls, bottom, dbottom)
+    settle_steps = settle(ctx, step, settle_ms)
     for _ in range(warmup):
         step()
     ctx.synchronize()
@@ -245,7 +268,7 @@ def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50):
            "cg_iter_per_s": round(ips, 2), "cg_roofline_frac": round(cg_bytes(nnz, mesh.n_own_nodes) * ips / 1e9
                                                                        / HBM_PEAK_GBS, 4),
            "cg_device_ms": round(st["solve_ms"], 2), "cg_spmv": SPMV_KERNELS.get(st["spmv_kernel"]),
-           "sparsity_ms": round(sp_ms, 1)}
+           "sparsity_ms": round(sp_ms, 1), "settle_ms": settle_ms, "settle_steps": settle_steps}
     out["roofline"]["traffic"], out["roofline"]["traffic_profile"] = pmc_traffic(
         os.path.join(ROOT, "profiles", f"pmc_assembly_n{n}.json"), n)
     ctx.free(dbottom)
@@ -730,6 +753,7 @@ def main():
     setup_s = time.perf_counter() - t_setup
     step = make_step(ctx, bsr, ls, bottom, dbottom)
 
+    settle_steps = settle(ctx, step, args.settle_ms)
     for _ in range(args.warmup):
         step()
     ctx.synchronize()
@@ -800,7 +824,7 @@ def main():
             dbottom = None
         legs = set() if args.no_extras or world > 1 else set(args.legs.split(","))
         if "c4" in legs and args.c4_n > 0 and not (args.scaling == "strong" and n == args.c4_n):
-            extras["c4"] = poisson_c4(ctx, af, args.c4_n)
+            extras["c4"] = poisson_c4(ctx, af, args.c4_n, settle_ms=args.settle_ms)
         if "c3" in legs:
             extras["c3"] = elasticity_c3(ctx, af, args.c3_n)
         if "c2_generic" in legs:
@@ -832,6 +856,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_ms": args.settle_ms,
+            "settle_steps": settle_steps,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
