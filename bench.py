@@ -9,8 +9,11 @@ Inputs (mesh, structure) are resident in HBM before the timed region.
 Afterwards a fixed number of Jacobi-PCG iterations on the assembled CSR is
 timed for the CG iter/s half of the metric.
 
-Timing: `value` = DoF assembled per second over the K timed steps (wall clock
-between barriers, max over ranks).  The roofline of the assembly kernels uses
+Timing: before the W untimed warmup steps the step runs back to back for
+--settle-ms (150) of wall time, untimed, so the GPU clocks have left their
+post-idle ramp (settle(); reported as settle_ms / settle_steps).  `value` = DoF
+assembled per second over the K timed steps (wall clock between barriers, max
+over ranks).  The roofline of the assembly kernels uses
 the MEDIAN of the per-step kernel durations (HIP events recorded on the
 context stream around each assembly launch; BASELINE.md §4 asks for medians);
 the committed rocprofv3 kernel-stats summary of the same command is in
