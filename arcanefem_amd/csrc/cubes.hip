@@ -129,6 +129,17 @@ __host__ __device__ constexpr bool is_edge(int a, int b)
   return e;
 }
 
+// lane L's value, wave-uniform (v_readlane into a scalar register: no LDS
+// permute, and the address arithmetic on it stays scalar)
+__device__ __forceinline__ int lane_i32(int v, int L) { return __builtin_amdgcn_readlane(v, L); }
+__device__ __forceinline__ int64_t lane_i64(int64_t v, int L)
+{
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, L);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), L);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double lane_f64(double v, int L) { return __longlong_as_double(lane_i64(__double_as_longlong(v), L)); }
+
 constexpr int kRun = 7;    // rows per x-run of a column
 constexpr int kRows = 49;  // rows per column layer
 constexpr int kCol = 9;    // staged nodes per x / y line (the column's rows + 1 halo line below)
@@ -309,8 +320,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     if constexpr (HAS_RHS) {  // lanes without a row repeat lane 0's store (always a row)
       if constexpr (CANON && RHS_ADD) pf_rhs = rhs[pf_r];
       const double rv = RHS_ADD ? pf_rhs + g.f_meas * meas : g.f_meas * meas;
-      const int64_t r0 = __shfl(pf_r, 0);
-      const double rv0 = __shfl(rv, 0);
+      const int64_t r0 = lane_i64(pf_r, 0);
+      const double rv0 = lane_f64(rv, 0);
       rhs[valid ? pf_r : r0] = valid ? rv : rv0;
     }
     // prefix of the row lengths within the x-run (7 lanes), the runs' offsets in the image
@@ -323,7 +334,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     int img0 = 0;  // image offset of this lane's run
 #pragma unroll
     for (int q = 0; q < kRun; ++q) {
-      const int rl = __shfl(p + len, kRun * q + kRun - 1);
+      const int rl = lane_i32(p + len, kRun * q + kRun - 1);
       if (q < ry) img0 += rl;
     }
     wave_lds_order();  // every lane's accumulator reads before the image overwrites them
@@ -372,12 +383,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     // A fixed count of unpredicated stores: lanes past a run repeat the first
     // value of run 0 (row 0 of the column is always a row: same address, same
     // value), so the next layer's waits on its coordinate loads count past them
-    const int64_t dst0 = __shfl(rb, 0);
+    const int64_t dst0 = lane_i64(rb, 0);
     int off = 0;
 #pragma unroll
     for (int q = 0; q < kRun; ++q) {
-      const int rl = __shfl(p + len, kRun * q + kRun - 1);
-      const int64_t dst = __shfl(rb, kRun * q);
+      const int rl = lane_i32(p + len, kRun * q + kRun - 1);
+      const int64_t dst = lane_i64(rb, kRun * q);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {  // rl <= 7 rows x 15 = 105
         const int t = lane + 64 * h;
