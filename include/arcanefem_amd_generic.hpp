@@ -81,6 +81,23 @@ enum class Mode : int {
 
 /* ------------------------------------------------------------ unit kernel */
 
+/* One wavefront per block: its LDS operations execute in issue order, so the
+ * phases of a unit (adds -> flush reads -> image -> stores -> zero fill) need
+ * only the compiler to keep their order, not the lgkmcnt(0) drain of
+ * __syncthreads (define AFEM_GENERIC_WAVESYNC 0 to restore it). */
+#ifndef AFEM_GENERIC_WAVESYNC
+#define AFEM_GENERIC_WAVESYNC 1
+#endif
+__device__ __forceinline__ void unit_lds_order()
+{
+#if AFEM_GENERIC_WAVESYNC
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#else
+  __syncthreads();
+#endif
+}
+
 /* Writes layer L of unit U (its LDS buffer) to the values and zeroes the buffer. */
 template <int K, bool WIDE>
 __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const afem_functor_unit& U, int L,
@@ -115,14 +132,14 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
       const int gl = __shfl(glen, 8 * g);
       if (g < (lane >> 3)) my_off += gl;
     }
-    __syncthreads();
+    unit_lds_order();
     if (row >= 0) {
       const int o = my_off + (int)(rb - rb0);
 #pragma unroll
       for (int s = 0; s < 16; ++s)
         if (s < len) buf[o + s] = v[s];
     }
-    __syncthreads();
+    unit_lds_order();
     int ib = 0;
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
@@ -135,7 +152,7 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
       }
       ib += gl;
     }
-    __syncthreads();
+    unit_lds_order();
   }
   else if (row >= 0) {
     for (int s = 0; s < len; ++s)
@@ -150,9 +167,9 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
           p.values[idx] = overwrite ? val : p.values[idx] + val;
         }
   }
-  __syncthreads();
+  unit_lds_order();
   for (int i = lane; i < bufsz; i += 64) buf[i] = 0.0;
-  __syncthreads();
+  unit_lds_order();
 }
 
 /* One wavefront per unit (blockDim 64); dynamic LDS: nbuf * width * K^2 * sr
@@ -184,7 +201,7 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
   const afem_functor_unit U = p.units[u];
   const int bufsz = p.width * KK * sr;
   for (int i = lane; i < p.nbuf * bufsz; i += 64) acc[i] = 0.0;
-  __syncthreads();
+  unit_lds_order();
   // the lane's entries of the next group are loaded one group ahead (the next
   // group of this stage, else the first group of the next stage), so their
   // latency hides behind the functors; tagged with the group's first entry (a
@@ -277,7 +294,7 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
         }
       }
     }
-    __syncthreads();
+    unit_lds_order();
     if (L > 0) flush_layer<K, WIDE>(p, U, L - 1, acc, bufsz, sr, swz, lane, overwrite);
   }
   flush_layer<K, WIDE>(p, U, U.n_stages - 1, acc, bufsz, sr, swz, lane, overwrite);
