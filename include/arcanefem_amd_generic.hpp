@@ -84,9 +84,11 @@ enum class Mode : int {
 /* One wavefront per block: its LDS operations execute in issue order, so the
  * phases of a unit (adds -> flush reads -> image -> stores -> zero fill) need
  * only the compiler to keep their order, not the lgkmcnt(0) drain of
- * __syncthreads (define AFEM_GENERIC_WAVESYNC 0 to restore it). */
+ * __syncthreads.  Measured equal here (r04at: 1.89-1.90 ms with the module's
+ * element, the kernel waits on its gathers, not on LDS), so the default stays
+ * __syncthreads; define AFEM_GENERIC_WAVESYNC 1 for the wave-scope order. */
 #ifndef AFEM_GENERIC_WAVESYNC
-#define AFEM_GENERIC_WAVESYNC 1
+#define AFEM_GENERIC_WAVESYNC 0
 #endif
 __device__ __forceinline__ void unit_lds_order()
 {
