@@ -629,6 +629,30 @@ def test_canonical_lattice_random_numbering(ctx, variant, n, nz, seed):
     _check_values(v2, v1)
 
 
+@pytest.mark.parametrize("knobs", [{"AFEM_CUBES_YEX": "0"}, {"AFEM_CUBES_XEX": "0"},
+                                   {"AFEM_CUBES_CARRY": "0", "AFEM_CUBES_STRIDE": "49"}])
+def test_cube_kernel_face_sharing_variants(ctx, variant, knobs):
+    """The cube kernel's face-sharing variants (y exchange off, x exchange off,
+    no carry at 49-row planes) on a box with partial columns and z segments:
+    the oracle's matrix and RHS (1e-12), the default's to rounding."""
+    mesh = af.Mesh.structured(ctx, 3, 17, 11, jitter=0.2, seed=8)
+    variant("AFEM_CUBES_ZS", "4")
+    b0, l0 = _assemble_gpu(ctx, mesh, 5.5)
+    v0, r0 = b0.download()[2], l0.rhs_host()
+    for k, v in knobs.items():
+        variant(k, v)
+    b1, l1 = _assemble_gpu(ctx, mesh, 5.5)
+    assert b1.stats()["last_kernel"] == 10
+    rows, cols, v1 = b1.download()
+    cells, coords, _ = mesh.download()
+    orp, ocols = O.sparsity(mesh.n_nodes, mesh.n_own_nodes, cells)
+    ovals, orhs = O.assemble_poisson(mesh.n_own_nodes, cells, coords, orp, ocols, 5.5)
+    _check_values(v1, ovals)
+    assert np.abs(l1.rhs_host() - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+    assert np.abs(v1 - v0).max() <= VAL_TOL * np.abs(v0).max()
+    assert np.abs(l1.rhs_host() - r0).max() <= VAL_TOL * np.abs(r0).max()
+
+
 @pytest.mark.parametrize("n,nz,seed", [(6, 6, 3), (9, 15, 4), (13, 5, 5), (1, 3, 6)])
 def test_cube_kernel_on_random_numbering(ctx, n, nz, seed):
     """The cube kernel on a lattice of Kuhn cubes handed over as arrays in a
