@@ -1,6 +1,7 @@
 """A/B on C2 handed over as arrays in a random numbering (bench.py's c2_arrays
 input: seed 1234) in ONE process: one structure per variant of a library knob
-(e.g. AFEM_CANON 1 / 0), assembly kernels timed interleaved (HIP events,
+(e.g. AFEM_CANON 1 / 0; the knob stays set for that variant's assemblies too),
+assembly kernels timed interleaved (HIP events,
 median of `reps`), values compared between the variants.
 usage: python tools/arrays_ab.py VAR valA valB [n] [reps]"""
 import os
@@ -36,16 +37,17 @@ for v in (va, vb):
     print(v, {k: st[k] for k in ("n_slices", "uniform_slices", "stencil_slices", "general_slices", "brick_order",
                                  "max_slice_nodes")}, flush=True)
     variants.append((v, bsr))
-af.set_variant(var, None)
 times = {v: [] for v, _ in variants}
 for r in range(reps + 2):
     for v, bsr in variants:
+        af.set_variant(var, v)  # knobs read at assembly time (AFEM_ASSEMBLY_CUBES) as well as at the build
         ctx.event_record(0)
         bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set")
         ctx.event_record(1)
         ctx.synchronize()
         if r >= 2:
             times[v].append(ctx.event_elapsed(0, 1))
+af.set_variant(var, None)
 vals = [bsr.download()[2] for _, bsr in variants]
 for v, _ in variants:
     print(f"{var}={v}: median {np.median(times[v]):.4f} ms  all {' '.join(f'{t:.3f}' for t in times[v])}", flush=True)
