@@ -84,7 +84,8 @@ class BsrStats(ctypes.Structure):
                 ("n_slices", ctypes.c_int64), ("brick_order", ctypes.c_int32), ("uniform_slices", ctypes.c_int32),
                 ("last_kernel", ctypes.c_int32), ("stencil_slices", ctypes.c_int32),
                 ("stencil_sig", ctypes.c_int32), ("shared_strip_slices", ctypes.c_int64),
-                ("uniform_instance_slices", ctypes.c_int64), ("general_slices", ctypes.c_int64)]
+                ("uniform_instance_slices", ctypes.c_int64), ("general_slices", ctypes.c_int64),
+                ("cube_lattice", ctypes.c_int32), ("cube_axes", ctypes.c_int32)]
 
 
 class SolverOpts(ctypes.Structure):

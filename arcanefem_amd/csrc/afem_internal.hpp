@@ -267,6 +267,15 @@ struct Structure {
   // canonical slot t (4 bits each)
   bool cube_ok = false;
   int64_t cube_L[3] = { 0, 0, 0 };
+  // a lattice of Kuhn cubes handed over as arrays in a NATURAL numbering:
+  // node id = lexicographic lattice index with the axes taken in the order
+  // cube_axes (fastest first; x + Lx (y + Ly z) is {0, 1, 2}), every node
+  // owned -- the generator's layout up to the axis order, so the cube
+  // kernel's plain instance runs on it (nat_L: the lattice's node counts in
+  // that axis order; no maps)
+  bool cube_natural = false;
+  int nat_axes[3] = { 0, 1, 2 };
+  int64_t nat_L[3] = { 0, 0, 0 };
   DevBuf<int32_t> cube_phys;
   DevBuf<int64_t> cube_rb;
   DevBuf<uint64_t> cube_slot;

@@ -680,12 +680,15 @@ int afem_bsr_get_stats(afem_bsr* b, afem_bsr_stats* st)
   st->max_slice_width = b->s.max_slice_w;
   st->n_slices = b->s.n_slices;
   st->brick_order = b->s.lattice ? 2 : b->s.brick_order ? 1 : 0;
+  st->cube_lattice = b->s.cube_natural ? 2 : (b->s.canon && b->s.cube_ok) ? 3
+                     : (b->mesh->st.valid && b->mesh->st.dim == 3 && !b->s.canon) ? 1 : 0;
   st->uniform_slices = (int32_t)b->s.n_uni;
   st->stencil_slices = (int32_t)b->s.n_k;
   st->stencil_sig = b->s.sig_k;
   st->shared_strip_slices = b->s.n_strip_shared;
   st->uniform_instance_slices = b->s.n_ur;
   st->general_slices = b->s.n_ms + b->s.n_mb;
+  st->cube_axes = b->s.cube_natural ? b->s.nat_axes[0] + 3 * b->s.nat_axes[1] + 9 * b->s.nat_axes[2] : 0;
   st->last_kernel = b->last_kernel;
   API_END
 }

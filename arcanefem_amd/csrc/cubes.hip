@@ -646,19 +646,25 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   const Structure& S = b.s;
   const char* ce = variant("AFEM_ASSEMBLY_CUBES");  // 0: the strip / stencil kernels
   if ((ce && atoi(ce) == 0) || m.nv != 4 || b.nb_dof != 1) return false;
-  // a generator box (or z-slab of one), or a lattice of Kuhn cubes in the caller's numbering
-  const bool canon = S.canon && S.cube_ok;
-  if (!canon && (!st.valid || st.dim != 3 || S.canon || st.lx > 0 || st.ly > 0 || st.n < 1)) return false;
+  // a generator box (or z-slab of one), a lattice of Kuhn cubes in a natural
+  // numbering (lexicographic in some axis order: the plain instance, with the
+  // lattice axes in that order -- the kernel's geometry reads the real
+  // coordinates, and the cube's 6 tets do not depend on the axis order), or
+  // one in any other numbering (the caller's maps)
+  const bool natural = S.cube_natural;
+  const bool canon = !natural && S.canon && S.cube_ok;
+  if (!canon && !natural && (!st.valid || st.dim != 3 || S.canon || st.lx > 0 || st.ly > 0 || st.n < 1)) return false;
   Ctx& ctx = *m.ctx;
   CubeGeom g{};
-  if (canon) {
-    g.npx = (int)S.cube_L[0];
-    g.npy = (int)S.cube_L[1];
-    g.nzc = (int)S.cube_L[2] - 1;
+  if (canon || natural) {
+    const int64_t* Lc = natural ? S.nat_L : S.cube_L;
+    g.npx = (int)Lc[0];
+    g.npy = (int)Lc[1];
+    g.nzc = (int)Lc[2] - 1;
     g.k0 = 0;
-    g.k1 = (int)S.cube_L[2];
+    g.k1 = (int)Lc[2];
     g.ghost_lo = g.ghost_hi = -1;
-    g.L = S.cube_L[0] * S.cube_L[1];
+    g.L = Lc[0] * Lc[1];
   }
   else {
     g.npx = g.npy = st.n + 1;

@@ -88,17 +88,32 @@ __global__ void k_scatter_back(int64_t n, const int64_t* __restrict__ src, const
   if (p < n) out[src[p]] = in[p];
 }
 
-// the caller's view rows -> linear-system rows (owned ones); lengths, then fill
+// the caller's view rows -> linear-system rows (owned ones); lengths, then fill.
+// Every linear-system row must be claimed by exactly one caller row (claim
+// counts, as k_map_row_len does for the other direction): a row claimed twice
+// would make k_lsmap_fill write one row's entries past its own range
 __global__ void k_lsmap_len(int32_t nb_row, int32_t nnz, const int32_t* __restrict__ rows,
                             const int32_t* __restrict__ index, int64_t n_index, int64_t n_ls_rows,
-                            int64_t* __restrict__ len)
+                            int64_t* __restrict__ len, int32_t* __restrict__ claim, int32_t* __restrict__ err)
 {
   const int32_t R = (int32_t)((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
   if (R >= nb_row || R >= n_index) return;
   const int32_t a = index[R];
   if (a < 0 || a >= n_ls_rows) return;
+  if (atomicAdd(&claim[a], 1) != 0) {
+    atomicOr(err, 2);
+    return;
+  }
   const int32_t e = R + 1 < nb_row ? rows[R + 1] : nnz;  // row end as femutils/HypreDoFLinearSystem.cc:140-141
   len[a] = e - rows[R];
+}
+
+// every owned linear-system row reached by one caller row, and not empty
+__global__ void k_lsmap_check(int64_t n_ls_rows, const int64_t* __restrict__ len, const int32_t* __restrict__ claim,
+                              int32_t* __restrict__ err)
+{
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a < n_ls_rows && (claim[a] != 1 || len[a] <= 0)) atomicOr(err, 4);
 }
 
 __global__ void k_lsmap_fill(int32_t nb_row, int32_t nnz, const int32_t* __restrict__ rows,
@@ -236,11 +251,23 @@ void ls_set_csr_mapped(LinearSystem& ls, const int32_t* rows, const int32_t* col
   DevBuf<int64_t> len;
   len.alloc(ls.n_rows + 1);
   AFEM_HIP(hipMemsetAsync(len.p, 0, len.bytes(), ctx.stream));
+  DevBuf<int32_t> claim;
+  claim.alloc(ls.n_rows > 0 ? ls.n_rows : 1);
+  AFEM_HIP(hipMemsetAsync(claim.p, 0, claim.bytes(), ctx.stream));
   if (nb_row > 0) {
     hipLaunchKernelGGL(k_lsmap_len, dim3(grid_for(nb_row, 256)), dim3(256), 0, ctx.stream, nb_row, nnz, rows, index.p,
-                       n_index, ls.n_rows, len.p);
+                       n_index, ls.n_rows, len.p, claim.p, err.p);
     AFEM_LAUNCHED();
   }
+  if (ls.n_rows > 0) {
+    hipLaunchKernelGGL(k_lsmap_check, dim3(grid_for(ls.n_rows, 256)), dim3(256), 0, ctx.stream, ls.n_rows, len.p,
+                       claim.p, err.p);
+    AFEM_LAUNCHED();
+  }
+  const int32_t map_err = read_flag(ctx, err.p);
+  AFEM_REQUIRE((map_err & 2) == 0, AFEM_ERR_ARG, "setCSRValues: two rows of the view map to one linear-system row");
+  AFEM_REQUIRE((map_err & 4) == 0, AFEM_ERR_ARG,
+               "setCSRValues: an owned linear-system row gets no row (or an empty one) from the view");
   ls.own_rows.alloc(ls.n_rows + 1);
   exclusive_scan_i64(ctx, len.p, ls.own_rows.p, ls.n_rows);
   const int64_t n_own_nz = read_i64(ctx, ls.own_rows.p + ls.n_rows);

@@ -789,7 +789,8 @@ __global__ __launch_bounds__(1024) void k_reduce(int64_t n, const double* __rest
 // Jacobi preconditioner + constraint-row flag: a row whose diagonal exceeds
 // the rest of the row by > 1e10 (penalty P = 1e30, eliminated identity rows)
 // is excluded from the reference value of the stopping test (same rule as
-// oracle/oracle.c::orc_pcg_jacobi).
+// oracle/oracle.c::orc_pcg_jacobi; duplicate (i,i) entries of a view add up,
+// as the SpMV applies them).
 // 16 lanes per row: the row's columns and values are read coalesced (one
 // thread per row walked 15 entries 120 B apart from its neighbours': 20 ms per
 // solve at C4), the diagonal and the |off-diagonal| sum are 16-lane

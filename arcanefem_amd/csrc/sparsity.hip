@@ -1972,6 +1972,122 @@ __global__ void k_cube_maps(int64_t n, const int32_t* __restrict__ inv, const in
   slot_out[i] = w;
 }
 
+// axis orders of a lexicographic numbering, fastest axis first
+constexpr int kAxisOrders[6][3] = { { 0, 1, 2 }, { 0, 2, 1 }, { 1, 0, 2 }, { 1, 2, 0 }, { 2, 0, 1 }, { 2, 1, 0 } };
+
+// ---- natural lattice numberings.  A cartesian mesh handed over as arrays
+// (Arcane's cartesian generator, a caller's own lexicographic loops) numbers
+// its nodes lexicographically: id = l_a + L_a (l_b + L_b l_c) for some order
+// (a, b, c) of the axes.  Up to that axis order this is the generator's box:
+// the cube kernel runs on the caller's arrays with no map, when every cell is
+// one of the 6 Kuhn tets of its lattice cube (the 6 tets of a cube are the 6
+// axis permutations of the path from its lower to its upper corner, a set
+// that does not depend on the axis order).
+
+// bit q of *bad: node i is not at lexicographic index i in axis order q
+__global__ void k_natural_ids(int64_t n, const int32_t* __restrict__ lx, const int32_t* __restrict__ ly,
+                              const int32_t* __restrict__ lz, int64_t L0, int64_t L1, int64_t L2,
+                              int32_t* __restrict__ bad)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t l[3] = { lx[i], ly[i], lz[i] };
+  const int64_t L[3] = { L0, L1, L2 };
+  int32_t b = 0;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int a = kAxisOrders[q][0], c = kAxisOrders[q][1], d = kAxisOrders[q][2];
+    if (l[a] + L[a] * (l[c] + L[c] * l[d]) != i) b |= 1 << q;
+  }
+  if (b) atomicOr(bad, b);
+}
+
+// every cell a Kuhn tet of its lattice cube, no cube holding one twice
+// (with 6 cells per cube: each cube holds all six)
+__global__ void k_kuhn_cubes(int64_t nc, const int32_t* __restrict__ cn, const int32_t* __restrict__ lx,
+                             const int32_t* __restrict__ ly, const int32_t* __restrict__ lz, int64_t L0, int64_t L1,
+                             int32_t* __restrict__ seen, int32_t* __restrict__ err)
+{
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  int x[4], y[4], z[4];
+  int mx = 1 << 30, my = 1 << 30, mz = 1 << 30;
+  for (int a = 0; a < 4; ++a) {
+    const int32_t v = cn[4 * c + a];
+    x[a] = lx[v];
+    y[a] = ly[v];
+    z[a] = lz[v];
+    mx = min(mx, x[a]);
+    my = min(my, y[a]);
+    mz = min(mz, z[a]);
+  }
+  // a Kuhn path climbs every lexicographic index at each step: sort by one
+  auto lid = [&](int a) { return (int64_t)x[a] + L0 * ((int64_t)y[a] + L1 * (int64_t)z[a]); };
+  for (int i = 1; i < 4; ++i)
+    for (int j = i; j > 0 && lid(j) < lid(j - 1); --j) {
+      const int tx = x[j], ty = y[j], tz = z[j];
+      x[j] = x[j - 1];
+      y[j] = y[j - 1];
+      z[j] = z[j - 1];
+      x[j - 1] = tx;
+      y[j - 1] = ty;
+      z[j - 1] = tz;
+    }
+  auto axis = [&](int a, int b) -> int {
+    const int dx = x[b] - x[a], dy = y[b] - y[a], dz = z[b] - z[a];
+    if (dx == 1 && dy == 0 && dz == 0) return 0;
+    if (dx == 0 && dy == 1 && dz == 0) return 1;
+    if (dx == 0 && dy == 0 && dz == 1) return 2;
+    return -1;
+  };
+  const int a0 = axis(0, 1), a1 = axis(1, 2), a2 = axis(2, 3);
+  if (a0 < 0 || a1 < 0 || a2 < 0 || a0 == a1 || a1 == a2 || a0 == a2 || mx + 1 >= L0 || my + 1 >= L1) {
+    *err = 1;
+    return;
+  }
+  const int bit = 1 << (3 * a0 + a1);
+  const int64_t cube = mx + (L0 - 1) * (my + (L1 - 1) * (int64_t)mz);
+  if (atomicOr(&seen[cube], bit) & bit) *err = 1;
+}
+
+// s.cube_natural (and the axis order) when the mesh is such a lattice
+bool natural_lattice(Mesh& m, Structure& s)
+{
+  Ctx& ctx = *m.ctx;
+  const int64_t n = s.n_rows;
+  DevBuf<int32_t> lat3[3];
+  int64_t L[3];
+  if (!lattice_coords(ctx, m, n, lat3, L)) return false;
+  const int64_t nc = m.n_cells;
+  const int64_t n_cubes = (L[0] - 1) * (L[1] - 1) * (L[2] - 1);
+  if (nc != 6 * n_cubes || nc == 0 || n > (int64_t)INT32_MAX) return false;
+  DevBuf<int32_t> flags, seen;
+  flags.alloc(2);
+  seen.alloc(n_cubes);
+  AFEM_HIP(hipMemsetAsync(flags.p, 0, flags.bytes(), ctx.stream));
+  AFEM_HIP(hipMemsetAsync(seen.p, 0, seen.bytes(), ctx.stream));
+  hipLaunchKernelGGL(k_natural_ids, dim3(grid_for(n, 256)), dim3(256), 0, ctx.stream, n, lat3[0].p, lat3[1].p,
+                     lat3[2].p, L[0], L[1], L[2], flags.p);
+  AFEM_LAUNCHED();
+  hipLaunchKernelGGL(k_kuhn_cubes, dim3(grid_for(nc, 256)), dim3(256), 0, ctx.stream, nc, m.cell_node.p, lat3[0].p,
+                     lat3[1].p, lat3[2].p, L[0], L[1], seen.p, flags.p + 1);
+  AFEM_LAUNCHED();
+  int32_t h[2] = { 0, 0 };
+  AFEM_HIP(hipMemcpyAsync(h, flags.p, sizeof(h), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  if (h[1] != 0) return false;
+  for (int q = 0; q < 6; ++q)
+    if (!((h[0] >> q) & 1)) {
+      s.cube_natural = true;
+      for (int a = 0; a < 3; ++a) {
+        s.nat_axes[a] = kAxisOrders[q][a];
+        s.nat_L[a] = L[kAxisOrders[q][a]];
+      }
+      return true;
+    }
+  return false;
+}
+
 // the canonical structure of a lattice mesh (see above) into s; false when it
 // does not apply or does not reach the stencil instance
 bool canonical_lattice(Mesh& m, Structure& s)
@@ -2110,11 +2226,30 @@ bool canonical_lattice(Mesh& m, Structure& s)
 void build_structure(Mesh& m, Structure& s, int nb_dof)
 {
   build_structure_impl(m, s);
+  if (!(nb_dof == 1 && s.lattice && m.nv == 4 && m.dim == 3 && m.n_nodes == m.n_own)) return;
+  // an array-fed Kuhn lattice in a natural numbering: the cube kernel as on
+  // the generator's box (AFEM_CUBE_NATURAL=0: not)
+  const char* ne = variant("AFEM_CUBE_NATURAL");
+  if (!(ne && atoi(ne) == 0)) (void)natural_lattice(m, s);
   // an array-fed lattice whose numbering keeps it off the stencil instance
+  // (for the strip kernels: a natural numbering in another axis order too)
   const char* ce = variant("AFEM_CANON");
-  if (nb_dof == 1 && s.lattice && m.nv == 4 && m.dim == 3 && m.n_nodes == m.n_own && s.n_k * 2 < s.n_slices &&
-      s.max_row_len <= 16 && !(ce && atoi(ce) == 0))
-    (void)canonical_lattice(m, s);
+  if (s.n_k * 2 < s.n_slices && s.max_row_len <= 16 && !(ce && atoi(ce) == 0)) {
+    const bool nat = s.cube_natural;
+    int ax[3];
+    int64_t nl[3];
+    for (int a = 0; a < 3; ++a) {
+      ax[a] = s.nat_axes[a];
+      nl[a] = s.nat_L[a];
+    }
+    if (canonical_lattice(m, s)) {
+      s.cube_natural = nat;
+      for (int a = 0; a < 3; ++a) {
+        s.nat_axes[a] = ax[a];
+        s.nat_L[a] = nl[a];
+      }
+    }
+  }
 }
 
 }  // namespace afem

@@ -69,10 +69,13 @@ def parse(argv=None):
     ap.add_argument("--cg-iters", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true",
                     help="skip the CPU baselines (the oracle timed at the C2 size on the host cores, N = 1 only)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_assembly_C2.json"))
     ap.add_argument("--no-extras", action="store_true", help="skip the side measurements (N = 1 only anyway)")
-    ap.add_argument("--legs", default="c4,c3,c2_generic,c2_arrays,unstructured,c5",
-                    help="the side measurements to run (comma list of c4, c3, c2_generic, c2_arrays, unstructured, c5)")
+    ap.add_argument("--legs", default="c4,c3,c2_generic,c2_arrays,c2_arrays_natural,unstructured,c5",
+                    help="the side measurements to run (comma list of c4, c3, c2_generic, c2_arrays, "
+                         "c2_arrays_natural, unstructured, c5)")
+    ap.add_argument("--no-headline", action="store_true",
+                    help="N = 1: skip the headline C2 step (and the CPU baselines), run only --legs (per-leg "
+                         "rocprofv3 runs, tools/profile_legs.sh)")
     ap.add_argument("--c3-n", type=int, default=170, help="C3 block-3 elasticity box (170 -> 5.0M nodes)")
     ap.add_argument("--c4-n", type=int, default=463, help="C4 Poisson box on one GPU (463 -> 99.9M DoF); 0: skip")
     ap.add_argument("--c5-n", type=int, default=128,
@@ -196,26 +199,72 @@ def roofline(bsr, mesh, kernel_ms):
     nnz = bsr.view().nnz_blocks
     ab = algorithmic_bytes(int(st["n_incidences"]), mesh.n_nodes, mesh.n_own_nodes, nnz)
     achieved = ab / (kernel_ms * 1e-3) / 1e9
+    if st.get("last_kernel") == 10:
+        kmin = cube_min_bytes(st, mesh.n_nodes, mesh.n_own_nodes, nnz)
+        kmin_note = "cube kernel: coordinates + row offsets (or canonical maps) + values + RHS"
+    else:
+        kmin = ab
+        kmin_note = ("strip kernels: per-row strips and slice node lists replace the incidence table; "
+                     "taken as the algorithmic bytes")
     return {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(ab),
+            "bytes_kernel_min": int(kmin), "bytes_kernel_min_note": kmin_note,
+            "frac_kernel_min": round(kmin / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "kernel_ms": round(kernel_ms, 4),
+            "cube_lattice": int(st.get("cube_lattice", 0)),
             "inc_padding": round(st["inc_table_entries"] / max(int(st["n_incidences"]), 1) - 1.0, 4),
             "uniform_slice_frac": round(st["uniform_slices"] / max(st["n_slices"], 1), 4),
             "stencil_slice_frac": round(st["stencil_slices"] / max(st["n_slices"], 1), 4),
             "shared_strip_frac": round(st.get("shared_strip_slices", 0) / max(st["n_slices"], 1), 4)}
 
 
-def pmc_traffic(path, n):
-    """HBM bytes per assembly launch from a committed PMC summary
-    (tools/collect_profiles.py) when it was taken at this size on one GPU."""
+def cube_min_bytes(st, n_local, n_own, nnz, rhs_read=False):
+    """What the cube kernel (cubes.hip) must move per launch: it derives the
+    connectivity from the lattice, so it reads the node coordinates (24 B),
+    the row offsets (8 B per row; canonical maps instead: caller id 4 B, first
+    value 8 B, slot map 8 B) and writes every value (8 B per non-zero) and the
+    RHS (8 B per row; + 8 B read when it adds).  VERDICT r4 #1: the
+    algorithmic bytes count the incidence table and the columns, which this
+    kernel never reads."""
+    rows = 20 * n_own if st.get("cube_lattice") == 3 else 8 * (n_own + 1)
+    return 24 * n_local + rows + 8 * nnz + (16 if rhs_read else 8) * n_own
+
+
+def leg_profile(leg, size):
+    """profiles/pmc_<leg>.json (tools/collect_leg.py) when it was taken at this
+    size on one GPU: the HBM bytes per launch of the leg's kernels from the
+    rocprofv3 PMC passes (2 FETCH_SIZE + WRITE_SIZE) and their rocprofv3
+    kernel-trace mean duration."""
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, "profiles", f"pmc_{leg}.json")) as f:
             pm = json.load(f)
-        if pm.get("n") == n and pm.get("world") in (None, 1):
-            return pm.get("hbm_bytes_per_launch"), pm.get("tag")
     except (OSError, ValueError):
-        pass
-    return None, None
+        return None
+    return pm if pm.get("size") == size and pm.get("world") in (None, 1) else None
+
+
+def with_traffic(rf, leg, size, kernel_ms):
+    """roofline.traffic / frac_traffic: the PMC bytes per
+    launch of the committed profile of this leg at this size, over this run's
+    kernel time; the same two fractions recomputed from the profile's own
+    rocprofv3 mean (frac_profile, frac_traffic_profile) so the line can be
+    checked against profiles/ alone."""
+    pm = leg_profile(leg, size)
+    rf["traffic"] = rf["frac_traffic"] = None
+    if pm is None:
+        return rf
+    b = pm["hbm_bytes_per_launch"]
+    rf["traffic"] = int(b)
+    rf["frac_traffic"] = round(b / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    rf["traffic_profile"] = pm.get("tag")
+    pk = pm.get("kernel_mean_ms")
+    if pk:
+        rf["profile_kernel_ms"] = round(pk, 4)
+        rf["frac_profile"] = round(rf["algorithmic_bytes_per_launch"] / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        rf["frac_traffic_profile"] = round(b / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if rf.get("bytes_kernel_min"):
+        rf["traffic_over_min"] = round(b / rf["bytes_kernel_min"], 3)
+    return rf
 
 
 def settle(ctx, step, ms):
@@ -236,6 +285,23 @@ def settle(ctx, step, ms):
         ctx.synchronize()
         k += 8
     return k
+
+
+def time_launches(ctx, fn, reps, warmup, settle_ms, base=200):
+    """A side leg's kernel timing, like the headline's: `fn` back to back for
+    settle_ms (untimed, the clocks' ramp), `warmup` untimed launches, then
+    `reps` launches each bracketed by HIP events on the context stream.
+    Returns (the per-launch ms, settle launches)."""
+    steps = settle(ctx, fn, settle_ms)
+    for _ in range(warmup):
+        fn()
+    ctx.synchronize()
+    for i in range(reps):
+        ctx.event_record(base + 2 * i)
+        fn()
+        ctx.event_record(base + 2 * i + 1)
+    ctx.synchronize()
+    return [ctx.event_elapsed(base + 2 * i, base + 2 * i + 1) for i in range(reps)], steps
 
 
 def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50, settle_ms=150.0):
@@ -272,8 +338,7 @@ def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50, settle_ms=150.0):
                                                                        / HBM_PEAK_GBS, 4),
            "cg_device_ms": round(st["solve_ms"], 2), "cg_spmv": SPMV_KERNELS.get(st["spmv_kernel"]),
            "sparsity_ms": round(sp_ms, 1), "settle_ms": settle_ms, "settle_steps": settle_steps}
-    out["roofline"]["traffic"], out["roofline"]["traffic_profile"] = pmc_traffic(
-        os.path.join(ROOT, "profiles", f"pmc_assembly_n{n}.json"), n)
+    with_traffic(out["roofline"], "c4", n, kms)
     ctx.free(dbottom)
     ls.reset()
     bsr.close()
@@ -281,7 +346,7 @@ def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50, settle_ms=150.0):
     return out
 
 
-def elasticity_c3(ctx, af, n, reps=10, warmup=2):
+def elasticity_c3(ctx, af, n, reps=10, warmup=2, settle_ms=150.0):
     """BASELINE config C3: block-3 P1 elasticity on tetrahedra (BSR, ordered per
     block), stiffness + body force fused, on fixed sparsity; kernel time = median
     of HIP-event launch times.  Algorithmic bytes per launch: incidence
@@ -298,15 +363,9 @@ def elasticity_c3(ctx, af, n, reps=10, warmup=2):
     sp_ms = (time.perf_counter() - t0) * 1e3
     rhs = ctx.malloc(8 * 3 * mesh.n_own_nodes)
     f = (0.0, 0.0, -1.0)
-    for _ in range(warmup):
-        bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs, rhs_mode="set")
-    ctx.synchronize()
-    for i in range(reps):
-        ctx.event_record(230 + 2 * i)
-        bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs, rhs_mode="set")
-        ctx.event_record(231 + 2 * i)
-    ctx.synchronize()
-    kms = float(np.median([ctx.event_elapsed(230 + 2 * i, 231 + 2 * i) for i in range(reps)]))
+    ks, settle_steps = time_launches(ctx, lambda: bsr.assembleElasticityP1Ex(lam, mu2, 0.0, f, rhs, rhs_mode="set"),
+                                     reps, warmup, settle_ms)
+    kms = float(np.median(ks))
     st = bsr.stats()
     v = bsr.view()
     nnz_b = v.nnz_blocks
@@ -318,8 +377,13 @@ def elasticity_c3(ctx, af, n, reps=10, warmup=2):
            "kernel": ELAST3_KERNELS.get(int(st["last_kernel"]), str(int(st["last_kernel"]))),
            "roofline": {"bound": "hbm", "achieved": round(ab / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(ab / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "algorithmic_bytes_per_launch": int(ab)},
+                        "algorithmic_bytes_per_launch": int(ab), "bytes_kernel_min": int(ab),
+                        "bytes_kernel_min_note": "strip kernels: per-row strips and slice node lists replace the "
+                                                 "incidence table; taken as the algorithmic bytes",
+                        "kernel_ms": round(kms, 4)},
+           "kernel_ms_all": [round(x, 4) for x in ks], "settle_steps": settle_steps,
            "sparsity_ms": round(sp_ms, 1)}
+    with_traffic(out["roofline"], "c3", n, kms)
     ctx.free(rhs)
     bsr.close()
     mesh.close()
@@ -354,7 +418,7 @@ def refine_tets(cells, coords, levels, device):
     return c.to(torch.int32).cpu().numpy(), x.cpu().numpy()
 
 
-def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2):
+def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2, settle_ms=150.0):
     """An unstructured mesh at the C2 scale: the reference's L-shape-3D Gmsh
     mesh refined `levels` times (levels = 6: 68 M tets, 12 M DoF).  No brick
     order, no uniform slices: Hilbert-curve slices and the general strip
@@ -373,20 +437,16 @@ def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2):
     ctx.synchronize()
     sp_ms = (time.perf_counter() - t0) * 1e3
     rhs = ctx.malloc(8 * mesh.n_own_nodes)
-    for _ in range(warmup):
-        bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set")
-    ctx.synchronize()
-    for i in range(reps):
-        ctx.event_record(240 + 2 * i)
-        bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set")
-        ctx.event_record(241 + 2 * i)
-    ctx.synchronize()
-    kms = float(np.median([ctx.event_elapsed(240 + 2 * i, 241 + 2 * i) for i in range(reps)]))
+    ks, settle_steps = time_launches(ctx, lambda: bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set"), reps, warmup,
+                                     settle_ms)
+    kms = float(np.median(ks))
     st = bsr.stats()
     out = {"config": f"{mesh_file} refined {levels}x ({mesh.n_own_nodes} DoF, {mesh.n_cells} tets, "
                      f"max row length {st['max_row_len']}), Hilbert-ordered slices, Poisson assembly + source",
            "dof": int(mesh.n_own_nodes), "value": round(mesh.n_own_nodes / (kms * 1e-3) / 1e6, 1),
-           "unit": "MDoF/s (assembly kernels)", "kernel_ms": round(kms, 4), "roofline": roofline(bsr, mesh, kms),
+           "unit": "MDoF/s (assembly kernels)", "kernel_ms": round(kms, 4),
+           "roofline": with_traffic(roofline(bsr, mesh, kms), "unstructured", levels, kms),
+           "kernel_ms_all": [round(x, 4) for x in ks], "settle_steps": settle_steps,
            "last_kernel": int(st["last_kernel"]), "max_slice_nodes": int(st["max_slice_nodes"]),
            "max_slice_width": int(st["max_slice_width"]), "sparsity_ms": round(sp_ms, 1)}
     ctx.free(rhs)
@@ -395,22 +455,32 @@ def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2):
     return out
 
 
-def c2_arrays_leg(ctx, af, n, reps=10, warmup=2):
+def c2_arrays_leg(ctx, af, n, natural=False, reps=10, warmup=2, settle_ms=150.0):
     """C2 handed over the way a caller's mesh arrives: the generator's box
-    downloaded, its nodes and cells renumbered by a seeded random permutation
-    (seed 1234, SURVEY §8d's robustness variant) and uploaded with
-    afem_mesh_create.  The structure build recovers the lattice from the
-    coordinates (brick_order 2) and the assembly runs the same instances as on
-    the generator's box.  Poisson assembly + source, median kernel time,
-    roofline as C2's."""
+    downloaded and uploaded with afem_mesh_create.
+    * natural=False (`c2_arrays`): nodes and cells renumbered by a seeded
+      random permutation (seed 1234, SURVEY §8d's robustness variant); the
+      structure build recovers the lattice from the coordinates and the cube
+      kernel runs through the caller-numbering maps (cube_lattice 3);
+    * natural=True (`c2_arrays_natural`): the nodes in the
+      lexicographic order of a cartesian Arcane mesh (x fastest: the
+      generator's own numbering), the cells in a random order with their
+      vertices rotated; the structure build recognises the natural lattice and
+      runs the headline cube kernel on the caller's arrays with no map
+      (cube_lattice 2).
+    Poisson assembly + source, median kernel time, roofline as C2's."""
     m0 = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
     cells, coords, _ = m0.download()
     m0.close()
     rng = np.random.default_rng(1234)
-    p = rng.permutation(coords.shape[0]).astype(np.int32)
-    cells = p[cells][rng.permutation(cells.shape[0])]
-    pc = np.empty_like(coords)
-    pc[p] = coords
+    if natural:
+        cells = np.ascontiguousarray(np.roll(cells[rng.permutation(cells.shape[0])], 1, axis=1))
+        pc = coords
+    else:
+        p = rng.permutation(coords.shape[0]).astype(np.int32)
+        cells = p[cells][rng.permutation(cells.shape[0])]
+        pc = np.empty_like(coords)
+        pc[p] = coords
     del coords
     mesh = af.Mesh.from_arrays(ctx, 3, cells, pc)
     del cells, pc
@@ -421,28 +491,28 @@ def c2_arrays_leg(ctx, af, n, reps=10, warmup=2):
     ctx.synchronize()
     sp_ms = (time.perf_counter() - t0) * 1e3
     rhs = ctx.malloc(8 * mesh.n_own_nodes)
-    for _ in range(warmup):
-        bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set")
-    ctx.synchronize()
-    for i in range(reps):
-        ctx.event_record(200 + 2 * i)
-        bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set")
-        ctx.event_record(201 + 2 * i)
-    ctx.synchronize()
-    kms = float(np.median([ctx.event_elapsed(200 + 2 * i, 201 + 2 * i) for i in range(reps)]))
+    ks, settle_steps = time_launches(ctx, lambda: bsr.assemblePoissonP1(1.0, 5.5, rhs, rhs_mode="set"), reps, warmup,
+                                     settle_ms)
+    kms = float(np.median(ks))
     st = bsr.stats()
-    out = {"config": f"C2 box n={n} via afem_mesh_create, nodes and cells in a random order (seed 1234): "
+    order = "lexicographic (x fastest) node order, cells in a random order" if natural else \
+        "nodes and cells in a random order (seed 1234)"
+    out = {"config": f"C2 box n={n} via afem_mesh_create, {order}: "
                      f"{mesh.n_own_nodes} DoF, {mesh.n_cells} tets, Poisson assembly + source",
            "dof": int(mesh.n_own_nodes), "value": round(mesh.n_own_nodes / (kms * 1e-3) / 1e6, 1),
-           "unit": "MDoF/s (assembly kernels)", "kernel_ms": round(kms, 4), "roofline": roofline(bsr, mesh, kms),
-           "brick_order": int(st["brick_order"]), "sparsity_ms": round(sp_ms, 1)}
+           "unit": "MDoF/s (assembly kernels)", "kernel_ms": round(kms, 4),
+           "roofline": with_traffic(roofline(bsr, mesh, kms), "c2_arrays_natural" if natural else "c2_arrays", n,
+                                    kms),
+           "kernel_ms_all": [round(x, 4) for x in ks], "settle_steps": settle_steps,
+           "brick_order": int(st["brick_order"]), "cube_lattice": int(st["cube_lattice"]),
+           "sparsity_ms": round(sp_ms, 1)}
     ctx.free(rhs)
     bsr.close()
     mesh.close()
     return out
 
 
-def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2):
+def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2, settle_ms=150.0):
     """C2 through the path an UNCHANGED module takes: BSRFormat::assembleBilinear
     with the module's own element lambda (_computeElementMatrixTetra4Gpu,
     modules/poisson/FemModule.h:177-186: examples/elements.hpp PoissonTet4,
@@ -465,21 +535,12 @@ def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2):
     ctx.synchronize()
     plan_ms = (time.perf_counter() - t0) * 1e3
 
-    def timed(fn, base, r, w):
-        for _ in range(w):
-            fn()
-        ctx.synchronize()
-        for i in range(r):
-            ctx.event_record(base + 2 * i)
-            fn()
-            ctx.event_record(base + 2 * i + 1)
-        ctx.synchronize()
-        return [ctx.event_elapsed(base + 2 * i, base + 2 * i + 1) for i in range(r)]
-
-    ks = timed(lambda: gx.assemble(bsr, gx.POISSON, gx.UNITS, overwrite=True), 150, reps, warmup)
+    ks, settle_steps = time_launches(ctx, lambda: gx.assemble(bsr, gx.POISSON, gx.UNITS, overwrite=True), reps,
+                                     warmup, settle_ms, base=150)
     kms = float(np.median(ks))
     vals_u = bsr.download()[2]
-    ka = timed(lambda: gx.assemble(bsr, gx.POISSON, gx.ATOMIC, overwrite=True), 190, atomic_reps, 1)
+    ka, _ = time_launches(ctx, lambda: gx.assemble(bsr, gx.POISSON, gx.ATOMIC, overwrite=True), atomic_reps, 1, 0.0,
+                          base=190)
     kam = float(np.median(ka))
     bsr.assemblePoissonP1(1.0, 0.0, None)
     vals_f = bsr.download()[2]
@@ -487,19 +548,31 @@ def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2):
     nnz = bsr.view().nnz_blocks
     ab = 4 * int(st["n_incidences"]) + 24 * mesh.n_nodes + 8 * (mesh.n_own_nodes + 1) + 12 * nnz
     ach = ab / (kms * 1e-3) / 1e9
+    # what k_assemble_units must move: its plan entries, the functor's own
+    # connectivity read per evaluation (4 x i32: the module's lambda reads
+    # cn_cv itself), coordinates, row offsets, values
+    ent_b = 24 if plan["wide"] else 16
+    kmin = (ent_b + 16) * plan["n_entries"] + 24 * mesh.n_nodes + 8 * (mesh.n_own_nodes + 1) + 8 * nnz
     out = {"config": f"C2 box n={n} ({mesh.n_own_nodes} DoF, {mesh.n_cells} tets): assembleBilinear(the Poisson "
                      f"module's tet4 element lambda) through the generic element-functor entry, values overwritten",
            "dof": int(mesh.n_own_nodes), "value": round(mesh.n_own_nodes / (kms * 1e-3) / 1e6, 1),
            "unit": "MDoF/s (assembly kernel)", "kernel_ms": round(kms, 4), "kernel_ms_all": [round(x, 4) for x in ks],
            "roofline": {"bound": "hbm", "kernel": "k_assemble_units<4,1,compact,PoissonTet4>",
                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(ab)},
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(ab),
+                        "bytes_kernel_min": int(kmin),
+                        "bytes_kernel_min_note": "plan entries + the functor's connectivity reads per evaluation "
+                                                 "+ coordinates + row offsets + values",
+                        "frac_kernel_min": round(kmin / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "kernel_ms": round(kms, 4)},
+           "settle_steps": settle_steps,
            "evaluations_per_cell": round(plan["n_entries"] / mesh.n_cells, 4),
            "plan": {k: int(plan[k]) for k in ("n_units", "n_stages", "n_entries", "rows_per_layer", "width", "nbuf",
                                               "wide", "lattice")},
            "plan_build_ms": round(plan_ms, 1),
            "atomic_kernel_ms": round(kam, 4), "atomic_frac": round(ab / (kam * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "vs_fixed_physics_max_rel": float(np.abs(vals_u - vals_f).max() / np.abs(vals_f).max())}
+    with_traffic(out["roofline"], "c2_generic", n, kms)
     bsr.close()
     mesh.close()
     return out
@@ -661,23 +734,27 @@ def cpu_baseline_cg(c2, iters=50, runs=3):
             ts.append(time.perf_counter() - t0)
         return float(np.median(ts))
 
+    runs_lease = runs
     t_lease = median_on(lease)
     # every core of the mask: one run when a cgroup quota caps the job below it
     # (the oversubscribed barrier-heavy loop took 27 s per run at 256 threads)
     quota = cgroup_cpu_limit()
+    runs_aff = runs
     if aff != lease:
-        runs = 1 if quota is not None and quota < aff else runs
+        runs_aff = runs = 1 if quota is not None and quota < aff else runs
         t_aff = median_on(aff)
     else:
         t_aff = t_lease
     t, threads = (t_lease, lease) if t_lease <= t_aff else (t_aff, aff)
     return {"value": round(iters / t, 2), "unit": "iter/s", "cores": threads, "kind": "port",
-            "value_lease_threads": round(iters / t_lease, 2), "lease_threads": lease,
-            "value_all_cores": round(iters / t_aff, 2), "affinity_cores": aff, "cgroup_cpu_quota": quota,
+            "value_lease_threads": round(iters / t_lease, 2), "lease_threads": lease, "runs_lease_threads": runs_lease,
+            "value_all_cores": round(iters / t_aff, 2), "affinity_cores": aff, "runs_all_cores": runs_aff,
+            "cgroup_cpu_quota": quota,
             "sample": f"Jacobi-PCG (oracle/oracle.c orc_pcg_jacobi_omp) on the C2 system ({rp.size - 1} DoF, "
                       f"{int(rp[-1])} nnz): {iters} fixed iterations: {t_lease * 1e3:.1f} ms on the lease's {lease} "
-                      f"OpenMP threads (median of 3), {t_aff * 1e3:.1f} ms on {aff} (every core of the affinity mask; "
-                      f"cgroup CPU quota {quota}); value = the faster ({threads} threads)"}
+                      f"OpenMP threads (median of {runs_lease}), {t_aff * 1e3:.1f} ms on {aff} (every core of the "
+                      f"affinity mask; {'median of ' + str(runs_aff) if runs_aff > 1 else 'ONE run'}; cgroup CPU "
+                      f"quota {quota}); value = the faster ({threads} threads)"}
 
 
 def cpu_baseline_c1(runs=3):
@@ -711,6 +788,27 @@ def cpu_baseline_c1(runs=3):
                       f"semantics end to end, median of {runs}; max|u| = {np.abs(x).max():.6g}"}
 
 
+def run_legs(ctx, af, args, legs):
+    """The N = 1 side measurements named in `legs`, each with its own settle."""
+    extras = {}
+    sm = args.settle_ms
+    if "c4" in legs and args.c4_n > 0:
+        extras["c4"] = poisson_c4(ctx, af, args.c4_n, settle_ms=sm)
+    if "c3" in legs:
+        extras["c3"] = elasticity_c3(ctx, af, args.c3_n, settle_ms=sm)
+    if "c2_generic" in legs:
+        extras["c2_generic"] = c2_generic_leg(ctx, af, 215, settle_ms=sm)
+    if "c2_arrays" in legs:
+        extras["c2_arrays"] = c2_arrays_leg(ctx, af, 215, settle_ms=sm)
+    if "c2_arrays_natural" in legs:
+        extras["c2_arrays_natural"] = c2_arrays_leg(ctx, af, 215, natural=True, settle_ms=sm)
+    if "unstructured" in legs and args.unstructured_levels > 0:
+        extras["unstructured"] = unstructured_leg(ctx, af, "L-shape-3D.msh", args.unstructured_levels, settle_ms=sm)
+    if "c5" in legs:
+        extras["c5"] = elastodynamics_c5(ctx, af, args.c5_n, args.c5_steps)
+    return extras
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -736,6 +834,12 @@ def main():
 
         dist.init_process_group("gloo")
     ctx = af.Context(local_rank % ndev)
+    if args.no_headline:
+        if world > 1:
+            raise SystemExit("bench.py: --no-headline runs the N = 1 side legs only")
+        print(json.dumps({"legs_only": True, "settle_ms": args.settle_ms,
+                          **run_legs(ctx, af, args, set(args.legs.split(",")))}), flush=True)
+        return
     n = args.n
     nz = n * world if args.scaling == "weak" else n
     t_setup = time.perf_counter()
@@ -756,6 +860,25 @@ def main():
     setup_s = time.perf_counter() - t_setup
     step = make_step(ctx, bsr, ls, bottom, dbottom)
 
+    # unsettled: W warmup steps and K timed steps right after the setup, before
+    # the clock-settle phase (the line reports both; the settled run
+    # below is `value`)
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    if dist:
+        dist.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    uslots = min(args.steps, 27)
+    for i in range(args.steps):
+        step(200 + 2 * i if i < uslots else None)
+    ctx.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed_unsettled = time.perf_counter() - t0
+    kernel_ms_unsettled = [ctx.event_elapsed(200 + 2 * i, 201 + 2 * i) for i in range(uslots)]
+
     settle_steps = settle(ctx, step, args.settle_ms)
     for _ in range(args.warmup):
         step()
@@ -775,9 +898,9 @@ def main():
     if dist:
         import torch
 
-        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = torch.tensor([elapsed, elapsed_unsettled], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
+        elapsed, elapsed_unsettled = float(t[0]), float(t[1])
         tot = torch.tensor([float(n_own)], dtype=torch.float64)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         total_dof = float(tot[0])
@@ -809,11 +932,12 @@ def main():
         kmed = float(np.median(kernel_ms))
         rf = roofline(bsr, mesh, kmed)
         rf["kernel_ms_mean"] = round(float(np.mean(kernel_ms)), 4)
+        rf["kernel_ms_unsettled"] = round(float(np.median(kernel_ms_unsettled)), 4)
+        rf["frac_unsettled"] = round(rf["algorithmic_bytes_per_launch"] / (rf["kernel_ms_unsettled"] * 1e-3) / 1e9
+                                     / HBM_PEAK_GBS, 4)
         rf["traffic"] = None
         if world == 1:
-            rf["traffic"], tag = pmc_traffic(args.pmc_json, n)
-            if tag:
-                rf["traffic_profile"] = tag
+            with_traffic(rf, "c2" if args.scaling == "weak" else "c4", n, kmed)
         extras = {}
         c2 = None
         if world == 1:
@@ -826,18 +950,9 @@ def main():
             mesh.close()
             dbottom = None
         legs = set() if args.no_extras or world > 1 else set(args.legs.split(","))
-        if "c4" in legs and args.c4_n > 0 and not (args.scaling == "strong" and n == args.c4_n):
-            extras["c4"] = poisson_c4(ctx, af, args.c4_n, settle_ms=args.settle_ms)
-        if "c3" in legs:
-            extras["c3"] = elasticity_c3(ctx, af, args.c3_n)
-        if "c2_generic" in legs:
-            extras["c2_generic"] = c2_generic_leg(ctx, af, 215)
-        if "c2_arrays" in legs:
-            extras["c2_arrays"] = c2_arrays_leg(ctx, af, 215)
-        if "unstructured" in legs and args.unstructured_levels > 0:
-            extras["unstructured"] = unstructured_leg(ctx, af, "L-shape-3D.msh", args.unstructured_levels)
-        if "c5" in legs:
-            extras["c5"] = elastodynamics_c5(ctx, af, args.c5_n, args.c5_steps)
+        if args.scaling == "strong" and n == args.c4_n:
+            legs.discard("c4")
+        extras = run_legs(ctx, af, args, legs)
         cpu = None
         if c2 is not None:
             cpu = cpu_baseline(c2)
@@ -862,6 +977,8 @@ def main():
             "settle_ms": args.settle_ms,
             "settle_steps": settle_steps,
             "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step_unsettled": round(elapsed_unsettled * 1e3 / args.steps, 4),
+            "value_unsettled": round(total_dof * args.steps / elapsed_unsettled / 1e6, 3),
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,

@@ -244,6 +244,12 @@ typedef struct afem_bsr_stats {
                                       compiled-in signature, not folded into the general list) */
   int64_t general_slices;   /* scalar assembly: slices of the general instance's lists (with the
                                folded uniform ones: a box's edge runs and corners) */
+  int32_t cube_lattice;     /* the cell-first cube kernel's view of the mesh (NB_DOF 1 tets): 1 a
+                               generator box or z-slab; 2 a Kuhn lattice given as arrays in a natural
+                               (lexicographic, any axis order) numbering: the same kernel, no map;
+                               3 a Kuhn lattice in any other numbering (canonical maps); 0 none */
+  int32_t cube_axes;        /* cube_lattice 2: the numbering's axis order, fastest first, as
+                               a0 + 3 a1 + 9 a2 (x + Lx (y + Ly z): 0 + 3 + 18 = 21) */
 } afem_bsr_stats;
 #define AFEM_KERNEL_NONE 0
 #define AFEM_KERNEL_STRIP 1          /* scalar row-strip kernel (uniform + general instances) */

@@ -542,7 +542,7 @@ int orc_pcg_jacobi(int64_t n, const int64_t* row_ptr, const int32_t* cols, const
     double d = 0.0, off = 0.0;
     for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k)
       if (cols[k] == i)
-        d = vals[k];
+        d += vals[k]; /* duplicate (i,i) entries add up, as the SpMV applies them */
       else
         off += fabs(vals[k]);
     dinv[i] = d != 0.0 ? 1.0 / d : 0.0;
@@ -767,7 +767,7 @@ int orc_pcg_jacobi_omp(int64_t n, const int64_t* row_ptr, const int32_t* cols, c
     double d = 0.0, off = 0.0;
     for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k)
       if (cols[k] == i)
-        d = vals[k];
+        d += vals[k]; /* duplicate (i,i) entries add up, as the SpMV applies them */
       else
         off += fabs(vals[k]);
     dinv[i] = d != 0.0 ? 1.0 / d : 0.0;

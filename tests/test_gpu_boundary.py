@@ -425,6 +425,101 @@ def test_host_csr_view_apply_bcs_then_solve(ctx, method):
     assert np.all(x[rc] == 0.5)
 
 
+def test_duplicate_diagonal_entries_add_up(ctx):
+    """ADVICE r4 (linear_system.hip k_inv_diag): a view whose rows repeat the
+    (i, i) entry (a module that adds its diagonal in two pieces).  The operator
+    applies both (SpMV, csr_to_dense), the Jacobi preconditioner and the
+    constraint test use their sum, in libafem and in the oracle alike: a fixed
+    number of PCG iterations gives the same iterate on both."""
+    gm = read_gmsh(path("circle_cut.msh"))
+    n = gm.n_nodes
+    orp, ocols = O.sparsity(n, n, gm.cells)
+    ovals, orhs = O.assemble_poisson(n, gm.cells, gm.coords, orp, ocols, 5.5)
+    O.dirichlet_penalty(gm.group_nodes("horizontal"), 0.5, 1e30, orp, ocols, ovals, orhs)
+    # every third row: the diagonal split into 0.25 d (in place) + 0.75 d (appended)
+    split = np.arange(0, n, 3)
+    rows, cols, vals = [], [], []
+    for r in range(n):
+        c = list(ocols[orp[r]:orp[r + 1]])
+        v = list(ovals[orp[r]:orp[r + 1]])
+        if r in set(split.tolist()):
+            k = c.index(r)
+            d = v[k]
+            v[k] = 0.25 * d
+            c.append(r)
+            v.append(0.75 * d)
+        rows.append(len(cols))
+        cols += c
+        vals += v
+    rp = np.array(rows + [len(cols)], dtype=np.int64)
+    cols = np.array(cols, dtype=np.int32)
+    vals = np.array(vals)
+    assert np.allclose(O.csr_to_dense(rp, cols, vals), O.csr_to_dense(orp, ocols, ovals), rtol=1e-15, atol=0)
+    ls = af.DoFLinearSystem().initialize(ctx, n)
+    ls.setCSRValues(rp[:-1].astype(np.int32), np.diff(rp).astype(np.int32), cols, vals)
+    ls.set_rhs_host(orhs)
+    ls.setSolverOptions(fixed_iterations=25)
+    ls.solve()
+    xo, _, _, _ = O.pcg_jacobi(rp, cols, vals, orhs, max_iter=-25)
+    xs, _, _, _ = O.pcg_jacobi(orp, ocols, ovals, orhs, max_iter=-25)  # the unsplit system: same iterate
+    x = ls.solution_host()
+    assert np.abs(xo - xs).max() <= 1e-10 * np.abs(xs).max()
+    assert np.abs(x - xo).max() <= 1e-10 * np.abs(xo).max()
+
+
+def test_mapped_view_rejects_duplicate_and_missing_rows(ctx):
+    """ADVICE r4 (handover.hip k_lsmap_len): afem_ls_set_csr_values_mapped with
+    a device view in the caller's numbering.  A valid permuted index solves like
+    the oracle; an index mapping two caller rows to one linear-system row, or
+    leaving an owned row without a caller row, is refused (it used to write one
+    row's entries past its range, or leave an empty row)."""
+    from arcanefem_amd._capi import call
+
+    gm = read_gmsh(path("circle_cut.msh"))
+    n = gm.n_nodes
+    orp, ocols = O.sparsity(n, n, gm.cells)
+    ovals, orhs = O.assemble_poisson(n, gm.cells, gm.coords, orp, ocols, 5.5)
+    O.dirichlet_penalty(gm.group_nodes("horizontal"), 0.5, 1e30, orp, ocols, ovals, orhs)
+    rows = orp[:-1].astype(np.int32)
+    cols = ocols.astype(np.int32)
+    bufs = []
+
+    def dev(a):
+        p = ctx.malloc(max(a.nbytes, 8))
+        ctx.to_device(p, a)
+        bufs.append(p)
+        return p
+
+    drows, dcols, dvals = dev(rows), dev(cols), dev(ovals.copy())
+
+    def mapped(index):
+        ls = af.DoFLinearSystem().initialize(ctx, n)
+        idx = np.ascontiguousarray(index, dtype=np.int32)
+        call("afem_ls_set_csr_values_mapped", ls.impl, drows, None, dcols, dvals, n, cols.size,
+             idx.ctypes.data, idx.size)
+        return ls
+
+    perm = np.random.default_rng(5).permutation(n).astype(np.int32)  # caller dof d -> ls row perm[d]
+    ls = mapped(perm)
+    b = np.empty(n)
+    b[perm] = orhs
+    ls.set_rhs_host(b)
+    ls.setSolverOptions(method="direct")
+    st = ls.solve()
+    xo = np.linalg.solve(O.csr_to_dense(orp, ocols, ovals), orhs)
+    assert st["converged"] and np.abs(ls.solution_host()[perm] - xo).max() / np.abs(xo).max() <= SOL_TOL
+    dup = perm.copy()
+    dup[3] = dup[11]  # two caller rows -> one ls row, and ls row perm[3] gets none
+    with pytest.raises(af.AfemError, match="two rows"):
+        mapped(dup)
+    missing = perm.copy()
+    missing[7] = -1  # caller row 7 is not owned: its ls row stays empty
+    with pytest.raises(af.AfemError, match="no row"):
+        mapped(missing)
+    for p in bufs:
+        ctx.free(p)
+
+
 def test_boundary_argument_checks(ctx):
     # ADVICE r1 (capi.cpp:544): a subdomain CSR has ghost columns, the linear
     # system must span them

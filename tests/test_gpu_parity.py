@@ -153,17 +153,26 @@ def test_cube_kernel_matches_oracle(ctx, variant, n, nz, zs):
     assert np.abs(ls.rhs_host() - rhs).max() <= VAL_TOL * np.abs(rhs).max()
 
 
-@pytest.mark.parametrize("nranks,stride,carry", [(2, "64", "1"), (3, "64", "1"), (3, "49", "0"), (2, "64", "0")])
-def test_cube_kernel_on_slabs(ctx, variant, nranks, stride, carry):
+@pytest.mark.parametrize("nranks,stride,carry,nz,zs", [(2, "64", "1", 11, None), (3, "64", "1", 11, None),
+                                                     (3, "49", "0", 11, None), (2, "64", "0", 11, None),
+                                                     (2, "64", "1", 11, "1"), (3, "64", "1", 11, "2"),
+                                                     (4, "64", "1", 5, "2"), (3, "64", "1", 2, None),
+                                                     (5, "64", "1", 6, "1")])
+def test_cube_kernel_on_slabs(ctx, variant, nranks, stride, carry, nz, zs):
     """z-slab subdomains (owned layers, then the ghost layer below, then the one
     above: a row next to the ghost layer below has its -z columns LAST in id
     order): every slab's matrix and RHS against the oracle on the same
-    subdomain, through the cube kernel."""
+    subdomain, through the cube kernel.  z segments of 1 and 2 layers
+    (AFEM_CUBES_ZS) start inside a slab next to its ghost layers,
+    and nz = 2 on 3 ranks / 6 on 5 leave slabs of ONE owned node layer."""
     variant("AFEM_ASSEMBLY_CUBES", "1")  # opt-in
     variant("AFEM_CUBES_STRIDE", stride)  # accumulator planes of 64 (default) or 49 rows
     variant("AFEM_CUBES_CARRY", carry)  # top-face sums carried in registers (default) or not
+    variant("AFEM_CUBES_ZS", zs)
+    owned = []
     for rank in range(nranks):
-        mesh = af.Mesh.structured(ctx, 3, 9, nz=11, jitter=0.2, seed=13, nranks=nranks, rank=rank)
+        mesh = af.Mesh.structured(ctx, 3, 9, nz=nz, jitter=0.2, seed=13, nranks=nranks, rank=rank)
+        owned.append(mesh.n_own_nodes // 100)
         bsr, ls = _assemble_gpu(ctx, mesh, 2.5)
         assert bsr.stats()["last_kernel"] == 10
         rows, cols, vals = bsr.download()
@@ -174,6 +183,9 @@ def test_cube_kernel_on_slabs(ctx, variant, nranks, stride, carry):
         _check_values(vals, ovals)
         assert np.abs(ls.rhs_host() - orhs).max() <= VAL_TOL * np.abs(orhs).max()
         mesh.close()
+    assert sum(owned) == nz + 1
+    if nz in (2, 6):
+        assert min(owned) == 1
 
 
 def test_uniform_strip_variant(ctx, variant):
@@ -700,6 +712,101 @@ def test_cube_kernel_on_random_numbering(ctx, n, nz, seed):
         assert np.array_equal(b2.download()[2], v1)
     else:
         _check_values(b2.download()[2], v1)
+
+
+AXIS_ORDERS = [(0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1), (2, 1, 0)]
+
+
+def natural_numbering(n, nz, order):
+    """New id of every generator node (id = x + (n+1)(y + (n+1) z)) when the
+    box is numbered lexicographically with the axes in `order`, fastest first
+    (Arcane's cartesian generator: x fastest = (0, 1, 2))."""
+    L = np.array([n + 1, n + 1, nz + 1], dtype=np.int64)
+    ids = np.arange(L.prod(), dtype=np.int64)
+    lat = np.stack([ids % L[0], (ids // L[0]) % L[1], ids // (L[0] * L[1])])
+    a, b, c = order
+    return lat[a] + L[a] * (lat[b] + L[b] * lat[c])
+
+
+@pytest.mark.parametrize("order", AXIS_ORDERS)
+@pytest.mark.parametrize("n,nz,seed", [(9, 15, 4), (13, 6, 5)])
+def test_cube_kernel_on_natural_numbering(ctx, variant, n, nz, seed, order):
+    """a lattice of Kuhn cubes handed over as arrays in a
+    NATURAL numbering (lexicographic in any axis order, cells in a random
+    order, vertices in any order) runs the headline cube kernel with no map
+    (cube_lattice 2).  The caller's structure and the oracle's on the same
+    arrays are equal, the values and RHS within 1e-12; for x-fastest order the
+    matrix is bitwise the generator box's; AFEM_CUBE_NATURAL=0 (the strip
+    kernels) agrees to rounding."""
+    m0 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=seed)
+    b0, l0 = _assemble_gpu(ctx, m0, 5.5)
+    cells0, coords0, _ = m0.download()
+    rng = np.random.default_rng(seed)
+    p = natural_numbering(n, nz, order)
+    cells = p[cells0].astype(np.int32)[rng.permutation(cells0.shape[0])]
+    cells = np.ascontiguousarray(np.take_along_axis(cells, rng.permuted(np.tile(np.arange(4), (cells.shape[0], 1)),
+                                                                        axis=1), axis=1))
+    coords = np.empty_like(coords0)
+    coords[p] = coords0
+    m1 = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    b1, l1 = _assemble_gpu(ctx, m1, 5.5)
+    st = b1.stats()
+    assert st["cube_lattice"] == 2 and st["last_kernel"] == 10, st
+    assert st["cube_axes"] == order[0] + 3 * order[1] + 9 * order[2]
+    rows, cols, vals = b1.download()
+    rhs = l1.rhs_host()
+    orp, ocols = O.sparsity(m1.n_nodes, m1.n_own_nodes, cells)
+    ovals, orhs = O.assemble_poisson(m1.n_own_nodes, cells, coords, orp, ocols, 5.5)
+    assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+    _check_values(vals, ovals)
+    assert np.abs(rhs - orhs).max() <= VAL_TOL * np.abs(orhs).max()
+    if order == (0, 1, 2):
+        assert np.array_equal(vals, b0.download()[2]) and np.array_equal(rhs, l0.rhs_host())
+    variant("AFEM_CUBE_NATURAL", "0")
+    m2 = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    b2, l2 = _assemble_gpu(ctx, m2, 5.5)
+    assert b2.stats()["cube_lattice"] != 2
+    _check_values(b2.download()[2], vals)
+    assert np.abs(l2.rhs_host() - rhs).max() <= VAL_TOL * np.abs(rhs).max()
+
+
+def test_natural_numbering_rejects_non_kuhn_lattices(ctx):
+    """A lattice whose cubes are not cut into the 6 Kuhn tets (here: one cube's
+    tets replaced by the other diagonal's) or whose numbering is not
+    lexicographic stays off the natural path, with the oracle's matrix."""
+    n = 6
+    m0 = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=2)
+    cells0, coords0, _ = m0.download()
+    # a node swap breaks the lexicographic numbering
+    p = np.arange(coords0.shape[0])
+    p[[5, 40]] = p[[40, 5]]
+    cells = p[cells0].astype(np.int32)
+    coords = np.empty_like(coords0)
+    coords[p] = coords0
+    for cc in (cells, None):
+        if cc is None:
+            # cube 0's six tets re-cut along the diagonal (1,0,0)-(0,1,1)
+            L = n + 1
+            v = lambda x, y, z: x + L * (y + L * z)  # noqa: E731
+            cc = cells0.copy()
+            # the monotone paths from (1,0,0) to (0,1,1) (x reflected)
+            six = [[v(1, 0, 0), v(0, 0, 0), v(0, 1, 0), v(0, 1, 1)], [v(1, 0, 0), v(0, 0, 0), v(0, 0, 1), v(0, 1, 1)],
+                   [v(1, 0, 0), v(1, 1, 0), v(0, 1, 0), v(0, 1, 1)], [v(1, 0, 0), v(1, 1, 0), v(1, 1, 1), v(0, 1, 1)],
+                   [v(1, 0, 0), v(1, 0, 1), v(0, 0, 1), v(0, 1, 1)], [v(1, 0, 0), v(1, 0, 1), v(1, 1, 1), v(0, 1, 1)]]
+            cube0 = np.where(np.all(np.isin(cc, [v(x, y, z) for x in (0, 1) for y in (0, 1) for z in (0, 1)]), axis=1))[0]
+            assert cube0.size == 6
+            cc[cube0] = np.array(six, dtype=np.int32)
+            crd = coords0
+        else:
+            crd = coords
+        m1 = af.Mesh.from_arrays(ctx, 3, cc, crd)
+        b1, l1 = _assemble_gpu(ctx, m1, 5.5)
+        assert b1.stats()["cube_lattice"] != 2
+        rows, cols, vals = b1.download()
+        orp, ocols = O.sparsity(m1.n_nodes, m1.n_own_nodes, cc)
+        ovals, orhs = O.assemble_poisson(m1.n_own_nodes, cc, crd, orp, ocols, 5.5)
+        assert np.array_equal(rows, orp) and np.array_equal(cols, ocols)
+        _check_values(vals, ovals)
 
 
 @pytest.mark.parametrize("knob,value", [("AFEM_BANK_PLACE_GENERAL", "1"), ("AFEM_ASSEMBLY_LOCAL", "1")])
