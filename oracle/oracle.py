@@ -292,7 +292,7 @@ def csr_to_dense(row_ptr, cols, vals, n_cols=None):
     A = np.zeros((n, m))
     for r in range(n):
         s, e = row_ptr[r], row_ptr[r + 1]
-        A[r, cols[s:e]] += vals[s:e]
+        np.add.at(A[r], cols[s:e], vals[s:e])  # duplicate (r, c) entries add up
     return A
 
 
