@@ -79,6 +79,7 @@ struct CubeGeom {
   int tx, ty, zs, ns;
   double s_coef;     // coef / 6
   double f_meas;     // f / 24
+  int full_flush;    // flush_full for layers whose rows are all complete (AFEM_CUBES_FULL=0: not)
 };
 
 // is global node layer k one of the slab's local layers (owned or ghost)?
@@ -264,6 +265,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   // their latency hides behind the cube arithmetic instead of stalling here.
   const int rx = lane % kRun, ry = lane / kRun;
   const int nx = cx0 + rx, ny = cy0 + ry;
+  const bool full_flush_on = g.full_flush != 0;
   int64_t pf_rb = 0, pf_re = 0, pf_r = 0;
   uint64_t pf_slot = 0;
   double pf_rhs = 0.0;
@@ -282,7 +284,74 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       if constexpr (RHS_ADD) pf_rhs = rhs[pf_r];
     }
   };
+  // a node layer whose 49 rows all have their 15 neighbours, in the sorted
+  // order of the offsets (the unit away from the x / y faces of the box, z
+  // off its bottom and top layers, the local layers in id order: not next to
+  // a slab's ghost layer below): the row's values go to the image at 15 L + o,
+  // and each x-run is 105 consecutive image values -- no masks, no
+  // compaction, constant LDS offsets (flush_full)
+  const bool xy_full = cx0 >= 1 && cx0 + kRun <= g.npx - 1 && cy0 >= 1 && cy0 + kRun <= g.npy - 1;
+  auto layer_full = [&](int z) {
+    return xy_full && z >= 1 && z + 1 <= g.nzc && local_layer(g, z - 1) < local_layer(g, z) &&
+           local_layer(g, z) < local_layer(g, z + 1);
+  };
+  auto flush_full = [&](int z) {
+    const int b = z & 1;
+    const int lr = min(lane, STRIDE - 1);  // lanes past the 49 rows read a row they do not use
+    double v[15];
+    double sum = 0.0;
+#pragma unroll
+    for (int o = 0; o < 15; ++o) {
+      v[o] = acc[b][o][lr];
+      if (o != 7) sum += v[o];
+    }
+    const double meas = v[7];
+    v[7] = -sum;
+    if constexpr (HAS_RHS) {  // lanes without a row repeat lane 0's store
+      const bool valid = lane < kRows;
+      const double rv = RHS_ADD ? pf_rhs + g.f_meas * meas : g.f_meas * meas;
+      const int64_t r0 = lane_i64(pf_r, 0);
+      const double rv0 = lane_f64(rv, 0);
+      rhs[valid ? pf_r : r0] = valid ? rv : rv0;
+    }
+    const int64_t rb = pf_rb;
+    wave_lds_order();  // every lane's accumulator reads before the image overwrites them
+    double* img = &acc[b][0][0];
+    // row L at [15 L, 15 L + 15): lanes past the 49 rows write into
+    // [735, 960) of the buffer, which no store reads
+#pragma unroll
+    for (int o = 0; o < 15; ++o) img[15 * lane + o] = v[o];
+    wave_lds_order();
+    // x-run q = rows 7q .. 7q + 6: 105 values contiguous in vals from row 7q's
+    // first one; the second store's lanes past 105 repeat value 104 (same
+    // address, same value)
+    const int t1 = min(lane + 64, 15 * kRun - 1);
+#pragma unroll
+    for (int q = 0; q < kRun; ++q) {
+      const int64_t dst = lane_i64(rb, kRun * q);
+      vals[dst + lane] = img[15 * kRun * q + lane];
+      vals[dst + t1] = img[15 * kRun * q + t1];
+    }
+    wave_lds_order();
+    if constexpr ((kAcc * STRIDE) % 2 == 0) {
+      double2* const img2 = reinterpret_cast<double2*>(img);
+#pragma unroll
+      for (int i = 0; i < (kAcc * STRIDE / 2 + 63) / 64; ++i)
+        img2[min(64 * i + lane, kAcc * STRIDE / 2 - 1)] = make_double2(0.0, 0.0);
+    }
+    else {
+#pragma unroll
+      for (int i = 0; i < (kAcc * STRIDE + 63) / 64; ++i) img[min(64 * i + lane, kAcc * STRIDE - 1)] = 0.0;
+    }
+    wave_lds_order();
+  };
   auto flush = [&](int z) {
+    if constexpr (!CANON && STRIDE == 64) {
+      if (full_flush_on && layer_full(z)) {
+        flush_full(z);
+        return;
+      }
+    }
     const int b = z & 1;
     const bool valid = lane < kRows && nx < g.npx && ny < g.npy;
     // present neighbours and the order of their local ids: the dz groups by local layer index
@@ -687,6 +756,8 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   g.ns = (g.n_own_layers + g.zs - 1) / g.zs;
   g.s_coef = coef / 6.0;
   g.f_meas = f / 24.0;
+  const char* fe = variant("AFEM_CUBES_FULL");
+  g.full_flush = (fe && atoi(fe) == 0) ? 0 : 1;
   const int64_t n_units = (int64_t)g.tx * g.ty * g.ns;
   AFEM_REQUIRE(n_units < (int64_t(1) << 31), AFEM_ERR_LIMIT, "cube kernel: too many units");
   // accumulator planes of 64 rows (19.3 KB of LDS, 8 waves per CU), or of 49
