@@ -180,7 +180,10 @@ struct CubeCanon {
   const uint64_t* slot;
 };
 
-template <int STRIDE, bool CARRY, bool XEX, bool YEX, bool CANON, bool HAS_RHS, bool RHS_ADD>
+// DIAG (diagnostic ablations, AFEM_CUBES_DIAG; values wrong): 1 no value
+// stores in the complete-layer flush, 2 one LDS add per cube (the sum of its
+// sums) instead of its 15, 4 no cube arithmetic, 8 no complete-layer flush
+template <int STRIDE, bool CARRY, bool XEX, bool YEX, bool CANON, bool HAS_RHS, bool RHS_ADD, int DIAG = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_assemble_cubes(
     CubeGeom g, const int64_t* __restrict__ rows, const double* __restrict__ coords, double* __restrict__ vals,
     double* __restrict__ rhs, CubeCanon cc)
@@ -329,8 +332,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 #pragma unroll
     for (int q = 0; q < kRun; ++q) {
       const int64_t dst = lane_i64(rb, kRun * q);
-      vals[dst + lane] = img[15 * kRun * q + lane];
-      vals[dst + t1] = img[15 * kRun * q + t1];
+      if constexpr (!(DIAG & 1)) {
+        vals[dst + lane] = img[15 * kRun * q + lane];
+        vals[dst + t1] = img[15 * kRun * q + t1];
+      }
     }
     wave_lds_order();
     if constexpr ((kAcc * STRIDE) % 2 == 0) {
@@ -348,7 +353,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   auto flush = [&](int z) {
     if constexpr (!CANON && STRIDE == 64) {
       if (full_flush_on && layer_full(z)) {
-        flush_full(z);
+        if constexpr (!(DIAG & 8)) flush_full(z);
         return;
       }
     }
@@ -562,7 +567,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       for (int b = 0; b < 8; ++b) ev[a][b] = 0.0;
     }
 #pragma unroll
-    for (int t = 0; t < 6; ++t) {
+    for (int t = 0; t < ((DIAG & 4) ? 0 : 6); ++t) {
       const int v1 = tet_v(t, 1), v2 = tet_v(t, 2);
       const P3 e1 = psub(X[v1], X[0]), e2 = psub(X[v2], X[0]), e3 = psub(X[7], X[0]);
       P3 k[4];
@@ -640,6 +645,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     int bb_, bt_;
     corner_frame(zc, inm, bb_, bt_);
     auto kept = [&](int c, double x) { return ((inm >> c) & 1u) ? x : 0.0; };
+    double dsum = 0.0;  // DIAG 2
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
@@ -647,13 +653,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
         if (is_edge(a, b) && !(CARRY && cbit(a, 2) && cbit(b, 2)) &&
             !(XEX && !cbit(a, 0) && !cbit(b, 0) && !(cbit(a, 2) && cbit(b, 2))) &&
             !(YEX && !cbit(a, 1) && !cbit(b, 1) && !(cbit(a, 2) && cbit(b, 2)))) {
-          atomicAdd(base_at(inm, bb_, bt_, a) + STRIDE * edge_o(a, b), kept(a, ev[a][b]));
-          atomicAdd(base_at(inm, bb_, bt_, b) + STRIDE * edge_o(b, a), kept(b, ev[a][b]));
+          if constexpr (DIAG & 2) {
+            dsum += ev[a][b];
+          }
+          else {
+            atomicAdd(base_at(inm, bb_, bt_, a) + STRIDE * edge_o(a, b), kept(a, ev[a][b]));
+            atomicAdd(base_at(inm, bb_, bt_, b) + STRIDE * edge_o(b, a), kept(b, ev[a][b]));
+          }
         }
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      if (!(CARRY && cbit(c, 2)) && !(XEX && !cbit(c, 0) && !cbit(c, 2)) && !(YEX && !cbit(c, 1) && !cbit(c, 2)))
-        atomicAdd(base_at(inm, bb_, bt_, c) + STRIDE * 7, kept(c, mv[c]));  // |det| sums
+      if (!(CARRY && cbit(c, 2)) && !(XEX && !cbit(c, 0) && !cbit(c, 2)) && !(YEX && !cbit(c, 1) && !cbit(c, 2))) {
+        if constexpr (DIAG & 2)
+          dsum += mv[c];
+        else
+          atomicAdd(base_at(inm, bb_, bt_, c) + STRIDE * 7, kept(c, mv[c]));  // |det| sums
+      }
+    if constexpr ((DIAG & 2) != 0) atomicAdd(&acc[bb_][0][rs], dsum);
   };
 
   // ---- walk the cube layers upwards (coordinates staged one layer ahead)
@@ -777,11 +793,23 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
 #define AFEM_CUBES_K(S, C, X, Y, N)                                                                                  \
   (rhs ? (rhs_add ? &k_assemble_cubes<S, C, X, Y, N, true, true> : &k_assemble_cubes<S, C, X, Y, N, true, false>)    \
        : &k_assemble_cubes<S, C, X, Y, N, false, false>)
+  const char* de = variant("AFEM_CUBES_DIAG");
+  const int diag = de ? atoi(de) : 0;
   auto* kern = canon ? AFEM_CUBES_K(64, true, true, true, true)
                : carry ? (xex ? (yex ? AFEM_CUBES_K(64, true, true, true, false) : AFEM_CUBES_K(64, true, true, false, false))
                               : AFEM_CUBES_K(64, true, false, false, false))
                        : (s49 ? AFEM_CUBES_K(49, false, false, false, false) : AFEM_CUBES_K(64, false, false, false, false));
 #undef AFEM_CUBES_K
+  if (diag && !canon && carry && xex && yex && rhs && !rhs_add) {
+    switch (diag) {
+#define AFEM_CUBES_D(D) \
+  case D: kern = &k_assemble_cubes<64, true, true, true, false, true, false, D>; break;
+      AFEM_CUBES_D(1) AFEM_CUBES_D(2) AFEM_CUBES_D(4) AFEM_CUBES_D(8) AFEM_CUBES_D(3) AFEM_CUBES_D(9)
+      AFEM_CUBES_D(6) AFEM_CUBES_D(12) AFEM_CUBES_D(14)
+#undef AFEM_CUBES_D
+      default: break;
+    }
+  }
   const CubeCanon cc{ canon ? S.cube_phys.p : nullptr, canon ? S.cube_rb.p : nullptr, canon ? S.cube_slot.p : nullptr };
   hipLaunchKernelGGL(kern, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, S.row_ptr.p, m.coords.p, b.values.p,
                      rhs, cc);
