@@ -182,7 +182,10 @@ struct CubeCanon {
 
 // DIAG (diagnostic ablations, AFEM_CUBES_DIAG; values wrong): 1 no value
 // stores in the complete-layer flush, 2 one LDS add per cube (the sum of its
-// sums) instead of its 15, 4 no cube arithmetic, 8 no complete-layer flush
+// sums) instead of its 15, 4 no cube arithmetic, 8 no complete-layer flush;
+// variants (values right): 16 the next layer's coordinates loaded before the
+// cubes, 32 non-temporal value stores in the complete-layer flush, 64 one
+// 16-B store per lane and x-run in the complete-layer flush
 template <int STRIDE, bool CARRY, bool XEX, bool YEX, bool CANON, bool HAS_RHS, bool RHS_ADD, int DIAG = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_assemble_cubes(
     CubeGeom g, const int64_t* __restrict__ rows, const double* __restrict__ coords, double* __restrict__ vals,
@@ -329,10 +332,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     // first one; the second store's lanes past 105 repeat value 104 (same
     // address, same value)
     const int t1 = min(lane + 64, 15 * kRun - 1);
+    // DIAG 64: one 16-B store per lane and run (values 2l, 2l + 1; lane 52
+    // stores 103, 104 -- value 103 twice with the same data -- and the lanes
+    // past it repeat lane 52's): 7 stores per layer instead of 14
+    const int t2 = min(2 * lane, 15 * kRun - 2);
 #pragma unroll
     for (int q = 0; q < kRun; ++q) {
       const int64_t dst = lane_i64(rb, kRun * q);
-      if constexpr (!(DIAG & 1)) {
+      if constexpr ((DIAG & 64) != 0) {
+        const double a0 = img[15 * kRun * q + t2], a1 = img[15 * kRun * q + t2 + 1];
+        typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
+        *reinterpret_cast<d2u*>(&vals[dst + t2]) = d2u{ a0, a1 };
+      }
+      else if constexpr ((DIAG & 32) != 0) {
+        __builtin_nontemporal_store(img[15 * kRun * q + lane], &vals[dst + lane]);
+        __builtin_nontemporal_store(img[15 * kRun * q + t1], &vals[dst + t1]);
+      }
+      else if constexpr (!(DIAG & 1)) {
         vals[dst + lane] = img[15 * kRun * q + lane];
         vals[dst + t1] = img[15 * kRun * q + t1];
       }
@@ -705,9 +721,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     // of layer zc + 2: the flush waits for the offsets only (counted vmcnt)
     prefetch_ids(zc + 2);  // CANON: the next staged layer's caller ids, in flight during the cubes
     prefetch_rows(zc);
+    if constexpr ((DIAG & 16) != 0) load_layer(zc + 2);  // before the cubes: their latency hides behind them
     wave_lds_order();
     cubes(zc);
-    load_layer(zc + 2);  // after the cubes: its 12 registers are not live across them
+    if constexpr ((DIAG & 16) == 0) load_layer(zc + 2);  // after the cubes: its 12 registers are not live across them
     wave_lds_order();
     flush(zc);
     store_layer(zc & 1);
@@ -805,7 +822,8 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
 #define AFEM_CUBES_D(D) \
   case D: kern = &k_assemble_cubes<64, true, true, true, false, true, false, D>; break;
       AFEM_CUBES_D(1) AFEM_CUBES_D(2) AFEM_CUBES_D(4) AFEM_CUBES_D(8) AFEM_CUBES_D(3) AFEM_CUBES_D(9)
-      AFEM_CUBES_D(6) AFEM_CUBES_D(12) AFEM_CUBES_D(14)
+      AFEM_CUBES_D(6) AFEM_CUBES_D(12) AFEM_CUBES_D(14) AFEM_CUBES_D(16) AFEM_CUBES_D(32) AFEM_CUBES_D(48)
+      AFEM_CUBES_D(17) AFEM_CUBES_D(64) AFEM_CUBES_D(80)
 #undef AFEM_CUBES_D
       default: break;
     }
