@@ -456,7 +456,7 @@ class DoFLinearSystem:
     SOLVERS = {"auto": C.AFEM_SOLVER_AUTO, "pcg": C.AFEM_SOLVER_PCG, "direct": C.AFEM_SOLVER_DIRECT}
 
     def setSolverOptions(self, rtol=None, atol=None, max_iter=None, check_every=None, fixed_iterations=None,
-                         method=None, initial_guess=None, preconditioner=None):
+                         method=None, initial_guess=None, preconditioner=None, profile_comm=None):
         """initial_guess: "zero" (default) or "current" (start the PCG from the
         solution vector's values); preconditioner: "jacobi" (default),
         "block3" (3x3 node-block Jacobi, NB_DOF = 3 systems), "multigrid"
@@ -477,6 +477,8 @@ class DoFLinearSystem:
             o.check_every = check_every
         if fixed_iterations is not None:
             o.fixed_iterations = fixed_iterations
+        if profile_comm is not None:
+            o.profile_comm = 1 if profile_comm else 0
         if initial_guess is not None:
             o.initial_guess = {"zero": 0, "current": 1}[initial_guess]
         if preconditioner is not None:
@@ -489,7 +491,9 @@ class DoFLinearSystem:
         st = C.SolveStats()
         call("afem_ls_solve", self.impl, ctypes.byref(st))
         return dict(iterations=st.iterations, converged=bool(st.converged), rel_residual=st.rel_residual,
-                    residual_norm=st.residual_norm, solve_ms=st.solve_ms, spmv_kernel=st.spmv_kernel)
+                    residual_norm=st.residual_norm, solve_ms=st.solve_ms, spmv_kernel=st.spmv_kernel,
+                    halo_wait_ms=st.halo_wait_ms, allreduce_ms=st.allreduce_ms, halo_bytes=st.halo_bytes,
+                    n_halo=st.n_halo, n_allreduce=st.n_allreduce)
 
     def spmv(self, x_dptr: int, y_dptr: int):
         call("afem_ls_spmv", self.impl, ctypes.c_void_p(x_dptr), ctypes.c_void_p(y_dptr))

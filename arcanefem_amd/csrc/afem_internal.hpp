@@ -383,6 +383,7 @@ struct MgDeleter {
 };
 struct LinearSystem {
   Ctx* ctx = nullptr;
+  std::vector<hipEvent_t> prof_ev;  // afem_solver_opts.profile_comm: event pool of the PCG loop's timings
   int64_t n_rows = 0, n_cols = 0;
   afem_solver_opts opts{};
   DevBuf<double> rhs, sol;

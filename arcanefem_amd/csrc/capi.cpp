@@ -1374,6 +1374,7 @@ int afem_ls_destroy(afem_ls* ls)
     ls->ctx->set_device();
     ls->ctx->sync();
     if (ls->pinned) (void)hipHostFree(ls->pinned);
+    for (hipEvent_t e : ls->prof_ev) (void)hipEventDestroy(e);
     delete ls;
   }
   API_END

@@ -342,7 +342,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       if constexpr ((DIAG & 64) != 0) {
         const double a0 = img[15 * kRun * q + t2], a1 = img[15 * kRun * q + t2 + 1];
         typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
-        *reinterpret_cast<d2u*>(&vals[dst + t2]) = d2u{ a0, a1 };
+        if constexpr ((DIAG & 32) != 0)
+          __builtin_nontemporal_store(d2u{ a0, a1 }, reinterpret_cast<d2u*>(&vals[dst + t2]));
+        else
+          *reinterpret_cast<d2u*>(&vals[dst + t2]) = d2u{ a0, a1 };
       }
       else if constexpr ((DIAG & 32) != 0) {
         __builtin_nontemporal_store(img[15 * kRun * q + lane], &vals[dst + lane]);
@@ -823,7 +826,7 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   case D: kern = &k_assemble_cubes<64, true, true, true, false, true, false, D>; break;
       AFEM_CUBES_D(1) AFEM_CUBES_D(2) AFEM_CUBES_D(4) AFEM_CUBES_D(8) AFEM_CUBES_D(3) AFEM_CUBES_D(9)
       AFEM_CUBES_D(6) AFEM_CUBES_D(12) AFEM_CUBES_D(14) AFEM_CUBES_D(16) AFEM_CUBES_D(32) AFEM_CUBES_D(48)
-      AFEM_CUBES_D(17) AFEM_CUBES_D(64) AFEM_CUBES_D(80)
+      AFEM_CUBES_D(17) AFEM_CUBES_D(64) AFEM_CUBES_D(80) AFEM_CUBES_D(96) AFEM_CUBES_D(112)
 #undef AFEM_CUBES_D
       default: break;
     }

@@ -1888,6 +1888,28 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     }
     n_int = ls.blist_nint;
   }
+  // afem_solver_opts.profile_comm: event pairs around each halo wait and
+  // all-reduce of the loop on the context stream, summed after the loop
+  const bool prof = ls.opts.profile_comm != 0 && comm != nullptr;
+  size_t prof_used = 0;
+  std::vector<std::pair<size_t, size_t>> prof_halo, prof_ar;
+  auto prof_event = [&]() -> size_t {
+    if (prof_used == ls.prof_ev.size()) {
+      hipEvent_t e;
+      AFEM_HIP(hipEventCreate(&e));
+      ls.prof_ev.push_back(e);
+    }
+    AFEM_HIP(hipEventRecord(ls.prof_ev[prof_used], ctx.stream));
+    return prof_used++;
+  };
+  int n_halo_loop = 0, n_ar_loop = 0;
+  auto loop_allreduce = [&](double* d) {
+    if (!comm) return;
+    const size_t a = prof ? prof_event() : 0;
+    comm_allreduce(comm, ctx, d, 1);
+    if (prof) prof_ar.emplace_back(a, prof_event());
+    ++n_ar_loop;
+  };
   // the part of an iteration after the SpMV (with_spmv: the whole iteration,
   // for the captured graph of the single-rank, non-split path)
   // AFEM_CG_VEC2=0: one row per thread and access in the vector kernels (variant)
@@ -1897,7 +1919,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     if (with_spmv)
       launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p, ls.csr_nnz);
     reduce_to(ctx, ls.partial.p, pl.nblocks, scal + 2);
-    if (comm) comm_allreduce(comm, ctx, scal + 2, 1);
+    loop_allreduce(scal + 2);
     if (use_mg) {
       hipLaunchKernelGGL(k_cg_xr, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p, ls.r.p,
                          ls.q.p);
@@ -1914,7 +1936,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
                          n, scal, par, ls.r.p, ls.q.p, ls.z.p, ls.dinv.p, ls.partial.p);
     AFEM_LAUNCHED();
     reduce_to(ctx, ls.partial.p, blk3 ? vb3 : vb, scal + (par ^ 1));
-    if (comm) comm_allreduce(comm, ctx, scal + (par ^ 1), 1);
+    loop_allreduce(scal + (par ^ 1));
     if (use_mg || blk3)
       hipLaunchKernelGGL(k_cg_dir, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.z.p, ls.p.p);
     else
@@ -1966,7 +1988,10 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
       };
       halo_begin(*ls.halo, ctx, ls.p.p);
       part(n_int, 0);
+      const size_t ha = prof ? prof_event() : 0;
       halo_end(*ls.halo, ctx, ls.p.p);
+      if (prof) prof_halo.emplace_back(ha, prof_event());
+      ++n_halo_loop;
       part(n_bd, n_int);
     }
     else if (graph && (it & 1) == 0 && it + gbatch <= max_it) {
@@ -1986,7 +2011,12 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
       goto checked;
     }
     else {
-      if (ls.halo) halo_exchange(*ls.halo, ctx, ls.p.p);
+      if (ls.halo) {
+        const size_t ha = prof ? prof_event() : 0;
+        halo_exchange(*ls.halo, ctx, ls.p.p);
+        if (prof) prof_halo.emplace_back(ha, prof_event());
+        ++n_halo_loop;
+      }
       launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p, ls.csr_nnz);
     }
     rest_of_iteration(par, false);
@@ -2022,6 +2052,20 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   rel = rz0 > 0 ? std::sqrt(std::fabs(ls.pinned[it & 1] / rz0)) : 0.0;
   if (ls.halo) halo_exchange(*ls.halo, ctx, ls.sol.p);  // m_u.synchronize()
   if (st) {
+    auto sum_ms = [&](const std::vector<std::pair<size_t, size_t>>& v) {
+      double t = 0.0;
+      for (const auto& e : v) {
+        float m = 0.f;
+        AFEM_HIP(hipEventElapsedTime(&m, ls.prof_ev[e.first], ls.prof_ev[e.second]));
+        t += m;
+      }
+      return t;
+    };
+    st->halo_wait_ms = prof ? sum_ms(prof_halo) : 0.0;
+    st->allreduce_ms = prof ? sum_ms(prof_ar) : 0.0;
+    st->halo_bytes = ls.halo ? 8 * ls.halo->n_send : 0;
+    st->n_halo = n_halo_loop;
+    st->n_allreduce = n_ar_loop;
     st->iterations = it;
     st->converged = fixed ? (rel <= o.rtol) : converged;
     st->rel_residual = rel;

@@ -391,6 +391,9 @@ typedef struct afem_solver_opts {
                                rebuilt at every solve; 2: built at the first solve
                                and reused while the matrix structure stays the same (time stepping with a
                                constant operator).  Other systems fall back to point Jacobi. */
+  int32_t profile_comm;     /* 1: time every halo wait and all-reduce of the PCG loop with HIP events on the
+                               context stream (afem_solve_stats.halo_wait_ms / allreduce_ms; diagnostic, adds
+                               event records to each iteration); 0: off (default) */
 } afem_solver_opts;
 
 typedef struct afem_solve_stats {
@@ -400,6 +403,16 @@ typedef struct afem_solve_stats {
   double residual_norm; /* ||b - A x||_2 over all ranks (recurrence residual) */
   double solve_ms;      /* device time of the solve */
   int32_t spmv_kernel;  /* AFEM_SPMV_*: the SpMV the iteration ran */
+  /* several ranks (halo attached): the communication of the PCG loop.  With
+   * afem_solver_opts.profile_comm the device time the context stream spent
+   * waiting for the halo of the search direction after its interior rows (the
+   * overlapped split) or in the whole exchange (no split), and in the scalar
+   * all-reduces, summed over the iterations; 0 otherwise */
+  double halo_wait_ms;
+  double allreduce_ms;
+  int64_t halo_bytes;   /* bytes this rank sends per halo exchange (8 per shared owned DoF and neighbour) */
+  int32_t n_halo;       /* halo exchanges of the loop */
+  int32_t n_allreduce;  /* scalar all-reduces of the loop */
 } afem_solve_stats;
 #define AFEM_SPMV_STREAM 0   /* CSR-stream (columns read from the CSR) */
 #define AFEM_SPMV_PATTERN 1  /* CSR-stream, interior-stencil rows form their columns */
