@@ -164,6 +164,16 @@ __device__ __forceinline__ void wave_lds_order()
 #endif
 }
 
+// a value store, non-temporal when NT (cubes: V bits 32 / 128)
+template <bool NT>
+__device__ __forceinline__ void put(double* p, double v)
+{
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
 // HAS_RHS / RHS_ADD at compile time: the flush's global stores are then a
 // fixed, branch-free sequence, so the waits for the next layer's coordinates
 // count past them (vmcnt(N)) instead of draining them (vmcnt(0))
@@ -180,13 +190,20 @@ struct CubeCanon {
   const uint64_t* slot;
 };
 
-// DIAG (diagnostic ablations, AFEM_CUBES_DIAG; values wrong): 1 no value
-// stores in the complete-layer flush, 2 one LDS add per cube (the sum of its
-// sums) instead of its 15, 4 no cube arithmetic, 8 no complete-layer flush;
-// variants (values right): 16 the next layer's coordinates loaded before the
-// cubes, 32 non-temporal value stores in the complete-layer flush, 64 one
-// 16-B store per lane and x-run in the complete-layer flush
-template <int STRIDE, bool CARRY, bool XEX, bool YEX, bool CANON, bool HAS_RHS, bool RHS_ADD, int DIAG = 0>
+// V: variant bits (AFEM_CUBES_V; the default kCubesV is what every result
+// uses).  Values right: 16 the next layer's coordinates loaded before the
+// cubes (their latency hides behind them), 32 non-temporal value stores in
+// the complete-layer flush (the values are not re-read by this launch; the
+// L2 keeps the coordinates the neighbouring units re-read), 64 one 16-B
+// store per lane and x-run there (7 stores per layer instead of 14), 128
+// non-temporal value and RHS stores in the other flushes.  Diagnostic
+// ablations (values wrong): 1 no value stores in the complete-layer flush, 2
+// one LDS add per cube (the sum of its sums) instead of its 15, 4 no cube
+// arithmetic, 8 no complete-layer flush.  Measured (r05d/e, C2 / C4, one
+// process, settled): 0.520 / 4.53 ms with none, 0.465 / 4.20 with 16 | 32 | 64.
+constexpr int kCubesV = 16 | 32 | 64 | 128;
+
+template <int STRIDE, bool CARRY, bool XEX, bool YEX, bool CANON, bool HAS_RHS, bool RHS_ADD, int DIAG = kCubesV>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_assemble_cubes(
     CubeGeom g, const int64_t* __restrict__ rows, const double* __restrict__ coords, double* __restrict__ vals,
     double* __restrict__ rhs, CubeCanon cc)
@@ -318,7 +335,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       const double rv = RHS_ADD ? pf_rhs + g.f_meas * meas : g.f_meas * meas;
       const int64_t r0 = lane_i64(pf_r, 0);
       const double rv0 = lane_f64(rv, 0);
-      rhs[valid ? pf_r : r0] = valid ? rv : rv0;
+      put<(DIAG & 128) != 0>(&rhs[valid ? pf_r : r0], valid ? rv : rv0);
     }
     const int64_t rb = pf_rb;
     wave_lds_order();  // every lane's accumulator reads before the image overwrites them
@@ -415,7 +432,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       const double rv = RHS_ADD ? pf_rhs + g.f_meas * meas : g.f_meas * meas;
       const int64_t r0 = lane_i64(pf_r, 0);
       const double rv0 = lane_f64(rv, 0);
-      rhs[valid ? pf_r : r0] = valid ? rv : rv0;
+      put<(DIAG & 128) != 0>(&rhs[valid ? pf_r : r0], valid ? rv : rv0);
     }
     // prefix of the row lengths within the x-run (7 lanes), the runs' offsets in the image
     int p = 0;
@@ -457,7 +474,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
         const int P = min(64 * i + lane, 15 * kRows - 1);
         const int L = P / 15, j = P - 15 * L;
         const bool ok = j < lens[L];
-        vals[ok ? rbs[L] + j : rb0] = img[ok ? P : 0];
+        put<(DIAG & 128) != 0>(&vals[ok ? rbs[L] + j : rb0], img[ok ? P : 0]);
       }
     }
     else {
@@ -486,7 +503,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
       for (int h = 0; h < 2; ++h) {  // rl <= 7 rows x 15 = 105
         const int t = lane + 64 * h;
         const bool ok = t < rl;
-        vals[ok ? dst + t : dst0] = img[ok ? off + t : 0];
+        put<(DIAG & 128) != 0>(&vals[ok ? dst + t : dst0], img[ok ? off + t : 0]);
       }
       off += rl;
     }
@@ -813,20 +830,24 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
 #define AFEM_CUBES_K(S, C, X, Y, N)                                                                                  \
   (rhs ? (rhs_add ? &k_assemble_cubes<S, C, X, Y, N, true, true> : &k_assemble_cubes<S, C, X, Y, N, true, false>)    \
        : &k_assemble_cubes<S, C, X, Y, N, false, false>)
-  const char* de = variant("AFEM_CUBES_DIAG");
-  const int diag = de ? atoi(de) : 0;
+  const char* de = variant("AFEM_CUBES_V");
+  const int diag = de ? atoi(de) : kCubesV;
   auto* kern = canon ? AFEM_CUBES_K(64, true, true, true, true)
                : carry ? (xex ? (yex ? AFEM_CUBES_K(64, true, true, true, false) : AFEM_CUBES_K(64, true, true, false, false))
                               : AFEM_CUBES_K(64, true, false, false, false))
                        : (s49 ? AFEM_CUBES_K(49, false, false, false, false) : AFEM_CUBES_K(64, false, false, false, false));
 #undef AFEM_CUBES_K
-  if (diag && !canon && carry && xex && yex && rhs && !rhs_add) {
+  // AFEM_CUBES_V: another variant of the headline instance (generator boxes and
+  // natural lattices, RHS set) or of the canonical one (RHS set)
+  if (diag != kCubesV && carry && xex && yex && rhs && !rhs_add) {
     switch (diag) {
-#define AFEM_CUBES_D(D) \
-  case D: kern = &k_assemble_cubes<64, true, true, true, false, true, false, D>; break;
-      AFEM_CUBES_D(1) AFEM_CUBES_D(2) AFEM_CUBES_D(4) AFEM_CUBES_D(8) AFEM_CUBES_D(3) AFEM_CUBES_D(9)
-      AFEM_CUBES_D(6) AFEM_CUBES_D(12) AFEM_CUBES_D(14) AFEM_CUBES_D(16) AFEM_CUBES_D(32) AFEM_CUBES_D(48)
-      AFEM_CUBES_D(17) AFEM_CUBES_D(64) AFEM_CUBES_D(80) AFEM_CUBES_D(96) AFEM_CUBES_D(112)
+#define AFEM_CUBES_D(D)                                                                                              \
+  case D:                                                                                                            \
+    kern = canon ? &k_assemble_cubes<64, true, true, true, true, true, false, D>                                    \
+                 : &k_assemble_cubes<64, true, true, true, false, true, false, D>;                                  \
+    break;
+      AFEM_CUBES_D(0) AFEM_CUBES_D(112) AFEM_CUBES_D(kCubesV | 1) AFEM_CUBES_D(kCubesV | 4)
+      AFEM_CUBES_D(kCubesV | 8) AFEM_CUBES_D(kCubesV | 2)
 #undef AFEM_CUBES_D
       default: break;
     }

@@ -25,6 +25,9 @@ ap.add_argument("--nz", type=int, default=None)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--settle", type=float, default=100.0)
+ap.add_argument("--mesh", choices=("box", "arrays", "natural"), default="box",
+                help="box: the generator's; arrays: the same box handed over in a random numbering (c2_arrays); "
+                     "natural: handed over in its own lexicographic numbering (c2_arrays_natural)")
 ap.add_argument("variants", nargs="+")
 a = ap.parse_args()
 
@@ -37,6 +40,20 @@ all_knobs = sorted({k for _, kn in variants for k in kn})
 
 ctx = af.Context(0)
 mesh = af.Mesh.structured(ctx, 3, a.n, nz=a.nz, jitter=0.2, seed=20250220)
+if a.mesh != "box":
+    cells, coords, _ = mesh.download()
+    mesh.close()
+    rng = np.random.default_rng(1234)
+    if a.mesh == "arrays":
+        p = rng.permutation(coords.shape[0]).astype(np.int32)
+        cells = p[cells][rng.permutation(cells.shape[0])]
+        pc = np.empty_like(coords)
+        pc[p] = coords
+        coords = pc
+    else:
+        cells = np.ascontiguousarray(cells[rng.permutation(cells.shape[0])])
+    mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    del cells, coords
 bsr = af.BSRFormat(mesh, 1).initialize(True)
 bsr.computeSparsity()
 rhs = ctx.malloc(8 * mesh.n_own_nodes)
