@@ -491,7 +491,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
       const int src = active ? lane : (int)__ffsll((long long)am) - 1;
       const double rv = __shfl(f_meas * macc, src);
       const int32_t rr = __shfl(row, src);
-      if (rhs) rhs[rr] = rhs_add ? rhs[rr] + rv : rv;
+      if (rhs) st_out(&rhs[rr], rhs_add ? rhs[rr] + rv : rv);
     }
     wave_sync_lds();
 
@@ -539,7 +539,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
         const int P = min(64 * k + lane, total - 1);
         const double v = tile.acc[P];
         const int m = map[P];
-        vals[rbs[m & 63] + (m >> 6)] = v;
+        st_out(&vals[rbs[m & 63] + (m >> 6)], v);
       }
     }
     else {  // rows longer than MAXW (not on the host-selected variants)
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(64, 2) void k_assemble_p1(int64_t n_slices, int64_t
       wave_sync_lds();
       for (int p = lane; p < total; p += 64) {
         const int ix = map[p];
-        vals[rbs[ix & 63] + (ix >> 6)] = tile.acc[ix];
+        st_out(&vals[rbs[ix & 63] + (ix >> 6)], tile.acc[ix]);
       }
     }
     wave_sync_lds();
@@ -647,6 +647,12 @@ extern "C" int afem_debug_wave_times(unsigned long long* out, int n)
 // path, so both give the same bits.
 // PERM: a canonical structure (Structure::canon): the slots are the lattice's
 // canonical ones and the write-back stores slot t at rb + cperm[16 p + t].
+// the general / uniform instances' write-back through a strided image (row
+// per 16 lanes) instead of the compacted one (AFEM_WB_STRIDED=0 builds the
+// latter, for A/B)
+#ifndef AFEM_WB_STRIDED
+#define AFEM_WB_STRIDED 1
+#endif
 template <int NV, int MAXC, int MAXW, int UMODE, bool PERM = false>
 __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64_t n_slices, const SliceRec* __restrict__ recs,
                                                           unsigned long long* __restrict__ tickets,
@@ -1014,7 +1020,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
       const int src = active ? lane : (int)__ffsll((long long)am) - 1;
       const double rv = __shfl(f_meas * macc, src);
       const int32_t rr = __shfl(row, src);
-      if (rhs) rhs[rr] = rhs_add ? rhs[rr] + rv : rv;
+      if (rhs) st_out(&rhs[rr], rhs_add ? rhs[rr] + rv : rv);
     }
     wave_sync_lds();
 
@@ -1047,6 +1053,34 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
 #pragma unroll
       for (int t = 0; t < MAXW; ++t)
         if (t < W) sum += rv[t];  // uniform bound
+#if AFEM_WB_STRIDED
+      // row L's values at [SW L, SW L + SW) of an image with an odd stride SW
+      // (the lanes' writes of one slot hit 32 distinct bank pairs; the
+      // compacted image -- row L at its prefix offset -- made them collide:
+      // unstructured meshes' rows differ in length), then 64 / LPR rows per
+      // store instruction, LPR = 16 (32) lanes per row (each row's values one
+      // contiguous range of vals, as in the compacted order).  The image overlays the
+      // accumulators and the first coordinates (64 (W + 1) doubles <= the
+      // accumulators' 64 w_cap + the coordinates' 256 w_cap bytes)
+      const int SW = W | 1;
+      int64_t* const wrb = reinterpret_cast<int64_t*>(li);  // row bases, then lengths (the index table is done)
+      int* const wlen = reinterpret_cast<int*>(wrb + 64);
+      (void)total;
+      wave_sync_lds();  // every lane's reads before the overlapping image writes
+#pragma unroll
+      for (int t = 0; t < MAXW; ++t)
+        if (t < len) acc[SW * lane + (PERM ? (int)pbyte(pq, t) : t)] = t == (int)dslot ? -sum : rv[t];
+      wrb[lane] = rb;
+      wlen[lane] = active ? len : 0;
+      wave_sync_lds();
+      constexpr int LPR = MAXW <= 16 ? 16 : (MAXW <= 32 ? 32 : 64);  // lanes per row
+      const int tl = lane & (LPR - 1);
+#pragma unroll
+      for (int k = 0; k < LPR; ++k) {
+        const int L = (64 / LPR) * k + lane / LPR;
+        if (tl < wlen[L]) st_out(&vals[wrb[L] + tl], acc[SW * L + tl]);
+      }
+#else
       uint32_t* const map32 = reinterpret_cast<uint32_t*>(cxyz);
       wave_sync_lds();  // every lane's reads before the overlapping flat writes
 #pragma unroll
@@ -1060,8 +1094,9 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
 #pragma unroll
       for (int k = 0; k < MAXW; ++k) {
         const int P = min(64 * k + lane, total - 1);
-        vals[map32[P]] = acc[P];
+        st_out(&vals[map32[P]], acc[P]);
       }
+#endif
     }
     else {
       if (dsl != 0xFFu) {
@@ -1076,7 +1111,7 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
       wave_sync_lds();
       for (int p = lane; p < total; p += 64) {
         const int ix = map[p];
-        vals[rbs[ix & 63] + (ix >> 6)] = acc[ix];
+        st_out(&vals[rbs[ix & 63] + (ix >> 6)], acc[ix]);
       }
     }
     wave_sync_lds();
@@ -1239,7 +1274,7 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
       const int src = active ? lane : (int)__ffsll((long long)am) - 1;
       const double rv = __shfl(f_meas * macc, src);
       const int32_t rr = __shfl(row, src);
-      if (rhs) rhs[rr] = rhs_add ? rhs[rr] + rv : rv;
+      if (rhs) st_out(&rhs[rr], rhs_add ? rhs[rr] + rv : rv);
     }
     // ---- diagonal (-sum of the row's other entries, in slot order) + write-back image
     double sum = 0.0;
@@ -1271,7 +1306,7 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
         const int P = 64 * k + lane;
         const int L = P / W;  // constant divisor
         const int64_t base = rbs[L];
-        if (base >= 0) vals[base + (P - L * W)] = flat[P];
+        if (base >= 0) st_out(&vals[base + (P - L * W)], flat[P]);
       }
     }
     else if (runs) {
@@ -1288,7 +1323,7 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
         const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)rb, 4 * r);
         const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)rb >> 32), 4 * r);
         double* const dst = vals + (int64_t)(((uint64_t)hi << 32) | lo);
-        dst[o] = flat[4 * W * r + o];
+        st_out(&dst[o], flat[4 * W * r + o]);
       }
     }
     else if (active) {
@@ -1296,7 +1331,7 @@ __device__ __forceinline__ void stencil_slice(const StripPre<MAXC>& cur, int nst
       // slices): each lane stores its row's W values straight from the registers
       // (no image, no owner table: nothing of this path is kept live across slices)
 #pragma unroll
-      for (int t = 0; t < W; ++t) vals[rb + t] = t == D ? -sum : acc[t];
+      for (int t = 0; t < W; ++t) st_out(&vals[rb + t], t == D ? -sum : acc[t]);
     }
     wave_sync_lds();
 }
@@ -1771,7 +1806,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
     }
     if (rhs && active) {
     const double rv = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
-    rhs[3 * (int64_t)row + ci] = rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv;
+    st_out(&rhs[3 * (int64_t)row + ci], rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv);
   }
     wave_sync_lds();
 
@@ -1793,7 +1828,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
             const int j = k + ci < 3 ? k + ci : k + ci - 3;
             const double v =
                 t == (int)dslot ? add_nc(-sum[k], k == 0 ? c0 * macc * (1.0 / 24.0) : 0.0) : acc_lane[192 * t + 64 * k];
-            vals[per_block ? 9 * (rb + t) + 3 * ci + j : 9 * rb + 3 * (int64_t)ci * len + 3 * t + j] = v;
+            st_out(&vals[per_block ? 9 * (rb + t) + 3 * ci + j : 9 * rb + 3 * (int64_t)ci * len + 3 * t + j], v);
           }
         }
       }
@@ -1854,7 +1889,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
       if (64 * k >= total) break;  // uniform
       const int Pc = min(64 * k + lane, total - 1);
       const int m = map[Pc];
-      vals[rbs[m & 63] + (m >> 6)] = acc[Pc];
+      st_out(&vals[rbs[m & 63] + (m >> 6)], acc[Pc]);
     }
     }
     wave_sync_lds();
@@ -2229,7 +2264,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
     }
     if (rhs && active) {
       const double rv = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
-      rhs[3 * (int64_t)row + ci] = rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv;
+      st_out(&rhs[3 * (int64_t)row + ci], rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv);
     }
     wave_sync_lds();
 
@@ -2342,21 +2377,21 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
             // threads past the run repeat its last value (same address and
             // value): no exec-mask branch between the image reads
             const int o = min(tid + 192 * i, RUN - 1);
-            dst[o] = src[o];
+            st_out(&dst[o], src[o]);
           }
         }
       }
       else {
         for (int P = tid; P < 64 * B; P += 192) {
           const int L = P / B;
-          vals[9 * rbs[L] + (P - L * B)] = flat[P];
+          st_out(&vals[9 * rbs[L] + (P - L * B)], flat[P]);
         }
       }
     }
     else {
       for (int P = tid; P < 9 * total; P += 192) {
         const int L = bown[P / 9];
-        vals[9 * rbs[L] + (P - 9 * fps[L])] = flat[P];
+        st_out(&vals[9 * rbs[L] + (P - 9 * fps[L])], flat[P]);
       }
     }
     __syncthreads();
@@ -2501,7 +2536,7 @@ __global__ __launch_bounds__(64) void k_assemble_elast_tet(int u_cap, int w_cap,
   }
   if (rhs && active) {
     const double rv = (ci == 0 ? fx : (ci == 1 ? fy : fz)) * macc * (1.0 / 24.0);
-    rhs[3 * (int64_t)row + ci] = rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv;
+    st_out(&rhs[3 * (int64_t)row + ci], rhs_add ? rhs[3 * (int64_t)row + ci] + rv : rv);
   }
   wave_sync_lds();
   // diagonal block row ci, then the row's 3*len values
@@ -2514,8 +2549,8 @@ __global__ __launch_bounds__(64) void k_assemble_elast_tet(int u_cap, int w_cap,
       acc_lane[192 * dslot + 64 * jj] = add_nc(-sum[jj], jj == ci ? c0 * macc * (1.0 / 24.0) : 0.0);
     for (int t = 0; t < len; ++t)
       for (int jj = 0; jj < 3; ++jj)
-        vals[per_block ? (rb + t) * 9 + 3 * ci + jj : rb * 9 + (int64_t)ci * 3 * len + 3 * t + jj] =
-          acc_lane[192 * t + 64 * jj];
+        st_out(&vals[per_block ? (rb + t) * 9 + 3 * ci + jj : rb * 9 + (int64_t)ci * 3 * len + 3 * t + jj],
+          acc_lane[192 * t + 64 * jj]);
   }
 }
 

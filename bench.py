@@ -891,6 +891,7 @@ def main():
     for i in range(args.steps):
         step(2 * i if i < slots else None)
     ctx.synchronize()
+    elapsed_own = time.perf_counter() - t0
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -917,6 +918,7 @@ def main():
     t0 = time.perf_counter()
     st = ls.solve()
     ctx.synchronize()
+    cg_s_own = time.perf_counter() - t0
     if dist:
         dist.barrier()
     cg_s = time.perf_counter() - t0
@@ -927,6 +929,33 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         cg_s = float(t[0])
     cg_iter_per_s = args.cg_iters / cg_s
+    per_rank = None
+    if dist:
+        # where each rank's time goes: its assembly kernel time,
+        # and a separate short PCG run with the loop's halo waits and scalar
+        # all-reduces timed by HIP events on the context stream (outside the
+        # timed region above: the event records would perturb it)
+        nit = min(20, args.cg_iters)
+        ls.setSolverOptions(fixed_iterations=nit, profile_comm=True)
+        ctx.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        sp = ls.solve()
+        ctx.synchronize()
+        prof_s = time.perf_counter() - t0
+        ls.setSolverOptions(profile_comm=False)
+        mine = {"rank": rank, "dof": int(n_own), "assembly_kernel_ms": round(float(np.median(kernel_ms)), 4),
+                "step_ms_own": round(elapsed_own * 1e3 / args.steps, 4),
+                "cg_ms_per_iter_own": round(cg_s_own * 1e3 / args.cg_iters, 4),
+                "cg_device_ms_per_iter": round(st["solve_ms"] / max(st["iterations"], 1), 4),
+                "profiled_cg_ms_per_iter": round(prof_s * 1e3 / nit, 4),
+                "halo_wait_ms_per_iter": round(sp["halo_wait_ms"] / max(sp["n_halo"], 1), 5),
+                "allreduce_ms_per_iter": round(sp["allreduce_ms"] / max(sp["iterations"], 1), 5),
+                "allreduces_per_iter": round(sp["n_allreduce"] / max(sp["iterations"], 1), 2),
+                "halo_bytes_per_exchange": int(sp["halo_bytes"])}
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        per_rank = gathered
 
     if rank == 0:
         kmed = float(np.median(kernel_ms))
@@ -1001,6 +1030,7 @@ def main():
             "cg_device_ms": round(st["solve_ms"], 3), "cg_spmv": SPMV_KERNELS.get(st["spmv_kernel"]),
             "sparsity_ms": round(sparsity_ms, 1),
             "setup_s": round(setup_s, 2),
+            **({"per_rank": per_rank} if per_rank else {}),
             **extras,
         }
         print(json.dumps(out), flush=True)

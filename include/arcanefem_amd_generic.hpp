@@ -100,6 +100,23 @@ __device__ __forceinline__ void unit_lds_order()
 #endif
 }
 
+/* A value store of the flush: non-temporal when it overwrites (the launch
+ * never re-reads the values; they would evict the coordinates and entries the
+ * next units read from L2).  AFEM_GENERIC_NT 0: plain stores. */
+#ifndef AFEM_GENERIC_NT
+#define AFEM_GENERIC_NT 1
+#endif
+__device__ __forceinline__ void flush_store(double* d, double val, int overwrite)
+{
+#if AFEM_GENERIC_NT
+  if (overwrite) {
+    __builtin_nontemporal_store(val, d);
+    return;
+  }
+#endif
+  *d = overwrite ? val : *d + val;
+}
+
 /* Writes layer L of unit U (its LDS buffer) to the values and zeroes the buffer. */
 template <int K, bool WIDE>
 __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const afem_functor_unit& U, int L,
@@ -148,9 +165,7 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
       const long long dst = __shfl(rb0, 8 * g);
       const int gl = __shfl(glen, 8 * g);
       for (int q = lane; q < gl; q += 64) {
-        double* d = p.values + dst + q;
-        const double val = buf[ib + q];
-        *d = overwrite ? val : *d + val;
+        flush_store(p.values + dst + q, buf[ib + q], overwrite);
       }
       ib += gl;
     }
@@ -166,7 +181,7 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
           const double val = buf[pl * sr + (lane ^ (pl & swz))];
           const int64_t idx = p.ordered_per_block ? (rb + s) * KK + i * K + j
                                                   : rb * KK + (int64_t)i * K * len + K * s + j;
-          p.values[idx] = overwrite ? val : p.values[idx] + val;
+          flush_store(p.values + idx, val, overwrite);
         }
   }
   unit_lds_order();

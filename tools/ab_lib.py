@@ -1,7 +1,8 @@
 """A/B of two builds of libafem on the same box: runs this script's timing
 part in two child processes (AFEM_LIB=libA, AFEM_LIB=libB) alternately.
 usage: python tools/ab_lib.py libA.so libB.so [n] [reps] [rounds] [mode]
-mode: poisson (C2-style scalar assembly, default) | c3 (block-3 elasticity)"""
+mode: poisson (C2-style scalar assembly, default) | c3 (block-3 elasticity) |
+      unstructured (L-shape-3D refined n times, Poisson: the general strip instances)"""
 import os
 import subprocess
 import sys
@@ -13,7 +14,14 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     import arcanefem_amd as af
     n, reps, mode = int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     ctx = af.Context(0)
-    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+    if mode == "unstructured":
+        import bench
+        from arcanefem_amd.gmsh import read_gmsh
+        gm = read_gmsh(os.path.join(ROOT, "tests", "golden", "L-shape-3D.msh"))
+        cells, coords = bench.refine_tets(gm.cells, gm.coords, n, "cpu")
+        mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    else:
+        mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
     k = 3 if mode == "c3" else 1
     bsr = af.BSRFormat(mesh, k).initialize(False if k == 3 else True)
     bsr.computeSparsity()
