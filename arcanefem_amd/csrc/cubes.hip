@@ -203,13 +203,22 @@ struct CubeCanon {
 // process, settled): 0.520 / 4.53 ms with none, 0.465 / 4.20 with 16 | 32 | 64.
 constexpr int kCubesV = 16 | 32 | 64 | 128;
 
+// register budget: 64-row planes + one coordinate layer = 17.3 KB of LDS, 9
+// waves per CU, so 2 per SIMD whatever the registers (256 VGPRs, no spill);
+// 49-row planes = 13.7 KB, 11 waves per CU: 3 per SIMD at <= 168 VGPRs
+template <int STRIDE>
+constexpr int cube_waves() { return STRIDE == 64 ? 2 : 3; }
 template <int STRIDE, bool CARRY, bool XEX, bool YEX, bool CANON, bool HAS_RHS, bool RHS_ADD, int DIAG = kCubesV>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_assemble_cubes(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<STRIDE>(), cube_waves<STRIDE>()))) void k_assemble_cubes(
     CubeGeom g, const int64_t* __restrict__ rows, const double* __restrict__ coords, double* __restrict__ vals,
     double* __restrict__ rhs, CubeCanon cc)
 {
   __shared__ __align__(16) double acc[2][kAcc][STRIDE];  // STRIDE >= 49 rows per offset plane
-  __shared__ double cz[2][3][kCol * kCol];  // SoA coordinates of two node layers
+  // SoA coordinates of the node layers being read: with the carry the bottom
+  // corners come from registers (Xc), so one layer -- the cube layer's top --
+  // is read, and the next one is staged over it after the cubes
+  constexpr int NCZ = CARRY ? 1 : 2;
+  __shared__ double cz[NCZ][3][kCol * kCol];
   const int lane = threadIdx.x;
   // XCD-aware: blocks go round-robin over the 8 XCDs; XCD x takes the x-th
   // contiguous eighth of the units (x fastest, then y, then segments)
@@ -273,6 +282,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     }
   };
   auto store_layer = [&](int buf) {
+    buf = NCZ == 1 ? 0 : buf;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int q = min(lane + 64 * h, kCol * kCol - 1);  // lanes past the 81 nodes repeat node 80's store
@@ -341,9 +351,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     wave_lds_order();  // every lane's accumulator reads before the image overwrites them
     double* img = &acc[b][0][0];
     // row L at [15 L, 15 L + 15): lanes past the 49 rows write into
-    // [735, 960) of the buffer, which no store reads
+    // [735, 960) of the buffer, which no store reads (64-row planes), or --
+    // 49-row planes, whose buffer ends at 735 -- repeat row 48's writes with
+    // row 48's values (they read row 48: same addresses, same values)
 #pragma unroll
-    for (int o = 0; o < 15; ++o) img[15 * lane + o] = v[o];
+    for (int o = 0; o < 15; ++o) img[15 * (STRIDE == 64 ? lane : lr) + o] = v[o];
     wave_lds_order();
     // x-run q = rows 7q .. 7q + 6: 105 values contiguous in vals from row 7q's
     // first one; the second store's lanes past 105 repeat value 104 (same
@@ -387,7 +399,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     wave_lds_order();
   };
   auto flush = [&](int z) {
-    if constexpr (!CANON && STRIDE == 64) {
+    if constexpr (!CANON) {
       if (full_flush_on && layer_full(z)) {
         if constexpr (!(DIAG & 8)) flush_full(z);
         return;
@@ -452,7 +464,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
     if constexpr (CANON) {
       // row L's values at [15 L, 15 L + 15) in the caller's column order; its
       // first value and length in the free coordinate buffer of layer z & 1
-      int64_t* const rbs = reinterpret_cast<int64_t*>(&cz[z & 1][0][0]);
+      int64_t* const rbs = reinterpret_cast<int64_t*>(&cz[NCZ == 1 ? 0 : (z & 1)][0][0]);
       int* const lens = reinterpret_cast<int*>(rbs + 64);
       rbs[lane] = rb;
       lens[lane] = len;
@@ -575,7 +587,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int q = (ci + cbit(c, 0)) + kCol * (cj + cbit(c, 1));
-      Xc[c] = P3{ cz[zc & 1][0][q], cz[zc & 1][1][q], cz[zc & 1][2][q] };
+      const int bz = NCZ == 1 ? 0 : (zc & 1);
+      Xc[c] = P3{ cz[bz][0][q], cz[bz][1][q], cz[bz][2][q] };
     }
   };
   auto cubes = [&](int zc) {
@@ -590,8 +603,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int q = (ci + cbit(c, 0)) + kCol * (cj + cbit(c, 1));
-      X[c] = CARRY ? Xc[c] : P3{ cz[bb][0][q], cz[bb][1][q], cz[bb][2][q] };
-      X[c + 4] = P3{ cz[bt][0][q], cz[bt][1][q], cz[bt][2][q] };
+      const int zb = NCZ == 1 ? 0 : bb, zt = NCZ == 1 ? 0 : bt;
+      X[c] = CARRY ? Xc[c] : P3{ cz[zb][0][q], cz[zb][1][q], cz[zb][2][q] };
+      X[c + 4] = P3{ cz[zt][0][q], cz[zt][1][q], cz[zt][2][q] };
       if constexpr (CARRY) Xc[c] = X[c + 4];
     }
     double ev[8][8];
@@ -720,9 +734,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
   store_layer(zc_first & 1);
   prefetch_ids(zc_first + 1);
   load_layer(zc_first + 1);
+  if constexpr (NCZ == 1) {  // the bottom layer into the corner registers before the top overwrites it
+    wave_lds_order();
+    prime_corners(zc_first);
+    wave_lds_order();
+  }
   store_layer((zc_first + 1) & 1);
   wave_lds_order();
-  if constexpr (CARRY) prime_corners(zc_first);
+  if constexpr (CARRY && NCZ == 2) prime_corners(zc_first);
   int zc = zc_first;
   if (zc < z0) {  // the cube layer below the segment: its top corners only, no flush
     prefetch_ids(zc + 2);
@@ -833,7 +852,9 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
   const char* de = variant("AFEM_CUBES_V");
   const int diag = de ? atoi(de) : kCubesV;
   auto* kern = canon ? AFEM_CUBES_K(64, true, true, true, true)
-               : carry ? (xex ? (yex ? AFEM_CUBES_K(64, true, true, true, false) : AFEM_CUBES_K(64, true, true, false, false))
+               : carry ? (xex ? (yex ? (s49 ? AFEM_CUBES_K(49, true, true, true, false)
+                                            : AFEM_CUBES_K(64, true, true, true, false))
+                                     : AFEM_CUBES_K(64, true, true, false, false))
                               : AFEM_CUBES_K(64, true, false, false, false))
                        : (s49 ? AFEM_CUBES_K(49, false, false, false, false) : AFEM_CUBES_K(64, false, false, false, false));
 #undef AFEM_CUBES_K
