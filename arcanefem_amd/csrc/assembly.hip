@@ -1922,6 +1922,11 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
 // the frame rotated by the wave's component row (three SoA reads at
 // rotated array offsets), so the element arithmetic is that of
 // k_assemble_elast_strip, entry for entry.
+// the stencil instance's full-slice x-run stores: 16 B per thread
+// (AFEM_WG_ST16=0 builds the 8-B stores, for A/B)
+#ifndef AFEM_WG_ST16
+#define AFEM_WG_ST16 1
+#endif
 __host__ __device__ constexpr int64_t elast_wg_bytes(int64_t u_cap, int64_t w_cap)
 {
   return 3 * 3 * 8 * 64 * w_cap + 3 * 8 * u_cap + 2 * 64 * w_cap + 64 * 8 + 64 * 4 + 64 + ((64 * w_cap + 15) & ~15);
@@ -2372,6 +2377,18 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
           const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)rb >> 32), 4 * r);
           double* const dst = vals + 9 * (int64_t)(((uint64_t)hi << 32) | lo);
           const double* const src = flat + RUN * r;
+#if AFEM_WG_ST16
+          // 16 B per thread (values 2 o', 2 o' + 1; the run start is 8-B aligned:
+          // unaligned 16-B stores), threads past the run repeat its last pair
+          // (same addresses, same values): 2 stores per thread and run, not 3
+          typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
+          static_assert(RUN % 2 == 0, "pairs");
+#pragma unroll
+          for (int i = 0; i < (RUN / 2 + 191) / 192; ++i) {
+            const int o = min(2 * (tid + 192 * i), RUN - 2);
+            st_out(reinterpret_cast<d2u*>(dst + o), d2u{ src[o], src[o + 1] });
+          }
+#else
 #pragma unroll
           for (int i = 0; i < (RUN + 191) / 192; ++i) {
             // threads past the run repeat its last value (same address and
@@ -2379,6 +2396,7 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
             const int o = min(tid + 192 * i, RUN - 1);
             st_out(&dst[o], src[o]);
           }
+#endif
         }
       }
       else {

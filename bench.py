@@ -70,9 +70,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true",
                     help="skip the CPU baselines (the oracle timed at the C2 size on the host cores, N = 1 only)")
     ap.add_argument("--no-extras", action="store_true", help="skip the side measurements (N = 1 only anyway)")
-    ap.add_argument("--legs", default="c4,c3,c2_generic,c2_arrays,c2_arrays_natural,unstructured,c5",
+    ap.add_argument("--legs", default="c4,c3,c2_generic,c2_arrays,c2_arrays_natural,unstructured,generic_unstructured,c5",
                     help="the side measurements to run (comma list of c4, c3, c2_generic, c2_arrays, "
-                         "c2_arrays_natural, unstructured, c5)")
+                         "c2_arrays_natural, unstructured, generic_unstructured, c5)")
     ap.add_argument("--no-headline", action="store_true",
                     help="N = 1: skip the headline C2 step (and the CPU baselines), run only --legs (per-leg "
                          "rocprofv3 runs, tools/profile_legs.sh)")
@@ -512,7 +512,7 @@ def c2_arrays_leg(ctx, af, n, natural=False, reps=10, warmup=2, settle_ms=150.0)
     return out
 
 
-def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2, settle_ms=150.0):
+def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2, settle_ms=150.0, unstructured_levels=0):
     """C2 through the path an UNCHANGED module takes: BSRFormat::assembleBilinear
     with the module's own element lambda (_computeElementMatrixTetra4Gpu,
     modules/poisson/FemModule.h:177-186: examples/elements.hpp PoissonTet4,
@@ -522,11 +522,24 @@ def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2, settle_ms=150.0
     The roofline's algorithmic bytes are the headline's without the RHS (no
     source term in assembleBilinear).  Also timed: the reference's algorithm
     (one lane per cell, f64 atomics into HBM: assemble_bilinear_atomic) on the
-    same structure, and the values against the fixed-physics strip kernel."""
+    same structure, and the values against the fixed-physics strip kernel.
+    unstructured_levels > 0 (`generic_unstructured`): the same
+    functor on the reference's L-shape-3D mesh refined that many times (the
+    unstructured leg's mesh: slice-piece units of the Hilbert order)."""
     sys.path.insert(0, os.path.join(ROOT, "examples"))
     import generic_example as gx
 
-    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+    if unstructured_levels > 0:
+        from arcanefem_amd.gmsh import read_gmsh
+
+        gm = read_gmsh(os.path.join(ROOT, "tests", "golden", "L-shape-3D.msh"))
+        cells, coords = refine_tets(gm.cells, gm.coords, unstructured_levels, "cpu")
+        mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
+        del cells, coords
+        what = f"L-shape-3D.msh refined {unstructured_levels}x"
+    else:
+        mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+        what = f"C2 box n={n}"
     bsr = af.BSRFormat(mesh, 1).initialize(True)
     bsr.computeSparsity()
     ctx.synchronize()
@@ -553,7 +566,7 @@ def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2, settle_ms=150.0
     # cn_cv itself), coordinates, row offsets, values
     ent_b = 24 if plan["wide"] else 16
     kmin = (ent_b + 16) * plan["n_entries"] + 24 * mesh.n_nodes + 8 * (mesh.n_own_nodes + 1) + 8 * nnz
-    out = {"config": f"C2 box n={n} ({mesh.n_own_nodes} DoF, {mesh.n_cells} tets): assembleBilinear(the Poisson "
+    out = {"config": f"{what} ({mesh.n_own_nodes} DoF, {mesh.n_cells} tets): assembleBilinear(the Poisson "
                      f"module's tet4 element lambda) through the generic element-functor entry, values overwritten",
            "dof": int(mesh.n_own_nodes), "value": round(mesh.n_own_nodes / (kms * 1e-3) / 1e6, 1),
            "unit": "MDoF/s (assembly kernel)", "kernel_ms": round(kms, 4), "kernel_ms_all": [round(x, 4) for x in ks],
@@ -572,7 +585,10 @@ def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2, settle_ms=150.0
            "plan_build_ms": round(plan_ms, 1),
            "atomic_kernel_ms": round(kam, 4), "atomic_frac": round(ab / (kam * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "vs_fixed_physics_max_rel": float(np.abs(vals_u - vals_f).max() / np.abs(vals_f).max())}
-    with_traffic(out["roofline"], "c2_generic", n, kms)
+    if unstructured_levels > 0:
+        with_traffic(out["roofline"], "generic_unstructured", unstructured_levels, kms)
+    else:
+        with_traffic(out["roofline"], "c2_generic", n, kms)
     bsr.close()
     mesh.close()
     return out
@@ -804,6 +820,9 @@ def run_legs(ctx, af, args, legs):
         extras["c2_arrays_natural"] = c2_arrays_leg(ctx, af, 215, natural=True, settle_ms=sm)
     if "unstructured" in legs and args.unstructured_levels > 0:
         extras["unstructured"] = unstructured_leg(ctx, af, "L-shape-3D.msh", args.unstructured_levels, settle_ms=sm)
+    if "generic_unstructured" in legs and args.unstructured_levels > 0:
+        extras["generic_unstructured"] = c2_generic_leg(ctx, af, 0, settle_ms=sm,
+                                                        unstructured_levels=args.unstructured_levels)
     if "c5" in legs:
         extras["c5"] = elastodynamics_c5(ctx, af, args.c5_n, args.c5_steps)
     return extras

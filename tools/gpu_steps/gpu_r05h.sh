@@ -13,5 +13,6 @@ timeout -k 10 300 python3 -u tools/ab_knobs.py --n 215 --rounds 3 --mesh arrays 
 timeout -k 10 400 python3 -u tools/ab_lib.py arcanefem_amd/libafem.so arcanefem_amd/libafem_wb0.so 5 20 2 unstructured > gpurun_out/r05h_ab_unstr_wb.log 2>&1 || exit $?
 timeout -k 10 400 python3 -u tools/ab_lib.py arcanefem_amd/libafem.so arcanefem_amd/libafem_nt0.so 5 20 2 unstructured > gpurun_out/r05h_ab_unstr_nt.log 2>&1 || exit $?
 timeout -k 10 300 python3 -u tools/ab_lib.py arcanefem_amd/libafem.so arcanefem_amd/libafem_nt0.so 170 15 2 c3 > gpurun_out/r05h_ab_c3_nt.log 2>&1 || exit $?
+timeout -k 10 300 python3 -u tools/ab_lib.py arcanefem_amd/libafem.so arcanefem_amd/libafem_wg0.so 170 15 2 c3 > gpurun_out/r05h_ab_c3_wg.log 2>&1 || exit $?
 PASSES="lds" bash tools/profile_legs.sh gpurun_out/r05h_prof unstructured || exit $?
 exit $RC

@@ -6,7 +6,7 @@
 # each under its own time limit; the script stops at the first failure.
 #   tools/profile_legs.sh <out_dir> <leg> [<leg> ...]
 # legs: c2 (the headline command), c4, c3, c2_generic, c2_arrays,
-# c2_arrays_natural, unstructured.  PASSES (env): pass names to run (default
+# c2_arrays_natural, unstructured, generic_unstructured.  PASSES (env): pass names to run (default
 # "trace fetch write").  Summarise with tools/collect_leg.py.
 export TMPDIR=/tmp
 OUT=$1
@@ -22,6 +22,7 @@ for LEG in "$@"; do
     c2_arrays) B="bench.py --no-headline --legs c2_arrays"; K="k_assemble_cubes" ;;
     c2_arrays_natural) B="bench.py --no-headline --legs c2_arrays_natural"; K="k_assemble_cubes" ;;
     unstructured) B="bench.py --no-headline --legs unstructured"; K="k_assemble_strip" ;;
+    generic_unstructured) B="bench.py --no-headline --legs generic_unstructured"; K="k_assemble_units" ;;
     *) echo "unknown leg $LEG"; exit 2 ;;
   esac
   D=$OUT/$LEG
