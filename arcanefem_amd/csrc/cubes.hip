@@ -196,7 +196,8 @@ struct CubeCanon {
 // the complete-layer flush (the values are not re-read by this launch; the
 // L2 keeps the coordinates the neighbouring units re-read), 64 one 16-B
 // store per lane and x-run there (7 stores per layer instead of 14), 128
-// non-temporal value and RHS stores in the other flushes.  Diagnostic
+// non-temporal value and RHS stores in the other flushes, 256 dummy rows for
+// the corners outside the unit (no zero selects; 64-row planes).  Diagnostic
 // ablations (values wrong): 1 no value stores in the complete-layer flush, 2
 // one LDS add per cube (the sum of its sums) instead of its 15, 4 no cube
 // arithmetic, 8 no complete-layer flush.  Measured (r05d/e, C2 / C4, one
@@ -567,6 +568,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
     const int buf = (cbit(c, 2) ? bt : bb) ^ (in ? 0 : 1);
     return &acc[buf][0][0] + (in ? r00 + cbit(c, 0) + kRun * cbit(c, 1) : rs);
   };
+  // DROWS (V bit 256, 64-row planes): a corner outside the unit (its row
+  // index rx or ry outside [0, 6]) adds its REAL sum into a dummy row of its
+  // own layer's buffer, rows 49..63, which no store reads: the x-outside
+  // lanes (one x edge of the 8 x 8 lanes) at 49 + cj, the other y-outside ones
+  // at 57 + rx -- 15 distinct rows for the 15 outside lanes of each corner, so
+  // no two lanes of one ds_add_f64 share an address.  No zero selects on the
+  // sums, no buffer swap; the rows of node layer z0 - 1 (below the segment,
+  // not this unit's) get real sums too, so that buffer is zeroed after the
+  // layer below (its next use is node layer z0 + 1).  Rows inside the unit but
+  // outside the box take their sums in their own slots and are never stored.
+  constexpr bool DROWS = (DIAG & 256) != 0 && STRIDE == 64;
+  int row4[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int rx = ci - 1 + (k & 1), ry = cj - 1 + (k >> 1);
+    const bool inx = rx >= 0 && rx < kRun, iny = ry >= 0 && ry < kRun;
+    row4[k] = (inx && iny) ? rx + kRun * ry : (!inx ? kRows + cj : kRows + 8 + rx);
+  }
+  auto base_d = [&](int bb, int bt, int c) { return &acc[cbit(c, 2) ? bt : bb][0][0] + row4[c & 3]; };
   // the top face's carried sums into LDS (the box's top node layer: no cube above)
   auto add_top = [&](int zc) {
     uint32_t inm;
@@ -576,11 +596,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
     constexpr int ta[5] = { 4, 4, 4, 5, 6 }, tb[5] = { 5, 6, 7, 7, 7 };
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-      atomicAdd(base_at(inm, bb, bt, ta[i]) + STRIDE * edge_o(ta[i], tb[i]), kept(ta[i], ce[i]));
-      atomicAdd(base_at(inm, bb, bt, tb[i]) + STRIDE * edge_o(tb[i], ta[i]), kept(tb[i], ce[i]));
+      if constexpr (DROWS) {
+        atomicAdd(base_d(bb, bt, ta[i]) + STRIDE * edge_o(ta[i], tb[i]), ce[i]);
+        atomicAdd(base_d(bb, bt, tb[i]) + STRIDE * edge_o(tb[i], ta[i]), ce[i]);
+      }
+      else {
+        atomicAdd(base_at(inm, bb, bt, ta[i]) + STRIDE * edge_o(ta[i], tb[i]), kept(ta[i], ce[i]));
+        atomicAdd(base_at(inm, bb, bt, tb[i]) + STRIDE * edge_o(tb[i], ta[i]), kept(tb[i], ce[i]));
+      }
     }
 #pragma unroll
-    for (int c = 4; c < 8; ++c) atomicAdd(base_at(inm, bb, bt, c) + STRIDE * 7, kept(c, cm[c - 4]));
+    for (int c = 4; c < 8; ++c) {
+      if constexpr (DROWS)
+        atomicAdd(base_d(bb, bt, c) + STRIDE * 7, cm[c - 4]);
+      else
+        atomicAdd(base_at(inm, bb, bt, c) + STRIDE * 7, kept(c, cm[c - 4]));
+    }
   };
   P3 Xc[4];  // the lane's cube's top corners, the next cube layer's bottom ones
   auto prime_corners = [&](int zc) {
@@ -706,6 +737,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
           if constexpr (DIAG & 2) {
             dsum += ev[a][b];
           }
+          else if constexpr (DROWS) {
+            atomicAdd(base_d(bb_, bt_, a) + STRIDE * edge_o(a, b), ev[a][b]);
+            atomicAdd(base_d(bb_, bt_, b) + STRIDE * edge_o(b, a), ev[a][b]);
+          }
           else {
             atomicAdd(base_at(inm, bb_, bt_, a) + STRIDE * edge_o(a, b), kept(a, ev[a][b]));
             atomicAdd(base_at(inm, bb_, bt_, b) + STRIDE * edge_o(b, a), kept(b, ev[a][b]));
@@ -716,6 +751,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
       if (!(CARRY && cbit(c, 2)) && !(XEX && !cbit(c, 0) && !cbit(c, 2)) && !(YEX && !cbit(c, 1) && !cbit(c, 2))) {
         if constexpr (DIAG & 2)
           dsum += mv[c];
+        else if constexpr (DROWS)
+          atomicAdd(base_d(bb_, bt_, c) + STRIDE * 7, mv[c]);  // |det| sums
         else
           atomicAdd(base_at(inm, bb_, bt_, c) + STRIDE * 7, kept(c, mv[c]));  // |det| sums
       }
@@ -749,6 +786,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
     wave_lds_order();
     cubes(zc);
     wave_lds_order();
+    if constexpr (DROWS) {  // node layer z0 - 1's buffer took real sums: clear it for node layer z0 + 1
+      double2* const b2 = reinterpret_cast<double2*>(&acc[zc & 1][0][0]);
+#pragma unroll
+      for (int i = 0; i < (kAcc * STRIDE / 2 + 63) / 64; ++i)
+        b2[min(64 * i + lane, kAcc * STRIDE / 2 - 1)] = make_double2(0.0, 0.0);
+      wave_lds_order();
+    }
     store_layer(zc & 1);
     ++zc;
   }
@@ -867,7 +911,7 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
     kern = canon ? &k_assemble_cubes<64, true, true, true, true, true, false, D>                                    \
                  : &k_assemble_cubes<64, true, true, true, false, true, false, D>;                                  \
     break;
-      AFEM_CUBES_D(0) AFEM_CUBES_D(112) AFEM_CUBES_D(kCubesV | 1) AFEM_CUBES_D(kCubesV | 4)
+      AFEM_CUBES_D(0) AFEM_CUBES_D(112) AFEM_CUBES_D(kCubesV | 1) AFEM_CUBES_D(kCubesV | 4) AFEM_CUBES_D(kCubesV | 256)
       AFEM_CUBES_D(kCubesV | 8) AFEM_CUBES_D(kCubesV | 2)
 #undef AFEM_CUBES_D
       default: break;
