@@ -1,7 +1,10 @@
 """GPU: BSRFormat::assembleBilinear(lambda) through the generic element-functor
 entry (include/arcanefem_amd_generic.hpp) -- the module's own element functor
-(a hipcc-compiled device lambda, examples/generic_assembly.hip) scattered cell
-by cell with f64 atomics, as femutils/BSRFormat.h:786-837 does.
+(a hipcc-compiled device lambda, examples/generic_assembly.hip) evaluated once
+per (unit, cell) by the cell-unit kernel k_assemble_units (rows of a unit in
+LDS, wavefront-local ds_add_f64 in program order, no global atomics: bitwise
+reproducible), and by the reference's own algorithm (one lane per cell, f64
+atomics into HBM, femutils/BSRFormat.h:786-837: assemble_bilinear_atomic).
 
 Gates per entry (summation order differs from the fixed-physics strip
 kernels, as the reference's atomics differ run to run): against the library's
