@@ -18,13 +18,13 @@
 
 namespace afem {
 
-// Value and RHS stores of the assembly kernels: non-temporal.  A launch never
-// re-reads what it writes, and the values (1.2 GB at C2, 5.4 GB at C3) stream
-// past every cache; plain stores evict the node coordinates the neighbouring
-// slices / units re-read from L2 (cube kernel, r05d-e: 0.520 -> 0.478 ms at
-// C2 from this alone).  Build with -DAFEM_NT_STORES=0 for plain stores (A/B).
+// Value and RHS stores of the row-strip / block-3 assembly kernels: plain by
+// default.  Non-temporal stores (-DAFEM_NT_STORES=1) pay off for long
+// contiguous runs (the cube kernel's complete-layer flush: 0.520 -> 0.478 ms
+// at C2, its V bit 32) but not for these kernels' row-wise write-backs: the
+// unstructured leg 0.246 -> 0.262 ms, C3 unchanged (r05h, tools/ab_lib.py).
 #ifndef AFEM_NT_STORES
-#define AFEM_NT_STORES 1
+#define AFEM_NT_STORES 0
 #endif
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v)

@@ -647,12 +647,6 @@ extern "C" int afem_debug_wave_times(unsigned long long* out, int n)
 // path, so both give the same bits.
 // PERM: a canonical structure (Structure::canon): the slots are the lattice's
 // canonical ones and the write-back stores slot t at rb + cperm[16 p + t].
-// the general / uniform instances' write-back through a strided image (row
-// per 16 lanes) instead of the compacted one (AFEM_WB_STRIDED=0 builds the
-// latter, for A/B)
-#ifndef AFEM_WB_STRIDED
-#define AFEM_WB_STRIDED 1
-#endif
 template <int NV, int MAXC, int MAXW, int UMODE, bool PERM = false>
 __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64_t n_slices, const SliceRec* __restrict__ recs,
                                                           unsigned long long* __restrict__ tickets,
@@ -1053,34 +1047,6 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
 #pragma unroll
       for (int t = 0; t < MAXW; ++t)
         if (t < W) sum += rv[t];  // uniform bound
-#if AFEM_WB_STRIDED
-      // row L's values at [SW L, SW L + SW) of an image with an odd stride SW
-      // (the lanes' writes of one slot hit 32 distinct bank pairs; the
-      // compacted image -- row L at its prefix offset -- made them collide:
-      // unstructured meshes' rows differ in length), then 64 / LPR rows per
-      // store instruction, LPR = 16 (32) lanes per row (each row's values one
-      // contiguous range of vals, as in the compacted order).  The image overlays the
-      // accumulators and the first coordinates (64 (W + 1) doubles <= the
-      // accumulators' 64 w_cap + the coordinates' 256 w_cap bytes)
-      const int SW = W | 1;
-      int64_t* const wrb = reinterpret_cast<int64_t*>(li);  // row bases, then lengths (the index table is done)
-      int* const wlen = reinterpret_cast<int*>(wrb + 64);
-      (void)total;
-      wave_sync_lds();  // every lane's reads before the overlapping image writes
-#pragma unroll
-      for (int t = 0; t < MAXW; ++t)
-        if (t < len) acc[SW * lane + (PERM ? (int)pbyte(pq, t) : t)] = t == (int)dslot ? -sum : rv[t];
-      wrb[lane] = rb;
-      wlen[lane] = active ? len : 0;
-      wave_sync_lds();
-      constexpr int LPR = MAXW <= 16 ? 16 : (MAXW <= 32 ? 32 : 64);  // lanes per row
-      const int tl = lane & (LPR - 1);
-#pragma unroll
-      for (int k = 0; k < LPR; ++k) {
-        const int L = (64 / LPR) * k + lane / LPR;
-        if (tl < wlen[L]) st_out(&vals[wrb[L] + tl], acc[SW * L + tl]);
-      }
-#else
       uint32_t* const map32 = reinterpret_cast<uint32_t*>(cxyz);
       wave_sync_lds();  // every lane's reads before the overlapping flat writes
 #pragma unroll
@@ -1096,7 +1062,6 @@ __global__ __launch_bounds__(64, UMODE == 1 ? 3 : 2) void k_assemble_strip(int64
         const int P = min(64 * k + lane, total - 1);
         st_out(&vals[map32[P]], acc[P]);
       }
-#endif
     }
     else {
       if (dsl != 0xFFu) {

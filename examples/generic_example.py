@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(_HERE, "libafem_generic_example.so")
+LIB = os.environ.get("AFEM_GENERIC_LIB") or os.path.join(_HERE, "libafem_generic_example.so")  # env: A/B builds
 POISSON, ELASTICITY, POISSON_LEAN = 0, 1, 2
 UNITS, ATOMIC = 0, 1
 _lib = None
