@@ -786,6 +786,34 @@ __global__ __launch_bounds__(1024) void k_reduce(int64_t n, const double* __rest
   }
 }
 
+// k_reduce over gridDim.x contiguous chunks of partial[0, n): chunk b's sum in out[b]
+__global__ __launch_bounds__(1024) void k_reduce_chunks(int64_t n, const double* __restrict__ partial,
+                                                        double* __restrict__ out)
+{
+  __shared__ double ws[16];
+  const int64_t c0 = n * blockIdx.x / gridDim.x, c1 = n * (blockIdx.x + 1) / gridDim.x;
+  double s = 0.0;
+  const int64_t step = blockDim.x;
+  int64_t i = c0 + threadIdx.x;
+  for (; i + 7 * step < c1; i += 8 * step) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = partial[i + u * step];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; i < c1; i += step) s += partial[i];
+  s = wave_sum(s);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) ws[wid] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += ws[w];
+    out[blockIdx.x] = t;
+  }
+}
+
 // Jacobi preconditioner + constraint-row flag: a row whose diagonal exceeds
 // the rest of the row by > 1e10 (penalty P = 1e30, eliminated identity rows)
 // is excluded from the reference value of the stopping test (same rule as
@@ -1538,8 +1566,19 @@ void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* ro
   AFEM_LAUNCHED();
 }
 
-void reduce_to(Ctx& ctx, const double* partial, int64_t n, double* out)
+// partial[0, n) -> *out.  Long partial arrays (the SpMV's block partials: 390 k at
+// C4, 3.1 MB for one workgroup: 37 us per reduce, 2 per CG iteration) go
+// through a first pass of kReduceChunks workgroups into scratch[0,
+// kReduceChunks) (each a contiguous chunk, fixed order: deterministic).
+constexpr int64_t kReduceChunks = 128;
+void reduce_to(Ctx& ctx, const double* partial, int64_t n, double* out, double* scratch = nullptr)
 {
+  if (scratch && n > 64 * 1024) {
+    hipLaunchKernelGGL(k_reduce_chunks, dim3((unsigned)kReduceChunks), dim3(1024), 0, ctx.stream, n, partial, scratch);
+    AFEM_LAUNCHED();
+    partial = scratch;
+    n = kReduceChunks;
+  }
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, ctx.stream, n, partial, out);
   AFEM_LAUNCHED();
 }
@@ -1918,7 +1957,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   auto rest_of_iteration = [&](int par, bool with_spmv) {
     if (with_spmv)
       launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p, ls.csr_nnz);
-    reduce_to(ctx, ls.partial.p, pl.nblocks, scal + 2);
+    reduce_to(ctx, ls.partial.p, pl.nblocks, scal + 2, ls.partial.p + pl.nblocks);
     loop_allreduce(scal + 2);
     if (use_mg) {
       hipLaunchKernelGGL(k_cg_xr, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p, ls.r.p,

@@ -34,6 +34,29 @@ def trace_means(d, rx):
     return out, (files[0] if files else None)
 
 
+def trace_spans(d, rx, names):
+    """Mean per-assembly span (ms) when an assembly launches several matching
+    kernels (they may overlap on two streams: the sum of their means would
+    count the overlap twice): the k-th dispatch of every kernel belongs to
+    assembly k; span = last end - first start.  None for a single kernel."""
+    if len(names) < 2:
+        return None
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        return None
+    per = collections.defaultdict(list)
+    for x in csv.DictReader(open(files[0])):
+        if x["Kernel_Name"] in names:
+            per[x["Kernel_Name"]].append((int(x["Start_Timestamp"]), int(x["End_Timestamp"])))
+    n = min(len(v) for v in per.values())
+    if n == 0:
+        return None
+    for v in per.values():
+        v.sort()
+    spans = [(max(per[k][i][1] for k in per) - min(per[k][i][0] for k in per)) * 1e-6 for i in range(n)]
+    return sum(spans) / n
+
+
 def counters(d, rx):
     """counter -> per-launch value (sum over matching kernels of the mean per dispatch)."""
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -58,10 +81,15 @@ def main():
         c.update(v)
         ndisp.update(n)
     kmean = sum(m for _, m in means.values()) if means else None
+    span = trace_spans(os.path.join(d, "trace"), rx, set(means))
+    if span is not None:
+        kmean = span
     lines = [f"# {tag} {leg} (size {size}): per launch = sum over the kernels matching /{kr}/ of their mean per "
              "dispatch (rocprofv3 --pmc, one pass per counter group)"]
     for k, (calls, m) in sorted(means.items()):
         lines.append(f"kernel {k}: {calls} dispatches, mean {m:.5f} ms (--kernel-trace --stats)")
+    if span is not None:
+        lines.append(f"per assembly (the k-th dispatch of each kernel; first start to last end): mean {span:.5f} ms")
     for k in sorted(c):
         lines.append(f"{k:32s} {c[k]:.6g}   ({sum(ndisp[k].values())} dispatches)")
     rec = {"leg": leg, "size": size, "world": 1, "tag": tag, "kernel_regex": kr,

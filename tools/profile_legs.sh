@@ -30,7 +30,9 @@ for LEG in "$@"; do
   for P in $PASSES; do
     echo "$LEG $P start $(date +%T)" >> $OUT/progress.log
     case $P in
-      trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $D/trace -o run -- python3 $B > $D/trace.log 2>&1 ;;
+      # the trace runs a 1.5-s settle: its mean over every dispatch of the process (the first ones run at
+      # ramping clocks) then matches the bench's settled median (bench.py settle())
+      trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $D/trace -o run -- python3 $B --settle-ms ${TRACE_SETTLE_MS:-1500} > $D/trace.log 2>&1 ;;
       fetch) timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -f csv -d $D/fetch -o run -- python3 $B --settle-ms 0 > $D/fetch.log 2>&1 ;;
       write) timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -f csv -d $D/write -o run -- python3 $B --settle-ms 0 > $D/write.log 2>&1 ;;
       sq) timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU --kernel-include-regex "$K" -f csv -d $D/sq -o run -- python3 $B --settle-ms 0 > $D/sq.log 2>&1 ;;
