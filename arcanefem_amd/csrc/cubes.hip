@@ -197,7 +197,8 @@ struct CubeCanon {
 // L2 keeps the coordinates the neighbouring units re-read), 64 one 16-B
 // store per lane and x-run there (7 stores per layer instead of 14), 128
 // non-temporal value and RHS stores in the other flushes, 256 dummy rows for
-// the corners outside the unit (no zero selects; 64-row planes).  Diagnostic
+// the corners outside the unit (no zero selects; 64-row planes), 512 16-B
+// row stores in the canonical flush.  Diagnostic
 // ablations (values wrong): 1 no value stores in the complete-layer flush, 2
 // one LDS add per cube (the sum of its sums) instead of its 15, 4 no cube
 // arithmetic, 8 no complete-layer flush.  Measured (r05d/e, C2 / C4, one
@@ -485,12 +486,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
       // row's length repeat row 0's first value (always a row), so the store
       // count is fixed
       const int64_t rb0 = rbs[0];
+      if constexpr ((DIAG & 512) != 0) {
+        // 16 B per lane: pair k of row L = values j, j + 1 with j = min(2k, len - 2)
+        // (the last pair overlaps the one before: same values), 8 pairs per row,
+        // 7 stores per layer instead of 12; rows without values repeat row 0's
+        // first pair
+        typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
 #pragma unroll
-      for (int i = 0; i < (15 * kRows + 63) / 64; ++i) {
-        const int P = min(64 * i + lane, 15 * kRows - 1);
-        const int L = P / 15, j = P - 15 * L;
-        const bool ok = j < lens[L];
-        put<(DIAG & 128) != 0>(&vals[ok ? rbs[L] + j : rb0], img[ok ? P : 0]);
+        for (int i = 0; i < (8 * kRows + 63) / 64; ++i) {
+          const int Q = min(64 * i + lane, 8 * kRows - 1);
+          const int L = Q >> 3, k = Q & 7;
+          const int len = lens[L];
+          const bool ok = len >= 2;
+          const int j = ok ? min(2 * k, len - 2) : 0;
+          const int src = ok ? 15 * L + j : 0;
+          *reinterpret_cast<d2u*>(&vals[ok ? rbs[L] + j : rb0]) = d2u{ img[src], img[src + 1] };
+        }
+      }
+      else {
+#pragma unroll
+        for (int i = 0; i < (15 * kRows + 63) / 64; ++i) {
+          const int P = min(64 * i + lane, 15 * kRows - 1);
+          const int L = P / 15, j = P - 15 * L;
+          const bool ok = j < lens[L];
+          put<(DIAG & 128) != 0>(&vals[ok ? rbs[L] + j : rb0], img[ok ? P : 0]);
+        }
       }
     }
     else {
@@ -915,7 +935,7 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
                  : &k_assemble_cubes<64, true, true, true, false, true, false, D>;                                  \
     break;
       AFEM_CUBES_D(0) AFEM_CUBES_D(112) AFEM_CUBES_D(kCubesV | 1) AFEM_CUBES_D(kCubesV | 4)
-      AFEM_CUBES_D(kCubesV | 8) AFEM_CUBES_D(kCubesV | 2)
+      AFEM_CUBES_D(kCubesV | 8) AFEM_CUBES_D(kCubesV | 2) AFEM_CUBES_D(kCubesV | 512)
 #undef AFEM_CUBES_D
       default: break;
     }

@@ -1079,7 +1079,9 @@ __global__ __launch_bounds__(kThreads) void k_cg_update_b3(int64_t nb, const dou
 // p = z + beta p: reads x, z, p, writes x, p) -- 80 B per row instead of the
 // 88 of k_cg_update + k_cg_dir; the same operations on the same values.
 // V2: two rows per thread and access (16-B loads / stores per lane)
-template <bool V2>
+// V2: 16-B accesses (two rows per access); U2 (with V2): two such accesses per
+// thread and iteration, [i] and [i + stride] (more loads in flight)
+template <bool V2, bool U2 = false>
 __global__ __launch_bounds__(kThreads) void k_cg_update_rz(int64_t n, const double* __restrict__ scal, int par,
                                                            double* __restrict__ r, const double* __restrict__ q,
                                                            double* __restrict__ z, const double* __restrict__ dinv,
@@ -1089,7 +1091,43 @@ __global__ __launch_bounds__(kThreads) void k_cg_update_rz(int64_t n, const doub
   const double alpha = (pq != 0.0) ? rz / pq : 0.0;
   double s = 0.0;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
-  if constexpr (V2) {
+  if constexpr (V2 && U2) {
+    double2* r2 = reinterpret_cast<double2*>(r);
+    double2* z2 = reinterpret_cast<double2*>(z);
+    const double2* q2 = reinterpret_cast<const double2*>(q);
+    const double2* d2 = reinterpret_cast<const double2*>(dinv);
+    const int64_t m = n >> 1;
+    for (int64_t i = t0; i < m; i += 2 * st) {
+      const bool two = i + st < m;
+      double2 ra = r2[i], rb = two ? r2[i + st] : make_double2(0.0, 0.0);
+      const double2 qa = q2[i], qb = two ? q2[i + st] : make_double2(0.0, 0.0);
+      const double2 da = d2[i], db = two ? d2[i + st] : make_double2(0.0, 0.0);
+      ra.x = ra.x - alpha * qa.x;
+      ra.y = ra.y - alpha * qa.y;
+      rb.x = rb.x - alpha * qb.x;
+      rb.y = rb.y - alpha * qb.y;
+      const double2 za = make_double2(ra.x * da.x, ra.y * da.y), zb = make_double2(rb.x * db.x, rb.y * db.y);
+      r2[i] = ra;
+      z2[i] = za;
+      if (two) {
+        r2[i + st] = rb;
+        z2[i + st] = zb;
+      }
+      s += ra.x * za.x;
+      s += ra.y * za.y;
+      s += rb.x * zb.x;
+      s += rb.y * zb.y;
+    }
+    if ((n & 1) && t0 == 0) {
+      const int64_t i = n - 1;
+      double ri = r[i] - alpha * q[i];
+      r[i] = ri;
+      double zi = ri * dinv[i];
+      z[i] = zi;
+      s += ri * zi;
+    }
+  }
+  else if constexpr (V2) {
     double2* r2 = reinterpret_cast<double2*>(r);
     double2* z2 = reinterpret_cast<double2*>(z);
     const double2* q2 = reinterpret_cast<const double2*>(q);
@@ -1126,7 +1164,7 @@ __global__ __launch_bounds__(kThreads) void k_cg_update_rz(int64_t n, const doub
   double bs = block_sum(s);
   if (threadIdx.x == 0) partial[blockIdx.x] = bs;
 }
-template <bool V2>
+template <bool V2, bool U2 = false>
 __global__ __launch_bounds__(kThreads) void k_cg_dir_x(int64_t n, const double* __restrict__ scal, int par,
                                                        double* __restrict__ x, const double* __restrict__ z,
                                                        double* __restrict__ p)
@@ -1135,7 +1173,36 @@ __global__ __launch_bounds__(kThreads) void k_cg_dir_x(int64_t n, const double* 
   const double alpha = (pq != 0.0) ? rz_old / pq : 0.0;
   const double beta = (rz_old != 0.0) ? rz_new / rz_old : 0.0;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
-  if constexpr (V2) {
+  if constexpr (V2 && U2) {
+    double2* x2 = reinterpret_cast<double2*>(x);
+    double2* p2 = reinterpret_cast<double2*>(p);
+    const double2* z2 = reinterpret_cast<const double2*>(z);
+    const int64_t m = n >> 1;
+    for (int64_t i = t0; i < m; i += 2 * st) {
+      const bool two = i + st < m;
+      const double2 pa = p2[i], za = z2[i];
+      double2 xa = x2[i];
+      const double2 pb = two ? p2[i + st] : make_double2(0.0, 0.0), zb = two ? z2[i + st] : make_double2(0.0, 0.0);
+      double2 xb = two ? x2[i + st] : make_double2(0.0, 0.0);
+      xa.x += alpha * pa.x;
+      xa.y += alpha * pa.y;
+      xb.x += alpha * pb.x;
+      xb.y += alpha * pb.y;
+      x2[i] = xa;
+      p2[i] = make_double2(za.x + beta * pa.x, za.y + beta * pa.y);
+      if (two) {
+        x2[i + st] = xb;
+        p2[i + st] = make_double2(zb.x + beta * pb.x, zb.y + beta * pb.y);
+      }
+    }
+    if ((n & 1) && t0 == 0) {
+      const int64_t i = n - 1;
+      const double pi = p[i];
+      x[i] += alpha * pi;
+      p[i] = z[i] + beta * pi;
+    }
+  }
+  else if constexpr (V2) {
     double2* x2 = reinterpret_cast<double2*>(x);
     double2* p2 = reinterpret_cast<double2*>(p);
     const double2* z2 = reinterpret_cast<const double2*>(z);
@@ -1954,6 +2021,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   // AFEM_CG_VEC2=0: one row per thread and access in the vector kernels (variant)
   const char* v2e = variant("AFEM_CG_VEC2");
   const bool vec2 = !(v2e && atoi(v2e) == 0);
+  const bool vec4 = v2e && atoi(v2e) == 2;  // AFEM_CG_VEC2=2: two 16-B accesses per thread and iteration
   auto rest_of_iteration = [&](int par, bool with_spmv) {
     if (with_spmv)
       launch_spmv(ctx, pl, n, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p, ls.csr_nnz);
@@ -1971,7 +2039,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
       hipLaunchKernelGGL(k_cg_update_b3, dim3(vb3), dim3(kThreads), 0, ctx.stream, nb3, scal, par, ls.sol.p, ls.p.p,
                          ls.r.p, ls.q.p, ls.z.p, ls.binv.p, ls.partial.p);
     else
-      hipLaunchKernelGGL(vec2 ? k_cg_update_rz<true> : k_cg_update_rz<false>, dim3(vb), dim3(kThreads), 0, ctx.stream,
+      hipLaunchKernelGGL(vec4 ? (k_cg_update_rz<true, true>) : vec2 ? (k_cg_update_rz<true>) : (k_cg_update_rz<false>), dim3(vb), dim3(kThreads), 0, ctx.stream,
                          n, scal, par, ls.r.p, ls.q.p, ls.z.p, ls.dinv.p, ls.partial.p);
     AFEM_LAUNCHED();
     reduce_to(ctx, ls.partial.p, blk3 ? vb3 : vb, scal + (par ^ 1));
@@ -1979,7 +2047,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     if (use_mg || blk3)
       hipLaunchKernelGGL(k_cg_dir, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.z.p, ls.p.p);
     else
-      hipLaunchKernelGGL(vec2 ? k_cg_dir_x<true> : k_cg_dir_x<false>, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal,
+      hipLaunchKernelGGL(vec4 ? (k_cg_dir_x<true, true>) : vec2 ? (k_cg_dir_x<true>) : (k_cg_dir_x<false>), dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal,
                          par, ls.sol.p, ls.z.p, ls.p.p);
     AFEM_LAUNCHED();
   };
