@@ -67,7 +67,8 @@ class FunctorPlan(ctypes.Structure):
                 ("ordered_per_block", ctypes.c_int32), ("lattice", ctypes.c_int32), ("units", ctypes.c_void_p),
                 ("stage_ptr", ctypes.c_void_p), ("layer_rows", ctypes.c_void_p), ("entries", ctypes.c_void_p),
                 ("entries2", ctypes.c_void_p), ("rows", ctypes.c_void_p), ("values", ctypes.c_void_p),
-                ("stream", ctypes.c_void_p)]
+                ("stream", ctypes.c_void_p), ("patterns", ctypes.c_void_p), ("n_patterns", ctypes.c_int64),
+                ("packed", ctypes.c_int32), ("reserved0", ctypes.c_int32)]
 
 
 class Csr32View(ctypes.Structure):

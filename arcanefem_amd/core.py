@@ -301,7 +301,8 @@ class BSRFormat:
         p = C.FunctorPlan()
         call("afem_bsr_functor_plan", self.h, ctypes.byref(p))
         return {k: getattr(p, k) for k, _ in p._fields_ if not k in
-                ("units", "stage_ptr", "layer_rows", "entries", "entries2", "rows", "values", "stream")}
+                ("units", "stage_ptr", "layer_rows", "entries", "entries2", "rows", "values", "stream",
+                 "patterns", "reserved0")}
 
     def download(self):
         """Block arrays: rows[n+1] int64, columns[nnz] int32, values[nnz*k*k]."""

@@ -319,7 +319,10 @@ struct FunctorPlan {
   DevBuf<afem_functor_unit> units;
   DevBuf<int64_t> stage_ptr;   // [n_stages + 1]
   DevBuf<int32_t> layer_rows;  // [n_stages * rl]
-  DevBuf<uint32_t> ent, ent2;  // compact: 4 u32 per entry; wide: 4 u32 slots + 2 u32 (cell, pos)
+  DevBuf<uint32_t> ent, ent2;  // compact: 4 u32 per entry; wide: 4 u32 slots + 2 u32 (cell, pos); packed: 2 u32
+  int packed = 0;
+  int64_t n_patterns = 0;
+  DevBuf<uint32_t> patterns;   // packed: 4 u32 per pattern {0, slots 0|1, slots 2|3, positions}
 };
 void functor_plan_build(struct Bsr& b);
 

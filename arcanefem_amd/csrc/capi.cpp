@@ -662,6 +662,10 @@ int afem_bsr_functor_plan(afem_bsr* b, afem_functor_plan* p)
   p->rows = b->s.row_ptr.p;
   p->values = b->values.p;
   p->stream = (void*)b->mesh->ctx->stream;
+  p->patterns = P.packed ? P.patterns.p : nullptr;
+  p->n_patterns = P.n_patterns;
+  p->packed = P.packed;
+  p->reserved0 = 0;
   API_END
 }
 

@@ -205,8 +205,9 @@ struct CubeCanon {
 // process, settled): 0.520 / 4.53 ms with none, 0.465 / 4.20 with 16 | 32 | 64;
 // adding 128 costs 5.6 % on the box and 11 % on the random arrays (r05h:
 // scattered 8-B RHS stores and 120-B rows are worse non-temporal); 256 on top
-// of 16 | 32 | 64: C2 0.4632 -> 0.4608 ms, C4 4.194 -> 4.097 ms (r05i).
-constexpr int kCubesV = 16 | 32 | 64 | 256;
+// of 16 | 32 | 64: C2 0.4632 -> 0.4608 ms, C4 4.194 -> 4.097 ms (r05i); 512:
+// random-numbered arrays (canonical path) 1.581 -> 1.538 ms (r05k).
+constexpr int kCubesV = 16 | 32 | 64 | 256 | 512;
 
 // register budget: 64-row planes + one coordinate layer = 17.3 KB of LDS, 9
 // waves per CU, so 2 per SIMD whatever the registers (256 VGPRs, no spill);
@@ -935,7 +936,7 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
                  : &k_assemble_cubes<64, true, true, true, false, true, false, D>;                                  \
     break;
       AFEM_CUBES_D(0) AFEM_CUBES_D(112) AFEM_CUBES_D(kCubesV | 1) AFEM_CUBES_D(kCubesV | 4)
-      AFEM_CUBES_D(kCubesV | 8) AFEM_CUBES_D(kCubesV | 2) AFEM_CUBES_D(kCubesV | 512)
+      AFEM_CUBES_D(kCubesV | 8) AFEM_CUBES_D(kCubesV | 2) AFEM_CUBES_D(kCubesV & ~512)
 #undef AFEM_CUBES_D
       default: break;
     }

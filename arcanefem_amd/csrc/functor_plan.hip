@@ -239,6 +239,120 @@ __global__ void k_fill_entries(int64_t n_ent, const unsigned long long* __restri
   }
 }
 
+// packed entries: the distinct (slots 0|1, slots 2|3, positions) words of the
+// compact entries, numbered in the order (positions with vertex 0's byte
+// first, then slots: two stable radix passes, slots first) -- the order of
+// the stage sort's lane key, so that the 64 translates of one cell a wave
+// evaluates together read consecutive patterns (a few cache lines, not 64);
+// an entry keeps its cell and the number
+__global__ void k_pat_key_slots(int64_t n, const uint32_t* __restrict__ ent, unsigned long long* __restrict__ key,
+                                int32_t* __restrict__ idx)
+{
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  key[e] = (unsigned long long)ent[4 * e + 1] | (unsigned long long)ent[4 * e + 2] << 32;
+  idx[e] = (int32_t)e;
+}
+
+__global__ void k_pat_key_pos(int64_t n, const uint32_t* __restrict__ ent, const int32_t* __restrict__ idx,
+                              uint32_t* __restrict__ key)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  key[i] = __builtin_bswap32(ent[4 * (int64_t)idx[i] + 3]);
+}
+
+__global__ void k_pat_flags(int64_t n, const uint32_t* __restrict__ ent, const int32_t* __restrict__ idx,
+                            int32_t* __restrict__ flag)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int f = 1;
+  if (i > 0) {
+    const int64_t a = idx[i], b = idx[i - 1];
+    f = ent[4 * a + 1] != ent[4 * b + 1] || ent[4 * a + 2] != ent[4 * b + 2] || ent[4 * a + 3] != ent[4 * b + 3];
+  }
+  flag[i] = f;
+}
+
+__global__ void k_pat_emit(int64_t n, const uint32_t* __restrict__ ent, const int32_t* __restrict__ idx,
+                           const int32_t* __restrict__ flag, const int32_t* __restrict__ pid,
+                           uint32_t* __restrict__ patterns, uint32_t* __restrict__ packed)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t e = idx[i];
+  const int32_t q = pid[i] - 1;
+  const uint4 w = reinterpret_cast<const uint4*>(ent)[e];
+  if (flag[i]) reinterpret_cast<uint4*>(patterns)[q] = make_uint4(0u, w.y, w.z, w.w);
+  reinterpret_cast<uint2*>(packed)[e] = make_uint2(w.x, (uint32_t)q);
+}
+
+// Replaces the compact entries by packed ones (AFEM_FUNCTOR_PACKED=1: always;
+// =auto: when the table, 16 B per pattern, is at most half of the 8 B per
+// entry saved and within 4 MB, one XCD's L2).  Off by default: C2 has 2901
+// patterns and 0.64 GB less traffic per launch, but the pattern gather -- one
+// more 64-lane, 64-line load per evaluation group, prefetched a group ahead --
+// costs more than the bytes save (r05o, one process: module element 1.83 vs
+// 1.77 ms, lean element 1.47 vs 1.30 ms).
+void pack_entries(Ctx& ctx, FunctorPlan& P)
+{
+  const int64_t n = P.n_entries;
+  const char* pe = variant("AFEM_FUNCTOR_PACKED");
+  if (P.wide || n <= 0 || !pe || (std::string(pe) != "1" && std::string(pe) != "auto")) return;
+  DevBuf<unsigned long long> k64, k64s;
+  DevBuf<int32_t> idx, idx1;
+  k64.alloc(n);
+  k64s.alloc(n);
+  idx.alloc(n);
+  idx1.alloc(n);
+  hipLaunchKernelGGL(k_pat_key_slots, dim3(grid_for(n, 256)), dim3(256), 0, ctx.stream, n, P.ent.p, k64.p, idx.p);
+  AFEM_LAUNCHED();
+  size_t tb = 0;
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k64.p, k64s.p, idx.p, idx1.p, (int)n, 0, 64, ctx.stream));
+  DevBuf<unsigned char> tmp;
+  tmp.alloc(tb > 0 ? tb : 1);
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k64.p, k64s.p, idx.p, idx1.p, (int)n, 0, 64, ctx.stream));
+  k64.reset();
+  k64s.reset();
+  DevBuf<uint32_t> k32, k32s;
+  k32.alloc(n);
+  k32s.alloc(n);
+  hipLaunchKernelGGL(k_pat_key_pos, dim3(grid_for(n, 256)), dim3(256), 0, ctx.stream, n, P.ent.p, idx1.p, k32.p);
+  AFEM_LAUNCHED();
+  size_t tb2 = 0;
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, k32.p, k32s.p, idx1.p, idx.p, (int)n, 0, 32, ctx.stream));
+  if (tb2 > tb) tmp.alloc(tb2);
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb2, k32.p, k32s.p, idx1.p, idx.p, (int)n, 0, 32, ctx.stream));
+  k32.reset();
+  k32s.reset();
+  // idx: entries in (positions, slots) order
+  DevBuf<int32_t>& flag = idx1;
+  hipLaunchKernelGGL(k_pat_flags, dim3(grid_for(n, 256)), dim3(256), 0, ctx.stream, n, P.ent.p, idx.p, flag.p);
+  AFEM_LAUNCHED();
+  DevBuf<int32_t> pid;
+  pid.alloc(n);
+  size_t tb3 = 0;
+  AFEM_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb3, flag.p, pid.p, (int)n, ctx.stream));
+  if (tb3 > tmp.bytes()) tmp.alloc(tb3);
+  AFEM_HIP(hipcub::DeviceScan::InclusiveSum(tmp.p, tb3, flag.p, pid.p, (int)n, ctx.stream));
+  int32_t n_pat = 0;
+  AFEM_HIP(hipMemcpyAsync(&n_pat, pid.p + (n - 1), sizeof(n_pat), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  P.n_patterns = n_pat;
+  const bool force = pe && std::string(pe) == "1";
+  if (!force && ((int64_t)n_pat > n / 4 || (int64_t)n_pat * 16 > (4 << 20))) return;
+  P.patterns.alloc((size_t)n_pat * 4);
+  DevBuf<uint32_t> packed;
+  packed.alloc((size_t)n * 2);
+  hipLaunchKernelGGL(k_pat_emit, dim3(grid_for(n, 256)), dim3(256), 0, ctx.stream, n, P.ent.p, idx.p, flag.p, pid.p,
+                     P.patterns.p, packed.p);
+  AFEM_LAUNCHED();
+  ctx.sync();
+  std::swap(P.ent, packed);
+  P.packed = 1;
+}
+
 // unit records; flag 1 when every layer's lanes 8q..8q+7 hold a prefix of
 // consecutive rows (their values are one contiguous range: coalesced stores)
 __global__ void k_units(int64_t n_units, UnitGeom g, const int32_t* __restrict__ lrows, int runs_ok,
@@ -352,6 +466,7 @@ void build_entries(Ctx& ctx, Bsr& b, const UnitGeom& g, const DevBuf<int64_t>& n
   AFEM_HIP(hipMemcpyAsync(&herr, err.p, sizeof(herr), hipMemcpyDeviceToHost, ctx.stream));
   ctx.sync();
   AFEM_REQUIRE(herr == 0, AFEM_ERR_STATE, "functor plan: a cell couples nodes outside the sparsity");
+  pack_entries(ctx, P);
 }
 
 }  // namespace

@@ -564,24 +564,27 @@ def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2, settle_ms=150.0
     # what k_assemble_units must move: its plan entries, the functor's own
     # connectivity read per evaluation (4 x i32: the module's lambda reads
     # cn_cv itself), coordinates, row offsets, values
-    ent_b = 24 if plan["wide"] else 16
-    kmin = (ent_b + 16) * plan["n_entries"] + 24 * mesh.n_nodes + 8 * (mesh.n_own_nodes + 1) + 8 * nnz
+    ent_b = 24 if plan["wide"] else 8 if plan["packed"] else 16
+    kmin = ((ent_b + 16) * plan["n_entries"] + 16 * plan["n_patterns"] * plan["packed"] + 24 * mesh.n_nodes
+            + 8 * (mesh.n_own_nodes + 1) + 8 * nnz)
+    fmt = "wide" if plan["wide"] else "packed" if plan["packed"] else "compact"
     out = {"config": f"{what} ({mesh.n_own_nodes} DoF, {mesh.n_cells} tets): assembleBilinear(the Poisson "
                      f"module's tet4 element lambda) through the generic element-functor entry, values overwritten",
            "dof": int(mesh.n_own_nodes), "value": round(mesh.n_own_nodes / (kms * 1e-3) / 1e6, 1),
            "unit": "MDoF/s (assembly kernel)", "kernel_ms": round(kms, 4), "kernel_ms_all": [round(x, 4) for x in ks],
-           "roofline": {"bound": "hbm", "kernel": "k_assemble_units<4,1,compact,PoissonTet4>",
+           "roofline": {"bound": "hbm", "kernel": f"k_assemble_units<4,1,{fmt},PoissonTet4>",
                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(ab),
                         "bytes_kernel_min": int(kmin),
-                        "bytes_kernel_min_note": "plan entries + the functor's connectivity reads per evaluation "
-                                                 "+ coordinates + row offsets + values",
+                        "bytes_kernel_min_note": "plan entries (+ pattern table when packed) + the functor's "
+                                                 "connectivity reads per evaluation + coordinates + row offsets "
+                                                 "+ values",
                         "frac_kernel_min": round(kmin / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "kernel_ms": round(kms, 4)},
            "settle_steps": settle_steps,
            "evaluations_per_cell": round(plan["n_entries"] / mesh.n_cells, 4),
            "plan": {k: int(plan[k]) for k in ("n_units", "n_stages", "n_entries", "rows_per_layer", "width", "nbuf",
-                                              "wide", "lattice")},
+                                              "wide", "lattice", "packed", "n_patterns")},
            "plan_build_ms": round(plan_ms, 1),
            "atomic_kernel_ms": round(kam, 4), "atomic_frac": round(ab / (kam * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "vs_fixed_physics_max_rel": float(np.abs(vals_u - vals_f).max() / np.abs(vals_f).max())}

@@ -331,11 +331,20 @@ typedef struct afem_functor_plan {
   const afem_functor_unit* units; /* device [n_units] */
   const int64_t* stage_ptr;  /* device [n_stages+1]: entries of stage s are [stage_ptr[s], stage_ptr[s+1]) */
   const int32_t* layer_rows; /* device [n_stages*rows_per_layer]: row of (stage, lane) or -1 */
-  const uint32_t* entries;   /* device, 16 B per entry (see above) */
+  const uint32_t* entries;   /* device, 16 B per entry (see above; 8 B when packed) */
   const uint32_t* entries2;  /* device, wide format: 8 B per entry (cell, positions); else NULL */
   const int64_t* rows;       /* device [n_rows+1] block-row offsets */
   double* values;            /* device, the matrix's values */
   void* stream;              /* hipStream_t of the structure's context */
+  /* packed entries (compact plans whose entries repeat few distinct slot /
+   * position words, e.g. lattice meshes in a lexicographic numbering): 8 B per
+   * entry {cell, pattern}, the pattern's 4 u32 {0, slots 0|1, slots 2|3,
+   * positions} in patterns[4 * pattern] -- the compact entry with the cell
+   * moved out */
+  const uint32_t* patterns;  /* device [n_patterns * 4] when packed, else NULL */
+  int64_t n_patterns;
+  int32_t packed;            /* 1: entries are 8 B {cell, pattern} */
+  int32_t reserved0;
 } afem_functor_plan;
 int afem_bsr_functor_plan(afem_bsr* bsr, afem_functor_plan* plan);
 /* BSRFormat::toLinearSystem with use_csr (femutils/BSRFormat.h:414-430 through

@@ -204,9 +204,22 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
  * 16 KB of LDS per unit leave 2-3 waves per SIMD).  The scatter order stays
  * the one-cell-at-a-time order (entry e's adds, then e + 64's, ...): the same
  * bits for every UN. */
-template <int NV, int K, bool WIDE, int UN, class F>
-__global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f, int sr, int swz, int overwrite)
+#ifndef AFEM_GENERIC_WAVES
+#define AFEM_GENERIC_WAVES 0
+#endif
+#if AFEM_GENERIC_WAVES > 0
+#define AFEM_GENERIC_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(AFEM_GENERIC_WAVES)))
+#else
+#define AFEM_GENERIC_WAVES_ATTR
+#endif
+template <int NV, int K, bool WIDE, bool PK, int SR, int UN, class F>
+__global__ void __launch_bounds__(64) AFEM_GENERIC_WAVES_ATTR k_assemble_units(afem_functor_plan p, F f, int sr_arg, int swz_arg,
+                                                                               int overwrite)
 {
+  // SR > 0: planes of SR rows, no swizzle, compiled in (the LDS address of an
+  // add is one shift-add of its slot); 0: the arguments
+  const int sr = SR ? SR : sr_arg;
+  const int swz = SR ? 0 : swz_arg;
   extern __shared__ __align__(16) double acc[];
   constexpr int KK = K * K;
   const int lane = threadIdx.x;
@@ -241,7 +254,11 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
         if (e < e1) {
           if (have) {
             m[v] = nxt[v];
-            m2[v] = nxt2[v];
+            if (WIDE || PK) m2[v] = nxt2[v];
+          }
+          else if (PK) {  // a chain break: entry and pattern in place
+            m2[v] = reinterpret_cast<const uint2*>(p.entries)[e];
+            m[v] = reinterpret_cast<const uint4*>(p.patterns)[m2[v].y];
           }
           else {
             m[v] = reinterpret_cast<const uint4*>(p.entries)[e];
@@ -249,66 +266,78 @@ __global__ void __launch_bounds__(64) k_assemble_units(afem_functor_plan p, F f,
           }
         }
       }
-      {
-        const bool more = eb + 64 * UN < e1;
-        const int64_t nb = more ? eb + 64 * UN : e1, lim = more ? e1 : e2;
-        nxt_base = lim > nb ? nb : -1;
+      const bool more = eb + 64 * UN < e1;
+      const int64_t nb = more ? eb + 64 * UN : e1, lim = more ? e1 : e2;
+      nxt_base = lim > nb ? nb : -1;
 #pragma unroll
-        for (int v = 0; v < UN; ++v) {
-          const int64_t en = nb + 64 * v + lane;
-          if (en < lim) {
+      for (int v = 0; v < UN; ++v) {
+        const int64_t en = nb + 64 * v + lane;
+        if (en < lim) {
+          if (PK) {
+            nxt2[v] = reinterpret_cast<const uint2*>(p.entries)[en];
+          }
+          else {
             nxt[v] = reinterpret_cast<const uint4*>(p.entries)[en];
             if (WIDE) nxt2[v] = reinterpret_cast<const uint2*>(p.entries2)[en];
           }
         }
       }
-      if (eb + lane >= e1) continue;  // no entry for this lane (then none of its later ones either)
-      uint32_t cell[UN], pos[UN], sl[UN][4];
+      if (eb + lane < e1) {  // else no entry for this lane (then none of its later ones either)
+        uint32_t cell[UN], pos[UN], sl[UN][4];
 #pragma unroll
-      for (int v = 0; v < UN; ++v) {
-        if (WIDE) {
-          sl[v][0] = m[v].x;
-          sl[v][1] = m[v].y;
-          sl[v][2] = m[v].z;
-          sl[v][3] = m[v].w;
-          cell[v] = m2[v].x;
-          pos[v] = m2[v].y;
-        }
-        else {
-          cell[v] = m[v].x;
-          sl[v][0] = m[v].y & 0xffffu;
-          sl[v][1] = m[v].y >> 16;
-          sl[v][2] = m[v].z & 0xffffu;
-          sl[v][3] = m[v].z >> 16;
-          pos[v] = m[v].w;
-        }
-      }
-      // a lane past the stage's end evaluates its first cell again (pure
-      // functor) and scatters nothing for it: no branch between the functors
-      decltype(f(0)) ke[UN];
-#pragma unroll
-      for (int v = 0; v < UN; ++v) ke[v] = f((int32_t)(eb + 64 * v + lane < e1 ? cell[v] : cell[0]));
-#pragma unroll
-      for (int v = 0; v < UN; ++v) {
-        if (eb + 64 * v + lane >= e1) break;
-#pragma unroll
-        for (int a = 0; a < NV; ++a) {
-          const uint32_t pa = (pos[v] >> (8 * a)) & 0xffu;
-          if (!(pa & 0x80u)) continue;
-          double* const bufp = acc + ((pa >> 6) & 1u) * bufsz;
-          const int row = (int)(pa & 63u);
-#pragma unroll
-          for (int b = 0; b < NV; ++b) {
-            const int s = WIDE ? (int)((sl[v][a] >> (8 * b)) & 0xffu) : (int)((sl[v][a] >> (4 * b)) & 0xfu);
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-#pragma unroll
-              for (int jj = 0; jj < K; ++jj) {
-                const int pl = s * KK + i * K + jj;
-                atomicAdd(bufp + pl * sr + (row ^ (pl & swz)), (double)ke[v](K * a + i, K * b + jj));
-              }
+        for (int v = 0; v < UN; ++v) {
+          if (WIDE) {
+            sl[v][0] = m[v].x;
+            sl[v][1] = m[v].y;
+            sl[v][2] = m[v].z;
+            sl[v][3] = m[v].w;
+            cell[v] = m2[v].x;
+            pos[v] = m2[v].y;
+          }
+          else {
+            cell[v] = PK ? m2[v].x : m[v].x;
+            sl[v][0] = m[v].y & 0xffffu;
+            sl[v][1] = m[v].y >> 16;
+            sl[v][2] = m[v].z & 0xffffu;
+            sl[v][3] = m[v].z >> 16;
+            pos[v] = m[v].w;
           }
         }
+        // a lane past the stage's end evaluates its first cell again (pure
+        // functor) and scatters nothing for it: no branch between the functors
+        decltype(f(0)) ke[UN];
+#pragma unroll
+        for (int v = 0; v < UN; ++v) ke[v] = f((int32_t)(eb + 64 * v + lane < e1 ? cell[v] : cell[0]));
+#pragma unroll
+        for (int v = 0; v < UN; ++v) {
+          if (eb + 64 * v + lane >= e1) break;
+#pragma unroll
+          for (int a = 0; a < NV; ++a) {
+            const uint32_t pa = (pos[v] >> (8 * a)) & 0xffu;
+            if (!(pa & 0x80u)) continue;
+            double* const bufp = acc + ((pa >> 6) & 1u) * bufsz;
+            const int row = (int)(pa & 63u);
+#pragma unroll
+            for (int b = 0; b < NV; ++b) {
+              const int s = WIDE ? (int)((sl[v][a] >> (8 * b)) & 0xffu) : (int)((sl[v][a] >> (4 * b)) & 0xfu);
+#pragma unroll
+              for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int jj = 0; jj < K; ++jj) {
+                  const int pl = s * KK + i * K + jj;
+                  atomicAdd(bufp + pl * sr + (row ^ (pl & swz)), (double)ke[v](K * a + i, K * b + jj));
+                }
+            }
+          }
+        }
+      }
+      // packed: the next group's patterns (L2-resident table), issued after
+      // this group's work so that its entries have arrived: the dependent load
+      // hides behind the next group's functors like the entries do
+      if (PK) {
+#pragma unroll
+        for (int v = 0; v < UN; ++v)
+          if (nb + 64 * v + lane < lim) nxt[v] = reinterpret_cast<const uint4*>(p.patterns)[nxt2[v].y];
       }
     }
     unit_lds_order();
@@ -427,10 +456,18 @@ int assemble_bilinear_unrolled(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate,
   if (p.n_units == 0) return AFEM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(p.stream);
   const int ow = mode == Mode::Overwrite ? 1 : 0;
+  const dim3 grid((unsigned)p.n_units);
+  const bool dense64 = sr == 64 && swz == 0;  // lattice columns of 8 x 8 rows (k = 1)
   if (p.wide)
-    hipLaunchKernelGGL((k_assemble_units<NV, K, true, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, sr, swz, ow);
+    hipLaunchKernelGGL((k_assemble_units<NV, K, true, false, 0, UN, F>), grid, dim3(64), lds, st, p, f, sr, swz, ow);
+  else if (p.packed && dense64)
+    hipLaunchKernelGGL((k_assemble_units<NV, K, false, true, 64, UN, F>), grid, dim3(64), lds, st, p, f, sr, swz, ow);
+  else if (p.packed)
+    hipLaunchKernelGGL((k_assemble_units<NV, K, false, true, 0, UN, F>), grid, dim3(64), lds, st, p, f, sr, swz, ow);
+  else if (dense64)
+    hipLaunchKernelGGL((k_assemble_units<NV, K, false, false, 64, UN, F>), grid, dim3(64), lds, st, p, f, sr, swz, ow);
   else
-    hipLaunchKernelGGL((k_assemble_units<NV, K, false, UN, F>), dim3((unsigned)p.n_units), dim3(64), lds, st, p, f, sr, swz, ow);
+    hipLaunchKernelGGL((k_assemble_units<NV, K, false, false, 0, UN, F>), grid, dim3(64), lds, st, p, f, sr, swz, ow);
   return hipGetLastError() == hipSuccess ? AFEM_OK : AFEM_ERR_HIP;
 }
 

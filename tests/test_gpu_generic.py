@@ -214,3 +214,34 @@ def test_unit_kernel_evaluations_per_cell(ctx, variant):
     assert ratio < 1.0 + 1 / 8 + 1 / 8 + 1 / 16, ratio
     bsr.close()
     mesh.close()
+
+
+@pytest.mark.parametrize("which,k", [("box", 1), ("box", 3), ("slab", 1), ("arrays_random", 1), ("sphere", 1)])
+def test_packed_entries_bitwise(ctx, variant, which, k):
+    """Packed plan entries (8 B {cell, pattern} + the table of distinct slot /
+    position words) give the bits of the 16-B entries: the same cells in the
+    same order, the same LDS adds.  Forced on (AFEM_FUNCTOR_PACKED=1: the
+    format is opt-in, and small meshes' boundary rows make many patterns)."""
+    import arcanefem_amd as af
+    import generic_example as gx
+
+    kind = gx.POISSON if k == 1 else gx.ELASTICITY
+    vals = {}
+    for pk in ("0", "1"):
+        variant("AFEM_FUNCTOR_PACKED", pk)
+        mesh = _mesh(ctx, which)
+        bsr = af.BSRFormat(mesh, k).initialize(True)
+        bsr.computeSparsity()
+        plan = bsr.functor_plan()
+        assert plan["packed"] == (1 if pk == "1" and not plan["wide"] else 0), plan
+        if plan["packed"]:
+            assert 0 < plan["n_patterns"] <= plan["n_entries"]
+        gx.assemble(bsr, kind, gx.UNITS, overwrite=True, lam=LAM_, mu=MU_)
+        vals[pk] = bsr.download()[2]
+        if pk == "1":
+            _, _, ov = _oracle(mesh, k, True)
+            sc = np.abs(ov).max()
+            assert np.abs(vals[pk] - ov).max() <= 1e-12 * sc
+        bsr.close()
+        mesh.close()
+    assert np.array_equal(vals["0"], vals["1"])

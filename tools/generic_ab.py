@@ -61,7 +61,7 @@ for spec in sys.argv[3:]:
         first = v
     err = f"{err:.1e} bits-as-first {np.array_equal(v, first)}"
     print(f"{spec:40s} units {plan['n_units']:6d} rl {plan['rows_per_layer']:2d} evals/cell "
-          f"{plan['n_entries'] / mesh.n_cells:.3f} coalesced {plan.get('n_coalesced', -1)} | module {out[0]} | "
+          f"{plan['n_entries'] / mesh.n_cells:.3f} packed {plan['packed']} patterns {plan['n_patterns']} | module {out[0]} | "
           f"lean {out[1]} | err {err}", flush=True)
     for k, _ in kv:
         af.set_variant(k, None)
