@@ -116,7 +116,9 @@ class HostTransport(ctypes.Structure):
 class NewmarkParams(ctypes.Structure):
     _fields_ = [("E", ctypes.c_double), ("nu", ctypes.c_double), ("rho", ctypes.c_double), ("dt", ctypes.c_double),
                 ("body_force", ctypes.c_double * 3), ("penalty", ctypes.c_double), ("gamma", ctypes.c_double),
-                ("beta", ctypes.c_double)]
+                ("beta", ctypes.c_double), ("etam", ctypes.c_double), ("etak", ctypes.c_double),
+                ("alpm", ctypes.c_double), ("alpf", ctypes.c_double), ("scheme", ctypes.c_int32),
+                ("reserved0", ctypes.c_int32)]
 
 
 P = ctypes.c_void_p

@@ -552,10 +552,14 @@ struct Elastodynamics {
   Ctx* ctx = nullptr;
   Comm* comm = nullptr;
   afem_newmark_params p{};
-  double lambda = 0, mu2 = 0, gamma = 0.5, beta = 0.25, c0 = 0, c3 = 0, c4 = 0;
-  Bsr K;                  // block-3, per-row (CSR) layout: values = c0 M + K
+  double lambda = 0, mu2 = 0, gamma = 0.5, beta = 0.25;
+  double c[11] = {};      // modules/elastodynamics/FemModule.cc:255-290 c0 .. c10
+  bool damped = false;    // a stiffness term on the RHS (etak != 0 or alpf != 0)
+  Bsr K;                  // block-3, per-row (CSR) layout: values = c0 M + K(c1, c2)
   DevBuf<double> mvals;   // consistent mass on K's structure (CSR order)
+  DevBuf<double> klvals, kmvals;  // damped: K(lambda = 1, 2 mu = 0) and K(0, 1) on K's structure
   LinearSystem ls, lsm;   // the solve, and the mass operator's SpMV
+  LinearSystem lsl, lsu;  // damped: the SpMVs of klvals / kmvals
   DevBuf<double> U, V, A, W, MW;
   DevBuf<int32_t> fixed;  // clamped DoFs
   DevBuf<int32_t> imp_ids;  // imposed displacements (afem_elastodynamics_set_dirichlet): owned DoFs

@@ -11,8 +11,11 @@
 // clamped DoFs are imposed by penalty, the Jacobi-PCG solves (halo exchange
 // and dot-product sums over ranks when a communicator is attached; warm
 // started from the Newmark predictor) and the Newmark update runs on the
-// device.  Rayleigh damping (etam, etak) and the
-// generalized-alpha variant are not implemented.
+// device.  Rayleigh damping (etam, etak) and the generalized-alpha scheme
+// (alpm, alpf) follow the module's constants c0 .. c10 (:255-290): the LHS is
+// c0 M + K(c1, c2) and the RHS adds K(lambda = 1) (-c5 U + c7 V + c8 A) +
+// K(2 mu = 1) (-c6 U + c9 V + c10 A) (:842-862) -- two more operators on the
+// same structure, assembled once.
 #include <cmath>
 #include <map>
 #include <vector>
@@ -75,6 +78,49 @@ void init_ls(LinearSystem& ls, Ctx* ctx, int64_t n, int64_t n_cols)
 }
 }  // namespace
 
+// modules/elastodynamics/FemModule.cc:255-290: the Newmark-beta and
+// generalized-alpha constants with Rayleigh damping (etam, etak)
+void dyn_coefficients(Elastodynamics* d)
+{
+  const afem_newmark_params& p = d->p;
+  const double lambda = d->lambda, mu = 0.5 * d->mu2, rho = p.rho, dt = p.dt, etam = p.etam, etak = p.etak;
+  double* c = d->c;
+  if (p.scheme == 1) {
+    const double alpm = p.alpm, alpf = p.alpf;
+    const double gamma = 0.5 + alpf - alpm, beta = 0.25 * (gamma + 0.5) * (gamma + 0.5);
+    d->gamma = gamma;
+    d->beta = beta;
+    c[0] = rho * (1. - alpm) / (beta * dt * dt) + etam * rho * gamma * (1 - alpf) / beta / dt;
+    c[1] = lambda * (1. - alpf) + lambda * etak * gamma * (1. - alpf) / beta / dt;
+    c[2] = 2. * mu * (1. - alpf) + 2. * mu * etak * gamma * (1. - alpf) / beta / dt;
+    c[3] = rho * (1. - alpm) / beta / dt - etam * rho * (1 - gamma * (1 - alpf) / beta);
+    c[4] = rho * ((1. - alpm) * (1. - 2. * beta) / 2. / beta - alpm - etam * dt * (1. - alpf) * (1. - gamma / 2 / beta));
+    c[5] = lambda * alpf - lambda * etak * gamma * (1. - alpf) / beta / dt;
+    c[6] = 2 * mu * alpf - 2. * mu * etak * gamma * (1. - alpf) / beta / dt;
+    c[7] = etak * lambda * (gamma * (1. - alpf) / beta - 1);
+    c[8] = etak * lambda * dt * (1. - alpf) * ((1. - 2 * beta) / 2. / beta - (1. - gamma));
+    c[9] = etak * 2 * mu * (gamma * (1. - alpf) / beta - 1);
+    c[10] = etak * 2 * mu * dt * (1. - alpf) * ((1. - 2 * beta) / 2. / beta - (1. - gamma));
+  }
+  else {
+    const double gamma = p.gamma > 0 ? p.gamma : 0.5;
+    const double beta = p.beta > 0 ? p.beta : 0.25 * (gamma + 0.5) * (gamma + 0.5);
+    d->gamma = gamma;
+    d->beta = beta;
+    c[0] = rho / (beta * dt * dt) + etam * rho * gamma / beta / dt;
+    c[1] = lambda + lambda * etak * gamma / beta / dt;
+    c[2] = 2. * mu + 2. * mu * etak * gamma / beta / dt;
+    c[3] = rho / beta / dt - etam * rho * (1 - gamma / beta);
+    c[4] = rho * ((1. - 2. * beta) / 2. / beta - etam * dt * (1. - gamma / 2 / beta));
+    c[5] = -lambda * etak * gamma / beta / dt;
+    c[6] = -2. * mu * etak * gamma / beta / dt;
+    c[7] = etak * lambda * (gamma / beta - 1);
+    c[8] = etak * lambda * dt * ((1. - 2 * beta) / 2. / beta - (1. - gamma));
+    c[9] = etak * 2 * mu * (gamma / beta - 1);
+    c[10] = etak * 2 * mu * dt * ((1. - 2 * beta) / 2. / beta - (1. - gamma));
+  }
+}
+
 Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* prm, const int32_t* fixed_nodes,
                            int64_t n_fixed, int mem)
 {
@@ -83,6 +129,8 @@ Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* pr
     AFEM_REQUIRE(prm->dt > 0 && prm->E > 0 && prm->nu > -1.0 && prm->nu < 0.5 && prm->rho >= 0, AFEM_ERR_ARG,
                  "elastodynamics: bad material or time step");
     AFEM_REQUIRE(n_fixed == 0 || fixed_nodes, AFEM_ERR_ARG, "fixed_nodes is NULL");
+    AFEM_REQUIRE(prm->scheme == 0 || prm->scheme == 1, AFEM_ERR_ARG,
+                 "elastodynamics: scheme 0 (Newmark-beta) or 1 (generalized-alpha)");
     if (comm)
       AFEM_REQUIRE(comm_nranks(comm) == 1 ||
                        (mesh->st.valid && mesh->st.nranks == comm_nranks(comm) && mesh->st.rank == comm_rank(comm)) ||
@@ -98,14 +146,11 @@ Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* pr
       d->comm = comm;
       d->p = *prm;
       if (!(d->p.penalty > 0)) d->p.penalty = 1.0e30;  // modules/elasticity/Fem.axl:37-41
-      // modules/elastodynamics/FemModule.cc:130-134 (Lame) and :255-270 (Newmark, etam = etak = 0)
+      // modules/elastodynamics/FemModule.cc:130-134 (Lame) and :255-290 (time scheme)
       d->mu2 = (prm->E / (2 * (1 + prm->nu))) * 2;
       d->lambda = prm->E * prm->nu / ((1 + prm->nu) * (1 - 2 * prm->nu));
-      d->gamma = prm->gamma > 0 ? prm->gamma : 0.5;
-      d->beta = prm->beta > 0 ? prm->beta : 0.25 * (d->gamma + 0.5) * (d->gamma + 0.5);
-      d->c0 = prm->rho / (d->beta * prm->dt * prm->dt);
-      d->c3 = prm->rho / d->beta / prm->dt;
-      d->c4 = prm->rho * ((1.0 - 2.0 * d->beta) / 2.0 / d->beta);
+      dyn_coefficients(d);
+      d->damped = prm->etak != 0.0 || (prm->scheme == 1 && prm->alpf != 0.0);
       d->n = 3 * mesh->n_own;
       d->n_cols = 3 * mesh->n_nodes;
       // structure once; stiffness and mass share it
@@ -119,10 +164,25 @@ Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* pr
       std::swap(d->K.values, d->mvals);
       assemble_elasticity_tet(d->K, 0.0, 0.0, 1.0, nullptr, nullptr, 0);  // M (c0 = 1)
       std::swap(d->K.values, d->mvals);
+      if (d->damped) {  // the RHS's stiffness operators K(lambda = 1) and K(2 mu = 1)
+        d->klvals.alloc((size_t)d->K.s.nnz * 9);
+        d->kmvals.alloc((size_t)d->K.s.nnz * 9);
+        std::swap(d->K.values, d->klvals);
+        assemble_elasticity_tet(d->K, 1.0, 0.0, 0.0, nullptr, nullptr, 0);
+        std::swap(d->K.values, d->klvals);
+        std::swap(d->K.values, d->kmvals);
+        assemble_elasticity_tet(d->K, 0.0, 1.0, 0.0, nullptr, nullptr, 0);
+        std::swap(d->K.values, d->kmvals);
+      }
       bsr_expand_scalar(d->K, nullptr);  // scalar rows / columns of the block-3 CSR (shared)
       init_ls(d->ls, &ctx, d->n, d->n_cols);
       init_ls(d->lsm, &ctx, d->n, d->n_cols);
-      for (LinearSystem* l : { &d->ls, &d->lsm }) {
+      if (d->damped) {
+        init_ls(d->lsl, &ctx, d->n, d->n_cols);
+        init_ls(d->lsu, &ctx, d->n, d->n_cols);
+      }
+      for (LinearSystem* l : { &d->ls, &d->lsm, &d->lsl, &d->lsu }) {
+        if (!l->ctx) continue;  // lsl / lsu without damping
         l->has_csr = true;
         l->csr_n = d->n;
         l->csr_nnz = d->K.s.nnz * 9;
@@ -150,6 +210,12 @@ Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* pr
       d->lsm.csr_vals = d->mvals.p;
       halo_for(d->ls, d->comm, *mesh);
       halo_for(d->lsm, d->comm, *mesh);
+      if (d->damped) {
+        d->lsl.csr_vals = d->klvals.p;
+        d->lsu.csr_vals = d->kmvals.p;
+        halo_for(d->lsl, d->comm, *mesh);
+        halo_for(d->lsu, d->comm, *mesh);
+      }
       for (auto* b : { &d->U, &d->V, &d->A, &d->MW }) {
         b->alloc(d->n);
         AFEM_HIP(hipMemsetAsync(b->p, 0, b->bytes(), ctx.stream));
@@ -187,12 +253,21 @@ void dyn_step(Elastodynamics* d, afem_solve_stats* st)
     Ctx& ctx = *d->ctx;
     ctx.set_device();
     const double f[3] = { d->p.body_force[0], d->p.body_force[1], d->p.body_force[2] };
-    // LHS c0 M + K and the body force (rhs = f |K|/4), re-assembled on the fixed structure
-    assemble_elasticity_tet(d->K, d->lambda, d->mu2, d->c0, f, d->ls.rhs.p, 0);
+    const double* c = d->c;
+    // LHS c0 M + K(c1, c2) and the body force (rhs = f |K|/4), re-assembled on the fixed structure
+    assemble_elasticity_tet(d->K, c[1], c[2], c[0], f, d->ls.rhs.p, 0);
     // rhs += M (c0 U + c3 V + c4 A)
-    vec_lincomb(ctx, d->n, d->c0, d->U.p, d->c3, d->V.p, d->c4, d->A.p, d->W.p);
+    vec_lincomb(ctx, d->n, c[0], d->U.p, c[3], d->V.p, c[4], d->A.p, d->W.p);
     ls_spmv(d->lsm, d->W.p, d->MW.p);
     vec_lincomb(ctx, d->n, 1.0, d->ls.rhs.p, 1.0, d->MW.p, 0.0, nullptr, d->ls.rhs.p);
+    if (d->damped) {  // rhs += K(lambda = 1) (-c5 U + c7 V + c8 A) + K(2 mu = 1) (-c6 U + c9 V + c10 A)
+      vec_lincomb(ctx, d->n, -c[5], d->U.p, c[7], d->V.p, c[8], d->A.p, d->W.p);
+      ls_spmv(d->lsl, d->W.p, d->MW.p);
+      vec_lincomb(ctx, d->n, 1.0, d->ls.rhs.p, 1.0, d->MW.p, 0.0, nullptr, d->ls.rhs.p);
+      vec_lincomb(ctx, d->n, -c[6], d->U.p, c[9], d->V.p, c[10], d->A.p, d->W.p);
+      ls_spmv(d->lsu, d->W.p, d->MW.p);
+      vec_lincomb(ctx, d->n, 1.0, d->ls.rhs.p, 1.0, d->MW.p, 0.0, nullptr, d->ls.rhs.p);
+    }
     // clamped DoFs by penalty (the reference's default Dirichlet treatment)
     if (d->fixed.n) ls_set_list(d->ls, d->fixed.p, (int64_t)d->fixed.n, AFEM_MEM_DEVICE, 0, 0.0, d->p.penalty);
     // imposed displacements: diagonal = penalty, rhs = u penalty
@@ -253,10 +328,9 @@ void dyn_set_time_step(Elastodynamics* d, double dt)
   AFEM_REQUIRE(dt > 0, AFEM_ERR_ARG, "afem_elastodynamics_set_time_step: dt must be > 0");
   if (dt == d->p.dt) return;
   d->p.dt = dt;
-  d->c0 = d->p.rho / (d->beta * dt * dt);
-  d->c3 = d->p.rho / d->beta / dt;
-  // c4 does not depend on dt; the operator c0 M + K does: a reused multigrid
-  // hierarchy is rebuilt at the next solve
+  dyn_coefficients(d);
+  // the operator c0 M + K(c1, c2) depends on dt: a reused multigrid hierarchy
+  // is rebuilt at the next solve
   d->ls.mg.reset();
 }
 
@@ -266,7 +340,8 @@ void dyn_destroy(Elastodynamics* d)
   d->ctx->set_device();
   (void)hipStreamSynchronize(d->ctx->stream);
   if (d->ls.pinned) (void)hipHostFree(d->ls.pinned);
-  if (d->lsm.pinned) (void)hipHostFree(d->lsm.pinned);
+  for (LinearSystem* l : { &d->lsm, &d->lsl, &d->lsu })
+    if (l->pinned) (void)hipHostFree(l->pinned);
   delete d;
 }
 

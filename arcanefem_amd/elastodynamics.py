@@ -5,11 +5,12 @@ Thin host mirror of the native time loop behind the C ABI
 restates the reference's time-stepping callers of the linear-system path:
 
 * ``modules/elastodynamics/FemModule.cc`` (2D TRIA3): Newmark-beta with
-  gamma = 1/2, beta = (gamma + 1/2)^2 / 4 (:256-270); LHS
-  ``c1 div-div + c2 strain + c0 consistent mass`` (:1130-1340, c1 = lambda and
-  c2 = 2 mu without Rayleigh damping, etak = 0); RHS
-  ``M (c0 U + c3 V + c4 A)`` + body force (:842-862); state update
-  ``_updateVariables`` (:429-455); the matrix re-assembled every step (:149-153).
+  gamma = 1/2, beta = (gamma + 1/2)^2 / 4 (:256-270) or generalized-alpha
+  (gamma = 1/2 + alpf - alpm, :275-290), Rayleigh damping etam / etak; LHS
+  ``c1 div-div + c2 strain + c0 consistent mass`` (:1130-1340); RHS
+  ``M (c0 U + c3 V + c4 A) - K(c5, c6) U + K(c7, c9) V + K(c8, c10) A`` + body
+  force (:842-862); state update ``_updateVariables`` (:429-455); the matrix
+  re-assembled every step (:149-153).
 * ``modules/passmo/ElastodynamicModule.cc`` (3D): re-assembly every step on a
   fixed structure (:469-536).
 
@@ -32,6 +33,9 @@ import numpy as np
 from . import _capi as C
 from ._capi import call
 from .core import Context, Mesh
+
+
+SCHEMES = {"newmark-beta": 0, "generalized-alpha": 1}
 
 
 def newmark_coefficients(rho: float, dt: float):
@@ -57,12 +61,19 @@ def young_from_lame(lam: float, mu: float):
 class Elastodynamics3D:
     def __init__(self, ctx: Context, mesh: Mesh, E: float, nu: float, rho: float, dt: float,
                  body_force=(0.0, 0.0, 0.0), fixed_nodes=None, penalty: float = 1.0e30, rtol: float = 1e-12,
-                 comm=None, max_iter: int = 20000, preconditioner: str = "jacobi"):
+                 comm=None, max_iter: int = 20000, preconditioner: str = "jacobi", etam: float = 0.0,
+                 etak: float = 0.0, alpm: float = 0.0, alpf: float = 0.0, time_discretization: str = "newmark-beta"):
+        """time_discretization, etam, etak, alpm, alpf: the module's
+        timeDiscretization and damping options (Fem.axl of
+        modules/elastodynamics; FemModule.cc:222-296)."""
         if mesh.dim != 3:
             raise ValueError("Elastodynamics3D needs a tetrahedral mesh")
+        if time_discretization.lower() not in SCHEMES:
+            raise ValueError("Only Newmark-beta | Generalized-alpha are supported for time-discretization")
         self.ctx, self.mesh, self.dt = ctx, mesh, dt
         self.n = 3 * mesh.n_own_nodes
-        p = C.NewmarkParams(E, nu, rho, dt, (ctypes.c_double * 3)(*[float(x) for x in body_force]), penalty, 0.0, 0.0)
+        p = C.NewmarkParams(E, nu, rho, dt, (ctypes.c_double * 3)(*[float(x) for x in body_force]), penalty, 0.0, 0.0,
+                            etam, etak, alpm, alpf, SCHEMES[time_discretization.lower()], 0)
         fixed = np.zeros(0, dtype=np.int32) if fixed_nodes is None else np.ascontiguousarray(fixed_nodes,
                                                                                             dtype=np.int32)
         h = ctypes.c_void_p()

@@ -546,8 +546,16 @@ typedef struct afem_newmark_params {
   double E, nu, rho, dt;
   double body_force[3];
   double penalty; /* <= 0: 1e30 (modules/elasticity/Fem.axl:37-41) */
-  double gamma;   /* <= 0: 1/2 */
-  double beta;    /* <= 0: (gamma + 1/2)^2 / 4 */
+  double gamma;   /* <= 0: 1/2 (scheme 0 only) */
+  double beta;    /* <= 0: (gamma + 1/2)^2 / 4 (scheme 0 only) */
+  /* Rayleigh damping C = etam M + etak K and the time scheme of
+   * modules/elastodynamics/FemModule.cc:222-296: scheme 0 Newmark-beta,
+   * 1 generalized-alpha (gamma = 1/2 + alpf - alpm, beta = (gamma + 1/2)^2 / 4).
+   * All zero: the undamped Newmark-beta step. */
+  double etam, etak;
+  double alpm, alpf;
+  int32_t scheme;
+  int32_t reserved0;
 } afem_newmark_params;
 /* fixed_nodes: local node ids (in `mem`) whose 3 DoFs are clamped to 0; comm
  * may be NULL (one subdomain). */

@@ -446,17 +446,56 @@ def check_node_result(values_by_uid: dict, golden: dict, eps: float, min_value: 
     return nb_error, max_rel
 
 
-def newmark_elastodynamics(n_nodes, cells, coords, E, nu, rho, dt, n_steps, body_force, fixed_nodes, penalty=1e30):
+def elastodynamics_constants(lam, mu, rho, dt, etam=0.0, etak=0.0, alpm=0.0, alpf=0.0, scheme="newmark-beta"):
+    """gamma, beta and c0 .. c10 of modules/elastodynamics/FemModule.cc:255-290
+    (Newmark-beta :256-270, generalized-alpha :275-290; Rayleigh damping
+    etam, etak)."""
+    if scheme == "generalized-alpha":
+        gamma = 0.5 + alpf - alpm
+        beta = (1.0 / 4.0) * (gamma + 0.5) * (gamma + 0.5)
+        c = [rho * (1. - alpm) / (beta * dt * dt) + etam * rho * gamma * (1 - alpf) / beta / dt,
+             lam * (1. - alpf) + lam * etak * gamma * (1. - alpf) / beta / dt,
+             2. * mu * (1. - alpf) + 2. * mu * etak * gamma * (1. - alpf) / beta / dt,
+             rho * (1. - alpm) / beta / dt - etam * rho * (1 - gamma * (1 - alpf) / beta),
+             rho * ((1. - alpm) * (1. - 2. * beta) / 2. / beta - alpm - etam * dt * (1. - alpf) * (1. - gamma / 2 / beta)),
+             lam * alpf - lam * etak * gamma * (1. - alpf) / beta / dt,
+             2 * mu * alpf - 2. * mu * etak * gamma * (1. - alpf) / beta / dt,
+             etak * lam * (gamma * (1. - alpf) / beta - 1),
+             etak * lam * dt * (1. - alpf) * ((1. - 2 * beta) / 2. / beta - (1. - gamma)),
+             etak * 2 * mu * (gamma * (1. - alpf) / beta - 1),
+             etak * 2 * mu * dt * (1. - alpf) * ((1. - 2 * beta) / 2. / beta - (1. - gamma))]
+    elif scheme == "newmark-beta":
+        gamma = 0.5
+        beta = (1. / 4.) * (gamma + 0.5) * (gamma + 0.5)
+        c = [rho / (beta * dt * dt) + etam * rho * gamma / beta / dt,
+             lam + lam * etak * gamma / beta / dt,
+             2. * mu + 2. * mu * etak * gamma / beta / dt,
+             rho / beta / dt - etam * rho * (1 - gamma / beta),
+             rho * ((1. - 2. * beta) / 2. / beta - etam * dt * (1. - gamma / 2 / beta)),
+             -lam * etak * gamma / beta / dt,
+             -2. * mu * etak * gamma / beta / dt,
+             etak * lam * (gamma / beta - 1),
+             etak * lam * dt * ((1. - 2 * beta) / 2. / beta - (1. - gamma)),
+             etak * 2 * mu * (gamma / beta - 1),
+             etak * 2 * mu * dt * ((1. - 2 * beta) / 2. / beta - (1. - gamma))]
+    else:
+        raise ValueError("Only Newmark-beta | Generalized-alpha are supported for time-discretization")
+    return gamma, beta, c
+
+
+def newmark_elastodynamics(n_nodes, cells, coords, E, nu, rho, dt, n_steps, body_force, fixed_nodes, penalty=1e30,
+                           etam=0.0, etak=0.0, alpm=0.0, alpf=0.0, scheme="newmark-beta"):
     """CPU restatement of the 3D elastodynamics time loop (per-step
-    re-assembly, Newmark-beta, modules/elastodynamics/FemModule.cc:255-264
-    coefficients, :842-862 RHS with etam = etak = 0, :429-455 update) on the
-    oracle's block-3 assembly, penalty Dirichlet (diagonal set to P, rhs = P*0)
-    and a dense direct solve.  Returns U, V, A (3 per node) after n_steps."""
+    re-assembly; modules/elastodynamics/FemModule.cc:255-290 coefficients,
+    LHS c0 M + K(lambda -> c1, 2 mu -> c2) (:1130-1340), :842-862 RHS
+    M (c0 U + c3 V + c4 A) - K(c5, c6) U + K(c7, c9) V + K(c8, c10) A + body
+    force, :429-455 update) on the oracle's block-3 assembly, penalty Dirichlet
+    (diagonal set to P, rhs = P*0) and a dense direct solve.  Returns U, V, A
+    (3 per node) after n_steps."""
     lam = E * nu / ((1 + nu) * (1 - 2 * nu))
-    mu2 = 2.0 * E / (2 * (1 + nu))
-    gamma = 0.5
-    beta = 0.25 * (gamma + 0.5) ** 2
-    c0, c3, c4 = rho / (beta * dt * dt), rho / beta / dt, rho * ((1.0 - 2.0 * beta) / 2.0 / beta)
+    mu = E / (2 * (1 + nu))
+    gamma, beta, c = elastodynamics_constants(lam, mu, rho, dt, etam, etak, alpm, alpf, scheme)
+    c0, c3, c4 = c[0], c[3], c[4]
     rp, cols = sparsity(n_nodes, n_nodes, cells)
     m_vals, _ = assemble_elasticity_tet(n_nodes, cells, coords, rp, cols, 0.0, 0.0, 1.0)
     n = 3 * n_nodes
@@ -469,12 +508,16 @@ def newmark_elastodynamics(n_nodes, cells, coords, E, nu, rho, dt, n_steps, body
         return A
 
     M = dense(m_vals)
+    # K(lambda', 2 mu') of the RHS terms: div-div and strain parts, linear in the two moduli
+    KL = dense(assemble_elasticity_tet(n_nodes, cells, coords, rp, cols, 1.0, 0.0, 0.0)[0])
+    KM = dense(assemble_elasticity_tet(n_nodes, cells, coords, rp, cols, 0.0, 1.0, 0.0)[0])
     fixed = (3 * np.asarray(fixed_nodes)[:, None] + np.arange(3)[None, :]).ravel()
     U, V, A = np.zeros(n), np.zeros(n), np.zeros(n)
     for _ in range(n_steps):
-        k_vals, f_rhs = assemble_elasticity_tet(n_nodes, cells, coords, rp, cols, lam, mu2, c0, body_force)
+        k_vals, f_rhs = assemble_elasticity_tet(n_nodes, cells, coords, rp, cols, c[1], c[2], c0, body_force)
         L = dense(k_vals)
         b = f_rhs + M @ (c0 * U + c3 * V + c4 * A)
+        b += KL @ (-c[5] * U + c[7] * V + c[8] * A) + KM @ (-c[6] * U + c[9] * V + c[10] * A)
         L[fixed, fixed] = penalty
         b[fixed] = penalty * 0.0
         Un = np.linalg.solve(L, b)

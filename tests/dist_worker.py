@@ -27,6 +27,8 @@ POISSON_MG = dict(n=8, nz=16)
 # large enough for distributed coarse levels (level 1: 9 x 9 x 17 nodes over the slabs, then the gathered box)
 POISSON_MG2 = dict(n=16, nz=32)
 DYN_MG = dict(n=8, nz=12, E=21e5, nu=0.28, rho=1.0, dt=1e-3, f=(0.0, -9.81, 1.0), steps=3)
+# generalized alpha with Rayleigh damping: the RHS's stiffness SpMVs exchange their operand's ghosts too
+DYN_DAMP = dict(etam=0.3, etak=1e-3, alpm=0.2, alpf=0.4, time_discretization="generalized-alpha")
 
 
 def main():
@@ -159,16 +161,17 @@ def main():
         st = ls.solve()
         res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
                    converged=int(st["converged"]), rel=st["rel_residual"], part=part)
-    elif case in ("elastodynamics", "elastodynamics_mg"):
+    elif case in ("elastodynamics", "elastodynamics_mg", "elastodynamics_damped"):
         from arcanefem_amd.elastodynamics import Elastodynamics3D
 
-        p = DYN if case == "elastodynamics" else DYN_MG
-        pc = "jacobi" if case == "elastodynamics" else "multigrid"
+        p = DYN_MG if case == "elastodynamics_mg" else DYN
+        pc = "multigrid" if case == "elastodynamics_mg" else "jacobi"
+        kw = DYN_DAMP if case == "elastodynamics_damped" else {}
         mesh = af.Mesh.structured(ctx, 3, p["n"], nz=p["nz"], jitter=0.2, seed=20250220, nranks=world, rank=rank)
         _, coords, l2g = mesh.download()
         fixed = np.nonzero(coords[:, 0] < 0.5 / p["n"])[0].astype(np.int32)  # the x = 0 layer, ghosts included
         sim = Elastodynamics3D(ctx, mesh, p["E"], p["nu"], p["rho"], p["dt"], body_force=p["f"], fixed_nodes=fixed,
-                               rtol=1e-14, comm=comm, preconditioner=pc)
+                               rtol=1e-14, comm=comm, preconditioner=pc, **kw)
         its = []
         for _ in range(p["steps"]):
             st = sim.step()

@@ -108,19 +108,24 @@ def test_distributed_poisson_solve(case, world, tmp_path):
         assert np.abs(r["x"][k:] - x[gid]).max() <= 1e-15 * np.abs(xg).max()
 
 
-@pytest.mark.parametrize("case,world", [("elastodynamics", 2), ("elastodynamics_mg", 2), ("elastodynamics_mg", 4)])
+@pytest.mark.parametrize("case,world", [("elastodynamics", 2), ("elastodynamics_mg", 2), ("elastodynamics_mg", 4),
+                                        ("elastodynamics_damped", 3)])
 def test_distributed_elastodynamics(tmp_path, case, world):
     """C5's loop over 2 slabs: point-Jacobi PCG, and the multigrid PCG over 2
     and 4 slabs (one global V-cycle: fine and coarse levels distributed down to
     the gather level, replicated below it) -- both
     must match the single-domain oracle Newmark loop; the multigrid one also
     the one-rank multigrid iteration counts."""
-    p = W.DYN if case == "elastodynamics" else W.DYN_MG
+    p = W.DYN_MG if case == "elastodynamics_mg" else W.DYN
     res = _run(case, world, tmp_path)
     g = O.structured_mesh(3, p["n"], nz=p["nz"])
     fixed = np.nonzero(g["coords"][:, 0] < 0.5 / p["n"])[0]
+    okw = {}
+    if case == "elastodynamics_damped":  # generalized alpha + Rayleigh damping
+        okw = dict(W.DYN_DAMP)
+        okw["scheme"] = okw.pop("time_discretization")
     Uo, Vo, Ao = O.newmark_elastodynamics(g["n_own"], g["cells"], g["coords"], p["E"], p["nu"], p["rho"], p["dt"],
-                                          p["steps"], p["f"], fixed)
+                                          p["steps"], p["f"], fixed, **okw)
     U = np.full(3 * g["n_own"], np.nan)
     V = U.copy()
     A = U.copy()

@@ -283,6 +283,41 @@ def test_elastodynamics_newmark_parity(ctx):
     sim.close()
 
 
+@pytest.mark.parametrize("kw", [dict(etam=0.3, etak=1e-3),
+                                dict(time_discretization="generalized-alpha", alpm=0.2, alpf=0.4),
+                                dict(time_discretization="generalized-alpha", alpm=0.2, alpf=0.4, etam=0.3,
+                                     etak=1e-3)],
+                         ids=["newmark-rayleigh", "alpha", "alpha-rayleigh"])
+def test_elastodynamics_damping_and_alpha_parity(ctx, kw):
+    """Rayleigh damping (etam, etak) and the generalized-alpha scheme
+    (modules/elastodynamics/FemModule.cc:222-296, RHS :842-862): 6 steps on the
+    C5-semantics box against the oracle's loop with the module's c0 .. c10."""
+    from arcanefem_amd.elastodynamics import Elastodynamics3D
+
+    mesh = af.Mesh.structured(ctx, 3, 3)
+    cells, coords, _ = mesh.download()
+    fixed = np.nonzero(coords[:, 0] < 0.5 / 3)[0]
+    E_, nu_, rho, dt = 21e5, 0.28, 1.0, 1e-3
+    f = (0.0, -9.81, 1.0)
+    sim = Elastodynamics3D(ctx, mesh, E_, nu_, rho, dt, body_force=f, fixed_nodes=fixed, rtol=1e-14, **kw)
+    for _ in range(6):
+        assert sim.step()["converged"]
+    U, V, A = sim.state_host()
+    okw = dict(kw)
+    if "time_discretization" in okw:
+        okw["scheme"] = okw.pop("time_discretization")
+    Uo, Vo, Ao = O.newmark_elastodynamics(mesh.n_nodes, cells, coords, E_, nu_, rho, dt, 6, f, fixed, **okw)
+    for g, o in ((U, Uo), (V, Vo), (A, Ao)):
+        assert np.abs(g - o).max() <= 1e-8 * np.abs(o).max(), np.abs(g - o).max() / np.abs(o).max()
+    # the undamped Newmark run differs (the options are not ignored)
+    sim0 = Elastodynamics3D(ctx, mesh, E_, nu_, rho, dt, body_force=f, fixed_nodes=fixed, rtol=1e-14)
+    for _ in range(6):
+        sim0.step()
+    assert np.abs(sim0.state_host()[0] - U).max() > 1e-6 * np.abs(U).max()
+    sim.close()
+    sim0.close()
+
+
 @pytest.mark.parametrize("which", ["sphere", "bigbox"])
 def test_block_jacobi3_static_solve(ctx, which):
     """precond_block = 3 (3x3 node-block Jacobi): a clamped static elasticity
