@@ -93,14 +93,16 @@ class SolverOpts(ctypes.Structure):
     _fields_ = [("method", ctypes.c_int32), ("max_iter", ctypes.c_int32), ("rtol", ctypes.c_double),
                 ("atol", ctypes.c_double), ("check_every", ctypes.c_int32), ("fixed_iterations", ctypes.c_int32),
                 ("initial_guess", ctypes.c_int32), ("precond_block", ctypes.c_int32), ("multigrid", ctypes.c_int32),
-                ("profile_comm", ctypes.c_int32)]
+                ("profile_comm", ctypes.c_int32), ("amg", ctypes.c_int32)]
 
 
 class SolveStats(ctypes.Structure):
     _fields_ = [("iterations", ctypes.c_int32), ("converged", ctypes.c_int32), ("rel_residual", ctypes.c_double),
                 ("residual_norm", ctypes.c_double), ("solve_ms", ctypes.c_double), ("spmv_kernel", ctypes.c_int32),
                 ("halo_wait_ms", ctypes.c_double), ("allreduce_ms", ctypes.c_double), ("halo_bytes", ctypes.c_int64),
-                ("n_halo", ctypes.c_int32), ("n_allreduce", ctypes.c_int32)]
+                ("n_halo", ctypes.c_int32), ("n_allreduce", ctypes.c_int32), ("amg_levels", ctypes.c_int32),
+                ("amg_coarse_rows", ctypes.c_int64), ("amg_complexity", ctypes.c_double),
+                ("amg_setup_ms", ctypes.c_double)]
 
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64)

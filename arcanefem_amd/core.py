@@ -462,8 +462,10 @@ class DoFLinearSystem:
         solution vector's values); preconditioner: "jacobi" (default),
         "block3" (3x3 node-block Jacobi, NB_DOF = 3 systems), "multigrid"
         (geometric multigrid V-cycle on structured boxes, one rank or z-slabs; rebuilt
-        every solve) or "multigrid-reuse" (built once, reused while the
-        matrix structure is unchanged)."""
+        every solve), "multigrid-reuse" (built once, reused while the
+        matrix structure is unchanged), "amg" / "amg-reuse" (algebraic
+        multigrid from the CSR: any mesh, one rank) or "multigrid+amg" (the
+        geometric hierarchy where it exists, else the algebraic one)."""
         o = C.SolverOpts()
         call("afem_ls_get_solver_options", self.impl, ctypes.byref(o))
         if method is not None:
@@ -483,8 +485,9 @@ class DoFLinearSystem:
         if initial_guess is not None:
             o.initial_guess = {"zero": 0, "current": 1}[initial_guess]
         if preconditioner is not None:
-            o.precond_block, o.multigrid = {"jacobi": (0, 0), "block3": (3, 0), "multigrid": (0, 1),
-                                            "multigrid-reuse": (0, 2)}[preconditioner]
+            o.precond_block, o.multigrid, o.amg = {
+                "jacobi": (0, 0, 0), "block3": (3, 0, 0), "multigrid": (0, 1, 0), "multigrid-reuse": (0, 2, 0),
+                "amg": (0, 0, 1), "amg-reuse": (0, 0, 2), "multigrid+amg": (0, 1, 1)}[preconditioner]
         call("afem_ls_set_solver_options", self.impl, ctypes.byref(o))
 
     def solve(self) -> dict:
@@ -494,7 +497,9 @@ class DoFLinearSystem:
         return dict(iterations=st.iterations, converged=bool(st.converged), rel_residual=st.rel_residual,
                     residual_norm=st.residual_norm, solve_ms=st.solve_ms, spmv_kernel=st.spmv_kernel,
                     halo_wait_ms=st.halo_wait_ms, allreduce_ms=st.allreduce_ms, halo_bytes=st.halo_bytes,
-                    n_halo=st.n_halo, n_allreduce=st.n_allreduce)
+                    n_halo=st.n_halo, n_allreduce=st.n_allreduce, amg_levels=st.amg_levels,
+                    amg_coarse_rows=st.amg_coarse_rows, amg_complexity=st.amg_complexity,
+                    amg_setup_ms=st.amg_setup_ms)
 
     def spmv(self, x_dptr: int, y_dptr: int):
         call("afem_ls_spmv", self.impl, ctypes.c_void_p(x_dptr), ctypes.c_void_p(y_dptr))

@@ -403,6 +403,10 @@ struct Multigrid;
 struct MgDeleter {
   void operator()(Multigrid* m) const;
 };
+struct Amg;
+struct AmgDeleter {
+  void operator()(Amg* a) const;
+};
 struct LinearSystem {
   Ctx* ctx = nullptr;
   std::vector<hipEvent_t> prof_ev;  // afem_solver_opts.profile_comm: event pool of the PCG loop's timings
@@ -476,6 +480,8 @@ struct LinearSystem {
   int mg_nzg = 0, mg_k0 = 0;
   bool mg_glo = false;
   std::unique_ptr<Multigrid, MgDeleter> mg;
+  std::unique_ptr<Amg, AmgDeleter> amg;  // algebraic multigrid (amg.hip, afem_solver_opts.amg)
+  std::shared_ptr<void> spmv_plan;       // the current solve's SpMV plan (linear_system.hip SpmvPlan)
 };
 
 // ------------------------------------------------------------------ kernels (host launchers)
@@ -519,6 +525,12 @@ void ls_mapped_scatter_back(LinearSystem& ls);
 void ls_mapped_point_update(LinearSystem& ls, int32_t row, int32_t col, double v, bool set);
 void ls_solve(LinearSystem& ls, afem_solve_stats* st);
 void ls_spmv(LinearSystem& ls, const double* x, double* y);
+void ls_spmv_planned(LinearSystem& ls, const double* x, double* y);
+// algebraic multigrid preconditioner (amg.hip)
+bool amg_available(const LinearSystem& ls);
+void amg_setup(LinearSystem& ls);
+void amg_apply(LinearSystem& ls, const double* r, double* z);
+void amg_stats(const LinearSystem& ls, int32_t* levels, int64_t* coarse_rows, double* complexity);
 void ls_build_from_host_coo(LinearSystem& ls);
 void ls_point_update(LinearSystem& ls, int32_t row, int32_t col, double v, bool set);
 // kind 0 penalty, 1 row elimination, 2 row+column elimination of the listed DoFs

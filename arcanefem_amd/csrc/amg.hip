@@ -1,0 +1,953 @@
+// Algebraic multigrid preconditioner for the PCG (afem_solver_opts.amg) on
+// systems that are NOT a structured Kuhn box -- Gmsh meshes, caller arrays,
+// anything the geometric hierarchy of multigrid.hip does not cover.  The
+// reference's GPU solve is Hypre PCG + BoomerAMG on any mesh
+// (femutils/HypreDoFLinearSystem.cc:686-742); this is an aggregation AMG built
+// from the assembled CSR alone, on the device, deterministic bit for bit:
+//  * strength: a_ij is strong when |a_ij| >= theta sqrt(|a_ii a_jj|)
+//    (AFEM_AMG_THETA, default 0.08); constraint rows (the PCG's `cons` flags:
+//    penalty / eliminated rows) and rows without a positive diagonal are
+//    outside the graph;
+//  * aggregation: a maximal independent set of the strength graph at distance
+//    2 (AFEM_AMG_HOPS0 / AFEM_AMG_HOPS: the fine / coarse levels) by hashed
+//    priorities (Luby-style rounds of
+//    max propagation over (state, hash(i), i) tuples: no atomics, the same set
+//    on every run); every root starts an aggregate, every other node joins the
+//    neighbouring root with the largest tuple (distance 2: the aggregate of
+//    its largest joined neighbour);
+//  * prolongation: piecewise constant on the aggregates (unsmoothed), R = P^T,
+//    coarse operator A_c = P^T A P: every strong-graph non-zero (i, j) keyed
+//    by (agg i, agg j), radix-sorted (stable), each key run summed by one
+//    thread in the CSR order -- fixed summation order;
+//  * cycle: V(nu, nu) with damped Jacobi, omega = 4 / (3 lambda_max(D^-1 A))
+//    per level (20 power iterations from a signed hashed vector, +10 %), the
+//    coarse correction scaled by AFEM_AMG_SCALE (default 1.7: unsmoothed
+//    aggregation under-corrects; 142 -> 92 iterations at 1.7, r05y); the
+//    fine level's products through the PCG's own SpMV plan; coarsest level (<= 1024 rows,
+//    AFEM_AMG_DENSE) inverted densely (host Cholesky at setup), else 24
+//    Jacobi sweeps;
+//  * constraint rows are taken out of the cycle as in multigrid.hip:
+//    z = F V(F r) + C D^-1 r.
+// One rank (the system carries no halo); a symmetric V-cycle, so the PCG's
+// preconditioner stays SPD.
+#include "afem_internal.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace afem {
+
+namespace {
+
+inline unsigned grid_for(int64_t n, int threads) { return (unsigned)((n + threads - 1) / threads); }
+constexpr int kDense = 1024;     // rows of a coarsest level inverted densely (AFEM_AMG_DENSE)
+constexpr int kMaxLevels = 16;
+constexpr int kCoarseSweeps = 24;
+constexpr int kPowerIts = 20;
+constexpr int kVec = 1024;       // grid of the vector kernels
+
+// ------------------------------------------------------------------ kernels
+
+__global__ void k_amg_diag(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                           const double* __restrict__ v, const uint8_t* __restrict__ cons, double* __restrict__ diag,
+                           uint8_t* __restrict__ in)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double d = 0.0;
+  for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+    if (ci[k] == i) d += v[k];
+  diag[i] = d;
+  in[i] = (d > 0.0 && !(cons && cons[i])) ? 1 : 0;
+}
+
+__device__ __forceinline__ uint32_t amg_hash(uint32_t x)
+{
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+// tuple (state, hash, index): state 2 root, 1 undecided, 0 out / outside the graph
+__global__ void k_amg_tuple_init(int64_t n, const uint8_t* __restrict__ in, uint64_t* __restrict__ t)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  t[i] = in[i] ? (1ull << 62) | (uint64_t)(amg_hash((uint32_t)i) >> 2) << 32 | (uint64_t)(uint32_t)i : 0ull;
+}
+
+__device__ __forceinline__ bool amg_strong(double aij, double di, double dj, double theta)
+{
+  return fabs(aij) >= theta * sqrt(di * dj);
+}
+
+// strong[k] = 1 when non-zero k = (i, j) is an edge of the strength graph
+// (8 lanes per row: the row's columns and values read coalesced)
+__global__ __launch_bounds__(256) void k_amg_strength(int64_t n, const int64_t* __restrict__ rp,
+                                                      const int32_t* __restrict__ ci, const double* __restrict__ v,
+                                                      const double* __restrict__ diag,
+                                                      const uint8_t* __restrict__ in, double theta,
+                                                      uint8_t* __restrict__ strong)
+{
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+  const int l = threadIdx.x & 7;
+  if (i >= n) return;
+  const bool ii = in[i];
+  const double di = diag[i];
+  for (int64_t k = rp[i] + l; k < rp[i + 1]; k += 8) {
+    const int32_t j = ci[k];
+    strong[k] = (ii && j != i && j >= 0 && j < n && in[j] && amg_strong(v[k], di, diag[j], theta)) ? 1 : 0;
+  }
+}
+
+// m[i] = max(t[i], t[j] for strong neighbours j); 8 lanes per row
+__global__ __launch_bounds__(256) void k_amg_maxprop(int64_t n, const int64_t* __restrict__ rp,
+                                                     const int32_t* __restrict__ ci,
+                                                     const uint8_t* __restrict__ strong,
+                                                     const uint64_t* __restrict__ t, uint64_t* __restrict__ m)
+{
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+  const int l = threadIdx.x & 7;
+  uint64_t b = 0;
+  if (i < n) {
+    b = t[i];
+    for (int64_t k = rp[i] + l; k < rp[i + 1]; k += 8)
+      if (strong[k]) {
+        const uint64_t tj = t[ci[k]];
+        b = tj > b ? tj : b;
+      }
+  }
+  for (int o = 1; o < 8; o <<= 1) {
+    const uint64_t x = (uint64_t)__shfl_xor((long long)b, o, 8);
+    b = x > b ? x : b;
+  }
+  if (i < n && l == 0) m[i] = b;
+}
+
+// undecided i: root when it is the maximum of its neighbourhood, out when a
+// root is in it; counts the undecided that remain
+__global__ void k_amg_mis_update(int64_t n, uint64_t* __restrict__ t, const uint64_t* __restrict__ m,
+                                 unsigned long long* __restrict__ left)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t ti = t[i];
+  if ((ti >> 62) != 1) return;
+  const uint64_t mi = m[i];
+  if (mi == ti)
+    t[i] = (2ull << 62) | (ti & ((1ull << 62) - 1));
+  else if ((mi >> 62) == 2)
+    t[i] = ti & ((1ull << 62) - 1);  // out
+  else
+    atomicAdd(left, 1ull);
+}
+
+__global__ void k_amg_root_flags(int64_t n, const uint64_t* __restrict__ t, int32_t* __restrict__ f)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  f[i] = (t[i] >> 62) == 2 ? 1 : 0;
+}
+
+// roots: their aggregate (rank among the roots); others -1
+__global__ void k_amg_root_agg(int64_t n, const uint64_t* __restrict__ t, const int64_t* __restrict__ rank,
+                               int32_t* __restrict__ agg, uint64_t* __restrict__ owner)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool root = (t[i] >> 62) == 2;
+  agg[i] = root ? (int32_t)rank[i] : -1;
+  owner[i] = root ? t[i] : 0ull;  // the tuple of the node's root (0: none yet)
+}
+
+// unassigned graph nodes join the strong neighbour whose root tuple is the
+// largest among the neighbours assigned in the previous pass (pass 1: roots)
+__global__ void k_amg_join(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                           const uint8_t* __restrict__ strong, const uint8_t* __restrict__ in,
+                           const int32_t* __restrict__ agg_in, const uint64_t* __restrict__ own_in,
+                           int32_t* __restrict__ agg_out, uint64_t* __restrict__ own_out)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t a = agg_in[i];
+  uint64_t o = own_in[i];
+  if (a < 0 && in[i]) {
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+      const int32_t j = ci[k];
+      if (!strong[k] || agg_in[j] < 0) continue;
+      if (own_in[j] > o) {
+        o = own_in[j];
+        a = agg_in[j];
+      }
+    }
+  }
+  agg_out[i] = a;
+  own_out[i] = o;
+}
+
+// graph nodes no root reaches (isolated, or distance > hops): flag, to become
+// singleton aggregates
+__global__ void k_amg_orphans(int64_t n, const uint8_t* __restrict__ in, const int32_t* __restrict__ agg,
+                              int32_t* __restrict__ f)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  f[i] = (in[i] && agg[i] < 0) ? 1 : 0;
+}
+
+__global__ void k_amg_orphan_agg(int64_t n, const int32_t* __restrict__ f, const int64_t* __restrict__ rank,
+                                 int32_t base, int32_t* __restrict__ agg)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (f[i]) agg[i] = base + (int32_t)rank[i];
+}
+
+// Galerkin keys of the non-zeros: (agg i, agg j), or all ones outside the graph
+__global__ void k_amg_keys(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                           const int32_t* __restrict__ agg, unsigned long long* __restrict__ key)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t ai = agg[i];
+  for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+    const int32_t j = ci[k];
+    const int32_t aj = (j >= 0 && j < n) ? agg[j] : -1;
+    key[k] = (ai >= 0 && aj >= 0) ? ((unsigned long long)(uint32_t)ai << 32 | (uint32_t)aj) : ~0ull;
+  }
+}
+
+__global__ void k_amg_iota(int64_t n, int64_t* __restrict__ x)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = i;
+}
+
+// run heads of the sorted keys (valid keys only)
+__global__ void k_amg_heads(int64_t m, const unsigned long long* __restrict__ key, int32_t* __restrict__ head)
+{
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  head[k] = key[k] != ~0ull && (k == 0 || key[k] != key[k - 1]) ? 1 : 0;
+}
+
+// run r = [pos of head r, next head): its sum in the sorted (= CSR) order
+__global__ void k_amg_runs(int64_t m, const unsigned long long* __restrict__ key, const int64_t* __restrict__ src,
+                           const double* __restrict__ v, const int32_t* __restrict__ head,
+                           const int64_t* __restrict__ hrank, int64_t* __restrict__ c_row_of,
+                           int32_t* __restrict__ c_col, double* __restrict__ c_val)
+{
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m || !head[k]) return;
+  const unsigned long long kk = key[k];
+  double s = 0.0;
+  for (int64_t q = k; q < m && key[q] == kk; ++q) s += v[src[q]];
+  const int64_t r = hrank[k];
+  c_row_of[r] = (int64_t)(kk >> 32);
+  c_col[r] = (int32_t)(kk & 0xffffffffu);
+  c_val[r] = s;
+}
+
+// CSR row pointer of the coarse non-zeros (sorted by row)
+__global__ void k_amg_rowptr(int64_t nnz, const int64_t* __restrict__ row_of, int64_t nc, int64_t* __restrict__ rp)
+{
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nnz) return;
+  const int64_t r = row_of[k];
+  const int64_t prev = k > 0 ? row_of[k - 1] : -1;
+  for (int64_t s = prev + 1; s <= r; ++s) rp[s] = k;
+  if (k == nnz - 1)
+    for (int64_t s = r + 1; s <= nc; ++s) rp[s] = nnz;
+}
+
+// aggregate member lists: members of aggregate a are mem[ap[a] .. ap[a+1]) in
+// increasing fine index (stable sort of (agg, i))
+__global__ void k_amg_member_keys(int64_t n, const int32_t* __restrict__ agg, uint32_t* __restrict__ key,
+                                  int32_t* __restrict__ idx)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  key[i] = agg[i] >= 0 ? (uint32_t)agg[i] : 0xffffffffu;
+  idx[i] = (int32_t)i;
+}
+
+__global__ void k_amg_member_ptr(int64_t n, const uint32_t* __restrict__ key, int64_t nc, int64_t* __restrict__ ap)
+{
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int64_t a = key[k] == 0xffffffffu ? nc : (int64_t)key[k];
+  const int64_t prev = k > 0 ? (key[k - 1] == 0xffffffffu ? nc : (int64_t)key[k - 1]) : -1;
+  for (int64_t s = prev + 1; s <= a && s <= nc; ++s) ap[s] = k;
+  if (k == n - 1)
+    for (int64_t s = a + 1; s <= nc; ++s) ap[s] = n;
+}
+
+// y = A x (EPI 0), y = x + omega dinv (b - A x) (EPI 1), y = b - A x (EPI 2);
+// 8 lanes per row, the row's products summed in a fixed butterfly order
+template <int EPI>
+__global__ __launch_bounds__(256) void k_amg_spmv(int64_t n, const int64_t* __restrict__ rp,
+                                                  const int32_t* __restrict__ ci, const double* __restrict__ v,
+                                                  const double* __restrict__ x, double* __restrict__ y,
+                                                  const double* __restrict__ b, const double* __restrict__ dinv,
+                                                  double omega)
+{
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+  const int l = threadIdx.x & 7;
+  double s = 0.0;
+  if (i < n)
+    for (int64_t k = rp[i] + l; k < rp[i + 1]; k += 8) s += v[k] * x[ci[k]];
+  s += __shfl_xor(s, 1, 8);
+  s += __shfl_xor(s, 2, 8);
+  s += __shfl_xor(s, 4, 8);
+  if (i < n && l == 0) {
+    if (EPI == 0) y[i] = s;
+    if (EPI == 1) y[i] = x[i] + omega * dinv[i] * (b[i] - s);
+    if (EPI == 2) y[i] = b[i] - s;
+  }
+}
+
+// the fine level's epilogues after the PCG's own SpMV (q = A x):
+// r = b - q, and x += omega dinv (b - q)
+__global__ void k_amg_resid(int64_t n, const double* __restrict__ b, const double* __restrict__ q,
+                            double* __restrict__ r)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    r[i] = b[i] - q[i];
+}
+
+__global__ void k_amg_jacobi(int64_t n, double omega, const double* __restrict__ dinv, const double* __restrict__ b,
+                             const double* __restrict__ q, double* __restrict__ x)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] += omega * dinv[i] * (b[i] - q[i]);
+}
+
+__global__ void k_amg_scale(int64_t n, double omega, const double* __restrict__ dinv, const double* __restrict__ b,
+                            double* __restrict__ x)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = omega * dinv[i] * b[i];
+}
+
+__global__ void k_amg_inv(int64_t n, const double* __restrict__ diag, const uint8_t* __restrict__ in,
+                          double* __restrict__ dinv)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dinv[i] = in[i] ? 1.0 / diag[i] : 0.0;
+}
+
+// b_c[a] = sum of the members' r, in member order
+__global__ void k_amg_restrict(int64_t nc, const int64_t* __restrict__ ap, const int32_t* __restrict__ mem,
+                               const double* __restrict__ r, double* __restrict__ bc)
+{
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= nc) return;
+  double s = 0.0;
+  for (int64_t q = ap[a]; q < ap[a + 1]; ++q) s += r[mem[q]];
+  bc[a] = s;
+}
+
+__global__ void k_amg_prolong(int64_t n, const int32_t* __restrict__ agg, double scale, const double* __restrict__ xc,
+                              double* __restrict__ x)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (agg[i] >= 0) x[i] += scale * xc[agg[i]];
+}
+
+__global__ void k_amg_mask(int64_t n, const uint8_t* __restrict__ cons, const double* __restrict__ r,
+                           double* __restrict__ b)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    b[i] = cons[i] ? 0.0 : r[i];
+}
+
+__global__ void k_amg_fix(int64_t n, const uint8_t* __restrict__ cons, const double* __restrict__ r,
+                          const double* __restrict__ dinv, double* __restrict__ z)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (cons[i]) z[i] = r[i] * dinv[i];
+}
+
+__global__ void k_amg_fill(int64_t n, const uint8_t* __restrict__ in, double* __restrict__ v)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    v[i] = in[i] ? (double)(h & 0xFFFF) / 32768.0 - 1.0 : 0.0;  // signed: every mode gets a share
+  }
+}
+
+// w = dinv .* w, block partials of w.w (and of v.v when v is given)
+__global__ void k_amg_dscale_dot(int64_t n, const double* __restrict__ dinv, double* __restrict__ w,
+                                 double* __restrict__ partial)
+{
+  __shared__ double sh[256];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double t = dinv ? dinv[i] * w[i] : w[i];
+    w[i] = t;
+    s += t * t;
+  }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+__global__ void k_amg_mul(int64_t n, double a, double* __restrict__ v)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    v[i] *= a;
+}
+
+__global__ __launch_bounds__(64) void k_amg_gemv(int n, const double* __restrict__ A, const double* __restrict__ b,
+                                                 double* __restrict__ x)
+{
+  const int i = blockIdx.x;
+  double s = 0.0;
+  for (int j = threadIdx.x; j < n; j += 64) s += A[(int64_t)i * n + j] * b[j];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (threadIdx.x == 0) x[i] = s;
+}
+
+double env_double(const char* name, double dflt)
+{
+  const char* v = variant(name);
+  return v && *v ? std::atof(v) : dflt;
+}
+
+}  // namespace
+
+struct AmgLevel {
+  int64_t n = 0, nnz = 0;
+  const int64_t* rp = nullptr;
+  const int32_t* ci = nullptr;
+  const double* v = nullptr;
+  DevBuf<int64_t> own_rp;
+  DevBuf<int32_t> own_ci;
+  DevBuf<double> own_v;
+  DevBuf<double> diag, dinv;
+  DevBuf<uint8_t> in;        // row in the strength graph
+  DevBuf<int32_t> agg;       // row -> aggregate of the next level, -1 outside
+  DevBuf<int64_t> ap;        // aggregate members (next level's rows): CSR over the fine rows
+  DevBuf<int32_t> mem;
+  DevBuf<double> x, t, b, r;
+  double omega = 0.0;
+};
+
+struct Amg {
+  std::vector<AmgLevel> lv;
+  DevBuf<double> ainv;
+  int n_dense = 0;
+  int sweeps = 1;
+  double scale = 1.0;
+  bool fine_planned = true;
+  // AFEM_AMG_GRAPH=1: the V-cycle replayed as a captured HIP graph (its
+  // launches are fixed once the hierarchy is); keyed on (r, z, the solve's
+  // SpMV plan).  Measured equal (2.93 ms per iteration either way, r05aa):
+  // the cycle is bound by its three fine-level products, not by launches
+  bool use_graph = true;
+  hipGraphExec_t gexec = nullptr;
+  const double* g_r = nullptr;
+  double* g_z = nullptr;
+  const void* g_plan = nullptr;  // the solve's SpMV plan the graph's fine products were captured with
+  ~Amg()
+  {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+  }
+  DevBuf<double> partial;
+  const void* key_rows = nullptr;
+  const void* key_vals = nullptr;
+  int64_t key_n = 0;
+};
+
+void AmgDeleter::operator()(Amg* a) const { delete a; }
+
+bool amg_available(const LinearSystem& ls)
+{
+  if (!ls.csr_rows || !ls.csr_cols || !ls.csr_vals || ls.n_rows <= 0) return false;
+  if (ls.halo && ls.halo->comm && comm_nranks(ls.halo->comm) > 1) return false;  // one rank
+  return ls.n_rows < (int64_t(1) << 31);
+}
+
+int amg_levels(const LinearSystem& ls) { return ls.amg ? (int)ls.amg->lv.size() : 0; }
+
+namespace {
+
+double host_sum(Ctx& ctx, const DevBuf<double>& partial, int n)
+{
+  std::vector<double> h(n);
+  AFEM_HIP(hipMemcpyAsync(h.data(), partial.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  double s = 0.0;
+  for (double v : h) s += v;
+  return s;
+}
+
+void spmv(Ctx& ctx, int epi, AmgLevel& L, const double* x, double* y, const double* b, double omega)
+{
+  const unsigned g = grid_for(L.n * 8, 256);
+  if (L.n == 0) return;
+  if (epi == 0)
+    hipLaunchKernelGGL(k_amg_spmv<0>, dim3(g), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci, L.v, x, y, b, L.dinv.p,
+                       omega);
+  else if (epi == 1)
+    hipLaunchKernelGGL(k_amg_spmv<1>, dim3(g), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci, L.v, x, y, b, L.dinv.p,
+                       omega);
+  else
+    hipLaunchKernelGGL(k_amg_spmv<2>, dim3(g), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci, L.v, x, y, b, L.dinv.p,
+                       omega);
+  AFEM_LAUNCHED();
+}
+
+double power_lambda(Ctx& ctx, Amg& a, AmgLevel& L)
+{
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
+  hipLaunchKernelGGL(k_amg_fill, dim3(g), dim3(256), 0, ctx.stream, L.n, L.in.p, L.x.p);
+  hipLaunchKernelGGL(k_amg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, (const double*)nullptr, L.x.p,
+                     a.partial.p);
+  AFEM_LAUNCHED();
+  double nv = std::sqrt(host_sum(ctx, a.partial, (int)g)), lam = 0.0;
+  for (int it = 0; it < kPowerIts; ++it) {
+    spmv(ctx, 0, L, L.x.p, L.t.p, nullptr, 0.0);
+    hipLaunchKernelGGL(k_amg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, (const double*)L.dinv.p, L.t.p,
+                       a.partial.p);
+    AFEM_LAUNCHED();
+    const double nw = std::sqrt(host_sum(ctx, a.partial, (int)g));
+    lam = nv > 0 ? nw / nv : 0.0;
+    if (!(nw > 0)) break;
+    hipLaunchKernelGGL(k_amg_mul, dim3(g), dim3(256), 0, ctx.stream, L.n, 1.0 / nw, L.t.p);
+    AFEM_LAUNCHED();
+    std::swap(L.x, L.t);
+    nv = 1.0;
+  }
+  return lam;
+}
+
+// the level's diagonal, graph membership, D^-1 and work vectors
+void level_prepare(Ctx& ctx, AmgLevel& L, const uint8_t* cons)
+{
+  L.diag.alloc(L.n > 0 ? L.n : 1);
+  L.in.alloc(L.n > 0 ? L.n : 1);
+  L.dinv.alloc(L.n > 0 ? L.n : 1);
+  for (auto* b : { &L.x, &L.t, &L.b, &L.r }) b->alloc(L.n > 0 ? L.n : 1);
+  if (L.n == 0) return;
+  hipLaunchKernelGGL(k_amg_diag, dim3(grid_for(L.n, 256)), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci, L.v, cons,
+                     L.diag.p, L.in.p);
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
+  hipLaunchKernelGGL(k_amg_inv, dim3(g), dim3(256), 0, ctx.stream, L.n, L.diag.p, L.in.p, L.dinv.p);
+  AFEM_LAUNCHED();
+}
+
+// aggregates of level L (L.agg, L.ap / L.mem); returns the aggregate count
+int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
+{
+  const int64_t n = L.n;
+  const unsigned g = grid_for(n, 256);
+  DevBuf<uint64_t> t, m;
+  t.alloc(n);
+  m.alloc(n);
+  hipLaunchKernelGGL(k_amg_tuple_init, dim3(g), dim3(256), 0, ctx.stream, n, L.in.p, t.p);
+  AFEM_LAUNCHED();
+  DevBuf<unsigned long long> left;
+  left.alloc(1);
+  DevBuf<uint8_t> strong;
+  strong.alloc(L.nnz > 0 ? L.nnz : 1);
+  const unsigned g8 = grid_for(n * 8, 256);
+  hipLaunchKernelGGL(k_amg_strength, dim3(g8), dim3(256), 0, ctx.stream, n, L.rp, L.ci, L.v, L.diag.p, L.in.p, theta,
+                     strong.p);
+  AFEM_LAUNCHED();
+  DevBuf<uint64_t> m2;
+  if (hops > 1) m2.alloc(n);
+  for (int round = 0; round < 64; ++round) {
+    // max over the distance-`hops` neighbourhood
+    hipLaunchKernelGGL(k_amg_maxprop, dim3(g8), dim3(256), 0, ctx.stream, n, L.rp, L.ci, (const uint8_t*)strong.p,
+                       (const uint64_t*)t.p, m.p);
+    for (int h = 1; h < hops; ++h) {
+      hipLaunchKernelGGL(k_amg_maxprop, dim3(g8), dim3(256), 0, ctx.stream, n, L.rp, L.ci, (const uint8_t*)strong.p,
+                         (const uint64_t*)m.p, m2.p);
+      std::swap(m, m2);
+    }
+    AFEM_HIP(hipMemsetAsync(left.p, 0, sizeof(unsigned long long), ctx.stream));
+    hipLaunchKernelGGL(k_amg_mis_update, dim3(g), dim3(256), 0, ctx.stream, n, t.p, (const uint64_t*)m.p, left.p);
+    AFEM_LAUNCHED();
+    unsigned long long hl = 0;
+    AFEM_HIP(hipMemcpyAsync(&hl, left.p, sizeof(hl), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    if (hl == 0) break;
+    AFEM_REQUIRE(round < 63, AFEM_ERR_STATE, "amg: the independent set did not converge");
+  }
+  DevBuf<int32_t> f;
+  DevBuf<int64_t> rank;
+  f.alloc(n);
+  rank.alloc(n + 1);
+  hipLaunchKernelGGL(k_amg_root_flags, dim3(g), dim3(256), 0, ctx.stream, n, (const uint64_t*)t.p, f.p);
+  AFEM_LAUNCHED();
+  exclusive_scan_i32_to_i64(ctx, f.p, rank.p, n);
+  const int64_t n_roots = read_i64(ctx, rank.p + n);
+  L.agg.alloc(n);
+  DevBuf<int32_t> agg2;
+  DevBuf<uint64_t> own, own2;
+  agg2.alloc(n);
+  own.alloc(n);
+  own2.alloc(n);
+  hipLaunchKernelGGL(k_amg_root_agg, dim3(g), dim3(256), 0, ctx.stream, n, (const uint64_t*)t.p, rank.p, L.agg.p,
+                     own.p);
+  AFEM_LAUNCHED();
+  for (int h = 0; h < hops; ++h) {
+    hipLaunchKernelGGL(k_amg_join, dim3(g), dim3(256), 0, ctx.stream, n, L.rp, L.ci, (const uint8_t*)strong.p,
+                       L.in.p, (const int32_t*)L.agg.p, (const uint64_t*)own.p, agg2.p, own2.p);
+    AFEM_LAUNCHED();
+    std::swap(L.agg, agg2);
+    std::swap(own, own2);
+  }
+  // orphans (no root within reach) become singletons after the roots' aggregates
+  hipLaunchKernelGGL(k_amg_orphans, dim3(g), dim3(256), 0, ctx.stream, n, L.in.p, L.agg.p, f.p);
+  AFEM_LAUNCHED();
+  exclusive_scan_i32_to_i64(ctx, f.p, rank.p, n);
+  const int64_t n_orph = read_i64(ctx, rank.p + n);
+  if (n_orph) {
+    hipLaunchKernelGGL(k_amg_orphan_agg, dim3(g), dim3(256), 0, ctx.stream, n, f.p, rank.p, (int32_t)n_roots,
+                       L.agg.p);
+    AFEM_LAUNCHED();
+  }
+  const int64_t nc = n_roots + n_orph;
+  // member lists
+  DevBuf<uint32_t> k1, k2;
+  DevBuf<int32_t> i1;
+  k1.alloc(n);
+  k2.alloc(n);
+  i1.alloc(n);
+  L.mem.alloc(n);
+  hipLaunchKernelGGL(k_amg_member_keys, dim3(g), dim3(256), 0, ctx.stream, n, L.agg.p, k1.p, i1.p);
+  AFEM_LAUNCHED();
+  size_t tb = 0;
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, i1.p, L.mem.p, (int)n, 0, 32, ctx.stream));
+  DevBuf<unsigned char> tmp;
+  tmp.alloc(tb > 0 ? tb : 1);
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, i1.p, L.mem.p, (int)n, 0, 32, ctx.stream));
+  L.ap.alloc(nc + 1);
+  AFEM_HIP(hipMemsetAsync(L.ap.p, 0, (nc + 1) * sizeof(int64_t), ctx.stream));
+  hipLaunchKernelGGL(k_amg_member_ptr, dim3(g), dim3(256), 0, ctx.stream, n, (const uint32_t*)k2.p, nc, L.ap.p);
+  AFEM_LAUNCHED();
+  ctx.sync();
+  return nc;
+}
+
+// C = P^T A P of level L's aggregates
+void galerkin(Ctx& ctx, AmgLevel& L, int64_t nc, AmgLevel& C)
+{
+  const int64_t nnz = L.nnz;
+  DevBuf<unsigned long long> key, key_s;
+  DevBuf<int64_t> src, src_s;
+  key.alloc(nnz > 0 ? nnz : 1);
+  key_s.alloc(nnz > 0 ? nnz : 1);
+  src.alloc(nnz > 0 ? nnz : 1);
+  src_s.alloc(nnz > 0 ? nnz : 1);
+  hipLaunchKernelGGL(k_amg_keys, dim3(grid_for(L.n, 256)), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci,
+                     (const int32_t*)L.agg.p, key.p);
+  hipLaunchKernelGGL(k_amg_iota, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz, src.p);
+  AFEM_LAUNCHED();
+  size_t tb = 0;
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.p, key_s.p, src.p, src_s.p, (int)nnz, 0, 64,
+                                              ctx.stream));
+  DevBuf<unsigned char> tmp;
+  tmp.alloc(tb > 0 ? tb : 1);
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, key.p, key_s.p, src.p, src_s.p, (int)nnz, 0, 64,
+                                              ctx.stream));
+  key.reset();
+  src.reset();
+  DevBuf<int32_t> head;
+  DevBuf<int64_t> hrank;
+  head.alloc(nnz > 0 ? nnz : 1);
+  hrank.alloc(nnz + 1);
+  hipLaunchKernelGGL(k_amg_heads, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz,
+                     (const unsigned long long*)key_s.p, head.p);
+  AFEM_LAUNCHED();
+  exclusive_scan_i32_to_i64(ctx, head.p, hrank.p, nnz);
+  const int64_t cnnz = read_i64(ctx, hrank.p + nnz);
+  DevBuf<int64_t> row_of;
+  row_of.alloc(cnnz > 0 ? cnnz : 1);
+  C.own_ci.alloc(cnnz > 0 ? cnnz : 1);
+  C.own_v.alloc(cnnz > 0 ? cnnz : 1);
+  hipLaunchKernelGGL(k_amg_runs, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz,
+                     (const unsigned long long*)key_s.p, src_s.p, L.v, head.p, hrank.p, row_of.p, C.own_ci.p,
+                     C.own_v.p);
+  AFEM_LAUNCHED();
+  C.own_rp.alloc(nc + 1);
+  AFEM_HIP(hipMemsetAsync(C.own_rp.p, 0, (nc + 1) * sizeof(int64_t), ctx.stream));
+  if (cnnz > 0) {
+    hipLaunchKernelGGL(k_amg_rowptr, dim3(grid_for(cnnz, 256)), dim3(256), 0, ctx.stream, cnnz, row_of.p, nc,
+                       C.own_rp.p);
+    AFEM_LAUNCHED();
+  }
+  ctx.sync();
+  C.n = nc;
+  C.nnz = cnnz;
+  C.rp = C.own_rp.p;
+  C.ci = C.own_ci.p;
+  C.v = C.own_v.p;
+}
+
+bool dense_inverse(Ctx& ctx, Amg& a, AmgLevel& L)
+{
+  const int m = (int)L.n;
+  std::vector<int64_t> rp(m + 1);
+  AFEM_HIP(hipMemcpyAsync(rp.data(), L.rp, (m + 1) * 8, hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  std::vector<int32_t> ci(rp[m]);
+  std::vector<double> v(rp[m]);
+  AFEM_HIP(hipMemcpyAsync(ci.data(), L.ci, rp[m] * 4, hipMemcpyDeviceToHost, ctx.stream));
+  AFEM_HIP(hipMemcpyAsync(v.data(), L.v, rp[m] * 8, hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  std::vector<double> A((size_t)m * m, 0.0);
+  for (int r = 0; r < m; ++r)
+    for (int64_t k = rp[r]; k < rp[r + 1]; ++k) A[(size_t)r * m + ci[k]] += v[k];
+  std::vector<double> sc(m);
+  for (int i = 0; i < m; ++i) {
+    if (!(A[(size_t)i * m + i] > 0)) return false;
+    sc[i] = 1.0 / std::sqrt(A[(size_t)i * m + i]);
+  }
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < m; ++j) A[(size_t)i * m + j] *= sc[i] * sc[j];
+  for (int j = 0; j < m; ++j) {
+    double d = A[(size_t)j * m + j];
+    for (int q = 0; q < j; ++q) d -= A[(size_t)j * m + q] * A[(size_t)j * m + q];
+    if (!(d > 1e-13)) return false;  // singular (no constraint reaches this level's operator): Jacobi sweeps
+    d = std::sqrt(d);
+    A[(size_t)j * m + j] = d;
+    for (int i = j + 1; i < m; ++i) {
+      double s = A[(size_t)i * m + j];
+      for (int q = 0; q < j; ++q) s -= A[(size_t)i * m + q] * A[(size_t)j * m + q];
+      A[(size_t)i * m + j] = s / d;
+    }
+  }
+  std::vector<double> inv((size_t)m * m), y(m);
+  for (int c = 0; c < m; ++c) {
+    for (int i = 0; i < m; ++i) {
+      double s = i == c ? 1.0 : 0.0;
+      for (int q = 0; q < i; ++q) s -= A[(size_t)i * m + q] * y[q];
+      y[i] = s / A[(size_t)i * m + i];
+    }
+    for (int i = m - 1; i >= 0; --i) {
+      double s = y[i];
+      for (int q = i + 1; q < m; ++q) s -= A[(size_t)q * m + i] * y[q];
+      y[i] = s / A[(size_t)i * m + i];
+    }
+    for (int i = 0; i < m; ++i) inv[(size_t)i * m + c] = y[i] * sc[i] * sc[c];
+  }
+  a.ainv.alloc((size_t)m * m);
+  AFEM_HIP(hipMemcpyAsync(a.ainv.p, inv.data(), inv.size() * 8, hipMemcpyHostToDevice, ctx.stream));
+  ctx.sync();
+  a.n_dense = m;
+  return true;
+}
+
+// fine: the system whose plan runs the level's products (level 0), else null
+void smooth(Ctx& ctx, Amg& a, AmgLevel& L, const double* b, int sweeps, bool from_zero, LinearSystem* fine)
+{
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
+  int s = 0;
+  if (from_zero) {
+    hipLaunchKernelGGL(k_amg_scale, dim3(g), dim3(256), 0, ctx.stream, L.n, L.omega, L.dinv.p, b, L.x.p);
+    AFEM_LAUNCHED();
+    s = 1;
+  }
+  for (; s < sweeps; ++s) {
+    if (fine) {
+      ls_spmv_planned(*fine, L.x.p, L.t.p);
+      hipLaunchKernelGGL(k_amg_jacobi, dim3(g), dim3(256), 0, ctx.stream, L.n, L.omega, L.dinv.p, b, L.t.p, L.x.p);
+      AFEM_LAUNCHED();
+    }
+    else {
+      spmv(ctx, 1, L, L.x.p, L.t.p, b, L.omega);
+      std::swap(L.x, L.t);
+    }
+  }
+}
+
+void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
+{
+  AmgLevel& L = a.lv[l];
+  if (l > 0) fine = nullptr;
+  if (l + 1 == a.lv.size()) {
+    if (a.n_dense == L.n && L.n > 0) {
+      hipLaunchKernelGGL(k_amg_gemv, dim3((unsigned)L.n), dim3(64), 0, ctx.stream, (int)L.n, a.ainv.p, b, L.x.p);
+      AFEM_LAUNCHED();
+    }
+    else {
+      smooth(ctx, a, L, b, l == 0 ? 2 * a.sweeps : kCoarseSweeps, true, fine);
+    }
+    return;
+  }
+  AmgLevel& C = a.lv[l + 1];
+  smooth(ctx, a, L, b, a.sweeps, true, fine);
+  if (fine) {
+    ls_spmv_planned(*fine, L.x.p, L.t.p);
+    const unsigned gv = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
+    hipLaunchKernelGGL(k_amg_resid, dim3(gv), dim3(256), 0, ctx.stream, L.n, b, L.t.p, L.r.p);
+    AFEM_LAUNCHED();
+  }
+  else {
+    spmv(ctx, 2, L, L.x.p, L.r.p, b, 0.0);
+  }
+  hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(C.n, 256)), dim3(256), 0, ctx.stream, C.n, L.ap.p, L.mem.p, L.r.p,
+                     C.b.p);
+  AFEM_LAUNCHED();
+  vcycle(ctx, a, l + 1, C.b.p, nullptr);
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
+  hipLaunchKernelGGL(k_amg_prolong, dim3(g), dim3(256), 0, ctx.stream, L.n, L.agg.p, a.scale, C.x.p, L.x.p);
+  AFEM_LAUNCHED();
+  smooth(ctx, a, L, b, a.sweeps, false, fine);
+}
+
+}  // namespace
+
+void amg_setup(LinearSystem& ls)
+{
+  Ctx& ctx = *ls.ctx;
+  AFEM_REQUIRE(amg_available(ls), AFEM_ERR_STATE, "amg: needs a CSR system on one rank");
+  if (ls.opts.amg == 2 && ls.amg && ls.amg->key_rows == ls.csr_rows && ls.amg->key_vals == ls.csr_vals &&
+      ls.amg->key_n == ls.n_rows)
+    return;
+  auto a = std::unique_ptr<Amg, AmgDeleter>(new Amg());
+  a->partial.alloc(kVec);
+  a->sweeps = (int)std::max(1.0, env_double("AFEM_AMG_SWEEPS", 1.0));
+  a->scale = env_double("AFEM_AMG_SCALE", 1.7);
+  a->fine_planned = env_double("AFEM_AMG_FINE_CSR", 0.0) == 0.0;
+  a->use_graph = env_double("AFEM_AMG_GRAPH", 0.0) != 0.0;
+  const double theta = env_double("AFEM_AMG_THETA", 0.08);
+  // aggregation distance: level 0 / the coarse levels (distance 1 stalls on the
+  // coarse Galerkin graphs: their degree falls with the level, r05w; distance 2
+  // everywhere: 108 iterations, 0.44 s with setup, at the unstructured leg's
+  // 11.5 M rows against 142 and 0.77 s for 1 / 2, r05aa)
+  const int hops0 = (int)std::min(2.0, std::max(1.0, env_double("AFEM_AMG_HOPS0", 2.0)));
+  const int hops = (int)std::min(2.0, std::max(1.0, env_double("AFEM_AMG_HOPS", 2.0)));
+  const int64_t dense = (int64_t)std::min(4096.0, std::max(1.0, env_double("AFEM_AMG_DENSE", kDense)));
+  {
+    AmgLevel L;
+    L.n = ls.n_rows;
+    L.nnz = ls.csr_nnz;
+    L.rp = ls.csr_rows;
+    L.ci = ls.csr_cols;
+    L.v = ls.csr_vals;
+    level_prepare(ctx, L, ls.cons.p);
+    a->lv.push_back(std::move(L));
+  }
+  const bool verbose = env_double("AFEM_AMG_VERBOSE", 0.0) > 0;
+  while ((int)a->lv.size() < kMaxLevels && a->lv.back().n > dense) {
+    AmgLevel& L = a->lv.back();
+    const int64_t nc = aggregate(ctx, L, theta, a->lv.size() == 1 ? hops0 : hops);
+    if (verbose) std::fprintf(stderr, "amg level %zu: %lld rows, %lld non-zeros -> %lld aggregates\n", a->lv.size() - 1,
+                              (long long)L.n, (long long)L.nnz, (long long)nc);
+    if (nc == 0 || nc * 10 > L.n * 9) {  // no coarse level, or coarsening stalls
+      L.agg.reset();
+      L.ap.reset();
+      L.mem.reset();
+      break;
+    }
+    AmgLevel C;
+    galerkin(ctx, L, nc, C);
+    level_prepare(ctx, C, nullptr);
+    a->lv.push_back(std::move(C));
+  }
+  for (auto& L : a->lv) {
+    // the power iteration approaches lambda_max from below: 10 % margin (an
+    // underestimate by 1.5x would make the smoother diverge)
+    const double lam = 1.1 * power_lambda(ctx, *a, L);
+    L.omega = lam > 0 ? 4.0 / (3.0 * lam) : 0.0;
+  }
+  AmgLevel& last = a->lv.back();
+  // the coarsest level inverted densely when small (a small system: the
+  // whole matrix, the PCG then converges in one or two iterations)
+  if (last.n <= dense) dense_inverse(ctx, *a, last);
+  a->key_rows = ls.csr_rows;
+  a->key_vals = ls.csr_vals;
+  a->key_n = ls.n_rows;
+  ls.amg = std::move(a);
+}
+
+namespace {
+void amg_apply_launch(LinearSystem& ls, const double* r, double* z);
+}
+
+void amg_apply(LinearSystem& ls, const double* r, double* z)
+{
+  Ctx& ctx = *ls.ctx;
+  Amg& a = *ls.amg;
+  if (!a.use_graph) {
+    amg_apply_launch(ls, r, z);
+    return;
+  }
+  if (!a.gexec || a.g_r != r || a.g_z != z || a.g_plan != ls.spmv_plan.get()) {
+    if (a.gexec) {
+      AFEM_HIP(hipGraphExecDestroy(a.gexec));
+      a.gexec = nullptr;
+    }
+    hipGraph_t graph = nullptr;
+    AFEM_HIP(hipStreamBeginCapture(ctx.stream, hipStreamCaptureModeThreadLocal));
+    try {
+      amg_apply_launch(ls, r, z);
+    }
+    catch (...) {
+      (void)hipStreamEndCapture(ctx.stream, &graph);
+      if (graph) (void)hipGraphDestroy(graph);
+      throw;
+    }
+    AFEM_HIP(hipStreamEndCapture(ctx.stream, &graph));
+    const hipError_t e = hipGraphInstantiate(&a.gexec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    AFEM_HIP(e);
+    a.g_r = r;
+    a.g_z = z;
+    a.g_plan = ls.spmv_plan.get();
+  }
+  AFEM_HIP(hipGraphLaunch(a.gexec, ctx.stream));
+}
+
+namespace {
+void amg_apply_launch(LinearSystem& ls, const double* r, double* z)
+{
+  Ctx& ctx = *ls.ctx;
+  Amg& a = *ls.amg;
+  AmgLevel& L0 = a.lv[0];
+  const int64_t n = ls.n_rows;
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (n + 255) / 256);
+  hipLaunchKernelGGL(k_amg_mask, dim3(g), dim3(256), 0, ctx.stream, n, ls.cons.p, r, L0.b.p);
+  AFEM_LAUNCHED();
+  // the fine level's products through the PCG's SpMV plan (AFEM_AMG_FINE_CSR=1: the 8-lane CSR kernel)
+  vcycle(ctx, a, 0, L0.b.p, a.fine_planned && ls.spmv_plan ? &ls : nullptr);
+  AFEM_HIP(hipMemcpyAsync(z, L0.x.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
+  hipLaunchKernelGGL(k_amg_fix, dim3(g), dim3(256), 0, ctx.stream, n, ls.cons.p, r, ls.dinv.p, z);
+  AFEM_LAUNCHED();
+}
+}  // namespace
+
+void amg_stats(const LinearSystem& ls, int32_t* levels, int64_t* coarse_rows, double* complexity)
+{
+  if (!ls.amg) {
+    *levels = 0;
+    *coarse_rows = 0;
+    *complexity = 0.0;
+    return;
+  }
+  *levels = (int32_t)ls.amg->lv.size();
+  *coarse_rows = ls.amg->lv.back().n;
+  double nz = 0.0;
+  for (const auto& L : ls.amg->lv) nz += (double)L.nnz;
+  *complexity = ls.amg->lv[0].nnz > 0 ? nz / (double)ls.amg->lv[0].nnz : 0.0;
+}
+
+}  // namespace afem

@@ -882,9 +882,13 @@ int afem_ls_set_solver_options(afem_ls* ls, const afem_solver_opts* o)
   AFEM_REQUIRE(o->precond_block == 0 || o->precond_block == 1 || o->precond_block == 3, AFEM_ERR_ARG,
                "precond_block must be 0, 1 or 3");
   AFEM_REQUIRE(o->multigrid >= 0 && o->multigrid <= 2, AFEM_ERR_ARG, "multigrid must be 0, 1 or 2");
+  AFEM_REQUIRE(o->amg >= 0 && o->amg <= 2, AFEM_ERR_ARG, "amg must be 0, 1 or 2");
+  AFEM_REQUIRE(!(o->amg && o->precond_block == 3), AFEM_ERR_ARG,
+               "amg and block Jacobi are alternative preconditioners");
   AFEM_REQUIRE(!(o->multigrid && o->precond_block == 3), AFEM_ERR_ARG,
                "multigrid and block Jacobi are alternative preconditioners");
   if (o->multigrid != ls->opts.multigrid) ls->mg.reset();
+  if (o->amg != ls->opts.amg) ls->amg.reset();
   ls->opts = *o;
   API_END
 }
@@ -1317,6 +1321,9 @@ int afem_elastodynamics_set_solver_options(afem_elastodynamics* h, const afem_so
   AFEM_REQUIRE(o->precond_block == 0 || o->precond_block == 1 || o->precond_block == 3, AFEM_ERR_ARG,
                "precond_block must be 0, 1 or 3");
   AFEM_REQUIRE(o->multigrid >= 0 && o->multigrid <= 2, AFEM_ERR_ARG, "multigrid must be 0, 1 or 2");
+  AFEM_REQUIRE(o->amg >= 0 && o->amg <= 2, AFEM_ERR_ARG, "amg must be 0, 1 or 2");
+  AFEM_REQUIRE(!(o->amg && o->precond_block == 3), AFEM_ERR_ARG,
+               "amg and block Jacobi are alternative preconditioners");
   AFEM_REQUIRE(!(o->multigrid && o->precond_block == 3), AFEM_ERR_ARG,
                "multigrid and block Jacobi are alternative preconditioners");
   h->d->ls.mg.reset();

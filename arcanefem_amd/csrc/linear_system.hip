@@ -6,6 +6,8 @@
 // (Aleph semantics, femutils/AlephDoFLinearSystem.cc:192-223,501-583).
 #include "afem_internal.hpp"
 
+#include <chrono>
+
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -1777,6 +1779,15 @@ void ls_apply_bcs(LinearSystem& ls)
   AFEM_LAUNCHED();
 }
 
+// y = A x with the plan of the current solve (single rank, no halo): the
+// algebraic multigrid's fine-level products run the PCG's own SpMV kernel
+void ls_spmv_planned(LinearSystem& ls, const double* x, double* y)
+{
+  AFEM_REQUIRE(ls.spmv_plan, AFEM_ERR_STATE, "no SpMV plan (outside a solve)");
+  const SpmvPlan& pl = *static_cast<const SpmvPlan*>(ls.spmv_plan.get());
+  launch_spmv(*ls.ctx, pl, ls.n_rows, ls.csr_rows, ls.csr_cols, ls.csr_vals, x, y, nullptr, ls.csr_nnz);
+}
+
 void ls_spmv(LinearSystem& ls, const double* x, double* y)
 {
   Ctx& ctx = *ls.ctx;
@@ -1861,6 +1872,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     AFEM_HIP(hipMemsetAsync(ls.p.p, 0, ls.p.bytes(), ctx.stream));
   }
   SpmvPlan pl = plan_spmv_ls(ctx, ls);
+  ls.spmv_plan = std::make_shared<SpmvPlan>(pl);  // the preconditioners' fine-level products (amg.hip)
   const int64_t n_part = 2 * std::max<int64_t>(pl.nblocks, kVecBlocks);
   if (ls.partial.n < (size_t)n_part) ls.partial.alloc(n_part);
   if (ls.cons.n != (size_t)n) ls.cons.alloc(n);
@@ -1892,15 +1904,30 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   }
   // geometric multigrid (structured box, one rank); other systems: point Jacobi
   // (several ranks: block-Jacobi V-cycles on the slabs' owned blocks, mg_available)
-  const bool use_mg = ls.opts.multigrid != 0 && !blk3 && mg_available(ls);
-  if (use_mg) mg_setup(ls);
+  const bool use_gmg = ls.opts.multigrid != 0 && !blk3 && mg_available(ls);
+  // algebraic multigrid where the geometric hierarchy does not exist (any mesh, one rank)
+  const bool use_amg = !use_gmg && ls.opts.amg != 0 && !blk3 && amg_available(ls);
+  const bool use_mg = use_gmg || use_amg;
+  if (use_gmg) mg_setup(ls);
+  double amg_setup_ms = 0.0;
+  if (use_amg) {
+    const auto t0 = std::chrono::steady_clock::now();
+    amg_setup(ls);
+    amg_setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  auto precond = [&](const double* rr, double* zz) {
+    if (use_amg)
+      amg_apply(ls, rr, zz);
+    else
+      mg_apply(ls, rr, zz);
+  };
   // r = b - A x0, z = M^-1 r, p = z and the r.z partials (all rows, free rows)
   auto cg_init = [&]() {
     if (use_mg) {
       hipLaunchKernelGGL(k_cg_init, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.rhs.p, ls.q.p, ls.r.p, ls.z.p,
                          ls.p.p, ls.dinv.p, ls.cons.p, ls.partial.p, ls.partial.p + vb);
       AFEM_LAUNCHED();
-      mg_apply(ls, ls.r.p, ls.z.p);
+      precond(ls.r.p, ls.z.p);
       AFEM_HIP(hipMemcpyAsync(ls.p.p, ls.z.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
       // r.z over all rows for both references (the constraint rows' z is r_i / a_ii: negligible)
       hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.r.p, ls.z.p, ls.partial.p);
@@ -2043,7 +2070,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
       hipLaunchKernelGGL(k_cg_xr, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.sol.p, ls.p.p, ls.r.p,
                          ls.q.p);
       AFEM_LAUNCHED();
-      mg_apply(ls, ls.r.p, ls.z.p);
+      precond(ls.r.p, ls.z.p);
       hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.r.p, ls.z.p, ls.partial.p);
       AFEM_LAUNCHED();
     }
@@ -2185,6 +2212,14 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     st->halo_bytes = ls.halo ? 8 * ls.halo->n_send : 0;
     st->n_halo = n_halo_loop;
     st->n_allreduce = n_ar_loop;
+    st->amg_setup_ms = amg_setup_ms;
+    if (use_amg)
+      amg_stats(ls, &st->amg_levels, &st->amg_coarse_rows, &st->amg_complexity);
+    else {
+      st->amg_levels = 0;
+      st->amg_coarse_rows = 0;
+      st->amg_complexity = 0.0;
+    }
     st->iterations = it;
     st->converged = fixed ? (rel <= o.rtol) : converged;
     st->rel_residual = rel;

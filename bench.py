@@ -70,9 +70,11 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true",
                     help="skip the CPU baselines (the oracle timed at the C2 size on the host cores, N = 1 only)")
     ap.add_argument("--no-extras", action="store_true", help="skip the side measurements (N = 1 only anyway)")
-    ap.add_argument("--legs", default="c4,c3,c2_generic,c2_arrays,c2_arrays_natural,unstructured,generic_unstructured,c5",
+    ap.add_argument("--legs", default="c4,c3,c2_generic,c2_arrays,c2_arrays_natural,unstructured,unstructured_solve,"
+                                      "generic_unstructured,c5",
                     help="the side measurements to run (comma list of c4, c3, c2_generic, c2_arrays, "
-                         "c2_arrays_natural, unstructured, generic_unstructured, c5)")
+                         "c2_arrays_natural, unstructured, unstructured_solve (the unstructured leg's system solved "
+                         "by the Jacobi- and the AMG-PCG), generic_unstructured, c5)")
     ap.add_argument("--no-headline", action="store_true",
                     help="N = 1: skip the headline C2 step (and the CPU baselines), run only --legs (per-leg "
                          "rocprofv3 runs, tools/profile_legs.sh)")
@@ -418,18 +420,25 @@ def refine_tets(cells, coords, levels, device):
     return c.to(torch.int32).cpu().numpy(), x.cpu().numpy()
 
 
-def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2, settle_ms=150.0):
+def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2, settle_ms=150.0, solve=False, rtol=1e-8):
     """An unstructured mesh at the C2 scale: the reference's L-shape-3D Gmsh
     mesh refined `levels` times (levels = 6: 68 M tets, 12 M DoF).  No brick
     order, no uniform slices: Hilbert-curve slices and the general strip
     instance.  Poisson assembly (+ source) on fixed sparsity, median kernel
-    time, roofline as C2's."""
+    time, roofline as C2's.  solve=True (`unstructured_solve` in --legs): the
+    assembled system with the z-min nodes clamped by penalty, solved to rtol
+    by the Jacobi-PCG and by the PCG with the algebraic multigrid V-cycle
+    (amg.hip; the reference's solve on such meshes is Hypre PCG + BoomerAMG,
+    femutils/HypreDoFLinearSystem.cc:686-742): iterations, setup and solve
+    times, and the two solutions' difference."""
     from arcanefem_amd.gmsh import read_gmsh
 
     gm = read_gmsh(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", mesh_file))
     cells, coords = refine_tets(gm.cells, gm.coords, levels, "cpu")
     mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
-    del cells, coords
+    z = coords[:, 2]
+    dn = np.nonzero(z <= z.min() + 1e-9 * max(1.0, abs(z.min())))[0].astype(np.int32) if solve else None
+    del cells, coords, z
     bsr = af.BSRFormat(mesh, 1).initialize(True)
     ctx.synchronize()
     t0 = time.perf_counter()
@@ -450,6 +459,37 @@ def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2, settle_ms=150
            "last_kernel": int(st["last_kernel"]), "max_slice_nodes": int(st["max_slice_nodes"]),
            "max_slice_width": int(st["max_slice_width"]), "sparsity_ms": round(sp_ms, 1)}
     ctx.free(rhs)
+    if solve:
+        ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes, mesh.n_nodes)
+        bsr.assemblePoissonP1(1.0, 5.5, ls.rhsVariable())
+        bsr.toLinearSystem(ls)
+        sols, res = {}, {}
+        for pc in ("jacobi", "amg"):
+            ls.applyDirichletViaPenalty(dn, 0.5, 1.0e30)
+            ls.setSolverOptions(rtol=rtol, max_iter=100000, method="pcg", preconditioner=pc)
+            t0 = time.perf_counter()
+            sst = ls.solve()
+            wall = (time.perf_counter() - t0) * 1e3
+            sols[pc] = ls.solution_host().copy()
+            r = {"iterations": int(sst["iterations"]), "converged": bool(sst["converged"]),
+                 "rel_residual": sst["rel_residual"], "solve_ms": round(sst["solve_ms"], 1),
+                 "wall_ms": round(wall, 1)}
+            if pc == "amg":
+                r.update(levels=int(sst["amg_levels"]), coarse_rows=int(sst["amg_coarse_rows"]),
+                         operator_complexity=round(sst["amg_complexity"], 3),
+                         setup_ms=round(sst["amg_setup_ms"], 1),
+                         ms_per_iteration=round((sst["solve_ms"] - sst["amg_setup_ms"]) / max(1, sst["iterations"]),
+                                                4))
+            else:
+                r["ms_per_iteration"] = round(sst["solve_ms"] / max(1, sst["iterations"]), 4)
+            res[pc] = r
+        res["rtol"] = rtol
+        res["dirichlet_nodes"] = int(dn.size)
+        res["max_rel_diff_amg_vs_jacobi"] = float(np.abs(sols["amg"] - sols["jacobi"]).max() /
+                                                  np.abs(sols["jacobi"]).max())
+        res["speedup_amg_vs_jacobi"] = round(res["jacobi"]["solve_ms"] / max(1e-9, res["amg"]["solve_ms"]), 2)
+        out["solve"] = res
+        del sols
     bsr.close()
     mesh.close()
     return out
@@ -821,8 +861,9 @@ def run_legs(ctx, af, args, legs):
         extras["c2_arrays"] = c2_arrays_leg(ctx, af, 215, settle_ms=sm)
     if "c2_arrays_natural" in legs:
         extras["c2_arrays_natural"] = c2_arrays_leg(ctx, af, 215, natural=True, settle_ms=sm)
-    if "unstructured" in legs and args.unstructured_levels > 0:
-        extras["unstructured"] = unstructured_leg(ctx, af, "L-shape-3D.msh", args.unstructured_levels, settle_ms=sm)
+    if ("unstructured" in legs or "unstructured_solve" in legs) and args.unstructured_levels > 0:
+        extras["unstructured"] = unstructured_leg(ctx, af, "L-shape-3D.msh", args.unstructured_levels, settle_ms=sm,
+                                                  solve="unstructured_solve" in legs)
     if "generic_unstructured" in legs and args.unstructured_levels > 0:
         extras["generic_unstructured"] = c2_generic_leg(ctx, af, 0, settle_ms=sm,
                                                         unstructured_levels=args.unstructured_levels)

@@ -403,6 +403,10 @@ typedef struct afem_solver_opts {
   int32_t profile_comm;     /* 1: time every halo wait and all-reduce of the PCG loop with HIP events on the
                                context stream (afem_solve_stats.halo_wait_ms / allreduce_ms; diagnostic, adds
                                event records to each iteration); 0: off (default) */
+  int32_t amg;              /* 0: off (default); 1: algebraic multigrid V-cycle preconditioner (aggregation AMG
+                               built from the CSR on the device: any mesh, one rank), rebuilt at every solve;
+                               2: built once and reused while the matrix arrays stay the same.  Where
+                               `multigrid` is set and the geometric hierarchy exists, that one is used. */
 } afem_solver_opts;
 
 typedef struct afem_solve_stats {
@@ -422,6 +426,11 @@ typedef struct afem_solve_stats {
   int64_t halo_bytes;   /* bytes this rank sends per halo exchange (8 per shared owned DoF and neighbour) */
   int32_t n_halo;       /* halo exchanges of the loop */
   int32_t n_allreduce;  /* scalar all-reduces of the loop */
+  /* the algebraic multigrid hierarchy of the solve (afem_solver_opts.amg; 0 without) */
+  int32_t amg_levels;
+  int64_t amg_coarse_rows;   /* rows of the coarsest level */
+  double amg_complexity;     /* operator complexity: non-zeros of all levels / the matrix's */
+  double amg_setup_ms;       /* host time of this solve's hierarchy build (0 when reused; inside solve_ms) */
 } afem_solve_stats;
 #define AFEM_SPMV_STREAM 0   /* CSR-stream (columns read from the CSR) */
 #define AFEM_SPMV_PATTERN 1  /* CSR-stream, interior-stencil rows form their columns */

@@ -1,0 +1,6 @@
+#!/bin/bash
+# round-5 GPU step y: AMG fine level through the PCG's SpMV plan; tests; probe of the cycle knobs
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests/test_gpu_amg.py > gpurun_out/r05y_amg_tests.log 2>&1 || exit $?
+timeout -k 10 900 python3 -u tools/amg_probe.py 6 1e-8 - AFEM_AMG_FINE_CSR=1 AFEM_AMG_SCALE=1.5 AFEM_AMG_SCALE=1.7 AFEM_AMG_HOPS0=2,AFEM_AMG_SCALE=1.7 AFEM_AMG_HOPS0=2,AFEM_AMG_SCALE=1.5 AFEM_AMG_SCALE=1.5,AFEM_AMG_THETA=0.04 > gpurun_out/r05y_amg.log 2>&1 || exit $?
