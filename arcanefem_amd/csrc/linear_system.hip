@@ -317,10 +317,6 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream4u(int64_t n_rows, int6
   const int64_t r1 = (r0 + kThreads < n_rows) ? r0 + kThreads : n_rows;
   const int64_t a = rows[r0], b = rows[r1];
   const int64_t q0 = (a & ~int64_t(3)) + 4 * (int64_t)threadIdx.x;
-  // the thread's row range for the final sum, loaded with the stream (not
-  // after the barrier: one memory round trip less per block)
-  const int64_t r = r0 + threadIdx.x;
-  const int64_t ra = r < r1 ? rows[r] : 0, re = r < r1 ? rows[r + 1] : 0;
   auto load4 = [&](int64_t q, int (&c)[4], double (&v)[4]) {
     if (q + 4 <= nnz) {
       const int4 c4 = *reinterpret_cast<const int4*>(cols + q);
@@ -393,10 +389,11 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream4u(int64_t n_rows, int6
     put4(q, v, xv);
   }
   __syncthreads();
+  const int64_t r = r0 + threadIdx.x;
   double d = 0.0;
   if (r < r1) {
     double s = 0.0;
-    for (int64_t k = ra - a, e = re - a; k < e; ++k) s += prod[k];
+    for (int64_t k = rows[r] - a, e = rows[r + 1] - a; k < e; ++k) s += prod[k];
     y[r] = s;
     if (DOT) d = x[r] * s;
   }
@@ -533,7 +530,7 @@ __global__ void k_pat_sample(int64_t n_rows, const int64_t* __restrict__ rows, c
   for (int k = 0; k < 16; ++k) out[17 * t + 1 + k] = k < len ? (int32_t)(cols[a + k] - r) : 0;
 }
 
-template <bool DOT, bool HOIST = false>
+template <bool DOT>
 __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t nnz, const int64_t* __restrict__ rows,
                                                        const int32_t* __restrict__ cols,
                                                        const double* __restrict__ vals,
@@ -554,31 +551,6 @@ __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t n
   const int64_t a = rows[r0], b = rows[r1];
   const int64_t a4 = a & ~int64_t(3);
   const int64_t r = r0 + threadIdx.x;
-  const int64_t q0 = a4 + 4 * (int64_t)threadIdx.x;
-  // the block's value stream: it depends only on the block's range, so
-  // HOIST = true has its loads in flight while the row offsets / flags arrive
-  // and the column image is written (kSpmvU groups of 4 per thread)
-  // (HOIST = false, the default: after the barrier; AFEM_SPMV_HOIST=1 before it)
-  double v[kSpmvU][4];
-  auto load_vals = [&]() {
-#pragma unroll
-    for (int u = 0; u < kSpmvU; ++u) {
-      const int64_t q = q0 + (int64_t)u * 4 * kThreads;
-      if (q < b && q + 4 <= nnz) {
-        const double2 v01 = *reinterpret_cast<const double2*>(vals + q);
-        const double2 v23 = *reinterpret_cast<const double2*>(vals + q + 2);
-        v[u][0] = v01.x;
-        v[u][1] = v01.y;
-        v[u][2] = v23.x;
-        v[u][3] = v23.y;
-      }
-      else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[u][j] = q < b && q + j < nnz ? vals[q + j] : 0.0;
-      }
-    }
-  };
-  if (HOIST) load_vals();
   int64_t ra = 0, re = 0;
   if (r < r1) {
     ra = rows[r];
@@ -593,12 +565,31 @@ __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t n
     }
   }
   __syncthreads();
-  if (!HOIST) load_vals();
+  const int64_t q0 = a4 + 4 * (int64_t)threadIdx.x;
+  auto load4 = [&](int64_t q, int (&c)[4], double (&v)[4]) {
+    const int4 c4 = *reinterpret_cast<const int4*>(cl + (q - a4));
+    c[0] = q >= a ? c4.x : 0;
+    c[1] = q + 1 >= a && q + 1 < b ? c4.y : 0;
+    c[2] = q + 2 >= a && q + 2 < b ? c4.z : 0;
+    c[3] = q + 3 >= a && q + 3 < b ? c4.w : 0;
+    if (q + 4 <= nnz) {
+      const double2 v01 = *reinterpret_cast<const double2*>(vals + q);
+      const double2 v23 = *reinterpret_cast<const double2*>(vals + q + 2);
+      v[0] = v01.x;
+      v[1] = v01.y;
+      v[2] = v23.x;
+      v[3] = v23.y;
+    }
+    else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = q + j < nnz ? vals[q + j] : 0.0;
+    }
+  };
   const int rot = (int)(threadIdx.x >> 3) & 3;
-  auto put4 = [&](int64_t q, const double (&vv)[4], const double (&xv)[4]) {
+  auto put4 = [&](int64_t q, const double (&v)[4], const double (&xv)[4]) {
     double pr[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pr[j] = vv[j] * xv[j];
+    for (int j = 0; j < 4; ++j) pr[j] = v[j] * xv[j];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = (t + rot) & 3;
@@ -608,19 +599,19 @@ __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t n
   };
   {
     int c[kSpmvU][4];
+    double v[kSpmvU][4];
 #pragma unroll
     for (int u = 0; u < kSpmvU; ++u) {
       const int64_t q = q0 + (int64_t)u * 4 * kThreads;
       if (q < b) {
-        const int4 c4 = *reinterpret_cast<const int4*>(cl + (q - a4));
-        c[u][0] = q >= a ? c4.x : 0;
-        c[u][1] = q + 1 >= a && q + 1 < b ? c4.y : 0;
-        c[u][2] = q + 2 >= a && q + 2 < b ? c4.z : 0;
-        c[u][3] = q + 3 >= a && q + 3 < b ? c4.w : 0;
+        load4(q, c[u], v[u]);
       }
       else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) c[u][j] = 0;
+        for (int j = 0; j < 4; ++j) {
+          c[u][j] = 0;
+          v[u][j] = 0.0;
+        }
       }
     }
     double xv[kSpmvU][4];
@@ -1595,15 +1586,12 @@ void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* ro
   }
   else if (pl.rpb == -3) {
     const size_t shm = (size_t)(8 * pl.max_seg + 32);
-    // AFEM_SPMV_HOIST=1: the value stream loaded before the column-image barrier
-    // (measured r05p, one process: C2 0.5685 vs 0.5611 ms per CG iteration, C4
-    // 6.161 vs 6.177: not kept)
-    const char* he = variant("AFEM_SPMV_HOIST");
-    const bool hoist = he && he[0] == '1';
-    auto* kern = partial ? (hoist ? &k_spmv_pat<true, true> : &k_spmv_pat<true, false>)
-                         : (hoist ? &k_spmv_pat<false, true> : &k_spmv_pat<false, false>);
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(kThreads), shm, ctx.stream, n_rows, nnz, rows, cols, vals, pl.pat_flag,
-                       pl.po, x, y, partial, pl.max_seg, nullptr);
+    if (partial)
+      hipLaunchKernelGGL(k_spmv_pat<true>, dim3(nb), dim3(kThreads), shm, ctx.stream, n_rows, nnz, rows, cols, vals,
+                         pl.pat_flag, pl.po, x, y, partial, pl.max_seg);
+    else
+      hipLaunchKernelGGL(k_spmv_pat<false>, dim3(nb), dim3(kThreads), shm, ctx.stream, n_rows, nnz, rows, cols, vals,
+                         pl.pat_flag, pl.po, x, y, partial, pl.max_seg);
   }
   else if (pl.rpb < 0) {
     if (partial)
