@@ -1642,7 +1642,8 @@ void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* ro
 constexpr int64_t kReduceChunks = 128;
 void reduce_to(Ctx& ctx, const double* partial, int64_t n, double* out, double* scratch = nullptr)
 {
-  if (scratch && n > 64 * 1024) {
+  const char* e2 = scratch ? variant("AFEM_REDUCE_2STAGE") : nullptr;  // =0: one workgroup (A/B)
+  if (scratch && !(e2 && e2[0] == '0') && n > 64 * 1024) {
     hipLaunchKernelGGL(k_reduce_chunks, dim3((unsigned)kReduceChunks), dim3(1024), 0, ctx.stream, n, partial, scratch);
     AFEM_LAUNCHED();
     partial = scratch;

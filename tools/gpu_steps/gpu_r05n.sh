@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-5 GPU step m: packed entries with patterns prefetched one group ahead; the unit kernel
+# round-5 GPU step n: packed entries with patterns prefetched one group ahead; the unit kernel
 # held to 3 waves per SIMD (AFEM_GENERIC_WAVES=3 build) -- A/B in one process per library
 export TMPDIR=/tmp
 mkdir -p gpurun_out
