@@ -530,8 +530,8 @@ __global__ void k_pat_sample(int64_t n_rows, const int64_t* __restrict__ rows, c
   for (int k = 0; k < 16; ++k) out[17 * t + 1 + k] = k < len ? (int32_t)(cols[a + k] - r) : 0;
 }
 
-template <bool DOT>
-__global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t nnz, const int64_t* __restrict__ rows,
+template <bool DOT, int BS = kThreads>
+__global__ __launch_bounds__(BS) void k_spmv_pat(int64_t n_rows, int64_t nnz, const int64_t* __restrict__ rows,
                                                        const int32_t* __restrict__ cols,
                                                        const double* __restrict__ vals,
                                                        const uint8_t* __restrict__ flag, PatOff po,
@@ -546,8 +546,8 @@ __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t n
   int32_t* cl = reinterpret_cast<int32_t*>(smem);
   // blist: the row blocks of this launch (the CG's interior / halo-boundary split)
   const int64_t blk = blist ? (int64_t)blist[blockIdx.x] : xcd_swizzle(blockIdx.x, gridDim.x);
-  const int64_t r0 = blk * kThreads;
-  const int64_t r1 = (r0 + kThreads < n_rows) ? r0 + kThreads : n_rows;
+  const int64_t r0 = blk * BS;
+  const int64_t r1 = (r0 + BS < n_rows) ? r0 + BS : n_rows;
   const int64_t a = rows[r0], b = rows[r1];
   const int64_t a4 = a & ~int64_t(3);
   const int64_t r = r0 + threadIdx.x;
@@ -602,7 +602,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t n
     double v[kSpmvU][4];
 #pragma unroll
     for (int u = 0; u < kSpmvU; ++u) {
-      const int64_t q = q0 + (int64_t)u * 4 * kThreads;
+      const int64_t q = q0 + (int64_t)u * 4 * BS;
       if (q < b) {
         load4(q, c[u], v[u]);
       }
@@ -621,7 +621,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_pat(int64_t n_rows, int64_t n
       for (int j = 0; j < 4; ++j) xv[u][j] = x[c[u][j]];
     __syncthreads();  // every column read before the products overwrite the column image
 #pragma unroll
-    for (int u = 0; u < kSpmvU; ++u) put4(q0 + (int64_t)u * 4 * kThreads, v[u], xv[u]);
+    for (int u = 0; u < kSpmvU; ++u) put4(q0 + (int64_t)u * 4 * BS, v[u], xv[u]);
   }
   __syncthreads();
   double d = 0.0;
@@ -1406,9 +1406,10 @@ struct SpmvPlan {
   int64_t blk_n = 0;
   const int64_t* blk_rows = nullptr;
   const int32_t* blk_cols = nullptr;
-  // rpb = -3: k_spmv_pat (pattern rows form their columns)
+  // rpb = -3: k_spmv_pat (pattern rows form their columns), rows per block bs
   const uint8_t* pat_flag = nullptr;
   PatOff po{};
+  int bs = kThreads;
 };
 
 __global__ void k_block_seg(int64_t n_rows, int rpb, const int64_t* __restrict__ row_ptr, unsigned long long* out)
@@ -1549,6 +1550,28 @@ SpmvPlan plan_spmv_ls(Ctx& ctx, const LinearSystem& ls)
         pl.rpb = -3;
         pl.po = po;
         pl.pat_flag = ls.pat_flag.p;
+        // row blocks of 64 (the default: one wave per block, 7.7 KB of LDS, its barriers
+        // wave-local): C2 0.503 vs 0.536 ms per CG iteration with 256, C4 5.64 vs 6.02
+        // (r05am, one process); AFEM_SPMV_BS=128 / 256 the larger blocks
+        const char* be = variant("AFEM_SPMV_BS");
+        const int bsz = be ? atoi(be) : 64;
+        if (bsz == 128 || bsz == 64) {
+          DevBuf<unsigned long long> mx;
+          mx.alloc(1);
+          AFEM_HIP(hipMemsetAsync(mx.p, 0, mx.bytes(), ctx.stream));
+          const int64_t nb128 = (ls.n_rows + bsz - 1) / bsz;
+          hipLaunchKernelGGL(k_block_seg, dim3(grid_for(nb128, 256)), dim3(256), 0, ctx.stream, ls.n_rows, bsz,
+                             ls.csr_rows, mx.p);
+          AFEM_LAUNCHED();
+          unsigned long long hm = 0;
+          AFEM_HIP(hipMemcpyAsync(&hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
+          ctx.sync();
+          if (hm + 3 <= (unsigned long long)(4 * bsz * kSpmvU)) {
+            pl.bs = bsz;
+            pl.max_seg = (int64_t)hm;
+            pl.nblocks = nb128;
+          }
+        }
         return pl;
       }
     }
@@ -1586,7 +1609,13 @@ void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* ro
   }
   else if (pl.rpb == -3) {
     const size_t shm = (size_t)(8 * pl.max_seg + 32);
-    if (partial)
+    if (pl.bs == 128 || pl.bs == 64) {
+      auto* kern = pl.bs == 128 ? (partial ? &k_spmv_pat<true, 128> : &k_spmv_pat<false, 128>)
+                                : (partial ? &k_spmv_pat<true, 64> : &k_spmv_pat<false, 64>);
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(pl.bs), shm, ctx.stream, n_rows, nnz, rows, cols, vals, pl.pat_flag,
+                         pl.po, x, y, partial, pl.max_seg, nullptr);
+    }
+    else if (partial)
       hipLaunchKernelGGL(k_spmv_pat<true>, dim3(nb), dim3(kThreads), shm, ctx.stream, n_rows, nnz, rows, cols, vals,
                          pl.pat_flag, pl.po, x, y, partial, pl.max_seg);
     else
@@ -1987,8 +2016,8 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   const bool overlap = multi && ((pl.rpb > 0 && pl.wide && pl.unroll) || pl.rpb == -2 || pl.rpb == -3);
   int64_t n_int = 0;
   if (overlap) {
-    // scalar rows per launch block: kThreads (CSR-stream) or K * 32 (node blocks)
-    const int rpb = pl.rpb == -2 ? pl.blk_k * 16 * kBlkRpg : kThreads;
+    // scalar rows per launch block: kThreads (CSR-stream), pl.bs (pattern) or K * 32 (node blocks)
+    const int rpb = pl.rpb == -2 ? pl.blk_k * 16 * kBlkRpg : pl.rpb == -3 ? pl.bs : kThreads;
     const uint64_t key = (uint64_t)(uintptr_t)ls.csr_rows ^ ((uint64_t)(uintptr_t)ls.csr_cols << 1) ^
                          ((uint64_t)n << 40) ^ (uint64_t)ls.csr_nnz ^ ((uint64_t)rpb << 52);
     if (ls.blist_key != key) {
@@ -2103,10 +2132,12 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
       const int64_t n_bd = pl.nblocks - n_int;
       auto part = [&](int64_t nbk, int64_t off) {
         if (nbk <= 0) return;
-        if (pl.rpb == -3)
-          hipLaunchKernelGGL(k_spmv_pat<true>, dim3((unsigned)nbk), dim3(kThreads), (size_t)(8 * pl.max_seg + 32),
-                             ctx.stream, n, ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, pl.pat_flag, pl.po,
-                             ls.p.p, ls.q.p, ls.partial.p + off, pl.max_seg, ls.blist.p + off);
+        if (pl.rpb == -3) {
+          auto* kern = pl.bs == 64 ? &k_spmv_pat<true, 64> : pl.bs == 128 ? &k_spmv_pat<true, 128> : &k_spmv_pat<true>;
+          hipLaunchKernelGGL(kern, dim3((unsigned)nbk), dim3(pl.bs), (size_t)(8 * pl.max_seg + 32), ctx.stream, n,
+                             ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, pl.pat_flag, pl.po, ls.p.p, ls.q.p,
+                             ls.partial.p + off, pl.max_seg, ls.blist.p + off);
+        }
         else if (pl.rpb != -2)
           hipLaunchKernelGGL(k_spmv_stream4u<true>, dim3((unsigned)nbk), dim3(kThreads), (size_t)pl.max_seg * 8,
                              ctx.stream, n, ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p,
