@@ -300,8 +300,8 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream4(int64_t n_rows, int64
 // 15-non-zero rows is ~4 groups per lane).  Longer segments finish in the
 // k_spmv_stream4 loop.
 constexpr int kSpmvU = 4;
-template <bool DOT>
-__global__ __launch_bounds__(kThreads) void k_spmv_stream4u(int64_t n_rows, int64_t nnz,
+template <bool DOT, int BS = kThreads>
+__global__ __launch_bounds__(BS) void k_spmv_stream4u(int64_t n_rows, int64_t nnz,
                                                             const int64_t* __restrict__ rows,
                                                             const int32_t* __restrict__ cols,
                                                             const double* __restrict__ vals,
@@ -313,8 +313,8 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream4u(int64_t n_rows, int6
   double* prod = reinterpret_cast<double*>(smem);
   // blist: the row blocks of this launch (the CG's interior / halo-boundary split)
   const int64_t blk = blist ? (int64_t)blist[blockIdx.x] : xcd_swizzle(blockIdx.x, gridDim.x);
-  const int64_t r0 = blk * kThreads;
-  const int64_t r1 = (r0 + kThreads < n_rows) ? r0 + kThreads : n_rows;
+  const int64_t r0 = blk * BS;
+  const int64_t r1 = (r0 + BS < n_rows) ? r0 + BS : n_rows;
   const int64_t a = rows[r0], b = rows[r1];
   const int64_t q0 = (a & ~int64_t(3)) + 4 * (int64_t)threadIdx.x;
   auto load4 = [&](int64_t q, int (&c)[4], double (&v)[4]) {
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream4u(int64_t n_rows, int6
     double v[kSpmvU][4];
 #pragma unroll
     for (int u = 0; u < kSpmvU; ++u) {
-      const int64_t q = q0 + (int64_t)u * 4 * kThreads;
+      const int64_t q = q0 + (int64_t)u * 4 * BS;
       if (q < b) {
         load4(q, c[u], v[u]);
       }
@@ -377,9 +377,9 @@ __global__ __launch_bounds__(kThreads) void k_spmv_stream4u(int64_t n_rows, int6
 #pragma unroll
       for (int j = 0; j < 4; ++j) xv[u][j] = x[c[u][j]];
 #pragma unroll
-    for (int u = 0; u < kSpmvU; ++u) put4(q0 + (int64_t)u * 4 * kThreads, v[u], xv[u]);
+    for (int u = 0; u < kSpmvU; ++u) put4(q0 + (int64_t)u * 4 * BS, v[u], xv[u]);
   }
-  for (int64_t q = q0 + (int64_t)kSpmvU * 4 * kThreads; q < b; q += 4 * kThreads) {
+  for (int64_t q = q0 + (int64_t)kSpmvU * 4 * BS; q < b; q += 4 * BS) {
     int c[4];
     double v[4];
     load4(q, c, v);
@@ -1452,6 +1452,24 @@ SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows, const int32_t*
     pl.max_seg = (int64_t)hm;
     pl.wide = (mode == 0 || mode == 3) && cols && vals && ((uintptr_t)cols & 15) == 0 && ((uintptr_t)vals & 15) == 0;
     pl.unroll = mode == 0;
+    // AFEM_SPMV_STREAM_BS=64 / 128: the unrolled stream kernel in smaller row blocks (its segment
+    // bound and block count for that size).  Not the default: unlike the pattern kernel (no column-image
+    // phase to overlap) it measured slower, C2 with the stream kernel 0.603 vs 0.597 ms per CG iteration,
+    // the unstructured system's Jacobi-PCG 0.812 vs 0.795-0.799 (r05ao)
+    const char* be = variant("AFEM_SPMV_STREAM_BS");
+    const int bsz = be ? atoi(be) : kThreads;
+    if (pl.unroll && pl.wide && (bsz == 64 || bsz == 128)) {
+      AFEM_HIP(hipMemsetAsync(mx.p, 0, mx.bytes(), ctx.stream));
+      const int64_t nbs = (n_rows + bsz - 1) / bsz;
+      hipLaunchKernelGGL(k_block_seg, dim3(grid_for(nbs, 256)), dim3(256), 0, ctx.stream, n_rows, bsz, rows, mx.p);
+      AFEM_LAUNCHED();
+      unsigned long long hs = 0;
+      AFEM_HIP(hipMemcpyAsync(&hs, mx.p, sizeof(hs), hipMemcpyDeviceToHost, ctx.stream));
+      ctx.sync();
+      pl.bs = bsz;
+      pl.max_seg = (int64_t)hs;
+      pl.nblocks = nbs;
+    }
   }
   else if (mode == 0 && hm >= 16ull * (unsigned long long)kThreads) {
     // long rows (block-3 elasticity: 45 non-zeros per scalar row): segments do
@@ -1630,7 +1648,13 @@ void launch_spmv(Ctx& ctx, const SpmvPlan& pl, int64_t n_rows, const int64_t* ro
                          partial);
   }
   else if (pl.rpb && pl.wide && pl.unroll) {
-    if (partial)
+    if (pl.bs == 64 || pl.bs == 128) {
+      auto* kern = pl.bs == 64 ? (partial ? &k_spmv_stream4u<true, 64> : &k_spmv_stream4u<false, 64>)
+                               : (partial ? &k_spmv_stream4u<true, 128> : &k_spmv_stream4u<false, 128>);
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(pl.bs), (size_t)pl.max_seg * 8, ctx.stream, n_rows, nnz, rows, cols,
+                         vals, x, y, partial, nullptr);
+    }
+    else if (partial)
       hipLaunchKernelGGL(k_spmv_stream4u<true>, dim3(nb), dim3(kThreads), (size_t)pl.max_seg * 8, ctx.stream, n_rows,
                          nnz, rows, cols, vals, x, y, partial);
     else
@@ -2017,7 +2041,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   int64_t n_int = 0;
   if (overlap) {
     // scalar rows per launch block: kThreads (CSR-stream), pl.bs (pattern) or K * 32 (node blocks)
-    const int rpb = pl.rpb == -2 ? pl.blk_k * 16 * kBlkRpg : pl.rpb == -3 ? pl.bs : kThreads;
+    const int rpb = pl.rpb == -2 ? pl.blk_k * 16 * kBlkRpg : pl.bs;
     const uint64_t key = (uint64_t)(uintptr_t)ls.csr_rows ^ ((uint64_t)(uintptr_t)ls.csr_cols << 1) ^
                          ((uint64_t)n << 40) ^ (uint64_t)ls.csr_nnz ^ ((uint64_t)rpb << 52);
     if (ls.blist_key != key) {
@@ -2139,9 +2163,14 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
                              ls.partial.p + off, pl.max_seg, ls.blist.p + off);
         }
         else if (pl.rpb != -2)
-          hipLaunchKernelGGL(k_spmv_stream4u<true>, dim3((unsigned)nbk), dim3(kThreads), (size_t)pl.max_seg * 8,
-                             ctx.stream, n, ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p,
-                             ls.partial.p + off, ls.blist.p + off);
+        {
+          auto* kern = pl.bs == 64    ? &k_spmv_stream4u<true, 64>
+                       : pl.bs == 128 ? &k_spmv_stream4u<true, 128>
+                                      : &k_spmv_stream4u<true>;
+          hipLaunchKernelGGL(kern, dim3((unsigned)nbk), dim3(pl.bs), (size_t)pl.max_seg * 8, ctx.stream, n,
+                             ls.csr_nnz, ls.csr_rows, ls.csr_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p + off,
+                             ls.blist.p + off);
+        }
         else if (pl.blk_k == 3)
           hipLaunchKernelGGL((k_spmv_blk<3, true>), dim3((unsigned)nbk), dim3(256), 0, ctx.stream, pl.blk_n,
                              pl.blk_rows, pl.blk_cols, ls.csr_vals, ls.p.p, ls.q.p, ls.partial.p + off,
