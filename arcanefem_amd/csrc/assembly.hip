@@ -3299,7 +3299,10 @@ void assemble_elasticity_tet(Bsr& b, double lambda, double mu2, double c0, const
         AFEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, fn, 192, shm));
         it = occ_wg.emplace(std::make_pair(fn, shm), q < 1 ? 1 : q).first;
       }
-      int64_t nblk = (int64_t)ctx.n_cu * it->second;
+      // AFEM_ELAST_WG_OCC: workgroups per CU of the persistent grid (diagnostic; default the occupancy)
+      const char* oe = variant("AFEM_ELAST_WG_OCC");
+      const int occ_wg_cu = oe && atoi(oe) > 0 ? std::min(atoi(oe), it->second) : it->second;
+      int64_t nblk = (int64_t)ctx.n_cu * occ_wg_cu;
       if (nblk > n_items) nblk = n_items < 8 ? 8 : n_items;
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(192), shm, ctx.stream, n_items, list, tk, (int)ucap2,
                          s.max_slice_w, b.order_per_block, s.perm.p, s.pos_rb.p, s.pos_dl.p, s.strip.p, s.lidx.p,
