@@ -298,6 +298,11 @@ struct Structure {
   DevBuf<int32_t> cube_phys;
   DevBuf<int64_t> cube_rb;
   DevBuf<uint64_t> cube_slot;
+  // the staged canonical path (cubes.hip, built at its first use): per CALLER
+  // row its lattice index and, per position p of its columns, the Kuhn offset
+  // o (0..14) whose value goes there (4 bits each)
+  DevBuf<int32_t> cube_lat;
+  DevBuf<uint64_t> cube_pinv;
 };
 
 struct LinearSystem;
@@ -351,6 +356,7 @@ struct Bsr {
   DevBuf<int32_t> gen_flag;  // error flag of the generic element-functor assembly (afem_bsr_assembly_view)
   FunctorPlan fplan;         // cell-unit plan of the generic assembly (built at its first use)
   HandOver hand;             // toLinearSystem in the caller's numbering (afem_bsr_to_csr32_mapped)
+  DevBuf<double> cube_stage; // staged canonical cube path: one 128-B line per lattice row (cubes.hip)
 };
 void bsr_csr32_mapped_build(Bsr& b, const int32_t* dof_of_host, int64_t n_dof_rows);
 double* bsr_csr32_mapped_values(Bsr& b);  // the values in the mapped CSR order (gathered, or aliased)

@@ -188,6 +188,7 @@ struct CubeCanon {
   const int32_t* phys;
   const int64_t* rb;
   const uint64_t* slot;
+  double* stage;  // STAGE: one 128-B line per lattice row
 };
 
 // V: variant bits (AFEM_CUBES_V; the default kCubesV is what every result
@@ -198,7 +199,10 @@ struct CubeCanon {
 // store per lane and x-run there (7 stores per layer instead of 14), 128
 // non-temporal value and RHS stores in the other flushes, 256 dummy rows for
 // the corners outside the unit (no zero selects; 64-row planes), 512 16-B
-// row stores in the canonical flush.  Diagnostic
+// row stores in the canonical flush, 1024 the canonical path STAGED (its rows
+// written in lattice order as one 128-B line each -- the 15 values by Kuhn
+// offset, the |det| sum at 15 -- and moved into the caller's rows by
+// k_cube_unstage, caller row by caller row: whole-line stores).  Diagnostic
 // ablations (values wrong): 1 no value stores in the complete-layer flush, 2
 // one LDS add per cube (the sum of its sums) instead of its 15, 4 no cube
 // arithmetic, 8 no complete-layer flush.  Measured (r05d/e, C2 / C4, one
@@ -206,8 +210,9 @@ struct CubeCanon {
 // adding 128 costs 5.6 % on the box and 11 % on the random arrays (r05h:
 // scattered 8-B RHS stores and 120-B rows are worse non-temporal); 256 on top
 // of 16 | 32 | 64: C2 0.4632 -> 0.4608 ms, C4 4.194 -> 4.097 ms (r05i); 512:
-// random-numbered arrays (canonical path) 1.581 -> 1.538 ms (r05k).
-constexpr int kCubesV = 16 | 32 | 64 | 256 | 512;
+// random-numbered arrays (canonical path) 1.581 -> 1.538 ms (r05k); 1024 there:
+// 1.539 -> 1.103 ms (r05as: 0.587 ms cube pass + 0.532 ms k_cube_unstage).
+constexpr int kCubesV = 16 | 32 | 64 | 256 | 512 | 1024;
 
 // register budget: 64-row planes + one coordinate layer = 17.3 KB of LDS, 9
 // waves per CU, so 2 per SIMD whatever the registers (256 VGPRs, no spill);
@@ -305,13 +310,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
   const int rx = lane % kRun, ry = lane / kRun;
   const int nx = cx0 + rx, ny = cy0 + ry;
   const bool full_flush_on = g.full_flush != 0;
+  constexpr bool STAGE = CANON && (DIAG & 1024) != 0;
   int64_t pf_rb = 0, pf_re = 0, pf_r = 0;
   uint64_t pf_slot = 0;
   double pf_rhs = 0.0;
   auto prefetch_rows = [&](int z) {  // clamped like load_layer: no branch
     const int zz = (z >= z0 && z < z1) ? z : z0;
     const int64_t li = (int64_t)local_layer(g, zz) * g.L + min(nx, g.npx - 1) + (int64_t)g.npx * min(ny, g.npy - 1);
-    if constexpr (CANON) {
+    if constexpr (STAGE) {
+      (void)li;  // the rows' maps are k_cube_unstage's
+    }
+    else if constexpr (CANON) {
       pf_r = cc.phys[li];
       pf_rb = cc.rb[li];
       pf_slot = cc.slot[li];
@@ -404,7 +413,63 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
     }
     wave_lds_order();
   };
+  // STAGE: node layer z's rows into their lattice-order lines, line L = the
+  // row's 15 values by Kuhn offset o and its |det| sum at 15 (an absent
+  // neighbour's value is the zero its slot holds and is never moved); x-run q
+  // = 7 lines = 112 consecutive doubles, one 16-B non-temporal store per lane
+  auto flush_stage = [&](int z) {
+    const int b = z & 1;
+    const bool valid = lane < kRows && nx < g.npx && ny < g.npy;
+    uint32_t mask = 0;
+#pragma unroll
+    for (int o = 0; o < 15; ++o) {
+      const int xx = nx + kOffX[o], yy = ny + kOffY[o], zz = z + kOffZ[o];
+      const uint32_t in = (uint32_t)(xx >= 0) & (uint32_t)(yy >= 0) & (uint32_t)(xx < g.npx) & (uint32_t)(yy < g.npy) &
+                          (uint32_t)(zz >= 0) & (uint32_t)(zz <= g.nzc);
+      mask |= in << o;
+    }
+    if (!valid) mask = 0;
+    double v[15];
+    double sum = 0.0;
+    const int lr = min(lane, STRIDE - 1);
+#pragma unroll
+    for (int o = 0; o < 15; ++o) {
+      v[o] = acc[b][o][lr];
+      if (o != 7 && ((mask >> o) & 1u)) sum += v[o];
+    }
+    const double meas = v[7];
+    v[7] = -sum;
+    wave_lds_order();  // every lane's accumulator reads before the image overwrites them
+    double* img = &acc[b][0][0];
+    if (lane < kRows) {  // 49 lines of 16 = 784 of the buffer's 960 doubles
+#pragma unroll
+      for (int o = 0; o < 15; ++o) img[16 * lane + o] = v[o];
+      img[16 * lane + 15] = meas;
+    }
+    wave_lds_order();
+    typedef double d2u __attribute__((ext_vector_type(2), aligned(16)));
+    const int64_t lz = (int64_t)local_layer(g, z) * g.L + cx0;
+    const bool xok = lane < 2 * 8 * kRun / 2 && cx0 + (lane >> 3) < g.npx;  // pair `lane` is line lane / 8's
+#pragma unroll
+    for (int q = 0; q < kRun; ++q) {
+      if (cy0 + q >= g.npy) break;  // uniform
+      // lanes without a line repeat lane 0's pair (same address, same values)
+      const int t = xok ? 2 * lane : 0;
+      const d2u w = d2u{ img[2 * 8 * kRun * q + t], img[2 * 8 * kRun * q + t + 1] };
+      __builtin_nontemporal_store(w, reinterpret_cast<d2u*>(&cc.stage[16 * (lz + (int64_t)g.npx * (cy0 + q)) + t]));
+    }
+    wave_lds_order();
+    double2* const img2 = reinterpret_cast<double2*>(img);
+#pragma unroll
+    for (int i = 0; i < (kAcc * STRIDE / 2 + 63) / 64; ++i)
+      img2[min(64 * i + lane, kAcc * STRIDE / 2 - 1)] = make_double2(0.0, 0.0);
+    wave_lds_order();
+  };
   auto flush = [&](int z) {
+    if constexpr (STAGE) {
+      flush_stage(z);
+      return;
+    }
     if constexpr (!CANON) {
       if (full_flush_on && layer_full(z)) {
         if constexpr (!(DIAG & 8)) flush_full(z);
@@ -846,13 +911,118 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
   }
 }
 
+// the staged canonical path's maps, per lattice node i (caller row phys[i]):
+// lat[row] = i, and for each position p of the row's columns the Kuhn offset o
+// whose value goes there (canonical slot t = the rank of o among the present
+// offsets, position = slot[i] >> 4t)
+__global__ void k_cube_stage_maps(int64_t n, int npx, int npy, int nzc, const int32_t* __restrict__ phys,
+                                  const uint64_t* __restrict__ slot, int32_t* __restrict__ lat,
+                                  uint64_t* __restrict__ pinv)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t L = (int64_t)npx * npy;
+  const int z = (int)(i / L);
+  const int64_t rem = i - (int64_t)z * L;
+  const int y = (int)(rem / npx), x = (int)(rem - (int64_t)y * npx);
+  uint32_t mask = 0;
+  for (int o = 0; o < 15; ++o) {
+    const int xx = x + kOffX[o], yy = y + kOffY[o], zz = z + kOffZ[o];
+    if (xx >= 0 && yy >= 0 && xx < npx && yy < npy && zz >= 0 && zz <= nzc) mask |= 1u << o;
+  }
+  const uint64_t sl = slot[i];
+  uint64_t w = 0;
+  for (int o = 0; o < 15; ++o)
+    if ((mask >> o) & 1u) {
+      const int t = __popc(mask & ((1u << o) - 1u));
+      const int pos = (int)((sl >> (4 * t)) & 15u);
+      w |= (uint64_t)o << (4 * pos);
+    }
+  const int32_t r = phys[i];
+  lat[r] = (int32_t)i;
+  pinv[r] = w;
+}
+
+// the staged canonical path, second pass: caller rows r = 64 w + lane of
+// wave w.  Each lane loads its row's lattice line (one aligned 128-B line:
+// 8 16-B loads), puts it in LDS, picks its values into the wave's image in
+// column order (row r at [rb_r - rb_0, +len)), and the wave stores the image
+// -- the 64 rows' values, contiguous in the caller's matrix -- with
+// consecutive lanes and 16-B stores: whole lines, where the single-pass
+// canonical flush wrote each 120-B row into lines that other units complete
+// at other times (WRITE_SIZE 1.77 GB for 1.28 GB)
+constexpr int kUnLine = 18;  // LDS doubles per line (16 + 2: 16-B aligned, lanes l and l + 16 share banks only)
+template <bool HAS_RHS, bool RHS_ADD>
+__global__ __launch_bounds__(64) void k_cube_unstage(int64_t n, const int64_t* __restrict__ rp,
+                                                      const int32_t* __restrict__ lat,
+                                                      const uint64_t* __restrict__ pinv,
+                                                      const double* __restrict__ stage, double f_meas,
+                                                      double* __restrict__ vals, double* __restrict__ rhs)
+{
+  __shared__ __align__(16) double line[64 * kUnLine];
+  __shared__ __align__(16) double out[64 * 15 + 2];
+  const int lane = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  const int64_t r = r0 + lane;
+  const bool valid = r < n;
+  const int64_t rc = valid ? r : n - 1;
+  const int64_t rb = rp[rc], re = rp[rc + 1];
+  const int64_t li = lat[rc];
+  const uint64_t m = pinv[rc];
+  typedef double d2a __attribute__((ext_vector_type(2), aligned(16)));
+  // load k: lanes 8 j .. 8 j + 7 read row 8 k + j's line, 16 B each (8 whole
+  // lines per instruction, not 64 pieces of 64 lines)
+  const int part = lane & 7;
+  d2a w[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t lk = __shfl((int)li, 8 * k + (lane >> 3));
+    w[k] = reinterpret_cast<const d2a*>(stage + 16 * lk)[part];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) reinterpret_cast<d2a*>(line + kUnLine * (8 * k + (lane >> 3)))[part] = w[k];
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if constexpr (HAS_RHS) {
+    const double meas = line[kUnLine * lane + 15];
+    if (valid) rhs[r] = RHS_ADD ? rhs[r] + f_meas * meas : f_meas * meas;
+  }
+  const int nv = (int)min((int64_t)64, n - r0);  // rows of this wave
+  const int64_t rb0 = rp[r0], re1 = rp[r0 + nv];
+  const int a = (int)(rb0 & 1);  // image offset: pairs 16-B aligned in the matrix
+  const int len = valid ? (int)(re - rb) : 0;
+  const int base = a + (int)(rb - rb0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int p = 0; p < 15; ++p)
+    if (p < len) out[base + p] = line[kUnLine * lane + (int)((m >> (4 * p)) & 15u)];
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const int total = a + (int)(re1 - rb0);
+#pragma unroll
+  for (int k = 0; k < (64 * 15 + 2) / 128 + 1; ++k) {
+    const int j = 2 * (64 * k + lane);
+    if (j < total) {
+      double* const g = vals + (rb0 - a + j);
+      const bool lo = j >= a, hi = j + 1 < total;
+      if (lo && hi)
+        *reinterpret_cast<d2a*>(g) = d2a{ out[j], out[j + 1] };
+      else if (lo)
+        g[0] = out[j];
+      else if (hi)
+        g[1] = out[j + 1];
+    }
+  }
+}
+
 }  // namespace
 
 bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
 {
   const Mesh& m = *b.mesh;
   const StructuredInfo& st = m.st;
-  const Structure& S = b.s;
+  Structure& S = b.s;
   const char* ce = variant("AFEM_ASSEMBLY_CUBES");  // 0: the strip / stencil kernels
   if ((ce && atoi(ce) == 0) || m.nv != 4 || b.nb_dof != 1) return false;
   // a generator box (or z-slab of one), a lattice of Kuhn cubes in a natural
@@ -919,7 +1089,10 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
        : &k_assemble_cubes<S, C, X, Y, N, false, false>)
   const char* de = variant("AFEM_CUBES_V");
   const int diag = de ? atoi(de) : kCubesV;
-  auto* kern = canon ? AFEM_CUBES_K(64, true, true, true, true)
+  // canonical structures: the staged instance (below), or the single-pass one (V without 1024)
+  auto* kern = canon ? (rhs ? (rhs_add ? &k_assemble_cubes<64, true, true, true, true, true, true, kCubesV & ~1024>
+                                       : &k_assemble_cubes<64, true, true, true, true, true, false, kCubesV & ~1024>)
+                            : &k_assemble_cubes<64, true, true, true, true, false, false, kCubesV & ~1024>)
                : carry ? (xex ? (yex ? (s49 ? AFEM_CUBES_K(49, true, true, true, false)
                                             : AFEM_CUBES_K(64, true, true, true, false))
                                      : AFEM_CUBES_K(64, true, true, false, false))
@@ -936,15 +1109,52 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
                  : &k_assemble_cubes<64, true, true, true, false, true, false, D>;                                  \
     break;
       AFEM_CUBES_D(0) AFEM_CUBES_D(112) AFEM_CUBES_D(kCubesV | 1) AFEM_CUBES_D(kCubesV | 4)
-      AFEM_CUBES_D(kCubesV | 8) AFEM_CUBES_D(kCubesV | 2) AFEM_CUBES_D(kCubesV & ~512)
+      AFEM_CUBES_D(kCubesV | 8) AFEM_CUBES_D(kCubesV | 2) AFEM_CUBES_D(kCubesV & ~512) AFEM_CUBES_D(kCubesV & ~1024)
 #undef AFEM_CUBES_D
       default: break;
     }
   }
-  const CubeCanon cc{ canon ? S.cube_phys.p : nullptr, canon ? S.cube_rb.p : nullptr, canon ? S.cube_slot.p : nullptr };
+  CubeCanon cc{ canon ? S.cube_phys.p : nullptr, canon ? S.cube_rb.p : nullptr, canon ? S.cube_slot.p : nullptr,
+                nullptr };
+  // the canonical path staged (V bit 1024): the cube kernel writes lattice-order
+  // lines (no row maps, no RHS), k_cube_unstage moves them into the caller's rows
+  const bool staged = canon && (diag & 1024) != 0;
+  if (staged) {
+    const int64_t n_lat = g.L * (int64_t)(g.nzc + 1);
+    AFEM_REQUIRE(n_lat == S.n_rows, AFEM_ERR_STATE, "cube kernel: lattice and rows differ");
+    if (S.cube_lat.n != (size_t)n_lat) {
+      S.cube_lat.alloc(n_lat);
+      S.cube_pinv.alloc(n_lat);
+      hipLaunchKernelGGL(k_cube_stage_maps, dim3(grid_for(n_lat, 256)), dim3(256), 0, ctx.stream, n_lat, g.npx, g.npy,
+                         g.nzc, S.cube_phys.p, S.cube_slot.p, S.cube_lat.p, S.cube_pinv.p);
+      AFEM_LAUNCHED();
+    }
+    if (b.cube_stage.n != (size_t)(16 * n_lat)) b.cube_stage.alloc(16 * n_lat);
+    cc.stage = b.cube_stage.p;
+    kern = &k_assemble_cubes<64, true, true, true, true, false, false, kCubesV | 1024>;
+    if (diag != kCubesV) {
+      switch (diag) {
+#define AFEM_CUBES_S(D)                                                                                              \
+  case D:                                                                                                            \
+    kern = &k_assemble_cubes<64, true, true, true, true, false, false, D>;                                          \
+    break;
+        AFEM_CUBES_S(kCubesV | 1024 | 1) AFEM_CUBES_S(kCubesV | 1024 | 4)
+#undef AFEM_CUBES_S
+        default: break;
+      }
+    }
+  }
   hipLaunchKernelGGL(kern, dim3((unsigned)n_units), dim3(64), 0, ctx.stream, g, S.row_ptr.p, m.coords.p, b.values.p,
                      rhs, cc);
   AFEM_LAUNCHED();
+  if (staged) {
+    const int64_t n = S.n_rows;
+    auto* un = rhs ? (rhs_add ? &k_cube_unstage<true, true> : &k_cube_unstage<true, false>)
+                   : &k_cube_unstage<false, false>;
+    hipLaunchKernelGGL(un, dim3((unsigned)grid_for(n, 64)), dim3(64), 0, ctx.stream, n, S.row_ptr.p, S.cube_lat.p,
+                       S.cube_pinv.p, b.cube_stage.p, g.f_meas, b.values.p, rhs);
+    AFEM_LAUNCHED();
+  }
   b.last_kernel = AFEM_KERNEL_CUBES;
   return true;
 }

@@ -714,6 +714,40 @@ def test_cube_kernel_on_random_numbering(ctx, n, nz, seed):
         _check_values(b2.download()[2], v1)
 
 
+CUBES_V = 16 | 32 | 64 | 256 | 512 | 1024  # cubes.hip kCubesV
+
+
+@pytest.mark.parametrize("n,nz,seed", [(6, 6, 3), (9, 15, 4), (13, 5, 5), (20, 7, 8)])
+def test_cube_kernel_staged_canonical(ctx, variant, n, nz, seed):
+    """The canonical cube path staged (V bit 1024: lattice-order 128-B lines,
+    then k_cube_unstage into the caller's rows) against the single-pass
+    canonical flush: the same matrix and RHS bits, set and add RHS modes, an
+    assembly repeated on the same structure (maps and stage built once)."""
+    m0 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=seed)
+    cells0, coords0, _ = m0.download()
+    rng = np.random.default_rng(seed)
+    nn = coords0.shape[0]
+    p = rng.permutation(nn)
+    cells = p[cells0].astype(np.int32)[rng.permutation(cells0.shape[0])]
+    coords = np.empty_like(coords0)
+    coords[p] = coords0
+    m1 = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    out = {}
+    for staged in (False, True):
+        variant("AFEM_CUBES_V", None if staged else str(CUBES_V & ~1024))
+        b1, l1 = _assemble_gpu(ctx, m1, 5.5)
+        assert b1.stats()["last_kernel"] == 10
+        rhs = l1.rhs_host()
+        b1.assemblePoissonP1(1.0, 5.5, l1.rhsVariable(), rhs_mode="add")
+        out[staged] = (b1.download(), rhs, l1.rhs_host())
+    (r0, c0, v0), s0, a0 = out[False]
+    (r1, c1, v1), s1, a1 = out[True]
+    assert np.array_equal(r0, r1) and np.array_equal(c0, c1)
+    assert np.array_equal(v0, v1)
+    assert np.array_equal(s0, s1)
+    assert np.array_equal(a0, a1)
+
+
 AXIS_ORDERS = [(0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1), (2, 1, 0)]
 
 

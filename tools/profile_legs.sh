@@ -19,7 +19,7 @@ for LEG in "$@"; do
     c4) B="bench.py --no-headline --legs c4"; K="k_assemble_cubes" ;;
     c3) B="bench.py --no-headline --legs c3"; K="k_assemble_elast" ;;
     c2_generic) B="bench.py --no-headline --legs c2_generic"; K="k_assemble_units" ;;
-    c2_arrays) B="bench.py --no-headline --legs c2_arrays"; K="k_assemble_cubes" ;;
+    c2_arrays) B="bench.py --no-headline --legs c2_arrays"; K="k_assemble_cubes|k_cube_unstage" ;;
     c2_arrays_natural) B="bench.py --no-headline --legs c2_arrays_natural"; K="k_assemble_cubes" ;;
     unstructured) B="bench.py --no-headline --legs unstructured"; K="k_assemble_strip" ;;
     generic_unstructured) B="bench.py --no-headline --legs generic_unstructured"; K="k_assemble_units" ;;
