@@ -3026,8 +3026,15 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       // the small lists' waves are dispatched first and the stencil grid fills
       // the rest of the chip beside them
       const bool k_side = use_k && side_mode == 2 && (s.n_ms > 0 || s.n_mb > 0);
+      // without uniform slices: the compact list, then the big one, on the context
+      // stream (AFEM_ASSEMBLY_BIG=2, the default); =1 the big list first; =0 the big
+      // list beside the compact one on the side stream.  Refined L-shape-3D (r05au,
+      // one process): 1.289 / 1.289 / 1.310 ms -- side by side, the two persistent
+      // grids share the chip and the big one's tail sets the end
+      const char* bge = variant("AFEM_ASSEMBLY_BIG");
+      const int big_mode = has_u ? 0 : (bge ? atoi(bge) : 2);
       const bool fork = k_side || (!serial_k && ((has_u && (s.n_ms > 0 || s.n_mb > 0 || (use_k && s.n_ur > 0))) ||
-                                                 (!has_u && s.n_ms > 0 && s.n_mb > 0)));
+                                                 (!has_u && big_mode == 0 && s.n_ms > 0 && s.n_mb > 0)));
       hipStream_t side = ctx.stream;
       if (fork) {
         side = ctx.side();
@@ -3040,7 +3047,13 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       const bool mb_ok = s.mb_w <= 32 && s.n_mb >= 0 && shm_mb <= kTileLdsMax;
       AFEM_REQUIRE(s.n_mb == 0 || (mb_ok && s.max_strip_c <= 4), AFEM_ERR_STATE, "strip lists exceed the kernels");
       hipStream_t s_ms = has_u && !serial_k ? side : ctx.stream;
-      hipStream_t s_mb = has_u && !serial_k ? side : (s.n_ms > 0 && !serial_k ? side : ctx.stream);
+      hipStream_t s_mb = has_u && !serial_k ? side : (s.n_ms > 0 && !serial_k && big_mode == 0 ? side : ctx.stream);
+      auto launch_mb = [&]() {
+        if (s.n_mb > 0)
+          launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 4, 32, 0>), k_assemble_strip<4, 4, 32, 0>, s.n_mb,
+                   s.rec_mb.p, tk0 + 256, shm_mb, s_mb, s.mb_nodes, s.mb_w);
+      };
+      if (big_mode == 1) launch_mb();
       // AFEM_ASSEMBLY_LOCAL=1: the compact list's slices of <= 256 nodes through the
       // local-index-stream instance (UMODE 3: no column-index table, no dependent
       // LDS read per step), the rest through UMODE 0.  Measured on the refined
@@ -3057,9 +3070,7 @@ void assemble_scalar(Bsr& b, double coef, double f, double* rhs, int rhs_add)
       if (s.n_ms > n_loc)
         launch_s(AFEM_SKF(4, 2, 16, 0), AFEM_SK(4, 2, 16, 0), s.n_ms - n_loc,
                  s.rec_ms.p + n_loc, tk0 + 128, shm_ms, s_ms, s.ms_nodes, ms_w);
-      if (s.n_mb > 0)
-        launch_s(reinterpret_cast<const void*>(&k_assemble_strip<4, 4, 32, 0>), k_assemble_strip<4, 4, 32, 0>, s.n_mb,
-                 s.rec_mb.p, tk0 + 256, shm_mb, s_mb, s.mb_nodes, s.mb_w);
+      if (big_mode != 1) launch_mb();
       if (use_k) {
         if (s.n_ur > 0) {
           const size_t shm_ur = (size_t)(8 * 64 * (int64_t)s.ur_w + strip_coord_bytes(dimc, s.ur_nodes, s.ur_w));

@@ -1118,10 +1118,10 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
                 nullptr };
   // the canonical path staged (V bit 1024): the cube kernel writes lattice-order
   // lines (no row maps, no RHS), k_cube_unstage moves them into the caller's rows
-  const bool staged = canon && (diag & 1024) != 0;
+  // (every lattice node one of this structure's rows, as canonical_lattice builds it)
+  const int64_t n_lat = g.L * (int64_t)(g.nzc + 1);
+  const bool staged = canon && (diag & 1024) != 0 && n_lat == S.n_rows;
   if (staged) {
-    const int64_t n_lat = g.L * (int64_t)(g.nzc + 1);
-    AFEM_REQUIRE(n_lat == S.n_rows, AFEM_ERR_STATE, "cube kernel: lattice and rows differ");
     if (S.cube_lat.n != (size_t)n_lat) {
       S.cube_lat.alloc(n_lat);
       S.cube_pinv.alloc(n_lat);
