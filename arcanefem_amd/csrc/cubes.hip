@@ -363,8 +363,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
       put<(DIAG & 128) != 0>(&rhs[valid ? pf_r : r0], valid ? rv : rv0);
     }
     const int64_t rb = pf_rb;
-    wave_lds_order();  // every lane's accumulator reads before the image overwrites them
     double* img = &acc[b][0][0];
+    // (each lane storing its own row from registers instead -- 7 16-B stores at a
+    // 120-B lane stride -- measured 3.19 against 0.456 ms, r05aw: the image stays)
+    wave_lds_order();  // every lane's accumulator reads before the image overwrites them
     // row L at [15 L, 15 L + 15): lanes past the 49 rows write into
     // [735, 960) of the buffer, which no store reads (64-row planes), or --
     // 49-row planes, whose buffer ends at 735 -- repeat row 48's writes with
@@ -383,7 +385,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
 #pragma unroll
     for (int q = 0; q < kRun; ++q) {
       const int64_t dst = lane_i64(rb, kRun * q);
-      if constexpr ((DIAG & 64) != 0) {
+      if constexpr ((DIAG & 1) != 0) {
+        (void)dst;  // diagnostic: no value stores
+      }
+      else if constexpr ((DIAG & 64) != 0) {
         const double a0 = img[15 * kRun * q + t2], a1 = img[15 * kRun * q + t2 + 1];
         typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
         if constexpr ((DIAG & 32) != 0)
@@ -395,7 +400,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(cube_waves<S
         __builtin_nontemporal_store(img[15 * kRun * q + lane], &vals[dst + lane]);
         __builtin_nontemporal_store(img[15 * kRun * q + t1], &vals[dst + t1]);
       }
-      else if constexpr (!(DIAG & 1)) {
+      else {
         vals[dst + lane] = img[15 * kRun * q + lane];
         vals[dst + t1] = img[15 * kRun * q + t1];
       }
@@ -1110,6 +1115,7 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
     break;
       AFEM_CUBES_D(0) AFEM_CUBES_D(112) AFEM_CUBES_D(kCubesV | 1) AFEM_CUBES_D(kCubesV | 4)
       AFEM_CUBES_D(kCubesV | 8) AFEM_CUBES_D(kCubesV | 2) AFEM_CUBES_D(kCubesV & ~512) AFEM_CUBES_D(kCubesV & ~1024)
+      AFEM_CUBES_D(kCubesV & ~32)
 #undef AFEM_CUBES_D
       default: break;
     }

@@ -25,6 +25,9 @@ VAL_TOL = 1e-12
 SOL_TOL = 1e-10
 
 
+CUBES_V = 16 | 32 | 64 | 256 | 512 | 1024  # cubes.hip kCubesV
+
+
 def _assemble_gpu(ctx, mesh, f):
     bsr = af.BSRFormat(mesh, 1).initialize(True)
     bsr.computeSparsity()
@@ -712,9 +715,6 @@ def test_cube_kernel_on_random_numbering(ctx, n, nz, seed):
         assert np.array_equal(b2.download()[2], v1)
     else:
         _check_values(b2.download()[2], v1)
-
-
-CUBES_V = 16 | 32 | 64 | 256 | 512 | 1024  # cubes.hip kCubesV
 
 
 @pytest.mark.parametrize("n,nz,seed", [(6, 6, 3), (9, 15, 4), (13, 5, 5), (20, 7, 8)])
