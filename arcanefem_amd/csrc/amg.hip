@@ -26,10 +26,16 @@
 //    fine level's products through the PCG's own SpMV plan; coarsest level (<= 1024 rows,
 //    AFEM_AMG_DENSE) inverted densely (host Cholesky at setup), else 24
 //    Jacobi sweeps;
+//  * K-cycle (AFEM_AMG_KCYCLE, default 2): levels 1..k solve their coarse
+//    problem by two flexible-CG steps preconditioned by the cycle below
+//    (Notay & Vassilevski), the step weights computed on the device -- the
+//    Krylov weights replace the 1.7 overcorrection there;
 //  * constraint rows are taken out of the cycle as in multigrid.hip:
 //    z = F V(F r) + C D^-1 r.
-// One rank (the system carries no halo); a symmetric V-cycle, so the PCG's
-// preconditioner stays SPD.
+// One rank (the system carries no halo).  The V-cycle is symmetric (an SPD
+// preconditioner); the K-cycle is a nonlinear one: the PCG keeps its
+// Fletcher-Reeves beta, which converges to the same solution (tested against
+// the Jacobi-PCG and the plain V-cycle, test_amg_kcycle).
 #include "afem_internal.hpp"
 
 #include <hipcub/hipcub.hpp>
@@ -422,6 +428,87 @@ __global__ __launch_bounds__(64) void k_amg_gemv(int n, const double* __restrict
   if (threadIdx.x == 0) x[i] = s;
 }
 
+// K-cycle (Notay-Vassilevski): the coarse problem of a level solved by two
+// flexible-CG steps preconditioned by the cycle below.  Dot products: block
+// partials over a fixed grid, summed in a fixed order by one block
+constexpr int kDotGrid = 256;
+template <int ND>
+__global__ __launch_bounds__(256) void k_amg_dots(int64_t n, const double* __restrict__ a0, const double* __restrict__ b0,
+                                                  const double* __restrict__ a1, const double* __restrict__ b1,
+                                                  const double* __restrict__ a2, const double* __restrict__ b2,
+                                                  double* __restrict__ partial)
+{
+  __shared__ double sh[ND][256];
+  double s[3] = { 0.0, 0.0, 0.0 };
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    s[0] += a0[i] * b0[i];
+    if (ND > 1) s[1] += a1[i] * b1[i];
+    if (ND > 2) s[2] += a2[i] * b2[i];
+  }
+#pragma unroll
+  for (int d = 0; d < ND; ++d) sh[d][threadIdx.x] = s[d];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+#pragma unroll
+      for (int d = 0; d < ND; ++d) sh[d][threadIdx.x] += sh[d][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < ND) partial[ND * blockIdx.x + threadIdx.x] = sh[threadIdx.x][0];
+}
+
+// the step coefficients from the partials (one block).  STEP 1: rho1 = c1.v1,
+// alpha1 = c1.r / rho1.  STEP 2: gamma = c2.v1, beta = c2.v2, delta = c2.rt,
+// alpha2 = delta / (beta - gamma^2 / rho1); x = (alpha1 - gamma alpha2 / rho1) c1
+// + alpha2 c2 (coef[2], coef[3]).  A zero or non-positive curvature drops the
+// step (its weight 0)
+template <int STEP>
+__global__ __launch_bounds__(256) void k_amg_kcoef(int nb, const double* __restrict__ partial, double* __restrict__ coef)
+{
+  constexpr int ND = STEP == 1 ? 2 : 3;
+  __shared__ double sh[ND][256];
+  for (int d = 0; d < ND; ++d) sh[d][threadIdx.x] = (int)threadIdx.x < nb ? partial[ND * threadIdx.x + d] : 0.0;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int d = 0; d < ND; ++d) sh[d][threadIdx.x] += sh[d][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (STEP == 1) {
+      const double rho = sh[0][0];
+      coef[0] = rho;
+      coef[1] = rho > 0.0 ? sh[1][0] / rho : 0.0;
+    }
+    else {
+      const double rho = coef[0], a1 = coef[1];
+      const double gam = sh[0][0], bet = sh[1][0], del = sh[2][0];
+      const double den = rho > 0.0 ? bet - gam * gam / rho : bet;
+      const double a2 = den > 0.0 ? del / den : 0.0;
+      coef[2] = rho > 0.0 ? a1 - gam * a2 / rho : a1;
+      coef[3] = a2;
+    }
+  }
+}
+
+// rt = b - alpha1 v1
+__global__ void k_amg_kresid(int64_t n, const double* __restrict__ coef, const double* __restrict__ b,
+                             const double* __restrict__ v1, double* __restrict__ rt)
+{
+  const double a1 = coef[1];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    rt[i] = b[i] - a1 * v1[i];
+}
+
+// x = w1 c1 + w2 x
+__global__ void k_amg_kcomb(int64_t n, const double* __restrict__ coef, const double* __restrict__ c1,
+                            double* __restrict__ x)
+{
+  const double w1 = coef[2], w2 = coef[3];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = w1 * c1[i] + w2 * x[i];
+}
+
 double env_double(const char* name, double dflt)
 {
   const char* v = variant(name);
@@ -444,6 +531,7 @@ struct AmgLevel {
   DevBuf<int64_t> ap;        // aggregate members (next level's rows): CSR over the fine rows
   DevBuf<int32_t> mem;
   DevBuf<double> x, t, b, r;
+  DevBuf<double> kc1, kv1, krt, kcoef;  // K-cycle level (Amg::kcycle)
   double omega = 0.0;
 };
 
@@ -453,6 +541,9 @@ struct Amg {
   int n_dense = 0;
   int sweeps = 1;
   double scale = 1.0;
+  // AFEM_AMG_KCYCLE=k: levels 1..k solve their coarse problem by two flexible-CG
+  // steps preconditioned by the cycle below (K-cycle) instead of one cycle
+  int kcycle = 0;
   bool fine_planned = true;
   // AFEM_AMG_GRAPH=1: the V-cycle replayed as a captured HIP graph (its
   // launches are fixed once the hierarchy is); keyed on (r, z, the solve's
@@ -778,6 +869,8 @@ void smooth(Ctx& ctx, Amg& a, AmgLevel& L, const double* b, int sweeps, bool fro
   }
 }
 
+void kcycle(Ctx& ctx, Amg& a, size_t l);
+
 void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
 {
   AmgLevel& L = a.lv[l];
@@ -806,11 +899,47 @@ void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
   hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(C.n, 256)), dim3(256), 0, ctx.stream, C.n, L.ap.p, L.mem.p, L.r.p,
                      C.b.p);
   AFEM_LAUNCHED();
-  vcycle(ctx, a, l + 1, C.b.p, nullptr);
+  const bool kc = C.kcoef.p != nullptr;
+  if (kc)
+    kcycle(ctx, a, l + 1);
+  else
+    vcycle(ctx, a, l + 1, C.b.p, nullptr);
   const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
-  hipLaunchKernelGGL(k_amg_prolong, dim3(g), dim3(256), 0, ctx.stream, L.n, L.agg.p, a.scale, C.x.p, L.x.p);
+  // (the K-cycle's Krylov weights are the coarse correction's scale)
+  hipLaunchKernelGGL(k_amg_prolong, dim3(g), dim3(256), 0, ctx.stream, L.n, L.agg.p, kc ? 1.0 : a.scale, C.x.p,
+                     L.x.p);
   AFEM_LAUNCHED();
   smooth(ctx, a, L, b, a.sweeps, false, fine);
+}
+
+// level l's coarse problem A x = b (b in L.b): c1 = B b, v1 = A c1, rt = b -
+// alpha1 v1, c2 = B rt, v2 = A c2, x = w1 c1 + w2 c2 (B: the cycle at this
+// level); every scalar stays on the device (graph-capturable, no host sync)
+void kcycle(Ctx& ctx, Amg& a, size_t l)
+{
+  AmgLevel& L = a.lv[l];
+  const int64_t n = L.n;
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (n + 255) / 256);
+  const unsigned gd = (unsigned)std::min<int64_t>(kDotGrid, (n + 255) / 256);
+  vcycle(ctx, a, l, L.b.p, nullptr);
+  AFEM_HIP(hipMemcpyAsync(L.kc1.p, L.x.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
+  spmv(ctx, 0, L, L.kc1.p, L.kv1.p, nullptr, 0.0);
+  hipLaunchKernelGGL(k_amg_dots<2>, dim3(gd), dim3(256), 0, ctx.stream, n, (const double*)L.kc1.p,
+                     (const double*)L.kv1.p, (const double*)L.kc1.p, (const double*)L.b.p, (const double*)nullptr,
+                     (const double*)nullptr, a.partial.p);
+  hipLaunchKernelGGL(k_amg_kcoef<1>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)a.partial.p, L.kcoef.p);
+  hipLaunchKernelGGL(k_amg_kresid, dim3(g), dim3(256), 0, ctx.stream, n, (const double*)L.kcoef.p, (const double*)L.b.p,
+                     (const double*)L.kv1.p, L.krt.p);
+  AFEM_LAUNCHED();
+  vcycle(ctx, a, l, L.krt.p, nullptr);
+  spmv(ctx, 0, L, L.x.p, L.t.p, nullptr, 0.0);
+  hipLaunchKernelGGL(k_amg_dots<3>, dim3(gd), dim3(256), 0, ctx.stream, n, (const double*)L.x.p, (const double*)L.kv1.p,
+                     (const double*)L.x.p, (const double*)L.t.p, (const double*)L.x.p, (const double*)L.krt.p,
+                     a.partial.p);
+  hipLaunchKernelGGL(k_amg_kcoef<2>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)a.partial.p, L.kcoef.p);
+  hipLaunchKernelGGL(k_amg_kcomb, dim3(g), dim3(256), 0, ctx.stream, n, (const double*)L.kcoef.p,
+                     (const double*)L.kc1.p, L.x.p);
+  AFEM_LAUNCHED();
 }
 
 }  // namespace
@@ -873,6 +1002,18 @@ void amg_setup(LinearSystem& ls)
   // the coarsest level inverted densely when small (a small system: the
   // whole matrix, the PCG then converges in one or two iterations)
   if (last.n <= dense) dense_inverse(ctx, *a, last);
+  // K-cycle on levels 1 and 2 (the unstructured leg's 11.5 M rows, r05ay: 108 -> 72
+  // iterations, 0.453 -> 0.389 s with setup; every level: 66, 0.407 s -- the small
+  // levels' launches, visited 2^l times, cost more than the iterations they save)
+  a->kcycle = (int)std::max(0.0, env_double("AFEM_AMG_KCYCLE", 2.0));
+  for (size_t l = 1; l < a->lv.size() && (int)l <= a->kcycle; ++l) {
+    AmgLevel& L = a->lv[l];
+    if (l + 1 == a->lv.size() && a->n_dense == L.n) break;  // the dense coarsest level: solved exactly
+    L.kc1.alloc(L.n);
+    L.kv1.alloc(L.n);
+    L.krt.alloc(L.n);
+    L.kcoef.alloc(8);
+  }
   a->key_rows = ls.csr_rows;
   a->key_vals = ls.csr_vals;
   a->key_n = ls.n_rows;

@@ -1,0 +1,8 @@
+#!/bin/bash
+# round-5 GPU step az: the K-cycle on levels 1-2 as the AMG default -- AMG tests, the probe
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python3 -u -m pytest -x -v -s --timeout 120 --timeout-method thread -m gpu tests/test_gpu_amg.py \
+  > gpurun_out/r05az_tests.log 2>&1 || exit $?
+timeout -k 10 400 python3 -u tools/amg_probe.py 6 1e-8 - AFEM_AMG_KCYCLE=0 AFEM_AMG_KCYCLE=3 \
+  AFEM_AMG_KCYCLE=2,AFEM_AMG_SWEEPS=2 > gpurun_out/r05az_amg.log 2>&1 || exit $?
