@@ -739,7 +739,10 @@ def test_cube_kernel_staged_canonical(ctx, variant, n, nz, seed):
         assert b1.stats()["last_kernel"] == 10
         rhs = l1.rhs_host()
         b1.assemblePoissonP1(1.0, 5.5, l1.rhsVariable(), rhs_mode="add")
-        out[staged] = (b1.download(), rhs, l1.rhs_host())
+        added = l1.rhs_host()
+        b1.resetMatrixValues()
+        b1.assemblePoissonP1(2.0)  # no RHS: the matrix alone (k_cube_unstage<false, false>)
+        out[staged] = (b1.download(), rhs, added)
     (r0, c0, v0), s0, a0 = out[False]
     (r1, c1, v1), s1, a1 = out[True]
     assert np.array_equal(r0, r1) and np.array_equal(c0, c1)
