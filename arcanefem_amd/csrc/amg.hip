@@ -40,6 +40,8 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include "kcycle.hpp"
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -426,87 +428,6 @@ __global__ __launch_bounds__(64) void k_amg_gemv(int n, const double* __restrict
   for (int j = threadIdx.x; j < n; j += 64) s += A[(int64_t)i * n + j] * b[j];
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   if (threadIdx.x == 0) x[i] = s;
-}
-
-// K-cycle (Notay-Vassilevski): the coarse problem of a level solved by two
-// flexible-CG steps preconditioned by the cycle below.  Dot products: block
-// partials over a fixed grid, summed in a fixed order by one block
-constexpr int kDotGrid = 256;
-template <int ND>
-__global__ __launch_bounds__(256) void k_amg_dots(int64_t n, const double* __restrict__ a0, const double* __restrict__ b0,
-                                                  const double* __restrict__ a1, const double* __restrict__ b1,
-                                                  const double* __restrict__ a2, const double* __restrict__ b2,
-                                                  double* __restrict__ partial)
-{
-  __shared__ double sh[ND][256];
-  double s[3] = { 0.0, 0.0, 0.0 };
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    s[0] += a0[i] * b0[i];
-    if (ND > 1) s[1] += a1[i] * b1[i];
-    if (ND > 2) s[2] += a2[i] * b2[i];
-  }
-#pragma unroll
-  for (int d = 0; d < ND; ++d) sh[d][threadIdx.x] = s[d];
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o)
-#pragma unroll
-      for (int d = 0; d < ND; ++d) sh[d][threadIdx.x] += sh[d][threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x < ND) partial[ND * blockIdx.x + threadIdx.x] = sh[threadIdx.x][0];
-}
-
-// the step coefficients from the partials (one block).  STEP 1: rho1 = c1.v1,
-// alpha1 = c1.r / rho1.  STEP 2: gamma = c2.v1, beta = c2.v2, delta = c2.rt,
-// alpha2 = delta / (beta - gamma^2 / rho1); x = (alpha1 - gamma alpha2 / rho1) c1
-// + alpha2 c2 (coef[2], coef[3]).  A zero or non-positive curvature drops the
-// step (its weight 0)
-template <int STEP>
-__global__ __launch_bounds__(256) void k_amg_kcoef(int nb, const double* __restrict__ partial, double* __restrict__ coef)
-{
-  constexpr int ND = STEP == 1 ? 2 : 3;
-  __shared__ double sh[ND][256];
-  for (int d = 0; d < ND; ++d) sh[d][threadIdx.x] = (int)threadIdx.x < nb ? partial[ND * threadIdx.x + d] : 0.0;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o)
-      for (int d = 0; d < ND; ++d) sh[d][threadIdx.x] += sh[d][threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    if (STEP == 1) {
-      const double rho = sh[0][0];
-      coef[0] = rho;
-      coef[1] = rho > 0.0 ? sh[1][0] / rho : 0.0;
-    }
-    else {
-      const double rho = coef[0], a1 = coef[1];
-      const double gam = sh[0][0], bet = sh[1][0], del = sh[2][0];
-      const double den = rho > 0.0 ? bet - gam * gam / rho : bet;
-      const double a2 = den > 0.0 ? del / den : 0.0;
-      coef[2] = rho > 0.0 ? a1 - gam * a2 / rho : a1;
-      coef[3] = a2;
-    }
-  }
-}
-
-// rt = b - alpha1 v1
-__global__ void k_amg_kresid(int64_t n, const double* __restrict__ coef, const double* __restrict__ b,
-                             const double* __restrict__ v1, double* __restrict__ rt)
-{
-  const double a1 = coef[1];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    rt[i] = b[i] - a1 * v1[i];
-}
-
-// x = w1 c1 + w2 x
-__global__ void k_amg_kcomb(int64_t n, const double* __restrict__ coef, const double* __restrict__ c1,
-                            double* __restrict__ x)
-{
-  const double w1 = coef[2], w2 = coef[3];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    x[i] = w1 * c1[i] + w2 * x[i];
 }
 
 double env_double(const char* name, double dflt)
@@ -924,20 +845,20 @@ void kcycle(Ctx& ctx, Amg& a, size_t l)
   vcycle(ctx, a, l, L.b.p, nullptr);
   AFEM_HIP(hipMemcpyAsync(L.kc1.p, L.x.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
   spmv(ctx, 0, L, L.kc1.p, L.kv1.p, nullptr, 0.0);
-  hipLaunchKernelGGL(k_amg_dots<2>, dim3(gd), dim3(256), 0, ctx.stream, n, (const double*)L.kc1.p,
+  hipLaunchKernelGGL(k_kc_dots<2>, dim3(gd), dim3(256), 0, ctx.stream, n, (const double*)L.kc1.p,
                      (const double*)L.kv1.p, (const double*)L.kc1.p, (const double*)L.b.p, (const double*)nullptr,
                      (const double*)nullptr, a.partial.p);
-  hipLaunchKernelGGL(k_amg_kcoef<1>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)a.partial.p, L.kcoef.p);
-  hipLaunchKernelGGL(k_amg_kresid, dim3(g), dim3(256), 0, ctx.stream, n, (const double*)L.kcoef.p, (const double*)L.b.p,
+  hipLaunchKernelGGL(k_kc_coef<1>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)a.partial.p, L.kcoef.p);
+  hipLaunchKernelGGL(k_kc_resid, dim3(g), dim3(256), 0, ctx.stream, n, (const double*)L.kcoef.p, (const double*)L.b.p,
                      (const double*)L.kv1.p, L.krt.p);
   AFEM_LAUNCHED();
   vcycle(ctx, a, l, L.krt.p, nullptr);
   spmv(ctx, 0, L, L.x.p, L.t.p, nullptr, 0.0);
-  hipLaunchKernelGGL(k_amg_dots<3>, dim3(gd), dim3(256), 0, ctx.stream, n, (const double*)L.x.p, (const double*)L.kv1.p,
+  hipLaunchKernelGGL(k_kc_dots<3>, dim3(gd), dim3(256), 0, ctx.stream, n, (const double*)L.x.p, (const double*)L.kv1.p,
                      (const double*)L.x.p, (const double*)L.t.p, (const double*)L.x.p, (const double*)L.krt.p,
                      a.partial.p);
-  hipLaunchKernelGGL(k_amg_kcoef<2>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)a.partial.p, L.kcoef.p);
-  hipLaunchKernelGGL(k_amg_kcomb, dim3(g), dim3(256), 0, ctx.stream, n, (const double*)L.kcoef.p,
+  hipLaunchKernelGGL(k_kc_coef<2>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)a.partial.p, L.kcoef.p);
+  hipLaunchKernelGGL(k_kc_comb, dim3(g), dim3(256), 0, ctx.stream, n, (const double*)L.kcoef.p,
                      (const double*)L.kc1.p, L.x.p);
   AFEM_LAUNCHED();
 }

@@ -35,6 +35,7 @@
 // everything below it (the one-rank hierarchy, the same arithmetic on every
 // rank).  Setup errors are agreed over the ranks (any_rank).
 #include "afem_internal.hpp"
+#include "kcycle.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -628,6 +629,7 @@ struct MgLevel {
   DevBuf<int32_t> own_bc;
   DevBuf<double> own_v, own_dinv;
   DevBuf<double> x, t, b, r;  // iterate (ping-pong x / t), right-hand side, residual
+  DevBuf<double> kc1, kv1, krt, kcoef;  // K-cycle level (AFEM_MG_KCYCLE)
   double omega = 0.0;
   // a distributed level (global V-cycle over z-slabs): the slab's owned rows in
   // local numbering (sm), the global box gd, the halo of its vectors (level 0:
@@ -1239,6 +1241,21 @@ void mg_setup(LinearSystem& ls)
   }
   MgLevel& Lc = mg->lv.back();
   if (mg->lv.size() > 1 && !Lc.dist && Lc.n <= kDenseMax) dense_inverse(ctx, *mg, Lc);
+  // AFEM_MG_KCYCLE=k: levels 1..k of a one-rank hierarchy run the K-cycle
+  // (kcycle.hpp) instead of one V-cycle for their coarse problem
+  {
+    const char* ke = variant("AFEM_MG_KCYCLE");
+    const int kcyc = ke ? std::max(0, atoi(ke)) : 0;
+    if (!mg->global && mg->partial.n >= 3 * (size_t)kDotGrid)
+      for (size_t l = 1; l < mg->lv.size() && (int)l <= kcyc; ++l) {
+        MgLevel& L = mg->lv[l];
+        if (l + 1 == mg->lv.size() && mg->n_dense == L.n) break;  // solved exactly
+        L.kc1.alloc(L.n);
+        L.kv1.alloc(L.n);
+        L.krt.alloc(L.n);
+        L.kcoef.alloc(8);
+      }
+  }
   mg->key_rows = krows;
   mg->key_vals = ls.csr_vals;
   mg->key_n = ls.n_rows;
@@ -1264,6 +1281,8 @@ void smooth(Ctx& ctx, Multigrid& mg, MgLevel& L, const double* b, int sweeps, bo
   }
 }
 
+void kcycle(Ctx& ctx, Multigrid& mg, size_t l);
+
 void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
 {
   MgLevel& L = mg.lv[l];
@@ -1286,7 +1305,10 @@ void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
                        L.r.p, C.b.p);
     AFEM_LAUNCHED();
   });
-  vcycle(ctx, mg, l + 1, C.b.p);
+  if (C.kcoef.p)
+    kcycle(ctx, mg, l + 1);
+  else
+    vcycle(ctx, mg, l + 1, C.b.p);
   dispatch_k(mg.k, [&](auto kc) {
     constexpr int K = decltype(kc)::value;
     hipLaunchKernelGGL(k_mg_prolong<K>, dim3((unsigned)grid_for(L.nn, 256)), dim3(256), 0, ctx.stream, L.d, C.d,
@@ -1294,6 +1316,35 @@ void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
     AFEM_LAUNCHED();
   });
   smooth(ctx, mg, L, b, mg.sweeps, false);
+}
+
+// K-cycle (AFEM_MG_KCYCLE=k, one rank): level l's coarse problem (b in L.b) by
+// two flexible-CG steps preconditioned by the cycle at this level (kcycle.hpp)
+void kcycle(Ctx& ctx, Multigrid& mg, size_t l)
+{
+  MgLevel& L = mg.lv[l];
+  const int64_t n = L.n;
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, (n + 255) / 256);
+  const unsigned gd = (unsigned)std::min<int64_t>(kDotGrid, (n + 255) / 256);
+  vcycle(ctx, mg, l, L.b.p);
+  AFEM_HIP(hipMemcpyAsync(L.kc1.p, L.x.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
+  spmv_blk_epi(ctx, mg.k, 0, L.nn, L.bp, L.bc, L.v, L.kc1.p, L.kv1.p, nullptr, nullptr, 0.0);
+  hipLaunchKernelGGL(k_kc_dots<2>, dim3(gd), dim3(256), 0, ctx.stream, n, (const double*)L.kc1.p,
+                     (const double*)L.kv1.p, (const double*)L.kc1.p, (const double*)L.b.p, (const double*)nullptr,
+                     (const double*)nullptr, mg.partial.p);
+  hipLaunchKernelGGL(k_kc_coef<1>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)mg.partial.p, L.kcoef.p);
+  hipLaunchKernelGGL(k_kc_resid, dim3(g), dim3(256), 0, ctx.stream, n, (const double*)L.kcoef.p, (const double*)L.b.p,
+                     (const double*)L.kv1.p, L.krt.p);
+  AFEM_LAUNCHED();
+  vcycle(ctx, mg, l, L.krt.p);
+  spmv_blk_epi(ctx, mg.k, 0, L.nn, L.bp, L.bc, L.v, L.x.p, L.t.p, nullptr, nullptr, 0.0);
+  hipLaunchKernelGGL(k_kc_dots<3>, dim3(gd), dim3(256), 0, ctx.stream, n, (const double*)L.x.p, (const double*)L.kv1.p,
+                     (const double*)L.x.p, (const double*)L.t.p, (const double*)L.x.p, (const double*)L.krt.p,
+                     mg.partial.p);
+  hipLaunchKernelGGL(k_kc_coef<2>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)mg.partial.p, L.kcoef.p);
+  hipLaunchKernelGGL(k_kc_comb, dim3(g), dim3(256), 0, ctx.stream, n, (const double*)L.kcoef.p, (const double*)L.kc1.p,
+                     L.x.p);
+  AFEM_LAUNCHED();
 }
 
 // a distributed level of the global V-cycle (the steps of vcycle on the slab's
