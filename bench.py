@@ -480,7 +480,9 @@ def unstructured_leg(ctx, af, mesh_file, levels, reps=7, warmup=2, settle_ms=150
                  "rel_residual": sst["rel_residual"], "solve_ms": round(sst["solve_ms"], 1),
                  "wall_ms": round(wall, 1)}
             if pc == "amg":
-                r.update(levels=int(sst["amg_levels"]), coarse_rows=int(sst["amg_coarse_rows"]),
+                r.update(cycle="V(1,1) damped Jacobi, K-cycle (two flexible-CG steps) on levels 1-2 "
+                               "(AFEM_AMG_KCYCLE)",
+                         levels=int(sst["amg_levels"]), coarse_rows=int(sst["amg_coarse_rows"]),
                          operator_complexity=round(sst["amg_complexity"], 3),
                          setup_ms=round(sst["amg_setup_ms"], 1),
                          ms_per_iteration=round((sst["solve_ms"] - sst["amg_setup_ms"]) / max(1, sst["iterations"]),
