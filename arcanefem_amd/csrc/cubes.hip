@@ -957,7 +957,10 @@ __global__ void k_cube_stage_maps(int64_t n, int npx, int npy, int nzc, const in
 // canonical flush wrote each 120-B row into lines that other units complete
 // at other times (WRITE_SIZE 1.77 GB for 1.28 GB)
 constexpr int kUnLine = 18;  // LDS doubles per line (16 + 2: 16-B aligned, lanes l and l + 16 share banks only)
-template <bool HAS_RHS, bool RHS_ADD>
+// UV: 1 non-temporal line loads, 2 non-temporal value stores -- both by default
+// (the lines are read once, the values not by this launch): c2_arrays 1.102 ->
+// 1.066 ms (r05bl; 1.094 / 1.075 with one of them); AFEM_UNSTAGE_V=0 / 1 / 2 for A/B
+template <bool HAS_RHS, bool RHS_ADD, int UV = 3>
 __global__ __launch_bounds__(64) void k_cube_unstage(int64_t n, const int64_t* __restrict__ rp,
                                                       const int32_t* __restrict__ lat,
                                                       const uint64_t* __restrict__ pinv,
@@ -982,7 +985,10 @@ __global__ __launch_bounds__(64) void k_cube_unstage(int64_t n, const int64_t* _
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int64_t lk = __shfl((int)li, 8 * k + (lane >> 3));
-    w[k] = reinterpret_cast<const d2a*>(stage + 16 * lk)[part];
+    if constexpr ((UV & 1) != 0)
+      w[k] = __builtin_nontemporal_load(reinterpret_cast<const d2a*>(stage + 16 * lk) + part);
+    else
+      w[k] = reinterpret_cast<const d2a*>(stage + 16 * lk)[part];
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) reinterpret_cast<d2a*>(line + kUnLine * (8 * k + (lane >> 3)))[part] = w[k];
@@ -1011,8 +1017,12 @@ __global__ __launch_bounds__(64) void k_cube_unstage(int64_t n, const int64_t* _
     if (j < total) {
       double* const g = vals + (rb0 - a + j);
       const bool lo = j >= a, hi = j + 1 < total;
-      if (lo && hi)
-        *reinterpret_cast<d2a*>(g) = d2a{ out[j], out[j + 1] };
+      if (lo && hi) {
+        if constexpr ((UV & 2) != 0)
+          __builtin_nontemporal_store(d2a{ out[j], out[j + 1] }, reinterpret_cast<d2a*>(g));
+        else
+          *reinterpret_cast<d2a*>(g) = d2a{ out[j], out[j + 1] };
+      }
       else if (lo)
         g[0] = out[j];
       else if (hi)
@@ -1157,6 +1167,11 @@ bool assemble_cubes(Bsr& b, double coef, double f, double* rhs, int rhs_add)
     const int64_t n = S.n_rows;
     auto* un = rhs ? (rhs_add ? &k_cube_unstage<true, true> : &k_cube_unstage<true, false>)
                    : &k_cube_unstage<false, false>;
+    const char* uve = variant("AFEM_UNSTAGE_V");
+    const int uv = uve ? atoi(uve) : 3;
+    if (rhs && !rhs_add && uv == 0) un = &k_cube_unstage<true, false, 0>;
+    if (rhs && !rhs_add && uv == 1) un = &k_cube_unstage<true, false, 1>;
+    if (rhs && !rhs_add && uv == 2) un = &k_cube_unstage<true, false, 2>;
     hipLaunchKernelGGL(un, dim3((unsigned)grid_for(n, 64)), dim3(64), 0, ctx.stream, n, S.row_ptr.p, S.cube_lat.p,
                        S.cube_pinv.p, b.cube_stage.p, g.f_meas, b.values.p, rhs);
     AFEM_LAUNCHED();
