@@ -1892,6 +1892,11 @@ __global__ __launch_bounds__(64) void k_assemble_elast_strip(int64_t n_items, co
 #ifndef AFEM_WG_ST16
 #define AFEM_WG_ST16 1
 #endif
+// the stencil instance's x-run stores non-temporal (the values are not re-read by the launch; C3
+// 1.72 -> 1.68 ms median, r05bn, tools/ab_lib.py against a -DAFEM_WG_NT=0 build)
+#ifndef AFEM_WG_NT
+#define AFEM_WG_NT 1
+#endif
 __host__ __device__ constexpr int64_t elast_wg_bytes(int64_t u_cap, int64_t w_cap)
 {
   return 3 * 3 * 8 * 64 * w_cap + 3 * 8 * u_cap + 2 * 64 * w_cap + 64 * 8 + 64 * 4 + 64 + ((64 * w_cap + 15) & ~15);
@@ -2351,7 +2356,11 @@ __global__ __launch_bounds__(192) void k_assemble_elast_wg(int64_t n_slices, con
 #pragma unroll
           for (int i = 0; i < (RUN / 2 + 191) / 192; ++i) {
             const int o = min(2 * (tid + 192 * i), RUN - 2);
+#if AFEM_WG_NT
+            __builtin_nontemporal_store(d2u{ src[o], src[o + 1] }, reinterpret_cast<d2u*>(dst + o));
+#else
             st_out(reinterpret_cast<d2u*>(dst + o), d2u{ src[o], src[o + 1] });
+#endif
           }
 #else
 #pragma unroll
