@@ -846,16 +846,18 @@ def test_natural_numbering_rejects_non_kuhn_lattices(ctx):
         _check_values(vals, ovals)
 
 
-@pytest.mark.parametrize("knob,value", [("AFEM_BANK_PLACE_GENERAL", "1"), ("AFEM_ASSEMBLY_LOCAL", "1")])
+@pytest.mark.parametrize("knob,value", [("AFEM_BANK_PLACE_GENERAL", "1"), ("AFEM_ASSEMBLY_LOCAL", "1"),
+                                        ("AFEM_ASSEMBLY_BIG", "0"), ("AFEM_ASSEMBLY_BIG", "1")])
 def test_general_slice_variants_bitwise(ctx, variant, knob, value):
-    """Two layouts of the general (unstructured) slices that must not change a
+    """Variants of the general (unstructured) slices that must not change a
     bit: LDS-bank-aware placement of their node lists (a greedy colouring of
     the positions mod 32 over the lanes that read them at each step,
-    sparsity.hip bank_place_general; opt-in) and the local-index stream
+    sparsity.hip bank_place_general; opt-in), the local-index stream
     instead of the column-index table (AFEM_ASSEMBLY_LOCAL=1: the slices of
-    <= 256 nodes through k_assemble_strip<4,2,16,3>; opt-in).  On an
-    unstructured mesh: the matrix and the RHS bitwise equal to the default's,
-    and the oracle's."""
+    <= 256 nodes through k_assemble_strip<4,2,16,3>; opt-in), and the order of
+    the compact and big lists (AFEM_ASSEMBLY_BIG 0: side by side, 1: big
+    first; the default compact first).  On an unstructured mesh: the matrix and
+    the RHS bitwise equal to the default's, and the oracle's."""
     import bench
 
     gm = read_gmsh(path("L-shape-3D.msh"))
