@@ -5,7 +5,7 @@
 # separate --pmc passes (FETCH_SIZE; WRITE_SIZE; optional SQ / LDS groups),
 # each under its own time limit; the script stops at the first failure.
 #   tools/profile_legs.sh <out_dir> <leg> [<leg> ...]
-# legs: c2 (the headline command), c4, c3, c2_generic, c2_arrays,
+# legs: c2 (the headline command), c4, c2_spmv / c4_spmv (their CG's pattern SpMV), c3, c2_generic, c2_arrays,
 # c2_arrays_natural, unstructured, generic_unstructured.  PASSES (env): pass names to run (default
 # "trace fetch write").  Summarise with tools/collect_leg.py.
 export TMPDIR=/tmp
@@ -17,6 +17,8 @@ for LEG in "$@"; do
   case $LEG in
     c2) B="bench.py --no-extras --no-cpu-baseline --cg-iters 20"; K="k_assemble_cubes" ;;
     c4) B="bench.py --no-headline --legs c4"; K="k_assemble_cubes" ;;
+    c2_spmv) B="bench.py --no-extras --no-cpu-baseline --cg-iters 20"; K="k_spmv_pat" ;;
+    c4_spmv) B="bench.py --no-headline --legs c4"; K="k_spmv_pat" ;;
     c3) B="bench.py --no-headline --legs c3"; K="k_assemble_elast" ;;
     c2_generic) B="bench.py --no-headline --legs c2_generic"; K="k_assemble_units" ;;
     c2_arrays) B="bench.py --no-headline --legs c2_arrays"; K="k_assemble_cubes|k_cube_unstage" ;;
