@@ -102,7 +102,15 @@ class SolveStats(ctypes.Structure):
                 ("halo_wait_ms", ctypes.c_double), ("allreduce_ms", ctypes.c_double), ("halo_bytes", ctypes.c_int64),
                 ("n_halo", ctypes.c_int32), ("n_allreduce", ctypes.c_int32), ("amg_levels", ctypes.c_int32),
                 ("amg_coarse_rows", ctypes.c_int64), ("amg_complexity", ctypes.c_double),
-                ("amg_setup_ms", ctypes.c_double)]
+                ("amg_setup_ms", ctypes.c_double), ("precond_ms", ctypes.c_double)]
+
+
+class StepTiming(ctypes.Structure):
+    _fields_ = [("assemble_ms", ctypes.c_double), ("rhs_ms", ctypes.c_double), ("bc_ms", ctypes.c_double),
+                ("solve_ms", ctypes.c_double), ("precond_ms", ctypes.c_double), ("update_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double), ("iterations", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+                ("nnz_blocks", ctypes.c_int64), ("n_incidences", ctypes.c_int64), ("n_nodes", ctypes.c_int64),
+                ("n_own_nodes", ctypes.c_int64)]
 
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64)
@@ -210,6 +218,9 @@ SIGNATURES = {
     "afem_elastodynamics_set_dirichlet": [P, P, P, I64, INT],
     "afem_elastodynamics_set_time_step": [P, D],
     "afem_elastodynamics_state": [P, PP, PP, PP],
+    "afem_elastodynamics_operators": [P, ctypes.POINTER(CsrView), PP, PP, PP, P],
+    "afem_elastodynamics_profile": [P, INT],
+    "afem_elastodynamics_step_timing": [P, ctypes.POINTER(StepTiming)],
     "afem_elastodynamics_destroy": [P],
     "afem_comm_host_async": [P, INT],
     "afem_comm_destroy": [P],

@@ -499,7 +499,7 @@ class DoFLinearSystem:
                     halo_wait_ms=st.halo_wait_ms, allreduce_ms=st.allreduce_ms, halo_bytes=st.halo_bytes,
                     n_halo=st.n_halo, n_allreduce=st.n_allreduce, amg_levels=st.amg_levels,
                     amg_coarse_rows=st.amg_coarse_rows, amg_complexity=st.amg_complexity,
-                    amg_setup_ms=st.amg_setup_ms)
+                    amg_setup_ms=st.amg_setup_ms, precond_ms=st.precond_ms)
 
     def spmv(self, x_dptr: int, y_dptr: int):
         call("afem_ls_spmv", self.impl, ctypes.c_void_p(x_dptr), ctypes.c_void_p(y_dptr))

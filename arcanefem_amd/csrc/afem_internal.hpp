@@ -534,7 +534,8 @@ void ls_spmv(LinearSystem& ls, const double* x, double* y);
 void ls_spmv_planned(LinearSystem& ls, const double* x, double* y);
 // algebraic multigrid preconditioner (amg.hip)
 bool amg_available(const LinearSystem& ls);
-void amg_setup(LinearSystem& ls);
+bool amg_nonlinear(const LinearSystem& ls);  // a K-cycle level: the preconditioner depends on r
+bool amg_setup(LinearSystem& ls);  // false: the amg-reuse hierarchy was kept
 void amg_apply(LinearSystem& ls, const double* r, double* z);
 void amg_stats(const LinearSystem& ls, int32_t* levels, int64_t* coarse_rows, double* complexity);
 void ls_build_from_host_coo(LinearSystem& ls);
@@ -584,12 +585,17 @@ struct Elastodynamics {
   DevBuf<double> imp_vals;  //   and their values
   int64_t n = 0, n_cols = 0;
   afem_solve_stats last{};
+  // afem_elastodynamics_profile: per-phase events of every step
+  bool profile = false;
+  hipEvent_t ev[6] = {};
+  afem_step_timing timing{};
 };
 Elastodynamics* dyn_create(Mesh* mesh, Comm* comm, const afem_newmark_params* prm, const int32_t* fixed_nodes,
                            int64_t n_fixed, int mem);
 void dyn_step(Elastodynamics* d, afem_solve_stats* st);
 void dyn_set_dirichlet(Elastodynamics* d, const int32_t* dofs, const double* values, int64_t n, int mem);
 void dyn_set_time_step(Elastodynamics* d, double dt);
+void dyn_profile(Elastodynamics* d, bool on);
 void dyn_destroy(Elastodynamics* d);
 
 void vec_lincomb(Ctx& ctx, int64_t n, double a, const double* x, double b, const double* y, double c, const double* z,

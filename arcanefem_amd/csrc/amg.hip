@@ -33,9 +33,9 @@
 //  * constraint rows are taken out of the cycle as in multigrid.hip:
 //    z = F V(F r) + C D^-1 r.
 // One rank (the system carries no halo).  The V-cycle is symmetric (an SPD
-// preconditioner); the K-cycle is a nonlinear one: the PCG keeps its
-// Fletcher-Reeves beta, which converges to the same solution (tested against
-// the Jacobi-PCG and the plain V-cycle, test_amg_kcycle).
+// preconditioner); the K-cycle is a nonlinear one: the PCG then takes the
+// flexible (Polak-Ribiere) beta, -(z.q)/(p.q) (linear_system.hip k_cg_dir_flex;
+// tested against the Jacobi-PCG and the plain V-cycle, test_amg_kcycle).
 #include "afem_internal.hpp"
 
 #include <hipcub/hipcub.hpp>
@@ -481,8 +481,9 @@ struct Amg {
   }
   DevBuf<double> partial;
   const void* key_rows = nullptr;
+  const void* key_cols = nullptr;
   const void* key_vals = nullptr;
-  int64_t key_n = 0;
+  int64_t key_n = 0, key_nnz = 0;
 };
 
 void AmgDeleter::operator()(Amg* a) const { delete a; }
@@ -491,7 +492,17 @@ bool amg_available(const LinearSystem& ls)
 {
   if (!ls.csr_rows || !ls.csr_cols || !ls.csr_vals || ls.n_rows <= 0) return false;
   if (ls.halo && ls.halo->comm && comm_nranks(ls.halo->comm) > 1) return false;  // one rank
-  return ls.n_rows < (int64_t(1) << 31);
+  // hipcub's sorts of the setup take int counts: the non-zeros of every level
+  // (the fine level's are the most) must stay below 2^31, else point Jacobi
+  return ls.n_rows < (int64_t(1) << 31) && ls.csr_nnz < (int64_t(1) << 31);
+}
+
+bool amg_nonlinear(const LinearSystem& ls)
+{
+  if (!ls.amg) return false;
+  for (const auto& L : ls.amg->lv)
+    if (L.kcoef.p) return true;
+  return false;
 }
 
 int amg_levels(const LinearSystem& ls) { return ls.amg ? (int)ls.amg->lv.size() : 0; }
@@ -599,7 +610,13 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
     AFEM_HIP(hipMemcpyAsync(&hl, left.p, sizeof(hl), hipMemcpyDeviceToHost, ctx.stream));
     ctx.sync();
     if (hl == 0) break;
-    AFEM_REQUIRE(round < 63, AFEM_ERR_STATE, "amg: the independent set did not converge");
+    if (round == 63) {
+      //  the independent set did not settle in 64 rounds: no coarse
+      // level below this one -- it becomes the coarsest, smoothed by Jacobi
+      // sweeps (amg_setup), instead of failing the solve
+      ctx.sync();
+      return 0;
+    }
   }
   DevBuf<int32_t> f;
   DevBuf<int64_t> rank;
@@ -865,13 +882,15 @@ void kcycle(Ctx& ctx, Amg& a, size_t l)
 
 }  // namespace
 
-void amg_setup(LinearSystem& ls)
+bool amg_setup(LinearSystem& ls)
 {
   Ctx& ctx = *ls.ctx;
   AFEM_REQUIRE(amg_available(ls), AFEM_ERR_STATE, "amg: needs a CSR system on one rank");
-  if (ls.opts.amg == 2 && ls.amg && ls.amg->key_rows == ls.csr_rows && ls.amg->key_vals == ls.csr_vals &&
-      ls.amg->key_n == ls.n_rows)
-    return;
+  // amg-reuse: the same CSR arrays at the same sizes (every entry point that
+  // installs or rebuilds a matrix also drops ls.amg, capi.cpp / elastodynamics.cpp)
+  if (ls.opts.amg == 2 && ls.amg && ls.amg->key_rows == ls.csr_rows && ls.amg->key_cols == ls.csr_cols &&
+      ls.amg->key_vals == ls.csr_vals && ls.amg->key_n == ls.n_rows && ls.amg->key_nnz == ls.csr_nnz)
+    return false;
   auto a = std::unique_ptr<Amg, AmgDeleter>(new Amg());
   a->partial.alloc(kVec);
   a->sweeps = (int)std::max(1.0, env_double("AFEM_AMG_SWEEPS", 1.0));
@@ -936,9 +955,12 @@ void amg_setup(LinearSystem& ls)
     L.kcoef.alloc(8);
   }
   a->key_rows = ls.csr_rows;
+  a->key_cols = ls.csr_cols;
   a->key_vals = ls.csr_vals;
   a->key_n = ls.n_rows;
+  a->key_nnz = ls.csr_nnz;
   ls.amg = std::move(a);
+  return true;
 }
 
 namespace {

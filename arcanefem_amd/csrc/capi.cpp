@@ -802,6 +802,7 @@ int afem_bsr_to_linear_system(afem_bsr* b, afem_ls* ls)
   ls->mg_k0 = box ? st.k0 : 0;
   ls->mg_glo = box && st.ghost_lo >= 0;
   ls->mg.reset();
+  ls->amg.reset();
   ls->has_csr = true;
   ls->csr_from_coo = false;
   ls->hv_rows = nullptr;
@@ -1049,6 +1050,7 @@ int afem_ls_set_csr_values(afem_ls* ls, const int32_t* rows, const int32_t* rows
   ls->blk_k = 0;
   ls->mg_k = 0;
   ls->mg.reset();
+  ls->amg.reset();
   ls->csr_n = nb_row;
   ls->csr_nnz = nb_nz;
   ls->has_csr = true;
@@ -1087,6 +1089,7 @@ int afem_ls_set_csr_values_mapped(afem_ls* ls, const int32_t* rows, const int32_
   ls->blk_k = 0;
   ls->mg_k = 0;
   ls->mg.reset();
+  ls->amg.reset();
   ls->has_csr = true;
   ls->csr_from_coo = false;
   ls->hv_rows = nullptr;
@@ -1219,6 +1222,7 @@ int afem_ls_clear_values(afem_ls* ls)
   ls->blk_k = 0;
   ls->mg_k = 0;
   ls->mg.reset();
+  ls->amg.reset();
   ls->csr_cols = nullptr;
   ls->csr_vals = nullptr;
   ls->hv_rows = nullptr;
@@ -1327,6 +1331,7 @@ int afem_elastodynamics_set_solver_options(afem_elastodynamics* h, const afem_so
   AFEM_REQUIRE(!(o->multigrid && o->precond_block == 3), AFEM_ERR_ARG,
                "multigrid and block Jacobi are alternative preconditioners");
   h->d->ls.mg.reset();
+  h->d->ls.amg.reset();
   h->d->ls.opts = *o;
   h->d->ls.opts.method = AFEM_SOLVER_PCG;
   API_END
@@ -1365,6 +1370,47 @@ int afem_elastodynamics_state(afem_elastodynamics* h, double** u, double** v, do
   if (u) *u = h->d->U.p;
   if (v) *v = h->d->V.p;
   if (a) *a = h->d->A.p;
+  API_END
+}
+
+int afem_elastodynamics_operators(afem_elastodynamics* h, afem_csr_view* lhs, const int64_t** scalar_rows,
+                                  const int32_t** scalar_cols, const double** mass_values, double* c)
+{
+  API_BEGIN
+  NOT_NULL(h);
+  Elastodynamics* d = h->d;
+  if (lhs) {
+    lhs->n_block_rows = d->K.s.n_rows;
+    lhs->n_block_cols = d->mesh->n_nodes;
+    lhs->nnz_blocks = d->K.s.nnz;
+    lhs->block_size = 3;
+    lhs->ordered_per_block = d->K.order_per_block ? 1 : 0;
+    lhs->rows = d->K.s.row_ptr.p;
+    lhs->columns = d->K.s.cols.p;
+    lhs->values = d->K.values.p;
+  }
+  if (scalar_rows) *scalar_rows = d->K.csr_rows.p;
+  if (scalar_cols) *scalar_cols = d->K.csr_cols.p;
+  if (mass_values) *mass_values = d->mvals.p;
+  if (c)
+    for (int i = 0; i < 11; ++i) c[i] = d->c[i];
+  API_END
+}
+
+int afem_elastodynamics_profile(afem_elastodynamics* h, int on)
+{
+  API_BEGIN
+  NOT_NULL(h);
+  dyn_profile(h->d, on != 0);
+  API_END
+}
+
+int afem_elastodynamics_step_timing(afem_elastodynamics* h, afem_step_timing* out)
+{
+  API_BEGIN
+  NOT_NULL(h);
+  NOT_NULL(out);
+  *out = h->d->timing;
   API_END
 }
 

@@ -254,8 +254,16 @@ void dyn_step(Elastodynamics* d, afem_solve_stats* st)
     ctx.set_device();
     const double f[3] = { d->p.body_force[0], d->p.body_force[1], d->p.body_force[2] };
     const double* c = d->c;
+    const bool prof = d->profile;
+    auto mark = [&](int i) {
+      if (prof) AFEM_HIP(hipEventRecord(d->ev[i], ctx.stream));
+    };
+    const int32_t prof_opt = d->ls.opts.profile_comm;
+    if (prof) d->ls.opts.profile_comm = 1;  // the PCG times its preconditioner applications
+    mark(0);
     // LHS c0 M + K(c1, c2) and the body force (rhs = f |K|/4), re-assembled on the fixed structure
     assemble_elasticity_tet(d->K, c[1], c[2], c[0], f, d->ls.rhs.p, 0);
+    mark(1);
     // rhs += M (c0 U + c3 V + c4 A)
     vec_lincomb(ctx, d->n, c[0], d->U.p, c[3], d->V.p, c[4], d->A.p, d->W.p);
     ls_spmv(d->lsm, d->W.p, d->MW.p);
@@ -268,6 +276,7 @@ void dyn_step(Elastodynamics* d, afem_solve_stats* st)
       ls_spmv(d->lsu, d->W.p, d->MW.p);
       vec_lincomb(ctx, d->n, 1.0, d->ls.rhs.p, 1.0, d->MW.p, 0.0, nullptr, d->ls.rhs.p);
     }
+    mark(2);
     // clamped DoFs by penalty (the reference's default Dirichlet treatment)
     if (d->fixed.n) ls_set_list(d->ls, d->fixed.p, (int64_t)d->fixed.n, AFEM_MEM_DEVICE, 0, 0.0, d->p.penalty);
     // imposed displacements: diagonal = penalty, rhs = u penalty
@@ -278,11 +287,30 @@ void dyn_step(Elastodynamics* d, afem_solve_stats* st)
     // (the PCG's stopping target is unchanged: the zero guess's residual)
     vec_lincomb(ctx, d->n, 1.0, d->U.p, d->p.dt, d->V.p, d->p.dt * d->p.dt * (0.5 - d->beta), d->A.p, d->ls.sol.p);
     d->ls.opts.initial_guess = 1;
+    mark(3);
     ls_solve(d->ls, &d->last);
+    d->ls.opts.profile_comm = prof_opt;
+    mark(4);
     // the imposed values re-applied to the solution (_doSolve, :2369-2371)
     if (d->imp_ids.n) vec_scatter(ctx, (int64_t)d->imp_ids.n, d->imp_ids.p, d->imp_vals.p, d->ls.sol.p);
     newmark_update(ctx, d->n, d->p.dt, d->beta, d->gamma, d->ls.sol.p, d->U.p, d->V.p, d->A.p);
+    mark(5);
     ctx.sync();
+    if (prof) {
+      float ms[5] = {};
+      for (int i = 0; i < 5; ++i) AFEM_HIP(hipEventElapsedTime(&ms[i], d->ev[i], d->ev[i + 1]));
+      float tot = 0.f;
+      AFEM_HIP(hipEventElapsedTime(&tot, d->ev[0], d->ev[5]));
+      afem_step_timing& t = d->timing;
+      t.assemble_ms = ms[0];
+      t.rhs_ms = ms[1];
+      t.bc_ms = ms[2];
+      t.solve_ms = ms[3];
+      t.precond_ms = d->last.precond_ms;
+      t.update_ms = ms[4];
+      t.total_ms = tot;
+      t.iterations = d->last.iterations;
+    }
     if (st) *st = d->last;
   }
 }
@@ -332,6 +360,20 @@ void dyn_set_time_step(Elastodynamics* d, double dt)
   // the operator c0 M + K(c1, c2) depends on dt: a reused multigrid hierarchy
   // is rebuilt at the next solve
   d->ls.mg.reset();
+  d->ls.amg.reset();
+}
+
+void dyn_profile(Elastodynamics* d, bool on)
+{
+  d->ctx->set_device();
+  if (on && !d->ev[0])
+    for (auto& e : d->ev) AFEM_HIP(hipEventCreate(&e));
+  d->profile = on;
+  afem_step_timing& t = d->timing;
+  t.nnz_blocks = d->K.s.nnz;
+  t.n_incidences = d->K.s.n_incidences;
+  t.n_nodes = d->mesh->n_nodes;
+  t.n_own_nodes = d->mesh->n_own;
 }
 
 void dyn_destroy(Elastodynamics* d)
@@ -339,6 +381,8 @@ void dyn_destroy(Elastodynamics* d)
   if (!d) return;
   d->ctx->set_device();
   (void)hipStreamSynchronize(d->ctx->stream);
+  for (auto& e : d->ev)
+    if (e) (void)hipEventDestroy(e);
   if (d->ls.pinned) (void)hipHostFree(d->ls.pinned);
   for (LinearSystem* l : { &d->lsm, &d->lsl, &d->lsu })
     if (l->pinned) (void)hipHostFree(l->pinned);

@@ -6,6 +6,8 @@
 // (Aleph semantics, femutils/AlephDoFLinearSystem.cc:192-223,501-583).
 #include "afem_internal.hpp"
 
+#include <functional>
+
 #include <chrono>
 
 #include <cstdio>
@@ -1255,6 +1257,18 @@ __global__ __launch_bounds__(kThreads) void k_cg_dir(int64_t n, const double* __
     p[i] = z[i] + beta * p[i];
 }
 
+// flexible CG (Polak-Ribiere; Notay's FCG(1)) for a nonlinear preconditioner
+// (the AMG K-cycle): beta = z_new.(r_new - r_old) / rz_old = -(z_new.q) / (p.q),
+// since r_new - r_old = -alpha q and alpha = rz_old / (p.q); scal[5] = z_new.q
+__global__ __launch_bounds__(kThreads) void k_cg_dir_flex(int64_t n, const double* __restrict__ scal,
+                                                          const double* __restrict__ z, double* __restrict__ p)
+{
+  const double pq = scal[2], zq = scal[5];
+  const double beta = (pq != 0.0) ? -zq / pq : 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = z[i] + beta * p[i];
+}
+
 __global__ __launch_bounds__(kThreads) void k_dot(int64_t n, const double* __restrict__ a,
                                                   const double* __restrict__ b, double* __restrict__ partial)
 {
@@ -1802,6 +1816,7 @@ void ls_build_from_host_coo(LinearSystem& ls)
   ls.blk_k = 0;
   ls.mg_k = 0;
   ls.mg.reset();
+  ls.amg.reset();
 }
 
 void ls_apply_bcs(LinearSystem& ls)
@@ -1956,10 +1971,20 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   double amg_setup_ms = 0.0;
   if (use_amg) {
     const auto t0 = std::chrono::steady_clock::now();
-    amg_setup(ls);
-    amg_setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (amg_setup(ls))
+      amg_setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
+  // the K-cycle makes the preconditioner nonlinear (its Krylov weights depend
+  // on r): the flexible beta then (AFEM_CG_FLEX=0: Fletcher-Reeves)
+  const char* fxe = variant("AFEM_CG_FLEX");
+  const bool flex = use_amg && amg_nonlinear(ls) && !(fxe && atoi(fxe) == 0);
+  // with afem_solver_opts.profile_comm the applications are timed (event pairs, prof_pc below)
+  std::function<void(const double*, double*)> precond_timed;
   auto precond = [&](const double* rr, double* zz) {
+    if (precond_timed) {
+      precond_timed(rr, zz);
+      return;
+    }
     if (use_amg)
       amg_apply(ls, rr, zz);
     else
@@ -2078,11 +2103,38 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     n_int = ls.blist_nint;
   }
   // afem_solver_opts.profile_comm: event pairs around each halo wait and
-  // all-reduce of the loop on the context stream, summed after the loop
+  // all-reduce of the loop on the context stream, summed in batches: a fixed
+  // pool of kProfEvents events, drained (one stream sync) when it is full
   const bool prof = ls.opts.profile_comm != 0 && comm != nullptr;
+  // ... and every preconditioner application (multigrid / AMG), any rank count
+  const bool prof_pc = ls.opts.profile_comm != 0 && use_mg;
+  constexpr size_t kProfEvents = 256;
   size_t prof_used = 0;
-  std::vector<std::pair<size_t, size_t>> prof_halo, prof_ar;
-  auto prof_event = [&]() -> size_t {
+  double prof_halo_ms = 0.0, prof_ar_ms = 0.0, prof_pc_ms = 0.0;
+  std::vector<std::pair<size_t, size_t>> prof_halo, prof_ar, prof_pcv;
+  auto prof_drain = [&]() {
+    if (prof_used == 0) return;
+    ctx.sync();
+    auto sum_ms = [&](const std::vector<std::pair<size_t, size_t>>& v) {
+      double t = 0.0;
+      for (const auto& e : v) {
+        float m = 0.f;
+        AFEM_HIP(hipEventElapsedTime(&m, ls.prof_ev[e.first], ls.prof_ev[e.second]));
+        t += m;
+      }
+      return t;
+    };
+    prof_halo_ms += sum_ms(prof_halo);
+    prof_ar_ms += sum_ms(prof_ar);
+    prof_pc_ms += sum_ms(prof_pcv);
+    prof_halo.clear();
+    prof_ar.clear();
+    prof_pcv.clear();
+    prof_used = 0;
+  };
+  // start = the first event of a pair: the pool is drained before a pair that would not fit
+  auto prof_event = [&](bool start = false) -> size_t {
+    if (start && prof_used + 2 > kProfEvents) prof_drain();
     if (prof_used == ls.prof_ev.size()) {
       hipEvent_t e;
       AFEM_HIP(hipEventCreate(&e));
@@ -2091,10 +2143,19 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     AFEM_HIP(hipEventRecord(ls.prof_ev[prof_used], ctx.stream));
     return prof_used++;
   };
+  if (prof_pc)
+    precond_timed = [&](const double* rr, double* zz) {
+      const size_t a = prof_event(true);
+      if (use_amg)
+        amg_apply(ls, rr, zz);
+      else
+        mg_apply(ls, rr, zz);
+      prof_pcv.emplace_back(a, prof_event());
+    };
   int n_halo_loop = 0, n_ar_loop = 0;
   auto loop_allreduce = [&](double* d) {
     if (!comm) return;
-    const size_t a = prof ? prof_event() : 0;
+    const size_t a = prof ? prof_event(true) : 0;
     comm_allreduce(comm, ctx, d, 1);
     if (prof) prof_ar.emplace_back(a, prof_event());
     ++n_ar_loop;
@@ -2116,6 +2177,11 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
       AFEM_LAUNCHED();
       precond(ls.r.p, ls.z.p);
       hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.r.p, ls.z.p, ls.partial.p);
+      if (flex) {
+        hipLaunchKernelGGL(k_dot, dim3(vb), dim3(kThreads), 0, ctx.stream, n, ls.z.p, ls.q.p, ls.partial.p + vb);
+        reduce_to(ctx, ls.partial.p + vb, vb, scal + 5);
+        loop_allreduce(scal + 5);
+      }
       AFEM_LAUNCHED();
     }
     else if (blk3)
@@ -2127,7 +2193,10 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     AFEM_LAUNCHED();
     reduce_to(ctx, ls.partial.p, blk3 ? vb3 : vb, scal + (par ^ 1));
     loop_allreduce(scal + (par ^ 1));
-    if (use_mg || blk3)
+    if (flex)
+      hipLaunchKernelGGL(k_cg_dir_flex, dim3(vb), dim3(kThreads), 0, ctx.stream, n, (const double*)scal, ls.z.p,
+                         ls.p.p);
+    else if (use_mg || blk3)
       hipLaunchKernelGGL(k_cg_dir, dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal, par, ls.z.p, ls.p.p);
     else
       hipLaunchKernelGGL(vec4 ? (k_cg_dir_x<true, true>) : vec2 ? (k_cg_dir_x<true>) : (k_cg_dir_x<false>), dim3(vb), dim3(kThreads), 0, ctx.stream, n, scal,
@@ -2185,7 +2254,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
       };
       halo_begin(*ls.halo, ctx, ls.p.p);
       part(n_int, 0);
-      const size_t ha = prof ? prof_event() : 0;
+      const size_t ha = prof ? prof_event(true) : 0;
       halo_end(*ls.halo, ctx, ls.p.p);
       if (prof) prof_halo.emplace_back(ha, prof_event());
       ++n_halo_loop;
@@ -2209,7 +2278,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
     }
     else {
       if (ls.halo) {
-        const size_t ha = prof ? prof_event() : 0;
+        const size_t ha = prof ? prof_event(true) : 0;
         halo_exchange(*ls.halo, ctx, ls.p.p);
         if (prof) prof_halo.emplace_back(ha, prof_event());
         ++n_halo_loop;
@@ -2249,17 +2318,10 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   rel = rz0 > 0 ? std::sqrt(std::fabs(ls.pinned[it & 1] / rz0)) : 0.0;
   if (ls.halo) halo_exchange(*ls.halo, ctx, ls.sol.p);  // m_u.synchronize()
   if (st) {
-    auto sum_ms = [&](const std::vector<std::pair<size_t, size_t>>& v) {
-      double t = 0.0;
-      for (const auto& e : v) {
-        float m = 0.f;
-        AFEM_HIP(hipEventElapsedTime(&m, ls.prof_ev[e.first], ls.prof_ev[e.second]));
-        t += m;
-      }
-      return t;
-    };
-    st->halo_wait_ms = prof ? sum_ms(prof_halo) : 0.0;
-    st->allreduce_ms = prof ? sum_ms(prof_ar) : 0.0;
+    if (prof || prof_pc) prof_drain();
+    st->precond_ms = prof_pc ? prof_pc_ms : 0.0;
+    st->halo_wait_ms = prof ? prof_halo_ms : 0.0;
+    st->allreduce_ms = prof ? prof_ar_ms : 0.0;
     st->halo_bytes = ls.halo ? 8 * ls.halo->n_send : 0;
     st->n_halo = n_halo_loop;
     st->n_allreduce = n_ar_loop;

@@ -83,8 +83,11 @@ class Elastodynamics3D:
         self.h = h
         # "multigrid": the geometric multigrid V-cycle on structured boxes (one rank or z-slabs), built at
         # the first step and reused (the Newmark operator c0 M + K is the same every step)
-        blk, mgm = {"jacobi": (0, 0), "block3": (3, 0), "multigrid": (0, 2)}[preconditioner]
+        # "amg-reuse": the algebraic multigrid (any mesh; rebuilt when dt changes the operator)
+        blk, mgm, amg = {"jacobi": (0, 0, 0), "block3": (3, 0, 0), "multigrid": (0, 2, 0),
+                         "amg-reuse": (0, 0, 2)}[preconditioner]
         o = C.SolverOpts(C.AFEM_SOLVER_PCG, max_iter, rtol, 0.0, 8, 0, 0, blk, mgm)
+        o.amg = amg
         call("afem_elastodynamics_set_solver_options", self.h, ctypes.byref(o))
         self.t = 0.0
         self.last_stats = None
@@ -94,7 +97,8 @@ class Elastodynamics3D:
         call("afem_elastodynamics_step", self.h, ctypes.byref(st))
         self.t += self.dt
         self.last_stats = dict(iterations=st.iterations, converged=bool(st.converged), rel_residual=st.rel_residual,
-                               residual_norm=st.residual_norm, solve_ms=st.solve_ms)
+                               residual_norm=st.residual_norm, solve_ms=st.solve_ms, amg_levels=st.amg_levels,
+                               amg_setup_ms=st.amg_setup_ms, precond_ms=st.precond_ms)
         return self.last_stats
 
     def setDirichlet(self, dofs, values):
@@ -111,6 +115,27 @@ class Elastodynamics3D:
         """dt from the next step on (passmo's shortened final step, :525-530)."""
         call("afem_elastodynamics_set_time_step", self.h, float(dt))
         self.dt = float(dt)
+
+    def profile(self, on: bool = True):
+        """Per-phase HIP-event times of every following step (step_timing())."""
+        call("afem_elastodynamics_profile", self.h, 1 if on else 0)
+
+    def step_timing(self) -> dict:
+        t = C.StepTiming()
+        call("afem_elastodynamics_step_timing", self.h, ctypes.byref(t))
+        return {f: getattr(t, f) for f, _ in C.StepTiming._fields_ if f != "reserved0"}
+
+    def operators(self):
+        """The last step's operators on the device: dict(lhs = CsrView of c0 M +
+        K (block 3, CSR-row order), scalar_rows / scalar_cols = device pointers
+        of the scalar CSR structure of those values, mass = device pointer of
+        the mass values on it, c = the constants c0 .. c10)."""
+        v = C.CsrView()
+        sr, sc, mp = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        c = (ctypes.c_double * 11)()
+        call("afem_elastodynamics_operators", self.h, ctypes.byref(v), ctypes.byref(sr), ctypes.byref(sc),
+             ctypes.byref(mp), c)
+        return dict(lhs=v, scalar_rows=sr.value, scalar_cols=sc.value, mass=mp.value, c=list(c))
 
     def state_dptrs(self):
         u, v, a = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()

@@ -274,6 +274,91 @@ def with_traffic(rf, leg, size, kernel_ms):
     return rf
 
 
+def cg_traffic(leg, size, n_own, iter_per_s):
+    """CG fraction in bytes actually moved: the SpMV's PMC
+    bytes per call from the committed profile (profiles/pmc_<leg>.json: the
+    pattern SpMV does not read the column indices cg_bytes counts) + the two
+    vector passes of an iteration (80 B per row, cg_bytes), times this run's
+    iterations per second; and the SpMV's own moved-byte fraction at the
+    profile's kernel mean."""
+    pm = leg_profile(leg, size)
+    if pm is None:
+        return {}
+    b = pm["hbm_bytes_per_launch"] + 80 * n_own
+    out = {"cg_traffic_per_iter": int(b), "cg_frac_traffic": round(b * iter_per_s / 1e9 / HBM_PEAK_GBS, 4),
+           "spmv_traffic": int(pm["hbm_bytes_per_launch"]), "spmv_profile": pm.get("tag")}
+    if pm.get("kernel_mean_ms"):
+        out["spmv_kernel_ms"] = round(pm["kernel_mean_ms"], 4)
+        out["spmv_frac_traffic"] = round(pm["hbm_bytes_per_launch"] / (pm["kernel_mean_ms"] * 1e-3) / 1e9
+                                         / HBM_PEAK_GBS, 4)
+    return out
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if d is not None and k in d}
+
+
+def compact_line(out):
+    """The LAST stdout line (the driver keeps ~8 KB of stdout
+    and only the contract keys of the parsed line): the contract keys, the
+    headline's roofline and CPU baseline without their notes, the CG half of
+    the metric with its moved-byte fraction, and one summary per side leg
+    (kernel ms, frac, frac_traffic ...).  The full record is the preceding
+    {"bench_detail": ...} line."""
+    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    c = _pick(out, keys)
+    cfg = out["config"]
+    c["config"] = {"workload": cfg["workload"].split(",")[0], **_pick(cfg, ("n", "dof_total", "nnz_rank0",
+                                                                           "parallelism"))}
+    c["roofline"] = _pick(out["roofline"], ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
+                                            "frac_traffic", "kernel_ms", "algorithmic_bytes_per_launch",
+                                            "bytes_kernel_min", "frac_kernel_min", "profile_kernel_ms",
+                                            "frac_profile", "traffic_profile"))
+    cpu = out.get("cpu_baseline")
+    if cpu:
+        c["cpu_baseline"] = {**_pick(cpu, ("value", "unit", "cores", "kind", "value_single_thread")),
+                             "sample": "C2 itself, oracle cell loop (OpenMP, atomic adds), median of 5"}
+    c.update(_pick(out, ("value_unsettled", "ms_per_step_unsettled", "cg_iter_per_s", "cg_roofline_frac",
+                         "cg_frac_traffic", "spmv_frac_traffic", "cg_ms_per_iter")))
+    if out.get("cpu_baseline_cg"):
+        c["cpu_cg_iter_per_s"] = out["cpu_baseline_cg"]["value"]
+
+    def leg(e, extra=()):
+        r = e.get("roofline", {})
+        s = {"ms": e.get("kernel_ms", e.get("kernel_ms_median")), "frac": r.get("frac"),
+             "frac_traffic": r.get("frac_traffic"), "frac_kernel_min": r.get("frac_kernel_min")}
+        s.update(_pick(e, extra))
+        return {k: v for k, v in s.items() if v is not None}
+
+    legs = {}
+    if "c4" in out:
+        legs["c4"] = leg(out["c4"], ("cg_iter_per_s", "cg_roofline_frac", "cg_frac_traffic"))
+    for k in ("c3", "c2_generic", "generic_unstructured", "c2_arrays", "c2_arrays_natural", "unstructured"):
+        if k in out:
+            legs[k] = leg(out[k], ("evaluations_per_cell",))
+    u = out.get("unstructured", {}).get("solve")
+    if u:
+        legs["unstructured"]["solve_ms"] = {"jacobi": u["jacobi"]["solve_ms"], "amg": u["amg"]["solve_ms"],
+                                            "amg_iterations": u["amg"]["iterations"]}
+    if "c5" in out:
+        c5 = out["c5"]
+        b = c5.get("breakdown", {})
+        legs["c5"] = {"ms_per_step": c5.get("ms_per_step"), "cg_iterations": c5.get("cg_iterations_per_step"),
+                      "converged": all(c5.get("converged", [False])),
+                      **_pick(b, ("assemble_ms", "rhs_ms", "solve_ms", "precond_ms", "pcg_spmv_vectors_ms",
+                                  "vcycle_ms_per_iteration")),
+                      "assembly_frac": b.get("assembly_roofline", {}).get("frac"),
+                      "jacobi_ms_per_step": c5.get("jacobi_ms_per_step")}
+    if legs:
+        c["legs"] = legs
+    if out.get("per_rank"):
+        c["per_rank"] = [_pick(p, ("rank", "assembly_kernel_ms", "step_ms_own", "cg_ms_per_iter_own",
+                                   "halo_wait_ms_per_iter", "allreduce_ms_per_iter")) for p in out["per_rank"]]
+    c["detail"] = "the bench_detail line above"
+    return c
+
+
 def settle(ctx, step, ms):
     """GPU clocks ramp over the first tens of milliseconds of load after an
     idle spell (tools/warm_probe.py, DESIGN.md section 5: the cube kernel's
@@ -345,6 +430,7 @@ def poisson_c4(ctx, af, n, reps=5, warmup=2, cg_iters=50, settle_ms=150.0):
                                                                        / HBM_PEAK_GBS, 4),
            "cg_device_ms": round(st["solve_ms"], 2), "cg_spmv": SPMV_KERNELS.get(st["spmv_kernel"]),
            "sparsity_ms": round(sp_ms, 1), "settle_ms": settle_ms, "settle_steps": settle_steps}
+    out.update(cg_traffic("c4_spmv", n, mesh.n_own_nodes, ips))
     with_traffic(out["roofline"], "c4", n, kms)
     ctx.free(dbottom)
     ls.reset()
@@ -644,7 +730,42 @@ def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2, settle_ms=150.0
     return out
 
 
-def elastodynamics_c5(ctx, af, n, steps, preconditioners=("multigrid", "jacobi")):
+def c5_breakdown(dyn, steps):
+    """Where a C5 step goes: `steps` more steps with the
+    per-phase HIP events of afem_elastodynamics_profile (outside the timed
+    steps above: the events and the per-cycle pairs would perturb them), the
+    median of each phase, and the block-3 roofline of the re-assembly kernel:
+    c0 M + K and the body-force RHS on the fixed structure, algorithmic bytes as
+    C3's (incidence table 4 B per (row, cell), coordinates 24 B per node, row
+    offsets 8 B, block columns 4 B + 72 B of values per block, RHS 24 B per
+    node)."""
+    dyn.profile(True)
+    ts = []
+    for _ in range(steps):
+        dyn.step()
+        ts.append(dyn.step_timing())
+    dyn.profile(False)
+    med = {k: float(np.median([t[k] for t in ts])) for k in ("assemble_ms", "rhs_ms", "bc_ms", "solve_ms",
+                                                              "precond_ms", "update_ms", "total_ms", "iterations")}
+    t0 = ts[0]
+    n_own, n_loc, nnz_b, n_inc = t0["n_own_nodes"], t0["n_nodes"], t0["nnz_blocks"], t0["n_incidences"]
+    ab = 4 * n_inc + 24 * n_loc + 8 * (n_own + 1) + 76 * nnz_b + 24 * n_own
+    ka = med["assemble_ms"]
+    it = max(med["iterations"], 1.0)
+    pcg_other = med["solve_ms"] - med["precond_ms"]
+    return {"steps": steps, "assemble_ms": round(ka, 4), "rhs_ms": round(med["rhs_ms"], 4),
+            "bc_ms": round(med["bc_ms"], 4), "solve_ms": round(med["solve_ms"], 3),
+            "precond_ms": round(med["precond_ms"], 3), "pcg_spmv_vectors_ms": round(pcg_other, 3),
+            "update_ms": round(med["update_ms"], 4), "total_ms": round(med["total_ms"], 3),
+            "iterations": med["iterations"], "vcycle_ms_per_iteration": round(med["precond_ms"] / it, 4),
+            "pcg_spmv_vectors_ms_per_iteration": round(pcg_other / it, 4),
+            "assembly_roofline": {"bound": "hbm", "kernel": "k_assemble_elast_strip (c0 M + K + body force)",
+                                  "algorithmic_bytes_per_launch": int(ab),
+                                  "achieved": round(ab / (ka * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(ab / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def elastodynamics_c5(ctx, af, n, steps, preconditioners=("multigrid", "jacobi"), profile_steps=3):
     """BASELINE config C5 on one GPU: 3D Newmark elastodynamics, every step
     re-assembles c0 M + K and the body-force RHS on the fixed block-3
     structure, adds M (c0 U + c3 V + c4 A), clamps the x = 0 face by penalty,
@@ -681,6 +802,8 @@ def elastodynamics_c5(ctx, af, n, steps, preconditioners=("multigrid", "jacobi")
         out[f"{key}iterations"] = iters
         out[f"{key}converged"] = conv
         out[f"{key}first_step_ms"] = round(first_ms, 1)
+        if pc == preconditioners[0]:
+            out["breakdown"] = c5_breakdown(dyn, profile_steps)
         dyn.close()
     mesh.close()
     return out
@@ -1103,7 +1226,10 @@ def main():
             **({"per_rank": per_rank} if per_rank else {}),
             **extras,
         }
-        print(json.dumps(out), flush=True)
+        if world == 1 and args.scaling == "weak":
+            out.update(cg_traffic("c2_spmv", n, n_own, cg_iter_per_s))
+        print(json.dumps({"bench_detail": out}), flush=True)
+        print(json.dumps(compact_line(out)), flush=True)
     if dbottom is not None:
         ctx.free(dbottom)
     if comm:

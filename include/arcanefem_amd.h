@@ -431,6 +431,9 @@ typedef struct afem_solve_stats {
   int64_t amg_coarse_rows;   /* rows of the coarsest level */
   double amg_complexity;     /* operator complexity: non-zeros of all levels / the matrix's */
   double amg_setup_ms;       /* host time of this solve's hierarchy build (0 when reused; inside solve_ms) */
+  /* with afem_solver_opts.profile_comm: device time of the loop's preconditioner
+   * applications (multigrid / AMG cycles, HIP events), else 0 */
+  double precond_ms;
 } afem_solve_stats;
 #define AFEM_SPMV_STREAM 0   /* CSR-stream (columns read from the CSR) */
 #define AFEM_SPMV_PATTERN 1  /* CSR-stream, interior-stencil rows form their columns */
@@ -588,6 +591,37 @@ int afem_elastodynamics_set_dirichlet(afem_elastodynamics* dyn, const int32_t* d
 int afem_elastodynamics_set_time_step(afem_elastodynamics* dyn, double dt);
 /* device arrays of 3*n_own_nodes doubles (DoF lid = 3 node + i) */
 int afem_elastodynamics_state(afem_elastodynamics* dyn, double** u, double** v, double** a);
+/* The step's operators on the device, for checks and callers that post-process
+ * (passmo assembles the same c0 M + K on the CPU, ElastodynamicModule.cc:
+ * 1389-1793): lhs = the last step's assembled c0 M + K(c1, c2) (block 3,
+ * CSR-row order, the clamped DoFs' penalty diagonal included); scalar_rows /
+ * scalar_cols = the same values' scalar CSR structure (3 n_block_rows + 1 row
+ * offsets, 9 nnz_blocks columns: what the PCG reads); mass_values = the
+ * consistent mass M on that structure; c[11] = the step's constants c0 .. c10
+ * (modules/elastodynamics/FemModule.cc:255-290).  Any out pointer may be NULL. */
+int afem_elastodynamics_operators(afem_elastodynamics* dyn, afem_csr_view* lhs, const int64_t** scalar_rows,
+                                  const int32_t** scalar_cols, const double** mass_values, double* c);
+/* Per-phase device times of every step while on (HIP events on the context
+ * stream; off by default: no events recorded).  Also times the PCG's
+ * preconditioner applications (afem_solve_stats.precond_ms). */
+int afem_elastodynamics_profile(afem_elastodynamics* dyn, int on);
+typedef struct afem_step_timing {
+  double assemble_ms;  /* fused block-3 re-assembly of c0 M + K + body force */
+  double rhs_ms;       /* RHS operators: lincombs + mass (and damping) SpMVs */
+  double bc_ms;        /* penalty lists + the Newmark predictor (the warm start) */
+  double solve_ms;     /* the PCG (setup of a new multigrid hierarchy included) */
+  double precond_ms;   /* part of solve_ms: the preconditioner applications */
+  double update_ms;    /* imposed values + Newmark state update */
+  double total_ms;     /* first to last event */
+  int32_t iterations;
+  int32_t reserved0;
+  int64_t nnz_blocks;   /* block non-zeros of the structure */
+  int64_t n_incidences; /* (owned row, incident cell) pairs of the structure */
+  int64_t n_nodes;      /* local nodes (owned + ghost) */
+  int64_t n_own_nodes;
+} afem_step_timing;
+/* the last profiled step's times (zeros before the first one) */
+int afem_elastodynamics_step_timing(afem_elastodynamics* dyn, afem_step_timing* out);
 int afem_elastodynamics_destroy(afem_elastodynamics* dyn);
 
 /* ---------------------------------------------------------------- communicator */

@@ -258,3 +258,73 @@ def test_amg_graph_replay_bitwise(ctx, variant):
     assert np.array_equal(xs["0"], xs["1"])
     bsr.close()
     mesh.close()
+
+
+def test_amg_reuse_rebuilds_on_new_values(ctx, variant):
+    """amg-reuse keeps the hierarchy only while the CSR arrays and sizes are
+    the same: a second setCSRValues with the same sizes (new device
+    buffers that may sit at the old addresses) rebuilds it, and the solve of the
+    doubled matrix is half the first solution."""
+    variant("AFEM_AMG_DENSE", "16")
+    mesh, gm = _gmsh_mesh(ctx, "sphere_cut.msh")
+    cells, coords, _ = mesh.download()
+    dn = _dirichlet_nodes(gm, coords, "sphere_cut.msh")
+    bsr, ls0 = _poisson(ctx, mesh)
+    rows, cols, vals = bsr.download()
+    rhs = ls0.rhs_host()
+    n = mesh.n_own_nodes
+    ls = af.DoFLinearSystem().initialize(ctx, n, mesh.n_nodes)
+    sols = []
+    for scale in (1.0, 2.0):
+        v = vals * scale
+        ls.setCSRValues(rows[:-1], None, cols, v)
+        ctx.to_device(ls.rhsVariable(), rhs)
+        ls.applyDirichletViaPenalty(dn, 0.5, 1e30)
+        x, st = _solve(ls, "amg-reuse")
+        assert st["amg_setup_ms"] > 0.0, (scale, st)  # built (first) / rebuilt (new values)
+        ctx.to_device(ls.rhsVariable(), rhs)
+        ls.applyDirichletViaPenalty(dn, 0.5, 1e30)
+        x2, st2 = _solve(ls, "amg-reuse")
+        assert st2["amg_setup_ms"] == 0.0 and np.array_equal(x, x2)  # kept
+        sols.append(x)
+    free = np.ones(n, dtype=bool)
+    free[dn] = False
+    # 2 A x' = b on the free rows with the same Dirichlet values: x' - g = (x - g) / 2
+    g = 0.5
+    assert np.abs((sols[1][free] - g) - 0.5 * (sols[0][free] - g)).max() <= 1e-9 * np.abs(sols[0]).max()
+    ls.reset()
+    ls0.reset()
+    bsr.close()
+    mesh.close()
+
+
+def test_amg_reuse_and_time_step_change(ctx, variant):
+    """Elastodynamics with the amg-reuse preconditioner: a dt change (passmo's
+    shortened last step, afem_elastodynamics_set_time_step) changes c0 M + K, so
+    the hierarchy is rebuilt at the next step; states equal the
+    Jacobi-PCG run's."""
+    from arcanefem_amd.elastodynamics import Elastodynamics3D
+
+    variant("AFEM_AMG_DENSE", "32")
+    mesh = af.Mesh.structured(ctx, 3, 6)
+    cells, coords, _ = mesh.download()
+    fixed = np.nonzero(coords[:, 0] < 0.5 / 6)[0]
+    kw = dict(body_force=(0.0, -9.81, 1.0), fixed_nodes=fixed, rtol=1e-13)
+    runs = {}
+    for pc in ("amg-reuse", "jacobi"):
+        sim = Elastodynamics3D(ctx, mesh, 21e5, 0.28, 1.0, 1e-3, preconditioner=pc, **kw)
+        setups = []
+        for k in range(5):
+            if k == 3:
+                sim.setTimeStep(4e-4)
+            st = sim.step()
+            assert st["converged"], (pc, k, st)
+            setups.append(st["amg_setup_ms"])
+        if pc == "amg-reuse":
+            assert setups[0] > 0 and setups[1] == 0 and setups[2] == 0, setups
+            assert setups[3] > 0 and setups[4] == 0, setups  # rebuilt after the dt change, then kept
+        runs[pc] = sim.state_host()
+        sim.close()
+    for a, b in zip(runs["amg-reuse"], runs["jacobi"]):
+        assert np.abs(a - b).max() <= 1e-8 * np.abs(b).max()
+    mesh.close()

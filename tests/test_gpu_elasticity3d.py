@@ -514,3 +514,110 @@ def test_c3_full_size_properties(ctx):
     ls.reset()
     bsr.close()
     mesh.close()
+
+
+def test_c5_full_size_properties(ctx):
+    """BASELINE config C5's per-step operator at the bench's size (n = 128:
+    2.15 M nodes, 6.45 M DoF), after Newmark steps with the
+    multigrid PCG (modules/passmo/ElastodynamicModule.cc:469-536 re-assembles
+    it every step): the re-assembled c0 M + K(c1, c2) read back through
+    afem_elastodynamics_operators --
+      * c0 = rho / (beta dt^2) and c1, c2 = lambda, 2 mu (FemModule.cc:255-264);
+      * symmetry on sampled scalar rows;
+      * the stiffness part lhs - c0 M has the six rigid-body modes in its kernel
+        on every unclamped row (orc_spmv on the host), and the clamped rows
+        carry the penalty diagonal;
+      * the consistent mass sums to 3 x volume (unit density; rho is in c0);
+      * sampled block rows equal the oracle's (orc_assemble_elasticity_tet with
+        c0 on the row's cube neighbourhood, generator coordinates) to 1e-12 of
+        the row's largest entry;
+      * every step converged, displacements finite and downward."""
+    from arcanefem_amd.elastodynamics import Elastodynamics3D
+
+    n = 128
+    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+    N = mesh.n_own_nodes
+    ids = np.arange(N)
+    fixed = ids[ids % (n + 1) == 0].astype(np.int32)
+    rho, dt = 2.5, 1e-3
+    dyn = Elastodynamics3D(ctx, mesh, E, NU, rho, dt, body_force=(0.0, 0.0, -1.0), fixed_nodes=fixed, rtol=1e-8,
+                           preconditioner="multigrid")
+    for _ in range(3):
+        st = dyn.step()
+        assert st["converged"], st
+    U = dyn.state_host()[0]
+    assert np.isfinite(U).all() and U[2::3].sum() < 0
+    ops = dyn.operators()
+    v, c = ops["lhs"], ops["c"]
+    beta = 0.25
+    assert abs(c[0] - rho / (beta * dt * dt)) <= 1e-12 * c[0]
+    assert abs(c[1] - LAM) <= 1e-12 * LAM and abs(c[2] - MU2) <= 1e-12 * MU2
+    nb, nnz_b = v.n_block_rows, v.nnz_blocks
+    assert nb == N and v.block_size == 3 and v.ordered_per_block == 0
+    n3, nnz = 3 * nb, 9 * nnz_b
+    brows = ctx.to_host(v.rows, nb + 1, np.int64)
+    bcols = ctx.to_host(v.columns, nnz_b, np.int32)
+    rows = ctx.to_host(ops["scalar_rows"], n3 + 1, np.int64)
+    cols = ctx.to_host(ops["scalar_cols"], nnz, np.int32)
+    lhs = ctx.to_host(v.values, nnz, np.float64)
+    mass = ctx.to_host(ops["mass"], nnz, np.float64)
+    cells, coords, _ = mesh.download()
+    dyn.close()
+    mesh.close()
+    # mass total (unit density) = 3 x volume of the jittered box
+    xc = coords[cells]
+    vol = np.abs(np.linalg.det(np.stack([xc[:, 1] - xc[:, 0], xc[:, 2] - xc[:, 0], xc[:, 3] - xc[:, 0]], 1))).sum() / 6
+    del xc
+    assert abs(mass.sum() - 3.0 * vol) <= 1e-11 * vol, (mass.sum(), 3 * vol)
+    clamped = np.zeros(n3, dtype=bool)
+    for d in range(3):
+        clamped[3 * fixed + d] = True
+    # stiffness part: rigid modes in its kernel on the unclamped rows
+    K = lhs - c[0] * mass
+    kmax = np.abs(K[np.abs(K) < 1e20]).max()
+    X = coords[:N]
+    modes = []
+    for a in range(3):
+        u = np.zeros((N, 3))
+        u[:, a] = 1.0
+        modes.append(u)
+    for w in np.eye(3):
+        modes.append(np.cross(w, X))
+    Kf = np.where(np.abs(K) < 1e20, K, 0.0)
+    worst = 0.0
+    for u in modes:
+        r = O.spmv(rows, cols, Kf, u.ravel())
+        worst = max(worst, np.abs(r[~clamped]).max() / (kmax * np.abs(u).max()))
+    del Kf
+    assert worst <= 1e-11, worst
+    # sampled scalar rows: symmetry, and the clamped rows' penalty diagonal
+    rng = np.random.default_rng(128)
+    for r in np.concatenate([rng.integers(0, n3, 300), 3 * fixed[:3]]):
+        s, e = rows[r], rows[r + 1]
+        cc = cols[s:e]
+        for t in range(s, e):
+            q = int(cols[t])
+            tt = rows[q] + np.searchsorted(cols[rows[q]:rows[q + 1]], r)
+            assert cols[tt] == r
+            if q != r:
+                assert abs(lhs[tt] - lhs[t]) <= 1e-13 * kmax
+        if clamped[r]:
+            assert lhs[s + np.searchsorted(cc, r)] == 1.0e30
+    # sampled block rows against the oracle's c0 M + K on the cube neighbourhood
+    worst_row = 0.0
+    np1 = n + 1
+    for g in rng.integers(0, N, 60):
+        if g % np1 == 0:
+            continue  # clamped node: its rows carry the penalty
+        nodes, local, xyz = _kuhn_neighbourhood(n, int(g))
+        orp, ocols = O.sparsity(nodes.shape[0], nodes.shape[0], local)
+        ov, _ = O.assemble_elasticity_tet(nodes.shape[0], local, xyz, orp, ocols, c[1], c[2], c0=c[0])
+        rl = int(np.searchsorted(nodes, g))
+        s, e = int(brows[g]), int(brows[g + 1])
+        assert np.array_equal(bcols[s:e], nodes[ocols[orp[rl]:orp[rl + 1]]])
+        orow = ov[9 * orp[rl]:9 * orp[rl + 1]].reshape(-1, 3, 3)
+        grow = lhs[9 * s:9 * e].reshape(3, e - s, 3).transpose(1, 0, 2)  # CSR-row order -> blocks
+        worst_row = max(worst_row, np.abs(grow - orow).max() / np.abs(orow).max())
+    assert worst_row <= VAL_TOL, worst_row
+    print(f"C5 n={n}: {n3} DoF, {nnz_b} blocks; rigid modes of lhs - c0 M: {worst:.2e}; mass total / 3V - 1 = "
+          f"{mass.sum() / (3 * vol) - 1:.2e}; sampled block rows vs oracle max rel {worst_row:.2e}")

@@ -261,3 +261,69 @@ def test_solution_parity_at_c2_size(ctx):
     assert res_g <= 2e-9 and res_o <= 2e-9
     assert np.abs(xg[bottom] - 0.5).max() <= 1e-12
     assert diff <= 1e-10
+
+
+def test_solution_parity_at_c4_size(ctx):
+    """The north-star solution gate at 10^8 DoF (SURVEY §7 2d;
+    the reference's solve on the same CSR, femutils/DoFLinearSystem.cc:106-164):
+    C4's problem (n = 463: 99.9 M DoF, 1.49e9 non-zeros, penalty Dirichlet
+    z = 0) solved on the GPU by the PCG with the algebraic multigrid to the
+    tightest attainable residual; the ORACLE then assembles its own matrix and
+    RHS (orc_assemble_poisson_omp + orc_dirichlet_penalty on the downloaded mesh
+    and structure) and the GPU solution's true residual b - A x over the free
+    rows is computed with that matrix on the host (orc_spmv).  Gate: the
+    rounding floor of A x itself, eps * (|A| |x|) per row -- the residual of
+    the exact solution evaluated in double cannot be smaller; the measured
+    ratio, the relative residual and the condition-number bound on the
+    solution's error (kappa ~ lambda_max / lambda_min, Gershgorin over the free
+    rows / the continuous (pi/2)^2 h^3 of the z = 0-clamped unit box) are
+    printed."""
+    n = 463
+    t0 = time.time()
+    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+    N = mesh.n_own_nodes
+    bsr, ls = _assemble(ctx, mesh, 5.5)
+    bsr.toLinearSystem(ls)
+    bottom = mesh.bottom_nodes()
+    ls.applyDirichletViaPenalty(bottom, 0.5, 1e30)
+    # n = 463 is prime: no geometric hierarchy; the algebraic multigrid (K-cycle, flexible CG)
+    ls.setSolverOptions(rtol=1e-15, max_iter=3000, preconditioner="amg")
+    st = ls.solve()
+    xg = ls.solution_host()
+    t_gpu = time.time() - t0
+    cells, coords, _ = mesh.download()
+    rows, cols, _ = bsr.download()
+    ls.reset()
+    bsr.close()
+    mesh.close()
+    t1 = time.time()
+    vals, rhs = O.assemble_poisson_omp(N, cells, coords, rows, cols, 5.5)
+    del cells, coords
+    O.dirichlet_penalty(bottom, 0.5, 1e30, rows, cols, vals, rhs)
+    t_orc = time.time() - t1
+    free = np.ones(N, dtype=bool)
+    free[bottom] = False
+    r = rhs - O.spmv(rows, cols, vals, xg)
+    bn = np.linalg.norm(rhs[free])
+    res = float(np.linalg.norm(r[free]) / bn)
+    # lambda_max by Gershgorin on the free rows (the penalty rows are decoupled constraints)
+    np.abs(vals, out=vals)
+    floor = np.finfo(np.float64).eps * O.spmv(rows, cols, vals, np.abs(xg))
+    floor_rel = float(np.linalg.norm(floor[free]) / bn)
+    rowabs = O.spmv(rows, cols, vals, np.ones(N))
+    lam_max = float(rowabs[free].max())
+    del vals, rows, cols
+    h = 1.0 / n
+    lam_min = (np.pi / 2) ** 2 * h ** 3
+    kappa = lam_max / lam_min
+    print(f"\nC4 solution parity: N={N} gpu AMG-PCG {st['iterations']} it ({st['amg_levels']} levels, setup {st['amg_setup_ms']:.0f} ms), rel_pcg {st['rel_residual']:.2e}, "
+          f"{t_gpu:.0f} s | oracle assembly {t_orc:.1f} s | true free-row residual with the oracle's A "
+          f"{res:.3e}, rounding floor eps|A||x| {floor_rel:.3e} (ratio {res / floor_rel:.2f}) | kappa ~ {kappa:.2e}: "
+          f"relative error bound kappa x residual {kappa * res:.2e}")
+    assert st["rel_residual"] <= 1e-13
+    assert np.abs(xg[bottom] - 0.5).max() <= 1e-12
+    # at the rounding floor: the residual of the computed x is within 10x of
+    # what evaluating A x in double resolves (the oracle's own Jacobi-PCG to
+    # rtol 1e-15 on its own matrix sits at 2.1x / 3.0x of this floor at n = 40 /
+    # 80: CG's attainable accuracy)
+    assert res <= 10.0 * floor_rel, (res, floor_rel)
