@@ -662,6 +662,14 @@ def c2_generic_leg(ctx, af, n, reps=10, warmup=6, atomic_reps=2, settle_ms=150.0
     sys.path.insert(0, os.path.join(ROOT, "examples"))
     import generic_example as gx
 
+    # the functor library is loaded (its code object registered) BEFORE the
+    # refinement imports torch: torch's wheel carries a second HIP + HSA runtime
+    # and rocprofiler-register (ROCm 7.0), and a code object first loaded after
+    # those under rocprofv3 --kernel-trace faults in the tool's launch hook
+    # (r05j; reproduced and isolated in r06c: tools/generic_trace_probe.py --
+    # torch first: SIGSEGV at the first k_assemble_units launch; library first,
+    # or no torch: clean; without the profiler all three run)
+    gx.load()
     if unstructured_levels > 0:
         from arcanefem_amd.gmsh import read_gmsh
 
