@@ -32,7 +32,13 @@
 //    Krylov weights replace the 1.7 overcorrection there;
 //  * constraint rows are taken out of the cycle as in multigrid.hip:
 //    z = F V(F r) + C D^-1 r.
-// One rank (the system carries no halo).  The V-cycle is symmetric (an SPD
+// Several ranks (a halo attached): the levels stay distributed -- each rank
+// aggregates its own rows, the coarse ghost columns and halo follow from the
+// fine halo (build_dist_coarse) -- until the global coarse size is below
+// AFEM_AMG_GATHER rows, then one level is gathered on every rank (all-reduce of
+// its COO) and the hierarchy below it is the one-rank one, built identically
+// everywhere; the Hypre BoomerAMG role on the Arcane communicator
+// (femutils/HypreDoFLinearSystem.cc:399-404, 686-742).  The V-cycle is symmetric (an SPD
 // preconditioner); the K-cycle is a nonlinear one: the PCG then takes the
 // flexible (Polak-Ribiere) beta, -(z.q)/(p.q) (linear_system.hip k_cg_dir_flex;
 // tested against the Jacobi-PCG and the plain V-cycle, test_amg_kcycle).
@@ -47,6 +53,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace afem {
@@ -220,20 +227,6 @@ __global__ void k_amg_orphan_agg(int64_t n, const int32_t* __restrict__ f, const
   if (f[i]) agg[i] = base + (int32_t)rank[i];
 }
 
-// Galerkin keys of the non-zeros: (agg i, agg j), or all ones outside the graph
-__global__ void k_amg_keys(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
-                           const int32_t* __restrict__ agg, unsigned long long* __restrict__ key)
-{
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int32_t ai = agg[i];
-  for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-    const int32_t j = ci[k];
-    const int32_t aj = (j >= 0 && j < n) ? agg[j] : -1;
-    key[k] = (ai >= 0 && aj >= 0) ? ((unsigned long long)(uint32_t)ai << 32 | (uint32_t)aj) : ~0ull;
-  }
-}
-
 __global__ void k_amg_iota(int64_t n, int64_t* __restrict__ x)
 {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -251,7 +244,7 @@ __global__ void k_amg_heads(int64_t m, const unsigned long long* __restrict__ ke
 // run r = [pos of head r, next head): its sum in the sorted (= CSR) order
 __global__ void k_amg_runs(int64_t m, const unsigned long long* __restrict__ key, const int64_t* __restrict__ src,
                            const double* __restrict__ v, const int32_t* __restrict__ head,
-                           const int64_t* __restrict__ hrank, int64_t* __restrict__ c_row_of,
+                           const int64_t* __restrict__ hrank, int64_t row_base, int64_t* __restrict__ c_row_of,
                            int32_t* __restrict__ c_col, double* __restrict__ c_val)
 {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -260,7 +253,7 @@ __global__ void k_amg_runs(int64_t m, const unsigned long long* __restrict__ key
   double s = 0.0;
   for (int64_t q = k; q < m && key[q] == kk; ++q) s += v[src[q]];
   const int64_t r = hrank[k];
-  c_row_of[r] = (int64_t)(kk >> 32);
+  c_row_of[r] = (int64_t)(kk >> 32) - row_base;
   c_col[r] = (int32_t)(kk & 0xffffffffu);
   c_val[r] = s;
 }
@@ -430,6 +423,50 @@ __global__ __launch_bounds__(64) void k_amg_gemv(int n, const double* __restrict
   if (threadIdx.x == 0) x[i] = s;
 }
 
+// an independent set that did not settle: its undecided nodes become roots
+// (aggregates may then touch; the aggregation stays valid)
+__global__ void k_amg_promote(int64_t n, uint64_t* __restrict__ t)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t ti = t[i];
+  if ((ti >> 62) == 1) t[i] = (2ull << 62) | (ti & ((1ull << 62) - 1));
+}
+
+// Galerkin keys through a column map: (row_base + agg i, cmap[j]) -- cmap is
+// agg on one rank, the coarse local index (owned aggregates, then the coarse
+// ghosts) on a distributed level, the global coarse index toward a gathered
+// level; all ones outside the graph
+__global__ void k_amg_keys_map(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                               const int32_t* __restrict__ agg, int64_t row_base, const int32_t* __restrict__ cmap,
+                               int64_t ncol, unsigned long long* __restrict__ key)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t ai = agg[i];
+  for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+    const int32_t j = ci[k];
+    const int32_t aj = (j >= 0 && j < ncol) ? cmap[j] : -1;
+    key[k] = (ai >= 0 && aj >= 0) ? ((unsigned long long)(uint32_t)(row_base + ai) << 32 | (uint32_t)aj) : ~0ull;
+  }
+}
+
+__global__ void k_amg_i2d(int64_t n, const int32_t* __restrict__ a, double* __restrict__ d)
+{
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = (double)a[i];
+}
+
+// the gathered level's global COO (all-reduced as doubles) -> row ids, columns
+__global__ void k_amg_coo_unpack(int64_t m, const double* __restrict__ r, const double* __restrict__ c,
+                                 int64_t* __restrict__ row_of, int32_t* __restrict__ col)
+{
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  row_of[k] = (int64_t)r[k];
+  col[k] = (int32_t)c[k];
+}
+
 double env_double(const char* name, double dflt)
 {
   const char* v = variant(name);
@@ -440,6 +477,16 @@ double env_double(const char* name, double dflt)
 
 struct AmgLevel {
   int64_t n = 0, nnz = 0;
+  // columns of the level's vectors: n on one rank and on replicated levels;
+  // owned + ghost columns on a distributed level (the ghost part filled by
+  // the level's halo exchange before every product)
+  int64_t ncol = 0;
+  bool dist = false;
+  Halo* H = nullptr;               // the level's halo (level 0: the system's; coarser: own_halo)
+  std::unique_ptr<Halo> own_halo;
+  // the next level replicated on every rank (gathered): this rank's
+  // aggregates are its rows [gather_off, gather_off + nc_local)
+  int64_t gather_off = -1, nc_local = 0;
   const int64_t* rp = nullptr;
   const int32_t* ci = nullptr;
   const double* v = nullptr;
@@ -466,10 +513,14 @@ struct Amg {
   // steps preconditioned by the cycle below (K-cycle) instead of one cycle
   int kcycle = 0;
   bool fine_planned = true;
+  // several ranks: the communicator of the distributed levels (null on one rank)
+  Comm* comm = nullptr;
+  DevBuf<double> sums;  // all-reduced scalars (power iterations, K-cycle steps)
   // AFEM_AMG_GRAPH=1: the V-cycle replayed as a captured HIP graph (its
   // launches are fixed once the hierarchy is); keyed on (r, z, the solve's
   // SpMV plan).  Measured equal (2.93 ms per iteration either way, r05aa):
-  // the cycle is bound by its three fine-level products, not by launches
+  // the cycle is bound by its three fine-level products, not by launches.
+  // One rank only (a distributed cycle exchanges halos through the transport)
   bool use_graph = true;
   hipGraphExec_t gexec = nullptr;
   const double* g_r = nullptr;
@@ -488,10 +539,14 @@ struct Amg {
 
 void AmgDeleter::operator()(Amg* a) const { delete a; }
 
+namespace {
+bool multi_rank(const LinearSystem& ls) { return ls.halo && ls.halo->comm && comm_nranks(ls.halo->comm) > 1; }
+}  // namespace
+
 bool amg_available(const LinearSystem& ls)
 {
   if (!ls.csr_rows || !ls.csr_cols || !ls.csr_vals || ls.n_rows <= 0) return false;
-  if (ls.halo && ls.halo->comm && comm_nranks(ls.halo->comm) > 1) return false;  // one rank
+  if (multi_rank(ls) && ls.n_cols < ls.n_rows) return false;
   // hipcub's sorts of the setup take int counts: the non-zeros of every level
   // (the fine level's are the most) must stay below 2^31, else point Jacobi
   return ls.n_rows < (int64_t(1) << 31) && ls.csr_nnz < (int64_t(1) << 31);
@@ -519,6 +574,31 @@ double host_sum(Ctx& ctx, const DevBuf<double>& partial, int n)
   return s;
 }
 
+// the sum of v over the ranks (v itself on one rank)
+double allsum(Ctx& ctx, Amg& a, double v)
+{
+  if (!a.comm) return v;
+  AFEM_HIP(hipMemcpyAsync(a.sums.p, &v, sizeof(double), hipMemcpyHostToDevice, ctx.stream));
+  comm_allreduce(a.comm, ctx, a.sums.p, 1);
+  double r = 0.0;
+  AFEM_HIP(hipMemcpyAsync(&r, a.sums.p, sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  return r;
+}
+
+// element-wise sums over the ranks of a host vector
+std::vector<double> allsum_vec(Ctx& ctx, Amg& a, std::vector<double> h)
+{
+  if (!a.comm || h.empty()) return h;
+  DevBuf<double> d;
+  d.alloc(h.size());
+  AFEM_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, ctx.stream));
+  comm_allreduce(a.comm, ctx, d.p, (int64_t)h.size());
+  AFEM_HIP(hipMemcpyAsync(h.data(), d.p, h.size() * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  return h;
+}
+
 void spmv(Ctx& ctx, int epi, AmgLevel& L, const double* x, double* y, const double* b, double omega)
 {
   const unsigned g = grid_for(L.n * 8, 256);
@@ -535,37 +615,61 @@ void spmv(Ctx& ctx, int epi, AmgLevel& L, const double* x, double* y, const doub
   AFEM_LAUNCHED();
 }
 
+// the ghost part of a distributed level's vector (nothing on other levels)
+void halo(Ctx& ctx, AmgLevel& L, double* x)
+{
+  if (L.dist && L.H) halo_exchange(*L.H, ctx, x);
+}
+
 double power_lambda(Ctx& ctx, Amg& a, AmgLevel& L)
 {
-  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
-  hipLaunchKernelGGL(k_amg_fill, dim3(g), dim3(256), 0, ctx.stream, L.n, L.in.p, L.x.p);
-  hipLaunchKernelGGL(k_amg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, (const double*)nullptr, L.x.p,
-                     a.partial.p);
-  AFEM_LAUNCHED();
-  double nv = std::sqrt(host_sum(ctx, a.partial, (int)g)), lam = 0.0;
-  for (int it = 0; it < kPowerIts; ++it) {
-    spmv(ctx, 0, L, L.x.p, L.t.p, nullptr, 0.0);
-    hipLaunchKernelGGL(k_amg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, (const double*)L.dinv.p, L.t.p,
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, std::max<int64_t>(1, (L.n + 255) / 256));
+  if (L.n > 0) {
+    hipLaunchKernelGGL(k_amg_fill, dim3(g), dim3(256), 0, ctx.stream, L.n, L.in.p, L.x.p);
+    hipLaunchKernelGGL(k_amg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, (const double*)nullptr, L.x.p,
                        a.partial.p);
     AFEM_LAUNCHED();
-    const double nw = std::sqrt(host_sum(ctx, a.partial, (int)g));
+  }
+  const bool d = L.dist;
+  double nv = std::sqrt(d ? allsum(ctx, a, L.n > 0 ? host_sum(ctx, a.partial, (int)g) : 0.0)
+                          : host_sum(ctx, a.partial, (int)g)),
+         lam = 0.0;
+  for (int it = 0; it < kPowerIts; ++it) {
+    halo(ctx, L, L.x.p);
+    spmv(ctx, 0, L, L.x.p, L.t.p, nullptr, 0.0);
+    if (L.n > 0) {
+      hipLaunchKernelGGL(k_amg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, (const double*)L.dinv.p, L.t.p,
+                         a.partial.p);
+      AFEM_LAUNCHED();
+    }
+    const double ls = L.n > 0 ? host_sum(ctx, a.partial, (int)g) : 0.0;
+    const double nw = std::sqrt(d ? allsum(ctx, a, ls) : ls);
     lam = nv > 0 ? nw / nv : 0.0;
     if (!(nw > 0)) break;
-    hipLaunchKernelGGL(k_amg_mul, dim3(g), dim3(256), 0, ctx.stream, L.n, 1.0 / nw, L.t.p);
-    AFEM_LAUNCHED();
+    if (L.n > 0) {
+      hipLaunchKernelGGL(k_amg_mul, dim3(g), dim3(256), 0, ctx.stream, L.n, 1.0 / nw, L.t.p);
+      AFEM_LAUNCHED();
+    }
     std::swap(L.x, L.t);
     nv = 1.0;
   }
   return lam;
 }
 
-// the level's diagonal, graph membership, D^-1 and work vectors
+// the level's diagonal, graph membership, D^-1 and work vectors (x, t, r over
+// the level's columns, zeroed: their ghost part is only ever written by the
+// halo exchange)
 void level_prepare(Ctx& ctx, AmgLevel& L, const uint8_t* cons)
 {
+  if (L.ncol < L.n) L.ncol = L.n;
   L.diag.alloc(L.n > 0 ? L.n : 1);
   L.in.alloc(L.n > 0 ? L.n : 1);
   L.dinv.alloc(L.n > 0 ? L.n : 1);
-  for (auto* b : { &L.x, &L.t, &L.b, &L.r }) b->alloc(L.n > 0 ? L.n : 1);
+  for (auto* b : { &L.x, &L.t, &L.r }) {
+    b->alloc(L.ncol > 0 ? L.ncol : 1);
+    AFEM_HIP(hipMemsetAsync(b->p, 0, b->bytes(), ctx.stream));
+  }
+  L.b.alloc(L.n > 0 ? L.n : 1);
   if (L.n == 0) return;
   hipLaunchKernelGGL(k_amg_diag, dim3(grid_for(L.n, 256)), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci, L.v, cons,
                      L.diag.p, L.in.p);
@@ -574,10 +678,20 @@ void level_prepare(Ctx& ctx, AmgLevel& L, const uint8_t* cons)
   AFEM_LAUNCHED();
 }
 
-// aggregates of level L (L.agg, L.ap / L.mem); returns the aggregate count
+// aggregates of level L's own rows (L.agg, L.ap / L.mem); returns the
+// aggregate count.  Ghost columns are outside the strength graph
+// (k_amg_strength: j < n): a distributed level aggregates within each rank
 int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
 {
   const int64_t n = L.n;
+  if (n == 0) {
+    L.agg.alloc(1);
+    L.mem.alloc(1);
+    L.ap.alloc(1);
+    AFEM_HIP(hipMemsetAsync(L.ap.p, 0, sizeof(int64_t), ctx.stream));
+    ctx.sync();
+    return 0;
+  }
   const unsigned g = grid_for(n, 256);
   DevBuf<uint64_t> t, m;
   t.alloc(n);
@@ -611,11 +725,10 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
     ctx.sync();
     if (hl == 0) break;
     if (round == 63) {
-      //  the independent set did not settle in 64 rounds: no coarse
-      // level below this one -- it becomes the coarsest, smoothed by Jacobi
-      // sweeps (amg_setup), instead of failing the solve
-      ctx.sync();
-      return 0;
+      //  the independent set did not settle in 64 rounds: the
+      // undecided nodes become roots instead of failing the solve
+      hipLaunchKernelGGL(k_amg_promote, dim3(g), dim3(256), 0, ctx.stream, n, t.p);
+      AFEM_LAUNCHED();
     }
   }
   DevBuf<int32_t> f;
@@ -675,8 +788,12 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
   return nc;
 }
 
-// C = P^T A P of level L's aggregates
-void galerkin(Ctx& ctx, AmgLevel& L, int64_t nc, AmgLevel& C)
+// The coarse operator's non-zeros of level L's rows, keyed (row_base + agg i,
+// cmap[j]): radix-sorted (stable), each run summed in the CSR order.  Out: the
+// rows (relative to row_base) of the n_out coarse rows, their columns and
+// values (COO in row order) and their count
+int64_t galerkin_coo(Ctx& ctx, AmgLevel& L, const int32_t* cmap, int64_t ncol, int64_t row_base,
+                     DevBuf<int64_t>& row_of, DevBuf<int32_t>& col, DevBuf<double>& val)
 {
   const int64_t nnz = L.nnz;
   DevBuf<unsigned long long> key, key_s;
@@ -685,10 +802,12 @@ void galerkin(Ctx& ctx, AmgLevel& L, int64_t nc, AmgLevel& C)
   key_s.alloc(nnz > 0 ? nnz : 1);
   src.alloc(nnz > 0 ? nnz : 1);
   src_s.alloc(nnz > 0 ? nnz : 1);
-  hipLaunchKernelGGL(k_amg_keys, dim3(grid_for(L.n, 256)), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci,
-                     (const int32_t*)L.agg.p, key.p);
-  hipLaunchKernelGGL(k_amg_iota, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz, src.p);
-  AFEM_LAUNCHED();
+  if (L.n > 0) {
+    hipLaunchKernelGGL(k_amg_keys_map, dim3(grid_for(L.n, 256)), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci,
+                       (const int32_t*)L.agg.p, row_base, cmap, ncol, key.p);
+    hipLaunchKernelGGL(k_amg_iota, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz, src.p);
+    AFEM_LAUNCHED();
+  }
   size_t tb = 0;
   AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.p, key_s.p, src.p, src_s.p, (int)nnz, 0, 64,
                                               ctx.stream));
@@ -702,32 +821,220 @@ void galerkin(Ctx& ctx, AmgLevel& L, int64_t nc, AmgLevel& C)
   DevBuf<int64_t> hrank;
   head.alloc(nnz > 0 ? nnz : 1);
   hrank.alloc(nnz + 1);
-  hipLaunchKernelGGL(k_amg_heads, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz,
-                     (const unsigned long long*)key_s.p, head.p);
-  AFEM_LAUNCHED();
+  if (nnz > 0) {
+    hipLaunchKernelGGL(k_amg_heads, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz,
+                       (const unsigned long long*)key_s.p, head.p);
+    AFEM_LAUNCHED();
+  }
   exclusive_scan_i32_to_i64(ctx, head.p, hrank.p, nnz);
   const int64_t cnnz = read_i64(ctx, hrank.p + nnz);
-  DevBuf<int64_t> row_of;
   row_of.alloc(cnnz > 0 ? cnnz : 1);
-  C.own_ci.alloc(cnnz > 0 ? cnnz : 1);
-  C.own_v.alloc(cnnz > 0 ? cnnz : 1);
-  hipLaunchKernelGGL(k_amg_runs, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz,
-                     (const unsigned long long*)key_s.p, src_s.p, L.v, head.p, hrank.p, row_of.p, C.own_ci.p,
-                     C.own_v.p);
-  AFEM_LAUNCHED();
-  C.own_rp.alloc(nc + 1);
-  AFEM_HIP(hipMemsetAsync(C.own_rp.p, 0, (nc + 1) * sizeof(int64_t), ctx.stream));
+  col.alloc(cnnz > 0 ? cnnz : 1);
+  val.alloc(cnnz > 0 ? cnnz : 1);
+  if (nnz > 0) {
+    hipLaunchKernelGGL(k_amg_runs, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz,
+                       (const unsigned long long*)key_s.p, src_s.p, L.v, head.p, hrank.p, row_base, row_of.p, col.p,
+                       val.p);
+    AFEM_LAUNCHED();
+  }
+  ctx.sync();
+  return cnnz;
+}
+
+// C's CSR from its COO (rows sorted): C.own_rp / own_ci / own_v
+void coo_to_level(Ctx& ctx, int64_t n_rows, int64_t cnnz, DevBuf<int64_t>& row_of, DevBuf<int32_t>& col,
+                  DevBuf<double>& val, AmgLevel& C)
+{
+  C.own_rp.alloc(n_rows + 1);
+  AFEM_HIP(hipMemsetAsync(C.own_rp.p, 0, (n_rows + 1) * sizeof(int64_t), ctx.stream));
   if (cnnz > 0) {
-    hipLaunchKernelGGL(k_amg_rowptr, dim3(grid_for(cnnz, 256)), dim3(256), 0, ctx.stream, cnnz, row_of.p, nc,
+    hipLaunchKernelGGL(k_amg_rowptr, dim3(grid_for(cnnz, 256)), dim3(256), 0, ctx.stream, cnnz, row_of.p, n_rows,
                        C.own_rp.p);
     AFEM_LAUNCHED();
   }
   ctx.sync();
-  C.n = nc;
+  C.own_ci = std::move(col);
+  C.own_v = std::move(val);
+  C.n = n_rows;
   C.nnz = cnnz;
   C.rp = C.own_rp.p;
   C.ci = C.own_ci.p;
   C.v = C.own_v.p;
+}
+
+// C = P^T A P of level L's aggregates on one rank (or a replicated level)
+void galerkin(Ctx& ctx, AmgLevel& L, int64_t nc, AmgLevel& C)
+{
+  DevBuf<int64_t> row_of;
+  DevBuf<int32_t> col;
+  DevBuf<double> val;
+  const int64_t cnnz = galerkin_coo(ctx, L, L.agg.p, L.n, 0, row_of, col, val);
+  coo_to_level(ctx, nc, cnnz, row_of, col, val, C);
+  C.ncol = nc;
+}
+
+// the host copy of a device int array
+std::vector<int32_t> to_host_i32(Ctx& ctx, const int32_t* d, int64_t n)
+{
+  std::vector<int32_t> h(n);
+  if (n) AFEM_HIP(hipMemcpyAsync(h.data(), d, n * sizeof(int32_t), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  return h;
+}
+
+// Level L (distributed) and its aggregates: for every ghost column, its
+// owner's aggregate (the aggregate ids exchanged through L's halo as doubles)
+// and its owner rank (the neighbour whose receive list holds it)
+void ghost_aggregates(Ctx& ctx, AmgLevel& L, std::vector<int32_t>& gagg, std::vector<int32_t>& gown)
+{
+  const int64_t ng = L.ncol - L.n;
+  DevBuf<double> gv;
+  gv.alloc(L.ncol > 0 ? L.ncol : 1);
+  AFEM_HIP(hipMemsetAsync(gv.p, 0, gv.bytes(), ctx.stream));
+  if (L.n > 0) {
+    hipLaunchKernelGGL(k_amg_i2d, dim3(grid_for(L.n, 256)), dim3(256), 0, ctx.stream, L.n, (const int32_t*)L.agg.p,
+                       gv.p);
+    AFEM_LAUNCHED();
+  }
+  halo_exchange(*L.H, ctx, gv.p);
+  std::vector<double> h(ng);
+  if (ng) AFEM_HIP(hipMemcpyAsync(h.data(), gv.p + L.n, ng * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  gagg.assign(ng, -1);
+  gown.assign(ng, -1);
+  const Halo& H = *L.H;
+  const std::vector<int32_t> rids = to_host_i32(ctx, H.recv_ids.p, H.n_recv);
+  for (size_t q = 0; q < H.nbr.size(); ++q)
+    for (int64_t k = H.recv_off[q]; k < H.recv_off[q + 1]; ++k) {
+      const int64_t j = rids[k] - L.n;
+      AFEM_REQUIRE(j >= 0 && j < ng, AFEM_ERR_STATE, "amg: a halo receive id outside the ghost columns");
+      gown[j] = H.nbr[q];
+      gagg[j] = (int32_t)h[j];
+    }
+}
+
+// the distributed coarse level of L: this rank's aggregates are its rows, the
+// aggregates of its ghosts its ghost columns (numbered neighbour by neighbour,
+// each neighbour's in increasing aggregate id), and the coarse halo follows
+// from L's: the aggregates of the rows L sends to rank s are what s receives
+// from this rank, in the same (increasing id) order on both sides
+void build_dist_coarse(Ctx& ctx, Amg& a, AmgLevel& L, int64_t nc, AmgLevel& C)
+{
+  std::vector<int32_t> gagg, gown;
+  ghost_aggregates(ctx, L, gagg, gown);
+  const Halo& H = *L.H;
+  const std::vector<int32_t> agg = to_host_i32(ctx, L.agg.p, L.n);
+  const std::vector<int32_t> sids = to_host_i32(ctx, H.send_ids.p, H.n_send);
+  const int nn = (int)H.nbr.size();
+  std::vector<int64_t> sc(nn), rc(nn);
+  std::vector<int32_t> si, ri;
+  std::vector<int32_t> cmap(L.ncol, -1);
+  for (int64_t i = 0; i < L.n; ++i) cmap[i] = agg[i];
+  int64_t next = nc;
+  for (int q = 0; q < nn; ++q) {
+    std::vector<int32_t> s;
+    for (int64_t k = H.send_off[q]; k < H.send_off[q + 1]; ++k)
+      if (agg[sids[k]] >= 0) s.push_back(agg[sids[k]]);
+    std::sort(s.begin(), s.end());
+    s.erase(std::unique(s.begin(), s.end()), s.end());
+    sc[q] = (int64_t)s.size();
+    si.insert(si.end(), s.begin(), s.end());
+    std::vector<int32_t> r;
+    for (int64_t j = 0; j < L.ncol - L.n; ++j)
+      if (gown[j] == H.nbr[q] && gagg[j] >= 0) r.push_back(gagg[j]);
+    std::sort(r.begin(), r.end());
+    r.erase(std::unique(r.begin(), r.end()), r.end());
+    rc[q] = (int64_t)r.size();
+    for (size_t t = 0; t < r.size(); ++t) ri.push_back((int32_t)(next + (int64_t)t));
+    for (int64_t j = 0; j < L.ncol - L.n; ++j)
+      if (gown[j] == H.nbr[q] && gagg[j] >= 0)
+        cmap[L.n + j] = (int32_t)(next + (std::lower_bound(r.begin(), r.end(), gagg[j]) - r.begin()));
+    next += (int64_t)r.size();
+  }
+  C.own_halo.reset(new Halo());
+  halo_setup(*C.own_halo, ctx, a.comm, nn, reinterpret_cast<const int32_t*>(H.nbr.data()), sc.data(), si.data(),
+             rc.data(), ri.data());
+  C.H = C.own_halo.get();
+  C.dist = true;
+  DevBuf<int32_t> dmap;
+  dmap.alloc(L.ncol > 0 ? L.ncol : 1);
+  if (L.ncol) AFEM_HIP(hipMemcpyAsync(dmap.p, cmap.data(), L.ncol * sizeof(int32_t), hipMemcpyHostToDevice, ctx.stream));
+  DevBuf<int64_t> row_of;
+  DevBuf<int32_t> col;
+  DevBuf<double> val;
+  const int64_t cnnz = galerkin_coo(ctx, L, dmap.p, L.ncol, 0, row_of, col, val);
+  coo_to_level(ctx, nc, cnnz, row_of, col, val, C);
+  C.ncol = next;
+}
+
+// the coarse level of L gathered on every rank: this rank's rows of P^T A P in
+// the global coarse numbering (aggregates numbered rank by rank), summed into
+// one COO over the ranks (all-reduce of zero-padded arrays: every coarse row is
+// one rank's), the same replicated CSR on every rank
+void build_gathered(Ctx& ctx, Amg& a, AmgLevel& L, int64_t nc, const std::vector<int64_t>& off, AmgLevel& C)
+{
+  const int nr = comm_nranks(a.comm), me = comm_rank(a.comm);
+  std::vector<int32_t> gagg, gown;
+  ghost_aggregates(ctx, L, gagg, gown);
+  const std::vector<int32_t> agg = to_host_i32(ctx, L.agg.p, L.n);
+  const int64_t NG = off[nr];
+  AFEM_REQUIRE(NG < (int64_t(1) << 31), AFEM_ERR_LIMIT, "amg: gathered level above 2^31 rows");
+  std::vector<int32_t> cmap(L.ncol, -1);
+  for (int64_t i = 0; i < L.n; ++i) cmap[i] = agg[i] >= 0 ? (int32_t)(off[me] + agg[i]) : -1;
+  for (int64_t j = 0; j < L.ncol - L.n; ++j)
+    if (gown[j] >= 0 && gagg[j] >= 0) cmap[L.n + j] = (int32_t)(off[gown[j]] + gagg[j]);
+  DevBuf<int32_t> dmap;
+  dmap.alloc(L.ncol > 0 ? L.ncol : 1);
+  if (L.ncol) AFEM_HIP(hipMemcpyAsync(dmap.p, cmap.data(), L.ncol * sizeof(int32_t), hipMemcpyHostToDevice, ctx.stream));
+  DevBuf<int64_t> row_of;
+  DevBuf<int32_t> col;
+  DevBuf<double> val;
+  const int64_t cnnz = galerkin_coo(ctx, L, dmap.p, L.ncol, 0, row_of, col, val);
+  // (galerkin_coo keys agg i + row_base: with row_base 0 the rows are my local
+  // aggregate ids; shifted to global ids below)
+  std::vector<double> cnt(nr, 0.0);
+  cnt[me] = (double)cnnz;
+  cnt = allsum_vec(ctx, a, cnt);
+  std::vector<int64_t> eoff(nr + 1, 0);
+  for (int r = 0; r < nr; ++r) eoff[r + 1] = eoff[r] + (int64_t)cnt[r];
+  const int64_t E = eoff[nr];
+  std::vector<int64_t> hr(cnnz);
+  std::vector<int32_t> hc(cnnz);
+  std::vector<double> hv(cnnz);
+  if (cnnz) {
+    AFEM_HIP(hipMemcpyAsync(hr.data(), row_of.p, cnnz * 8, hipMemcpyDeviceToHost, ctx.stream));
+    AFEM_HIP(hipMemcpyAsync(hc.data(), col.p, cnnz * 4, hipMemcpyDeviceToHost, ctx.stream));
+    AFEM_HIP(hipMemcpyAsync(hv.data(), val.p, cnnz * 8, hipMemcpyDeviceToHost, ctx.stream));
+  }
+  ctx.sync();
+  std::vector<double> R(E, 0.0), Cc(E, 0.0), V(E, 0.0);
+  for (int64_t k = 0; k < cnnz; ++k) {
+    R[eoff[me] + k] = (double)(off[me] + hr[k]);
+    Cc[eoff[me] + k] = (double)hc[k];
+    V[eoff[me] + k] = hv[k];
+  }
+  R = allsum_vec(ctx, a, std::move(R));
+  Cc = allsum_vec(ctx, a, std::move(Cc));
+  V = allsum_vec(ctx, a, std::move(V));
+  DevBuf<double> dr, dc;
+  dr.alloc(E > 0 ? E : 1);
+  dc.alloc(E > 0 ? E : 1);
+  row_of.alloc(E > 0 ? E : 1);
+  col.alloc(E > 0 ? E : 1);
+  val.alloc(E > 0 ? E : 1);
+  if (E) {
+    AFEM_HIP(hipMemcpyAsync(dr.p, R.data(), E * 8, hipMemcpyHostToDevice, ctx.stream));
+    AFEM_HIP(hipMemcpyAsync(dc.p, Cc.data(), E * 8, hipMemcpyHostToDevice, ctx.stream));
+    AFEM_HIP(hipMemcpyAsync(val.p, V.data(), E * 8, hipMemcpyHostToDevice, ctx.stream));
+    hipLaunchKernelGGL(k_amg_coo_unpack, dim3(grid_for(E, 256)), dim3(256), 0, ctx.stream, E, dr.p, dc.p, row_of.p,
+                       col.p);
+    AFEM_LAUNCHED();
+  }
+  coo_to_level(ctx, NG, E, row_of, col, val, C);
+  C.ncol = NG;
+  C.dist = false;
+  L.gather_off = off[me];
+  L.nc_local = nc;
 }
 
 bool dense_inverse(Ctx& ctx, Amg& a, AmgLevel& L)
@@ -784,17 +1091,21 @@ bool dense_inverse(Ctx& ctx, Amg& a, AmgLevel& L)
   return true;
 }
 
-// fine: the system whose plan runs the level's products (level 0), else null
+// fine: the system whose plan runs the level's products (level 0), else null;
+// a distributed level exchanges its iterate's ghosts before every product
 void smooth(Ctx& ctx, Amg& a, AmgLevel& L, const double* b, int sweeps, bool from_zero, LinearSystem* fine)
 {
-  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, std::max<int64_t>(1, (L.n + 255) / 256));
   int s = 0;
   if (from_zero) {
-    hipLaunchKernelGGL(k_amg_scale, dim3(g), dim3(256), 0, ctx.stream, L.n, L.omega, L.dinv.p, b, L.x.p);
-    AFEM_LAUNCHED();
+    if (L.n > 0) {
+      hipLaunchKernelGGL(k_amg_scale, dim3(g), dim3(256), 0, ctx.stream, L.n, L.omega, L.dinv.p, b, L.x.p);
+      AFEM_LAUNCHED();
+    }
     s = 1;
   }
   for (; s < sweeps; ++s) {
+    halo(ctx, L, L.x.p);
     if (fine) {
       ls_spmv_planned(*fine, L.x.p, L.t.p);
       hipLaunchKernelGGL(k_amg_jacobi, dim3(g), dim3(256), 0, ctx.stream, L.n, L.omega, L.dinv.p, b, L.t.p, L.x.p);
@@ -814,7 +1125,7 @@ void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
   AmgLevel& L = a.lv[l];
   if (l > 0) fine = nullptr;
   if (l + 1 == a.lv.size()) {
-    if (a.n_dense == L.n && L.n > 0) {
+    if (a.n_dense == L.n && L.n > 0 && !L.dist) {
       hipLaunchKernelGGL(k_amg_gemv, dim3((unsigned)L.n), dim3(64), 0, ctx.stream, (int)L.n, a.ainv.p, b, L.x.p);
       AFEM_LAUNCHED();
     }
@@ -825,6 +1136,7 @@ void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
   }
   AmgLevel& C = a.lv[l + 1];
   smooth(ctx, a, L, b, a.sweeps, true, fine);
+  halo(ctx, L, L.x.p);
   if (fine) {
     ls_spmv_planned(*fine, L.x.p, L.t.p);
     const unsigned gv = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
@@ -834,47 +1146,78 @@ void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
   else {
     spmv(ctx, 2, L, L.x.p, L.r.p, b, 0.0);
   }
-  hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(C.n, 256)), dim3(256), 0, ctx.stream, C.n, L.ap.p, L.mem.p, L.r.p,
-                     C.b.p);
-  AFEM_LAUNCHED();
+  // restriction: into the coarse level's own rows, or (gathered) into this
+  // rank's rows of the replicated coarse vector, summed over the ranks
+  const bool gathered = L.gather_off >= 0;
+  const int64_t nloc = gathered ? L.nc_local : C.n;
+  double* cb = C.b.p + (gathered ? L.gather_off : 0);
+  if (gathered) AFEM_HIP(hipMemsetAsync(C.b.p, 0, C.n * sizeof(double), ctx.stream));
+  if (nloc > 0) {
+    hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(nloc, 256)), dim3(256), 0, ctx.stream, nloc, L.ap.p, L.mem.p,
+                       L.r.p, cb);
+    AFEM_LAUNCHED();
+  }
+  if (gathered) comm_allreduce(a.comm, ctx, C.b.p, C.n);
   const bool kc = C.kcoef.p != nullptr;
   if (kc)
     kcycle(ctx, a, l + 1);
   else
     vcycle(ctx, a, l + 1, C.b.p, nullptr);
-  const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
-  // (the K-cycle's Krylov weights are the coarse correction's scale)
-  hipLaunchKernelGGL(k_amg_prolong, dim3(g), dim3(256), 0, ctx.stream, L.n, L.agg.p, kc ? 1.0 : a.scale, C.x.p,
-                     L.x.p);
-  AFEM_LAUNCHED();
+  if (L.n > 0) {
+    const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
+    // (the K-cycle's Krylov weights are the coarse correction's scale)
+    hipLaunchKernelGGL(k_amg_prolong, dim3(g), dim3(256), 0, ctx.stream, L.n, L.agg.p, kc ? 1.0 : a.scale,
+                       (const double*)(C.x.p + (gathered ? L.gather_off : 0)), L.x.p);
+    AFEM_LAUNCHED();
+  }
   smooth(ctx, a, L, b, a.sweeps, false, fine);
 }
 
 // level l's coarse problem A x = b (b in L.b): c1 = B b, v1 = A c1, rt = b -
 // alpha1 v1, c2 = B rt, v2 = A c2, x = w1 c1 + w2 c2 (B: the cycle at this
-// level); every scalar stays on the device (graph-capturable, no host sync)
+// level); one rank: every scalar stays on the device (graph-capturable, no host
+// sync); a distributed level all-reduces the step's dot products
 void kcycle(Ctx& ctx, Amg& a, size_t l)
 {
   AmgLevel& L = a.lv[l];
   const int64_t n = L.n;
-  const unsigned g = (unsigned)std::min<int64_t>(kVec, (n + 255) / 256);
-  const unsigned gd = (unsigned)std::min<int64_t>(kDotGrid, (n + 255) / 256);
+  const unsigned g = (unsigned)std::min<int64_t>(kVec, std::max<int64_t>(1, (n + 255) / 256));
+  const unsigned gd = (unsigned)std::min<int64_t>(kDotGrid, std::max<int64_t>(1, (n + 255) / 256));
+  auto coef = [&](auto step) {
+    constexpr int STEP = decltype(step)::value;
+    constexpr int ND = STEP == 1 ? 2 : 3;
+    if (!L.dist) {
+      hipLaunchKernelGGL(k_kc_coef<STEP>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)a.partial.p,
+                         L.kcoef.p);
+    }
+    else {
+      hipLaunchKernelGGL(k_kc_sum<ND>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)a.partial.p,
+                         a.sums.p);
+      comm_allreduce(a.comm, ctx, a.sums.p, ND);
+      hipLaunchKernelGGL(k_kc_coef_sums<STEP>, dim3(1), dim3(64), 0, ctx.stream, (const double*)a.sums.p, L.kcoef.p);
+    }
+    AFEM_LAUNCHED();
+  };
   vcycle(ctx, a, l, L.b.p, nullptr);
   AFEM_HIP(hipMemcpyAsync(L.kc1.p, L.x.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
+  halo(ctx, L, L.kc1.p);
   spmv(ctx, 0, L, L.kc1.p, L.kv1.p, nullptr, 0.0);
   hipLaunchKernelGGL(k_kc_dots<2>, dim3(gd), dim3(256), 0, ctx.stream, n, (const double*)L.kc1.p,
                      (const double*)L.kv1.p, (const double*)L.kc1.p, (const double*)L.b.p, (const double*)nullptr,
                      (const double*)nullptr, a.partial.p);
-  hipLaunchKernelGGL(k_kc_coef<1>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)a.partial.p, L.kcoef.p);
+  AFEM_LAUNCHED();
+  coef(std::integral_constant<int, 1>());
   hipLaunchKernelGGL(k_kc_resid, dim3(g), dim3(256), 0, ctx.stream, n, (const double*)L.kcoef.p, (const double*)L.b.p,
                      (const double*)L.kv1.p, L.krt.p);
   AFEM_LAUNCHED();
   vcycle(ctx, a, l, L.krt.p, nullptr);
+  halo(ctx, L, L.x.p);
   spmv(ctx, 0, L, L.x.p, L.t.p, nullptr, 0.0);
   hipLaunchKernelGGL(k_kc_dots<3>, dim3(gd), dim3(256), 0, ctx.stream, n, (const double*)L.x.p, (const double*)L.kv1.p,
                      (const double*)L.x.p, (const double*)L.t.p, (const double*)L.x.p, (const double*)L.krt.p,
                      a.partial.p);
-  hipLaunchKernelGGL(k_kc_coef<2>, dim3(1), dim3(256), 0, ctx.stream, (int)gd, (const double*)a.partial.p, L.kcoef.p);
+  AFEM_LAUNCHED();
+  coef(std::integral_constant<int, 2>());
   hipLaunchKernelGGL(k_kc_comb, dim3(g), dim3(256), 0, ctx.stream, n, (const double*)L.kcoef.p,
                      (const double*)L.kc1.p, L.x.p);
   AFEM_LAUNCHED();
@@ -885,7 +1228,7 @@ void kcycle(Ctx& ctx, Amg& a, size_t l)
 bool amg_setup(LinearSystem& ls)
 {
   Ctx& ctx = *ls.ctx;
-  AFEM_REQUIRE(amg_available(ls), AFEM_ERR_STATE, "amg: needs a CSR system on one rank");
+  AFEM_REQUIRE(amg_available(ls), AFEM_ERR_STATE, "amg: needs a CSR system (below 2^31 rows and non-zeros)");
   // amg-reuse: the same CSR arrays at the same sizes (every entry point that
   // installs or rebuilds a matrix also drops ls.amg, capi.cpp / elastodynamics.cpp)
   if (ls.opts.amg == 2 && ls.amg && ls.amg->key_rows == ls.csr_rows && ls.amg->key_cols == ls.csr_cols &&
@@ -893,10 +1236,13 @@ bool amg_setup(LinearSystem& ls)
     return false;
   auto a = std::unique_ptr<Amg, AmgDeleter>(new Amg());
   a->partial.alloc(kVec);
+  a->sums.alloc(8);
+  const bool dist = multi_rank(ls);
+  a->comm = dist ? ls.halo->comm : nullptr;
   a->sweeps = (int)std::max(1.0, env_double("AFEM_AMG_SWEEPS", 1.0));
   a->scale = env_double("AFEM_AMG_SCALE", 1.7);
   a->fine_planned = env_double("AFEM_AMG_FINE_CSR", 0.0) == 0.0;
-  a->use_graph = env_double("AFEM_AMG_GRAPH", 0.0) != 0.0;
+  a->use_graph = !dist && env_double("AFEM_AMG_GRAPH", 0.0) != 0.0;
   const double theta = env_double("AFEM_AMG_THETA", 0.08);
   // aggregation distance: level 0 / the coarse levels (distance 1 stalls on the
   // coarse Galerkin graphs: their degree falls with the level, r05w; distance 2
@@ -905,30 +1251,56 @@ bool amg_setup(LinearSystem& ls)
   const int hops0 = (int)std::min(2.0, std::max(1.0, env_double("AFEM_AMG_HOPS0", 2.0)));
   const int hops = (int)std::min(2.0, std::max(1.0, env_double("AFEM_AMG_HOPS", 2.0)));
   const int64_t dense = (int64_t)std::min(4096.0, std::max(1.0, env_double("AFEM_AMG_DENSE", kDense)));
+  // several ranks: distributed levels while the global coarse size exceeds
+  // AFEM_AMG_GATHER rows, then one level gathered on every rank (its hierarchy
+  // below is the one-rank one, built identically on every rank)
+  const int64_t gather_rows = (int64_t)std::max(1.0, env_double("AFEM_AMG_GATHER", 65536.0));
   {
     AmgLevel L;
     L.n = ls.n_rows;
+    L.ncol = dist ? ls.n_cols : ls.n_rows;
     L.nnz = ls.csr_nnz;
     L.rp = ls.csr_rows;
     L.ci = ls.csr_cols;
     L.v = ls.csr_vals;
+    L.dist = dist;
+    L.H = dist ? ls.halo.get() : nullptr;
     level_prepare(ctx, L, ls.cons.p);
     a->lv.push_back(std::move(L));
   }
   const bool verbose = env_double("AFEM_AMG_VERBOSE", 0.0) > 0;
-  while ((int)a->lv.size() < kMaxLevels && a->lv.back().n > dense) {
+  while ((int)a->lv.size() < kMaxLevels) {
     AmgLevel& L = a->lv.back();
+    const int64_t n_glob = L.dist ? (int64_t)allsum(ctx, *a, (double)L.n) : L.n;
+    if (n_glob <= dense) break;
     const int64_t nc = aggregate(ctx, L, theta, a->lv.size() == 1 ? hops0 : hops);
-    if (verbose) std::fprintf(stderr, "amg level %zu: %lld rows, %lld non-zeros -> %lld aggregates\n", a->lv.size() - 1,
-                              (long long)L.n, (long long)L.nnz, (long long)nc);
-    if (nc == 0 || nc * 10 > L.n * 9) {  // no coarse level, or coarsening stalls
+    const int64_t nc_glob = L.dist ? (int64_t)allsum(ctx, *a, (double)nc) : nc;
+    if (verbose)
+      std::fprintf(stderr, "amg level %zu%s: %lld rows, %lld non-zeros -> %lld aggregates (global %lld -> %lld)\n",
+                   a->lv.size() - 1, L.dist ? " (distributed)" : "", (long long)L.n, (long long)L.nnz, (long long)nc,
+                   (long long)n_glob, (long long)nc_glob);
+    if (nc_glob == 0 || nc_glob * 10 > n_glob * 9) {  // no coarse level, or coarsening stalls (every rank agrees)
       L.agg.reset();
       L.ap.reset();
       L.mem.reset();
       break;
     }
     AmgLevel C;
-    galerkin(ctx, L, nc, C);
+    if (!L.dist) {
+      galerkin(ctx, L, nc, C);
+    }
+    else if (nc_glob <= gather_rows) {
+      const int nr = comm_nranks(a->comm);
+      std::vector<double> cnt(nr, 0.0);
+      cnt[comm_rank(a->comm)] = (double)nc;
+      cnt = allsum_vec(ctx, *a, cnt);
+      std::vector<int64_t> off(nr + 1, 0);
+      for (int r = 0; r < nr; ++r) off[r + 1] = off[r] + (int64_t)cnt[r];
+      build_gathered(ctx, *a, L, nc, off, C);
+    }
+    else {
+      build_dist_coarse(ctx, *a, L, nc, C);
+    }
     level_prepare(ctx, C, nullptr);
     a->lv.push_back(std::move(C));
   }
@@ -940,18 +1312,20 @@ bool amg_setup(LinearSystem& ls)
   }
   AmgLevel& last = a->lv.back();
   // the coarsest level inverted densely when small (a small system: the
-  // whole matrix, the PCG then converges in one or two iterations)
-  if (last.n <= dense) dense_inverse(ctx, *a, last);
+  // whole matrix, the PCG then converges in one or two iterations); a
+  // distributed coarsest level (no gathered one below) is smoothed
+  if (!last.dist && last.n <= dense) dense_inverse(ctx, *a, last);
   // K-cycle on levels 1 and 2 (the unstructured leg's 11.5 M rows, r05ay: 108 -> 72
   // iterations, 0.453 -> 0.389 s with setup; every level: 66, 0.407 s -- the small
   // levels' launches, visited 2^l times, cost more than the iterations they save)
   a->kcycle = (int)std::max(0.0, env_double("AFEM_AMG_KCYCLE", 2.0));
   for (size_t l = 1; l < a->lv.size() && (int)l <= a->kcycle; ++l) {
     AmgLevel& L = a->lv[l];
-    if (l + 1 == a->lv.size() && a->n_dense == L.n) break;  // the dense coarsest level: solved exactly
-    L.kc1.alloc(L.n);
-    L.kv1.alloc(L.n);
-    L.krt.alloc(L.n);
+    if (l + 1 == a->lv.size() && a->n_dense == L.n && !L.dist) break;  // the dense coarsest level: solved exactly
+    L.kc1.alloc(L.ncol > 0 ? L.ncol : 1);
+    AFEM_HIP(hipMemsetAsync(L.kc1.p, 0, L.kc1.bytes(), ctx.stream));
+    L.kv1.alloc(L.n > 0 ? L.n : 1);
+    L.krt.alloc(L.n > 0 ? L.n : 1);
     L.kcoef.alloc(8);
   }
   a->key_rows = ls.csr_rows;

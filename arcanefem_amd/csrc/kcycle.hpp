@@ -73,6 +73,42 @@ __global__ __launch_bounds__(256) void k_kc_coef(int nb, const double* __restric
   }
 }
 
+// several ranks: the partials summed into ND device scalars (one block, fixed
+// order), all-reduced by the caller, then the coefficients from the sums
+template <int ND>
+__global__ __launch_bounds__(256) void k_kc_sum(int nb, const double* __restrict__ partial, double* __restrict__ sums)
+{
+  __shared__ double sh[ND][256];
+  for (int d = 0; d < ND; ++d) sh[d][threadIdx.x] = (int)threadIdx.x < nb ? partial[ND * threadIdx.x + d] : 0.0;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int d = 0; d < ND; ++d) sh[d][threadIdx.x] += sh[d][threadIdx.x + o];
+    __syncthreads();
+  }
+  if ((int)threadIdx.x < ND) sums[threadIdx.x] = sh[threadIdx.x][0];
+}
+
+// k_kc_coef's arithmetic on the (all-reduced) sums
+template <int STEP>
+__global__ void k_kc_coef_sums(const double* __restrict__ sums, double* __restrict__ coef)
+{
+  if (threadIdx.x != 0) return;
+  if (STEP == 1) {
+    const double rho = sums[0];
+    coef[0] = rho;
+    coef[1] = rho > 0.0 ? sums[1] / rho : 0.0;
+  }
+  else {
+    const double rho = coef[0], a1 = coef[1];
+    const double gam = sums[0], bet = sums[1], del = sums[2];
+    const double den = rho > 0.0 ? bet - gam * gam / rho : bet;
+    const double a2 = den > 0.0 ? del / den : 0.0;
+    coef[2] = rho > 0.0 ? a1 - gam * a2 / rho : a1;
+    coef[3] = a2;
+  }
+}
+
 // rt = b - alpha1 v1
 __global__ void k_kc_resid(int64_t n, const double* __restrict__ coef, const double* __restrict__ b,
                              const double* __restrict__ v1, double* __restrict__ rt)

@@ -132,6 +132,57 @@ def main():
         st = ls.solve()
         res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
                    converged=int(st["converged"]), rel=st["rel_residual"], synced=synced, spmv=st["spmv_kernel"])
+    elif case.startswith("amg:"):
+        # the algebraic multigrid PCG over RCB subdomains (amg.hip: per-rank
+        # aggregation, distributed coarse levels, then one gathered level):
+        # "amg:<golden case>" (coarsest level held to 16 rows, as the one-rank
+        # AMG tests do) or "amg:refined<k>" (L-shape-3D refined k times, z-min
+        # nodes clamped by penalty)
+        from golden_cases import CASES
+        from arcanefem_amd.gmsh import read_gmsh
+
+        name = case[4:]
+        if name.endswith("_dist"):
+            # distributed coarse levels (per-rank aggregation of a distributed
+            # operator, coarse ghosts and halo) down to 200 global rows, then the gather
+            af.set_variant("AFEM_AMG_GATHER", "200")
+            name = name[:-len("_dist")]
+        if name.startswith("refined"):
+            import bench
+
+            gm = read_gmsh(os.path.join(ROOT, "tests", "golden", "L-shape-3D.msh"))
+            cells, coords = bench.refine_tets(gm.cells, gm.coords, int(name[7:]), "cpu")
+            dim, f, P = 3, 5.5, 1e30
+            z = coords[:, 2]
+            bcs = [(np.nonzero(z <= z.min() + 1e-9)[0], 0.5)]
+        else:
+            af.set_variant("AFEM_AMG_DENSE", "16")
+            mfile, f, bcs0, _, P = CASES[name]
+            gm = read_gmsh(os.path.join(ROOT, "tests", "golden", mfile))
+            cells, coords, dim = gm.cells, gm.coords, gm.dim
+            bcs = [(gm.group_nodes(g), v) for g, v in bcs0]
+        part = af.partition_rcb(dim, coords, world)
+        mesh = af.Mesh.subdomain(ctx, dim, cells, coords, part, world, rank)
+        _, _, l2g = mesh.download()
+        g2l = np.full(coords.shape[0], -1, dtype=np.int64)
+        g2l[l2g] = np.arange(l2g.size)
+        bsr = af.BSRFormat(mesh, 1).initialize(True)
+        bsr.computeSparsity()
+        ls = af.DoFLinearSystem().initialize(ctx, mesh.n_own_nodes, mesh.n_nodes)
+        bsr.assemblePoissonP1(1.0, f, ls.rhsVariable(), rhs_mode="set")
+        bsr.toLinearSystem(ls)
+        for nodes, v in bcs:
+            loc = g2l[nodes]
+            own = loc[(loc >= 0) & (loc < mesh.n_own_nodes)].astype(np.int32)
+            if own.size:
+                ls.applyDirichletViaPenalty(own, v, P)
+        if world > 1:
+            ls.set_halo_mesh(comm, mesh)
+        ls.setSolverOptions(rtol=1e-14, max_iter=20000, method="pcg", preconditioner="amg")
+        st = ls.solve()
+        res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
+                   converged=int(st["converged"]), rel=st["rel_residual"], levels=st["amg_levels"],
+                   coarse=st["amg_coarse_rows"])
     elif case.startswith("gmsh:"):
         # a reference Gmsh mesh partitioned by libafem's RCB into `world`
         # ghosted subdomains (afem_mesh_create_subdomain), Poisson + penalty
