@@ -487,6 +487,10 @@ struct AmgLevel {
   // the next level replicated on every rank (gathered): this rank's
   // aggregates are its rows [gather_off, gather_off + nc_local)
   int64_t gather_off = -1, nc_local = 0;
+  // a distributed level small enough to be solved whole: gathered as it is
+  // (identity aggregates) onto the next level, its cycle = gather b, solve
+  // there, take back this rank's part (no smoothing here)
+  bool pass = false;
   const int64_t* rp = nullptr;
   const int32_t* ci = nullptr;
   const double* v = nullptr;
@@ -1037,6 +1041,34 @@ void build_gathered(Ctx& ctx, Amg& a, AmgLevel& L, int64_t nc, const std::vector
   L.nc_local = nc;
 }
 
+// the identity aggregation of a distributed level (every row its own
+// aggregate) and the level gathered whole onto C (build_gathered)
+void build_passthrough(Ctx& ctx, Amg& a, AmgLevel& L, AmgLevel& C)
+{
+  const int64_t n = L.n;
+  L.agg.alloc(n > 0 ? n : 1);
+  L.mem.alloc(n > 0 ? n : 1);
+  L.ap.alloc(n + 1);
+  std::vector<int32_t> id(n);
+  std::vector<int64_t> ap(n + 1);
+  for (int64_t i = 0; i < n; ++i) id[i] = (int32_t)i;
+  for (int64_t i = 0; i <= n; ++i) ap[i] = i;
+  if (n) {
+    AFEM_HIP(hipMemcpyAsync(L.agg.p, id.data(), n * 4, hipMemcpyHostToDevice, ctx.stream));
+    AFEM_HIP(hipMemcpyAsync(L.mem.p, id.data(), n * 4, hipMemcpyHostToDevice, ctx.stream));
+  }
+  AFEM_HIP(hipMemcpyAsync(L.ap.p, ap.data(), (n + 1) * 8, hipMemcpyHostToDevice, ctx.stream));
+  ctx.sync();
+  const int nr = comm_nranks(a.comm);
+  std::vector<double> cnt(nr, 0.0);
+  cnt[comm_rank(a.comm)] = (double)n;
+  cnt = allsum_vec(ctx, a, cnt);
+  std::vector<int64_t> off(nr + 1, 0);
+  for (int r = 0; r < nr; ++r) off[r + 1] = off[r] + (int64_t)cnt[r];
+  build_gathered(ctx, a, L, n, off, C);
+  L.pass = true;
+}
+
 bool dense_inverse(Ctx& ctx, Amg& a, AmgLevel& L)
 {
   const int m = (int)L.n;
@@ -1135,6 +1167,19 @@ void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
     return;
   }
   AmgLevel& C = a.lv[l + 1];
+  if (L.pass) {  // gathered whole: C's solution, this rank's part
+    AFEM_HIP(hipMemsetAsync(C.b.p, 0, C.n * sizeof(double), ctx.stream));
+    if (L.n > 0)
+      AFEM_HIP(hipMemcpyAsync(C.b.p + L.gather_off, b, L.n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
+    comm_allreduce(a.comm, ctx, C.b.p, C.n);
+    if (C.kcoef.p)
+      kcycle(ctx, a, l + 1);
+    else
+      vcycle(ctx, a, l + 1, C.b.p, nullptr);
+    if (L.n > 0)
+      AFEM_HIP(hipMemcpyAsync(L.x.p, C.x.p + L.gather_off, L.n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
+    return;
+  }
   smooth(ctx, a, L, b, a.sweeps, true, fine);
   halo(ctx, L, L.x.p);
   if (fine) {
@@ -1254,7 +1299,9 @@ bool amg_setup(LinearSystem& ls)
   // several ranks: distributed levels while the global coarse size exceeds
   // AFEM_AMG_GATHER rows, then one level gathered on every rank (its hierarchy
   // below is the one-rank one, built identically on every rank)
-  const int64_t gather_rows = (int64_t)std::max(1.0, env_double("AFEM_AMG_GATHER", 65536.0));
+  // (at least the dense size: a distributed level never ends the hierarchy
+  // below it unless coarsening stalls)
+  const int64_t gather_rows = std::max<int64_t>(dense, (int64_t)std::max(1.0, env_double("AFEM_AMG_GATHER", 65536.0)));
   {
     AmgLevel L;
     L.n = ls.n_rows;
@@ -1272,7 +1319,17 @@ bool amg_setup(LinearSystem& ls)
   while ((int)a->lv.size() < kMaxLevels) {
     AmgLevel& L = a->lv.back();
     const int64_t n_glob = L.dist ? (int64_t)allsum(ctx, *a, (double)L.n) : L.n;
-    if (n_glob <= dense) break;
+    auto pass = [&]() {  // a small distributed level: gathered whole, solved below
+      AmgLevel C;
+      build_passthrough(ctx, *a, L, C);
+      level_prepare(ctx, C, nullptr);
+      a->lv.push_back(std::move(C));
+    };
+    if (n_glob <= dense) {
+      if (!L.dist) break;
+      pass();
+      continue;
+    }
     const int64_t nc = aggregate(ctx, L, theta, a->lv.size() == 1 ? hops0 : hops);
     const int64_t nc_glob = L.dist ? (int64_t)allsum(ctx, *a, (double)nc) : nc;
     if (verbose)
@@ -1283,6 +1340,10 @@ bool amg_setup(LinearSystem& ls)
       L.agg.reset();
       L.ap.reset();
       L.mem.reset();
+      if (L.dist && n_glob <= gather_rows) {  // gathered whole: its one-rank hierarchy below
+        pass();
+        continue;
+      }
       break;
     }
     AmgLevel C;
