@@ -402,6 +402,7 @@ void halo_begin(Halo& h, Ctx& ctx, double* x);
 void halo_end(Halo& h, Ctx& ctx, double* x);
 void comm_allreduce(Comm* c, Ctx& ctx, double* d, int64_t n);
 bool comm_is_host(Comm* c);  // host-transport communicator
+bool comm_self_loop();  // AFEM_COMM_SELF=1: one-rank collectives run anyway (comm.hip)
 void comm_set_host_async(Comm* c, bool on);  // host transport: exchange on a worker thread (halo_begin/end)
 
 // ------------------------------------------------------------------ linear system

@@ -544,7 +544,10 @@ struct Amg {
 void AmgDeleter::operator()(Amg* a) const { delete a; }
 
 namespace {
-bool multi_rank(const LinearSystem& ls) { return ls.halo && ls.halo->comm && comm_nranks(ls.halo->comm) > 1; }
+bool multi_rank(const LinearSystem& ls)
+{
+  return ls.halo && ls.halo->comm && (comm_nranks(ls.halo->comm) > 1 || comm_self_loop());
+}
 }  // namespace
 
 bool amg_available(const LinearSystem& ls)

@@ -1524,8 +1524,8 @@ int afem_ls_set_halo(afem_ls* ls, afem_comm* comm, int n_nbr, const int32_t* nbr
   AFEM_REQUIRE(n_nbr >= 0, AFEM_ERR_ARG, "negative neighbour count");
   int64_t ns = 0, nr = 0;
   for (int i = 0; i < n_nbr; ++i) {
-    AFEM_REQUIRE(nbr[i] >= 0 && nbr[i] < comm_nranks(comm->c) && nbr[i] != comm_rank(comm->c), AFEM_ERR_ARG,
-                 "bad neighbour rank");
+    AFEM_REQUIRE(nbr[i] >= 0 && nbr[i] < comm_nranks(comm->c) && (nbr[i] != comm_rank(comm->c) || comm_self_loop()),
+                 AFEM_ERR_ARG, "bad neighbour rank");
     ns += send_counts[i];
     nr += recv_counts[i];
   }

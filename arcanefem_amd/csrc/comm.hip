@@ -7,6 +7,7 @@
 // Hypre (femutils/HypreDoFLinearSystem.cc:731-742).
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -105,9 +106,25 @@ void comm_destroy(Comm* c)
   delete c;
 }
 
+// AFEM_COMM_SELF=1 (diagnostic): a one-rank communicator runs its collectives
+// anyway -- ncclAllReduce over one rank, the halo's ncclSend / ncclRecv to
+// itself in one group -- so the RCCL data path (groups, the halo stream and
+// its events, the PCG's split exchange) runs on a one-GPU box; a halo may then
+// name the own rank as its neighbour (tests/test_gpu_parity.py
+// test_rccl_self_loop_*)
+bool comm_self_loop()
+{
+  const char* v = variant("AFEM_COMM_SELF");
+  return v && std::atoi(v) == 1;
+}
+
+namespace {
+bool trivial(const Comm* c) { return !c || (c->nranks == 1 && !comm_self_loop()); }
+}  // namespace
+
 void comm_allreduce(Comm* c, Ctx& ctx, double* d, int64_t n)
 {
-  if (!c || c->nranks == 1 || n <= 0) return;
+  if (trivial(c) || n <= 0) return;
   if (c->host) {
     double* h = c->stage((size_t)n);
     AFEM_HIP(hipMemcpyAsync(h, d, n * sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
@@ -239,7 +256,7 @@ void host_end_async(Halo& h, Ctx& ctx, double* x)
 
 void halo_begin(Halo& h, Ctx& ctx, double* x)
 {
-  if (!h.comm || h.comm->nranks == 1 || h.nbr.empty()) return;
+  if (trivial(h.comm) || h.nbr.empty()) return;
   if (h.comm->host) {
     if (h.comm->host_async)
       host_begin_async(h, ctx, x);
@@ -265,7 +282,7 @@ void halo_begin(Halo& h, Ctx& ctx, double* x)
 
 void halo_end(Halo& h, Ctx& ctx, double* x)
 {
-  if (!h.comm || h.comm->nranks == 1 || h.nbr.empty()) return;
+  if (trivial(h.comm) || h.nbr.empty()) return;
   if (h.comm->host) {
     host_end_async(h, ctx, x);  // no-op unless halo_begin started a worker
     return;
@@ -280,7 +297,7 @@ void halo_end(Halo& h, Ctx& ctx, double* x)
 
 void halo_exchange(Halo& h, Ctx& ctx, double* x)
 {
-  if (!h.comm || h.comm->nranks == 1 || h.nbr.empty()) return;
+  if (trivial(h.comm) || h.nbr.empty()) return;
   if (h.n_send) {
     hipLaunchKernelGGL(k_gather, dim3(grid_for(h.n_send, 256)), dim3(256), 0, ctx.stream, h.n_send, h.send_ids.p, x,
                        h.send_buf.p);

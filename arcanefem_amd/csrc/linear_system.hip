@@ -1910,7 +1910,7 @@ void ls_solve(LinearSystem& ls, afem_solve_stats* st)
   require_csr(ls);
   AFEM_REQUIRE(ls.csr_n == ls.n_rows, AFEM_ERR_ARG, "CSR view row count differs from the linear system size");
   ls_apply_bcs(ls);
-  const bool multi = ls.halo && ls.halo->comm && comm_nranks(ls.halo->comm) > 1;
+  const bool multi = ls.halo && ls.halo->comm && (comm_nranks(ls.halo->comm) > 1 || comm_self_loop());
   int method = ls.opts.method;
   if (method == AFEM_SOLVER_AUTO)  // femutils/DoFLinearSystem.cc:127-136: direct below 500 rows
     method = (!multi && ls.n_rows < 500 && ls.opts.fixed_iterations <= 0) ? AFEM_SOLVER_DIRECT : AFEM_SOLVER_PCG;

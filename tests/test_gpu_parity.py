@@ -1088,3 +1088,65 @@ def test_cg_graph_replay_bitwise(ctx, variant, mode):
         out.append((st["iterations"], ls.solution_host()))
     assert out[0][0] == out[1][0]
     assert np.array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("pc", ["jacobi", "amg"])
+def test_rccl_self_loop_solve(ctx, variant, pc):
+    """The RCCL data path on ONE GPU (AFEM_COMM_SELF=1: a one-rank communicator
+    runs its collectives, a halo may name the own rank): the sphere's Poisson
+    system with 40 owned DoFs also addressed as ghost columns (half of their
+    couplings in the CSR go to the ghost alias, whose value the halo's
+    ncclSend / ncclRecv to self fills), solved by the distributed PCG -- the
+    split SpMV with the exchange on the halo stream, ncclAllReduce of the
+    scalars, and for pc = amg the distributed AMG (aggregation ghost-blind,
+    coarse ghost columns and halo, the gathered level) -- equals the plain
+    system's solution.  What the driver's 8-GPU run executes, minus the
+    second device."""
+    variant("AFEM_COMM_SELF", "1")
+    if pc == "amg":
+        variant("AFEM_AMG_DENSE", "16")
+    gm = read_gmsh(path("sphere_cut.msh"))
+    n = gm.n_nodes
+    rp, cols = O.sparsity(n, n, gm.cells)
+    vals, rhs = O.assemble_poisson(n, gm.cells, gm.coords, rp, cols, 5.5)
+    dn = gm.group_nodes("horizontal")
+    O.dirichlet_penalty(dn, 0.5, 1e30, rp, cols, vals, rhs)
+    rng = np.random.default_rng(40)
+    S = np.sort(rng.choice(n, 40, replace=False)).astype(np.int32)
+    alias = {int(s): n + k for k, s in enumerate(S)}
+    gcols = cols.copy()
+    gvals = vals.copy()
+    for i in range(n):
+        seg = slice(rp[i], rp[i + 1])
+        c = np.array([alias[int(x)] if (int(x) in alias and int(x) != i and i % 2 == 0) else int(x)
+                      for x in cols[seg]], dtype=np.int32)
+        o = np.argsort(c, kind="stable")
+        gcols[seg] = c[o]
+        gvals[seg] = vals[seg][o]
+    assert (gcols >= n).sum() > 40
+    uid = af.Communicator.unique_id()
+    comm = af.Communicator(ctx, 1, 0, uid)
+    try:
+        sols, its = [], []
+        for ghosts in (False, True):
+            ls = af.DoFLinearSystem().initialize(ctx, n, n + 40)
+            if ghosts:
+                ls.setCSRValues(rp[:-1].astype(np.int32), None, gcols, gvals)
+                ls.set_halo(comm, [0], [S], [np.arange(n, n + 40, dtype=np.int32)])
+            else:
+                ls.setCSRValues(rp[:-1].astype(np.int32), None, cols, vals)
+            ls.set_rhs_host(rhs)
+            ls.setSolverOptions(rtol=1e-13, max_iter=20000, method="pcg", preconditioner=pc)
+            st = ls.solve()
+            assert st["converged"], (ghosts, st)
+            sols.append(ls.solution_host().copy())
+            its.append(st["iterations"])
+            if ghosts:
+                assert st["n_allreduce"] > 0 and st["n_halo"] > 0  # the RCCL calls ran
+            ls.reset()
+        xo = np.linalg.solve(O.csr_to_dense(rp, cols, vals), rhs)
+        for x in sols:
+            assert np.abs(x - xo).max() <= 1e-10 * np.abs(xo).max()
+        print(f"\nRCCL self loop, {pc}: iterations plain / with the self halo {its}")
+    finally:
+        comm.close()

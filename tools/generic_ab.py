@@ -5,7 +5,9 @@ module's element (elements::PoissonTet4) and the lean cofactor element.
 Variant keys UN=k (k = 1..4, 6, 8) and PAD=p (-1: XOR-swizzled rows) run the kernel with k functor
 evaluations in flight per lane and LDS planes of rows + p (gx_assemble_unrolled;
 defaults: the header's, 4 and 0).
-usage: python tools/generic_ab.py n reps variant [variant ...]"""
+usage: python tools/generic_ab.py n reps variant [variant ...]
+n = "lshape<k>": the unstructured leg's mesh instead (L-shape-3D refined k times, slice-piece units;
+the functor library loaded before the refinement imports torch, bench.py c2_generic_leg)."""
 import os
 import sys
 
@@ -17,9 +19,19 @@ sys.path.insert(0, os.path.join(ROOT, "examples"))
 import arcanefem_amd as af  # noqa: E402
 import generic_example as gx  # noqa: E402
 
-n, reps = int(sys.argv[1]), int(sys.argv[2])
+reps = int(sys.argv[2])
 ctx = af.Context(0)
-mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=20250220)
+gx.load()
+if sys.argv[1].startswith("lshape"):
+    import bench
+    from arcanefem_amd.gmsh import read_gmsh
+
+    gm = read_gmsh(os.path.join(ROOT, "tests", "golden", "L-shape-3D.msh"))
+    cells, coords = bench.refine_tets(gm.cells, gm.coords, int(sys.argv[1][6:]), "cpu")
+    mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    del cells, coords
+else:
+    mesh = af.Mesh.structured(ctx, 3, int(sys.argv[1]), jitter=0.2, seed=20250220)
 ref = None
 first = None
 for spec in sys.argv[3:]:
