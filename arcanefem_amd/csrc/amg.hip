@@ -552,7 +552,9 @@ bool multi_rank(const LinearSystem& ls)
 
 bool amg_available(const LinearSystem& ls)
 {
-  if (!ls.csr_rows || !ls.csr_cols || !ls.csr_vals || ls.n_rows <= 0) return false;
+  // (several ranks: a rank without rows still takes part -- every rank must
+  // make the same choice, or the collectives of the setup and the cycle mismatch)
+  if (!ls.csr_rows || !ls.csr_cols || !ls.csr_vals || (ls.n_rows <= 0 && !multi_rank(ls))) return false;
   if (multi_rank(ls) && ls.n_cols < ls.n_rows) return false;
   // hipcub's sorts of the setup take int counts: the non-zeros of every level
   // (the fine level's are the most) must stay below 2^31, else point Jacobi

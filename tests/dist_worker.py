@@ -27,6 +27,9 @@ POISSON_MG = dict(n=8, nz=16)
 # large enough for distributed coarse levels (level 1: 9 x 9 x 17 nodes over the slabs, then the gathered box)
 POISSON_MG2 = dict(n=16, nz=32)
 DYN_MG = dict(n=8, nz=12, E=21e5, nu=0.28, rho=1.0, dt=1e-3, f=(0.0, -9.81, 1.0), steps=3)
+# BASELINE config C5 at its per-GPU size: n = 128 per rank (2.15 M nodes, the config's ~2e6 nodes per
+# GPU), 2 ranks stacked in z, the bench's material / step / clamp
+DYN_C5 = dict(n=128, nz=256, E=21e5, nu=0.28, rho=1.0, dt=1e-3, f=(0.0, 0.0, -1.0), steps=3)
 # generalized alpha with Rayleigh damping: the RHS's stiffness SpMVs exchange their operand's ghosts too
 DYN_DAMP = dict(etam=0.3, etak=1e-3, alpm=0.2, alpf=0.4, time_discretization="generalized-alpha")
 
@@ -212,6 +215,41 @@ def main():
         st = ls.solve()
         res = dict(l2g=l2g, n_own=mesh.n_own_nodes, x=ls.solution_host(with_ghosts=True), iters=st["iterations"],
                    converged=int(st["converged"]), rel=st["rel_residual"], part=part)
+    elif case == "elastodynamics_c5":
+        # C5 at its configured per-GPU size over 2 slabs (host transport), multigrid PCG; rank 0 also runs
+        # the single-domain loop of the same global mesh (decomposition invariance at size)
+        from arcanefem_amd.elastodynamics import Elastodynamics3D
+
+        p = DYN_C5
+        n, nz = p["n"], p["nz"]
+
+        def run(mesh, cm):
+            ids = np.arange(mesh.n_nodes)
+            _, _, l2g_ = mesh.download()
+            fixed = ids[l2g_ % (n + 1) == 0].astype(np.int32)  # node x-index 0, as the bench's c5 leg
+            sim = Elastodynamics3D(ctx, mesh, p["E"], p["nu"], p["rho"], p["dt"], body_force=p["f"],
+                                   fixed_nodes=fixed, rtol=1e-10, comm=cm, preconditioner="multigrid")
+            its = []
+            for _ in range(p["steps"]):
+                st = sim.step()
+                assert st["converged"], st
+                its.append(st["iterations"])
+            U = sim.state_host()[0]
+            sim.close()
+            return U, l2g_, its
+
+        mesh = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=20250220, nranks=world, rank=rank)
+        U, l2g, its = run(mesh, comm)
+        res = dict(l2g=l2g, n_own=mesh.n_own_nodes, U=U, iters=np.array(its))
+        mesh.close()
+        dist.barrier()
+        if rank == 0:
+            m1 = af.Mesh.structured(ctx, 3, n, nz=nz, jitter=0.2, seed=20250220)
+            U1, _, its1 = run(m1, None)
+            res["U_single"] = U1
+            res["iters_single"] = np.array(its1)
+            m1.close()
+        dist.barrier()
     elif case in ("elastodynamics", "elastodynamics_mg", "elastodynamics_damped"):
         from arcanefem_amd.elastodynamics import Elastodynamics3D
 
