@@ -35,8 +35,10 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 namespace afem {
 namespace {
@@ -388,6 +390,65 @@ __global__ void k_count_flags(int64_t n, const afem_functor_unit* __restrict__ u
   if (u < n && (units[u].flags & 1)) atomicAdd(out, 1ull);
 }
 
+// Unit rows of a non-lattice plan grown as clusters (round 6): in the
+// processing (Hilbert) order, every row not yet taken seeds a unit that takes
+// rows breadth first over the structure's couplings until it holds rl rows;
+// the unit's LDS rows are then a compact blob of the mesh instead of rl
+// consecutive curve positions, and fewer of its cells are shared with other
+// units (L-shape-3D refined 5x, emulated: 2.02 -> 1.80 evaluations per cell
+// against 64-node Morton pieces).  Out: the position -> row map (rl per unit,
+// -1 = idle lane) and the unit count.  AFEM_FUNCTOR_CLUSTER=0: the curve
+// pieces (k_rowmap_slices).
+std::vector<int32_t> cluster_positions(Ctx& ctx, const Structure& s, int rl, int64_t& n_units)
+{
+  const int64_t n = s.n_rows;
+  std::vector<int64_t> rp(n + 1);
+  std::vector<int32_t> perm((size_t)s.n_slices * 64);
+  AFEM_HIP(hipMemcpyAsync(rp.data(), s.row_ptr.p, (n + 1) * 8, hipMemcpyDeviceToHost, ctx.stream));
+  AFEM_HIP(hipMemcpyAsync(perm.data(), s.perm.p, perm.size() * 4, hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  std::vector<int32_t> ci(rp[n]);
+  if (rp[n]) AFEM_HIP(hipMemcpyAsync(ci.data(), s.cols.p, rp[n] * 4, hipMemcpyDeviceToHost, ctx.stream));
+  ctx.sync();
+  std::vector<int32_t> unit_of(n, -1);
+  std::vector<int32_t> pos;
+  pos.reserve((size_t)n + n / 8);
+  std::vector<int32_t> q;
+  q.reserve(rl);
+  int64_t u = 0;
+  for (int32_t seed : perm) {
+    if (seed < 0 || seed >= n || unit_of[seed] >= 0) continue;
+    q.clear();
+    q.push_back(seed);
+    unit_of[seed] = (int32_t)u;
+    for (size_t h = 0; h < q.size() && (int)q.size() < rl; ++h) {
+      const int32_t v = q[h];
+      for (int64_t k = rp[v]; k < rp[v + 1] && (int)q.size() < rl; ++k) {
+        const int32_t w = ci[k];
+        if (w < 0 || w >= n || unit_of[w] >= 0) continue;
+        unit_of[w] = (int32_t)u;
+        q.push_back(w);
+      }
+    }
+    for (int t = 0; t < rl; ++t) pos.push_back(t < (int)q.size() ? q[t] : -1);
+    ++u;
+  }
+  n_units = u;
+  return pos;
+}
+
+__global__ void k_rowmap_positions(int64_t n_pos, const int32_t* __restrict__ pos, int rl, int32_t* __restrict__ r_unit,
+                                   int32_t* __restrict__ r_li, int32_t* __restrict__ lrows)
+{
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pos) return;
+  const int32_t r = pos[p];
+  lrows[p] = r;
+  if (r < 0) return;
+  r_unit[r] = (int32_t)(p / rl);
+  r_li[r] = (int32_t)(p % rl);
+}
+
 int64_t env_int(const char* name, int64_t dflt)
 {
   const char* v = variant(name);
@@ -517,6 +578,7 @@ void functor_plan_build(Bsr& b)
   r_li.alloc(n_rows);
   err.alloc(1);
 
+  std::vector<int32_t> clpos;  // non-lattice plans: the clusters' position -> row map
   for (int attempt = 0; attempt < 2; ++attempt) {
     UnitGeom g{};
     g.nv = m.nv;
@@ -554,9 +616,18 @@ void functor_plan_build(Bsr& b)
       g.lattice = 0;
       g.rl = 64 / (k * k);
       g.zs = 1;
-      // 64 / k^2 rows per piece: the last piece may be partial (k = 3: 7 rows,
-      // 64 positions per slice are 9 pieces and one row of the next)
-      P.n_units = (s.n_slices * 64 + g.rl - 1) / g.rl;
+      const char* ce = variant("AFEM_FUNCTOR_CLUSTER");
+      if (!(ce && atoi(ce) == 0)) {
+        // breadth-first clusters of rl rows seeded in the processing order
+        clpos = cluster_positions(ctx, s, g.rl, P.n_units);
+      }
+      else {
+        // 64 / k^2 rows per piece of the processing order: the last piece may
+        // be partial (k = 3: 7 rows, 64 positions per slice are 9 pieces and
+        // one row of the next)
+        clpos.clear();
+        P.n_units = (s.n_slices * 64 + g.rl - 1) / g.rl;
+      }
       P.n_stages = P.n_units;
       P.nbuf = 1;
     }
@@ -567,12 +638,23 @@ void functor_plan_build(Bsr& b)
     P.zs = g.zs;
     P.layer_rows.alloc((size_t)P.n_stages * g.rl);
     AFEM_HIP(hipMemsetAsync(P.layer_rows.p, 0xFF, P.layer_rows.bytes(), ctx.stream));
-    if (g.lattice)
+    if (g.lattice) {
       hipLaunchKernelGGL(k_rowmap_lattice, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx.stream, n_rows, lat[0].p,
                          lat[1].p, lat[2].p, g, r_unit.p, r_li.p, P.layer_rows.p);
-    else
+    }
+    else if (!clpos.empty()) {
+      DevBuf<int32_t> dpos;
+      dpos.alloc(clpos.size());
+      AFEM_HIP(hipMemcpyAsync(dpos.p, clpos.data(), clpos.size() * 4, hipMemcpyHostToDevice, ctx.stream));
+      hipLaunchKernelGGL(k_rowmap_positions, dim3(grid_for((int64_t)clpos.size(), 256)), dim3(256), 0, ctx.stream,
+                         (int64_t)clpos.size(), dpos.p, g.rl, r_unit.p, r_li.p, P.layer_rows.p);
+      AFEM_LAUNCHED();
+      ctx.sync();
+    }
+    else {
       hipLaunchKernelGGL(k_rowmap_slices, dim3(grid_for(s.n_slices * 64, 256)), dim3(256), 0, ctx.stream,
                          s.n_slices * 64, s.perm.p, g.rl, r_unit.p, r_li.p, P.layer_rows.p);
+    }
     AFEM_LAUNCHED();
     bool span_ok = true;
     if (m.nv == 4)
