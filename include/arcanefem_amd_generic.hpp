@@ -106,8 +106,18 @@ __device__ __forceinline__ void unit_lds_order()
 #ifndef AFEM_GENERIC_NT
 #define AFEM_GENERIC_NT 1
 #endif
+/* AFEM_GENERIC_DIAG (diagnostic builds, values wrong): bit 1 no LDS adds (the
+ * element entries summed into a register instead), bit 2 no value stores in
+ * the flush -- where the unit kernel's time goes (tools/generic_ab.py with
+ * AFEM_GENERIC_LIB pointing at such a build). */
+#ifndef AFEM_GENERIC_DIAG
+#define AFEM_GENERIC_DIAG 0
+#endif
 __device__ __forceinline__ void flush_store(double* d, double val, int overwrite)
 {
+#if AFEM_GENERIC_DIAG & 2
+  if (val != 12345.678) return;  // (never taken: keeps the LDS reads)
+#endif
 #if AFEM_GENERIC_NT
   if (overwrite) {
     __builtin_nontemporal_store(val, d);
@@ -170,6 +180,25 @@ __device__ __forceinline__ void flush_layer(const afem_functor_plan& p, const af
       ib += gl;
     }
     unit_lds_order();
+  }
+  else if (K == 1 && swz == 15) {
+    // rows of arbitrary places (slice pieces, clusters): each row's values are one
+    // contiguous range; 16 lanes store 16 consecutive values of one row (4 rows per
+    // instruction) instead of every lane its own row (64 scattered 8-B stores).
+    // The planes are XOR-swizzled by the slot (row' = row ^ (slot & 15)), so the 16
+    // lanes reading one row across 16 planes hit 16 distinct banks.  Measured (r06q,
+    // AFEM_GENERIC_DIAG=2, L-shape-3D refined 6x): the per-lane stores cost 0.45 ms
+    // of 2.98 with the module's element, 0.88 of 2.90 with the lean one; this flush:
+    // 3.10 -> 2.74 and 2.99 -> 2.38 ms (r06r/r06s; one stream of the layer's segments,
+    // a lane per value found by a binary search over the offsets: 2.95 / 2.62 ms)
+    const int sub = lane & 15;
+#pragma unroll 4
+    for (int g = 0; g < 16; ++g) {
+      const int L = 4 * g + (lane >> 4);
+      const long long rbL = __shfl((long long)rb, L);
+      const int lenL = __shfl(len, L);
+      for (int s = sub; s < lenL; s += 16) flush_store(p.values + rbL + s, buf[s * sr + (L ^ (s & 15))], overwrite);
+    }
   }
   else if (row >= 0) {
     for (int s = 0; s < len; ++s)
@@ -239,6 +268,9 @@ __global__ void __launch_bounds__(64) AFEM_GENERIC_WAVES_ATTR k_assemble_units(a
   uint4 nxt[UN];
   uint2 nxt2[UN];
   int64_t nxt_base = -1;
+#if AFEM_GENERIC_DIAG & 1
+  double diag_sink = 0.0;
+#endif
   for (int L = 0; L < U.n_stages; ++L) {
     const int64_t e0 = p.stage_ptr[U.first_stage + L], e1 = p.stage_ptr[U.first_stage + L + 1];
     const int64_t e2 = L + 1 < U.n_stages ? p.stage_ptr[U.first_stage + L + 2] : e1;
@@ -325,7 +357,11 @@ __global__ void __launch_bounds__(64) AFEM_GENERIC_WAVES_ATTR k_assemble_units(a
 #pragma unroll
                 for (int jj = 0; jj < K; ++jj) {
                   const int pl = s * KK + i * K + jj;
+#if AFEM_GENERIC_DIAG & 1
+                  diag_sink += (double)ke[v](K * a + i, K * b + jj) + (double)(pl * sr + row);
+#else
                   atomicAdd(bufp + pl * sr + (row ^ (pl & swz)), (double)ke[v](K * a + i, K * b + jj));
+#endif
                 }
             }
           }
@@ -344,6 +380,9 @@ __global__ void __launch_bounds__(64) AFEM_GENERIC_WAVES_ATTR k_assemble_units(a
     if (L > 0) flush_layer<K, WIDE>(p, U, L - 1, acc, bufsz, sr, swz, lane, overwrite);
   }
   flush_layer<K, WIDE>(p, U, U.n_stages - 1, acc, bufsz, sr, swz, lane, overwrite);
+#if AFEM_GENERIC_DIAG & 1
+  if (diag_sink == 12345.678) p.values[0] = diag_sink;  // (never taken: keeps the functors)
+#endif
 }
 
 /* Functor evaluations in flight per lane: 4 for element matrices up to 4 x 4
@@ -357,6 +396,10 @@ __global__ void __launch_bounds__(64) AFEM_GENERIC_WAVES_ATTR k_assemble_units(a
 #endif
 #ifndef AFEM_GENERIC_PAD
 #define AFEM_GENERIC_PAD 0
+#endif
+/* the coalesced flush of units without a lattice (flush_layer; 0: the per-lane row stores) */
+#ifndef AFEM_GENERIC_TRFLUSH
+#define AFEM_GENERIC_TRFLUSH 1
 #endif
 constexpr int default_unroll(int nk) { return nk * nk <= 16 ? AFEM_GENERIC_UNROLL : 1; }
 
@@ -444,8 +487,11 @@ int assemble_bilinear_unrolled(afem_bsr* bsr, F f, Mode mode = Mode::Accumulate,
   // pad < 0: no padding, the rows of plane pl XOR-swizzled by pl mod 16 instead
   // (power-of-two planes of at least 16 rows)
   const int RL = p.rows_per_layer;
-  const int swz = pad < 0 && RL >= 16 && (RL & (RL - 1)) == 0 ? 15 : 0;
-  if (pad < 0) pad = 0;
+  // units of arbitrary rows (no lattice; K = 1, 64 rows): XOR-swizzled planes, for
+  // the coalesced flush (flush_layer)
+  const bool tr = !p.lattice && K == 1 && RL == 64 && AFEM_GENERIC_TRFLUSH;
+  const int swz = tr || (pad < 0 && RL >= 16 && (RL & (RL - 1)) == 0) ? 15 : 0;
+  if (pad < 0 || tr) pad = 0;
   int sr = p.rows_per_layer + pad;
   size_t lds = (size_t)p.nbuf * p.width * K * K * sr * sizeof(double);
   if (lds > 64 * 1024 && pad) {  // no room for the padding: dense planes
