@@ -50,6 +50,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -124,14 +125,18 @@ __global__ __launch_bounds__(256) void k_amg_strength(int64_t n, const int64_t* 
   }
 }
 
-// m[i] = max(t[i], t[j] for strong neighbours j); 8 lanes per row
+// m[i] = max(t[i], t[j] for strong neighbours j); 8 lanes per row.  gate (the
+// round's last hop): only the undecided rows' maxima are read (k_amg_mis_update),
+// the others are skipped
 __global__ __launch_bounds__(256) void k_amg_maxprop(int64_t n, const int64_t* __restrict__ rp,
                                                      const int32_t* __restrict__ ci,
                                                      const uint8_t* __restrict__ strong,
-                                                     const uint64_t* __restrict__ t, uint64_t* __restrict__ m)
+                                                     const uint64_t* __restrict__ t, uint64_t* __restrict__ m,
+                                                     const uint64_t* __restrict__ gate)
 {
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
   const int l = threadIdx.x & 7;
+  if (gate && i < n && (gate[i] >> 62) != 1) return;
   uint64_t b = 0;
   if (i < n) {
     b = t[i];
@@ -154,16 +159,23 @@ __global__ void k_amg_mis_update(int64_t n, uint64_t* __restrict__ t, const uint
                                  unsigned long long* __restrict__ left)
 {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t ti = t[i];
-  if ((ti >> 62) != 1) return;
-  const uint64_t mi = m[i];
-  if (mi == ti)
-    t[i] = (2ull << 62) | (ti & ((1ull << 62) - 1));
-  else if ((mi >> 62) == 2)
-    t[i] = ti & ((1ull << 62) - 1);  // out
-  else
-    atomicAdd(left, 1ull);
+  bool undecided = false;
+  if (i < n) {
+    const uint64_t ti = t[i];
+    if ((ti >> 62) == 1) {
+      const uint64_t mi = m[i];
+      if (mi == ti)
+        t[i] = (2ull << 62) | (ti & ((1ull << 62) - 1));
+      else if ((mi >> 62) == 2)
+        t[i] = ti & ((1ull << 62) - 1);  // out
+      else
+        undecided = true;
+    }
+  }
+  // one count per wave (a thread's own atomic on the one address serialised
+  // millions of them in the first rounds)
+  const unsigned long long w = __ballot(undecided);
+  if ((threadIdx.x & 63) == 0 && w) atomicAdd(left, (unsigned long long)__popcll(w));
 }
 
 __global__ void k_amg_root_flags(int64_t n, const uint64_t* __restrict__ t, int32_t* __restrict__ f)
@@ -227,10 +239,10 @@ __global__ void k_amg_orphan_agg(int64_t n, const int32_t* __restrict__ f, const
   if (f[i]) agg[i] = base + (int32_t)rank[i];
 }
 
-__global__ void k_amg_iota(int64_t n, int64_t* __restrict__ x)
+__global__ void k_amg_iota32(int64_t n, int32_t* __restrict__ x)
 {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) x[i] = i;
+  if (i < n) x[i] = (int32_t)i;
 }
 
 // run heads of the sorted keys (valid keys only)
@@ -242,10 +254,10 @@ __global__ void k_amg_heads(int64_t m, const unsigned long long* __restrict__ ke
 }
 
 // run r = [pos of head r, next head): its sum in the sorted (= CSR) order
-__global__ void k_amg_runs(int64_t m, const unsigned long long* __restrict__ key, const int64_t* __restrict__ src,
+__global__ void k_amg_runs(int64_t m, const unsigned long long* __restrict__ key, const int32_t* __restrict__ src,
                            const double* __restrict__ v, const int32_t* __restrict__ head,
-                           const int64_t* __restrict__ hrank, int64_t row_base, int64_t* __restrict__ c_row_of,
-                           int32_t* __restrict__ c_col, double* __restrict__ c_val)
+                           const int64_t* __restrict__ hrank, int64_t row_base, int cbits,
+                           int64_t* __restrict__ c_row_of, int32_t* __restrict__ c_col, double* __restrict__ c_val)
 {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= m || !head[k]) return;
@@ -253,8 +265,8 @@ __global__ void k_amg_runs(int64_t m, const unsigned long long* __restrict__ key
   double s = 0.0;
   for (int64_t q = k; q < m && key[q] == kk; ++q) s += v[src[q]];
   const int64_t r = hrank[k];
-  c_row_of[r] = (int64_t)(kk >> 32) - row_base;
-  c_col[r] = (int32_t)(kk & 0xffffffffu);
+  c_row_of[r] = (int64_t)(kk >> cbits) - row_base;
+  c_col[r] = (int32_t)(kk & ((1ull << cbits) - 1));
   c_val[r] = s;
 }
 
@@ -413,6 +425,36 @@ __global__ void k_amg_mul(int64_t n, double a, double* __restrict__ v)
     v[i] *= a;
 }
 
+// power iteration on the device (one rank): st = {norm of the previous iterate,
+// lambda, 1 / norm of this one, stopped}.  The partials summed in order by one
+// thread (the host loop's sum, bit for bit); first = the initial vector's norm
+__global__ void k_amg_pw_norm(const double* __restrict__ partial, int g, int first, double* __restrict__ st)
+{
+  if (threadIdx.x != 0 || st[3] != 0.0) return;
+  double s = 0.0;
+  for (int k = 0; k < g; ++k) s += partial[k];
+  const double nw = sqrt(s);
+  if (first) {
+    st[0] = nw;
+    return;
+  }
+  st[1] = st[0] > 0 ? nw / st[0] : 0.0;
+  if (!(nw > 0)) {
+    st[3] = 1.0;
+    return;
+  }
+  st[2] = 1.0 / nw;
+  st[0] = 1.0;
+}
+
+__global__ void k_amg_mul_dev(int64_t n, const double* __restrict__ st, double* __restrict__ v)
+{
+  if (st[3] != 0.0) return;
+  const double a = st[2];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    v[i] *= a;
+}
+
 __global__ __launch_bounds__(64) void k_amg_gemv(int n, const double* __restrict__ A, const double* __restrict__ b,
                                                  double* __restrict__ x)
 {
@@ -439,7 +481,7 @@ __global__ void k_amg_promote(int64_t n, uint64_t* __restrict__ t)
 // level; all ones outside the graph
 __global__ void k_amg_keys_map(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
                                const int32_t* __restrict__ agg, int64_t row_base, const int32_t* __restrict__ cmap,
-                               int64_t ncol, unsigned long long* __restrict__ key)
+                               int64_t ncol, int cbits, unsigned long long* __restrict__ key)
 {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -447,7 +489,7 @@ __global__ void k_amg_keys_map(int64_t n, const int64_t* __restrict__ rp, const 
   for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
     const int32_t j = ci[k];
     const int32_t aj = (j >= 0 && j < ncol) ? cmap[j] : -1;
-    key[k] = (ai >= 0 && aj >= 0) ? ((unsigned long long)(uint32_t)(row_base + ai) << 32 | (uint32_t)aj) : ~0ull;
+    key[k] = (ai >= 0 && aj >= 0) ? ((unsigned long long)(row_base + ai) << cbits | (uint32_t)aj) : ~0ull;
   }
 }
 
@@ -640,6 +682,26 @@ double power_lambda(Ctx& ctx, Amg& a, AmgLevel& L)
     AFEM_LAUNCHED();
   }
   const bool d = L.dist;
+  if (!d && L.n > 0) {
+    // one rank: no host round trip per iteration (the same arithmetic and order)
+    DevBuf<double> st;
+    st.alloc(4);
+    AFEM_HIP(hipMemsetAsync(st.p, 0, st.bytes(), ctx.stream));
+    hipLaunchKernelGGL(k_amg_pw_norm, dim3(1), dim3(64), 0, ctx.stream, (const double*)a.partial.p, (int)g, 1, st.p);
+    for (int it = 0; it < kPowerIts; ++it) {
+      spmv(ctx, 0, L, L.x.p, L.t.p, nullptr, 0.0);
+      hipLaunchKernelGGL(k_amg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, (const double*)L.dinv.p, L.t.p,
+                         a.partial.p);
+      hipLaunchKernelGGL(k_amg_pw_norm, dim3(1), dim3(64), 0, ctx.stream, (const double*)a.partial.p, (int)g, 0, st.p);
+      hipLaunchKernelGGL(k_amg_mul_dev, dim3(g), dim3(256), 0, ctx.stream, L.n, (const double*)st.p, L.t.p);
+      AFEM_LAUNCHED();
+      std::swap(L.x, L.t);
+    }
+    double lam = 0.0;
+    AFEM_HIP(hipMemcpyAsync(&lam, st.p + 1, sizeof(double), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    return lam;
+  }
   double nv = std::sqrt(d ? allsum(ctx, a, L.n > 0 ? host_sum(ctx, a.partial, (int)g) : 0.0)
                           : host_sum(ctx, a.partial, (int)g)),
          lam = 0.0;
@@ -720,10 +782,10 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
   for (int round = 0; round < 64; ++round) {
     // max over the distance-`hops` neighbourhood
     hipLaunchKernelGGL(k_amg_maxprop, dim3(g8), dim3(256), 0, ctx.stream, n, L.rp, L.ci, (const uint8_t*)strong.p,
-                       (const uint64_t*)t.p, m.p);
+                       (const uint64_t*)t.p, m.p, hops == 1 ? (const uint64_t*)t.p : nullptr);
     for (int h = 1; h < hops; ++h) {
       hipLaunchKernelGGL(k_amg_maxprop, dim3(g8), dim3(256), 0, ctx.stream, n, L.rp, L.ci, (const uint8_t*)strong.p,
-                         (const uint64_t*)m.p, m2.p);
+                         (const uint64_t*)m.p, m2.p, h + 1 == hops ? (const uint64_t*)t.p : nullptr);
       std::swap(m, m2);
     }
     AFEM_HIP(hipMemsetAsync(left.p, 0, sizeof(unsigned long long), ctx.stream));
@@ -732,7 +794,10 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
     unsigned long long hl = 0;
     AFEM_HIP(hipMemcpyAsync(&hl, left.p, sizeof(hl), hipMemcpyDeviceToHost, ctx.stream));
     ctx.sync();
-    if (hl == 0) break;
+    if (hl == 0) {
+      if (env_double("AFEM_AMG_VERBOSE", 0.0) > 0) std::fprintf(stderr, "amg: independent set in %d rounds\n", round + 1);
+      break;
+    }
     if (round == 63) {
       //  the independent set did not settle in 64 rounds: the
       // undecided nodes become roots instead of failing the solve
@@ -800,29 +865,45 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
 // The coarse operator's non-zeros of level L's rows, keyed (row_base + agg i,
 // cmap[j]): radix-sorted (stable), each run summed in the CSR order.  Out: the
 // rows (relative to row_base) of the n_out coarse rows, their columns and
-// values (COO in row order) and their count
-int64_t galerkin_coo(Ctx& ctx, AmgLevel& L, const int32_t* cmap, int64_t ncol, int64_t row_base,
-                     DevBuf<int64_t>& row_of, DevBuf<int32_t>& col, DevBuf<double>& val)
+// values (COO in row order) and their count.  row_bound / col_bound: exclusive
+// bounds of row_base + agg i and of cmap[j]; the key packs them into
+// bitlen(row_bound) + bitlen(col_bound - 1) bits and the sort runs over those
+// only (5 digit passes instead of 8 at the unstructured leg's 11.5 M rows), with
+// 32-bit source positions (amg_available: nnz < 2^31).  An invalid key (~0) is
+// all ones in the sorted bits, which no valid key is (row < 2^rbits - 1).
+int64_t galerkin_coo(Ctx& ctx, AmgLevel& L, const int32_t* cmap, int64_t ncol, int64_t row_base, int64_t row_bound,
+                     int64_t col_bound, DevBuf<int64_t>& row_of, DevBuf<int32_t>& col, DevBuf<double>& val)
 {
   const int64_t nnz = L.nnz;
+  auto bitlen = [](uint64_t x) {
+    int b = 0;
+    while (x) {
+      ++b;
+      x >>= 1;
+    }
+    return b;
+  };
+  const int cbits = std::max(1, bitlen((uint64_t)std::max<int64_t>(col_bound - 1, 0)));
+  const int rbits = bitlen((uint64_t)std::max<int64_t>(row_bound, 1));
+  AFEM_REQUIRE(cbits <= 32 && cbits + rbits <= 64, AFEM_ERR_LIMIT, "amg: coarse key above 64 bits");
   DevBuf<unsigned long long> key, key_s;
-  DevBuf<int64_t> src, src_s;
+  DevBuf<int32_t> src, src_s;
   key.alloc(nnz > 0 ? nnz : 1);
   key_s.alloc(nnz > 0 ? nnz : 1);
   src.alloc(nnz > 0 ? nnz : 1);
   src_s.alloc(nnz > 0 ? nnz : 1);
   if (L.n > 0) {
     hipLaunchKernelGGL(k_amg_keys_map, dim3(grid_for(L.n, 256)), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci,
-                       (const int32_t*)L.agg.p, row_base, cmap, ncol, key.p);
-    hipLaunchKernelGGL(k_amg_iota, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz, src.p);
+                       (const int32_t*)L.agg.p, row_base, cmap, ncol, cbits, key.p);
+    hipLaunchKernelGGL(k_amg_iota32, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz, src.p);
     AFEM_LAUNCHED();
   }
   size_t tb = 0;
-  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.p, key_s.p, src.p, src_s.p, (int)nnz, 0, 64,
-                                              ctx.stream));
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.p, key_s.p, src.p, src_s.p, (int)nnz, 0,
+                                              cbits + rbits, ctx.stream));
   DevBuf<unsigned char> tmp;
   tmp.alloc(tb > 0 ? tb : 1);
-  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, key.p, key_s.p, src.p, src_s.p, (int)nnz, 0, 64,
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, key.p, key_s.p, src.p, src_s.p, (int)nnz, 0, cbits + rbits,
                                               ctx.stream));
   key.reset();
   src.reset();
@@ -842,8 +923,8 @@ int64_t galerkin_coo(Ctx& ctx, AmgLevel& L, const int32_t* cmap, int64_t ncol, i
   val.alloc(cnnz > 0 ? cnnz : 1);
   if (nnz > 0) {
     hipLaunchKernelGGL(k_amg_runs, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz,
-                       (const unsigned long long*)key_s.p, src_s.p, L.v, head.p, hrank.p, row_base, row_of.p, col.p,
-                       val.p);
+                       (const unsigned long long*)key_s.p, (const int32_t*)src_s.p, L.v, head.p, hrank.p, row_base,
+                       cbits, row_of.p, col.p, val.p);
     AFEM_LAUNCHED();
   }
   ctx.sync();
@@ -877,7 +958,7 @@ void galerkin(Ctx& ctx, AmgLevel& L, int64_t nc, AmgLevel& C)
   DevBuf<int64_t> row_of;
   DevBuf<int32_t> col;
   DevBuf<double> val;
-  const int64_t cnnz = galerkin_coo(ctx, L, L.agg.p, L.n, 0, row_of, col, val);
+  const int64_t cnnz = galerkin_coo(ctx, L, L.agg.p, L.n, 0, nc, nc, row_of, col, val);
   coo_to_level(ctx, nc, cnnz, row_of, col, val, C);
   C.ncol = nc;
 }
@@ -971,7 +1052,7 @@ void build_dist_coarse(Ctx& ctx, Amg& a, AmgLevel& L, int64_t nc, AmgLevel& C)
   DevBuf<int64_t> row_of;
   DevBuf<int32_t> col;
   DevBuf<double> val;
-  const int64_t cnnz = galerkin_coo(ctx, L, dmap.p, L.ncol, 0, row_of, col, val);
+  const int64_t cnnz = galerkin_coo(ctx, L, dmap.p, L.ncol, 0, nc, next, row_of, col, val);
   coo_to_level(ctx, nc, cnnz, row_of, col, val, C);
   C.ncol = next;
 }
@@ -998,7 +1079,7 @@ void build_gathered(Ctx& ctx, Amg& a, AmgLevel& L, int64_t nc, const std::vector
   DevBuf<int64_t> row_of;
   DevBuf<int32_t> col;
   DevBuf<double> val;
-  const int64_t cnnz = galerkin_coo(ctx, L, dmap.p, L.ncol, 0, row_of, col, val);
+  const int64_t cnnz = galerkin_coo(ctx, L, dmap.p, L.ncol, 0, nc, NG, row_of, col, val);
   // (galerkin_coo keys agg i + row_base: with row_base 0 the rows are my local
   // aggregate ids; shifted to global ids below)
   std::vector<double> cnt(nr, 0.0);
@@ -1321,6 +1402,16 @@ bool amg_setup(LinearSystem& ls)
     a->lv.push_back(std::move(L));
   }
   const bool verbose = env_double("AFEM_AMG_VERBOSE", 0.0) > 0;
+  // AFEM_AMG_VERBOSE: wall time of the setup phases (the device drained at each mark)
+  auto t_last = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!verbose) return;
+    ctx.sync();
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "amg setup %-28s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
+  mark("fine level");
   while ((int)a->lv.size() < kMaxLevels) {
     AmgLevel& L = a->lv.back();
     const int64_t n_glob = L.dist ? (int64_t)allsum(ctx, *a, (double)L.n) : L.n;
@@ -1336,6 +1427,7 @@ bool amg_setup(LinearSystem& ls)
       continue;
     }
     const int64_t nc = aggregate(ctx, L, theta, a->lv.size() == 1 ? hops0 : hops);
+    mark("aggregate");
     const int64_t nc_glob = L.dist ? (int64_t)allsum(ctx, *a, (double)nc) : nc;
     if (verbose)
       std::fprintf(stderr, "amg level %zu%s: %lld rows, %lld non-zeros -> %lld aggregates (global %lld -> %lld)\n",
@@ -1367,8 +1459,10 @@ bool amg_setup(LinearSystem& ls)
     else {
       build_dist_coarse(ctx, *a, L, nc, C);
     }
+    mark("coarse operator");
     level_prepare(ctx, C, nullptr);
     a->lv.push_back(std::move(C));
+    mark("coarse level prepared");
   }
   for (auto& L : a->lv) {
     // the power iteration approaches lambda_max from below: 10 % margin (an
@@ -1376,6 +1470,7 @@ bool amg_setup(LinearSystem& ls)
     const double lam = 1.1 * power_lambda(ctx, *a, L);
     L.omega = lam > 0 ? 4.0 / (3.0 * lam) : 0.0;
   }
+  mark("power iterations");
   AmgLevel& last = a->lv.back();
   // the coarsest level inverted densely when small (a small system: the
   // whole matrix, the PCG then converges in one or two iterations); a
@@ -1394,6 +1489,7 @@ bool amg_setup(LinearSystem& ls)
     L.krt.alloc(L.n > 0 ? L.n : 1);
     L.kcoef.alloc(8);
   }
+  mark("dense coarsest, K-cycle buffers");
   a->key_rows = ls.csr_rows;
   a->key_cols = ls.csr_cols;
   a->key_vals = ls.csr_vals;
