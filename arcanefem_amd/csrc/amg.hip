@@ -127,23 +127,31 @@ __global__ __launch_bounds__(256) void k_amg_strength(int64_t n, const int64_t* 
 
 // m[i] = max(t[i], t[j] for strong neighbours j); 8 lanes per row.  gate (the
 // round's last hop): only the undecided rows' maxima are read (k_amg_mis_update),
-// the others are skipped
+// the others are skipped; those rows mark (mark[i] = mark[j] = markv) the rows
+// whose first-hop maxima they read, and the next round's first hop computes only
+// the rows marked for it (relg[i] == relv: the undecided set only shrinks, so
+// they are all the next round reads)
 __global__ __launch_bounds__(256) void k_amg_maxprop(int64_t n, const int64_t* __restrict__ rp,
                                                      const int32_t* __restrict__ ci,
                                                      const uint8_t* __restrict__ strong,
                                                      const uint64_t* __restrict__ t, uint64_t* __restrict__ m,
-                                                     const uint64_t* __restrict__ gate)
+                                                     const uint64_t* __restrict__ gate, const uint8_t* __restrict__ relg,
+                                                     int relv, uint8_t* __restrict__ mark, int markv)
 {
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
   const int l = threadIdx.x & 7;
   if (gate && i < n && (gate[i] >> 62) != 1) return;
+  if (relg && i < n && relg[i] != (uint8_t)relv) return;
   uint64_t b = 0;
   if (i < n) {
     b = t[i];
+    if (mark && l == 0) mark[i] = (uint8_t)markv;
     for (int64_t k = rp[i] + l; k < rp[i + 1]; k += 8)
       if (strong[k]) {
-        const uint64_t tj = t[ci[k]];
+        const int32_t j = ci[k];
+        const uint64_t tj = t[j];
         b = tj > b ? tj : b;
+        if (mark) mark[j] = (uint8_t)markv;
       }
   }
   for (int o = 1; o < 8; o <<= 1) {
@@ -172,10 +180,15 @@ __global__ void k_amg_mis_update(int64_t n, uint64_t* __restrict__ t, const uint
         undecided = true;
     }
   }
-  // one count per wave (a thread's own atomic on the one address serialised
-  // millions of them in the first rounds)
+  // one count per workgroup (a thread's own atomic on the one address serialised
+  // millions of them in the first rounds; one per wave still cost 0.2-0.7 ms a round)
+  __shared__ unsigned int cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
   const unsigned long long w = __ballot(undecided);
-  if ((threadIdx.x & 63) == 0 && w) atomicAdd(left, (unsigned long long)__popcll(w));
+  if ((threadIdx.x & 63) == 0 && w) atomicAdd(&cnt, (unsigned int)__popcll(w));
+  __syncthreads();
+  if (threadIdx.x == 0 && cnt) atomicAdd(left, (unsigned long long)cnt);
 }
 
 __global__ void k_amg_root_flags(int64_t n, const uint64_t* __restrict__ t, int32_t* __restrict__ f)
@@ -239,12 +252,6 @@ __global__ void k_amg_orphan_agg(int64_t n, const int32_t* __restrict__ f, const
   if (f[i]) agg[i] = base + (int32_t)rank[i];
 }
 
-__global__ void k_amg_iota32(int64_t n, int32_t* __restrict__ x)
-{
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) x[i] = (int32_t)i;
-}
-
 // run heads of the sorted keys (valid keys only)
 __global__ void k_amg_heads(int64_t m, const unsigned long long* __restrict__ key, int32_t* __restrict__ head)
 {
@@ -254,8 +261,8 @@ __global__ void k_amg_heads(int64_t m, const unsigned long long* __restrict__ ke
 }
 
 // run r = [pos of head r, next head): its sum in the sorted (= CSR) order
-__global__ void k_amg_runs(int64_t m, const unsigned long long* __restrict__ key, const int32_t* __restrict__ src,
-                           const double* __restrict__ v, const int32_t* __restrict__ head,
+__global__ void k_amg_runs(int64_t m, const unsigned long long* __restrict__ key, const double* __restrict__ vs,
+                           const int32_t* __restrict__ head,
                            const int64_t* __restrict__ hrank, int64_t row_base, int cbits,
                            int64_t* __restrict__ c_row_of, int32_t* __restrict__ c_col, double* __restrict__ c_val)
 {
@@ -263,7 +270,7 @@ __global__ void k_amg_runs(int64_t m, const unsigned long long* __restrict__ key
   if (k >= m || !head[k]) return;
   const unsigned long long kk = key[k];
   double s = 0.0;
-  for (int64_t q = k; q < m && key[q] == kk; ++q) s += v[src[q]];
+  for (int64_t q = k; q < m && key[q] == kk; ++q) s += vs[q];
   const int64_t r = hrank[k];
   c_row_of[r] = (int64_t)(kk >> cbits) - row_base;
   c_col[r] = (int32_t)(kk & ((1ull << cbits) - 1));
@@ -364,8 +371,23 @@ __global__ void k_amg_restrict(int64_t nc, const int64_t* __restrict__ ap, const
 {
   const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= nc) return;
+  // the members 16 at a time: their indices, then their values, all in flight
+  // together, summed in member order (the serial loop's sum, bit for bit; it
+  // waited on two dependent loads per member: 210 us per level-0 restriction at
+  // 11.5 M rows, r06y)
   double s = 0.0;
-  for (int64_t q = ap[a]; q < ap[a + 1]; ++q) s += r[mem[q]];
+  const int64_t q0 = ap[a], q1 = ap[a + 1];
+  for (int64_t qb = q0; qb < q1; qb += 16) {
+    int32_t mi[16];
+    double rv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) mi[u] = qb + u < q1 ? mem[qb + u] : -1;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) rv[u] = mi[u] >= 0 ? r[mi[u]] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (qb + u < q1) s += rv[u];
+  }
   bc[a] = s;
 }
 
@@ -778,14 +800,22 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
                      strong.p);
   AFEM_LAUNCHED();
   DevBuf<uint64_t> m2;
-  if (hops > 1) m2.alloc(n);
+  DevBuf<uint8_t> rel;
+  if (hops > 1) {
+    m2.alloc(n);
+    rel.alloc(n);
+    AFEM_HIP(hipMemsetAsync(rel.p, 0, n, ctx.stream));
+  }
   for (int round = 0; round < 64; ++round) {
-    // max over the distance-`hops` neighbourhood
+    // max over the distance-`hops` neighbourhood (hops 2: the first hop over the rows
+    // the previous round marked, the second over the undecided rows)
     hipLaunchKernelGGL(k_amg_maxprop, dim3(g8), dim3(256), 0, ctx.stream, n, L.rp, L.ci, (const uint8_t*)strong.p,
-                       (const uint64_t*)t.p, m.p, hops == 1 ? (const uint64_t*)t.p : nullptr);
+                       (const uint64_t*)t.p, m.p, hops == 1 ? (const uint64_t*)t.p : nullptr,
+                       hops > 1 && round > 0 ? (const uint8_t*)rel.p : nullptr, round, (uint8_t*)nullptr, 0);
     for (int h = 1; h < hops; ++h) {
       hipLaunchKernelGGL(k_amg_maxprop, dim3(g8), dim3(256), 0, ctx.stream, n, L.rp, L.ci, (const uint8_t*)strong.p,
-                         (const uint64_t*)m.p, m2.p, h + 1 == hops ? (const uint64_t*)t.p : nullptr);
+                         (const uint64_t*)m.p, m2.p, h + 1 == hops ? (const uint64_t*)t.p : nullptr,
+                         (const uint8_t*)nullptr, 0, h + 1 == hops ? rel.p : (uint8_t*)nullptr, round + 1);
       std::swap(m, m2);
     }
     AFEM_HIP(hipMemsetAsync(left.p, 0, sizeof(unsigned long long), ctx.stream));
@@ -868,9 +898,11 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
 // values (COO in row order) and their count.  row_bound / col_bound: exclusive
 // bounds of row_base + agg i and of cmap[j]; the key packs them into
 // bitlen(row_bound) + bitlen(col_bound - 1) bits and the sort runs over those
-// only (5 digit passes instead of 8 at the unstructured leg's 11.5 M rows), with
-// 32-bit source positions (amg_available: nnz < 2^31).  An invalid key (~0) is
-// all ones in the sorted bits, which no valid key is (row < 2^rbits - 1).
+// only (5 digit passes instead of 8 at the unstructured leg's 11.5 M rows); the
+// sort carries the values themselves (the runs then sum contiguous values: the
+// gather through sorted source positions cost 16 ms at that size, r06y).  An
+// invalid key (~0) is all ones in the sorted bits, which no valid key is
+// (row < 2^rbits - 1).
 int64_t galerkin_coo(Ctx& ctx, AmgLevel& L, const int32_t* cmap, int64_t ncol, int64_t row_base, int64_t row_bound,
                      int64_t col_bound, DevBuf<int64_t>& row_of, DevBuf<int32_t>& col, DevBuf<double>& val)
 {
@@ -887,26 +919,24 @@ int64_t galerkin_coo(Ctx& ctx, AmgLevel& L, const int32_t* cmap, int64_t ncol, i
   const int rbits = bitlen((uint64_t)std::max<int64_t>(row_bound, 1));
   AFEM_REQUIRE(cbits <= 32 && cbits + rbits <= 64, AFEM_ERR_LIMIT, "amg: coarse key above 64 bits");
   DevBuf<unsigned long long> key, key_s;
-  DevBuf<int32_t> src, src_s;
+  DevBuf<double> val_s;
   key.alloc(nnz > 0 ? nnz : 1);
   key_s.alloc(nnz > 0 ? nnz : 1);
-  src.alloc(nnz > 0 ? nnz : 1);
-  src_s.alloc(nnz > 0 ? nnz : 1);
+  val_s.alloc(nnz > 0 ? nnz : 1);
   if (L.n > 0) {
     hipLaunchKernelGGL(k_amg_keys_map, dim3(grid_for(L.n, 256)), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci,
                        (const int32_t*)L.agg.p, row_base, cmap, ncol, cbits, key.p);
-    hipLaunchKernelGGL(k_amg_iota32, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz, src.p);
     AFEM_LAUNCHED();
   }
   size_t tb = 0;
-  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.p, key_s.p, src.p, src_s.p, (int)nnz, 0,
-                                              cbits + rbits, ctx.stream));
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.p, key_s.p, L.v, val_s.p, (int)nnz, 0, cbits + rbits,
+                                              ctx.stream));
   DevBuf<unsigned char> tmp;
   tmp.alloc(tb > 0 ? tb : 1);
-  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, key.p, key_s.p, src.p, src_s.p, (int)nnz, 0, cbits + rbits,
+  AFEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, key.p, key_s.p, L.v, val_s.p, (int)nnz, 0, cbits + rbits,
                                               ctx.stream));
   key.reset();
-  src.reset();
+  tmp.reset();
   DevBuf<int32_t> head;
   DevBuf<int64_t> hrank;
   head.alloc(nnz > 0 ? nnz : 1);
@@ -923,8 +953,8 @@ int64_t galerkin_coo(Ctx& ctx, AmgLevel& L, const int32_t* cmap, int64_t ncol, i
   val.alloc(cnnz > 0 ? cnnz : 1);
   if (nnz > 0) {
     hipLaunchKernelGGL(k_amg_runs, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz,
-                       (const unsigned long long*)key_s.p, (const int32_t*)src_s.p, L.v, head.p, hrank.p, row_base,
-                       cbits, row_of.p, col.p, val.p);
+                       (const unsigned long long*)key_s.p, (const double*)val_s.p, head.p, hrank.p, row_base, cbits,
+                       row_of.p, col.p, val.p);
     AFEM_LAUNCHED();
   }
   ctx.sync();
