@@ -358,6 +358,125 @@ __global__ void k_amg_scale(int64_t n, double omega, const double* __restrict__ 
     x[i] = omega * dinv[i] * b[i];
 }
 
+// the fine level's cycle products on an fp32 copy of its values (AFEM_AMG_F32):
+// CSR-stream over 256-row blocks (the block's value / column segment read with
+// 16-B loads, four groups of 4 per lane in flight, products to LDS in a rotated
+// order, one lane per row sums its products in CSR order) with the cycle's
+// epilogue fused: EPI 2 y = b - A x (the residual), EPI 1 y = x + omega dinv
+// (b - A x) (a Jacobi sweep; y must not be x).  The values are the preconditioner's
+// only: the PCG's own product stays in fp64.  8 instead of 12 B per non-zero
+__global__ void k_amg_d2f(int64_t n, const double* __restrict__ v, float* __restrict__ f)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    f[i] = (float)v[i];
+}
+
+__global__ __launch_bounds__(256) void k_amg_seg256(int64_t n_rows, const int64_t* __restrict__ rp,
+                                                    unsigned long long* __restrict__ mx)
+{
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r0 = b * 256;
+  if (r0 >= n_rows) return;
+  const int64_t r1 = r0 + 256 < n_rows ? r0 + 256 : n_rows;
+  atomicMax(mx, (unsigned long long)(rp[r1] - rp[r0]));
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) void k_amg_f32(int64_t n_rows, int64_t nnz, const int64_t* __restrict__ rp,
+                                                 const int32_t* __restrict__ ci, const float* __restrict__ vf,
+                                                 const double* __restrict__ x, const double* __restrict__ b,
+                                                 const double* __restrict__ dinv, double omega,
+                                                 double* __restrict__ y)
+{
+  constexpr int U = 4;
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* prod = reinterpret_cast<double*>(smem);
+  const int64_t q8 = gridDim.x >> 3, rem = gridDim.x & 7;
+  const int64_t xcd = blockIdx.x & 7;
+  const int64_t blk = xcd * q8 + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);  // each XCD a contiguous range
+  const int64_t r0 = blk * 256;
+  const int64_t r1 = r0 + 256 < n_rows ? r0 + 256 : n_rows;
+  const int64_t a = rp[r0], e = rp[r1];
+  const int64_t q0 = (a & ~int64_t(3)) + 4 * (int64_t)threadIdx.x;
+  auto load4 = [&](int64_t q, int (&c)[4], double (&v)[4]) {
+    if (q + 4 <= nnz) {
+      const int4 c4 = *reinterpret_cast<const int4*>(ci + q);
+      const float4 f4 = *reinterpret_cast<const float4*>(vf + q);
+      c[0] = c4.x;
+      c[1] = c4.y;
+      c[2] = c4.z;
+      c[3] = c4.w;
+      v[0] = f4.x;
+      v[1] = f4.y;
+      v[2] = f4.z;
+      v[3] = f4.w;
+    }
+    else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = q + j < nnz ? ci[q + j] : 0;
+        v[j] = q + j < nnz ? (double)vf[q + j] : 0.0;
+      }
+    }
+  };
+  const int rot = (int)(threadIdx.x >> 3) & 3;
+  auto put4 = [&](int64_t q, const double (&v)[4], const double (&xv)[4]) {
+    double pr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pr[j] = v[j] * xv[j];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = (t + rot) & 3;
+      const double w = j == 0 ? pr[0] : (j == 1 ? pr[1] : (j == 2 ? pr[2] : pr[3]));
+      if (q + j >= a && q + j < e) prod[q + j - a] = w;
+    }
+  };
+  {
+    int c[U][4];
+    double v[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = q0 + (int64_t)u * 1024;
+      if (q < e) {
+        load4(q, c[u], v[u]);
+      }
+      else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          c[u][j] = 0;
+          v[u][j] = 0.0;
+        }
+      }
+    }
+    double xv[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xv[u][j] = x[c[u][j]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) put4(q0 + (int64_t)u * 1024, v[u], xv[u]);
+  }
+  for (int64_t q = q0 + (int64_t)U * 1024; q < e; q += 1024) {
+    int c[4];
+    double v[4];
+    load4(q, c, v);
+    double xv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] = x[c[j]];
+    put4(q, v, xv);
+  }
+  __syncthreads();
+  const int64_t r = r0 + threadIdx.x;
+  if (r < r1) {
+    double s = 0.0;
+    for (int64_t k = rp[r] - a, kend = rp[r + 1] - a; k < kend; ++k) s += prod[k];
+    if (EPI == 2)
+      y[r] = b[r] - s;
+    else
+      y[r] = x[r] + omega * dinv[r] * (b[r] - s);
+  }
+}
+
 __global__ void k_amg_inv(int64_t n, const double* __restrict__ diag, const uint8_t* __restrict__ in,
                           double* __restrict__ dinv)
 {
@@ -581,6 +700,10 @@ struct Amg {
   // steps preconditioned by the cycle below (K-cycle) instead of one cycle
   int kcycle = 0;
   bool fine_planned = true;
+  // AFEM_AMG_F32 (one rank): the fine level's cycle products on an fp32 copy of
+  // its values (k_amg_f32, epilogues fused); f32_seg: the largest 256-row segment
+  DevBuf<float> v32;
+  int64_t f32_seg = 0;
   // several ranks: the communicator of the distributed levels (null on one rank)
   Comm* comm = nullptr;
   DevBuf<double> sums;  // all-reduced scalars (power iterations, K-cycle steps)
@@ -692,6 +815,30 @@ void spmv(Ctx& ctx, int epi, AmgLevel& L, const double* x, double* y, const doub
 void halo(Ctx& ctx, AmgLevel& L, double* x)
 {
   if (L.dist && L.H) halo_exchange(*L.H, ctx, x);
+}
+
+// the fine level's cycle product on the fp32 values with its epilogue (k_amg_f32)
+void f32_product(Ctx& ctx, Amg& a, AmgLevel& L, int epi, const double* x, const double* b, double* y)
+{
+  if (L.n == 0) return;
+  const unsigned nb = (unsigned)((L.n + 255) / 256);
+  const size_t shm = (size_t)a.f32_seg * 8 + 32;
+  if (epi == 2)
+    hipLaunchKernelGGL(k_amg_f32<2>, dim3(nb), dim3(256), shm, ctx.stream, L.n, L.nnz, L.rp, L.ci,
+                       (const float*)a.v32.p, x, b, (const double*)L.dinv.p, L.omega, y);
+  else
+    hipLaunchKernelGGL(k_amg_f32<1>, dim3(nb), dim3(256), shm, ctx.stream, L.n, L.nnz, L.rp, L.ci,
+                       (const float*)a.v32.p, x, b, (const double*)L.dinv.p, L.omega, y);
+  AFEM_LAUNCHED();
+}
+
+// the fp32 copy of the fine level's values (setup, and every reuse of a kept hierarchy)
+void f32_refresh(Ctx& ctx, Amg& a, const AmgLevel& L)
+{
+  if (!a.v32.p || L.nnz == 0) return;
+  hipLaunchKernelGGL(k_amg_d2f, dim3((unsigned)std::min<int64_t>(kVec, (L.nnz + 255) / 256)), dim3(256), 0,
+                     ctx.stream, L.nnz, L.v, a.v32.p);
+  AFEM_LAUNCHED();
 }
 
 double power_lambda(Ctx& ctx, Amg& a, AmgLevel& L)
@@ -1254,7 +1401,11 @@ void smooth(Ctx& ctx, Amg& a, AmgLevel& L, const double* b, int sweeps, bool fro
   }
   for (; s < sweeps; ++s) {
     halo(ctx, L, L.x.p);
-    if (fine) {
+    if (fine && a.v32.p) {
+      f32_product(ctx, a, L, 1, L.x.p, b, L.t.p);
+      std::swap(L.x, L.t);
+    }
+    else if (fine) {
       ls_spmv_planned(*fine, L.x.p, L.t.p);
       hipLaunchKernelGGL(k_amg_jacobi, dim3(g), dim3(256), 0, ctx.stream, L.n, L.omega, L.dinv.p, b, L.t.p, L.x.p);
       AFEM_LAUNCHED();
@@ -1298,7 +1449,10 @@ void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
   }
   smooth(ctx, a, L, b, a.sweeps, true, fine);
   halo(ctx, L, L.x.p);
-  if (fine) {
+  if (fine && a.v32.p) {
+    f32_product(ctx, a, L, 2, L.x.p, b, L.r.p);
+  }
+  else if (fine) {
     ls_spmv_planned(*fine, L.x.p, L.t.p);
     const unsigned gv = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
     hipLaunchKernelGGL(k_amg_resid, dim3(gv), dim3(256), 0, ctx.stream, L.n, b, L.t.p, L.r.p);
@@ -1393,8 +1547,10 @@ bool amg_setup(LinearSystem& ls)
   // amg-reuse: the same CSR arrays at the same sizes (every entry point that
   // installs or rebuilds a matrix also drops ls.amg, capi.cpp / elastodynamics.cpp)
   if (ls.opts.amg == 2 && ls.amg && ls.amg->key_rows == ls.csr_rows && ls.amg->key_cols == ls.csr_cols &&
-      ls.amg->key_vals == ls.csr_vals && ls.amg->key_n == ls.n_rows && ls.amg->key_nnz == ls.csr_nnz)
+      ls.amg->key_vals == ls.csr_vals && ls.amg->key_n == ls.n_rows && ls.amg->key_nnz == ls.csr_nnz) {
+    f32_refresh(ctx, *ls.amg, ls.amg->lv[0]);  // the fine products follow the live values, as the fp64 ones do
     return false;
+  }
   auto a = std::unique_ptr<Amg, AmgDeleter>(new Amg());
   a->partial.alloc(kVec);
   a->sums.alloc(8);
@@ -1430,6 +1586,24 @@ bool amg_setup(LinearSystem& ls)
     L.H = dist ? ls.halo.get() : nullptr;
     level_prepare(ctx, L, ls.cons.p);
     a->lv.push_back(std::move(L));
+  }
+  // AFEM_AMG_F32 (default 1; one rank, 16-B aligned CSR arrays, 256-row segments within 64 KB of LDS)
+  if (!dist && env_double("AFEM_AMG_F32", 1.0) != 0.0 && ls.csr_nnz >= 4 && ((uintptr_t)ls.csr_cols & 15) == 0 &&
+      ((uintptr_t)ls.csr_vals & 15) == 0) {
+    DevBuf<unsigned long long> mx;
+    mx.alloc(1);
+    AFEM_HIP(hipMemsetAsync(mx.p, 0, mx.bytes(), ctx.stream));
+    const int64_t nb = (ls.n_rows + 255) / 256;
+    hipLaunchKernelGGL(k_amg_seg256, dim3(grid_for(nb, 256)), dim3(256), 0, ctx.stream, ls.n_rows, ls.csr_rows, mx.p);
+    AFEM_LAUNCHED();
+    unsigned long long hm = 0;
+    AFEM_HIP(hipMemcpyAsync(&hm, mx.p, sizeof(hm), hipMemcpyDeviceToHost, ctx.stream));
+    ctx.sync();
+    if (hm * 8 + 32 <= 64 * 1024) {
+      a->f32_seg = (int64_t)hm;
+      a->v32.alloc(ls.csr_nnz);
+      f32_refresh(ctx, *a, a->lv[0]);
+    }
   }
   const bool verbose = env_double("AFEM_AMG_VERBOSE", 0.0) > 0;
   // AFEM_AMG_VERBOSE: wall time of the setup phases (the device drained at each mark)
