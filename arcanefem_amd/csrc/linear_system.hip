@@ -740,6 +740,116 @@ __global__ __launch_bounds__(256) void k_spmv_blk(int64_t n_brows, const int64_t
   }
 }
 
+// The block-3 product on an fp32 copy of the values in a private layout
+// (multigrid smoothing and residual on the fine level, AFEM_MG_F32): block q's
+// row a is one 16-B word vf[4 (3 q + a) ..] = {v_a0, v_a1, v_a2, 0}, so a lane
+// reads its block with three 16-B loads (the fp64 CSR order takes nine 8-B
+// loads; a first fp32 version in the CSR order, nine 4-B loads per block, was
+// slower than fp64 -- r05, the loads' count, not their bytes, set its rate).
+// 52 instead of 76 B per block.  Same lanes, reduction and epilogues as
+// k_spmv_blk<3, false, EPI>; products and sums in fp64.
+template <int EPI>
+__global__ __launch_bounds__(256) void k_spmv_blk3f(int64_t n_brows, const int64_t* __restrict__ bp,
+                                                    const int32_t* __restrict__ bc, const float4* __restrict__ vf,
+                                                    const double* __restrict__ x, double* __restrict__ y,
+                                                    const double* __restrict__ b, const double* __restrict__ dinv,
+                                                    double omega)
+{
+  constexpr int K = 3;
+  const int l16 = threadIdx.x & 15;
+  const int64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t r0 = ((blk * 256 + threadIdx.x) >> 4) * kBlkRpg;
+  int64_t b0[kBlkRpg];
+  int len[kBlkRpg];
+#pragma unroll
+  for (int i = 0; i < kBlkRpg; ++i) {
+    const int64_t r = r0 + i < n_brows ? r0 + i : n_brows - 1;
+    b0[i] = bp[r];
+    len[i] = r0 + i < n_brows ? (int)(bp[r + 1] - b0[i]) : 0;
+  }
+  double s[kBlkRpg][K];
+  {
+    int32_t c[kBlkRpg];
+    float4 v[kBlkRpg][K];
+#pragma unroll
+    for (int i = 0; i < kBlkRpg; ++i) {
+      const bool in = l16 < len[i];
+      const int64_t q = in ? b0[i] + l16 : 0;
+      c[i] = in ? bc[q] : 0;
+#pragma unroll
+      for (int a = 0; a < K; ++a) v[i][a] = vf[3 * q + a];
+      if (!in) {
+#pragma unroll
+        for (int a = 0; a < K; ++a) v[i][a] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kBlkRpg; ++i) {
+      double xv[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) xv[j] = x[K * (int64_t)c[i] + j];
+#pragma unroll
+      for (int a = 0; a < K; ++a) {
+        double t = (double)v[i][a].x * xv[0];
+        t = fma((double)v[i][a].y, xv[1], t);
+        t = fma((double)v[i][a].z, xv[2], t);
+        s[i][a] = t;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kBlkRpg; ++i)
+    for (int t = l16 + 16; t < len[i]; t += 16) {
+      const int64_t q = b0[i] + t;
+      const int64_t cb = K * (int64_t)bc[q];
+#pragma unroll
+      for (int a = 0; a < K; ++a) {
+        const float4 w = vf[3 * q + a];
+        double u = s[i][a];
+        u = fma((double)w.x, x[cb], u);
+        u = fma((double)w.y, x[cb + 1], u);
+        u = fma((double)w.z, x[cb + 2], u);
+        s[i][a] = u;
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < kBlkRpg; ++i)
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) s[i][a] += __shfl_xor(s[i][a], o, 16);
+  if (l16 < K * kBlkRpg) {
+    double si = s[0][0];
+#pragma unroll
+    for (int q = 1; q < K * kBlkRpg; ++q)
+      if (l16 == q) si = s[q / K][q % K];
+    const int64_t r = K * r0 + l16;
+    if (r < K * n_brows) {
+      if constexpr (EPI == 1) y[r] = x[r] + omega * dinv[r] * (b[r] - si);
+      else if constexpr (EPI == 2) y[r] = b[r] - si;
+      else y[r] = si;
+    }
+  }
+}
+
+// the private fp32 layout from BSRFormat's CSR order (16 lanes per node row, lane t:
+// blocks t, t + 16, ...)
+__global__ __launch_bounds__(256) void k_blk3_to_f32(int64_t n_brows, const int64_t* __restrict__ bp,
+                                                     const double* __restrict__ vals, float4* __restrict__ vf)
+{
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int l16 = threadIdx.x & 15;
+  if (r >= n_brows) return;
+  const int64_t b0 = bp[r];
+  const int len = (int)(bp[r + 1] - b0);
+  for (int t = l16; t < len; t += 16) {
+    const double* vr = vals + 9 * b0 + 3 * t;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+      vf[3 * (b0 + t) + a] = make_float4((float)vr[3 * a * len], (float)vr[3 * a * len + 1], (float)vr[3 * a * len + 2], 0.f);
+  }
+}
+
 // Fallback for segments that do not fit LDS: one lane per row.
 template <bool DOT>
 __global__ __launch_bounds__(kThreads) void k_spmv_row(int64_t n_rows, const int64_t* __restrict__ rows,
@@ -1495,6 +1605,29 @@ SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows, const int32_t*
 }
 
 }  // namespace
+
+void spmv_blk3f_epi(Ctx& ctx, int epi, int64_t n_brows, const int64_t* bp, const int32_t* bc, const float* vf,
+                    const double* x, double* y, const double* b, const double* dinv, double omega)
+{
+  const unsigned nb = (unsigned)((n_brows + 16 * kBlkRpg - 1) / (16 * kBlkRpg));
+  if (nb == 0) return;
+  const float4* v4 = reinterpret_cast<const float4*>(vf);
+  if (epi == 1)
+    hipLaunchKernelGGL(k_spmv_blk3f<1>, dim3(nb), dim3(256), 0, ctx.stream, n_brows, bp, bc, v4, x, y, b, dinv, omega);
+  else if (epi == 2)
+    hipLaunchKernelGGL(k_spmv_blk3f<2>, dim3(nb), dim3(256), 0, ctx.stream, n_brows, bp, bc, v4, x, y, b, dinv, omega);
+  else
+    hipLaunchKernelGGL(k_spmv_blk3f<0>, dim3(nb), dim3(256), 0, ctx.stream, n_brows, bp, bc, v4, x, y, b, dinv, omega);
+  AFEM_LAUNCHED();
+}
+
+void blk3_to_f32(Ctx& ctx, int64_t n_brows, const int64_t* bp, const double* vals, float* vf)
+{
+  if (n_brows <= 0) return;
+  hipLaunchKernelGGL(k_blk3_to_f32, dim3(grid_for(n_brows * 16, 256)), dim3(256), 0, ctx.stream, n_brows, bp, vals,
+                     reinterpret_cast<float4*>(vf));
+  AFEM_LAUNCHED();
+}
 
 void spmv_blk_epi(Ctx& ctx, int k, int epi, int64_t n_brows, const int64_t* bp, const int32_t* bc, const double* vals,
                   const double* x, double* y, const double* b, const double* dinv, double omega)

@@ -655,6 +655,10 @@ struct Multigrid {
   DevBuf<double> ainv;  // dense inverse of the coarsest level (n_dense x n_dense) or empty
   int n_dense = 0;
   DevBuf<double> partial;
+  // AFEM_MG_F32 (block-3 systems): the fine level's smoothing and residual products on
+  // an fp32 copy of its values in k_spmv_blk3f's layout (12 floats per block), refreshed
+  // at every solve; the PCG's own product stays fp64
+  DevBuf<float> v32;
   // reuse key (multigrid = 2): the fine structure the hierarchy was built for
   const void* key_rows = nullptr;
   const void* key_vals = nullptr;
@@ -1072,8 +1076,14 @@ void mg_setup(LinearSystem& ls)
   AFEM_REQUIRE(mg_available(ls), AFEM_ERR_STATE, "multigrid: not a structured box / z-slab system");
   const bool reuse = ls.opts.multigrid == 2;
   const void* krows = ls.mg_k == 1 ? (const void*)ls.csr_rows : (const void*)ls.blk_rows;
-  if (reuse && ls.mg && ls.mg->key_rows == krows && ls.mg->key_vals == ls.csr_vals && ls.mg->key_n == ls.n_rows)
+  if (reuse && ls.mg && ls.mg->key_rows == krows && ls.mg->key_vals == ls.csr_vals && ls.mg->key_n == ls.n_rows) {
+    // the fine products follow the live values (re-assembled in place every C5 step), as the fp64 ones do
+    if (ls.mg->v32.p) {
+      const MgLevel& L0 = ls.mg->lv[0];
+      blk3_to_f32(ctx, L0.nn, L0.bp, L0.v, ls.mg->v32.p);
+    }
     return;
+  }
   auto mg = std::unique_ptr<Multigrid, MgDeleter>(new Multigrid());
   const int k = ls.mg_k;
   mg->k = k;
@@ -1259,6 +1269,18 @@ void mg_setup(LinearSystem& ls)
   mg->key_rows = krows;
   mg->key_vals = ls.csr_vals;
   mg->key_n = ls.n_rows;
+  // AFEM_MG_F32 (default 1): block-3 systems' fine smoothing / residual products in fp32
+  if (k == 3 && !mg->lv.empty()) {
+    const char* fe = variant("AFEM_MG_F32");
+    const MgLevel& L0 = mg->lv[0];
+    if (!(fe && atoi(fe) == 0) && L0.nn > 0 && L0.v) {
+      int64_t nnzb = 0;
+      AFEM_HIP(hipMemcpyAsync(&nnzb, L0.bp + L0.nn, sizeof(int64_t), hipMemcpyDeviceToHost, ctx.stream));
+      ctx.sync();
+      mg->v32.alloc((size_t)(12 * (nnzb > 0 ? nnzb : 1)));
+      blk3_to_f32(ctx, L0.nn, L0.bp, L0.v, mg->v32.p);
+    }
+  }
   ls.mg = std::move(mg);
 }
 
@@ -1266,6 +1288,16 @@ namespace {
 
 // `sweeps` damped-Jacobi sweeps on level L from x = 0 (first sweep: omega D^-1 b)
 // or from the current iterate; the result is left in L.x
+// a product with its epilogue on level L: the fine level on the fp32 copy when there is one
+void level_product(Ctx& ctx, Multigrid& mg, MgLevel& L, int epi, const double* x, double* y, const double* b,
+                   const double* dinv, double omega)
+{
+  if (mg.v32.p && &L == &mg.lv[0])
+    spmv_blk3f_epi(ctx, epi, L.nn, L.bp, L.bc, mg.v32.p, x, y, b, dinv, omega);
+  else
+    spmv_blk_epi(ctx, mg.k, epi, L.nn, L.bp, L.bc, L.v, x, y, b, dinv, omega);
+}
+
 void smooth(Ctx& ctx, Multigrid& mg, MgLevel& L, const double* b, int sweeps, bool from_zero)
 {
   const unsigned g = (unsigned)std::min<int64_t>(kVec, (L.n + 255) / 256);
@@ -1276,7 +1308,7 @@ void smooth(Ctx& ctx, Multigrid& mg, MgLevel& L, const double* b, int sweeps, bo
     s = 1;
   }
   for (; s < sweeps; ++s) {
-    spmv_blk_epi(ctx, mg.k, 1, L.nn, L.bp, L.bc, L.v, L.x.p, L.t.p, b, L.dinv, L.omega);
+    level_product(ctx, mg, L, 1, L.x.p, L.t.p, b, L.dinv, L.omega);
     std::swap(L.x, L.t);
   }
 }
@@ -1298,7 +1330,7 @@ void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
   }
   MgLevel& C = mg.lv[l + 1];
   smooth(ctx, mg, L, b, mg.sweeps, true);
-  spmv_blk_epi(ctx, mg.k, 2, L.nn, L.bp, L.bc, L.v, L.x.p, L.r.p, b, nullptr, 0.0);
+  level_product(ctx, mg, L, 2, L.x.p, L.r.p, b, nullptr, 0.0);
   dispatch_k(mg.k, [&](auto kc) {
     constexpr int K = decltype(kc)::value;
     hipLaunchKernelGGL(k_mg_restrict<K>, dim3((unsigned)grid_for(C.nn, 256)), dim3(256), 0, ctx.stream, L.d, C.d,
@@ -1367,7 +1399,7 @@ void vcycle_dist(LinearSystem& ls, Multigrid& mg, size_t l, const double* b)
   if (last) return;  // coarsest level, distributed: smoothing only (the one-rank counts)
   MgLevel& C = mg.lv[l + 1];
   halo_exchange(H, ctx, L.x.p);
-  spmv_blk_epi(ctx, mg.k, 2, L.nn, L.bp, L.bc, L.v, L.x.p, L.r.p, b, nullptr, 0.0);
+  level_product(ctx, mg, L, 2, L.x.p, L.r.p, b, nullptr, 0.0);
   if (C.dist) {
     halo_exchange(H, ctx, L.r.p);
     dispatch_k(mg.k, [&](auto kc) {
