@@ -629,6 +629,7 @@ struct MgLevel {
   DevBuf<int32_t> own_bc;
   DevBuf<double> own_v, own_dinv;
   DevBuf<double> x, t, b, r;  // iterate (ping-pong x / t), right-hand side, residual
+  DevBuf<float> v32;          // AFEM_MG_F32: the values in k_spmv_blk3f's layout (block-3 levels)
   DevBuf<double> kc1, kv1, krt, kcoef;  // K-cycle level (AFEM_MG_KCYCLE)
   double omega = 0.0;
   // a distributed level (global V-cycle over z-slabs): the slab's owned rows in
@@ -655,10 +656,6 @@ struct Multigrid {
   DevBuf<double> ainv;  // dense inverse of the coarsest level (n_dense x n_dense) or empty
   int n_dense = 0;
   DevBuf<double> partial;
-  // AFEM_MG_F32 (block-3 systems): the fine level's smoothing and residual products on
-  // an fp32 copy of its values in k_spmv_blk3f's layout (12 floats per block), refreshed
-  // at every solve; the PCG's own product stays fp64
-  DevBuf<float> v32;
   // reuse key (multigrid = 2): the fine structure the hierarchy was built for
   const void* key_rows = nullptr;
   const void* key_vals = nullptr;
@@ -1078,10 +1075,8 @@ void mg_setup(LinearSystem& ls)
   const void* krows = ls.mg_k == 1 ? (const void*)ls.csr_rows : (const void*)ls.blk_rows;
   if (reuse && ls.mg && ls.mg->key_rows == krows && ls.mg->key_vals == ls.csr_vals && ls.mg->key_n == ls.n_rows) {
     // the fine products follow the live values (re-assembled in place every C5 step), as the fp64 ones do
-    if (ls.mg->v32.p) {
-      const MgLevel& L0 = ls.mg->lv[0];
-      blk3_to_f32(ctx, L0.nn, L0.bp, L0.v, ls.mg->v32.p);
-    }
+    MgLevel& L0 = ls.mg->lv[0];
+    if (L0.v32.p) blk3_to_f32(ctx, L0.nn, L0.bp, L0.v, L0.v32.p);
     return;
   }
   auto mg = std::unique_ptr<Multigrid, MgDeleter>(new Multigrid());
@@ -1269,16 +1264,22 @@ void mg_setup(LinearSystem& ls)
   mg->key_rows = krows;
   mg->key_vals = ls.csr_vals;
   mg->key_n = ls.n_rows;
-  // AFEM_MG_F32 (default 1): block-3 systems' fine smoothing / residual products in fp32
-  if (k == 3 && !mg->lv.empty()) {
+  // AFEM_MG_F32 (default 1): block-3 systems' cycle products (smoothing sweeps and residuals,
+  // not the PCG's own product) on fp32 copies of the levels' values in k_spmv_blk3f's layout
+  // (12 floats per block); the fine copy is refreshed at every solve (its values are
+  // re-assembled in place), the coarse operators are fixed with the hierarchy.  =1 the fine
+  // level only, =2 (default) every level
+  if (k == 3) {
     const char* fe = variant("AFEM_MG_F32");
-    const MgLevel& L0 = mg->lv[0];
-    if (!(fe && atoi(fe) == 0) && L0.nn > 0 && L0.v) {
+    const int f32 = fe ? atoi(fe) : 2;
+    for (size_t l = 0; l < mg->lv.size() && f32 > 0; ++l) {
+      MgLevel& L = mg->lv[l];
+      if ((l > 0 && f32 < 2) || L.nn <= 0 || !L.v) continue;
       int64_t nnzb = 0;
-      AFEM_HIP(hipMemcpyAsync(&nnzb, L0.bp + L0.nn, sizeof(int64_t), hipMemcpyDeviceToHost, ctx.stream));
+      AFEM_HIP(hipMemcpyAsync(&nnzb, L.bp + L.nn, sizeof(int64_t), hipMemcpyDeviceToHost, ctx.stream));
       ctx.sync();
-      mg->v32.alloc((size_t)(12 * (nnzb > 0 ? nnzb : 1)));
-      blk3_to_f32(ctx, L0.nn, L0.bp, L0.v, mg->v32.p);
+      L.v32.alloc((size_t)(12 * (nnzb > 0 ? nnzb : 1)));
+      blk3_to_f32(ctx, L.nn, L.bp, L.v, L.v32.p);
     }
   }
   ls.mg = std::move(mg);
@@ -1288,12 +1289,12 @@ namespace {
 
 // `sweeps` damped-Jacobi sweeps on level L from x = 0 (first sweep: omega D^-1 b)
 // or from the current iterate; the result is left in L.x
-// a product with its epilogue on level L: the fine level on the fp32 copy when there is one
+// a product with its epilogue on level L: on the level's fp32 copy when it has one
 void level_product(Ctx& ctx, Multigrid& mg, MgLevel& L, int epi, const double* x, double* y, const double* b,
                    const double* dinv, double omega)
 {
-  if (mg.v32.p && &L == &mg.lv[0])
-    spmv_blk3f_epi(ctx, epi, L.nn, L.bp, L.bc, mg.v32.p, x, y, b, dinv, omega);
+  if (L.v32.p)
+    spmv_blk3f_epi(ctx, epi, L.nn, L.bp, L.bc, L.v32.p, x, y, b, dinv, omega);
   else
     spmv_blk_epi(ctx, mg.k, epi, L.nn, L.bp, L.bc, L.v, x, y, b, dinv, omega);
 }
