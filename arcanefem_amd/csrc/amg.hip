@@ -312,10 +312,14 @@ __global__ void k_amg_member_ptr(int64_t n, const uint32_t* __restrict__ key, in
 }
 
 // y = A x (EPI 0), y = x + omega dinv (b - A x) (EPI 1), y = b - A x (EPI 2);
-// 8 lanes per row, the row's products summed in a fixed butterfly order
-template <int EPI>
+// 8 lanes per row, the row's products summed in a fixed butterfly order.  A
+// lane's entries k, k + 8, ... four at a time: their columns and values, then
+// the gathers, all in flight together (the sum in the same order as one entry
+// at a time, bit for bit).  VT float: a level's fp32 copy of its values
+// (AFEM_AMG_F32 = 2, the coarse levels)
+template <int EPI, typename VT>
 __global__ __launch_bounds__(256) void k_amg_spmv(int64_t n, const int64_t* __restrict__ rp,
-                                                  const int32_t* __restrict__ ci, const double* __restrict__ v,
+                                                  const int32_t* __restrict__ ci, const VT* __restrict__ v,
                                                   const double* __restrict__ x, double* __restrict__ y,
                                                   const double* __restrict__ b, const double* __restrict__ dinv,
                                                   double omega)
@@ -323,8 +327,25 @@ __global__ __launch_bounds__(256) void k_amg_spmv(int64_t n, const int64_t* __re
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
   const int l = threadIdx.x & 7;
   double s = 0.0;
-  if (i < n)
-    for (int64_t k = rp[i] + l; k < rp[i + 1]; k += 8) s += v[k] * x[ci[k]];
+  if (i < n) {
+    const int64_t k1 = rp[i + 1];
+    for (int64_t kb = rp[i] + l; kb < k1; kb += 32) {
+      int32_t c[4];
+      VT w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t k = kb + 8 * u;
+        c[u] = k < k1 ? ci[k] : 0;
+        w[u] = k < k1 ? v[k] : VT(0);
+      }
+      double xv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xv[u] = x[c[u]];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (kb + 8 * u < k1) s += (double)w[u] * xv[u];
+    }
+  }
   s += __shfl_xor(s, 1, 8);
   s += __shfl_xor(s, 2, 8);
   s += __shfl_xor(s, 4, 8);
@@ -687,6 +708,7 @@ struct AmgLevel {
   DevBuf<int32_t> mem;
   DevBuf<double> x, t, b, r;
   DevBuf<double> kc1, kv1, krt, kcoef;  // K-cycle level (Amg::kcycle)
+  DevBuf<float> v32;                    // AFEM_AMG_F32 = 2: a coarse level's values in fp32 (its cycle products)
   double omega = 0.0;
 };
 
@@ -795,19 +817,30 @@ std::vector<double> allsum_vec(Ctx& ctx, Amg& a, std::vector<double> h)
   return h;
 }
 
-void spmv(Ctx& ctx, int epi, AmgLevel& L, const double* x, double* y, const double* b, double omega)
+void spmv(Ctx& ctx, int epi, AmgLevel& L, const double* x, double* y, const double* b, double omega,
+          bool exact = false)
 {
   const unsigned g = grid_for(L.n * 8, 256);
   if (L.n == 0) return;
-  if (epi == 0)
-    hipLaunchKernelGGL(k_amg_spmv<0>, dim3(g), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci, L.v, x, y, b, L.dinv.p,
-                       omega);
-  else if (epi == 1)
-    hipLaunchKernelGGL(k_amg_spmv<1>, dim3(g), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci, L.v, x, y, b, L.dinv.p,
-                       omega);
-  else
-    hipLaunchKernelGGL(k_amg_spmv<2>, dim3(g), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci, L.v, x, y, b, L.dinv.p,
-                       omega);
+  // exact: the products that must be the level's operator itself (power iteration, K-cycle Krylov steps)
+  const float* vf = exact ? nullptr : L.v32.p;
+#define AFEM_AMG_SPMV(E)                                                                                         \
+  if (vf)                                                                                                        \
+    hipLaunchKernelGGL((k_amg_spmv<E, float>), dim3(g), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci, vf, x, y, b,   \
+                       L.dinv.p, omega);                                                                          \
+  else                                                                                                           \
+    hipLaunchKernelGGL((k_amg_spmv<E, double>), dim3(g), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci, L.v, x, y, b, \
+                       L.dinv.p, omega);
+  if (epi == 0) {
+    AFEM_AMG_SPMV(0)
+  }
+  else if (epi == 1) {
+    AFEM_AMG_SPMV(1)
+  }
+  else {
+    AFEM_AMG_SPMV(2)
+  }
+#undef AFEM_AMG_SPMV
   AFEM_LAUNCHED();
 }
 
@@ -1587,8 +1620,8 @@ bool amg_setup(LinearSystem& ls)
     level_prepare(ctx, L, ls.cons.p);
     a->lv.push_back(std::move(L));
   }
-  // AFEM_AMG_F32 (default 1; one rank, 16-B aligned CSR arrays, 256-row segments within 64 KB of LDS)
-  if (!dist && env_double("AFEM_AMG_F32", 1.0) != 0.0 && ls.csr_nnz >= 4 && ((uintptr_t)ls.csr_cols & 15) == 0 &&
+  // AFEM_AMG_F32 (>= 1, default 2; one rank, 16-B aligned CSR arrays, 256-row segments within 64 KB of LDS)
+  if (!dist && env_double("AFEM_AMG_F32", 2.0) >= 1.0 && ls.csr_nnz >= 4 && ((uintptr_t)ls.csr_cols & 15) == 0 &&
       ((uintptr_t)ls.csr_vals & 15) == 0) {
     DevBuf<unsigned long long> mx;
     mx.alloc(1);
@@ -1692,6 +1725,18 @@ bool amg_setup(LinearSystem& ls)
     L.kv1.alloc(L.n > 0 ? L.n : 1);
     L.krt.alloc(L.n > 0 ? L.n : 1);
     L.kcoef.alloc(8);
+  }
+  // AFEM_AMG_F32 = 2 (the default): the coarse levels' cycle and K-cycle products on fp32
+  // copies of their values (fixed with the hierarchy; the power iterations above ran on fp64)
+  if (env_double("AFEM_AMG_F32", 2.0) >= 2.0) {
+    for (size_t l = 1; l < a->lv.size(); ++l) {
+      AmgLevel& L = a->lv[l];
+      if (L.nnz <= 0 || !L.v) continue;
+      L.v32.alloc(L.nnz);
+      hipLaunchKernelGGL(k_amg_d2f, dim3((unsigned)std::min<int64_t>(kVec, (L.nnz + 255) / 256)), dim3(256), 0,
+                         ctx.stream, L.nnz, L.v, L.v32.p);
+      AFEM_LAUNCHED();
+    }
   }
   mark("dense coarsest, K-cycle buffers");
   a->key_rows = ls.csr_rows;
