@@ -645,10 +645,11 @@ __global__ void k_amg_keys_map(int64_t n, const int64_t* __restrict__ rp, const 
                                const int32_t* __restrict__ agg, int64_t row_base, const int32_t* __restrict__ cmap,
                                int64_t ncol, int cbits, unsigned long long* __restrict__ key)
 {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // 8 lanes per row (the row's columns read and its keys written coalesced)
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
   if (i >= n) return;
   const int32_t ai = agg[i];
-  for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+  for (int64_t k = rp[i] + (threadIdx.x & 7); k < rp[i + 1]; k += 8) {
     const int32_t j = ci[k];
     const int32_t aj = (j >= 0 && j < ncol) ? cmap[j] : -1;
     key[k] = (ai >= 0 && aj >= 0) ? ((unsigned long long)(row_base + ai) << cbits | (uint32_t)aj) : ~0ull;
@@ -1104,7 +1105,7 @@ int64_t galerkin_coo(Ctx& ctx, AmgLevel& L, const int32_t* cmap, int64_t ncol, i
   key_s.alloc(nnz > 0 ? nnz : 1);
   val_s.alloc(nnz > 0 ? nnz : 1);
   if (L.n > 0) {
-    hipLaunchKernelGGL(k_amg_keys_map, dim3(grid_for(L.n, 256)), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci,
+    hipLaunchKernelGGL(k_amg_keys_map, dim3(grid_for(L.n * 8, 256)), dim3(256), 0, ctx.stream, L.n, L.rp, L.ci,
                        (const int32_t*)L.agg.p, row_base, cmap, ncol, cbits, key.p);
     AFEM_LAUNCHED();
   }
