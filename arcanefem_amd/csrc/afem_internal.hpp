@@ -526,7 +526,8 @@ void spmv_blk_epi(Ctx& ctx, int k, int epi, int64_t n_brows, const int64_t* bp, 
                   const double* x, double* y, const double* b, const double* dinv, double omega);
 // the block-3 product on the private fp32 layout (k_spmv_blk3f) and that layout from the CSR order
 void spmv_blk3f_epi(Ctx& ctx, int epi, int64_t n_brows, const int64_t* bp, const int32_t* bc, const float* vf,
-                    const double* x, double* y, const double* b, const double* dinv, double omega);
+                    const double* x, double* y, const double* b, const double* dinv, double omega,
+                    const uint8_t* cons = nullptr, const double* rin = nullptr, const double* dfix = nullptr);
 void blk3_to_f32(Ctx& ctx, int64_t n_brows, const int64_t* bp, const double* vals, float* vf);
 void ls_apply_bcs(LinearSystem& ls);
 void ls_set_csr_mapped(LinearSystem& ls, const int32_t* rows, const int32_t* columns, double* values, int32_t nb_row,

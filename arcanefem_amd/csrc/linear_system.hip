@@ -747,13 +747,18 @@ __global__ __launch_bounds__(256) void k_spmv_blk(int64_t n_brows, const int64_t
 // loads; a first fp32 version in the CSR order, nine 4-B loads per block, was
 // slower than fp64 -- r05, the loads' count, not their bytes, set its rate).
 // 52 instead of 76 B per block.  Same lanes, reduction and epilogues as
-// k_spmv_blk<3, false, EPI>; products and sums in fp64.
+// k_spmv_blk<3, false, EPI>; products and sums in fp64.  EPI 3: the multigrid
+// preconditioner's last sweep written straight into z with its constraint rows
+// (z = x + omega dinv (b - A x), constraint rows rin dfix: mg_apply's copy and
+// k_mg_fix folded in)
 template <int EPI>
 __global__ __launch_bounds__(256) void k_spmv_blk3f(int64_t n_brows, const int64_t* __restrict__ bp,
                                                     const int32_t* __restrict__ bc, const float4* __restrict__ vf,
                                                     const double* __restrict__ x, double* __restrict__ y,
                                                     const double* __restrict__ b, const double* __restrict__ dinv,
-                                                    double omega)
+                                                    double omega, const uint8_t* __restrict__ cons = nullptr,
+                                                    const double* __restrict__ rin = nullptr,
+                                                    const double* __restrict__ dfix = nullptr)
 {
   constexpr int K = 3;
   const int l16 = threadIdx.x & 15;
@@ -826,6 +831,7 @@ __global__ __launch_bounds__(256) void k_spmv_blk3f(int64_t n_brows, const int64
     const int64_t r = K * r0 + l16;
     if (r < K * n_brows) {
       if constexpr (EPI == 1) y[r] = x[r] + omega * dinv[r] * (b[r] - si);
+      else if constexpr (EPI == 3) y[r] = cons[r] ? rin[r] * dfix[r] : x[r] + omega * dinv[r] * (b[r] - si);
       else if constexpr (EPI == 2) y[r] = b[r] - si;
       else y[r] = si;
     }
@@ -1607,12 +1613,16 @@ SpmvPlan plan_spmv(Ctx& ctx, const int64_t* rows, int64_t n_rows, const int32_t*
 }  // namespace
 
 void spmv_blk3f_epi(Ctx& ctx, int epi, int64_t n_brows, const int64_t* bp, const int32_t* bc, const float* vf,
-                    const double* x, double* y, const double* b, const double* dinv, double omega)
+                    const double* x, double* y, const double* b, const double* dinv, double omega,
+                    const uint8_t* cons, const double* rin, const double* dfix)
 {
   const unsigned nb = (unsigned)((n_brows + 16 * kBlkRpg - 1) / (16 * kBlkRpg));
   if (nb == 0) return;
   const float4* v4 = reinterpret_cast<const float4*>(vf);
-  if (epi == 1)
+  if (epi == 3)
+    hipLaunchKernelGGL(k_spmv_blk3f<3>, dim3(nb), dim3(256), 0, ctx.stream, n_brows, bp, bc, v4, x, y, b, dinv, omega,
+                       cons, rin, dfix);
+  else if (epi == 1)
     hipLaunchKernelGGL(k_spmv_blk3f<1>, dim3(nb), dim3(256), 0, ctx.stream, n_brows, bp, bc, v4, x, y, b, dinv, omega);
   else if (epi == 2)
     hipLaunchKernelGGL(k_spmv_blk3f<2>, dim3(nb), dim3(256), 0, ctx.stream, n_brows, bp, bc, v4, x, y, b, dinv, omega);

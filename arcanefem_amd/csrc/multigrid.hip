@@ -190,6 +190,18 @@ __global__ void k_mg_scale(int64_t n, double omega, const double* __restrict__ d
     x[i] = omega * dinv[i] * b[i];
 }
 
+// b = F r and the first sweep from zero x = omega dinv b in one pass (mg_apply's entry)
+__global__ void k_mg_mask_scale(int64_t n, const uint8_t* __restrict__ cons, const double* __restrict__ r,
+                                double omega, const double* __restrict__ dinv, double* __restrict__ b,
+                                double* __restrict__ x)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double bi = cons[i] ? 0.0 : r[i];
+    b[i] = bi;
+    x[i] = omega * dinv[i] * bi;
+  }
+}
+
 // F r (constraint rows zeroed)
 __global__ void k_mg_mask(int64_t n, const uint8_t* __restrict__ cons, const double* __restrict__ r,
                           double* __restrict__ b)
@@ -1316,9 +1328,22 @@ void smooth(Ctx& ctx, Multigrid& mg, MgLevel& L, const double* b, int sweeps, bo
 
 void kcycle(Ctx& ctx, Multigrid& mg, size_t l);
 
-void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
+// mg_apply's fused entry / exit on level 0 (one rank, block-3 fp32 copy): the first
+// sweep already done by k_mg_mask_scale; the last sweep writes z with the
+// constraint rows (k_spmv_blk3f<3>) -- done reports it
+struct MgExit {
+  double* z = nullptr;
+  const double* r = nullptr;
+  const uint8_t* cons = nullptr;
+  const double* dfix = nullptr;
+  bool x_ready = false;
+  bool done = false;
+};
+
+void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b, MgExit* ex = nullptr)
 {
   MgLevel& L = mg.lv[l];
+  if (l > 0) ex = nullptr;
   if (l + 1 == mg.lv.size()) {
     if (mg.n_dense == L.n && l > 0) {
       hipLaunchKernelGGL(k_mg_gemv, dim3((unsigned)L.n), dim3(64), 0, ctx.stream, (int)L.n, mg.ainv.p, b, L.x.p);
@@ -1330,7 +1355,10 @@ void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
     return;
   }
   MgLevel& C = mg.lv[l + 1];
-  smooth(ctx, mg, L, b, mg.sweeps, true);
+  if (ex && ex->x_ready)
+    smooth(ctx, mg, L, b, mg.sweeps - 1, false);  // (the first sweep from zero came with the mask)
+  else
+    smooth(ctx, mg, L, b, mg.sweeps, true);
   level_product(ctx, mg, L, 2, L.x.p, L.r.p, b, nullptr, 0.0);
   dispatch_k(mg.k, [&](auto kc) {
     constexpr int K = decltype(kc)::value;
@@ -1348,7 +1376,14 @@ void vcycle(Ctx& ctx, Multigrid& mg, size_t l, const double* b)
                        C.x.p, L.x.p);
     AFEM_LAUNCHED();
   });
-  smooth(ctx, mg, L, b, mg.sweeps, false);
+  if (ex && L.v32.p && mg.sweeps >= 1) {
+    smooth(ctx, mg, L, b, mg.sweeps - 1, false);
+    spmv_blk3f_epi(ctx, 3, L.nn, L.bp, L.bc, L.v32.p, L.x.p, ex->z, b, L.dinv, L.omega, ex->cons, ex->r, ex->dfix);
+    ex->done = true;
+  }
+  else {
+    smooth(ctx, mg, L, b, mg.sweeps, false);
+  }
 }
 
 // K-cycle (AFEM_MG_KCYCLE=k, one rank): level l's coarse problem (b in L.b) by
@@ -1449,15 +1484,34 @@ void mg_apply(LinearSystem& ls, const double* r, double* z)
   MgLevel& L0 = mg.lv[0];
   const unsigned g = (unsigned)std::min<int64_t>(kVec, (L0.n + 255) / 256);
   const int64_t n = ls.n_rows;  // < L0.n when the slab's box is padded
-  if (n == L0.n)
-    hipLaunchKernelGGL(k_mg_mask, dim3(g), dim3(256), 0, ctx.stream, L0.n, ls.cons.p, r, L0.b.p);
-  else
-    hipLaunchKernelGGL(k_mg_mask_pad, dim3(g), dim3(256), 0, ctx.stream, n, L0.n, ls.cons.p, r, L0.b.p);
-  AFEM_LAUNCHED();
-  if (mg.global)
-    vcycle_dist(ls, mg, 0, L0.b.p);
-  else
-    vcycle(ctx, mg, 0, L0.b.p);
+  // one rank, block-3 fp32 copy, more than one level: the entry (mask + first sweep) and the
+  // exit (last sweep into z + constraint rows) fused (AFEM_MG_FUSE=0: separate passes)
+  const char* fe = variant("AFEM_MG_FUSE");
+  const bool fuse = !mg.global && n == L0.n && L0.v32.p && mg.lv.size() > 1 && mg.sweeps >= 1 && !(fe && atoi(fe) == 0);
+  if (fuse) {
+    hipLaunchKernelGGL(k_mg_mask_scale, dim3(g), dim3(256), 0, ctx.stream, L0.n, ls.cons.p, r, L0.omega, L0.dinv,
+                       L0.b.p, L0.x.p);
+    AFEM_LAUNCHED();
+    MgExit ex;
+    ex.z = z;
+    ex.r = r;
+    ex.cons = ls.cons.p;
+    ex.dfix = ls.dinv.p;
+    ex.x_ready = true;
+    vcycle(ctx, mg, 0, L0.b.p, &ex);
+    if (ex.done) return;
+  }
+  else {
+    if (n == L0.n)
+      hipLaunchKernelGGL(k_mg_mask, dim3(g), dim3(256), 0, ctx.stream, L0.n, ls.cons.p, r, L0.b.p);
+    else
+      hipLaunchKernelGGL(k_mg_mask_pad, dim3(g), dim3(256), 0, ctx.stream, n, L0.n, ls.cons.p, r, L0.b.p);
+    AFEM_LAUNCHED();
+    if (mg.global)
+      vcycle_dist(ls, mg, 0, L0.b.p);
+    else
+      vcycle(ctx, mg, 0, L0.b.p);
+  }
   AFEM_HIP(hipMemcpyAsync(z, L0.x.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
   hipLaunchKernelGGL(k_mg_fix, dim3(g), dim3(256), 0, ctx.stream, n, ls.cons.p, r, ls.dinv.p, z);
   AFEM_LAUNCHED();
