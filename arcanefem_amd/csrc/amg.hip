@@ -384,7 +384,9 @@ __global__ void k_amg_scale(int64_t n, double omega, const double* __restrict__ 
 // 16-B loads, four groups of 4 per lane in flight, products to LDS in a rotated
 // order, one lane per row sums its products in CSR order) with the cycle's
 // epilogue fused: EPI 2 y = b - A x (the residual), EPI 1 y = x + omega dinv
-// (b - A x) (a Jacobi sweep; y must not be x).  The values are the preconditioner's
+// (b - A x) (a Jacobi sweep; y must not be x), EPI 3 the sweep written into the
+// preconditioner's output with its constraint rows (rin dfix: amg_apply's copy
+// and k_amg_fix folded in).  The values are the preconditioner's
 // only: the PCG's own product stays in fp64.  8 instead of 12 B per non-zero
 __global__ void k_amg_d2f(int64_t n, const double* __restrict__ v, float* __restrict__ f)
 {
@@ -407,7 +409,9 @@ __global__ __launch_bounds__(256) void k_amg_f32(int64_t n_rows, int64_t nnz, co
                                                  const int32_t* __restrict__ ci, const float* __restrict__ vf,
                                                  const double* __restrict__ x, const double* __restrict__ b,
                                                  const double* __restrict__ dinv, double omega,
-                                                 double* __restrict__ y)
+                                                 double* __restrict__ y, const uint8_t* __restrict__ cons = nullptr,
+                                                 const double* __restrict__ rin = nullptr,
+                                                 const double* __restrict__ dfix = nullptr)
 {
   constexpr int U = 4;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -493,6 +497,8 @@ __global__ __launch_bounds__(256) void k_amg_f32(int64_t n_rows, int64_t nnz, co
     for (int64_t k = rp[r] - a, kend = rp[r + 1] - a; k < kend; ++k) s += prod[k];
     if (EPI == 2)
       y[r] = b[r] - s;
+    else if (EPI == 3)
+      y[r] = cons[r] ? rin[r] * dfix[r] : x[r] + omega * dinv[r] * (b[r] - s);
     else
       y[r] = x[r] + omega * dinv[r] * (b[r] - s);
   }
@@ -543,6 +549,18 @@ __global__ void k_amg_mask(int64_t n, const uint8_t* __restrict__ cons, const do
 {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     b[i] = cons[i] ? 0.0 : r[i];
+}
+
+// b = F r and the first sweep from zero x = omega dinv b in one pass (amg_apply's entry)
+__global__ void k_amg_mask_scale(int64_t n, const uint8_t* __restrict__ cons, const double* __restrict__ r,
+                                 double omega, const double* __restrict__ dinv, double* __restrict__ b,
+                                 double* __restrict__ x)
+{
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double bi = cons[i] ? 0.0 : r[i];
+    b[i] = bi;
+    x[i] = omega * dinv[i] * bi;
+  }
 }
 
 __global__ void k_amg_fix(int64_t n, const uint8_t* __restrict__ cons, const double* __restrict__ r,
@@ -852,12 +870,16 @@ void halo(Ctx& ctx, AmgLevel& L, double* x)
 }
 
 // the fine level's cycle product on the fp32 values with its epilogue (k_amg_f32)
-void f32_product(Ctx& ctx, Amg& a, AmgLevel& L, int epi, const double* x, const double* b, double* y)
+void f32_product(Ctx& ctx, Amg& a, AmgLevel& L, int epi, const double* x, const double* b, double* y,
+                 const uint8_t* cons = nullptr, const double* rin = nullptr, const double* dfix = nullptr)
 {
   if (L.n == 0) return;
   const unsigned nb = (unsigned)((L.n + 255) / 256);
   const size_t shm = (size_t)a.f32_seg * 8 + 32;
-  if (epi == 2)
+  if (epi == 3)
+    hipLaunchKernelGGL(k_amg_f32<3>, dim3(nb), dim3(256), shm, ctx.stream, L.n, L.nnz, L.rp, L.ci,
+                       (const float*)a.v32.p, x, b, (const double*)L.dinv.p, L.omega, y, cons, rin, dfix);
+  else if (epi == 2)
     hipLaunchKernelGGL(k_amg_f32<2>, dim3(nb), dim3(256), shm, ctx.stream, L.n, L.nnz, L.rp, L.ci,
                        (const float*)a.v32.p, x, b, (const double*)L.dinv.p, L.omega, y);
   else
@@ -1453,10 +1475,24 @@ void smooth(Ctx& ctx, Amg& a, AmgLevel& L, const double* b, int sweeps, bool fro
 
 void kcycle(Ctx& ctx, Amg& a, size_t l);
 
-void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
+// amg_apply's fused entry / exit on level 0 (one rank, fp32 fine copy): the first
+// sweep already done by k_amg_mask_scale; the last sweep writes z with the
+// constraint rows (k_amg_f32<3>) -- done reports it
+struct AmgExit {
+  double* z = nullptr;
+  const double* r = nullptr;
+  const uint8_t* cons = nullptr;
+  const double* dfix = nullptr;
+  bool done = false;
+};
+
+void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine, AmgExit* ex = nullptr)
 {
   AmgLevel& L = a.lv[l];
-  if (l > 0) fine = nullptr;
+  if (l > 0) {
+    fine = nullptr;
+    ex = nullptr;
+  }
   if (l + 1 == a.lv.size()) {
     if (a.n_dense == L.n && L.n > 0 && !L.dist) {
       hipLaunchKernelGGL(k_amg_gemv, dim3((unsigned)L.n), dim3(64), 0, ctx.stream, (int)L.n, a.ainv.p, b, L.x.p);
@@ -1481,7 +1517,10 @@ void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
       AFEM_HIP(hipMemcpyAsync(L.x.p, C.x.p + L.gather_off, L.n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
     return;
   }
-  smooth(ctx, a, L, b, a.sweeps, true, fine);
+  if (ex)
+    smooth(ctx, a, L, b, a.sweeps - 1, false, fine);  // (the first sweep from zero came with the mask)
+  else
+    smooth(ctx, a, L, b, a.sweeps, true, fine);
   halo(ctx, L, L.x.p);
   if (fine && a.v32.p) {
     f32_product(ctx, a, L, 2, L.x.p, b, L.r.p);
@@ -1519,7 +1558,14 @@ void vcycle(Ctx& ctx, Amg& a, size_t l, const double* b, LinearSystem* fine)
                        (const double*)(C.x.p + (gathered ? L.gather_off : 0)), L.x.p);
     AFEM_LAUNCHED();
   }
-  smooth(ctx, a, L, b, a.sweeps, false, fine);
+  if (ex) {
+    smooth(ctx, a, L, b, a.sweeps - 1, false, fine);
+    f32_product(ctx, a, L, 3, L.x.p, b, ex->z, ex->cons, ex->r, ex->dfix);
+    ex->done = true;
+  }
+  else {
+    smooth(ctx, a, L, b, a.sweeps, false, fine);
+  }
 }
 
 // level l's coarse problem A x = b (b in L.b): c1 = B b, v1 = A c1, rt = b -
@@ -1795,10 +1841,28 @@ void amg_apply_launch(LinearSystem& ls, const double* r, double* z)
   AmgLevel& L0 = a.lv[0];
   const int64_t n = ls.n_rows;
   const unsigned g = (unsigned)std::min<int64_t>(kVec, (n + 255) / 256);
-  hipLaunchKernelGGL(k_amg_mask, dim3(g), dim3(256), 0, ctx.stream, n, ls.cons.p, r, L0.b.p);
-  AFEM_LAUNCHED();
-  // the fine level's products through the PCG's SpMV plan (AFEM_AMG_FINE_CSR=1: the 8-lane CSR kernel)
-  vcycle(ctx, a, 0, L0.b.p, a.fine_planned && ls.spmv_plan ? &ls : nullptr);
+  LinearSystem* fine = a.fine_planned && ls.spmv_plan ? &ls : nullptr;
+  // one rank with the fp32 fine copy and a coarse level: the entry (mask + first sweep) and the exit
+  // (last sweep into z + constraint rows) fused (AFEM_AMG_FUSE=0: separate passes)
+  if (fine && a.v32.p && a.lv.size() > 1 && !L0.dist && L0.n == n && a.sweeps >= 1 &&
+      env_double("AFEM_AMG_FUSE", 1.0) != 0.0) {
+    hipLaunchKernelGGL(k_amg_mask_scale, dim3(g), dim3(256), 0, ctx.stream, n, ls.cons.p, r, L0.omega,
+                       (const double*)L0.dinv.p, L0.b.p, L0.x.p);
+    AFEM_LAUNCHED();
+    AmgExit ex;
+    ex.z = z;
+    ex.r = r;
+    ex.cons = ls.cons.p;
+    ex.dfix = ls.dinv.p;
+    vcycle(ctx, a, 0, L0.b.p, fine, &ex);
+    if (ex.done) return;
+  }
+  else {
+    hipLaunchKernelGGL(k_amg_mask, dim3(g), dim3(256), 0, ctx.stream, n, ls.cons.p, r, L0.b.p);
+    AFEM_LAUNCHED();
+    // the fine level's products through the PCG's SpMV plan (AFEM_AMG_FINE_CSR=1: the 8-lane CSR kernel)
+    vcycle(ctx, a, 0, L0.b.p, fine);
+  }
   AFEM_HIP(hipMemcpyAsync(z, L0.x.p, n * sizeof(double), hipMemcpyDeviceToDevice, ctx.stream));
   hipLaunchKernelGGL(k_amg_fix, dim3(g), dim3(256), 0, ctx.stream, n, ls.cons.p, r, ls.dinv.p, z);
   AFEM_LAUNCHED();
