@@ -260,18 +260,28 @@ __global__ void k_amg_heads(int64_t m, const unsigned long long* __restrict__ ke
   head[k] = key[k] != ~0ull && (k == 0 || key[k] != key[k - 1]) ? 1 : 0;
 }
 
-// run r = [pos of head r, next head): its sum in the sorted (= CSR) order
-__global__ void k_amg_runs(int64_t m, const unsigned long long* __restrict__ key, const double* __restrict__ vs,
-                           const int32_t* __restrict__ head,
-                           const int64_t* __restrict__ hrank, int64_t row_base, int cbits,
-                           int64_t* __restrict__ c_row_of, int32_t* __restrict__ c_col, double* __restrict__ c_val)
+// the start of every run (heads scattered to their rank)
+__global__ void k_amg_run_starts(int64_t m, const int32_t* __restrict__ head, const int64_t* __restrict__ hrank,
+                                 int64_t* __restrict__ start)
 {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= m || !head[k]) return;
-  const unsigned long long kk = key[k];
+  if (k < m && head[k]) start[hrank[k]] = k;
+}
+
+// run r = [start r, start r+1): one thread per run, its sum in the sorted (=
+// CSR) order (a thread per key whose heads looped over their runs left ~60 of
+// 64 lanes idle: 10 ms at 172 M keys, r06aq)
+__global__ void k_amg_runs(int64_t n_runs, int64_t m, const unsigned long long* __restrict__ key,
+                           const double* __restrict__ vs, const int64_t* __restrict__ start, int64_t row_base,
+                           int cbits, int64_t* __restrict__ c_row_of, int32_t* __restrict__ c_col,
+                           double* __restrict__ c_val)
+{
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_runs) return;
+  const int64_t k0 = start[r];
+  const unsigned long long kk = key[k0];
   double s = 0.0;
-  for (int64_t q = k; q < m && key[q] == kk; ++q) s += vs[q];
-  const int64_t r = hrank[k];
+  for (int64_t q = k0; q < m && key[q] == kk; ++q) s += vs[q];
   c_row_of[r] = (int64_t)(kk >> cbits) - row_base;
   c_col[r] = (int32_t)(kk & ((1ull << cbits) - 1));
   c_val[r] = s;
@@ -495,7 +505,9 @@ __global__ __launch_bounds__(256) void k_amg_f32(int64_t n_rows, int64_t nnz, co
   if (r < r1) {
     double s = 0.0;
     for (int64_t k = rp[r] - a, kend = rp[r + 1] - a; k < kend; ++k) s += prod[k];
-    if (EPI == 2)
+    if (EPI == 0)
+      y[r] = s;
+    else if (EPI == 2)
       y[r] = b[r] - s;
     else if (EPI == 3)
       y[r] = cons[r] ? rin[r] * dfix[r] : x[r] + omega * dinv[r] * (b[r] - s);
@@ -612,7 +624,15 @@ __global__ void k_amg_pw_norm(const double* __restrict__ partial, int g, int fir
 {
   if (threadIdx.x != 0 || st[3] != 0.0) return;
   double s = 0.0;
-  for (int k = 0; k < g; ++k) s += partial[k];
+  int k = 0;
+  for (; k + 8 <= g; k += 8) {  // the loads in flight together, the adds in order
+    double p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p[u] = partial[k + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += p[u];
+  }
+  for (; k < g; ++k) s += partial[k];
   const double nw = sqrt(s);
   if (first) {
     st[0] = nw;
@@ -879,6 +899,9 @@ void f32_product(Ctx& ctx, Amg& a, AmgLevel& L, int epi, const double* x, const 
   if (epi == 3)
     hipLaunchKernelGGL(k_amg_f32<3>, dim3(nb), dim3(256), shm, ctx.stream, L.n, L.nnz, L.rp, L.ci,
                        (const float*)a.v32.p, x, b, (const double*)L.dinv.p, L.omega, y, cons, rin, dfix);
+  else if (epi == 0)
+    hipLaunchKernelGGL(k_amg_f32<0>, dim3(nb), dim3(256), shm, ctx.stream, L.n, L.nnz, L.rp, L.ci,
+                       (const float*)a.v32.p, x, b, (const double*)L.dinv.p, L.omega, y);
   else if (epi == 2)
     hipLaunchKernelGGL(k_amg_f32<2>, dim3(nb), dim3(256), shm, ctx.stream, L.n, L.nnz, L.rp, L.ci,
                        (const float*)a.v32.p, x, b, (const double*)L.dinv.p, L.omega, y);
@@ -913,8 +936,14 @@ double power_lambda(Ctx& ctx, Amg& a, AmgLevel& L)
     st.alloc(4);
     AFEM_HIP(hipMemsetAsync(st.p, 0, st.bytes(), ctx.stream));
     hipLaunchKernelGGL(k_amg_pw_norm, dim3(1), dim3(64), 0, ctx.stream, (const double*)a.partial.p, (int)g, 1, st.p);
+    // (the fine level's products on its fp32 copy when it has one: lambda_max of the fp32-rounded
+    // operator, the one the cycle's sweeps apply)
+    const bool f32 = a.v32.p && &L == &a.lv[0];
     for (int it = 0; it < kPowerIts; ++it) {
-      spmv(ctx, 0, L, L.x.p, L.t.p, nullptr, 0.0);
+      if (f32)
+        f32_product(ctx, a, L, 0, L.x.p, nullptr, L.t.p);
+      else
+        spmv(ctx, 0, L, L.x.p, L.t.p, nullptr, 0.0);
       hipLaunchKernelGGL(k_amg_dscale_dot, dim3(g), dim3(256), 0, ctx.stream, L.n, (const double*)L.dinv.p, L.t.p,
                          a.partial.p);
       hipLaunchKernelGGL(k_amg_pw_norm, dim3(1), dim3(64), 0, ctx.stream, (const double*)a.partial.p, (int)g, 0, st.p);
@@ -1154,10 +1183,14 @@ int64_t galerkin_coo(Ctx& ctx, AmgLevel& L, const int32_t* cmap, int64_t ncol, i
   row_of.alloc(cnnz > 0 ? cnnz : 1);
   col.alloc(cnnz > 0 ? cnnz : 1);
   val.alloc(cnnz > 0 ? cnnz : 1);
-  if (nnz > 0) {
-    hipLaunchKernelGGL(k_amg_runs, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz,
-                       (const unsigned long long*)key_s.p, (const double*)val_s.p, head.p, hrank.p, row_base, cbits,
-                       row_of.p, col.p, val.p);
+  if (nnz > 0 && cnnz > 0) {
+    DevBuf<int64_t> start;
+    start.alloc(cnnz);
+    hipLaunchKernelGGL(k_amg_run_starts, dim3(grid_for(nnz, 256)), dim3(256), 0, ctx.stream, nnz, head.p, hrank.p,
+                       start.p);
+    hipLaunchKernelGGL(k_amg_runs, dim3(grid_for(cnnz, 256)), dim3(256), 0, ctx.stream, cnnz, nnz,
+                       (const unsigned long long*)key_s.p, (const double*)val_s.p, (const int64_t*)start.p, row_base,
+                       cbits, row_of.p, col.p, val.p);
     AFEM_LAUNCHED();
   }
   ctx.sync();
