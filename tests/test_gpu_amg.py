@@ -157,6 +157,36 @@ def test_amg_kcycle(ctx, variant):
     mesh.close()
 
 
+def test_amg_fp32_cycle_products(ctx, variant):
+    """The AMG cycle's products on fp32 copies (AFEM_AMG_F32: 0 none, 1 the
+    fine level, 2 every level -- the default) and the fused entry / exit
+    (AFEM_AMG_FUSE) on the refined L-shape: the PCG's own product stays fp64, so
+    every variant reaches the Jacobi-PCG's solution at the tolerance in about the
+    same iterations; the fused entry / exit gives the bits of the separate passes."""
+    gm = read_gmsh(path("L-shape-3D.msh"))
+    cells, coords = _refine(gm.cells, gm.coords, 3)
+    mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    z = coords[:, 2]
+    dn = np.nonzero(z <= z.min() + 1e-9)[0].astype(np.int32)
+    bsr, ls = _poisson(ctx, mesh)
+    ls.applyDirichletViaPenalty(dn, 0.5, 1e30)
+    x_j, _ = _solve(ls, "jacobi", rtol=1e-12)
+    xs, its = {}, {}
+    for f32, fuse in (("0", "0"), ("1", "1"), ("2", "0"), ("2", "1")):
+        variant("AFEM_AMG_F32", f32)
+        variant("AFEM_AMG_FUSE", fuse)
+        ls.applyDirichletViaPenalty(dn, 0.5, 1e30)
+        xs[f32 + fuse], st = _solve(ls, "amg", rtol=1e-12)
+        its[f32 + fuse] = st["iterations"]
+    print(f"AMG fp32 variants: iterations {its}")
+    for k, x in xs.items():
+        assert np.abs(x - x_j).max() <= 1e-8 * np.abs(x_j).max(), k
+        assert abs(its[k] - its["00"]) <= 3, its
+    assert np.array_equal(xs["20"], xs["21"]) and its["20"] == its["21"]
+    bsr.close()
+    mesh.close()
+
+
 def test_amg_small_system_is_a_direct_solve(ctx):
     """Below 1024 rows the hierarchy is the matrix itself, inverted densely:
     the PCG converges in one or two iterations."""

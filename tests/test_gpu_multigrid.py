@@ -94,6 +94,48 @@ def test_multigrid_elasticity_matches_direct(ctx, use_csr):
     assert 4 * it_mg <= it_j, (it_mg, it_j)
 
 
+def test_multigrid_fp32_cycle_products(ctx, variant):
+    """Block-3 multigrid with the cycle's products on fp32 copies (AFEM_MG_F32:
+    0 none, 1 the fine level, 2 every level -- the default) and the fused entry
+    / exit (AFEM_MG_FUSE): the PCG's own product stays fp64, so every variant
+    reaches the same solution at the tolerance (the oracle's direct solve) in
+    about the same iterations; the fused entry / exit gives the bits of the
+    separate passes."""
+    n = 16  # 16 -> 8 -> 4 cells: two coarse grids
+    mesh = af.Mesh.structured(ctx, 3, n, jitter=0.2, seed=7)
+    cells, coords, _ = mesh.download()
+    bsr = af.BSRFormat(mesh, 3).initialize(True)
+    bsr.computeSparsity()
+    ls = af.DoFLinearSystem().initialize(ctx, 3 * mesh.n_own_nodes, 3 * mesh.n_nodes)
+    bsr.assembleElasticityP1Ex(LAM, MU2, 0.0, (0.0, 0.0, -1.0), ls.rhsVariable(), rhs_mode="set")
+    bsr.toLinearSystem(ls)
+    fixed = np.arange((n + 1) ** 2)  # the bottom node layer clamped
+    dofs = (3 * fixed[:, None] + np.arange(3)[None, :]).ravel().astype(np.int32)
+    xs, its = {}, {}
+    for f32, fuse in (("0", "0"), ("1", "1"), ("2", "0"), ("2", "1")):
+        variant("AFEM_MG_F32", f32)
+        variant("AFEM_MG_FUSE", fuse)
+        ls.applyDirichletViaPenalty(dofs, 0.0, 1e30)
+        xs[f32 + fuse], its[f32 + fuse] = _solve(ls, "multigrid", rtol=1e-12)
+    nn = mesh.n_own_nodes
+    rp, cols = O.sparsity(mesh.n_nodes, nn, cells)
+    vals, rhs = O.assemble_elasticity_tet(nn, cells, coords, rp, cols, LAM, MU2, 0.0, (0.0, 0.0, -1.0))
+    blk_row = np.repeat(np.arange(nn), np.diff(rp))
+    ii = (3 * blk_row[:, None, None] + np.arange(3)[None, :, None] + 0 * np.arange(3)[None, None, :]).ravel()
+    jj = (3 * cols[:, None, None] + 0 * np.arange(3)[None, :, None] + np.arange(3)[None, None, :]).ravel()
+    A = sp.csr_matrix((vals, (ii, jj)), shape=(3 * nn, 3 * nn)).tolil()
+    for d in dofs:
+        A[d, d] = 1e30
+    rhs[dofs] = 0.0
+    xo = spla.spsolve(A.tocsc(), rhs)
+    print(f"multigrid fp32 variants: iterations {its}")
+    for k, x in xs.items():
+        assert np.abs(x - xo).max() <= 1e-8 * np.abs(xo).max(), k
+        assert abs(its[k] - its["00"]) <= 2, its
+    # the fused entry / exit: the same bits as the separate passes
+    assert np.array_equal(xs["20"], xs["21"]) and its["20"] == its["21"]
+
+
 def test_multigrid_row_elimination(ctx):
     # eliminated rows (identity rows, columns kept: a non-symmetric matrix) stay
     # out of the V-cycle: same solution as the Jacobi-PCG
