@@ -210,28 +210,49 @@ __global__ void k_amg_root_agg(int64_t n, const uint64_t* __restrict__ t, const 
 }
 
 // unassigned graph nodes join the strong neighbour whose root tuple is the
-// largest among the neighbours assigned in the previous pass (pass 1: roots)
-__global__ void k_amg_join(int64_t n, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
-                           const uint8_t* __restrict__ strong, const uint8_t* __restrict__ in,
-                           const int32_t* __restrict__ agg_in, const uint64_t* __restrict__ own_in,
-                           int32_t* __restrict__ agg_out, uint64_t* __restrict__ own_out)
+// largest among the neighbours assigned in the previous pass (pass 1: roots).
+// 8 lanes per row (its columns read coalesced), the largest tuple by a butterfly
+// over the lanes: root tuples are unique per root, so equal tuples carry the same
+// aggregate and the result is the row-order scan's
+__global__ __launch_bounds__(256) void k_amg_join(int64_t n, const int64_t* __restrict__ rp,
+                                                  const int32_t* __restrict__ ci, const uint8_t* __restrict__ strong,
+                                                  const uint8_t* __restrict__ in, const int32_t* __restrict__ agg_in,
+                                                  const uint64_t* __restrict__ own_in, int32_t* __restrict__ agg_out,
+                                                  uint64_t* __restrict__ own_out)
 {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int32_t a = agg_in[i];
-  uint64_t o = own_in[i];
-  if (a < 0 && in[i]) {
-    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-      const int32_t j = ci[k];
-      if (!strong[k] || agg_in[j] < 0) continue;
-      if (own_in[j] > o) {
-        o = own_in[j];
-        a = agg_in[j];
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+  const int l = threadIdx.x & 7;
+  int32_t a = -1;
+  uint64_t o = 0;
+  if (i < n) {
+    a = agg_in[i];
+    o = own_in[i];
+    if (a < 0 && in[i]) {
+      for (int64_t k = rp[i] + l; k < rp[i + 1]; k += 8) {
+        const int32_t j = ci[k];
+        if (!strong[k]) continue;
+        const int32_t aj = agg_in[j];
+        if (aj < 0) continue;
+        const uint64_t oj = own_in[j];
+        if (oj > o) {
+          o = oj;
+          a = aj;
+        }
       }
     }
   }
-  agg_out[i] = a;
-  own_out[i] = o;
+  for (int w = 1; w < 8; w <<= 1) {
+    const uint64_t ox = (uint64_t)__shfl_xor((long long)o, w, 8);
+    const int32_t ax = __shfl_xor(a, w, 8);
+    if (ox > o) {
+      o = ox;
+      a = ax;
+    }
+  }
+  if (i < n && l == 0) {
+    agg_out[i] = a;
+    own_out[i] = o;
+  }
 }
 
 // graph nodes no root reaches (isolated, or distance > hops): flag, to become
@@ -1038,6 +1059,8 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
     rel.alloc(n);
     AFEM_HIP(hipMemsetAsync(rel.p, 0, n, ctx.stream));
   }
+  const bool verbose_rounds = env_double("AFEM_AMG_VERBOSE", 0.0) > 1;
+  auto t_round = std::chrono::steady_clock::now();
   for (int round = 0; round < 64; ++round) {
     // max over the distance-`hops` neighbourhood (hops 2: the first hop over the rows
     // the previous round marked, the second over the undecided rows)
@@ -1056,6 +1079,12 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
     unsigned long long hl = 0;
     AFEM_HIP(hipMemcpyAsync(&hl, left.p, sizeof(hl), hipMemcpyDeviceToHost, ctx.stream));
     ctx.sync();
+    if (verbose_rounds) {  // AFEM_AMG_VERBOSE=2: each round's wall time and undecided rows
+      const auto t = std::chrono::steady_clock::now();
+      std::fprintf(stderr, "amg round %2d: %8.3f ms, %llu undecided\n", round,
+                   std::chrono::duration<double, std::milli>(t - t_round).count(), hl);
+      t_round = t;
+    }
     if (hl == 0) {
       if (env_double("AFEM_AMG_VERBOSE", 0.0) > 0) std::fprintf(stderr, "amg: independent set in %d rounds\n", round + 1);
       break;
@@ -1067,6 +1096,7 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
       AFEM_LAUNCHED();
     }
   }
+  auto t_tail = std::chrono::steady_clock::now();
   DevBuf<int32_t> f;
   DevBuf<int64_t> rank;
   f.alloc(n);
@@ -1085,7 +1115,7 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
                      own.p);
   AFEM_LAUNCHED();
   for (int h = 0; h < hops; ++h) {
-    hipLaunchKernelGGL(k_amg_join, dim3(g), dim3(256), 0, ctx.stream, n, L.rp, L.ci, (const uint8_t*)strong.p,
+    hipLaunchKernelGGL(k_amg_join, dim3(grid_for(n * 8, 256)), dim3(256), 0, ctx.stream, n, L.rp, L.ci, (const uint8_t*)strong.p,
                        L.in.p, (const int32_t*)L.agg.p, (const uint64_t*)own.p, agg2.p, own2.p);
     AFEM_LAUNCHED();
     std::swap(L.agg, agg2);
@@ -1121,6 +1151,9 @@ int64_t aggregate(Ctx& ctx, AmgLevel& L, double theta, int hops)
   hipLaunchKernelGGL(k_amg_member_ptr, dim3(g), dim3(256), 0, ctx.stream, n, (const uint32_t*)k2.p, nc, L.ap.p);
   AFEM_LAUNCHED();
   ctx.sync();
+  if (verbose_rounds)
+    std::fprintf(stderr, "amg aggregates from the set (joins, orphans, members): %8.3f ms\n",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_tail).count());
   return nc;
 }
 

@@ -34,7 +34,8 @@ for spec in ["jacobi"] + sys.argv[3:]:
     kv = [] if spec in ("-", "jacobi") else [x.split("=") for x in spec.split(",")]
     for k, v in kv:
         af.set_variant(k, v)
-    af.set_variant("AFEM_AMG_VERBOSE", "1")
+    if not any(k == "AFEM_AMG_VERBOSE" for k, _ in kv):
+        af.set_variant("AFEM_AMG_VERBOSE", "1")  # (=2 in a variant: each independent-set round too)
     ls.applyDirichletViaPenalty(dn, 0.5, 1.0e30)
     ls.setSolverOptions(rtol=rtol, max_iter=100000, method="pcg", preconditioner="jacobi" if spec == "jacobi" else "amg")
     t0 = time.perf_counter()
