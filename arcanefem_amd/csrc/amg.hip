@@ -5,7 +5,7 @@
 // (femutils/HypreDoFLinearSystem.cc:686-742); this is an aggregation AMG built
 // from the assembled CSR alone, on the device, deterministic bit for bit:
 //  * strength: a_ij is strong when |a_ij| >= theta sqrt(|a_ii a_jj|)
-//    (AFEM_AMG_THETA, default 0.08); constraint rows (the PCG's `cons` flags:
+//    (AFEM_AMG_THETA, default 0.05); constraint rows (the PCG's `cons` flags:
 //    penalty / eliminated rows) and rows without a positive diagonal are
 //    outside the graph;
 //  * aggregation: a maximal independent set of the strength graph at distance
@@ -1706,7 +1706,7 @@ bool amg_setup(LinearSystem& ls)
   a->scale = env_double("AFEM_AMG_SCALE", 1.7);
   a->fine_planned = env_double("AFEM_AMG_FINE_CSR", 0.0) == 0.0;
   a->use_graph = !dist && env_double("AFEM_AMG_GRAPH", 0.0) != 0.0;
-  const double theta = env_double("AFEM_AMG_THETA", 0.08);
+  const double theta = env_double("AFEM_AMG_THETA", 0.05);
   // aggregation distance: level 0 / the coarse levels (distance 1 stalls on the
   // coarse Galerkin graphs: their degree falls with the level, r05w; distance 2
   // everywhere: 108 iterations, 0.44 s with setup, at the unstructured leg's
