@@ -16,8 +16,9 @@ import sys
 GROUPS = [
     ("reassembly (c0 M + K, RHS)", r"k_assemble_elast|k_apply_bcs|k_lincomb"),
     ("PCG SpMV + p.q (node blocks)", r"k_spmv_blk<3, true"),
-    ("multigrid smoothing sweeps (node blocks)", r"k_spmv_blk<3, false, 1>"),
-    ("multigrid residuals (node blocks)", r"k_spmv_blk<3, false, 2>"),
+    ("multigrid smoothing sweeps (node blocks)", r"k_spmv_blk<3, false, 1>|k_spmv_blk3f<[13]>"),
+    ("multigrid residuals (node blocks)", r"k_spmv_blk<3, false, 2>|k_spmv_blk3f<2>"),
+    ("multigrid fp32 copy of the fine values", r"k_blk3_to_f32"),
     ("multigrid transfer + scaling", r"k_mg_restrict|k_mg_prolong|k_mg_scale|k_mg_mask|k_mg_fix|k_mg_gemv"),
     ("PCG vectors + reductions", r"k_cg_|k_reduce|k_dot"),
     ("Newmark state update", r"k_newmark"),
