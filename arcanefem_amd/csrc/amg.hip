@@ -422,7 +422,8 @@ __global__ void k_amg_scale(int64_t n, double omega, const double* __restrict__ 
 __global__ void k_amg_d2f(int64_t n, const double* __restrict__ v, float* __restrict__ f)
 {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    f[i] = (float)v[i];
+    f[i] = (float)fmin(fmax(v[i], -3.4028234663852886e38), 3.4028234663852886e38);  // (a penalty beyond fp32: its
+                                                                                      // largest value, never inf)
 }
 
 __global__ __launch_bounds__(256) void k_amg_seg256(int64_t n_rows, const int64_t* __restrict__ rp,

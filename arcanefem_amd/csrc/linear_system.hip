@@ -838,6 +838,13 @@ __global__ __launch_bounds__(256) void k_spmv_blk3f(int64_t n_brows, const int64
   }
 }
 
+// fp32 saturated (a penalty beyond the fp32 range becomes its largest value, never inf: inf * 0 on a
+// constraint row would be NaN)
+__device__ __forceinline__ float f32_sat(double v)
+{
+  return (float)fmin(fmax(v, -3.4028234663852886e38), 3.4028234663852886e38);
+}
+
 // the private fp32 layout from BSRFormat's CSR order (16 lanes per node row, lane t:
 // blocks t, t + 16, ...)
 __global__ __launch_bounds__(256) void k_blk3_to_f32(int64_t n_brows, const int64_t* __restrict__ bp,
@@ -852,7 +859,8 @@ __global__ __launch_bounds__(256) void k_blk3_to_f32(int64_t n_brows, const int6
     const double* vr = vals + 9 * b0 + 3 * t;
 #pragma unroll
     for (int a = 0; a < 3; ++a)
-      vf[3 * (b0 + t) + a] = make_float4((float)vr[3 * a * len], (float)vr[3 * a * len + 1], (float)vr[3 * a * len + 2], 0.f);
+      vf[3 * (b0 + t) + a] = make_float4(f32_sat(vr[3 * a * len]), f32_sat(vr[3 * a * len + 1]),
+                                         f32_sat(vr[3 * a * len + 2]), 0.f);
   }
 }
 

@@ -187,6 +187,27 @@ def test_amg_fp32_cycle_products(ctx, variant):
     mesh.close()
 
 
+def test_amg_penalty_beyond_fp32(ctx):
+    """A penalty above the fp32 range (1e40) on the clamped rows: the cycle's
+    fp32 copies saturate it (never inf, whose product with the constraint rows'
+    zero iterate would be NaN), and the AMG-PCG reaches the Jacobi-PCG's solution."""
+    gm = read_gmsh(path("L-shape-3D.msh"))
+    cells, coords = _refine(gm.cells, gm.coords, 2)
+    mesh = af.Mesh.from_arrays(ctx, 3, cells, coords)
+    z = coords[:, 2]
+    dn = np.nonzero(z <= z.min() + 1e-9)[0].astype(np.int32)
+    bsr, ls = _poisson(ctx, mesh)
+    ls.applyDirichletViaPenalty(dn, 0.5, 1e40)
+    x_j, _ = _solve(ls, "jacobi", rtol=1e-12)
+    ls.applyDirichletViaPenalty(dn, 0.5, 1e40)
+    x_a, st = _solve(ls, "amg", rtol=1e-12)
+    assert np.isfinite(x_a).all()
+    assert np.abs(x_a - x_j).max() <= 1e-8 * np.abs(x_j).max()
+    assert np.allclose(x_a[dn], 0.5)
+    bsr.close()
+    mesh.close()
+
+
 def test_amg_small_system_is_a_direct_solve(ctx):
     """Below 1024 rows the hierarchy is the matrix itself, inverted densely:
     the PCG converges in one or two iterations."""

@@ -136,6 +136,26 @@ def test_multigrid_fp32_cycle_products(ctx, variant):
     assert np.array_equal(xs["20"], xs["21"]) and its["20"] == its["21"]
 
 
+def test_multigrid_penalty_beyond_fp32(ctx):
+    """Block-3 multigrid with a penalty above the fp32 range (1e40): the fp32
+    cycle copies saturate it and the PCG reaches the Jacobi-PCG's solution."""
+    n = 8
+    mesh = af.Mesh.structured(ctx, 3, n, seed=3)
+    bsr = af.BSRFormat(mesh, 3).initialize(True)
+    bsr.computeSparsity()
+    ls = af.DoFLinearSystem().initialize(ctx, 3 * mesh.n_own_nodes, 3 * mesh.n_nodes)
+    bsr.assembleElasticityP1Ex(LAM, MU2, 0.0, (0.0, 0.0, -1.0), ls.rhsVariable(), rhs_mode="set")
+    bsr.toLinearSystem(ls)
+    fixed = np.arange((n + 1) ** 2)
+    dofs = (3 * fixed[:, None] + np.arange(3)[None, :]).ravel().astype(np.int32)
+    ls.applyDirichletViaPenalty(dofs, 0.0, 1e40)
+    x_mg, _ = _solve(ls, "multigrid", rtol=1e-12)
+    ls.applyDirichletViaPenalty(dofs, 0.0, 1e40)
+    x_j, _ = _solve(ls, "jacobi", rtol=1e-12)
+    assert np.isfinite(x_mg).all()
+    assert np.abs(x_mg - x_j).max() <= 1e-8 * np.abs(x_j).max()
+
+
 def test_multigrid_row_elimination(ctx):
     # eliminated rows (identity rows, columns kept: a non-symmetric matrix) stay
     # out of the V-cycle: same solution as the Jacobi-PCG
