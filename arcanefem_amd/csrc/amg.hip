@@ -23,7 +23,10 @@
 //    per level (20 power iterations from a signed hashed vector, +10 %), the
 //    coarse correction scaled by AFEM_AMG_SCALE (default 1.7: unsmoothed
 //    aggregation under-corrects; 142 -> 92 iterations at 1.7, r05y); the
-//    fine level's products through the PCG's own SpMV plan; coarsest level (<= 1024 rows,
+//    cycle's products on fp32 copies of the values (AFEM_AMG_F32: 2 every level,
+//    the default; 1 the fine level, whose product has the residual / Jacobi
+//    epilogue fused, k_amg_f32; 0 fp64 -- the fine level then through the PCG's
+//    own SpMV plan); the PCG's own product is always fp64; coarsest level (<= 1024 rows,
 //    AFEM_AMG_DENSE) inverted densely (host Cholesky at setup), else 24
 //    Jacobi sweeps;
 //  * K-cycle (AFEM_AMG_KCYCLE, default 2): levels 1..k solve their coarse
@@ -31,7 +34,8 @@
 //    (Notay & Vassilevski), the step weights computed on the device -- the
 //    Krylov weights replace the 1.7 overcorrection there;
 //  * constraint rows are taken out of the cycle as in multigrid.hip:
-//    z = F V(F r) + C D^-1 r.
+//    z = F V(F r) + C D^-1 r (one rank: the mask fused with the first sweep and
+//    the fix with the last, AFEM_AMG_FUSE).
 // Several ranks (a halo attached): the levels stay distributed -- each rank
 // aggregates its own rows, the coarse ghost columns and halo follow from the
 // fine halo (build_dist_coarse) -- until the global coarse size is below
