@@ -18,6 +18,10 @@
 //    over by themselves;
 //  * smoothing: damped Jacobi, omega = 4 / (3 lambda_max(D^-1 A)) from a power
 //    iteration per level, one sweep before and one after (symmetric V-cycle);
+//    block-3 systems run the cycle's products (sweeps, residuals) on fp32 copies
+//    of every level's values in a 16-B-per-block-row layout (k_spmv_blk3f,
+//    AFEM_MG_F32; the PCG's own product stays fp64), on one rank with the mask
+//    fused into the first sweep and the constraint fix into the last (AFEM_MG_FUSE);
 //  * coarsest level: dense inverse (<= kDenseMax DoF, symmetric scaling +
 //    Cholesky on the host at setup), else 16 Jacobi sweeps;
 //  * constraint rows (penalty / eliminated, the PCG's `cons` flags) are taken
