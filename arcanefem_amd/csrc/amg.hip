@@ -20,7 +20,8 @@
 //    by (agg i, agg j), radix-sorted (stable), each key run summed by one
 //    thread in the CSR order -- fixed summation order;
 //  * cycle: V(nu, nu) with damped Jacobi, omega = 4 / (3 lambda_max(D^-1 A))
-//    per level (20 power iterations from a signed hashed vector, +10 %), the
+//    per level (8 power iterations from a signed hashed vector, +10 %: 20 cost
+//    10 ms more setup and 70 instead of 64 PCG iterations, r06bm), the
 //    coarse correction scaled by AFEM_AMG_SCALE (default 1.7: unsmoothed
 //    aggregation under-corrects; 142 -> 92 iterations at 1.7, r05y); the
 //    cycle's products on fp32 copies of the values (AFEM_AMG_F32: 2 every level,
@@ -69,7 +70,7 @@ inline unsigned grid_for(int64_t n, int threads) { return (unsigned)((n + thread
 constexpr int kDense = 1024;     // rows of a coarsest level inverted densely (AFEM_AMG_DENSE)
 constexpr int kMaxLevels = 16;
 constexpr int kCoarseSweeps = 24;
-constexpr int kPowerIts = 20;
+constexpr int kPowerIts = 8;    // per level (AFEM_AMG_POWER_ITS)
 constexpr int kVec = 1024;       // grid of the vector kernels
 
 // ------------------------------------------------------------------ kernels
@@ -783,6 +784,8 @@ struct Amg {
   int n_dense = 0;
   int sweeps = 1;
   double scale = 1.0;
+  // AFEM_AMG_POWER_ITS: power iterations per level for lambda_max (kPowerIts)
+  int power_its = kPowerIts;
   // AFEM_AMG_KCYCLE=k: levels 1..k solve their coarse problem by two flexible-CG
   // steps preconditioned by the cycle below (K-cycle) instead of one cycle
   int kcycle = 0;
@@ -965,7 +968,7 @@ double power_lambda(Ctx& ctx, Amg& a, AmgLevel& L)
     // (the fine level's products on its fp32 copy when it has one: lambda_max of the fp32-rounded
     // operator, the one the cycle's sweeps apply)
     const bool f32 = a.v32.p && &L == &a.lv[0];
-    for (int it = 0; it < kPowerIts; ++it) {
+    for (int it = 0; it < a.power_its; ++it) {
       if (f32)
         f32_product(ctx, a, L, 0, L.x.p, nullptr, L.t.p);
       else
@@ -985,7 +988,7 @@ double power_lambda(Ctx& ctx, Amg& a, AmgLevel& L)
   double nv = std::sqrt(d ? allsum(ctx, a, L.n > 0 ? host_sum(ctx, a.partial, (int)g) : 0.0)
                           : host_sum(ctx, a.partial, (int)g)),
          lam = 0.0;
-  for (int it = 0; it < kPowerIts; ++it) {
+  for (int it = 0; it < a.power_its; ++it) {
     halo(ctx, L, L.x.p);
     spmv(ctx, 0, L, L.x.p, L.t.p, nullptr, 0.0);
     if (L.n > 0) {
@@ -1709,6 +1712,7 @@ bool amg_setup(LinearSystem& ls)
   a->comm = dist ? ls.halo->comm : nullptr;
   a->sweeps = (int)std::max(1.0, env_double("AFEM_AMG_SWEEPS", 1.0));
   a->scale = env_double("AFEM_AMG_SCALE", 1.7);
+  a->power_its = (int)std::min(200.0, std::max(1.0, env_double("AFEM_AMG_POWER_ITS", kPowerIts)));
   a->fine_planned = env_double("AFEM_AMG_FINE_CSR", 0.0) == 0.0;
   a->use_graph = !dist && env_double("AFEM_AMG_GRAPH", 0.0) != 0.0;
   const double theta = env_double("AFEM_AMG_THETA", 0.05);
