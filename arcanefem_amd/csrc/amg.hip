@@ -786,6 +786,7 @@ struct Amg {
   double scale = 1.0;
   // AFEM_AMG_POWER_ITS: power iterations per level for lambda_max (kPowerIts)
   int power_its = kPowerIts;
+  double omega_scale = 1.0;  // AFEM_AMG_OMEGA: a factor on every level's omega (measurements)
   // AFEM_AMG_KCYCLE=k: levels 1..k solve their coarse problem by two flexible-CG
   // steps preconditioned by the cycle below (K-cycle) instead of one cycle
   int kcycle = 0;
@@ -1712,6 +1713,7 @@ bool amg_setup(LinearSystem& ls)
   a->comm = dist ? ls.halo->comm : nullptr;
   a->sweeps = (int)std::max(1.0, env_double("AFEM_AMG_SWEEPS", 1.0));
   a->scale = env_double("AFEM_AMG_SCALE", 1.7);
+  a->omega_scale = std::min(2.0, std::max(0.1, env_double("AFEM_AMG_OMEGA", 1.0)));
   a->power_its = (int)std::min(200.0, std::max(1.0, env_double("AFEM_AMG_POWER_ITS", kPowerIts)));
   a->fine_planned = env_double("AFEM_AMG_FINE_CSR", 0.0) == 0.0;
   a->use_graph = !dist && env_double("AFEM_AMG_GRAPH", 0.0) != 0.0;
@@ -1827,7 +1829,7 @@ bool amg_setup(LinearSystem& ls)
     // the power iteration approaches lambda_max from below: 10 % margin (an
     // underestimate by 1.5x would make the smoother diverge)
     const double lam = 1.1 * power_lambda(ctx, *a, L);
-    L.omega = lam > 0 ? 4.0 / (3.0 * lam) : 0.0;
+    L.omega = lam > 0 ? a->omega_scale * 4.0 / (3.0 * lam) : 0.0;
   }
   mark("power iterations");
   AmgLevel& last = a->lv.back();

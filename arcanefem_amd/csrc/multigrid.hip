@@ -1259,6 +1259,8 @@ void mg_setup(LinearSystem& ls)
     L.b.alloc(L.n);
     const double lam = dist ? power_lambda_global(ls, *mg, L) : power_lambda(ctx, *mg, L);
     L.omega = lam > 0 ? 4.0 / (3.0 * 1.05 * lam) : 0.6;
+    const char* oe = variant("AFEM_MG_OMEGA");  // a factor on every level's omega (measurements)
+    if (oe && std::atof(oe) > 0) L.omega *= std::atof(oe);
   }
   MgLevel& Lc = mg->lv.back();
   if (mg->lv.size() > 1 && !Lc.dist && Lc.n <= kDenseMax) dense_inverse(ctx, *mg, Lc);
