@@ -71,8 +71,9 @@ int afem_device_count(int* count);
  * AFEM_CG_GRAPH (1: replay the single-rank CG iterations as a HIP graph; off by
  * default, slower on MI355X),
  * AFEM_ORDER / AFEM_BRICKS / AFEM_BANK_PLACE / _MAX (structure build),
- * AFEM_MG_F32 / _FUSE / _KCYCLE, AFEM_AMG_F32 / _FUSE / _KCYCLE / _VERBOSE and the
- * other AFEM_AMG_* setup knobs (preconditioners: the fp32 cycle products change
+ * AFEM_MG_F32 / _FUSE / _KCYCLE / _OMEGA, AFEM_AMG_F32 / _FUSE / _KCYCLE /
+ * _POWER_ITS / _OMEGA / _VERBOSE and the other AFEM_AMG_* setup knobs
+ * (preconditioners: the fp32 cycle products and the smoother's omega change
  * the preconditioner, never the PCG's own fp64 product or its tolerance),
  * AFEM_DEBUG_SLICES / _PATTERNS (stderr dumps).  Without an explicit value a
  * knob takes the process environment's value at its first use; unset means
